@@ -1,0 +1,145 @@
+"""FileSystem abstraction (hadoop-1.0.3/src/core/org/apache/hadoop/fs/FileSystem.java).
+
+hbmr targets one 8×MI355X node, so HDFS is replaced by the local file system
+(NVMe / page cache); ``file://`` and bare paths resolve to it.  The interface
+keeps the Hadoop operations the MapReduce layer uses: listStatus with hidden
+file filtering (``_``/``.`` prefixes, as FileInputFormat's hiddenFileFilter),
+create/open/rename/delete/mkdirs and block-size metadata for split sizing.
+"""
+from __future__ import annotations
+
+import glob as _glob
+import os
+import shutil
+from dataclasses import dataclass
+
+DEFAULT_BLOCK_SIZE = 64 * 1024 * 1024  # dfs.block.size default (hdfs-default.xml:259-260)
+
+
+def strip_scheme(path) -> str:
+    p = str(path)
+    if p.startswith("file://"):
+        p = p[len("file://"):]
+    return p
+
+
+@dataclass
+class FileStatus:
+    path: str
+    length: int
+    is_dir: bool
+    block_size: int = DEFAULT_BLOCK_SIZE
+    modification_time: float = 0.0
+
+    def getLen(self):  # noqa: N802
+        return self.length
+
+    def getPath(self):  # noqa: N802
+        return self.path
+
+    def isDir(self):  # noqa: N802
+        return self.is_dir
+
+    def getBlockSize(self):  # noqa: N802
+        return self.block_size
+
+
+def hidden(name: str) -> bool:
+    base = os.path.basename(name.rstrip("/"))
+    return base.startswith("_") or base.startswith(".")
+
+
+class LocalFileSystem:
+    scheme = "file"
+
+    def __init__(self, conf=None):
+        self.conf = conf
+        bs = conf.get_long("fs.local.block.size", DEFAULT_BLOCK_SIZE) if conf is not None else \
+            DEFAULT_BLOCK_SIZE
+        self.block_size = bs
+
+    def get_file_status(self, path) -> FileStatus:
+        p = strip_scheme(path)
+        st = os.stat(p)
+        return FileStatus(p, st.st_size, os.path.isdir(p), self.block_size, st.st_mtime)
+
+    getFileStatus = get_file_status  # noqa: N815
+
+    def exists(self, path) -> bool:
+        return os.path.exists(strip_scheme(path))
+
+    def is_dir(self, path) -> bool:
+        return os.path.isdir(strip_scheme(path))
+
+    def list_status(self, path, filter_hidden=True) -> list[FileStatus]:
+        p = strip_scheme(path)
+        if not os.path.isdir(p):
+            return [self.get_file_status(p)]
+        out = []
+        for name in sorted(os.listdir(p)):
+            if filter_hidden and hidden(name):
+                continue
+            out.append(self.get_file_status(os.path.join(p, name)))
+        return out
+
+    listStatus = list_status  # noqa: N815
+
+    def glob_status(self, pattern) -> list[FileStatus]:
+        return [self.get_file_status(p) for p in sorted(_glob.glob(strip_scheme(pattern)))]
+
+    globStatus = glob_status  # noqa: N815
+
+    def mkdirs(self, path):
+        os.makedirs(strip_scheme(path), exist_ok=True)
+        return True
+
+    def create(self, path, overwrite=True):
+        p = strip_scheme(path)
+        if not overwrite and os.path.exists(p):
+            raise FileExistsError(p)
+        d = os.path.dirname(p)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        return open(p, "wb")
+
+    def open(self, path):
+        return open(strip_scheme(path), "rb")
+
+    def rename(self, src, dst) -> bool:
+        s, d = strip_scheme(src), strip_scheme(dst)
+        if not os.path.exists(s):
+            return False
+        parent = os.path.dirname(d)
+        if parent:
+            os.makedirs(parent, exist_ok=True)
+        if os.path.isdir(d):
+            d = os.path.join(d, os.path.basename(s.rstrip("/")))
+        os.replace(s, d)
+        return True
+
+    def delete(self, path, recursive=True) -> bool:
+        p = strip_scheme(path)
+        if not os.path.exists(p):
+            return False
+        if os.path.isdir(p):
+            if not recursive and os.listdir(p):
+                raise OSError(f"{p} is a non-empty directory")
+            shutil.rmtree(p)
+        else:
+            os.remove(p)
+        return True
+
+    def get_default_block_size(self):
+        return self.block_size
+
+    getDefaultBlockSize = get_default_block_size  # noqa: N815
+
+
+def get_fs(path=None, conf=None) -> LocalFileSystem:
+    p = str(path or "")
+    if "://" in p and not p.startswith("file://"):
+        raise ValueError(f"unsupported filesystem scheme in {p!r} (hbmr is single-node: use file://)")
+    return LocalFileSystem(conf)
+
+
+FileSystem = LocalFileSystem

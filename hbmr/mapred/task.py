@@ -1,0 +1,526 @@
+"""Map and reduce task execution (the CPU data path).
+
+MapTask (hadoop-1.0.3/src/mapred/org/apache/hadoop/mapred/MapTask.java):
+  record reader -> MapRunnable -> MapOutputBuffer (collect; sort by
+  (partition, key) when the buffer passes ``io.sort.mb × io.sort.spill.percent``;
+  combiner per spill; spills merged with ``io.sort.factor`` fan-in into
+  ``file.out`` + ``file.out.index``, MapTask.java:869-1621), or straight to the
+  OutputFormat when there are no reducers (DirectMapOutputCollector, :805).
+
+ReduceTask (ReduceTask.java:348): fetch each map's segment of this partition
+(on one node the map outputs are local files — the reference's HTTP fetch,
+ReduceTask.java:1231-1775, becomes a read), k-way merge (Merger.java:236-365),
+group by the grouping comparator and call the Reducer; output goes through the
+OutputCommitter's task work dir.
+
+The GPU data path (split-level GPU mappers, RCCL shuffle) lives in
+:mod:`hbmr.gpu`; it plugs in at the same MapTask boundary.
+"""
+from __future__ import annotations
+
+import heapq
+import io
+import itertools
+import logging
+import os
+import threading
+import time
+
+from ..io.compress import get_codec
+from ..io.ifile import IFileWriter, SpillRecord, read_segment
+from ..utils.reflection import new_instance
+from . import counters as C
+from .api import OutputCollector, Reporter
+from .committer import FileOutputCommitter
+from .formats import FileSplit
+
+log = logging.getLogger("hbmr.task")
+
+
+class TaskReporter(Reporter):
+    """Collects progress/status/counters of one task attempt (Task.TaskReporter,
+    Task.java:554); the TaskTracker reads ``snapshot()`` on each heartbeat."""
+
+    def __init__(self, split=None, listener=None):
+        self.counters = C.Counters()
+        self.status = ""
+        self.progress_value = 0.0
+        self.split = split
+        self.last_progress = time.time()
+        self.listener = listener
+        self._lock = threading.Lock()
+
+    def setStatus(self, status):  # noqa: N802
+        self.status = status
+        self.progress()
+
+    def progress(self):
+        self.last_progress = time.time()
+
+    def set_progress(self, p):
+        self.progress_value = float(p)
+        self.progress()
+
+    def getCounter(self, group, name=None):  # noqa: N802
+        if name is None and isinstance(group, tuple):
+            group, name = group
+        return self.counters.find_counter(group, name)
+
+    def incrCounter(self, group, name, amount=1):  # noqa: N802
+        self.counters.incr(group, name, amount)
+
+    def getInputSplit(self):  # noqa: N802
+        return self.split
+
+    def getProgress(self):  # noqa: N802
+        return self.progress_value
+
+
+class _Interrupted(Exception):
+    pass
+
+
+class Task:
+    """Base of MapTask / ReduceTask: identity, placement and the commit protocol."""
+
+    def __init__(self, job, attempt_id, partition: int):
+        self.job = job
+        self.attempt_id = attempt_id
+        self.partition = partition
+        self.reporter = TaskReporter()
+        self.run_on_gpu = False        # Task.runOnGPU (Task.java:169-207)
+        self.gpu_device_id = -1        # Task.GPUDeviceId
+        self.kill_event = threading.Event()
+        self.local_dir = None
+        self.start_time = 0.0
+        self.finish_time = 0.0
+
+    @property
+    def is_map(self):
+        return self.attempt_id.is_map
+
+    def runOnGPU(self):  # noqa: N802
+        return self.run_on_gpu
+
+    def setRunOnGPU(self, b):  # noqa: N802
+        self.run_on_gpu = bool(b)
+
+    def setGPUDeviceId(self, d):  # noqa: N802
+        self.gpu_device_id = int(d)
+
+    def check_killed(self):
+        if self.kill_event.is_set():
+            raise _Interrupted(str(self.attempt_id))
+
+    def committer(self):
+        cls = self.job.get_output_committer()
+        return cls() if isinstance(cls, type) else FileOutputCommitter()
+
+    def _task_conf(self):
+        """Per-attempt JobConf with the committer's work dir set."""
+        conf = type(self.job)(self.job)
+        wp = None
+        com = self.committer()
+        if hasattr(com, "work_path"):
+            wp = com.work_path(self.job, self.attempt_id)
+        if wp:
+            conf.set("mapred.work.output.dir", wp)
+        conf.set("mapred.task.id", str(self.attempt_id))
+        conf.set("mapred.task.partition", self.partition)
+        conf.set("mapred.task.is.map", self.is_map)
+        return conf
+
+
+# ------------------------------------------------------------------- map side
+class _DirectCollector(OutputCollector):
+    def __init__(self, writer, reporter):
+        self.writer = writer
+        self.reporter = reporter
+        self.n = 0
+
+    def collect(self, key, value):
+        self.writer.write(key, value)
+        self.n += 1
+
+    def flush(self):
+        self.writer.close(self.reporter)
+        self.reporter.incrCounter(C.TASK_GROUP, C.MAP_OUTPUT_RECORDS, self.n)
+
+
+class _ListCollector(OutputCollector):
+    def __init__(self):
+        self.out = []
+
+    def collect(self, key, value):
+        self.out.append((key, value))
+
+
+def group_sorted(records, group_key, vcls):
+    """records: iterable of (sort_key, kb, vb) sorted; yields (kb, values_iter)."""
+    it = iter(records)
+    try:
+        first = next(it)
+    except StopIteration:
+        return
+    pending = [first]
+
+    while pending:
+        head = pending.pop()
+        gk = group_key(head[1])
+        state = {"next": None}
+
+        def values(head=head, gk=gk, state=state):
+            yield vcls.deserialize(head[2])
+            for rec in it:
+                if group_key(rec[1]) != gk:
+                    state["next"] = rec
+                    return
+                yield vcls.deserialize(rec[2])
+
+        vals = values()
+        yield head[1], vals
+        # drain unconsumed values of this group
+        for _ in vals:
+            pass
+        if state["next"] is not None:
+            pending.append(state["next"])
+
+
+def run_combiner(combiner_cls, job, kcls, vcls, records, reporter):
+    """Apply the combiner to sorted (sk, kb, vb) records of ONE partition.
+    Returns a new sorted list of (sk, kb, vb)."""
+    comb = new_instance(combiner_cls, job)
+    col = _ListCollector()
+    sort_key = job.get_output_key_comparator()
+    group_key = job.get_output_value_grouping_comparator()
+    recs = list(records)
+    nin = len(recs)
+    for kb, vals in group_sorted(recs, group_key, vcls):
+        comb.reduce(kcls.deserialize(kb), vals, col, reporter)
+    comb.close()
+    reporter.incrCounter(C.TASK_GROUP, C.COMBINE_INPUT_RECORDS, nin)
+    reporter.incrCounter(C.TASK_GROUP, C.COMBINE_OUTPUT_RECORDS, len(col.out))
+    out = []
+    for k, v in col.out:
+        kb = k.serialize()
+        out.append((sort_key(kb), kb, v.serialize()))
+    out.sort(key=lambda r: r[0])
+    return out
+
+
+class MapOutputBuffer(OutputCollector):
+    """Collect → partition → sort → (combine) → spill, then merge spills."""
+
+    def __init__(self, task: "MapTask", job, reporter, out_dir):
+        self.task = task
+        self.job = job
+        self.reporter = reporter
+        self.R = job.get_num_reduce_tasks()
+        self.kcls = job.get_map_output_key_class()
+        self.vcls = job.get_map_output_value_class()
+        self.sort_key = job.get_output_key_comparator()
+        self.partitioner = new_instance(job.get_partitioner_class(), job)
+        self.combiner_cls = job.get_combiner_class()
+        sort_mb = job.get_int("io.sort.mb", 100)
+        self.soft_limit = int(sort_mb * (1 << 20) * job.get_float("io.sort.spill.percent", 0.8))
+        self.factor = max(2, job.get_int("io.sort.factor", 10))
+        self.min_spills_for_combine = job.get_int("min.num.spills.for.combine", 3)
+        self.codec = get_codec(job.get("mapred.map.output.compression.codec",
+                                       "org.apache.hadoop.io.compress.DefaultCodec")) \
+            if job.get_compress_map_output() else None
+        self.out_dir = out_dir
+        os.makedirs(out_dir, exist_ok=True)
+        self.buf: list = []
+        self.buf_bytes = 0
+        self.spills: list[tuple[str, SpillRecord]] = []
+        self.n_out = 0
+        self.bytes_out = 0
+
+    def collect(self, key, value):
+        if not isinstance(key, self.kcls):
+            raise TypeError(f"Type mismatch in key from map: expected {self.kcls.__name__}, "
+                            f"received {type(key).__name__}")
+        if not isinstance(value, self.vcls):
+            raise TypeError(f"Type mismatch in value from map: expected {self.vcls.__name__}, "
+                            f"received {type(value).__name__}")
+        part = self.partitioner.getPartition(key, value, self.R)
+        if not 0 <= part < self.R:
+            raise ValueError(f"Illegal partition for {key!r} ({part})")
+        kb = key.serialize()
+        vb = value.serialize()
+        self.buf.append((part, self.sort_key(kb), kb, vb))
+        sz = len(kb) + len(vb) + 16  # 16 B accounting per record (MapTask.java:890-903)
+        self.buf_bytes += sz
+        self.n_out += 1
+        self.bytes_out += len(kb) + len(vb)
+        if self.buf_bytes >= self.soft_limit:
+            self.sort_and_spill()
+
+    def _sorted_partitions(self):
+        self.buf.sort(key=lambda r: (r[0], r[1]))
+        parts = [[] for _ in range(self.R)]
+        for p, sk, kb, vb in self.buf:
+            parts[p].append((sk, kb, vb))
+        return parts
+
+    def sort_and_spill(self):
+        if not self.buf and self.spills:
+            return
+        self.task.check_killed()
+        parts = self._sorted_partitions()
+        self.buf = []
+        self.buf_bytes = 0
+        idx = len(self.spills)
+        path = os.path.join(self.out_dir, f"spill{idx}.out")
+        rec = SpillRecord(self.R)
+        spilled = 0
+        with open(path, "wb") as f:
+            for p in range(self.R):
+                recs = parts[p]
+                if self.combiner_cls is not None and recs:
+                    recs = run_combiner(self.combiner_cls, self.job, self.kcls, self.vcls, recs,
+                                        self.reporter)
+                w = IFileWriter(f, self.codec)
+                for _sk, kb, vb in recs:
+                    w.append(kb, vb)
+                spilled += len(recs)
+                rec.put(p, *w.close())
+        rec.write(path + ".index")
+        self.spills.append((path, rec))
+        self.reporter.incrCounter(C.TASK_GROUP, C.SPILLED_RECORDS, spilled)
+
+    def flush(self):
+        """Final spill + merge into file.out / file.out.index."""
+        self.sort_and_spill()
+        final = os.path.join(self.out_dir, "file.out")
+        if len(self.spills) == 1:
+            path, rec = self.spills[0]
+            os.replace(path, final)
+            os.replace(path + ".index", final + ".index")
+        else:
+            self._merge_parts(final)
+        self.reporter.incrCounter(C.TASK_GROUP, C.MAP_OUTPUT_RECORDS, self.n_out)
+        self.reporter.incrCounter(C.TASK_GROUP, C.MAP_OUTPUT_BYTES, self.bytes_out)
+        return final
+
+    def _merge_parts(self, final):
+        rec_out = SpillRecord(self.R)
+        spilled = 0
+        with open(final, "wb") as f:
+            for p in range(self.R):
+                segs = []
+                for path, rec in self.spills:
+                    start, _raw, plen = rec.get(p)
+                    with open(path, "rb") as sf:
+                        sf.seek(start)
+                        data = sf.read(plen)
+                    segs.append([(self.sort_key(kb), kb, vb)
+                                 for kb, vb in read_segment(data, self.codec)])
+                merged = merge_segments(segs, self.factor)
+                if self.combiner_cls is not None and len(self.spills) >= \
+                        self.min_spills_for_combine:
+                    merged = run_combiner(self.combiner_cls, self.job, self.kcls, self.vcls,
+                                          list(merged), self.reporter)
+                w = IFileWriter(f, self.codec)
+                n = 0
+                for _sk, kb, vb in merged:
+                    w.append(kb, vb)
+                    n += 1
+                spilled += n
+                rec_out.put(p, *w.close())
+        rec_out.write(final + ".index")
+        for path, _ in self.spills:
+            for q in (path, path + ".index"):
+                if os.path.exists(q):
+                    os.remove(q)
+        self.reporter.incrCounter(C.TASK_GROUP, C.SPILLED_RECORDS, spilled)
+
+
+def merge_segments(segments, factor: int = 10):
+    """k-way merge of sorted (sk, kb, vb) runs, at most ``factor`` runs per pass
+    (Merger.MergeQueue). Stable: earlier segments win ties."""
+    segs = [s for s in segments if s]
+    while len(segs) > factor:
+        nxt = []
+        for i in range(0, len(segs), factor):
+            grp = segs[i:i + factor]
+            nxt.append(list(_heap_merge(grp)))
+        segs = nxt
+    return _heap_merge(segs)
+
+
+def _decorate(si, seg):
+    for ri, r in enumerate(seg):
+        yield (r[0], si, ri, r)
+
+
+def _heap_merge(segs):
+    for _sk, _si, _ri, r in heapq.merge(*[_decorate(si, s) for si, s in enumerate(segs)]):
+        yield r
+
+
+class MapTask(Task):
+    def __init__(self, job, attempt_id, partition, split):
+        super().__init__(job, attempt_id, partition)
+        self.split = split
+        self.reporter.split = split
+        self.output_file = None  # (path to file.out) when R > 0
+
+    def run(self, local_dir: str):
+        self.start_time = time.time()
+        job = self._task_conf()
+        self.local_dir = local_dir
+        rep = self.reporter
+        R = job.get_num_reduce_tasks()
+        committer = self.committer()
+        committer.setup_task(job, self.attempt_id)
+        informat = new_instance(job.get_input_format(), job)
+        reader = informat.getRecordReader(self.split, job, rep)
+        if isinstance(self.split, FileSplit):
+            rep.incrCounter(C.TASK_GROUP, C.MAP_INPUT_BYTES, self.split.length)
+        if R == 0:
+            outfmt = new_instance(job.get_output_format(), job)
+            name = f"part-{self.partition:05d}"
+            collector = _DirectCollector(outfmt.getRecordWriter(None, job, name, rep), rep)
+        else:
+            collector = MapOutputBuffer(self, job, rep, os.path.join(local_dir, "output"))
+        runner_cls = job.get_map_runner_class()
+        runner = new_instance(runner_cls, job)
+        try:
+            runner.run(_ProgressReader(reader, rep, self), collector, rep)
+        finally:
+            reader.close()
+        if R == 0:
+            collector.flush()
+            if committer.needs_task_commit(job, self.attempt_id):
+                committer.commit_task(job, self.attempt_id)
+        else:
+            self.output_file = collector.flush()
+        rep.set_progress(1.0)
+        self.finish_time = time.time()
+        return self.output_file
+
+
+class _ProgressReader:
+    def __init__(self, reader, reporter, task):
+        self.r = reader
+        self.rep = reporter
+        self.task = task
+        self.n = 0
+
+    def next(self):
+        kv = self.r.next()
+        self.n += 1
+        if (self.n & 4095) == 0:
+            self.task.check_killed()
+            try:
+                self.rep.progress_value = self.r.getProgress()
+            except Exception:
+                pass
+        return kv
+
+    def __iter__(self):
+        while True:
+            kv = self.next()
+            if kv is None:
+                return
+            yield kv
+
+    def getProgress(self):  # noqa: N802
+        return self.r.getProgress()
+
+    def close(self):
+        self.r.close()
+
+
+# ------------------------------------------------------------------- reduce side
+class MapOutputLocation:
+    """Where to fetch one map's output (the reference's task-completion event +
+    TaskTracker /mapOutput URL, ReduceTask.java:1476)."""
+
+    def __init__(self, map_attempt, path, fetch=None):
+        self.map_attempt = map_attempt
+        self.path = path
+        self.fetch = fetch  # optional callable(partition) -> bytes (remote shuffle)
+
+    def read_partition(self, part):
+        if self.fetch is not None:
+            return self.fetch(part)
+        idx = SpillRecord.read(self.path + ".index")
+        start, _raw, plen = idx.get(part)
+        with open(self.path, "rb") as f:
+            f.seek(start)
+            return f.read(plen)
+
+
+class ReduceTask(Task):
+    def __init__(self, job, attempt_id, partition, num_maps):
+        super().__init__(job, attempt_id, partition)
+        self.num_maps = num_maps
+        self.locations: list[MapOutputLocation] = []
+
+    def add_map_output(self, loc: MapOutputLocation):
+        self.locations.append(loc)
+
+    def run(self, local_dir: str):
+        self.start_time = time.time()
+        job = self._task_conf()
+        self.local_dir = local_dir
+        rep = self.reporter
+        codec = get_codec(job.get("mapred.map.output.compression.codec",
+                                  "org.apache.hadoop.io.compress.DefaultCodec")) \
+            if job.get_compress_map_output() else None
+        kcls = job.get_map_output_key_class()
+        vcls = job.get_map_output_value_class()
+        sort_key = job.get_output_key_comparator()
+        group_key = job.get_output_value_grouping_comparator()
+        # copy phase
+        segs = []
+        shuffled = 0
+        for loc in self.locations:
+            self.check_killed()
+            data = loc.read_partition(self.partition)
+            shuffled += len(data)
+            segs.append([(sort_key(kb), kb, vb) for kb, vb in read_segment(data, codec)])
+        rep.incrCounter(C.TASK_GROUP, C.REDUCE_SHUFFLE_BYTES, shuffled)
+        rep.set_progress(1 / 3)
+        # sort phase (merge)
+        merged = merge_segments(segs, job.get_int("io.sort.factor", 10))
+        rep.set_progress(2 / 3)
+        # reduce phase
+        committer = self.committer()
+        committer.setup_task(job, self.attempt_id)
+        outfmt = new_instance(job.get_output_format(), job)
+        writer = outfmt.getRecordWriter(None, job, f"part-{self.partition:05d}", rep)
+        reducer = new_instance(job.get_reducer_class(), job)
+        n_in = itertools.count()
+        n_out = [0]
+        n_groups = 0
+
+        class _Out(OutputCollector):
+            def collect(self_inner, k, v):
+                writer.write(k, v)
+                n_out[0] += 1
+
+        counted = ((next(n_in), r)[1] for r in merged)
+        out = _Out()
+        try:
+            for kb, vals in group_sorted(counted, group_key, vcls):
+                n_groups += 1
+                if (n_groups & 1023) == 0:
+                    self.check_killed()
+                reducer.reduce(kcls.deserialize(kb), vals, out, rep)
+        finally:
+            reducer.close()
+            writer.close(rep)
+        rep.incrCounter(C.TASK_GROUP, C.REDUCE_INPUT_GROUPS, n_groups)
+        rep.incrCounter(C.TASK_GROUP, C.REDUCE_INPUT_RECORDS, next(n_in))
+        rep.incrCounter(C.TASK_GROUP, C.REDUCE_OUTPUT_RECORDS, n_out[0])
+        if committer.needs_task_commit(job, self.attempt_id):
+            committer.commit_task(job, self.attempt_id)
+        rep.set_progress(1.0)
+        self.finish_time = time.time()
+
+
+def iter_bytes(data: bytes):
+    return io.BytesIO(data)

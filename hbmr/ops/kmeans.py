@@ -1,0 +1,176 @@
+"""K-Means map/combine/reduce ops on MI355X (HIP kernels in native/kernels/kmeans.hip).
+
+Data layout contract (built by :class:`hbmr.gpu.split_cache.SplitCache`):
+
+* points: ``bf16 [n, dp]`` with ``dp`` in {64, 128, 256} (feature dim zero-padded),
+* centroids: fp32 master copy ``[k, d]`` plus a bf16 image ``[k_pad, dp]`` and
+  ``chalf = -||c||²/2`` (fp32, ``[k_pad]``); padded clusters carry -1e30 so they
+  never win the arg-max,
+* partial sums: **int64 fixed point** ``[k, dp]`` (``Σ round(x·2^fx_shift)``) and
+  int64 counts ``[k]`` — exact and order-independent, so K-Means results are
+  bitwise reproducible for any placement of map tasks over CPUs/GPUs and any
+  GPU count (integer RCCL all-reduce is exact too).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+
+SUPPORTED_DP = (64, 128, 256)
+FX_SHIFT = 24  # fixed-point fraction bits of the partial sums
+
+
+def padded_dim(d: int) -> int:
+    for dp in SUPPORTED_DP:
+        if d <= dp:
+            return dp
+    raise ValueError(f"feature dim {d} > {SUPPORTED_DP[-1]} not supported by the MFMA kernel")
+
+
+def padded_k(k: int) -> int:
+    return ((k + 63) // 64) * 64
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def new_partials(k: int, dp: int, device) -> tuple[torch.Tensor, torch.Tensor]:
+    return (torch.zeros(k, dp, dtype=torch.int64, device=device),
+            torch.zeros(k, dtype=torch.int64, device=device))
+
+
+def partials_to_float(sums: torch.Tensor, counts: torch.Tensor, d: int | None = None,
+                      fx_shift: int = FX_SHIFT):
+    s = sums.to(torch.float64) / float(1 << fx_shift)
+    if d is not None:
+        s = s[:, :d]
+    return s, counts.to(torch.float64)
+
+
+class CentroidImage:
+    """Device-resident centroids in the layout the assign kernel consumes."""
+
+    def __init__(self, centroids: torch.Tensor, device, fx_shift: int = FX_SHIFT):
+        c = centroids.detach().to(device=device, dtype=torch.float32).contiguous()
+        self.k, self.d = c.shape
+        self.dp = padded_dim(self.d)
+        self.k_pad = padded_k(self.k)
+        self.fx_shift = fx_shift
+        self.device = c.device
+        self.cen = c
+        self.cbf = torch.zeros(self.k_pad, self.dp, dtype=torch.bfloat16, device=device)
+        self.chalf = torch.empty(self.k_pad, dtype=torch.float32, device=device)
+        self.shift2 = torch.zeros(self.k, dtype=torch.float32, device=device)
+        self.refresh()
+
+    def refresh(self, sums=None, counts=None, stream=None):
+        """Reduce-side update: c = sums/counts (clusters with count 0 keep their
+        centroid), then rebuild the bf16 image and -||c||²/2."""
+        lib = _lib.load()
+        rc = lib.hbmr_kmeans_update(_ptr(sums), _ptr(counts), self.fx_shift, self.k, self.d,
+                                    self.dp, self.k_pad, _ptr(self.cen), _ptr(self.cbf),
+                                    _ptr(self.chalf), _ptr(self.shift2),
+                                    _lib.stream_handle(stream))
+        _lib.check(rc, "hbmr_kmeans_update")
+
+    def set_centroids(self, centroids: torch.Tensor, stream=None):
+        self.cen.copy_(centroids.to(self.cen.device, torch.float32))
+        self.refresh(stream=stream)
+
+    def max_shift(self) -> float:
+        return float(self.shift2.max().sqrt().item()) if self.k else 0.0
+
+
+def assign(points: torch.Tensor, img: CentroidImage, labels: torch.Tensor | None = None,
+           scores: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """labels[i] = argmin_j ||x_i - c_j||² (MFMA bf16 GEMM + fused arg-max)."""
+    n, dp = points.shape
+    if points.dtype != torch.bfloat16 or dp != img.dp or not points.is_contiguous():
+        raise ValueError("points must be contiguous bf16 [n, dp] matching the centroid image")
+    if labels is None:
+        labels = torch.empty(n, dtype=torch.int32, device=points.device)
+    lib = _lib.load()
+    rc = lib.hbmr_kmeans_assign_bf16(_ptr(points), n, dp, _ptr(img.cbf), _ptr(img.chalf),
+                                     img.k_pad, _ptr(labels), _ptr(scores),
+                                     _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_kmeans_assign_bf16")
+    return labels
+
+
+ACCUM_AUTO, ACCUM_LDS, ACCUM_SORTED = 0, 1, 2
+_workspaces: dict = {}
+
+
+def accum_workspace(n: int, k: int, device) -> torch.Tensor:
+    """Per-(device, stream-free) scratch for the sorted combiner, grown on demand.
+
+    Reused across calls on the same device; callers that run accumulations on
+    several streams concurrently must pass their own ``workspace``."""
+    lib = _lib.load()
+    need = int(lib.hbmr_kmeans_accum_workspace_bytes(n, k))
+    key = torch.device(device)
+    ws = _workspaces.get(key)
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(max(need, 1 << 20), dtype=torch.uint8, device=key)
+        _workspaces[key] = ws
+    return ws
+
+
+def accumulate(points: torch.Tensor, labels: torch.Tensor, k: int, sums: torch.Tensor,
+               counts: torch.Tensor, fx_shift: int = FX_SHIFT, stream=None,
+               workspace: torch.Tensor | None = None, mode: int = ACCUM_AUTO) -> None:
+    """sums[label] += round(x·2^fx_shift), counts[label] += 1 (int64 fixed point).
+
+    Small k uses LDS-privatised accumulators; large k a counting sort of the
+    labels followed by a segmented row sum (no atomics in the hot loop)."""
+    n, dp = points.shape
+    if sums.shape != (k, dp) or sums.dtype != torch.int64:
+        raise ValueError(f"sums must be int64 [{k}, {dp}]")
+    if counts.shape != (k,) or counts.dtype != torch.int64:
+        raise ValueError(f"counts must be int64 [{k}]")
+    lib = _lib.load()
+    if workspace is None and mode != ACCUM_LDS:
+        workspace = accum_workspace(n, k, points.device)
+    rc = lib.hbmr_kmeans_accum_bf16(_ptr(points), n, dp, _ptr(labels), k, _ptr(sums),
+                                    _ptr(counts), fx_shift, _ptr(workspace),
+                                    0 if workspace is None else workspace.numel(), mode,
+                                    _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_kmeans_accum_bf16")
+
+
+def map_split_gpu(points, img: CentroidImage, sums, counts, labels=None, stream=None):
+    """One GPU K-Means map task over an HBM-resident split: assign + combine."""
+    labels = assign(points, img, labels=labels, stream=stream)
+    accumulate(points, labels, img.k, sums, counts, fx_shift=img.fx_shift, stream=stream)
+    return labels
+
+
+def map_split_cpu(points: torch.Tensor, centroids: torch.Tensor, sums: torch.Tensor,
+                  counts: torch.Tensor, nthreads: int = 1, labels: torch.Tensor | None = None,
+                  fx_shift: int = FX_SHIFT):
+    """CPU K-Means map task (native C++, fp32 math, int64 fixed-point partials).
+
+    ``sums`` is int64 ``[k, d]`` (or ``[k, dp]``: only the first d columns are
+    touched).  Returns the partial cost Σ min_j ||x - c_j||².
+    """
+    x = points.detach().to(torch.float32).contiguous()
+    c = centroids.detach().to(torch.float32).contiguous()
+    n, d = x.shape
+    k = c.shape[0]
+    if counts.shape != (k,) or counts.dtype != torch.int64 or sums.dtype != torch.int64:
+        raise ValueError("sums/counts must be int64")
+    target = sums
+    if sums.shape != (k, d):
+        target = torch.zeros(k, d, dtype=torch.int64)
+    cost = ctypes.c_double(0.0)
+    lib = _lib.load()
+    rc = lib.hbmr_kmeans_map_cpu_f32(_ptr(x), n, d, _ptr(c), k, _ptr(labels), _ptr(target),
+                                     _ptr(counts), ctypes.byref(cost), fx_shift, int(nthreads))
+    _lib.check(rc, "hbmr_kmeans_map_cpu_f32")
+    if target is not sums:
+        sums[:, :d] += target
+    return cost.value

@@ -1,0 +1,136 @@
+"""Native build for hbmr: HIP kernels + C++ runtime pieces, gfx950 only.
+
+Produces (all in-tree so they travel to the GPU box with the repo snapshot):
+
+* ``hbmr/lib/libhbmr.so``      – HIP kernels (native/kernels/*.hip) + CPU kernels
+                                  and native I/O (native/cpu/*.cc), C ABI, loaded
+                                  by ``hbmr.ops`` via ctypes next to PyTorch.
+* ``hbmr/lib/libhbmr_pipes.a`` – the Pipes child-side runtime (native/pipes).
+* ``hbmr/bin/*``               – Pipes task executables (native/apps), e.g. the
+                                  HIP K-Means GPU map binary.
+
+No hipify, no CUDA shims: sources are HIP/C++ written for CDNA4 and compiled
+with ``hipcc --offload-arch=gfx950``.  Rebuilds are incremental on mtimes
+(headers included conservatively).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+NATIVE = ROOT / "native"
+BUILD = ROOT / "build" / "native"
+LIBDIR = ROOT / "hbmr" / "lib"
+BINDIR = ROOT / "hbmr" / "bin"
+ARCH = os.environ.get("HBMR_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CXX = os.environ.get("CXX", "g++")
+
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+             "-Wno-unused-result", "-Wno-unused-value", f"-I{NATIVE / 'include'}"]
+CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-mavx2", "-mfma", "-pthread",
+             f"-I{NATIVE / 'include'}", "-DHBMR_NO_HIP_DECLS"]
+
+
+def _headers(d: Path):
+    return [p for p in d.rglob("*.h")] + [p for p in d.rglob("*.hh")]
+
+
+def _stale(out: Path, deps) -> bool:
+    if not out.exists():
+        return True
+    t = out.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(str(c) for c in cmd), flush=True)
+    r = subprocess.run([str(c) for c in cmd], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"native build failed: {' '.join(map(str, cmd))}\n{r.stdout}\n{r.stderr}")
+    return r
+
+
+def _compile_jobs(srcs, compiler, flags, objdir, hdrs):
+    jobs = []
+    for s in srcs:
+        o = objdir / (s.relative_to(NATIVE).as_posix().replace("/", "__") + ".o")
+        if _stale(o, [s, *hdrs, Path(__file__)]):
+            jobs.append((s, o, [compiler, *flags, "-c", s, "-o", o]))
+        else:
+            jobs.append((s, o, None))
+    return jobs
+
+
+def build(verbose: bool = False, jobs: int | None = None) -> dict:
+    BUILD.mkdir(parents=True, exist_ok=True)
+    LIBDIR.mkdir(parents=True, exist_ok=True)
+    BINDIR.mkdir(parents=True, exist_ok=True)
+    hdrs = _headers(NATIVE)
+    hip_srcs = sorted((NATIVE / "kernels").glob("*.hip"))
+    cpu_srcs = sorted((NATIVE / "cpu").glob("*.cc"))
+    pipes_srcs = sorted((NATIVE / "pipes").rglob("*.cc"))
+
+    work = []
+    work += _compile_jobs(hip_srcs, HIPCC, HIP_FLAGS, BUILD, hdrs)
+    work += _compile_jobs(cpu_srcs, CXX, CXX_FLAGS, BUILD, hdrs)
+    pipes_flags = CXX_FLAGS + [f"-I{NATIVE / 'pipes' / 'api'}", f"-I{NATIVE / 'pipes'}"]
+    work += _compile_jobs(pipes_srcs, CXX, pipes_flags, BUILD, hdrs)
+
+    n = jobs or min(8, os.cpu_count() or 4)
+    todo = [w for w in work if w[2] is not None]
+    with cf.ThreadPoolExecutor(max_workers=n) as ex:
+        list(ex.map(lambda w: _run(w[2], verbose), todo))
+
+    objs = {s: o for s, o, _ in work}
+    lib = LIBDIR / "libhbmr.so"
+    lib_objs = [objs[s] for s in hip_srcs + cpu_srcs]
+    if _stale(lib, lib_objs):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *lib_objs,
+              "-pthread"], verbose)
+
+    out = {"libhbmr": str(lib)}
+    if pipes_srcs:
+        alib = LIBDIR / "libhbmr_pipes.a"
+        pobjs = [objs[s] for s in pipes_srcs]
+        if _stale(alib, pobjs):
+            if alib.exists():
+                alib.unlink()
+            _run(["ar", "rcs", alib, *pobjs], verbose)
+        out["libhbmr_pipes"] = str(alib)
+        out.update(_build_apps(verbose, lib, alib, hdrs))
+    return out
+
+
+def _build_apps(verbose, lib, alib, hdrs):
+    """Each native/apps/<name>.cc (CPU) or .hip (GPU) becomes hbmr/bin/<name>."""
+    apps = {}
+    srcs = sorted((NATIVE / "apps").glob("*.cc")) + sorted((NATIVE / "apps").glob("*.hip"))
+    inc = [f"-I{NATIVE / 'include'}", f"-I{NATIVE / 'pipes' / 'api'}", f"-I{NATIVE / 'pipes'}"]
+    cmds = []
+    for s in srcs:
+        exe = BINDIR / s.stem
+        deps = [s, alib, *hdrs]
+        if s.suffix == ".hip":
+            deps.append(lib)
+            cmd = [HIPCC, *HIP_FLAGS, *inc, s, "-o", exe, alib, f"-L{LIBDIR}", "-lhbmr",
+                   f"-Wl,-rpath,$ORIGIN/../lib", "-pthread"]
+        else:
+            cmd = [CXX, *CXX_FLAGS, *inc, s, "-o", exe, alib, "-pthread"]
+        apps[s.stem] = str(exe)
+        if _stale(exe, deps):
+            cmds.append(cmd)
+    n = min(8, os.cpu_count() or 4)
+    with cf.ThreadPoolExecutor(max_workers=n) as ex:
+        list(ex.map(lambda c: _run(c, verbose), cmds))
+    return {"apps": apps}
+
+
+if __name__ == "__main__":
+    res = build(verbose="-v" in sys.argv)
+    print(res)

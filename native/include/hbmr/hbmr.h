@@ -1,0 +1,41 @@
+// hbmr native C API (libhbmr.so).
+//
+// GPU entry points take raw device pointers and the hipStream_t to launch on;
+// they return 0 on success or a hipError_t code.  CPU entry points return 0 on
+// success or a negative errno-style code.  The Python runtime binds these with
+// ctypes (hbmr/ops/_lib.py); the Pipes GPU task binaries link the same objects.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* hbmr_stream_t;
+
+// ---- K-Means (native/kernels/kmeans.hip) -----------------------------------
+#ifndef HBMR_NO_HIP_DECLS
+#include <hip/hip_runtime_api.h>
+int hbmr_kmeans_assign_bf16(const void* X, long n, int dp, const void* C, const float* chalf,
+                            int k_pad, int32_t* labels, float* scores, hipStream_t st);
+// sums/counts are 64-bit fixed point: sum = Σ round(x · 2^fx_shift)
+// mode 0 = auto, 1 = LDS-privatised, 2 = counting-sort + segmented sum (needs workspace)
+int hbmr_kmeans_accum_bf16(const void* X, long n, int dp, const int32_t* labels, int k,
+                           long long* sums, long long* counts, int fx_shift, void* ws,
+                           long ws_bytes, int mode, hipStream_t st);
+int hbmr_kmeans_update(const long long* sums, const long long* counts, int fx_shift, int k, int d,
+                       int dp, int k_pad, float* cen, void* cbf, float* chalf, float* shift2,
+                       hipStream_t st);
+#endif
+int hbmr_kmeans_padded_k(int k);
+long hbmr_kmeans_accum_workspace_bytes(long n, int k);
+
+// ---- CPU kernels (native/cpu) ------------------------------------------------
+int hbmr_kmeans_map_cpu_f32(const float* X, long n, int d, const float* C, int k,
+                            int32_t* labels, long long* sums, long long* counts, double* cost,
+                            int fx_shift, int nthreads);
+
+#ifdef __cplusplus
+}
+#endif

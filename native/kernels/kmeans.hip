@@ -1,0 +1,780 @@
+// K-Means map-side kernels for MI355X (gfx950).
+//
+// These are the GPU "map function + combiner" of a K-Means MapReduce
+// iteration.  In the reference the GPU map task is an external Pipes binary
+// launched per task (hadoop-1.0.3/src/mapred/org/apache/hadoop/mapred/pipes/
+// Application.java:162-181, PipesGPUMapRunner.java:66-118) and the combiner is
+// the C++ CombineRunner (src/c++/pipes/impl/HadoopPipes.cc:660-705); there is no
+// GPU code in the reference, so these kernels are designed from scratch
+// (SURVEY.md §2.11 K1-K3).
+//
+//  kmeans_assign   : labels[i] = argmin_j ||x_i - c_j||^2 computed as an MFMA
+//                    GEMM  S = C · Xᵀ  (v_mfma_f32_32x32x16_bf16, fp32 accum)
+//                    with the centroid tiles staged in LDS by global_load_lds
+//                    and a fused running-argmax epilogue on
+//                    score = x·c - ||c||²/2 (the -||c||²/2 term is loaded as
+//                    the MFMA's initial accumulator, so no subtraction).
+//                    Points sit on the MFMA *column* (lane) axis so each
+//                    lane's arg-max is register-local: no cross-lane
+//                    reduction until the very end.
+//  kmeans_accum_*  : per-cluster partial sums / counts (the combiner) with
+//                    LDS-privatised accumulators; one global atomic flush per
+//                    workgroup instead of one per point (global f32 atomics
+//                    run at ≈1.3 TB/s chip-wide: MI355X_MICROARCH.md).
+//  kmeans_update   : reduce side: c_j = sum_j / count_j, emits the bf16
+//                    centroid image + -||c||²/2 for the next iteration.
+#include "common.h"
+#include "../include/hbmr/hbmr.h"
+#include <algorithm>
+
+namespace {
+
+constexpr int kWaves = 4;
+constexpr int kThreads = kWaves * HBMR_WAVE;
+constexpr int kCK = 64;  // clusters per LDS chunk (two 32-row MFMA blocks)
+
+template <int D> struct AssignCfg {
+  static constexpr int KS = D / 16;             // MFMA k-steps (K=16 each)
+  static constexpr int CPR = D / 8;             // 16-byte pieces per row
+  static constexpr int SWZ = CPR >= 16 ? 15 : CPR - 1;
+  static constexpr int PB = D <= 128 ? 2 : 1;   // 32-point blocks per wave
+  static constexpr int PTS = kWaves * PB * 32;  // points per workgroup
+  static constexpr int CHUNK_BYTES = kCK * D * 2;
+  static constexpr int BUF_BYTES = CHUNK_BYTES + kCK * 4;
+  static constexpr int LDS_BYTES = 2 * BUF_BYTES;
+};
+
+// Stage centroid chunk `chunk` (kCK rows × D bf16) plus its -||c||²/2 values
+// into LDS buffer `buf`.  The LDS image is lane-linear (global_load_lds writes
+// base + lane*16) so the bank-conflict XOR swizzle is applied to the SOURCE
+// address: LDS piece (row, p) holds global piece (row, p ^ (row & SWZ))
+// (cdna_hip_programming.md §5.4 rule 21).
+template <int D>
+__device__ __forceinline__ void stage_chunk(char* buf, const __bf16* __restrict__ C,
+                                            const float* __restrict__ chalf, int chunk,
+                                            int wave, int lane) {
+  using Cfg = AssignCfg<D>;
+  constexpr int PIECES = kCK * Cfg::CPR;  // 16-B pieces in the chunk
+  constexpr int ROUNDS = PIECES / kThreads;
+  static_assert(PIECES % kThreads == 0, "chunk must tile the workgroup");
+  const char* gbase = reinterpret_cast<const char*>(C) + (size_t)chunk * Cfg::CHUNK_BYTES;
+#pragma unroll
+  for (int i = 0; i < ROUNDS; ++i) {
+    const int base = (i * kWaves + wave) * HBMR_WAVE;
+    const int p = base + lane;
+    const int row = p / Cfg::CPR;
+    const int cpos = p % Cfg::CPR;
+    const int src = cpos ^ (row & Cfg::SWZ);
+    const char* g = gbase + row * (D * 2) + src * 16;
+    __builtin_amdgcn_global_load_lds((const void*)g, (void*)(buf + base * 16), 16, 0, 0);
+  }
+  if (wave == 0) {
+    const float* g = chalf + (size_t)chunk * kCK + lane;
+    __builtin_amdgcn_global_load_lds((const void*)g, (void*)(buf + Cfg::CHUNK_BYTES), 4, 0, 0);
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(kThreads, 2) void kmeans_assign_kernel(
+    const __bf16* __restrict__ X, long n, const __bf16* __restrict__ C,
+    const float* __restrict__ chalf, int nchunks, int32_t* __restrict__ labels,
+    float* __restrict__ scores) {
+  using Cfg = AssignCfg<D>;
+  constexpr int KS = Cfg::KS, PB = Cfg::PB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / HBMR_WAVE);
+  const int lane = tid & (HBMR_WAVE - 1);
+  const int h = lane >> 5;   // lane half: selects k-offset 8h in A/B fragments
+  const int col = lane & 31;
+  const long blk = hbmr_xcd_remap(blockIdx.x, gridDim.x);
+  const long p0 = blk * Cfg::PTS + (long)wave * PB * 32;
+
+  // Kick off chunk 0 first so it overlaps the point-fragment loads.
+  stage_chunk<D>(smem, C, chalf, 0, wave, lane);
+
+  // B operand = points: lane holds X[p][16s + 8h .. +7] for its column p.
+  bf16x8 bfrag[PB][KS];
+#pragma unroll
+  for (int pb = 0; pb < PB; ++pb) {
+    long p = p0 + pb * 32 + col;
+    if (p >= n) p = n - 1;
+    const uint4* row = reinterpret_cast<const uint4*>(X + p * D);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      uint4 v = row[2 * s + h];
+      bfrag[pb][s] = __builtin_bit_cast(bf16x8, v);
+    }
+  }
+
+  float best[PB][16];
+#pragma unroll
+  for (int pb = 0; pb < PB; ++pb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) best[pb][r] = -3.0e38f;
+
+  // Retire the fragment loads here and launder the registers through an asm
+  // so hipcc's waitcnt pass does not see them as pending inside the chunk loop
+  // (it would otherwise emit vmcnt(0) at the first MFMA and drain the next
+  // chunk's global_load_lds prefetch every iteration).
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  uint32_t vmask;
+  asm volatile("v_mov_b32 %0, 0xffffff00" : "=v"(vmask));
+#pragma unroll
+  for (int pb = 0; pb < PB; ++pb)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(bfrag[pb][s]));
+  __syncthreads();
+
+  for (int c = 0; c < nchunks; ++c) {
+    char* cur = smem + (c & 1) * Cfg::BUF_BYTES;
+    if (c + 1 < nchunks)
+      stage_chunk<D>(smem + ((c + 1) & 1) * Cfg::BUF_BYTES, C, chalf, c + 1, wave, lane);
+    const float* ch = reinterpret_cast<const float*>(cur + Cfg::CHUNK_BYTES);
+#pragma unroll
+    for (int cb = 0; cb < kCK / 32; ++cb) {
+      f32x16 acc[PB];
+      // Initial accumulator = -||c||²/2 of the cluster on this register's row:
+      // row(reg, lane) = (reg & 3) + 8 * (reg >> 2) + 4 * h.
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(ch + cb * 32 + 8 * g + 4 * h);
+#pragma unroll
+        for (int pb = 0; pb < PB; ++pb) {
+          acc[pb][4 * g + 0] = v[0];
+          acc[pb][4 * g + 1] = v[1];
+          acc[pb][4 * g + 2] = v[2];
+          acc[pb][4 * g + 3] = v[3];
+        }
+      }
+      const int arow = cb * 32 + col;
+      const char* abase = cur + arow * (D * 2);
+      const int aswz = arow & Cfg::SWZ;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int q = 2 * s + h;
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(abase + ((q ^ aswz) << 4));
+#pragma unroll
+        for (int pb = 0; pb < PB; ++pb)
+          acc[pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfrag[pb][s], acc[pb], 0, 0, 0);
+      }
+      // Running arg-max per register slot: the 32-cluster tile index is packed
+      // into the low 8 mantissa bits (2^-15 relative, far below the bf16
+      // operand rounding of 2^-9), so one v_and_or + one v_max per element.
+      const uint32_t tcode = 255u - (uint32_t)(c * (kCK / 32) + cb);
+#pragma unroll
+      for (int pb = 0; pb < PB; ++pb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          // hi_mask lives in a VGPR (vmask) so the selector can form one
+          // v_and_or_b32 (VOP3 may read only one SGPR on gfx950); the op itself
+          // stays compiler-visible so MFMA->VALU hazards are padded.
+          const uint32_t u = (__float_as_uint(acc[pb][r]) & vmask) | tcode;
+          best[pb][r] = __builtin_fmaxf(best[pb][r], __uint_as_float(u));
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+
+  // Finish: arg-max over the 16 register slots, then across the lane halves.
+#pragma unroll
+  for (int pb = 0; pb < PB; ++pb) {
+    float bv = best[pb][0];
+    int br = 0;
+#pragma unroll
+    for (int r = 1; r < 16; ++r)
+      if (best[pb][r] > bv) { bv = best[pb][r]; br = r; }
+    const uint32_t bu = __float_as_uint(bv);
+    const int tile = 255 - (int)(bu & 0xffu);
+    int cluster = tile * 32 + (br & 3) + 8 * (br >> 2) + 4 * h;
+    float ov = __shfl_xor(bv, 32);
+    int oc = __shfl_xor(cluster, 32);
+    if (ov > bv || (ov == bv && oc < cluster)) { bv = ov; cluster = oc; }
+    const long p = p0 + pb * 32 + col;
+    if (h == 0 && p < n) {
+      labels[p] = cluster;
+      if (scores) scores[p] = __uint_as_float(__float_as_uint(bv) & 0xffffff00u);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Combiner: per-cluster sums and counts, LDS-privatised, in 64-bit FIXED POINT.
+//
+// gfx950 executes ds_add_f32 at ~0.4 lane-ops/clk/CU versus ~14.5 for
+// ds_add_u32 (tools/ubench_lds_atomics.hip, profiles/lds_atomics.txt), so the
+// partial sums are accumulated as int64 = round(x · 2^shift) with integer LDS
+// atomics (ds_add_u64) and flushed with integer global atomics.  Integer sums
+// are associative: the combiner output is bitwise identical for any task
+// placement, kernel schedule or GPU count (and stays exact through the RCCL
+// all-reduce).  bf16 inputs are exact in fixed point whenever |x| ≥ 2^(shift-31)
+// ... i.e. every bf16 with ulp ≥ 2^-shift (shift = 24: |x| ≥ 2^-17).
+//
+// LDS image of the sums: element (row r, dim i) at r*RS + i + (i >> 3) (u64
+// units).  A point is handled by D/8 lanes, lane `sub` owning dims
+// [8 sub, 8 sub + 8) (one 16-B global load); at step j the 16 lanes of a point
+// touch dwords 2(9 sub + j) + {0,1}: all 32 banks exactly once.
+typedef unsigned long long u64;
+
+template <int D> struct AccCfg {
+  static constexpr int RS = D + D / 8 + 1;  // padded row stride (u64 elements)
+  static constexpr int TPP = D / 8;         // lanes per point
+};
+
+template <int D>
+__device__ __forceinline__ void lds_add_row(u64* s_rows, int r, int sub, const uint4 v,
+                                            float scale) {
+  float f[8];
+  hbmr_unpack8(v, f);
+  u64* dst = s_rows + r * AccCfg<D>::RS + sub * 9;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const long long q = __float2ll_rn(f[j] * scale);
+    if (q) atomicAdd(dst + j, (u64)q);
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void flush_rows(const u64* s_rows, const uint32_t* s_cnt, int c0, int cc,
+                                           long long* __restrict__ sums,
+                                           long long* __restrict__ counts, int tid, int nt) {
+  for (int e = tid; e < cc * D; e += nt) {
+    const int r = e / D, i = e % D;
+    const u64 v = s_rows[r * AccCfg<D>::RS + i + (i >> 3)];
+    if (v) atomicAdd(reinterpret_cast<u64*>(sums) + (size_t)(c0 + r) * D + i, v);
+  }
+  for (int r = tid; r < cc; r += nt) {
+    const uint32_t v = s_cnt[r];
+    if (v) atomicAdd(reinterpret_cast<u64*>(counts) + c0 + r, (u64)v);
+  }
+}
+
+// Small k: every workgroup holds all k rows in LDS; grid-stride over points.
+// Each lane group keeps U rows (and labels) in flight before its LDS adds.
+template <int D, int U>
+__global__ __launch_bounds__(256) void kmeans_accum_lds_kernel(
+    const __bf16* __restrict__ X, long n, const int32_t* __restrict__ labels, int k,
+    long long* __restrict__ sums, long long* __restrict__ counts, float scale) {
+  using A = AccCfg<D>;
+  extern __shared__ __attribute__((aligned(16))) u64 s_acc[];  // k*RS sums, then k counts
+  const int tid = threadIdx.x;
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_acc + k * A::RS);
+  for (int i = tid; i < k * A::RS; i += 256) s_acc[i] = 0ull;
+  for (int i = tid; i < k; i += 256) s_cnt[i] = 0u;
+  __syncthreads();
+  constexpr int PPI = 256 / A::TPP;  // point slots per workgroup
+  const int sub = tid % A::TPP;
+  const int pi = tid / A::TPP;
+  const long stride = (long)gridDim.x * PPI;
+  long p = (long)blockIdx.x * PPI + pi;
+  for (; p + (U - 1) * stride < n; p += U * stride) {
+    int lab[U];
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      lab[u] = labels[p + u * stride];
+      v[u] = reinterpret_cast<const uint4*>(X + (p + u * stride) * D)[sub];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      lds_add_row<D>(s_acc, lab[u], sub, v[u], scale);
+      if (sub == 0) atomicAdd(s_cnt + lab[u], 1u);
+    }
+  }
+  for (; p < n; p += stride) {
+    const int l0 = labels[p];
+    lds_add_row<D>(s_acc, l0, sub, reinterpret_cast<const uint4*>(X + p * D)[sub], scale);
+    if (sub == 0) atomicAdd(s_cnt + l0, 1u);
+  }
+  __syncthreads();
+  flush_rows<D>(s_acc, s_cnt, 0, k, sums, counts, tid, 256);
+}
+
+// Large k: grid.y walks cluster chunks of CC clusters.  Each wave scans 256
+// labels per step (one int4 per lane), compacts the points whose label falls in
+// this workgroup's chunk into a wave-private LDS queue (ballot + prefix count),
+// then drains the queue with U rows in flight per lane group.  Every row is
+// gathered exactly once over the whole grid; labels are re-read per chunk
+// (from L2 / Infinity Cache when the split is small, as map splits are).
+constexpr int kAccWaves = 8;
+constexpr int kQueue = 256;  // queue entries per wave (one step's worth)
+
+template <int D, int U>
+__global__ __launch_bounds__(512) void kmeans_accum_chunked_kernel(
+    const __bf16* __restrict__ X, long n, const int32_t* __restrict__ labels, int k, int CC,
+    long pts_per_block, long long* __restrict__ sums, long long* __restrict__ counts,
+    float scale) {
+  using A = AccCfg<D>;
+  extern __shared__ __attribute__((aligned(16))) u64 s_acc[];
+  // layout: CC*RS u64 sums | kAccWaves*kQueue u32 queue | CC u32 counts
+  constexpr int NT = kAccWaves * HBMR_WAVE;
+  const int tid = threadIdx.x;
+  const int c0 = blockIdx.y * CC;
+  const int cc = min(CC, k - c0);
+  for (int i = tid; i < CC * A::RS; i += NT) s_acc[i] = 0ull;
+  uint32_t* s_q = reinterpret_cast<uint32_t*>(s_acc + CC * A::RS);
+  uint32_t* s_cnt = s_q + kAccWaves * kQueue;
+  for (int i = tid; i < CC; i += NT) s_cnt[i] = 0u;
+  __syncthreads();
+  const int wave = tid / HBMR_WAVE, lane = tid & 63;
+  uint32_t* q = s_q + wave * kQueue;
+  constexpr int GPW = HBMR_WAVE / A::TPP;  // points per wave-instruction
+  const int grp = lane / A::TPP, sub = lane % A::TPP;
+  const unsigned long long lt_mask = (1ull << lane) - 1ull;
+  const long pb = (long)blockIdx.x * pts_per_block;
+  const long pe = min(n, pb + pts_per_block);
+  for (long base = pb + (long)wave * kQueue; base < pe; base += (long)kAccWaves * kQueue) {
+    int lab[4];
+    const long p4 = base + 4 * lane;
+    if (p4 + 3 < pe) {
+      const int4 l4 = *reinterpret_cast<const int4*>(labels + p4);
+      lab[0] = l4.x; lab[1] = l4.y; lab[2] = l4.z; lab[3] = l4.w;
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) lab[t] = (p4 + t < pe) ? labels[p4 + t] : -1;
+    }
+    int cnt = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int rel = lab[t] - c0;
+      const bool mine = (unsigned)rel < (unsigned)cc;
+      const unsigned long long m = __ballot(mine);
+      if (mine) q[cnt + __popcll(m & lt_mask)] = ((uint32_t)(4 * lane + t) << 16) | (uint32_t)rel;
+      cnt += __popcll(m);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    for (int e = 0; e < cnt; e += U * GPW) {
+      uint4 v[U];
+      uint32_t ent[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int idx = e + u * GPW + grp;
+        ent[u] = idx < cnt ? q[idx] : 0xffffffffu;
+        if (ent[u] != 0xffffffffu)
+          v[u] = reinterpret_cast<const uint4*>(X + (base + (ent[u] >> 16)) * D)[sub];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (ent[u] != 0xffffffffu) {
+          const int r = (int)(ent[u] & 0xffffu);
+          lds_add_row<D>(s_acc, r, sub, v[u], scale);
+          if (sub == 0) atomicAdd(s_cnt + r, 1u);
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  flush_rows<D>(s_acc, s_cnt, c0, cc, sums, counts, tid, NT);
+}
+
+// ---------------------------------------------------------------------------
+// Sorted (counting-sort) combiner for large k: no LDS float/int atomics in
+// the hot loop at all.
+//   1. kmeans_hist      : hist[label]++            (LDS u32 atomics, 1/point)
+//   2. kmeans_scan      : offsets = exclusive_scan(hist); cursor = offsets;
+//                         counts += hist
+//   3. kmeans_scatter   : perm[offsets[l] + rank] = i, rank from a per-block
+//                         LDS histogram (ds_add_rtn_u32) + one global atomic
+//                         per (block, present label)
+//   4. kmeans_segsum    : walk perm in order; each 16-lane group accumulates
+//                         whole rows of one cluster in int64 registers and
+//                         flushes once per cluster run (global u64 atomics).
+// The gather in (4) re-reads each row once; run right after the assign kernel
+// on a split of ≤ ~128 MB the rows come from the 256 MiB Infinity Cache.
+constexpr int kScatterPts = 4096;  // points per scatter workgroup (16 per thread)
+
+__global__ __launch_bounds__(256) void kmeans_hist_kernel(const int32_t* __restrict__ labels,
+                                                          long n, int k,
+                                                          uint32_t* __restrict__ hist) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];
+  for (int i = threadIdx.x; i < k; i += 256) s_h[i] = 0u;
+  __syncthreads();
+  const long n4 = n / 4;
+  const int4* l4 = reinterpret_cast<const int4*>(labels);
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    const int4 v = l4[i];
+    atomicAdd(s_h + v.x, 1u);
+    atomicAdd(s_h + v.y, 1u);
+    atomicAdd(s_h + v.z, 1u);
+    atomicAdd(s_h + v.w, 1u);
+  }
+  if (blockIdx.x == 0)
+    for (long i = n4 * 4 + threadIdx.x; i < n; i += 256) atomicAdd(s_h + labels[i], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i < k; i += 256)
+    if (s_h[i]) atomicAdd(hist + i, s_h[i]);
+}
+
+// single workgroup: exclusive scan of hist (k ≤ 1024*64), counts += hist
+__global__ __launch_bounds__(1024) void kmeans_scan_kernel(const uint32_t* __restrict__ hist,
+                                                           int k, uint32_t* __restrict__ offsets,
+                                                           uint32_t* __restrict__ cursor,
+                                                           long long* __restrict__ counts) {
+  __shared__ uint32_t s_part[1024];
+  const int t = threadIdx.x;
+  const int per = (k + 1023) / 1024;
+  const int lo = min(k, t * per), hi = min(k, lo + per);
+  uint32_t s = 0;
+  for (int i = lo; i < hi; ++i) s += hist[i];
+  s_part[t] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+    const uint32_t v = t >= off ? s_part[t - off] : 0u;
+    __syncthreads();
+    s_part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = s_part[t] - s;  // exclusive prefix of this thread's range
+  for (int i = lo; i < hi; ++i) {
+    const uint32_t h = hist[i];
+    offsets[i] = run;
+    cursor[i] = run;
+    if (counts) counts[i] += h;
+    run += h;
+  }
+  if (t == 1023) offsets[k] = s_part[1023];
+}
+
+__global__ __launch_bounds__(256) void kmeans_scatter_kernel(const int32_t* __restrict__ labels,
+                                                             long n, int k,
+                                                             uint32_t* __restrict__ cursor,
+                                                             uint32_t* __restrict__ perm) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];  // k counters, then k bases
+  uint32_t* s_base = s_h + k;
+  const int t = threadIdx.x;
+  for (int i = t; i < k; i += 256) s_h[i] = 0u;
+  __syncthreads();
+  constexpr int PER = kScatterPts / 256;
+  const long p0 = (long)blockIdx.x * kScatterPts + (long)t * PER;
+  int lab[PER];
+  uint32_t rank[PER];
+#pragma unroll
+  for (int j = 0; j < PER; j += 4) {
+    if (p0 + j + 3 < n) {
+      const int4 v = *reinterpret_cast<const int4*>(labels + p0 + j);
+      lab[j] = v.x; lab[j + 1] = v.y; lab[j + 2] = v.z; lab[j + 3] = v.w;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) lab[j + q] = (p0 + j + q < n) ? labels[p0 + j + q] : -1;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) rank[j] = lab[j] >= 0 ? atomicAdd(s_h + lab[j], 1u) : 0u;
+  __syncthreads();
+  for (int i = t; i < k; i += 256) {
+    const uint32_t c = s_h[i];
+    s_base[i] = c ? atomicAdd(cursor + i, c) : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    if (lab[j] >= 0) perm[s_base[lab[j]] + rank[j]] = (uint32_t)(p0 + j);
+}
+
+template <int D, int U>
+__global__ __launch_bounds__(256) void kmeans_segsum_kernel(
+    const __bf16* __restrict__ X, long n, const uint32_t* __restrict__ perm,
+    const uint32_t* __restrict__ offsets, int k, long chunk, long long* __restrict__ sums,
+    float scale) {
+  constexpr int TPP = D / 8;              // lanes per row
+  constexpr int GPW = HBMR_WAVE / TPP;    // row groups per wave
+  const int lane = threadIdx.x & 63;
+  const int grp = lane / TPP, sub = lane % TPP;
+  const long wid = (long)blockIdx.x * (blockDim.x / HBMR_WAVE) + threadIdx.x / HBMR_WAVE;
+  const long s = wid * chunk;
+  if (s >= n) return;
+  const long e = min(n, s + chunk);
+  // first cluster whose segment contains position s: upper_bound(offsets, s) - 1
+  int lo = 0, hi = k;  // invariant offsets[lo] <= s < offsets[hi] (offsets[k] = n)
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if ((long)offsets[mid] <= s) lo = mid; else hi = mid;
+  }
+  int cur = lo;
+  long bound = offsets[cur + 1];
+  long long acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0;
+  auto flush = [&]() {
+    u64* dst = reinterpret_cast<u64*>(sums) + (size_t)cur * D + sub * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (acc[j]) atomicAdd(dst + j, (u64)acc[j]);
+      acc[j] = 0;
+    }
+  };
+  for (long base = s + grp; base < e; base += (long)U * GPW) {
+    uint32_t idx[U];
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long p = base + (long)u * GPW;
+      idx[u] = p < e ? perm[p] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long p = base + (long)u * GPW;
+      if (p < e) v[u] = reinterpret_cast<const uint4*>(X + (size_t)idx[u] * D)[sub];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long p = base + (long)u * GPW;
+      if (p < e) {
+        while (p >= bound) {
+          flush();
+          ++cur;
+          bound = offsets[cur + 1];
+        }
+        float f[8];
+        hbmr_unpack8(v[u], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += __float2ll_rn(f[j] * scale);
+      }
+    }
+  }
+  // Final flush: when every group of the wave ended in the same cluster (the
+  // common case), reduce across groups in registers first so one group issues
+  // the atomics.
+  const int c0 = __shfl(cur, 0);
+  if (__all(cur == c0)) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+      for (int off = TPP; off < HBMR_WAVE; off <<= 1) {
+        const long long o = __shfl_xor(acc[j], off);
+        acc[j] += o;
+      }
+    }
+    if (grp == 0) flush();
+  } else {
+    flush();
+  }
+}
+
+// Reduce side + next-iteration prep.  One workgroup per cluster.
+// sums are fixed-point int64 [k, dp], counts int64 [k].
+__global__ __launch_bounds__(128) void kmeans_update_kernel(
+    const long long* __restrict__ sums, const long long* __restrict__ counts, int k, int d,
+    int dp, float inv_scale, float* __restrict__ cen, __bf16* __restrict__ cbf,
+    float* __restrict__ chalf, float* __restrict__ shift2) {
+  const int j = blockIdx.x;
+  const int tid = threadIdx.x;
+  __shared__ float red[2][128];
+  const long long cnt = counts ? counts[j] : 0;
+  const double inv = cnt > 0 ? (double)inv_scale / (double)cnt : 0.0;
+  float nrm = 0.f, dsq = 0.f;
+  uint16_t* cb = reinterpret_cast<uint16_t*>(cbf) + (size_t)j * dp;
+  for (int i = tid; i < dp; i += 128) {
+    float v = 0.f;
+    if (i < d) {
+      const float old = cen[(size_t)j * d + i];
+      v = cnt > 0 ? (float)((double)sums[(size_t)j * dp + i] * inv) : old;
+      dsq += (v - old) * (v - old);
+      cen[(size_t)j * d + i] = v;
+    }
+    const uint16_t b = hbmr_f32_to_bf16(v);
+    cb[i] = b;
+    const float vb = hbmr_bf16_to_f32(b);
+    nrm += vb * vb;
+  }
+  red[0][tid] = nrm;
+  red[1][tid] = dsq;
+  __syncthreads();
+  for (int s = 64; s > 0; s >>= 1) {
+    if (tid < s) {
+      red[0][tid] += red[0][tid + s];
+      red[1][tid] += red[1][tid + s];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    chalf[j] = -0.5f * red[0][0];
+    if (shift2) shift2[j] = red[1][0];
+  }
+}
+
+__global__ void kmeans_pad_clusters_kernel(__bf16* cbf, float* chalf, int k, int k_pad, int dp) {
+  const int j = k + blockIdx.x;
+  if (j >= k_pad) return;
+  uint16_t* cb = reinterpret_cast<uint16_t*>(cbf) + (size_t)j * dp;
+  for (int i = threadIdx.x; i < dp; i += blockDim.x) cb[i] = 0;
+  if (threadIdx.x == 0) chalf[j] = -1.0e30f;
+}
+
+template <int D>
+int launch_assign(const void* X, long n, const void* C, const float* chalf, int k_pad,
+                  int32_t* labels, float* scores, hipStream_t st) {
+  using Cfg = AssignCfg<D>;
+  if (n <= 0) return 0;
+  if (k_pad % kCK) return (int)hipErrorInvalidValue;
+  const long nblk = (n + Cfg::PTS - 1) / Cfg::PTS;
+  if (nblk > 0x7fffffffL) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kmeans_assign_kernel<D>, dim3((unsigned)nblk), dim3(kThreads),
+                     Cfg::LDS_BYTES, st, reinterpret_cast<const __bf16*>(X), n,
+                     reinterpret_cast<const __bf16*>(C), chalf, k_pad / kCK, labels, scores);
+  return (int)hipGetLastError();
+}
+
+template <int D>
+int launch_accum(const void* Xv, long n, const int32_t* labels, int k, long long* sums,
+                 long long* counts, float scale, int num_cu, hipStream_t st) {
+  using A = AccCfg<D>;
+  if (n <= 0) return 0;
+  const __bf16* X = reinterpret_cast<const __bf16*>(Xv);
+  const size_t small_bytes = (size_t)k * A::RS * 8 + (size_t)k * 4;
+  if (small_bytes <= 76 * 1024) {
+    constexpr int U = 8;
+    const long per_block = 256 / A::TPP * U;
+    long grid = std::min<long>((n + per_block - 1) / per_block, (long)num_cu * 2);
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL((kmeans_accum_lds_kernel<D, U>), dim3((unsigned)grid), dim3(256),
+                       small_bytes, st, X, n, labels, k, sums, counts, scale);
+  } else {
+    // one workgroup per CU: CC u64 rows + queues + counts within ~150 KiB
+    constexpr int U = 8;
+    const size_t qbytes = (size_t)kAccWaves * kQueue * 4;
+    int CC = (int)((150 * 1024 - qbytes) / ((size_t)A::RS * 8 + 4));
+    CC = (CC / 8) * 8;
+    if (CC > k) CC = k;
+    const int nchunk = (k + CC - 1) / CC;
+    long nb = ((long)num_cu + nchunk - 1) / nchunk;
+    long ppb = (n + nb - 1) / nb;
+    ppb = ((ppb + 2047) / 2048) * 2048;
+    nb = (n + ppb - 1) / ppb;
+    const size_t lds = (size_t)CC * A::RS * 8 + qbytes + (size_t)CC * 4;
+    hipLaunchKernelGGL((kmeans_accum_chunked_kernel<D, U>), dim3((unsigned)nb, (unsigned)nchunk),
+                       dim3(kAccWaves * HBMR_WAVE), lds, st, X, n, labels, k, CC, ppb, sums,
+                       counts, scale);
+  }
+  return (int)hipGetLastError();
+}
+
+int cu_count() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
+bool set_lds_limits() {
+  // Opt every kernel that asks for >64 KiB of dynamic LDS into the full 160 KiB.
+  static bool done = false;
+  if (!done) {
+#define HBMR_LDS_OPTIN(fn) hipFuncSetAttribute((const void*)(fn), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)
+    HBMR_LDS_OPTIN((kmeans_accum_lds_kernel<64, 8>));
+    HBMR_LDS_OPTIN((kmeans_accum_lds_kernel<128, 8>));
+    HBMR_LDS_OPTIN((kmeans_accum_lds_kernel<256, 8>));
+    HBMR_LDS_OPTIN((kmeans_accum_chunked_kernel<64, 8>));
+    HBMR_LDS_OPTIN((kmeans_accum_chunked_kernel<128, 8>));
+    HBMR_LDS_OPTIN((kmeans_accum_chunked_kernel<256, 8>));
+#undef HBMR_LDS_OPTIN
+    done = true;
+  }
+  return done;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hbmr_kmeans_assign_bf16(const void* X, long n, int dp, const void* C, const float* chalf,
+                            int k_pad, int32_t* labels, float* scores, hipStream_t st) {
+  switch (dp) {
+    case 64: return launch_assign<64>(X, n, C, chalf, k_pad, labels, scores, st);
+    case 128: return launch_assign<128>(X, n, C, chalf, k_pad, labels, scores, st);
+    case 256: return launch_assign<256>(X, n, C, chalf, k_pad, labels, scores, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+// Workspace of the sorted combiner: hist[k] | offsets[k+1] | cursor[k] | perm[n]
+// (u32 each, regions 256-B aligned).
+static size_t ws_align(size_t b) { return (b + 255) & ~(size_t)255; }
+
+long hbmr_kmeans_accum_workspace_bytes(long n, int k) {
+  return (long)(3 * ws_align(((size_t)k + 1) * 4) + ws_align((size_t)n * 4));
+}
+
+int hbmr_kmeans_accum_bf16(const void* X, long n, int dp, const int32_t* labels, int k,
+                           long long* sums, long long* counts, int fx_shift, void* ws,
+                           long ws_bytes, int mode, hipStream_t st) {
+  set_lds_limits();
+  const int cus = cu_count();
+  const float scale = ldexpf(1.0f, fx_shift);
+  if (n <= 0) return 0;
+  // mode: 0 = auto, 1 = LDS-privatised (small k / chunked), 2 = sorted
+  const bool small = ((size_t)k * AccCfg<128>::RS * 8 + (size_t)k * 4) <= 76 * 1024 && dp <= 128;
+  const bool sorted = mode == 2 || (mode == 0 && !small && ws != nullptr &&
+                                    ws_bytes >= hbmr_kmeans_accum_workspace_bytes(n, k));
+  if (sorted) {
+    if (ws == nullptr || ws_bytes < hbmr_kmeans_accum_workspace_bytes(n, k) || n >= (1L << 32))
+      return (int)hipErrorInvalidValue;
+    char* w = reinterpret_cast<char*>(ws);
+    const size_t kb = ws_align(((size_t)k + 1) * 4);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(w);
+    uint32_t* offsets = reinterpret_cast<uint32_t*>(w + kb);
+    uint32_t* cursor = reinterpret_cast<uint32_t*>(w + 2 * kb);
+    uint32_t* perm = reinterpret_cast<uint32_t*>(w + 3 * kb);
+    HBMR_RETURN_IF_ERROR(hipMemsetAsync(hist, 0, (size_t)k * 4, st));
+    const size_t hlds = (size_t)k * 4;
+    long hgrid = std::min<long>((n / 4 + 255) / 256 + 1, (long)cus * 2);
+    hipLaunchKernelGGL(kmeans_hist_kernel, dim3((unsigned)hgrid), dim3(256), hlds, st, labels, n,
+                       k, hist);
+    hipLaunchKernelGGL(kmeans_scan_kernel, dim3(1), dim3(1024), 0, st, hist, k, offsets, cursor,
+                       counts);
+    const long sgrid = (n + kScatterPts - 1) / kScatterPts;
+    hipLaunchKernelGGL(kmeans_scatter_kernel, dim3((unsigned)sgrid), dim3(256), 2 * hlds, st,
+                       labels, n, k, cursor, perm);
+    // segsum: one chunk per wave, ~8 waves per CU worth of chunks at least
+    // short chunks keep the per-wave dependent-load chain short for small
+    // splits; long chunks amortise flush atomics for big ones
+    long chunk = (n + (long)cus * 16 - 1) / ((long)cus * 16);
+    chunk = std::min<long>(4096, std::max<long>(128, ((chunk + 63) / 64) * 64));
+    const long nw = (n + chunk - 1) / chunk;
+    const long sblocks = (nw + 3) / 4;
+    switch (dp) {
+#define HBMR_SEG(DD)                                                                        \
+  case DD:                                                                                 \
+    hipLaunchKernelGGL((kmeans_segsum_kernel<DD, 8>), dim3((unsigned)sblocks), dim3(256), 0, \
+                       st, reinterpret_cast<const __bf16*>(X), n, perm, offsets, k, chunk,  \
+                       sums, scale);                                                        \
+    break;
+      HBMR_SEG(64)
+      HBMR_SEG(128)
+      HBMR_SEG(256)
+#undef HBMR_SEG
+      default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+  }
+  switch (dp) {
+    case 64: return launch_accum<64>(X, n, labels, k, sums, counts, scale, cus, st);
+    case 128: return launch_accum<128>(X, n, labels, k, sums, counts, scale, cus, st);
+    case 256: return launch_accum<256>(X, n, labels, k, sums, counts, scale, cus, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+int hbmr_kmeans_update(const long long* sums, const long long* counts, int fx_shift, int k, int d,
+                       int dp, int k_pad, float* cen, void* cbf, float* chalf, float* shift2,
+                       hipStream_t st) {
+  if (k <= 0) return 0;
+  hipLaunchKernelGGL(kmeans_update_kernel, dim3(k), dim3(128), 0, st, sums, counts, k, d, dp,
+                     ldexpf(1.0f, -fx_shift), cen, reinterpret_cast<__bf16*>(cbf), chalf, shift2);
+  if (k_pad > k)
+    hipLaunchKernelGGL(kmeans_pad_clusters_kernel, dim3(k_pad - k), dim3(64), 0, st,
+                       reinterpret_cast<__bf16*>(cbf), chalf, k, k_pad, dp);
+  return (int)hipGetLastError();
+}
+
+int hbmr_kmeans_padded_k(int k) { return ((k + kCK - 1) / kCK) * kCK; }
+
+}  // extern "C"
