@@ -1,0 +1,84 @@
+"""HBM-resident split cache.
+
+Each tracker keeps the splits its GPU tasks materialised, keyed by
+(split key, device), so later jobs over the same input (every K-Means
+iteration) find their data already in HBM — "locality" for the scheduler means
+*resident in this GPU's HBM* (SURVEY.md §7 "HBM-resident split sizing").
+Capacity is bounded by ``hbmr.gpu.hbm.reserve.gb`` below the device's free
+memory; eviction is LRU.  The tracker reports additions/evictions in its next
+heartbeat so the JobTracker's locality view stays current.
+"""
+from __future__ import annotations
+
+import collections
+import threading
+
+
+class SplitCache:
+    def __init__(self, capacity_bytes_per_device: dict | None = None):
+        self._lock = threading.Lock()
+        self._entries: "collections.OrderedDict[tuple, tuple]" = collections.OrderedDict()
+        self._bytes = collections.Counter()
+        self.capacity = dict(capacity_bytes_per_device or {})
+        self.added: list = []
+        self.removed: list = []
+        self.hits = 0
+        self.misses = 0
+
+    def get(self, key, device):
+        with self._lock:
+            k = (key, device)
+            e = self._entries.get(k)
+            if e is not None:
+                self._entries.move_to_end(k)
+                self.hits += 1
+                return e[0]
+            self.misses += 1
+            return None
+
+    def put(self, key, device, data, nbytes: int):
+        with self._lock:
+            k = (key, device)
+            if k in self._entries:
+                return
+            cap = self.capacity.get(device)
+            if cap is not None:
+                while self._bytes[device] + nbytes > cap:
+                    victim = next((kk for kk in self._entries if kk[1] == device), None)
+                    if victim is None:
+                        break
+                    _, vb = self._entries.pop(victim)
+                    self._bytes[device] -= vb
+                    self.removed.append(list(victim))
+            self._entries[k] = (data, nbytes)
+            self._bytes[device] += nbytes
+            self.added.append([key, device])
+
+    def get_or_load(self, key, device, loader, nbytes_fn):
+        data = self.get(key, device)
+        if data is not None:
+            return data, True
+        data = loader()
+        self.put(key, device, data, nbytes_fn(data))
+        return data, False
+
+    def drain_changes(self):
+        with self._lock:
+            a, r = self.added, self.removed
+            self.added, self.removed = [], []
+            return a, r
+
+    def resident(self):
+        with self._lock:
+            return [list(k) for k in self._entries]
+
+    def bytes_on(self, device):
+        return self._bytes[device]
+
+    def clear(self, device=None):
+        with self._lock:
+            for k in list(self._entries):
+                if device is None or k[1] == device:
+                    _, b = self._entries.pop(k)
+                    self._bytes[k[1]] -= b
+                    self.removed.append(list(k))

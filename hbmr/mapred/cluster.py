@@ -1,0 +1,71 @@
+"""In-process node cluster: one JobTracker plus N TaskTrackers in this process.
+
+The analogue of the reference's MiniMRCluster (src/test/org/apache/hadoop/
+mapred/MiniMRCluster.java: JobTracker thread + N TaskTracker threads, each with
+its own local dir and fake host name).  Used by tests and by single-process
+runs (``mapred.job.tracker=inproc``).  Trackers share an
+:class:`~hbmr.parallel.collectives.InProcessComm` so collective reduces run
+the same code as the multi-process RCCL path.
+"""
+from __future__ import annotations
+
+import logging
+import tempfile
+
+from ..parallel.collectives import InProcessComm, SoloComm
+from .jobclient import RunningJob
+from .jobconf import JobConf, as_jobconf
+from .jobtracker import JobTracker
+from .tasktracker import TaskTracker
+
+log = logging.getLogger("hbmr.cluster")
+
+_default = None
+
+
+class LocalCluster:
+    def __init__(self, conf=None, num_trackers=1, gpus=None, cpu_slots=None, reduce_slots=None,
+                 gpu_slots_per_device=None, local_dir=None):
+        """gpus: list per tracker of device ids, e.g. [[0], [1]]; None = CPU only."""
+        self.conf = as_jobconf(conf or JobConf())
+        self.jt = JobTracker(self.conf)
+        self.local_dir = local_dir or tempfile.mkdtemp(prefix="hbmr-cluster-")
+        comms = InProcessComm.group(num_trackers) if num_trackers > 1 else [SoloComm()]
+        gpus = gpus or [[] for _ in range(num_trackers)]
+        self.trackers = []
+        for i in range(num_trackers):
+            tt = TaskTracker(self.conf, self.jt, name=f"tracker_{i}", rank=i,
+                             world_size=num_trackers, gpu_devices=gpus[i], cpu_slots=cpu_slots,
+                             reduce_slots=reduce_slots, gpu_slots_per_device=gpu_slots_per_device,
+                             comm=comms[i], local_dir=f"{self.local_dir}/tt{i}")
+            self.trackers.append(tt)
+        for tt in self.trackers:
+            tt.start()
+        if not self.jt.wait_for_trackers(num_trackers, timeout=60):
+            raise RuntimeError("trackers failed to register")
+        self.jt.start_expiry_thread()
+
+    def submit_job(self, job) -> RunningJob:
+        rj = self.jt.submit_job(as_jobconf(job))
+        return rj
+
+    def job_result(self, rj: RunningJob, tracker=0):
+        return self.trackers[tracker].job_result(rj.getID())
+
+    def shutdown(self):
+        for tt in self.trackers:
+            tt.stop()
+        self.jt.shutdown()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.shutdown()
+
+
+def default_cluster(conf):
+    global _default
+    if _default is None:
+        _default = LocalCluster(conf)
+    return _default

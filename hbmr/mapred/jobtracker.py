@@ -1,0 +1,752 @@
+"""JobTracker: job queue, task bookkeeping, heartbeat-driven scheduling, failure handling.
+
+Behaviour modelled on hadoop-1.0.3/src/mapred/org/apache/hadoop/mapred/
+JobTracker.java (heartbeat :3308, processHeartbeat :3670, updateTaskStatuses
+:4717, ExpireTrackers :440, lostTaskTracker :4811, FaultyTrackersInfo :814),
+JobInProgress.java (initTasks :789, findNewMapTask :2371, completedTask :2673,
+speculation :2312, finishedCPU/GPUMapTasks :114-115, 2780-2784) and
+TaskInProgress.java (attempts, speculation, generateSingleReport :481).
+
+Differences by design (SURVEY.md §2.1 bugs B1-B13):
+* heartbeats are event-driven (a tracker calls in as soon as a slot frees)
+  and the interval defaults to 100 ms, not a 3 s floor (B13);
+* per-task CPU/GPU timings update an O(1) cost model on completion instead of
+  being rebuilt from every TaskReport per heartbeat (B6);
+* a lost tracker decrements only the counters of the tasks it really ran (B5);
+* reports carry the placement of the *successful* attempt (G11);
+* locality includes "split resident in this GPU's HBM".
+"""
+from __future__ import annotations
+
+import itertools
+import logging
+import threading
+import time
+
+from ..utils.reflection import load_class, new_instance
+from . import counters as C
+from . import protocol as P
+from .counters import Counters
+from .ids import JobID, TaskAttemptID, TaskID
+from .jobclient import FAILED, KILLED, PREP, RUNNING, SUCCEEDED, JobStatus, RunningJob
+from .scheduler.costmodel import CostModel
+
+log = logging.getLogger("hbmr.jobtracker")
+
+
+class TrackerInfo:
+    def __init__(self, status: P.TaskTrackerStatus, now):
+        self.name = status.tracker_name
+        self.status = status
+        self.last_seen = now
+        self.running: set[str] = set()           # attempt ids
+        self.running_gpu: dict[int, int] = {}    # device -> running GPU attempts
+        self.running_cpu = 0
+        self.running_reduce = 0
+        self.cached: set[tuple] = set()          # (split_key, device)
+        self.failures = 0
+        self.blacklisted = False
+        self.jobs_seen: set[str] = set()
+        self.wake = False
+
+    def gpu_devices(self):
+        return [g["device"] for g in self.status.gpus]
+
+    def gpu_capacity(self, dev):
+        for g in self.status.gpus:
+            if g["device"] == dev:
+                return g["max_slots"]
+        return 0
+
+
+class Attempt:
+    __slots__ = ("aid", "tip", "tracker", "run_on_gpu", "device", "state", "progress",
+                 "start", "finish", "counters", "output", "diagnostic", "speculative",
+                 "device_time")
+
+    def __init__(self, aid, tip, tracker, run_on_gpu, device, speculative=False):
+        self.aid = aid
+        self.tip = tip
+        self.tracker = tracker
+        self.run_on_gpu = run_on_gpu
+        self.device = device
+        self.state = P.RUNNING
+        self.progress = 0.0
+        self.start = time.time()
+        self.finish = 0.0
+        self.counters = {}
+        self.output = {}
+        self.diagnostic = ""
+        self.speculative = speculative
+        self.device_time = 0.0
+
+
+class TaskInProgress:
+    def __init__(self, job, tid: TaskID, split=None, partition=0, pinned_tracker=None):
+        self.job = job
+        self.tid = tid
+        self.split = split
+        self.partition = partition
+        self.pinned_tracker = pinned_tracker
+        self.attempts: dict[str, Attempt] = {}
+        self.next_attempt = 0
+        self.failures = 0
+        self.failed_trackers: set[str] = set()
+        self.successful: Attempt | None = None
+        self.commit_granted: str | None = None
+        self.killed = False
+
+    @property
+    def is_map(self):
+        return self.tid.is_map
+
+    def is_complete(self):
+        return self.successful is not None
+
+    def running_attempts(self):
+        return [a for a in self.attempts.values() if a.state in (P.RUNNING, P.COMMIT_PENDING)]
+
+    def is_running(self):
+        return bool(self.running_attempts())
+
+    def new_attempt_id(self) -> TaskAttemptID:
+        aid = TaskAttemptID(self.tid, self.next_attempt)
+        self.next_attempt += 1
+        return aid
+
+    def locations(self):
+        return (self.split or {}).get("locations", []) if isinstance(self.split, dict) else []
+
+    def split_key(self):
+        return (self.split or {}).get("key") if isinstance(self.split, dict) else None
+
+    def report(self):
+        """TaskReport of the successful attempt (else the latest one), with its
+        placement (fixes G11, which tagged the first attempt)."""
+        from .local_runner import TaskReport
+        a = self.successful
+        if a is None and self.attempts:
+            a = max(self.attempts.values(), key=lambda x: x.start)
+        if a is None:
+            return TaskReport(self.tid, 0.0, P.UNASSIGNED, 0.0, 0.0, Counters())
+        state = P.SUCCEEDED if self.successful else a.state
+        return TaskReport(self.tid, 1.0 if self.successful else a.progress, state, a.start,
+                          a.finish, Counters.from_dict(a.counters), a.run_on_gpu, a.device,
+                          a.tracker)
+
+
+class JobInProgress:
+    def __init__(self, jt, job_id: JobID, conf):
+        self.jt = jt
+        self.job_id = job_id
+        self.conf = conf
+        self.status = JobStatus(job_id, PREP)
+        self.counters = Counters()
+        self.maps: list[TaskInProgress] = []
+        self.reduces: list[TaskInProgress] = []
+        self.done = threading.Event()
+        self.split_job = None
+        self.collective_reduce = False
+        self.priority = conf.get("mapred.job.priority", "NORMAL")
+        self.submit_time = time.time()
+        self.launch_time = 0.0
+        self.finished_cpu_maps = 0
+        self.finished_gpu_maps = 0
+        self.completion_events: list[dict] = []
+        self.map_index: dict[str, TaskInProgress] = {}
+        self.pending_maps: list[TaskInProgress] = []   # not yet started, FIFO
+        self.by_split_key: dict = {}
+        self.signature = conf.get("hbmr.job.signature") or self._signature(conf)
+        self.gpu_capable = conf.is_gpu_capable()
+        self.cpu_capable = conf.get_boolean("hbmr.job.cpu.capable", True)
+        self.speculative = conf.get_map_speculative_execution()
+        self.max_map_attempts = conf.get_max_map_attempts()
+        self.max_reduce_attempts = conf.get_max_reduce_attempts()
+        self.result = None
+        self.conf_dict = conf.to_dict()
+
+    @staticmethod
+    def _signature(conf):
+        return "|".join(str(conf.get(k, "")) for k in (
+            "hbmr.splitjob.class", "mapred.mapper.class", "hadoop.pipes.executable",
+            "hadoop.pipes.gpu.executable", "mapred.input.format.class", "hbmr.split.size"))
+
+    # -- init ---------------------------------------------------------------------
+    def init_tasks(self):
+        conf = self.conf
+        sj_cls = conf.get("hbmr.splitjob.class")
+        trackers = self.jt.tracker_names()
+        if sj_cls:
+            self.split_job = new_instance(sj_cls, conf)
+            splits = self.split_job.get_splits(conf, trackers)
+            self.collective_reduce = bool(getattr(self.split_job, "collective_reduce", True))
+            split_dicts = [s.to_dict() for s in splits]
+        else:
+            informat = new_instance(conf.get_input_format(), conf)
+            splits = informat.getSplits(conf, conf.get_num_map_tasks())
+            split_dicts = [{"kind": "class", "cls": f"{type(s).__module__}:{type(s).__qualname__}",
+                            "data": s.serialize().hex(),
+                            "locations": list(s.getLocations() or []),
+                            "length": s.getLength()} for s in splits]
+        for i, sd in enumerate(split_dicts):
+            tip = TaskInProgress(self, TaskID(self.job_id, True, i), split=sd, partition=i)
+            self.maps.append(tip)
+            self.map_index[str(tip.tid)] = tip
+            self.pending_maps.append(tip)
+            if sd.get("key"):
+                self.by_split_key[sd["key"]] = tip
+        if self.collective_reduce and self.split_job is not None:
+            # one pinned reduce per tracker: the collective (RCCL) reduce gang
+            nred = len(trackers) if getattr(self.split_job, "needs_reduce", True) else 0
+            for r in range(nred):
+                self.reduces.append(TaskInProgress(self, TaskID(self.job_id, False, r),
+                                                   partition=r, pinned_tracker=trackers[r]))
+        else:
+            for r in range(conf.get_num_reduce_tasks()):
+                self.reduces.append(TaskInProgress(self, TaskID(self.job_id, False, r),
+                                                   partition=r))
+        self.status.state = RUNNING
+        self.launch_time = time.time()
+        self.jt.history.log("JOB_INITED", job=str(self.job_id), maps=len(self.maps),
+                            reduces=len(self.reduces), signature=self.signature)
+
+    # -- scheduling helpers ----------------------------------------------------------------
+    def pending_map_count(self):
+        return len(self.pending_maps)
+
+    def running_maps(self, on_gpu=None):
+        n = 0
+        for t in self.maps:
+            for a in t.running_attempts():
+                if on_gpu is None or a.run_on_gpu == on_gpu:
+                    n += 1
+        return n
+
+    def maps_complete(self):
+        return all(t.is_complete() for t in self.maps)
+
+    def obtain_map(self, tracker: TrackerInfo, on_gpu: bool, device: int, allow_nonlocal=True):
+        """findNewMapTask with locality levels: split cached in this device's HBM
+        > cached elsewhere on this tracker > node-local (split locations) > any."""
+        if not self.pending_maps:
+            return None
+        best = None
+        best_level = 99
+        for tip in self.pending_maps:
+            if tracker.name in tip.failed_trackers and len(self.jt.trackers) > 1:
+                continue
+            key = tip.split_key()
+            level = 3
+            if key is not None:
+                if on_gpu and (key, device) in tracker.cached:
+                    level = 0
+                elif any(k == key for k, _ in tracker.cached):
+                    level = 1
+            if level > 1 and tracker.name in tip.locations():
+                level = 2
+            if level < best_level:
+                best, best_level = tip, level
+                if level == 0:
+                    break
+        if best is None:
+            return None
+        if best_level == 3 and not allow_nonlocal:
+            return None
+        self.pending_maps.remove(best)
+        return best, best_level
+
+    def completed(self):
+        return self.status.is_complete()
+
+
+class JobHistory:
+    """Job history event log (JobHistory.java) as JSON lines; the hbmr twist is
+    that every map attempt records run_on_gpu / device (the fork's history did not)."""
+
+    def __init__(self, path=None):
+        self.path = path
+        self._lock = threading.Lock()
+        self.events: list[dict] = []
+        self.max_events = 200_000
+
+    def log(self, event, **kw):
+        rec = {"ts": time.time(), "event": event, **kw}
+        with self._lock:
+            if len(self.events) < self.max_events:
+                self.events.append(rec)
+            if self.path:
+                import json
+                with open(self.path, "a") as f:
+                    f.write(json.dumps(rec) + "\n")
+
+
+class _JTJobHandle:
+    """RunningJob backend for jobs submitted to an in-process JobTracker."""
+
+    def __init__(self, jip: JobInProgress):
+        self.jip = jip
+
+    def status(self):
+        return self.jip.status
+
+    def counters(self):
+        return self.jip.counters
+
+    def wait(self, timeout=None):
+        return self.jip.done.wait(timeout)
+
+    def kill(self):
+        self.jip.jt.kill_job(self.jip.job_id)
+
+    def task_reports(self, is_map=True):
+        return [t.report() for t in (self.jip.maps if is_map else self.jip.reduces)]
+
+    @property
+    def result(self):
+        return self.jip.result
+
+
+class JobTracker:
+    def __init__(self, conf, name=None):
+        self.conf = conf
+        self.name = name or time.strftime("%Y%m%d%H%M")
+        self.lock = threading.RLock()
+        self.cv = threading.Condition(self.lock)
+        self.jobs: dict[str, JobInProgress] = {}
+        self.job_queue: list[JobInProgress] = []
+        self.trackers: dict[str, TrackerInfo] = {}
+        self.attempt_index: dict[str, Attempt] = {}
+        self.cost_model = CostModel(conf.get_float("hbmr.costmodel.ewma.alpha", 0.3))
+        sched_cls = conf.get("mapred.jobtracker.taskScheduler",
+                             "hbmr.mapred.scheduler.hybrid:HybridTaskScheduler")
+        self.scheduler = load_class(sched_cls)(self, conf)
+        self.history = JobHistory(conf.get("hbmr.history.file"))
+        self.heartbeat_interval = conf.get_int("hbmr.heartbeat.interval.ms", 100) / 1000.0
+        self.tracker_expiry = conf.get_int("mapred.tasktracker.expiry.interval", 600000) / 1000.0
+        self.max_tracker_failures = conf.get_int("mapred.max.tracker.failures", 4)
+        self._seq = itertools.count(1)
+        self._expire_thread = None
+        self._stop = threading.Event()
+        self.listeners = []
+        self.start_time = time.time()
+
+    # -- trackers -------------------------------------------------------------------
+    def tracker_names(self):
+        with self.lock:
+            return sorted(self.trackers, key=lambda n: (self.trackers[n].status.rank, n))
+
+    def wait_for_trackers(self, n, timeout=60.0):
+        t0 = time.time()
+        while time.time() - t0 < timeout:
+            with self.lock:
+                if len(self.trackers) >= n:
+                    return True
+            time.sleep(0.005)
+        return False
+
+    def start_expiry_thread(self):
+        if self._expire_thread is None:
+            self._expire_thread = threading.Thread(target=self._expire_loop, daemon=True,
+                                                   name="ExpireTrackers")
+            self._expire_thread.start()
+
+    def _expire_loop(self):
+        while not self._stop.wait(min(1.0, self.tracker_expiry / 4)):
+            now = time.time()
+            with self.lock:
+                for name, tr in list(self.trackers.items()):
+                    if now - tr.last_seen > self.tracker_expiry:
+                        self.lost_tracker(name, "expired")
+
+    def lost_tracker(self, name, why="lost"):
+        """lostTaskTracker (JobTracker.java:4811): fail its running attempts and
+        re-execute its completed maps whose output lived on it."""
+        with self.lock:
+            tr = self.trackers.pop(name, None)
+            if tr is None:
+                return
+            log.warning("tracker %s %s", name, why)
+            self.history.log("TRACKER_LOST", tracker=name, why=why)
+            for aid in list(tr.running):
+                a = self.attempt_index.get(aid)
+                if a is not None:
+                    self._attempt_failed(a, f"tracker {name} {why}", killed=True)
+            for jip in self.jobs.values():
+                if jip.completed():
+                    continue
+                for tip in jip.maps:
+                    a = tip.successful
+                    if a is not None and a.tracker == name and jip.reduces:
+                        # its map output is gone with the tracker
+                        tip.successful = None
+                        if a.run_on_gpu:
+                            jip.finished_gpu_maps -= 1
+                        else:
+                            jip.finished_cpu_maps -= 1
+                        jip.pending_maps.append(tip)
+
+    # -- jobs -----------------------------------------------------------------------
+    def new_job_id(self):
+        return JobID(self.name, next(self._seq))
+
+    def submit_job(self, conf) -> RunningJob:
+        jid = self.new_job_id()
+        jip = JobInProgress(self, jid, conf)
+        with self.lock:
+            self.jobs[str(jid)] = jip
+            self.history.log("JOB_SUBMITTED", job=str(jid), name=conf.get_job_name(),
+                             user=conf.get_user())
+            try:
+                jip.init_tasks()
+            except Exception as e:  # noqa: BLE001
+                log.exception("job init failed")
+                self._finish_job(jip, FAILED, f"init failed: {type(e).__name__}: {e}")
+                return RunningJob(jid, _JTJobHandle(jip), conf)
+            self.job_queue.append(jip)
+            if not jip.maps and not jip.reduces:
+                self._finish_job(jip, SUCCEEDED)
+            self.cv.notify_all()
+        for cb in self.listeners:
+            cb("submitted", jip)
+        return RunningJob(jid, _JTJobHandle(jip), conf)
+
+    def kill_job(self, job_id):
+        with self.lock:
+            jip = self.jobs.get(str(job_id))
+            if jip is None or jip.completed():
+                return
+            self._finish_job(jip, KILLED, "killed by user")
+
+    def _finish_job(self, jip: JobInProgress, state, info=""):
+        if jip.completed():
+            return
+        st = jip.status
+        st.state = state
+        st.failure_info = info
+        st.finish_time = time.time()
+        if state == SUCCEEDED:
+            st.map_progress = st.reduce_progress = 1.0
+        for tip in jip.maps + jip.reduces:
+            tip.killed = state != SUCCEEDED
+        if jip in self.job_queue:
+            self.job_queue.remove(jip)
+        jip.counters.incr(C.JOB_GROUP, C.CPU_MAP_TASKS, jip.finished_cpu_maps)
+        jip.counters.incr(C.JOB_GROUP, C.GPU_MAP_TASKS, jip.finished_gpu_maps)
+        self.history.log("JOB_FINISHED", job=str(jip.job_id), state=state,
+                         makespan=st.finish_time - jip.submit_time,
+                         cpu_maps=jip.finished_cpu_maps, gpu_maps=jip.finished_gpu_maps,
+                         info=info)
+        if state == SUCCEEDED and jip.split_job is not None:
+            try:
+                jip.split_job.job_succeeded(jip)
+            except Exception:  # noqa: BLE001
+                log.exception("job_succeeded hook failed")
+        jip.done.set()
+        for cb in self.listeners:
+            cb("finished", jip)
+
+    # -- heartbeat ----------------------------------------------------------------------
+    def wakeup(self, tracker_name: str):
+        """A tracker has news (a task finished): end its long-poll heartbeat now."""
+        with self.lock:
+            tr = self.trackers.get(tracker_name)
+            if tr is not None:
+                tr.wake = True
+            self.cv.notify_all()
+
+    def notify(self):
+        with self.lock:
+            self.cv.notify_all()
+
+    def heartbeat(self, status: dict, initial: bool = False, accept_new_tasks: bool = True,
+                  block: float = 0.0):
+        """Process a tracker's status and return {"actions": [...], "interval": s}.
+
+        With ``block`` > 0 and nothing to hand out, the call long-polls (up to
+        ``block`` seconds) until new work exists or the tracker calls wakeup(),
+        so idle trackers learn about new tasks immediately instead of on their
+        next periodic heartbeat (the reference's 3 s floor, B13)."""
+        resp = self._heartbeat(status, initial, accept_new_tasks)
+        if getattr(self, "_shutdown_trackers", False):
+            resp["actions"].append(P.shutdown_action())
+            return resp
+        if resp["actions"] or block <= 0 or not accept_new_tasks:
+            return resp
+        name = status["tracker_name"] if isinstance(status, dict) else status.tracker_name
+        deadline = time.time() + block
+        with self.lock:
+            tr = self.trackers.get(name)
+            if tr is None:
+                return resp
+            tr.wake = False
+            while not resp["actions"]:
+                left = deadline - time.time()
+                if left <= 0 or tr.wake or self._stop.is_set():
+                    break
+                if getattr(self, "_shutdown_trackers", False):
+                    resp["actions"].append(P.shutdown_action())
+                    break
+                self.cv.wait(left)
+                if tr.wake or self.trackers.get(name) is not tr:
+                    break
+                if tr.status.healthy and not tr.blacklisted:
+                    resp["actions"] += self.scheduler.assign_tasks(tr)
+            tr.wake = False
+        return resp
+
+    def _heartbeat(self, status, initial, accept_new_tasks):
+        st = P.TaskTrackerStatus.from_dict(status) if isinstance(status, dict) else status
+        now = time.time()
+        actions = []
+        with self.lock:
+            tr = self.trackers.get(st.tracker_name)
+            if tr is None:
+                if not initial:
+                    # unknown tracker (e.g. after JT restart / expiry): re-initialise
+                    return {"actions": [P.reinit_action()], "interval": self.heartbeat_interval}
+                tr = self.trackers[st.tracker_name] = TrackerInfo(st, now)
+                self.history.log("TRACKER_JOINED", tracker=st.tracker_name, host=st.host,
+                                 cpu_slots=st.max_cpu_map_slots,
+                                 gpus=[g["device"] for g in st.gpus])
+            tr.status = st
+            tr.last_seen = now
+            for k in st.cached_splits_added:
+                tr.cached.add(tuple(k))
+            for k in st.cached_splits_removed:
+                tr.cached.discard(tuple(k))
+            for rep in st.task_reports:
+                self._update_task_status(tr, P.TaskStatus.from_dict(rep), actions)
+            if accept_new_tasks and st.healthy and not tr.blacklisted:
+                actions += self.scheduler.assign_tasks(tr)
+            # kill attempts of jobs that are done / tasks already completed
+            for aid in list(tr.running):
+                a = self.attempt_index.get(aid)
+                if a is not None and (a.tip.job.completed() or
+                                      (a.tip.successful is not None and a.tip.successful is not a)):
+                    actions.append(P.kill_task_action(aid))
+        return {"actions": actions, "interval": self.heartbeat_interval}
+
+    def _update_task_status(self, tr: TrackerInfo, ts: P.TaskStatus, actions):
+        a = self.attempt_index.get(ts.attempt_id)
+        if a is None or a.state in P.TERMINAL:
+            return
+        a.progress = ts.progress
+        a.counters = ts.counters or a.counters
+        if ts.start_time:
+            a.start = ts.start_time
+        jip = a.tip.job
+        if ts.state == P.SUCCEEDED:
+            a.finish = ts.finish_time or time.time()
+            a.output = ts.output
+            a.device_time = ts.device_time
+            self._attempt_succeeded(a)
+        elif ts.state in (P.FAILED, P.KILLED, P.FAILED_UNCLEAN):
+            a.finish = ts.finish_time or time.time()
+            self._attempt_failed(a, ts.diagnostic, killed=ts.state == P.KILLED)
+        elif ts.state == P.COMMIT_PENDING:
+            a.state = P.COMMIT_PENDING
+            tip = a.tip
+            if tip.commit_granted is None and tip.successful is None:
+                tip.commit_granted = a.aid
+                actions.append(P.commit_action(a.aid))
+            elif tip.commit_granted != a.aid:
+                actions.append(P.kill_task_action(a.aid))
+        self._update_progress(jip)
+
+    def _release(self, a: Attempt):
+        tr = self.trackers.get(a.tracker)
+        if tr is not None and a.aid in tr.running:
+            tr.running.discard(a.aid)
+            if a.tip.is_map:
+                if a.run_on_gpu:
+                    tr.running_gpu[a.device] = max(0, tr.running_gpu.get(a.device, 1) - 1)
+                else:
+                    tr.running_cpu = max(0, tr.running_cpu - 1)
+            else:
+                tr.running_reduce = max(0, tr.running_reduce - 1)
+
+    def _attempt_succeeded(self, a: Attempt):
+        tip = a.tip
+        jip = tip.job
+        a.state = P.SUCCEEDED
+        self._release(a)
+        if tip.is_map:
+            if a.run_on_gpu and a.device_time > 0:
+                # GPU attempts are timed by HIP events: device time, not queue time
+                self.cost_model.task_finished(jip.signature, a.aid, True, 0.0, a.device_time)
+            else:
+                self.cost_model.task_finished(jip.signature, a.aid, a.run_on_gpu, a.start,
+                                              a.finish)
+        if tip.successful is not None or tip.killed:
+            return  # a speculative twin already won
+        tip.successful = a
+        jip.counters.incr_all(Counters.from_dict(a.counters))
+        if not tip.is_map and isinstance(a.output, dict) and a.output.get("result") is not None:
+            if jip.result is None:
+                jip.result = {}
+            jip.result[tip.partition] = a.output["result"]
+        if tip.is_map:
+            if a.run_on_gpu:
+                jip.finished_gpu_maps += 1
+            else:
+                jip.finished_cpu_maps += 1
+            jip.completion_events.append({"map": str(tip.tid), "attempt": a.aid,
+                                          "tracker": a.tracker, "output": a.output,
+                                          "gpu": a.run_on_gpu, "device": a.device})
+        # kill other running attempts of this TIP
+        for other in tip.running_attempts():
+            if other is not a:
+                other.state = P.KILLED
+                self._release(other)
+                if tip.is_map:
+                    self.cost_model.task_finished(jip.signature, other.aid, other.run_on_gpu,
+                                                  other.start, time.time(), succeeded=False)
+        self.history.log("TASK_FINISHED", attempt=a.aid, tracker=a.tracker,
+                         gpu=a.run_on_gpu, device=a.device, start=a.start, finish=a.finish,
+                         device_time=a.device_time)
+        self._check_job_done(jip)
+        if tip.is_map and jip.reduces and jip.maps_complete():
+            self.cv.notify_all()  # reduces became schedulable: wake long-polling trackers
+
+    def _attempt_failed(self, a: Attempt, diag, killed=False):
+        tip = a.tip
+        jip = tip.job
+        if a.state in P.TERMINAL:
+            return
+        a.state = P.KILLED if killed else P.FAILED
+        a.diagnostic = diag
+        self._release(a)
+        if tip.is_map:
+            self.cost_model.task_finished(jip.signature, a.aid, a.run_on_gpu, a.start,
+                                          time.time(), succeeded=False)
+        self.history.log("TASK_FAILED" if not killed else "TASK_KILLED", attempt=a.aid,
+                         tracker=a.tracker, gpu=a.run_on_gpu, diag=diag[:500])
+        if tip.commit_granted == a.aid:
+            tip.commit_granted = None
+        if jip.completed() or tip.successful is not None:
+            return
+        if not killed:
+            tip.failures += 1
+            tip.failed_trackers.add(a.tracker)
+            jip.counters.incr(C.JOB_GROUP, C.NUM_FAILED_MAPS if tip.is_map else
+                              C.NUM_FAILED_REDUCES)
+            tr = self.trackers.get(a.tracker)
+            if tr is not None:
+                tr.failures += 1
+                if tr.failures >= self.max_tracker_failures * 4 and len(self.trackers) > 1:
+                    tr.blacklisted = True
+                    self.history.log("TRACKER_BLACKLISTED", tracker=tr.name)
+        limit = jip.max_map_attempts if tip.is_map else jip.max_reduce_attempts
+        if tip.failures >= limit:
+            self._finish_job(jip, FAILED, f"Task {tip.tid} failed {tip.failures} times: {diag}")
+            return
+        if not tip.running_attempts():
+            if tip.is_map:
+                if tip not in jip.pending_maps:
+                    jip.pending_maps.insert(0, tip)  # failed tasks first (findNewMapTask)
+            elif jip.collective_reduce:
+                # a collective gang cannot restart one member: fail the job
+                self._finish_job(jip, FAILED, f"collective reduce {tip.tid} failed: {diag}")
+
+    def _update_progress(self, jip: JobInProgress):
+        if jip.maps:
+            jip.status.map_progress = sum(
+                1.0 if t.is_complete() else max((a.progress for a in t.attempts.values()),
+                                                default=0.0) for t in jip.maps) / len(jip.maps)
+        if jip.reduces:
+            jip.status.reduce_progress = sum(
+                1.0 if t.is_complete() else max((a.progress for a in t.attempts.values()),
+                                                default=0.0) for t in jip.reduces) / len(jip.reduces)
+
+    def _check_job_done(self, jip: JobInProgress):
+        if all(t.is_complete() for t in jip.maps) and all(t.is_complete() for t in jip.reduces):
+            self._finish_job(jip, SUCCEEDED)
+
+    # -- launching (called by the scheduler under the lock) -------------------------------
+    def launch(self, tr: TrackerInfo, tip: TaskInProgress, on_gpu=False, device=-1,
+               speculative=False, extra=None):
+        jip = tip.job
+        aid = tip.new_attempt_id()
+        a = Attempt(str(aid), tip, tr.name, on_gpu, device, speculative)
+        tip.attempts[a.aid] = a
+        self.attempt_index[a.aid] = a
+        tr.running.add(a.aid)
+        if tip.is_map:
+            if on_gpu:
+                tr.running_gpu[device] = tr.running_gpu.get(device, 0) + 1
+            else:
+                tr.running_cpu += 1
+            self.cost_model.task_started(jip.signature, a.aid, on_gpu, a.start)
+            jip.counters.incr(C.JOB_GROUP, C.TOTAL_LAUNCHED_MAPS)
+        else:
+            tr.running_reduce += 1
+            jip.counters.incr(C.JOB_GROUP, C.TOTAL_LAUNCHED_REDUCES)
+        spec = P.TaskSpec(attempt_id=a.aid, job_id=str(jip.job_id), is_map=tip.is_map,
+                          partition=tip.partition, run_on_gpu=on_gpu, gpu_device_id=device,
+                          split=tip.split or {}, num_maps=len(jip.maps),
+                          num_reduces=len(jip.reduces), collective=jip.collective_reduce)
+        if extra:
+            for k, v in extra.items():
+                setattr(spec, k, v)
+        if str(jip.job_id) not in tr.jobs_seen:
+            spec.conf = jip.conf_dict
+            tr.jobs_seen.add(str(jip.job_id))
+        self.history.log("TASK_LAUNCHED", attempt=a.aid, tracker=tr.name, gpu=on_gpu,
+                         device=device, speculative=speculative)
+        return P.launch_action(spec)
+
+    def reduce_inputs(self, jip: JobInProgress, tracker_name=None):
+        """Map outputs a reduce needs: classic = every map's output location;
+        collective = the committed map attempts that ran on ``tracker_name``."""
+        if jip.collective_reduce:
+            return [[str(t.tid), t.successful.aid, t.successful.output] for t in jip.maps
+                    if t.successful is not None and t.successful.tracker == tracker_name]
+        return [[str(t.tid), t.successful.aid, t.successful.output] for t in jip.maps
+                if t.successful is not None]
+
+    # -- RPC-facing job submission protocol (JobSubmissionProtocol) -------------------------
+    def rpc_submit_job(self, conf_dict):
+        from .jobconf import JobConf
+        conf = JobConf()
+        for k, v in conf_dict.items():
+            conf.set(k, v)
+        return str(self.submit_job(conf).getID())
+
+    def rpc_job_status(self, jid):
+        jip = self.jobs[str(jid)]
+        st = jip.status
+        return {"state": st.state, "map_progress": st.map_progress,
+                "reduce_progress": st.reduce_progress, "start_time": st.start_time,
+                "finish_time": st.finish_time, "failure_info": st.failure_info,
+                "counters": jip.counters.to_dict()}
+
+    def rpc_kill_job(self, jid):
+        self.kill_job(jid)
+
+    def rpc_job_result(self, jid):
+        return self.jobs[str(jid)].result
+
+    def rpc_cluster_status(self):
+        with self.lock:
+            return {"trackers": {n: {"cpu_slots": t.status.max_cpu_map_slots,
+                                     "gpus": t.gpu_devices(), "running": len(t.running),
+                                     "blacklisted": t.blacklisted}
+                                 for n, t in self.trackers.items()},
+                    "jobs": {j: jip.status.state for j, jip in self.jobs.items()},
+                    "cost_model": self.cost_model.snapshot()}
+
+    def broadcast_shutdown(self):
+        """Tell every tracker to exit on its next heartbeat."""
+        with self.lock:
+            self._shutdown_trackers = True
+            self.cv.notify_all()
+
+    def shutdown(self):
+        self._stop.set()
+        with self.lock:
+            self.cv.notify_all()
+
+
+def job_result(rj: RunningJob):
+    impl = rj._impl
+    return getattr(impl, "result", None)

@@ -1,0 +1,113 @@
+"""Multi-process node bring-up: one process per GPU, JobTracker on rank 0.
+
+Launch with ``torchrun --nproc-per-node N`` (or ``python -m torch.distributed.run``).
+Every rank runs a TaskTracker for its GPU (LOCAL_RANK) plus its CPU slots;
+rank 0 additionally hosts the JobTracker and its RPC endpoint, whose address is
+published in the torch.distributed store.  Collectives of the data plane use
+the process group: ``nccl`` (RCCL over xGMI) for device tensors and a ``gloo``
+group for host tensors.
+"""
+from __future__ import annotations
+
+import datetime
+import logging
+import os
+import socket
+import time
+
+import torch
+
+from ..parallel.collectives import SoloComm, TorchComm
+from .jobconf import JobConf
+from .jobtracker import JobTracker
+from .rpc import JT_METHODS, JobTrackerProxy, RpcServer
+from .tasktracker import TaskTracker
+
+log = logging.getLogger("hbmr.node")
+
+
+class Node:
+    def __init__(self, conf: JobConf | None = None, use_gpu: bool | None = None,
+                 backend: str | None = None):
+        self.conf = conf or JobConf()
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.use_gpu = torch.cuda.is_available() if use_gpu is None else use_gpu
+        self.jt = None
+        self.server = None
+        self.dist = None
+        self.comm = SoloComm()
+        if self.use_gpu:
+            torch.cuda.set_device(self.local_rank)
+        if self.world > 1:
+            import torch.distributed as dist
+            self.dist = dist
+            be = backend or ("nccl" if self.use_gpu else "gloo")
+            kw = {}
+            if be == "nccl":
+                kw["device_id"] = torch.device("cuda", self.local_rank)
+            dist.init_process_group(be, timeout=datetime.timedelta(seconds=600), **kw)
+            cpu_group = dist.new_group(backend="gloo") if be != "gloo" else None
+            self.comm = TorchComm(group=None, cpu_group=cpu_group)
+            self.store = dist.distributed_c10d._get_default_store()
+        if self.rank == 0:
+            self.jt = JobTracker(self.conf)
+            if self.world > 1:
+                self.server = RpcServer(self.jt, JT_METHODS).start()
+                host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+                self.store.set("hbmr/jobtracker", f"{host}:{self.server.port}")
+            jt_handle = self.jt
+        else:
+            addr = self.store.get("hbmr/jobtracker").decode()
+            jt_handle = JobTrackerProxy(addr)
+        gpus = [self.local_rank] if self.use_gpu else []
+        self.tt = TaskTracker(self.conf, jt_handle,
+                              name=f"tracker_{socket.gethostname()}_r{self.rank}", rank=self.rank,
+                              world_size=self.world, gpu_devices=gpus, comm=self.comm)
+        self.tt.start()
+        if self.jt is not None:
+            if not self.jt.wait_for_trackers(self.world, timeout=300):
+                raise RuntimeError("not all TaskTrackers registered with the JobTracker")
+            self.jt.start_expiry_thread()
+
+    @property
+    def is_master(self):
+        return self.rank == 0
+
+    def submit_job(self, job):
+        return self.jt.submit_job(job)
+
+    def job_result(self, rj, partition=0):
+        r = rj._impl.jip.result
+        return None if r is None else r.get(partition)
+
+    def serve_until_shutdown(self):
+        """Non-master ranks: run the tracker until the JobTracker says shutdown."""
+        while not self.tt._stop.is_set():
+            time.sleep(0.05)
+
+    def shutdown(self):
+        if self.jt is not None:
+            self.jt.broadcast_shutdown()
+            # wait for the other trackers to receive the shutdown action
+            deadline = time.time() + 30
+            while time.time() < deadline:
+                with self.jt.lock:
+                    others = [t for t in self.jt.trackers.values()
+                              if t.name != self.tt.name and time.time() - t.last_seen < 0.5]
+                if not others or time.time() > deadline:
+                    break
+                time.sleep(0.1)
+        self.tt.stop()
+        if self.jt is not None:
+            time.sleep(0.2)
+            self.jt.shutdown()
+        if self.dist is not None:
+            try:
+                self.dist.barrier(group=self.comm.cpu_group)
+            except Exception:  # noqa: BLE001
+                pass
+            self.dist.destroy_process_group()
+        if self.server is not None:
+            self.server.stop()

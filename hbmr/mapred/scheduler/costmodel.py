@@ -1,0 +1,166 @@
+"""Profiled CPU-vs-GPU cost model (the fork's scheduler inputs, redesigned).
+
+The reference recomputes mean CPU/GPU map-task times by regenerating every
+TaskReport of every running job on every heartbeat under the JobTracker lock
+(JobInProgress.java:508-618 → JobTracker.getMapTaskReports),
+takes the accel factor from the last job only (B5) and leaves its
+min-makespan solver commented out (JobQueueTaskScheduler.java:181-220, G3).
+
+Here:
+* per job *signature* (mapper/input format/split size), O(1) running stats of
+  completed CPU and GPU map-task durations (mean + EWMA), shared across jobs of
+  the same signature so iterative jobs (K-Means iterations) start profiled;
+* running attempts give a censored lower bound: a CPU probe that has run for
+  t seconds proves t_cpu ≥ t, so the GPU/CPU ratio is bounded before the probe
+  finishes;
+* the min-makespan split of P pending maps over C CPU and G GPU slots,
+  ``min_x max(ceil(x/C)·t_c, ceil((P-x)/G)·t_g)``, is solved exactly in O(P/C).
+"""
+from __future__ import annotations
+
+import math
+import threading
+from dataclasses import dataclass, field
+
+
+@dataclass
+class TimeStats:
+    n: int = 0
+    total: float = 0.0
+    ewma: float = 0.0
+    min: float = math.inf
+    max: float = 0.0
+    running: dict = field(default_factory=dict)   # attempt -> start time
+    lower_bound: float = 0.0   # censored: killed/failed attempts ran at least this long
+
+    def add(self, dt: float, alpha: float):
+        self.n += 1
+        self.total += dt
+        self.ewma = dt if self.n == 1 else (alpha * dt + (1 - alpha) * self.ewma)
+        self.min = min(self.min, dt)
+        self.max = max(self.max, dt)
+
+    @property
+    def mean(self):
+        return self.total / self.n if self.n else 0.0
+
+    def estimate(self, now: float):
+        """(estimate seconds or None, is_lower_bound)."""
+        if self.n:
+            est = self.ewma
+            # a running attempt older than the estimate raises it (stragglers)
+            oldest = max((now - s for s in self.running.values()), default=0.0)
+            if oldest > 2 * est:
+                return oldest, True
+            return est, False
+        lb = max([now - s for s in self.running.values()] + [self.lower_bound])
+        if lb > 0:
+            return lb, True
+        return None, False
+
+
+class CostModel:
+    def __init__(self, alpha: float = 0.3):
+        self.alpha = alpha
+        self._lock = threading.Lock()
+        self._stats: dict[str, dict[str, TimeStats]] = {}
+
+    def _get(self, sig):
+        d = self._stats.get(sig)
+        if d is None:
+            d = self._stats[sig] = {"cpu": TimeStats(), "gpu": TimeStats()}
+        return d
+
+    def task_started(self, sig, attempt, on_gpu, t):
+        with self._lock:
+            self._get(sig)["gpu" if on_gpu else "cpu"].running[attempt] = t
+
+    def task_finished(self, sig, attempt, on_gpu, start, finish, succeeded=True):
+        with self._lock:
+            st = self._get(sig)["gpu" if on_gpu else "cpu"]
+            st.running.pop(attempt, None)
+            if succeeded and finish >= start:
+                st.add(finish - start, self.alpha)
+            elif not succeeded and finish > start:
+                # a killed attempt (e.g. a CPU probe overtaken by its GPU backup)
+                # still proves the task takes at least this long on that slot type
+                st.lower_bound = max(st.lower_bound, finish - start)
+
+    def stats(self, sig, on_gpu) -> TimeStats:
+        with self._lock:
+            return self._get(sig)["gpu" if on_gpu else "cpu"]
+
+    def finished_counts(self, sig):
+        with self._lock:
+            d = self._get(sig)
+            return d["cpu"].n, d["gpu"].n
+
+    def mean_times(self, sig):
+        with self._lock:
+            d = self._get(sig)
+            return d["cpu"].mean, d["gpu"].mean
+
+    def acceleration(self, sig, now: float):
+        """GPU speed-up t_cpu / t_gpu (the reference's accelarationFactor,
+        JobQueueTaskScheduler.java:175-177), or None when unknown.  Returns
+        (value, is_lower_bound)."""
+        with self._lock:
+            d = self._get(sig)
+            tc, tc_lb = d["cpu"].estimate(now)
+            tg, _ = d["gpu"].estimate(now)
+        if tc is None or tg is None or tg <= 0:
+            return None, False
+        return tc / tg, tc_lb
+
+    def snapshot(self):
+        with self._lock:
+            return {sig: {k: {"n": v.n, "mean": v.mean, "ewma": v.ewma, "running": len(v.running)}
+                          for k, v in d.items()} for sig, d in self._stats.items()}
+
+
+def min_makespan_cpu_tasks(pending: int, cpu_slots: int, gpu_slots: int, t_cpu: float,
+                           t_gpu: float) -> int:
+    """Number of the ``pending`` tasks to give CPU slots so the makespan
+    max(ceil(x/C)·t_c, ceil((P-x)/G)·t_g) is minimal (Shirahata et al.'s
+    objective, made live).  Ties go to fewer CPU tasks."""
+    if pending <= 0:
+        return 0
+    if gpu_slots <= 0:
+        return pending
+    if cpu_slots <= 0 or t_cpu is None or t_gpu is None:
+        return 0
+    best_x, best = 0, math.ceil(pending / gpu_slots) * t_gpu
+    waves = math.ceil(pending / cpu_slots)
+    for w in range(1, waves + 1):
+        x = min(pending, w * cpu_slots)
+        cost = max(w * t_cpu, math.ceil((pending - x) / gpu_slots) * t_gpu)
+        if cost < best - 1e-12:
+            best, best_x = cost, x
+    return best_x
+
+
+def makespan_estimates(pending, cpu_slots, gpu_slots, t_cpu, t_gpu):
+    """CPU-only, GPU-only, greedy and optimal makespan estimates (the quantities
+    the reference logs at JobQueueTaskScheduler.java:181-220)."""
+    out = {}
+    if t_cpu and cpu_slots:
+        out["cpu_only"] = math.ceil(pending / cpu_slots) * t_cpu
+    if t_gpu and gpu_slots:
+        out["gpu_only"] = math.ceil(pending / gpu_slots) * t_gpu
+    if t_cpu and t_gpu and cpu_slots and gpu_slots:
+        x = min_makespan_cpu_tasks(pending, cpu_slots, gpu_slots, t_cpu, t_gpu)
+        out["optimal"] = max(math.ceil(x / cpu_slots) * t_cpu if x else 0.0,
+                             math.ceil((pending - x) / gpu_slots) * t_gpu)
+        out["optimal_cpu_tasks"] = x
+        # greedy: every slot takes the next task as it frees
+        tc = [0.0] * cpu_slots
+        tg = [0.0] * gpu_slots
+        for _ in range(pending):
+            ic = min(range(cpu_slots), key=lambda i: tc[i])
+            ig = min(range(gpu_slots), key=lambda i: tg[i])
+            if tc[ic] <= tg[ig]:
+                tc[ic] += t_cpu
+            else:
+                tg[ig] += t_gpu
+        out["greedy"] = max(max(tc), max(tg))
+    return out

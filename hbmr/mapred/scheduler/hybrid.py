@@ -1,0 +1,197 @@
+"""GPU-aware map-task schedulers.
+
+:class:`HybridTaskScheduler` is the redesign of the fork's
+JobQueueTaskScheduler (hadoop-1.0.3/src/mapred/org/apache/hadoop/mapred/
+JobQueueTaskScheduler.java:86-575).  Per heartbeat of a
+tracker it fills free GPU slots (device by device, data-locality first, every
+GPU attempt told its device id) and then decides how many CPU map tasks a job
+should get, under ``hbmr.scheduler.policy``:
+
+* ``stock``    – GPU-unaware FIFO: every free slot takes the next task (the
+                 baseline of Shirahata et al. and of the non-GPU-aware
+                 schedulers, B10);
+* ``optional`` – the fork's live rule (JobQueueTaskScheduler.java:290-291): CPU
+                 slots stay idle while ``pending < accel × total GPU slots``;
+* ``hybrid``   – (default) the fork's dead min-makespan solver made live
+                 (JobQueueTaskScheduler.java:181-220): CPU slots take a task only
+                 while the job's running CPU tasks are below the count x* that
+                 minimises max(ceil(x/C)·t_cpu, ceil((P-x)/G)·t_gpu).  Before a
+                 CPU profile exists one probe task runs on a CPU slot; a running
+                 probe already bounds t_cpu from below (costmodel.py).
+
+Locality (``obtain_map``): split resident in this device's HBM > resident on
+this tracker > node-local by split locations > any, with delay scheduling
+(``hbmr.locality.delay.heartbeats``) before a GPU takes a non-local split.
+Reduces: classic reduces go to free reduce slots once all maps are done;
+collective (RCCL) reduces are gang-launched, one pinned to each tracker.
+"""
+from __future__ import annotations
+
+import logging
+import time
+
+from .costmodel import min_makespan_cpu_tasks
+
+log = logging.getLogger("hbmr.scheduler")
+
+
+class TaskScheduler:
+    def __init__(self, jt, conf):
+        self.jt = jt
+        self.conf = conf
+
+    def assign_tasks(self, tracker):
+        raise NotImplementedError
+
+
+class HybridTaskScheduler(TaskScheduler):
+    def __init__(self, jt, conf):
+        super().__init__(jt, conf)
+        self.policy = conf.get("hbmr.scheduler.policy", "hybrid").lower()
+        if conf.get_boolean("mapred.jobtracker.map.optionalscheduling", False) and \
+                self.policy == "hybrid" and conf.get("hbmr.scheduler.policy.explicit") is None:
+            self.policy = "optional"
+        self.queue_depth = max(1, conf.get_int("hbmr.gpu.queue.depth", 4))
+        self.locality_wait = conf.get_int("hbmr.locality.wait.ms", 500) / 1000.0
+        self.max_reduces_per_hb = conf.get_int("hbmr.scheduler.max.reduces.per.heartbeat", 4)
+        self.speculate_after = conf.get_float("hbmr.speculative.slowdown", 3.0)
+        self._skips: dict = {}
+        self.decisions = 0
+
+    # -- cluster capacity ----------------------------------------------------------------
+    def _totals(self):
+        cpu = gpu = 0
+        for t in self.jt.trackers.values():
+            if t.blacklisted:
+                continue
+            cpu += t.status.max_cpu_map_slots
+            gpu += sum(g["max_slots"] for g in t.status.gpus)
+        return cpu, gpu
+
+    def _cpu_allowed(self, jip, total_cpu, total_gpu, now):
+        if not jip.cpu_capable:
+            return 0
+        running_cpu = jip.running_maps(on_gpu=False)
+        pending = jip.pending_map_count()
+        if not jip.gpu_capable or total_gpu == 0:
+            return pending
+        if self.policy == "stock":
+            return pending
+        cm = self.jt.cost_model
+        sig = jip.signature
+        if self.policy == "optional":
+            accel, _ = cm.acceleration(sig, now)
+            if accel is None:
+                accel = 1.0
+            # !(optional && pendingMaps < accel * gpuSlots)  → CPU may take work
+            return pending if not (pending < accel * total_gpu) else 0
+        # hybrid (min-makespan)
+        cs, gs = cm.stats(sig, False), cm.stats(sig, True)
+        t_cpu, _ = cs.estimate(now)
+        t_gpu, _ = gs.estimate(now)
+        if t_cpu is None:
+            # profile: one CPU probe per signature (if none is running)
+            return 1 if running_cpu == 0 and not cs.running else 0
+        if t_gpu is None:
+            return 0 if running_cpu else min(1, pending)
+        x = min_makespan_cpu_tasks(pending + running_cpu, total_cpu, total_gpu, t_cpu, t_gpu)
+        return max(0, x - running_cpu)
+
+    # -- main entry -----------------------------------------------------------------
+    def assign_tasks(self, tr):
+        jt = self.jt
+        actions = []
+        now = time.time()
+        total_cpu, total_gpu = self._totals()
+        cpu_free = tr.status.max_cpu_map_slots - tr.running_cpu
+        reduce_free = tr.status.max_reduce_slots - tr.running_reduce
+        gpu_free = {g["device"]: g["max_slots"] * self.queue_depth - tr.running_gpu.get(
+            g["device"], 0) for g in tr.status.gpus}
+        for jip in sorted(jt.job_queue, key=lambda j: (_prio(j.priority), j.submit_time)):
+            if jip.completed():
+                continue
+            # ---- reduces
+            if jip.reduces and jip.maps_complete():
+                n_red = 0
+                for tip in jip.reduces:
+                    if tip.is_complete() or tip.is_running():
+                        continue
+                    if jip.collective_reduce:
+                        if tip.pinned_tracker != tr.name:
+                            continue
+                    elif reduce_free <= 0 or n_red >= self.max_reduces_per_hb:
+                        break
+                    extra = {"map_outputs": jt.reduce_inputs(jip, tr.name)}
+                    actions.append(jt.launch(tr, tip, extra=extra))
+                    n_red += 1
+                    reduce_free -= 1
+            if not jip.pending_maps:
+                continue
+            # ---- GPU maps
+            if jip.gpu_capable:
+                for dev in sorted(gpu_free):
+                    while gpu_free[dev] > 0 and jip.pending_maps:
+                        # delay scheduling: a GPU waits up to locality_wait for a
+                        # split it holds in HBM / that names it before it steals a
+                        # non-local one (a non-local split must be re-materialised)
+                        key = (str(jip.job_id), tr.name, dev)
+                        first = self._skips.get(key)
+                        allow_nonlocal = self.policy == "stock" or (
+                            first is not None and now - first >= self.locality_wait)
+                        got = jip.obtain_map(tr, True, dev, allow_nonlocal=allow_nonlocal)
+                        if got is None:
+                            if first is None:
+                                self._skips[key] = now
+                            break
+                        tip, level = got
+                        if level < 3:
+                            self._skips.pop(key, None)
+                        actions.append(jt.launch(tr, tip, on_gpu=True, device=dev))
+                        gpu_free[dev] -= 1
+                        self.decisions += 1
+            # ---- CPU maps
+            if cpu_free > 0 and jip.pending_maps:
+                allowed = self._cpu_allowed(jip, total_cpu, total_gpu, now)
+                while cpu_free > 0 and allowed > 0 and jip.pending_maps:
+                    got = jip.obtain_map(tr, False, -1, allow_nonlocal=True)
+                    if got is None:
+                        break
+                    tip, _ = got
+                    actions.append(jt.launch(tr, tip, on_gpu=False))
+                    cpu_free -= 1
+                    allowed -= 1
+                    self.decisions += 1
+            # ---- speculative backups of stragglers onto idle GPUs
+            if jip.speculative and jip.gpu_capable and not jip.pending_maps:
+                for dev in sorted(gpu_free):
+                    if gpu_free[dev] < tr.gpu_capacity(dev) * self.queue_depth:
+                        continue  # only fully idle devices back up stragglers
+                    tip = self._straggler(jip, now)
+                    if tip is None:
+                        break
+                    actions.append(jt.launch(tr, tip, on_gpu=True, device=dev, speculative=True))
+                    gpu_free[dev] -= 1
+        return actions
+
+    def _straggler(self, jip, now):
+        """A running map whose only attempt is on a CPU (or has run > slowdown ×
+        the GPU estimate) and has no backup yet."""
+        cm = self.jt.cost_model
+        t_gpu, _ = cm.stats(jip.signature, True).estimate(now)
+        for tip in jip.maps:
+            if tip.is_complete():
+                continue
+            run = tip.running_attempts()
+            if len(run) != 1:
+                continue
+            a = run[0]
+            elapsed = now - a.start
+            if not a.run_on_gpu and t_gpu is not None and elapsed > t_gpu * 2:
+                return tip
+            if a.run_on_gpu and t_gpu is not None and elapsed > self.speculate_after * t_gpu + 1.0:
+                return tip
+        return None
+
+
+def _prio(p):
+    return {"VERY_HIGH": 0, "HIGH": 1, "NORMAL": 2, "LOW": 3, "VERY_LOW": 4}.get(str(p).upper(), 2)

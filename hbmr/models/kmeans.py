@@ -1,0 +1,431 @@
+"""K-Means as a MapReduce job family — BASELINE configs 2 and 3.
+
+One Lloyd iteration = one job (as in Shirahata et al.'s K-Means on Hadoop,
+where iterations are chained jobs and the centroids travel in the
+DistributedCache):
+
+* map (per split)      : assign every point to its nearest centroid and
+                         combine in-task to per-cluster (sum, count) partials.
+                         GPU slots run the MFMA kernels of
+                         native/kernels/kmeans.hip on the HBM-resident split;
+                         CPU slots run the native C++ map (native/cpu).
+                         Partials are int64 fixed point → exact and
+                         placement-independent.
+* combine (per tracker): sum the committed attempts' partials on the device.
+* reduce (collective)  : one all-reduce of the [k, dp+1] int64 partials over
+                         RCCL (xGMI), then every tracker computes the new
+                         centroids and keeps them resident for the next
+                         iteration — the DistributedCache broadcast becomes a
+                         no-op.  Reducer r commits clusters of partition r to
+                         the job output directory (if one is set).
+
+Inputs: ``synthetic:<points>:<seed>`` (a Gaussian mixture generated directly
+into HBM by a counter-based generator, identical on CPU and GPU) or a path of
+SequenceFiles of (LongWritable, FloatVectorWritable).
+"""
+from __future__ import annotations
+
+import base64
+import logging
+import math
+import threading
+import time
+
+import numpy as np
+import torch
+
+from ..gpu.splitjob import SplitJob, SplitSpec
+from ..mapred import counters as C
+
+log = logging.getLogger("hbmr.kmeans")
+
+K_KEY = "hbmr.kmeans.k"
+D_KEY = "hbmr.kmeans.dims"
+INPUT_KEY = "hbmr.kmeans.input"
+SPLIT_PTS_KEY = "hbmr.split.points"
+CIN_KEY = "hbmr.kmeans.centroids.in"
+COUT_KEY = "hbmr.kmeans.centroids.out"
+INIT_KEY = "hbmr.kmeans.centroids.init"     # base64 fp32 [k, d] (first iteration only)
+NCENTERS_KEY = "hbmr.kmeans.synthetic.centers"
+
+# --------------------------------------------------------------------------- data
+_M32 = 0xFFFFFFFF
+
+
+def _mix32(x: torch.Tensor) -> torch.Tensor:
+    """32-bit integer finaliser (values kept in int64, all products < 2^63)."""
+    x = x & _M32
+    x = ((x ^ (x >> 16)) * 0x45D9F3B) & _M32
+    x = ((x ^ (x >> 16)) * 0x45D9F3B) & _M32
+    return x ^ (x >> 16)
+
+
+def _uniform(c: torch.Tensor) -> torch.Tensor:
+    return (_mix32(c).to(torch.float64) + 0.5) * (1.0 / 4294967296.0)
+
+
+def _gauss(c1: torch.Tensor, c2: torch.Tensor) -> torch.Tensor:
+    u1 = _uniform(c1)
+    u2 = _uniform(c2)
+    return torch.sqrt(-2.0 * torch.log(u1)) * torch.cos(2.0 * math.pi * u2)
+
+
+def synthetic_points(seed: int, start: int, n: int, d: int, centers: int, device,
+                     chunk: int = 1 << 18) -> torch.Tensor:
+    """Gaussian-mixture points [n, d] (float32) for global indices [start, start+n).
+
+    Counter-based: point p, dim j depends only on (seed, p, j), so any split is
+    generated independently and identically on CPU or GPU."""
+    dev = torch.device(device)
+    out = torch.empty(n, d, dtype=torch.float32, device=dev)
+    j = torch.arange(d, dtype=torch.int64, device=dev)
+    cidx = torch.arange(centers, dtype=torch.int64, device=dev)
+    s = (seed * 0x9E3779B1) & _M32
+    # centers: 10 × N(0,1) per (center, dim)
+    cc = (cidx[:, None] * 131071 + j[None, :] + s * 7) & _M32
+    cen = 10.0 * _gauss(cc * 2 + 1, cc * 2 + 2)
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        p = torch.arange(start + a, start + b, dtype=torch.int64, device=dev)
+        lab = _mix32(p * 3 + s) % centers
+        base = ((p[:, None] & 0xFFFFFF) * 1024 + j[None, :] + (s << 7)) & _M32
+        noise = _gauss(base * 2 + 11, base * 2 + 12 + (p[:, None] >> 24))
+        out[a:b] = (cen[lab] + noise).to(torch.float32)
+    return out
+
+
+def encode_centroids(c: torch.Tensor) -> str:
+    a = c.detach().to("cpu", torch.float32).contiguous().numpy()
+    return f"{a.shape[0]}x{a.shape[1]}:" + base64.b64encode(a.tobytes()).decode()
+
+
+def decode_centroids(s: str) -> torch.Tensor:
+    shp, b = s.split(":", 1)
+    k, d = map(int, shp.split("x"))
+    return torch.from_numpy(np.frombuffer(base64.b64decode(b), dtype=np.float32).copy()
+                            ).reshape(k, d)
+
+
+# --------------------------------------------------------------------------- side data
+class CentroidStore:
+    """Per-process centroid versions, the DistributedCache analogue: key →
+    fp32 host centroids and per-device bf16 images (CentroidImage)."""
+
+    def __init__(self):
+        self.lock = threading.Lock()
+        self.host: dict[str, torch.Tensor] = {}
+        self.images: dict[tuple, object] = {}
+        self.order: list[str] = []
+        self.keep = 4
+
+    def put_host(self, key, cen):
+        with self.lock:
+            self.host[key] = cen
+            self._touch(key)
+
+    def put_image(self, key, device, img):
+        with self.lock:
+            self.images[(key, str(device))] = img
+            self._touch(key)
+
+    def _touch(self, key):
+        if key in self.order:
+            self.order.remove(key)
+        self.order.append(key)
+        while len(self.order) > self.keep:
+            old = self.order.pop(0)
+            self.host.pop(old, None)
+            for k in [k for k in self.images if k[0] == old]:
+                self.images.pop(k)
+
+    def host_centroids(self, key):
+        with self.lock:
+            c = self.host.get(key)
+            if c is not None:
+                return c
+            for (k, _dev), img in self.images.items():
+                if k == key:
+                    c = img.cen.detach().to("cpu")
+                    self.host[key] = c
+                    return c
+        return None
+
+    def image(self, key, device):
+        from ..ops import kmeans as km
+        with self.lock:
+            img = self.images.get((key, str(device)))
+        if img is not None:
+            return img
+        cen = self.host_centroids(key)
+        if cen is None:
+            raise KeyError(f"centroids {key!r} not resident on this tracker")
+        img = km.CentroidImage(cen, device)
+        self.put_image(key, device, img)
+        return img
+
+
+STORE = CentroidStore()
+
+
+# --------------------------------------------------------------------------- the job
+class KMeansSplitJob(SplitJob):
+    collective_reduce = True
+    needs_reduce = True
+
+    def configure(self, conf):
+        self.conf = conf
+        self.k = conf.get_int(K_KEY, 64)
+        self.d = conf.get_int(D_KEY, 128)
+        self.input = conf.get(INPUT_KEY, "synthetic:100000:1")
+        self.split_points = conf.get_int(SPLIT_PTS_KEY, 500_000)
+        self.cin = conf.get(CIN_KEY)
+        self.cout = conf.get(COUT_KEY)
+        self.centers = conf.get_int(NCENTERS_KEY, self.k)
+        self.fx_shift = conf.get_int("hbmr.kmeans.fx.shift", 24)
+        init = conf.get(INIT_KEY)
+        if init and self.cin and STORE.host_centroids(self.cin) is None:
+            STORE.put_host(self.cin, decode_centroids(init))
+
+    # -- splits -------------------------------------------------------------------
+    def get_splits(self, conf, trackers):
+        if self.input.startswith("synthetic:"):
+            _, n, seed = self.input.split(":")
+            n, seed = int(n), int(seed)
+            per = self.split_points
+            nsplits = max(1, math.ceil(n / per))
+            out = []
+            for i in range(nsplits):
+                a = i * per
+                m = min(per, n - a)
+                key = f"kmeans-syn:{seed}:{self.d}:{self.centers}:{a}:{m}"
+                loc = [trackers[i * len(trackers) // nsplits]] if trackers else []
+                out.append(SplitSpec(i, key, "synthetic",
+                                     {"seed": seed, "start": a, "n": m}, loc, m * self.d * 2))
+            return out
+        from ..mapred.formats import FileInputFormat, SequenceFileInputFormat
+        from ..mapred.jobconf import JobConf
+        jc = JobConf(conf)
+        FileInputFormat.setInputPaths(jc, self.input)
+        fmt = SequenceFileInputFormat()
+        splits = fmt.getSplits(jc, max(1, conf.get_int("mapred.map.tasks", 1)))
+        out = []
+        for i, s in enumerate(splits):
+            key = f"kmeans-file:{s.path}:{s.start}:{s.length}"
+            loc = [trackers[i % len(trackers)]] if trackers else []
+            out.append(SplitSpec(i, key, "file", {"path": s.path, "start": s.start,
+                                                  "length": s.length}, loc, s.length))
+        return out
+
+    def _load_fp32(self, spec: SplitSpec, device):
+        if spec.kind == "synthetic":
+            p = spec.params
+            x = synthetic_points(p["seed"], p["start"], p["n"], self.d, self.centers, device)
+        else:
+            from ..mapred.formats import FileSplit, SequenceFileRecordReader
+            from ..mapred.jobconf import JobConf
+            p = spec.params
+            rr = SequenceFileRecordReader(JobConf(), FileSplit(p["path"], p["start"],
+                                                               p["length"]))
+            rows = []
+            while True:
+                raw = rr.next_raw()
+                if raw is None:
+                    break
+                rows.append(np.frombuffer(raw[1][4:], dtype=">f4"))
+            rr.close()
+            arr = np.stack(rows).astype(np.float32) if rows else np.zeros((0, self.d), np.float32)
+            x = torch.from_numpy(arr).to(device)
+        # bf16 is the storage precision of the points on every slot type
+        return x.to(torch.bfloat16)
+
+    def load_split(self, spec: SplitSpec, device):
+        from ..ops import kmeans as km
+        xb = self._load_fp32(spec, device)
+        if str(device) == "cpu":
+            return xb.to(torch.float32)
+        dp = km.padded_dim(self.d)
+        if dp == self.d:
+            return xb.contiguous()
+        out = torch.zeros(xb.shape[0], dp, dtype=torch.bfloat16, device=device)
+        out[:, :self.d] = xb
+        return out
+
+    # -- map ------------------------------------------------------------------------
+    def map_gpu(self, ctx, points):
+        from ..ops import kmeans as km
+        img = STORE.image(self.cin, ctx.device)
+        sums, counts = km.new_partials(self.k, img.dp, ctx.device)
+        ws = ctx.job.scratch.get(("ws", id(ctx.stream)))
+        n = points.shape[0]
+        need = km.workspace_bytes(n, self.k)
+        if ws is None or ws.numel() < need:
+            ws = torch.empty(max(need, 1 << 20), dtype=torch.uint8, device=ctx.device)
+            ctx.job.scratch[("ws", id(ctx.stream))] = ws
+        labels = ctx.job.scratch.get(("lab", id(ctx.stream)))
+        if labels is None or labels.numel() < n:
+            labels = torch.empty(max(n, 1), dtype=torch.int32, device=ctx.device)
+            ctx.job.scratch[("lab", id(ctx.stream))] = labels
+        km.assign(points, img, labels=labels[:n], stream=ctx.stream)
+        km.accumulate(points, labels[:n], self.k, sums, counts, fx_shift=self.fx_shift,
+                      stream=ctx.stream, workspace=ws)
+        ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, n)
+        return sums, counts
+
+    def map_cpu(self, ctx, points):
+        from ..ops import kmeans as km
+        cen = STORE.host_centroids(self.cin)
+        if cen is None:
+            raise KeyError(f"centroids {self.cin!r} not resident")
+        sums, counts = km.new_partials(self.k, self.d, "cpu")
+        km.map_split_cpu(points, cen, sums, counts, nthreads=ctx.cpu_threads,
+                         fx_shift=self.fx_shift)
+        ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, points.shape[0])
+        return sums, counts
+
+    # -- combine + reduce -------------------------------------------------------------------
+    def combine(self, ctx, outputs):
+        from ..ops import kmeans as km
+        dev = ctx.device if ctx.device is not None else torch.device("cpu")
+        dp = km.padded_dim(self.d) if dev.type == "cuda" else self.d
+        sums = torch.zeros(self.k, dp, dtype=torch.int64, device=dev)
+        counts = torch.zeros(self.k, dtype=torch.int64, device=dev)
+        for s, c in outputs:
+            sums[:, :s.shape[1]] += s.to(dev, non_blocking=True)
+            counts += c.to(dev, non_blocking=True)
+        return sums, counts
+
+    def reduce(self, ctx, combined):
+        from ..ops import kmeans as km
+        sums, counts = combined
+        k, dp = sums.shape
+        packed = torch.cat([sums.reshape(-1), counts])
+        ctx.comm.all_reduce(packed)        # exact: int64 over RCCL / gloo
+        sums = packed[:k * dp].view(k, dp)
+        counts = packed[k * dp:]
+        if sums.device.type == "cuda":
+            old = STORE.image(self.cin, sums.device)
+            img = km.CentroidImage.__new__(km.CentroidImage)
+            img.__dict__.update(old.__dict__)
+            img.cen = old.cen.clone()
+            img.cbf = old.cbf.clone()
+            img.chalf = old.chalf.clone()
+            img.shift2 = torch.zeros_like(old.shift2)
+            img.refresh(sums, counts)
+            STORE.put_image(self.cout, sums.device, img)
+            shift = img.max_shift()
+            new_cen = None
+        else:
+            old = STORE.host_centroids(self.cin)
+            cnt = counts.to(torch.float64)[:, None]
+            s = sums[:, :self.d].to(torch.float64) / float(1 << self.fx_shift)
+            new_cen = torch.where(cnt > 0, s / cnt.clamp(min=1), old.to(torch.float64)).to(
+                torch.float32)
+            shift = float((new_cen - old).norm(dim=1).max()) if self.k else 0.0
+            STORE.put_host(self.cout, new_cen)
+        self._write_output(ctx, counts, new_cen)
+        return {"shift": shift, "points": int(counts.sum().item()), "centroids_key": self.cout}
+
+    def _write_output(self, ctx, counts, new_cen):
+        out = self.conf.get("mapred.output.dir")
+        if not out:
+            return
+        import os
+
+        from ..io import sequencefile as seqf
+        from ..io.writable import FloatVectorWritable, IntWritable
+        cen = new_cen if new_cen is not None else STORE.host_centroids(self.cout)
+        W = ctx.world_size
+        per = math.ceil(self.k / W)
+        lo, hi = ctx.rank * per, min(self.k, (ctx.rank + 1) * per)
+        os.makedirs(out, exist_ok=True)
+        with seqf.Writer(os.path.join(out, f"part-{ctx.rank:05d}"), IntWritable,
+                         FloatVectorWritable) as w:
+            for j in range(lo, hi):
+                w.append(IntWritable(j), FloatVectorWritable(cen[j].numpy()))
+
+
+# --------------------------------------------------------------------------- driver
+def make_iteration_conf(base, k, d, inp, split_points, cin, cout, init=None):
+    from ..mapred.jobconf import JobConf
+    job = JobConf(base)
+    job.set_job_name(f"kmeans {cin}->{cout}")
+    job.set("hbmr.splitjob.class", "hbmr.models.kmeans:KMeansSplitJob")
+    job.set("hbmr.gpu.mapper.class", "hbmr.models.kmeans:KMeansSplitJob")
+    job.set_int(K_KEY, k)
+    job.set_int(D_KEY, d)
+    job.set(INPUT_KEY, inp)
+    job.set_int(SPLIT_PTS_KEY, split_points)
+    job.set(CIN_KEY, cin)
+    job.set(COUT_KEY, cout)
+    job.set("hbmr.job.signature", f"kmeans|{inp}|{k}|{d}|{split_points}")
+    if init is not None:
+        job.set(INIT_KEY, encode_centroids(init))
+    return job
+
+
+def initial_centroids(inp, k, d, centers=None):
+    """First k points of the input (deterministic)."""
+    if inp.startswith("synthetic:"):
+        _, _n, seed = inp.split(":")
+        x = synthetic_points(int(seed), 0, k, d, centers or k, "cpu")
+        return x.to(torch.bfloat16).to(torch.float32)
+    from ..io import sequencefile as seqf
+    import os
+    path = inp
+    if os.path.isdir(path):
+        path = os.path.join(path, sorted(f for f in os.listdir(path) if not f.startswith(("_", ".")))[0])
+    rows = []
+    with seqf.Reader(path) as r:
+        while len(rows) < k:
+            raw = r.next_raw()
+            if raw is None:
+                break
+            rows.append(np.frombuffer(raw[1][4:], dtype=">f4").astype(np.float32))
+    return torch.from_numpy(np.stack(rows)).to(torch.bfloat16).to(torch.float32)
+
+
+class KMeansDriver:
+    """Chains K-Means iteration jobs (what the paper's K-Means driver does with
+    separate Hadoop jobs)."""
+
+    def __init__(self, submit, result_of, conf=None, k=64, d=128, inp="synthetic:100000:1",
+                 split_points=500_000, run_id=None):
+        self.submit = submit          # conf -> RunningJob
+        self.result_of = result_of    # RunningJob -> reduce result dict
+        self.base = conf
+        self.k, self.d, self.inp, self.split_points = k, d, inp, split_points
+        self.run_id = run_id or f"km{int(time.time() * 1e3) & 0xFFFFFF:x}"
+        self.iteration = 0
+        self.history = []
+
+    def key(self, i):
+        return f"{self.run_id}:{i}"
+
+    def step(self):
+        i = self.iteration
+        init = initial_centroids(self.inp, self.k, self.d) if i == 0 else None
+        if init is not None:
+            STORE.put_host(self.key(0), init)
+        job = make_iteration_conf(self.base, self.k, self.d, self.inp, self.split_points,
+                                  self.key(i), self.key(i + 1), init=init)
+        t0 = time.time()
+        rj = self.submit(job)
+        rj.waitForCompletion()
+        if not rj.isSuccessful():
+            raise RuntimeError(f"K-Means iteration {i} failed: {rj.getFailureInfo()}")
+        res = dict(self.result_of(rj) or {})
+        res.update(iteration=i, seconds=time.time() - t0, job=str(rj.getID()),
+                   counters=rj.getCounters())
+        self.history.append(res)
+        self.iteration += 1
+        return res
+
+    def run(self, max_iter=10, tol=0.0):
+        for _ in range(max_iter):
+            r = self.step()
+            if r.get("shift", 1.0) <= tol:
+                break
+        return self.centroids()
+
+    def centroids(self):
+        return STORE.host_centroids(self.key(self.iteration))

@@ -105,6 +105,10 @@ ACCUM_AUTO, ACCUM_LDS, ACCUM_SORTED = 0, 1, 2
 _workspaces: dict = {}
 
 
+def workspace_bytes(n: int, k: int) -> int:
+    return int(_lib.load().hbmr_kmeans_accum_workspace_bytes(n, k))
+
+
 def accum_workspace(n: int, k: int, device) -> torch.Tensor:
     """Per-(device, stream-free) scratch for the sorted combiner, grown on demand.
 

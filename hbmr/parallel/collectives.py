@@ -1,0 +1,177 @@
+"""Collective communication for the MapReduce data plane.
+
+The reference moves map output over an HTTP shuffle (TaskTracker
+MapOutputServlet, TaskTracker.java:4050-4180; ReduceTask copier threads,
+ReduceTask.java:1231-1922) and ships side data through the DistributedCache.
+On one 8×MI355X node those become collectives over xGMI:
+
+* shuffle of partitioned map output      -> all-to-all(v)
+* combine-then-reduce of small partials  -> all-reduce (or reduce-scatter)
+* DistributedCache side data (centroids) -> broadcast / all-gather
+
+:class:`TorchComm` drives ``torch.distributed`` (backend ``nccl`` = RCCL for
+device tensors, ``gloo`` for CPU tensors, one process per GPU).
+:class:`InProcessComm` lets several TaskTrackers living in one process (the
+mini-cluster used by tests, like the reference's MiniMRCluster) run the same
+collective code paths.  :class:`SoloComm` is the 1-tracker no-op.
+"""
+from __future__ import annotations
+
+import threading
+
+import torch
+
+
+class Comm:
+    rank = 0
+    world_size = 1
+
+    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError
+
+    def all_gather(self, t: torch.Tensor) -> list:
+        raise NotImplementedError
+
+    def all_to_all(self, outs: list) -> list:
+        """outs[j] goes to rank j; returns ins[j] received from rank j."""
+        raise NotImplementedError
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        raise NotImplementedError
+
+    def barrier(self):
+        raise NotImplementedError
+
+    def reduce_scatter(self, t: torch.Tensor) -> torch.Tensor:
+        """Sum over ranks, rank r keeps rows [r*n/W, (r+1)*n/W) (dim 0 padded by caller)."""
+        full = self.all_reduce(t)
+        n = full.shape[0]
+        per = (n + self.world_size - 1) // self.world_size
+        return full[self.rank * per:min(n, (self.rank + 1) * per)]
+
+
+class SoloComm(Comm):
+    def all_reduce(self, t):
+        return t
+
+    def all_gather(self, t):
+        return [t]
+
+    def all_to_all(self, outs):
+        return list(outs)
+
+    def broadcast(self, t, src=0):
+        return t
+
+    def barrier(self):
+        pass
+
+
+class _Rendezvous:
+    def __init__(self, n):
+        self.n = n
+        self.barrier_obj = threading.Barrier(n)
+        self.slots = [None] * n
+        self.lock = threading.Lock()
+
+
+class InProcessComm(Comm):
+    """Collectives among ``world_size`` threads of one process."""
+
+    def __init__(self, rv: _Rendezvous, rank: int):
+        self.rv = rv
+        self.rank = rank
+        self.world_size = rv.n
+
+    @classmethod
+    def group(cls, n):
+        rv = _Rendezvous(n)
+        return [cls(rv, r) for r in range(n)]
+
+    def _exchange(self, obj):
+        rv = self.rv
+        rv.slots[self.rank] = obj
+        rv.barrier_obj.wait()
+        got = list(rv.slots)
+        rv.barrier_obj.wait()
+        return got
+
+    def all_reduce(self, t):
+        # exchange snapshots: peers may still be reading while we write into t
+        got = self._exchange(t.detach().clone())
+        out = got[0].to(t.device).clone()
+        for g in got[1:]:
+            out += g.to(t.device)
+        t.copy_(out)
+        return t
+
+    def all_gather(self, t):
+        return [g.to(t.device) for g in self._exchange(t)]
+
+    def all_to_all(self, outs):
+        got = self._exchange(list(outs))
+        return [got[j][self.rank] for j in range(self.world_size)]
+
+    def broadcast(self, t, src=0):
+        got = self._exchange(t.detach().clone())
+        t.copy_(got[src].to(t.device))
+        return t
+
+    def barrier(self):
+        self.rv.barrier_obj.wait()
+
+
+class TorchComm(Comm):
+    """torch.distributed collectives (nccl/RCCL for device tensors, gloo for host)."""
+
+    def __init__(self, group=None, cpu_group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.cpu_group = cpu_group
+        self.rank = dist.get_rank()
+        self.world_size = dist.get_world_size()
+
+    def _grp(self, t):
+        if t.device.type == "cpu" and self.cpu_group is not None:
+            return self.cpu_group
+        return self.group
+
+    def all_reduce(self, t):
+        self.dist.all_reduce(t, group=self._grp(t))
+        return t
+
+    def all_gather(self, t):
+        out = [torch.empty_like(t) for _ in range(self.world_size)]
+        self.dist.all_gather(out, t.contiguous(), group=self._grp(t))
+        return out
+
+    def all_to_all(self, outs):
+        # sizes first (tensors may differ in length along dim 0)
+        dev = outs[0].device
+        sizes = torch.tensor([o.shape[0] for o in outs], dtype=torch.int64, device=dev)
+        in_sizes = torch.empty_like(sizes)
+        self.dist.all_to_all_single(in_sizes, sizes, group=self._grp(outs[0]))
+        ins = [torch.empty((int(n),) + tuple(outs[0].shape[1:]), dtype=outs[0].dtype, device=dev)
+               for n in in_sizes.tolist()]
+        self.dist.all_to_all(ins, [o.contiguous() for o in outs], group=self._grp(outs[0]))
+        return ins
+
+    def broadcast(self, t, src=0):
+        self.dist.broadcast(t, src, group=self._grp(t))
+        return t
+
+    def barrier(self):
+        self.dist.barrier(group=self.cpu_group or self.group)
+
+    def reduce_scatter(self, t):
+        n = t.shape[0]
+        per = (n + self.world_size - 1) // self.world_size
+        if per * self.world_size != n:
+            pad = torch.zeros((per * self.world_size - n,) + tuple(t.shape[1:]), dtype=t.dtype,
+                              device=t.device)
+            t = torch.cat([t, pad])
+        out = torch.empty((per,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        self.dist.reduce_scatter_tensor(out, t.contiguous(), group=self._grp(t))
+        lo = self.rank * per
+        return out[:max(0, min(per, n - lo))]
