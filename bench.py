@@ -108,6 +108,14 @@ def main():
         cpu_maps = sum(h["counters"].get("org.apache.hadoop.mapred.JobInProgress$Counter",
                                          "CPU_MAP_TASKS") for h in hist)
         ms = dt / a.steps * 1e3
+        tls = [h.get("timeline") for h in hist if h.get("timeline")]
+
+        def _avg(key):
+            v = [t[key] for t in tls if t.get(key) is not None]
+            return round(1e3 * sum(v) / len(v), 3) if v else None
+        phases_ms = {"submit_to_first_map": _avg("first_map"), "submit_to_maps_done": _avg(
+            "maps_done"), "submit_to_first_reduce": _avg("first_reduce"),
+            "submit_to_finish": _avg("finish")}
         splits = -(-a.points // a.split_points)
         value = splits * a.steps / dt
         cm = node.jt.cost_model.snapshot()
@@ -132,6 +140,7 @@ def main():
                        "map_tasks_per_job": splits, "policy": a.policy,
                        "cpu_slots_per_tracker": a.cpu_slots, "gpu_slots_per_gpu": a.gpu_slots},
             "job_makespan_ms": round(ms, 3),
+            "phases_ms": phases_ms,
             "points_per_sec": round(a.points * a.steps / dt, 1),
             "maps_launched": n_maps, "gpu_maps": gpu_maps, "cpu_maps": cpu_maps,
             "warmup_seconds": round(t_warm, 2),

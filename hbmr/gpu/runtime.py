@@ -56,6 +56,7 @@ class GpuRuntime:
         self.tracker = tracker
         self.devices = {d: _Device(d, max(1, slots_per_device)) for d in devices}
         self.slots_per_device = max(1, slots_per_device)
+        self.max_batch = max(1, tracker.conf.get_int("hbmr.gpu.batch.max", 64))
         self._stop = threading.Event()
         reserve = tracker.conf.get_float("hbmr.gpu.hbm.reserve.gb", 16.0) * (1 << 30)
         for d, dev in self.devices.items():
@@ -102,6 +103,20 @@ class GpuRuntime:
         self.devices[d].q.put(run)
 
     # -- launcher -----------------------------------------------------------------------
+    def _drain(self, dev: _Device, first):
+        """first + whatever else is queued right now (up to max_batch)."""
+        runs = [first]
+        while len(runs) < self.max_batch:
+            try:
+                r = dev.q.get_nowait()
+            except queue.Empty:
+                break
+            if r is None:
+                dev.q.put(None)
+                break
+            runs.append(r)
+        return runs
+
     def _worker(self, dev: _Device):
         torch.cuda.set_device(dev.index)
         tracker = self.tracker
@@ -111,65 +126,105 @@ class GpuRuntime:
             run = dev.q.get()
             if run is None:
                 break
-            if run.kill.is_set():
-                tracker._finish(run, P.KILLED, "killed before start")
-                continue
-            slot = dev.slots[dev.rr % len(dev.slots)]
-            dev.rr += 1
-            js = run.job
-            rep = TaskReporter()
-
-            class _Shim:
-                reporter = rep
-                kill_event = run.kill
-            run.task = _Shim()
-            try:
-                tracker._maybe_inject_fault(run)
+            groups: dict = {}
+            for r in self._drain(dev, run):
+                if r.kill.is_set():
+                    tracker._finish(r, P.KILLED, "killed before start")
+                    continue
+                groups.setdefault(id(r.job), []).append(r)
+            for runs in groups.values():
+                js = runs[0].job
                 sj = js.split_job
-                if sj is None:
-                    raise RuntimeError("GPU map of a non split-level job requires the Pipes GPU "
-                                       "runner (hadoop.pipes.gpu.executable)")
-                sspec = SplitSpec.from_dict(run.spec.split)
-                ctx = TaskContext(tracker, js, run.spec, rep, device=dev.torch_device,
-                                  stream=slot.stream)
-                run.status.start_time = time.time()
-                with torch.cuda.stream(slot.stream):
-                    ev0 = torch.cuda.Event(enable_timing=True)
-                    ev1 = torch.cuda.Event(enable_timing=True)
-                    data, hit = tracker.split_cache.get_or_load(
-                        sspec.key, dev.index, lambda: sj.load_split(sspec, dev.torch_device),
-                        sj.split_nbytes)
+                # split a job's batch over the slots so streams overlap
+                nslot = len(dev.slots) if hasattr(sj, "map_gpu_batch") else len(runs)
+                per = max(1, -(-len(runs) // max(1, nslot)))
+                for i in range(0, len(runs), per):
+                    self._launch_batch(dev, runs[i:i + per], js, sj, SplitSpec, TaskContext)
+
+    def _launch_batch(self, dev, runs, js, sj, SplitSpec, TaskContext):  # noqa: N803
+        tracker = self.tracker
+        slot = dev.slots[dev.rr % len(dev.slots)]
+        dev.rr += 1
+        live = []
+        try:
+            if sj is None:
+                raise RuntimeError("GPU map of a non split-level job requires the Pipes GPU "
+                                   "runner (hadoop.pipes.gpu.executable)")
+            now = time.time()
+            ctxs, datas = [], []
+            with torch.cuda.stream(slot.stream):
+                for r in runs:
+                    rep = TaskReporter()
+                    r.task = _Shim(rep, r.kill)
+                    try:
+                        tracker._maybe_inject_fault(r)
+                        sspec = SplitSpec.from_dict(r.spec.split)
+                        data, hit = tracker.split_cache.get_or_load(
+                            sspec.key, dev.index,
+                            lambda s=sspec: sj.load_split(s, dev.torch_device), sj.split_nbytes)
+                    except BaseException as e:  # noqa: BLE001
+                        tracker._finish(r, P.FAILED, f"{type(e).__name__}: {e}\n"
+                                                     f"{traceback.format_exc()[-2000:]}")
+                        continue
                     rep.incrCounter("hbmr.GpuCounters",
                                     "GPU_SPLIT_CACHE_HITS" if hit else "GPU_SPLIT_CACHE_MISSES")
-                    ev0.record(slot.stream)
-                    out = sj.map_gpu(ctx, data)
-                    ev1.record(slot.stream)
-                slot.inflight += 1
-                slot.done_q.put((run, ev0, ev1, out))
-            except BaseException as e:  # noqa: BLE001
-                tracker._finish(run, P.FAILED,
-                                f"{type(e).__name__}: {e}\n{traceback.format_exc()[-2000:]}")
+                    r.status.start_time = now
+                    ctxs.append(TaskContext(tracker, js, r.spec, rep, device=dev.torch_device,
+                                            stream=slot.stream))
+                    datas.append(data)
+                    live.append(r)
+                if not live:
+                    return
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev0.record(slot.stream)
+                if len(live) > 1 and hasattr(sj, "map_gpu_batch"):
+                    outs = sj.map_gpu_batch(ctxs, datas)
+                else:
+                    outs = [sj.map_gpu(c, d) for c, d in zip(ctxs, datas)]
+                ev1.record(slot.stream)
+            slot.inflight += len(live)
+            slot.done_q.put((live, ev0, ev1, outs))
+        except BaseException as e:  # noqa: BLE001
+            for r in (live or runs):
+                if r.status.state not in P.TERMINAL:
+                    tracker._finish(r, P.FAILED,
+                                    f"{type(e).__name__}: {e}\n{traceback.format_exc()[-2000:]}")
 
     def _completer(self, slot: _Slot):
         torch.cuda.set_device(slot.device)
         tracker = self.tracker
+        where = f"cuda:{slot.device.index}"
         while True:
             item = slot.done_q.get()
             if item is None:
                 break
-            run, ev0, ev1, out = item
+            runs, ev0, ev1, outs = item
             try:
                 ev1.synchronize()
-                dt = ev0.elapsed_time(ev1) / 1000.0
-                js = run.job
+                # a batch completes together; its device time is shared evenly
+                dt = ev0.elapsed_time(ev1) / 1000.0 / max(1, len(runs))
+                js = runs[0].job
                 with js.lock:
-                    js.map_outputs[run.spec.attempt_id] = out
-                run.task.reporter.incrCounter("hbmr.GpuCounters", "GPU_KERNEL_MS", int(dt * 1e6))
-                tracker._finish(run, P.SUCCEEDED, output={"tracker": tracker.name,
-                                                          "where": f"cuda:{slot.device.index}"},
-                                device_time=dt)
+                    for r, out in zip(runs, outs):
+                        js.map_outputs[r.spec.attempt_id] = out
+                for r in runs:
+                    r.task.reporter.incrCounter("hbmr.GpuCounters", "GPU_KERNEL_US", int(dt * 1e6))
+                    tracker._finish(r, P.SUCCEEDED, output={"tracker": tracker.name,
+                                                            "where": where},
+                                    device_time=dt, wake=False)
+                tracker.notify_jobtracker()
             except BaseException as e:  # noqa: BLE001
-                tracker._finish(run, P.FAILED,
-                                f"{type(e).__name__}: {e}\n{traceback.format_exc()[-2000:]}")
+                for r in runs:
+                    tracker._finish(r, P.FAILED,
+                                    f"{type(e).__name__}: {e}\n{traceback.format_exc()[-2000:]}")
             finally:
-                slot.inflight -= 1
+                slot.inflight -= len(runs)
+
+
+class _Shim:
+    __slots__ = ("reporter", "kill_event")
+
+    def __init__(self, reporter, kill_event):
+        self.reporter = reporter
+        self.kill_event = kill_event

@@ -62,7 +62,7 @@ class TrackerInfo:
 class Attempt:
     __slots__ = ("aid", "tip", "tracker", "run_on_gpu", "device", "state", "progress",
                  "start", "finish", "counters", "output", "diagnostic", "speculative",
-                 "device_time")
+                 "device_time", "_released")
 
     def __init__(self, aid, tip, tracker, run_on_gpu, device, speculative=False):
         self.aid = aid
@@ -150,11 +150,20 @@ class JobInProgress:
         self.priority = conf.get("mapred.job.priority", "NORMAL")
         self.submit_time = time.time()
         self.launch_time = 0.0
+        self.t_first_map = 0.0       # first map attempt launched
+        self.t_maps_done = 0.0       # last map completed
+        self.t_first_reduce = 0.0    # first reduce attempt launched
+        self.maps_done = 0
+        self.reduces_done = 0
+        self.running_cpu = 0         # running CPU map attempts (O(1) for the scheduler)
+        self.running_gpu = 0
+        self.pending_counters: list = []
+        self._loc_index: dict = {}
         self.finished_cpu_maps = 0
         self.finished_gpu_maps = 0
         self.completion_events: list[dict] = []
         self.map_index: dict[str, TaskInProgress] = {}
-        self.pending_maps: list[TaskInProgress] = []   # not yet started, FIFO
+        self.pending_maps: dict = {}   # TIP -> None: not yet started, insertion (FIFO) order
         self.by_split_key: dict = {}
         self.signature = conf.get("hbmr.job.signature") or self._signature(conf)
         self.gpu_capable = conf.is_gpu_capable()
@@ -192,7 +201,7 @@ class JobInProgress:
             tip = TaskInProgress(self, TaskID(self.job_id, True, i), split=sd, partition=i)
             self.maps.append(tip)
             self.map_index[str(tip.tid)] = tip
-            self.pending_maps.append(tip)
+            self.pending_maps[tip] = None
             if sd.get("key"):
                 self.by_split_key[sd["key"]] = tip
         if self.collective_reduce and self.split_job is not None:
@@ -215,48 +224,88 @@ class JobInProgress:
         return len(self.pending_maps)
 
     def running_maps(self, on_gpu=None):
-        n = 0
-        for t in self.maps:
-            for a in t.running_attempts():
-                if on_gpu is None or a.run_on_gpu == on_gpu:
-                    n += 1
-        return n
+        if on_gpu is None:
+            return self.running_cpu + self.running_gpu
+        return self.running_gpu if on_gpu else self.running_cpu
 
     def maps_complete(self):
-        return all(t.is_complete() for t in self.maps)
+        return self.maps_done == len(self.maps)
+
+    def fold_counters(self) -> Counters:
+        """Merge the counters of newly succeeded attempts into the job's."""
+        pend, self.pending_counters = self.pending_counters, []
+        for d in pend:
+            if d:
+                self.counters.incr_all(Counters.from_dict(d))
+        return self.counters
+
+    def _index(self, tracker: TrackerInfo, on_gpu, device):
+        """Per-(tracker, device) queues of pending TIPs by locality level, built
+        once per job and consumed with lazy deletion: O(1) amortised per
+        assignment instead of the reference's scan of every TIP."""
+        key = (tracker.name, device if on_gpu else None)
+        idx = self._loc_index.get(key)
+        if idx is None or idx[3] != len(tracker.cached):
+            lv0, lv1, lv2 = [], [], []
+            cached_keys = {k for k, _ in tracker.cached}
+            for tip in self.pending_maps:
+                sk = tip.split_key()
+                if sk is not None and on_gpu and (sk, device) in tracker.cached:
+                    lv0.append(tip)
+                elif sk is not None and sk in cached_keys:
+                    lv1.append(tip)
+                elif tracker.name in tip.locations():
+                    lv2.append(tip)
+            idx = [lv0[::-1], lv1[::-1], lv2[::-1], len(tracker.cached)]
+            self._loc_index[key] = idx
+        return idx
 
     def obtain_map(self, tracker: TrackerInfo, on_gpu: bool, device: int, allow_nonlocal=True):
         """findNewMapTask with locality levels: split cached in this device's HBM
         > cached elsewhere on this tracker > node-local (split locations) > any."""
         if not self.pending_maps:
             return None
-        best = None
-        best_level = 99
+        multi = len(self.jt.trackers) > 1
+        idx = self._index(tracker, on_gpu, device)
+        for level in (0, 1, 2):
+            stack = idx[level]
+            while stack:
+                tip = stack.pop()
+                if tip in self.pending_maps and not (multi and tracker.name in tip.failed_trackers):
+                    self._take(tip)
+                    return tip, level
+        if not allow_nonlocal:
+            return None
         for tip in self.pending_maps:
-            if tracker.name in tip.failed_trackers and len(self.jt.trackers) > 1:
+            if multi and tracker.name in tip.failed_trackers:
                 continue
-            key = tip.split_key()
-            level = 3
-            if key is not None:
-                if on_gpu and (key, device) in tracker.cached:
-                    level = 0
-                elif any(k == key for k, _ in tracker.cached):
-                    level = 1
-            if level > 1 and tracker.name in tip.locations():
-                level = 2
-            if level < best_level:
-                best, best_level = tip, level
-                if level == 0:
-                    break
-        if best is None:
-            return None
-        if best_level == 3 and not allow_nonlocal:
-            return None
-        self.pending_maps.remove(best)
-        return best, best_level
+            self._take(tip)
+            return tip, 3
+        return None
+
+    def _take(self, tip):
+        del self.pending_maps[tip]
+
+    def add_pending(self, tip, front=False):
+        if tip in self.pending_maps:
+            return
+        if front:
+            self.pending_maps = {tip: None, **self.pending_maps}
+        else:
+            self.pending_maps[tip] = None
+        self._loc_index.clear()
 
     def completed(self):
         return self.status.is_complete()
+
+    def timeline(self) -> dict:
+        """Phase breakdown in seconds (submit → first map launch → last map done
+        → first reduce launch → finish)."""
+        st = self.status
+        t0 = self.submit_time
+        rel = lambda t: round(t - t0, 6) if t else None  # noqa: E731
+        return {"first_map": rel(self.t_first_map), "maps_done": rel(self.t_maps_done),
+                "first_reduce": rel(self.t_first_reduce), "finish": rel(st.finish_time)}
 
 
 class JobHistory:
@@ -290,7 +339,8 @@ class _JTJobHandle:
         return self.jip.status
 
     def counters(self):
-        return self.jip.counters
+        with self.jip.jt.lock:
+            return self.jip.fold_counters()
 
     def wait(self, timeout=None):
         return self.jip.done.wait(timeout)
@@ -383,7 +433,7 @@ class JobTracker:
                             jip.finished_gpu_maps -= 1
                         else:
                             jip.finished_cpu_maps -= 1
-                        jip.pending_maps.append(tip)
+                        jip.add_pending(tip)
 
     # -- jobs -----------------------------------------------------------------------
     def new_job_id(self):
@@ -430,6 +480,7 @@ class JobTracker:
             tip.killed = state != SUCCEEDED
         if jip in self.job_queue:
             self.job_queue.remove(jip)
+        jip.fold_counters()
         jip.counters.incr(C.JOB_GROUP, C.CPU_MAP_TASKS, jip.finished_cpu_maps)
         jip.counters.incr(C.JOB_GROUP, C.GPU_MAP_TASKS, jip.finished_gpu_maps)
         self.history.log("JOB_FINISHED", job=str(jip.job_id), state=state,
@@ -554,6 +605,13 @@ class JobTracker:
         self._update_progress(jip)
 
     def _release(self, a: Attempt):
+        if a.tip.is_map and not getattr(a, "_released", False):
+            jip = a.tip.job
+            if a.run_on_gpu:
+                jip.running_gpu = max(0, jip.running_gpu - 1)
+            else:
+                jip.running_cpu = max(0, jip.running_cpu - 1)
+        a._released = True
         tr = self.trackers.get(a.tracker)
         if tr is not None and a.aid in tr.running:
             tr.running.discard(a.aid)
@@ -580,7 +638,11 @@ class JobTracker:
         if tip.successful is not None or tip.killed:
             return  # a speculative twin already won
         tip.successful = a
-        jip.counters.incr_all(Counters.from_dict(a.counters))
+        if tip.is_map:
+            jip.maps_done += 1
+        else:
+            jip.reduces_done += 1
+        jip.pending_counters.append(a.counters)   # folded lazily (fold_counters)
         if not tip.is_map and isinstance(a.output, dict) and a.output.get("result") is not None:
             if jip.result is None:
                 jip.result = {}
@@ -604,6 +666,8 @@ class JobTracker:
         self.history.log("TASK_FINISHED", attempt=a.aid, tracker=a.tracker,
                          gpu=a.run_on_gpu, device=a.device, start=a.start, finish=a.finish,
                          device_time=a.device_time)
+        if tip.is_map and jip.maps_complete():
+            jip.t_maps_done = time.time()
         self._check_job_done(jip)
         if tip.is_map and jip.reduces and jip.maps_complete():
             self.cv.notify_all()  # reduces became schedulable: wake long-polling trackers
@@ -642,21 +706,17 @@ class JobTracker:
             return
         if not tip.running_attempts():
             if tip.is_map:
-                if tip not in jip.pending_maps:
-                    jip.pending_maps.insert(0, tip)  # failed tasks first (findNewMapTask)
+                jip.add_pending(tip, front=True)  # failed tasks first (findNewMapTask)
             elif jip.collective_reduce:
                 # a collective gang cannot restart one member: fail the job
                 self._finish_job(jip, FAILED, f"collective reduce {tip.tid} failed: {diag}")
 
     def _update_progress(self, jip: JobInProgress):
+        # O(1): completed fraction (the reference recomputed this from every TIP)
         if jip.maps:
-            jip.status.map_progress = sum(
-                1.0 if t.is_complete() else max((a.progress for a in t.attempts.values()),
-                                                default=0.0) for t in jip.maps) / len(jip.maps)
+            jip.status.map_progress = jip.maps_done / len(jip.maps)
         if jip.reduces:
-            jip.status.reduce_progress = sum(
-                1.0 if t.is_complete() else max((a.progress for a in t.attempts.values()),
-                                                default=0.0) for t in jip.reduces) / len(jip.reduces)
+            jip.status.reduce_progress = jip.reduces_done / len(jip.reduces)
 
     def _check_job_done(self, jip: JobInProgress):
         if all(t.is_complete() for t in jip.maps) and all(t.is_complete() for t in jip.reduces):
@@ -672,13 +732,19 @@ class JobTracker:
         self.attempt_index[a.aid] = a
         tr.running.add(a.aid)
         if tip.is_map:
+            if not jip.t_first_map:
+                jip.t_first_map = a.start
             if on_gpu:
                 tr.running_gpu[device] = tr.running_gpu.get(device, 0) + 1
+                jip.running_gpu += 1
             else:
                 tr.running_cpu += 1
+                jip.running_cpu += 1
             self.cost_model.task_started(jip.signature, a.aid, on_gpu, a.start)
             jip.counters.incr(C.JOB_GROUP, C.TOTAL_LAUNCHED_MAPS)
         else:
+            if not jip.t_first_reduce:
+                jip.t_first_reduce = a.start
             tr.running_reduce += 1
             jip.counters.incr(C.JOB_GROUP, C.TOTAL_LAUNCHED_REDUCES)
         spec = P.TaskSpec(attempt_id=a.aid, job_id=str(jip.job_id), is_map=tip.is_map,
@@ -718,7 +784,7 @@ class JobTracker:
         return {"state": st.state, "map_progress": st.map_progress,
                 "reduce_progress": st.reduce_progress, "start_time": st.start_time,
                 "finish_time": st.finish_time, "failure_info": st.failure_info,
-                "counters": jip.counters.to_dict()}
+                "counters": jip.fold_counters().to_dict()}
 
     def rpc_kill_job(self, jid):
         self.kill_job(jid)

@@ -15,7 +15,7 @@ whenever the wire format changes (the fork did not: B9).
 """
 from __future__ import annotations
 
-from dataclasses import asdict, dataclass, field
+from dataclasses import dataclass, field
 
 PROTOCOL_VERSION = 2
 
@@ -52,7 +52,7 @@ class TaskStatus:
         return not self.run_on_gpu
 
     def to_dict(self):
-        return asdict(self)
+        return dict(self.__dict__)   # shallow: fields are plain values / dicts
 
     @classmethod
     def from_dict(cls, d):
@@ -92,7 +92,7 @@ class TaskTrackerStatus:
         return sum(g["max_slots"] for g in self.gpus)
 
     def to_dict(self):
-        return asdict(self)
+        return dict(self.__dict__)   # shallow: fields are plain values / dicts
 
     @classmethod
     def from_dict(cls, d):
@@ -117,7 +117,7 @@ class TaskSpec:
     conf: dict | None = None                      # job conf (sent once per tracker per job)
 
     def to_dict(self):
-        return asdict(self)
+        return dict(self.__dict__)   # shallow: fields are plain values / dicts
 
     @classmethod
     def from_dict(cls, d):

@@ -185,7 +185,7 @@ class TaskTracker:
             self._changed.add(aid)
         self._news.set()
 
-    def _finish(self, run: _Running, state, diag="", output=None, device_time=0.0):
+    def _finish(self, run: _Running, state, diag="", output=None, device_time=0.0, wake=True):
         st = run.status
         st.state = state
         st.finish_time = time.time()
@@ -198,6 +198,12 @@ class TaskTracker:
         st.progress = 1.0 if state == P.SUCCEEDED else st.progress
         self.tasks_done += 1
         self._mark(st.attempt_id)
+        if wake:
+            self.notify_jobtracker()
+
+    def notify_jobtracker(self):
+        """Cut our long-polling heartbeat short so finished tasks are reported now."""
+        self._news.set()
         try:
             self.jt.wakeup(self.name)
         except Exception:  # noqa: BLE001

@@ -251,25 +251,41 @@ class KMeansSplitJob(SplitJob):
         return out
 
     # -- map ------------------------------------------------------------------------
-    def map_gpu(self, ctx, points):
+    @staticmethod
+    def _scratch(ctx, n, k):
+        """Per-(tracker, stream) label + combiner workspace, reused across tasks
+        (tasks on one stream are ordered, so reuse is race-free)."""
         from ..ops import kmeans as km
-        img = STORE.image(self.cin, ctx.device)
-        sums, counts = km.new_partials(self.k, img.dp, ctx.device)
-        ws = ctx.job.scratch.get(("ws", id(ctx.stream)))
-        n = points.shape[0]
-        need = km.workspace_bytes(n, self.k)
+        key = ("kmeans-scratch", str(ctx.device), id(ctx.stream))
+        store = ctx.tracker.__dict__.setdefault("_scratch", {})
+        ws, labels = store.get(key, (None, None))
+        need = km.workspace_bytes(n, k)
         if ws is None or ws.numel() < need:
             ws = torch.empty(max(need, 1 << 20), dtype=torch.uint8, device=ctx.device)
-            ctx.job.scratch[("ws", id(ctx.stream))] = ws
-        labels = ctx.job.scratch.get(("lab", id(ctx.stream)))
         if labels is None or labels.numel() < n:
             labels = torch.empty(max(n, 1), dtype=torch.int32, device=ctx.device)
-            ctx.job.scratch[("lab", id(ctx.stream))] = labels
-        km.assign(points, img, labels=labels[:n], stream=ctx.stream)
-        km.accumulate(points, labels[:n], self.k, sums, counts, fx_shift=self.fx_shift,
-                      stream=ctx.stream, workspace=ws)
-        ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, n)
-        return sums, counts
+        store[key] = (ws, labels)
+        return ws, labels
+
+    def map_gpu(self, ctx, points):
+        return self.map_gpu_batch([ctx], [points])[0]
+
+    def map_gpu_batch(self, ctxs, datas):
+        """All queued map tasks of this job on one stream, launched by one
+        native call (hbmr_kmeans_map_batch); each task keeps its own slab."""
+        from ..ops import kmeans as km
+        ctx = ctxs[0]
+        img = STORE.image(self.cin, ctx.device)
+        B = len(datas)
+        nmax = max(d.shape[0] for d in datas)
+        ws, labels = self._scratch(ctx, nmax, self.k)
+        sums = torch.empty(B, self.k, img.dp, dtype=torch.int64, device=ctx.device)
+        counts = torch.empty(B, self.k, dtype=torch.int64, device=ctx.device)
+        km.map_batch_gpu(datas, img, sums, counts, labels, ws, stream=ctx.stream,
+                         zero_outputs=True)
+        for c, d in zip(ctxs, datas):
+            c.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, d.shape[0])
+        return [(sums[i], counts[i]) for i in range(B)]
 
     def map_cpu(self, ctx, points):
         from ..ops import kmeans as km
@@ -287,9 +303,16 @@ class KMeansSplitJob(SplitJob):
         from ..ops import kmeans as km
         dev = ctx.device if ctx.device is not None else torch.device("cpu")
         dp = km.padded_dim(self.d) if dev.type == "cuda" else self.d
-        sums = torch.zeros(self.k, dp, dtype=torch.int64, device=dev)
-        counts = torch.zeros(self.k, dtype=torch.int64, device=dev)
-        for s, c in outputs:
+        same = [(s, c) for s, c in outputs if s.device == dev and s.shape[1] == dp]
+        other = [(s, c) for s, c in outputs if not (s.device == dev and s.shape[1] == dp)]
+        if same:
+            # one reduction kernel over all task slabs instead of one add per task
+            sums = torch.stack([s for s, _ in same]).sum(0)
+            counts = torch.stack([c for _, c in same]).sum(0)
+        else:
+            sums = torch.zeros(self.k, dp, dtype=torch.int64, device=dev)
+            counts = torch.zeros(self.k, dtype=torch.int64, device=dev)
+        for s, c in other:  # e.g. CPU-slot partials on a GPU tracker ([k, d], host)
             sums[:, :s.shape[1]] += s.to(dev, non_blocking=True)
             counts += c.to(dev, non_blocking=True)
         return sums, counts
@@ -414,6 +437,9 @@ class KMeansDriver:
         if not rj.isSuccessful():
             raise RuntimeError(f"K-Means iteration {i} failed: {rj.getFailureInfo()}")
         res = dict(self.result_of(rj) or {})
+        jip = getattr(rj._impl, "jip", None)
+        if jip is not None:
+            res["timeline"] = jip.timeline()
         res.update(iteration=i, seconds=time.time() - t0, job=str(rj.getID()),
                    counters=rj.getCounters())
         self.history.append(res)

@@ -146,6 +146,34 @@ def accumulate(points: torch.Tensor, labels: torch.Tensor, k: int, sums: torch.T
     _lib.check(rc, "hbmr_kmeans_accum_bf16")
 
 
+def map_batch_gpu(splits: list, img: CentroidImage, sums: torch.Tensor, counts: torch.Tensor,
+                  labels: torch.Tensor, workspace: torch.Tensor, stream=None,
+                  zero_outputs: bool = True) -> None:
+    """A batch of map tasks in one native call: splits[t] (bf16 [n_t, dp]) →
+    sums[t] ([B, k, dp] int64), counts[t] ([B, k] int64)."""
+    B = len(splits)
+    if B == 0:
+        return
+    for s in splits:
+        if s.dtype != torch.bfloat16 or s.shape[1] != img.dp or not s.is_contiguous():
+            raise ValueError("splits must be contiguous bf16 [n, dp]")
+    if sums.shape != (B, img.k, img.dp) or counts.shape != (B, img.k):
+        raise ValueError("batch output shape mismatch")
+    nmax = max(s.shape[0] for s in splits)
+    if labels.numel() < nmax:
+        raise ValueError("labels scratch too small")
+    lib = _lib.load()
+    if workspace.numel() < workspace_bytes(nmax, img.k):
+        raise ValueError("workspace too small")
+    ptrs = (ctypes.c_void_p * B)(*[s.data_ptr() for s in splits])
+    ns = (ctypes.c_long * B)(*[s.shape[0] for s in splits])
+    rc = lib.hbmr_kmeans_map_batch(B, ptrs, ns, img.dp, _ptr(img.cbf), _ptr(img.chalf), img.k_pad,
+                                   img.k, _ptr(labels), _ptr(workspace), workspace.numel(),
+                                   _ptr(sums), _ptr(counts), img.fx_shift, int(zero_outputs),
+                                   _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_kmeans_map_batch")
+
+
 def map_split_gpu(points, img: CentroidImage, sums, counts, labels=None, stream=None):
     """One GPU K-Means map task over an HBM-resident split: assign + combine."""
     labels = assign(points, img, labels=labels, stream=stream)

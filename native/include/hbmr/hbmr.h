@@ -27,6 +27,11 @@ int hbmr_kmeans_accum_bf16(const void* X, long n, int dp, const int32_t* labels,
 int hbmr_kmeans_update(const long long* sums, const long long* counts, int fx_shift, int k, int d,
                        int dp, int k_pad, float* cen, void* cbf, float* chalf, float* shift2,
                        hipStream_t st);
+// a batch of map tasks (one per split): assign + combine into sums[t] / counts[t]
+int hbmr_kmeans_map_batch(int ntasks, const void* const* X, const long* n, int dp,
+                          const void* C, const float* chalf, int k_pad, int k, int32_t* labels,
+                          void* ws, long ws_bytes, long long* sums, long long* counts,
+                          int fx_shift, int zero_outputs, hipStream_t st);
 #endif
 int hbmr_kmeans_padded_k(int k);
 long hbmr_kmeans_accum_workspace_bytes(long n, int k);

@@ -777,4 +777,27 @@ int hbmr_kmeans_update(const long long* sums, const long long* counts, int fx_sh
 
 int hbmr_kmeans_padded_k(int k) { return ((k + kCK - 1) / kCK) * kCK; }
 
+// A batch of K-Means map tasks (one per split) launched from C++ in one call:
+// assign + combine per split into its own output slab sums[t] / counts[t]
+// (zeroed here).  Removes the per-task host overhead of the runtime's launch
+// path; each task still gets its own map output (attempt isolation).
+int hbmr_kmeans_map_batch(int ntasks, const void* const* X, const long* n, int dp,
+                          const void* C, const float* chalf, int k_pad, int k, int32_t* labels,
+                          void* ws, long ws_bytes, long long* sums, long long* counts,
+                          int fx_shift, int zero_outputs, hipStream_t st) {
+  if (ntasks <= 0) return 0;
+  if (zero_outputs) {
+    HBMR_RETURN_IF_ERROR(hipMemsetAsync(sums, 0, (size_t)ntasks * k * dp * 8, st));
+    HBMR_RETURN_IF_ERROR(hipMemsetAsync(counts, 0, (size_t)ntasks * k * 8, st));
+  }
+  for (int t = 0; t < ntasks; ++t) {
+    int rc = hbmr_kmeans_assign_bf16(X[t], n[t], dp, C, chalf, k_pad, labels, nullptr, st);
+    if (rc) return rc;
+    rc = hbmr_kmeans_accum_bf16(X[t], n[t], dp, labels, k, sums + (size_t)t * k * dp,
+                                counts + (size_t)t * k, fx_shift, ws, ws_bytes, 0, st);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 }  // extern "C"
