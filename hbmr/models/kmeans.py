@@ -252,18 +252,18 @@ class KMeansSplitJob(SplitJob):
 
     # -- map ------------------------------------------------------------------------
     @staticmethod
-    def _scratch(ctx, n, k):
+    def _scratch(ctx, ns, k):
         """Per-(tracker, stream) label + combiner workspace, reused across tasks
         (tasks on one stream are ordered, so reuse is race-free)."""
         from ..ops import kmeans as km
         key = ("kmeans-scratch", str(ctx.device), id(ctx.stream))
         store = ctx.tracker.__dict__.setdefault("_scratch", {})
         ws, labels = store.get(key, (None, None))
-        need = km.workspace_bytes(n, k)
-        if ws is None or ws.numel() < need:
-            ws = torch.empty(max(need, 1 << 20), dtype=torch.uint8, device=ctx.device)
-        if labels is None or labels.numel() < n:
-            labels = torch.empty(max(n, 1), dtype=torch.int32, device=ctx.device)
+        need_lab, need_ws = km.batch_scratch_sizes(ns, k)
+        if ws is None or ws.numel() < need_ws:
+            ws = torch.empty(max(need_ws, 1 << 20), dtype=torch.uint8, device=ctx.device)
+        if labels is None or labels.numel() < need_lab:
+            labels = torch.empty(max(need_lab, 1), dtype=torch.int32, device=ctx.device)
         store[key] = (ws, labels)
         return ws, labels
 
@@ -277,8 +277,7 @@ class KMeansSplitJob(SplitJob):
         ctx = ctxs[0]
         img = STORE.image(self.cin, ctx.device)
         B = len(datas)
-        nmax = max(d.shape[0] for d in datas)
-        ws, labels = self._scratch(ctx, nmax, self.k)
+        ws, labels = self._scratch(ctx, [d.shape[0] for d in datas], self.k)
         sums = torch.empty(B, self.k, img.dp, dtype=torch.int64, device=ctx.device)
         counts = torch.empty(B, self.k, dtype=torch.int64, device=ctx.device)
         km.map_batch_gpu(datas, img, sums, counts, labels, ws, stream=ctx.stream,

@@ -31,6 +31,7 @@ _SIGS = {
     "hbmr_kmeans_accum_bf16": (c_int, [c_void_p, c_long, c_int, c_void_p, c_int, c_void_p,
                                        c_void_p, c_int, c_void_p, c_long, c_int, c_void_p]),
     "hbmr_kmeans_accum_workspace_bytes": (c_long, [c_long, c_int]),
+    "hbmr_kmeans_batch_workspace_bytes": (c_long, [c_long, c_int, c_int]),
     "hbmr_kmeans_map_batch": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
                                       c_int, c_void_p, c_void_p, c_long, c_void_p, c_void_p,
                                       c_int, c_int, c_void_p]),

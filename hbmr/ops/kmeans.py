@@ -109,6 +109,16 @@ def workspace_bytes(n: int, k: int) -> int:
     return int(_lib.load().hbmr_kmeans_accum_workspace_bytes(n, k))
 
 
+def batch_scratch_sizes(ns: list, k: int) -> tuple[int, int]:
+    """(label entries, workspace bytes) a map batch over splits of sizes ``ns`` needs
+    (grouped kernels keep every split's labels/permutation side by side)."""
+    lib = _lib.load()
+    total = int(sum(ns))
+    ws = max(int(lib.hbmr_kmeans_batch_workspace_bytes(total, len(ns), k)),
+             int(lib.hbmr_kmeans_accum_workspace_bytes(max(ns), k)))
+    return total, ws
+
+
 def accum_workspace(n: int, k: int, device) -> torch.Tensor:
     """Per-(device, stream-free) scratch for the sorted combiner, grown on demand.
 
@@ -159,11 +169,11 @@ def map_batch_gpu(splits: list, img: CentroidImage, sums: torch.Tensor, counts: 
             raise ValueError("splits must be contiguous bf16 [n, dp]")
     if sums.shape != (B, img.k, img.dp) or counts.shape != (B, img.k):
         raise ValueError("batch output shape mismatch")
-    nmax = max(s.shape[0] for s in splits)
-    if labels.numel() < nmax:
+    need_lab, need_ws = batch_scratch_sizes([s.shape[0] for s in splits], img.k)
+    if labels.numel() < need_lab:
         raise ValueError("labels scratch too small")
     lib = _lib.load()
-    if workspace.numel() < workspace_bytes(nmax, img.k):
+    if workspace.numel() < need_ws:
         raise ValueError("workspace too small")
     ptrs = (ctypes.c_void_p * B)(*[s.data_ptr() for s in splits])
     ns = (ctypes.c_long * B)(*[s.shape[0] for s in splits])

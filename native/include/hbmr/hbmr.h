@@ -35,6 +35,7 @@ int hbmr_kmeans_map_batch(int ntasks, const void* const* X, const long* n, int d
 #endif
 int hbmr_kmeans_padded_k(int k);
 long hbmr_kmeans_accum_workspace_bytes(long n, int k);
+long hbmr_kmeans_batch_workspace_bytes(long total_n, int ntasks, int k);
 
 // ---- CPU kernels (native/cpu) ------------------------------------------------
 int hbmr_kmeans_map_cpu_f32(const float* X, long n, int d, const float* C, int k,

@@ -26,6 +26,7 @@
 #include "common.h"
 #include "../include/hbmr/hbmr.h"
 #include <algorithm>
+#include <cstring>
 
 namespace {
 
@@ -74,21 +75,22 @@ __device__ __forceinline__ void stage_chunk(char* buf, const __bf16* __restrict_
   }
 }
 
+// One workgroup's tile of points [blk*PTS, (blk+1)*PTS) of one split.
 template <int D>
-__global__ __launch_bounds__(kThreads, 2) void kmeans_assign_kernel(
-    const __bf16* __restrict__ X, long n, const __bf16* __restrict__ C,
-    const float* __restrict__ chalf, int nchunks, int32_t* __restrict__ labels,
-    float* __restrict__ scores) {
+__device__ __forceinline__ void assign_tile(const __bf16* __restrict__ X, long n,
+                                            const __bf16* __restrict__ C,
+                                            const float* __restrict__ chalf, int nchunks,
+                                            int32_t* __restrict__ labels,
+                                            float* __restrict__ scores,
+                                            uint32_t* __restrict__ hist, long blk, char* smem) {
   using Cfg = AssignCfg<D>;
   constexpr int KS = Cfg::KS, PB = Cfg::PB;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid / HBMR_WAVE);
   const int lane = tid & (HBMR_WAVE - 1);
   const int h = lane >> 5;   // lane half: selects k-offset 8h in A/B fragments
   const int col = lane & 31;
-  const long blk = hbmr_xcd_remap(blockIdx.x, gridDim.x);
   const long p0 = blk * Cfg::PTS + (long)wave * PB * 32;
 
   // Kick off chunk 0 first so it overlaps the point-fragment loads.
@@ -196,8 +198,53 @@ __global__ __launch_bounds__(kThreads, 2) void kmeans_assign_kernel(
     if (h == 0 && p < n) {
       labels[p] = cluster;
       if (scores) scores[p] = __uint_as_float(__float_as_uint(bv) & 0xffffff00u);
+      if (hist) atomicAdd(hist + cluster, 1u);  // fused histogram for the sorted combiner
     }
   }
+}
+
+template <int D>
+__global__ __launch_bounds__(kThreads, 2) void kmeans_assign_kernel(
+    const __bf16* __restrict__ X, long n, const __bf16* __restrict__ C,
+    const float* __restrict__ chalf, int nchunks, int32_t* __restrict__ labels,
+    float* __restrict__ scores) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  assign_tile<D>(X, n, C, chalf, nchunks, labels, scores, nullptr,
+                 hbmr_xcd_remap(blockIdx.x, gridDim.x), smem);
+}
+
+// ---------------------------------------------------------------------------
+// Grouped (batched) map kernels: one launch covers every split of a batch of
+// map tasks.  Each workgroup finds its split in a small table passed by value.
+constexpr int kMaxGroup = 64;
+
+struct SplitTable {
+  int nsplit;
+  int k;
+  const __bf16* X[kMaxGroup];
+  long n[kMaxGroup];
+  long off[kMaxGroup];        // offset of the split's points in the batch arrays
+  long blk[kMaxGroup + 1];    // prefix sum of workgroups per split (per kernel)
+};
+
+__device__ __forceinline__ int find_split(const SplitTable& t, long b) {
+  int lo = 0, hi = t.nsplit;  // t.blk[lo] <= b < t.blk[hi]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (t.blk[mid] <= b) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+template <int D>
+__global__ __launch_bounds__(kThreads, 2) void kmeans_assign_grouped_kernel(
+    const SplitTable tbl, const __bf16* __restrict__ C, const float* __restrict__ chalf,
+    int nchunks, int32_t* __restrict__ labels, uint32_t* __restrict__ hist) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const long b = hbmr_xcd_remap(blockIdx.x, gridDim.x);
+  const int s = __builtin_amdgcn_readfirstlane(find_split(tbl, b));
+  assign_tile<D>(tbl.X[s], tbl.n[s], C, chalf, nchunks, labels + tbl.off[s], nullptr,
+                 hist + (size_t)s * tbl.k, b - tbl.blk[s], smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -555,6 +602,168 @@ __global__ __launch_bounds__(256) void kmeans_segsum_kernel(
   }
 }
 
+// ---- grouped sorted combiner ------------------------------------------------------
+// hist[s][k] comes fused from the grouped assign.  Every scatter workgroup
+// rebuilds the exclusive scan of its split's histogram in LDS (k ≤ 8192: a few
+// µs) so no separate scan launch or grid-wide sync is needed; the workgroup
+// with local index 0 of each split also publishes offsets[s] (for the segsum
+// launch) and adds the histogram to that task's counts.
+__device__ void block_exclusive_scan(const uint32_t* __restrict__ in, int k, uint32_t* out,
+                                     uint32_t* total) {
+  __shared__ uint32_t s_part[256];
+  const int t = threadIdx.x;
+  const int per = (k + 255) / 256;
+  const int lo = min(k, t * per), hi = min(k, lo + per);
+  uint32_t s = 0;
+  for (int i = lo; i < hi; ++i) s += in[i];
+  // wave-level inclusive scan, then across the 4 waves
+  const int lane = t & 63, w = t >> 6;
+  uint32_t v = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(v, o);
+    if (lane >= o) v += u;
+  }
+  if (lane == 63) s_part[w] = v;
+  __syncthreads();
+  uint32_t wbase = 0;
+  for (int i = 0; i < w; ++i) wbase += s_part[i];
+  uint32_t run = wbase + v - s;
+  for (int i = lo; i < hi; ++i) {
+    out[i] = run;
+    run += in[i];
+  }
+  if (t == 255) *total = wbase + v;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void kmeans_scatter_grouped_kernel(
+    const SplitTable tbl, const int32_t* __restrict__ labels, const uint32_t* __restrict__ hist,
+    uint32_t* __restrict__ cursor, uint32_t* __restrict__ offsets, uint32_t* __restrict__ perm,
+    long long* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];  // off[k] | cnt[k] | base[k]
+  const int k = tbl.k;
+  uint32_t* s_off = s_h;
+  uint32_t* s_cnt = s_h + k;
+  uint32_t* s_base = s_h + 2 * k;
+  __shared__ uint32_t s_total;
+  const int s = __builtin_amdgcn_readfirstlane(find_split(tbl, blockIdx.x));
+  const long local = blockIdx.x - tbl.blk[s];
+  const long n = tbl.n[s];
+  const uint32_t* hs = hist + (size_t)s * k;
+  const int t = threadIdx.x;
+  for (int i = t; i < k; i += 256) s_cnt[i] = 0u;
+  block_exclusive_scan(hs, k, s_off, &s_total);
+  if (local == 0) {
+    uint32_t* os = offsets + (size_t)s * (k + 1);
+    for (int i = t; i < k; i += 256) {
+      os[i] = s_off[i];
+      counts[(size_t)s * k + i] += hs[i];
+    }
+    if (t == 0) os[k] = s_total;
+  }
+  constexpr int PER = kScatterPts / 256;
+  const int32_t* lab_s = labels + tbl.off[s];
+  const long p0 = local * kScatterPts + (long)t * PER;
+  int lab[PER];
+  uint32_t rank[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) lab[j] = (p0 + j < n) ? lab_s[p0 + j] : -1;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) rank[j] = lab[j] >= 0 ? atomicAdd(s_cnt + lab[j], 1u) : 0u;
+  __syncthreads();
+  uint32_t* cur_s = cursor + (size_t)s * k;
+  for (int i = t; i < k; i += 256) {
+    const uint32_t c = s_cnt[i];
+    s_base[i] = c ? s_off[i] + atomicAdd(cur_s + i, c) : 0u;
+  }
+  __syncthreads();
+  uint32_t* perm_s = perm + tbl.off[s];
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    if (lab[j] >= 0) perm_s[s_base[lab[j]] + rank[j]] = (uint32_t)(p0 + j);
+}
+
+template <int D, int U>
+__global__ __launch_bounds__(256) void kmeans_segsum_grouped_kernel(
+    const SplitTable tbl, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ offsets,
+    long chunk, long long* __restrict__ sums, float scale) {
+  constexpr int TPP = D / 8;
+  constexpr int GPW = HBMR_WAVE / TPP;
+  const int k = tbl.k;
+  const int lane = threadIdx.x & 63;
+  const int grp = lane / TPP, sub = lane % TPP;
+  const long wid = (long)blockIdx.x * (blockDim.x / HBMR_WAVE) + threadIdx.x / HBMR_WAVE;
+  // tbl.blk holds the prefix sum of WAVES (chunks) per split for this launch
+  if (wid >= tbl.blk[tbl.nsplit]) return;
+  const int sidx = find_split(tbl, wid);
+  const long n = tbl.n[sidx];
+  const long s0 = (wid - tbl.blk[sidx]) * chunk;
+  const long e = min(n, s0 + chunk);
+  const __bf16* X = tbl.X[sidx];
+  const uint32_t* pm = perm + tbl.off[sidx];
+  const uint32_t* of = offsets + (size_t)sidx * (k + 1);
+  u64* out = reinterpret_cast<u64*>(sums) + (size_t)sidx * k * D;
+  int lo = 0, hi = k;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if ((long)of[mid] <= s0) lo = mid; else hi = mid;
+  }
+  int cur = lo;
+  long bound = of[cur + 1];
+  long long acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0;
+  auto flush = [&]() {
+    u64* dst = out + (size_t)cur * D + sub * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (acc[j]) atomicAdd(dst + j, (u64)acc[j]);
+      acc[j] = 0;
+    }
+  };
+  for (long base = s0 + grp; base < e; base += (long)U * GPW) {
+    uint32_t idx[U];
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long p = base + (long)u * GPW;
+      idx[u] = p < e ? pm[p] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long p = base + (long)u * GPW;
+      if (p < e) v[u] = reinterpret_cast<const uint4*>(X + (size_t)idx[u] * D)[sub];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long p = base + (long)u * GPW;
+      if (p < e) {
+        while (p >= bound) {
+          flush();
+          ++cur;
+          bound = of[cur + 1];
+        }
+        float f[8];
+        hbmr_unpack8(v[u], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += __float2ll_rn(f[j] * scale);
+      }
+    }
+  }
+  const int c0 = __shfl(cur, 0);
+  if (__all(cur == c0)) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#pragma unroll
+      for (int off = TPP; off < HBMR_WAVE; off <<= 1) acc[j] += __shfl_xor(acc[j], off);
+    }
+    if (grp == 0) flush();
+  } else {
+    flush();
+  }
+}
+
 // Reduce side + next-iteration prep.  One workgroup per cluster.
 // sums are fixed-point int64 [k, dp], counts int64 [k].
 __global__ __launch_bounds__(128) void kmeans_update_kernel(
@@ -675,6 +884,7 @@ bool set_lds_limits() {
     HBMR_LDS_OPTIN((kmeans_accum_chunked_kernel<64, 8>));
     HBMR_LDS_OPTIN((kmeans_accum_chunked_kernel<128, 8>));
     HBMR_LDS_OPTIN((kmeans_accum_chunked_kernel<256, 8>));
+    HBMR_LDS_OPTIN(kmeans_scatter_grouped_kernel);
 #undef HBMR_LDS_OPTIN
     done = true;
   }
@@ -781,6 +991,101 @@ int hbmr_kmeans_padded_k(int k) { return ((k + kCK - 1) / kCK) * kCK; }
 // assign + combine per split into its own output slab sums[t] / counts[t]
 // (zeroed here).  Removes the per-task host overhead of the runtime's launch
 // path; each task still gets its own map output (attempt isolation).
+long hbmr_kmeans_batch_workspace_bytes(long total_n, int ntasks, int k) {
+  return (long)(ws_align((size_t)ntasks * k * 4) * 2 + ws_align((size_t)ntasks * (k + 1) * 4) +
+                ws_align((size_t)total_n * 4));
+}
+
+// Grouped path: 1 memset + 3 launches for the whole batch (assign+hist,
+// scan+scatter, segmented sum).  labels must hold Σ n[t] entries.
+static int map_batch_grouped(int ntasks, const void* const* X, const long* n, int dp,
+                             const void* C, const float* chalf, int k_pad, int k,
+                             int32_t* labels, void* ws, long long* sums, long long* counts,
+                             int fx_shift, hipStream_t st, int cus) {
+  SplitTable t;
+  memset(&t, 0, sizeof(t));
+  t.nsplit = ntasks;
+  t.k = k;
+  long total = 0;
+  for (int i = 0; i < ntasks; ++i) {
+    t.X[i] = reinterpret_cast<const __bf16*>(X[i]);
+    t.n[i] = n[i];
+    t.off[i] = total;
+    total += n[i];
+  }
+  char* w = reinterpret_cast<char*>(ws);
+  const size_t hb = ws_align((size_t)ntasks * k * 4);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(w);
+  uint32_t* cursor = reinterpret_cast<uint32_t*>(w + hb);
+  uint32_t* offsets = reinterpret_cast<uint32_t*>(w + 2 * hb);
+  uint32_t* perm = reinterpret_cast<uint32_t*>(w + 2 * hb + ws_align((size_t)ntasks * (k + 1) * 4));
+  HBMR_RETURN_IF_ERROR(hipMemsetAsync(hist, 0, 2 * hb, st));  // hist + cursor
+  // 1. assign (+ fused histogram)
+  long nb = 0;
+  int pts = 0;
+  switch (dp) {
+    case 64: pts = AssignCfg<64>::PTS; break;
+    case 128: pts = AssignCfg<128>::PTS; break;
+    case 256: pts = AssignCfg<256>::PTS; break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  for (int i = 0; i < ntasks; ++i) {
+    t.blk[i] = nb;
+    nb += (n[i] + pts - 1) / pts;
+  }
+  t.blk[ntasks] = nb;
+  if (nb > 0) {
+    switch (dp) {
+#define HBMR_GA(DD)                                                                          \
+  case DD:                                                                                   \
+    hipLaunchKernelGGL(kmeans_assign_grouped_kernel<DD>, dim3((unsigned)nb), dim3(kThreads),  \
+                       AssignCfg<DD>::LDS_BYTES, st, t, reinterpret_cast<const __bf16*>(C),  \
+                       chalf, k_pad / kCK, labels, hist);                                    \
+    break;
+      HBMR_GA(64)
+      HBMR_GA(128)
+      HBMR_GA(256)
+#undef HBMR_GA
+    }
+    HBMR_RETURN_IF_ERROR(hipGetLastError());
+  }
+  // 2. scan + scatter (+ counts, offsets)
+  nb = 0;
+  for (int i = 0; i < ntasks; ++i) {
+    t.blk[i] = nb;
+    nb += std::max<long>(1, (n[i] + kScatterPts - 1) / kScatterPts);
+  }
+  t.blk[ntasks] = nb;
+  hipLaunchKernelGGL(kmeans_scatter_grouped_kernel, dim3((unsigned)nb), dim3(256),
+                     (size_t)3 * k * 4, st, t, labels, hist, cursor, offsets, perm, counts);
+  HBMR_RETURN_IF_ERROR(hipGetLastError());
+  // 3. segmented row sums: chunks sized so the batch yields ≥ 16 waves per CU
+  long chunk = (total + (long)cus * 16 - 1) / ((long)cus * 16);
+  chunk = std::min<long>(4096, std::max<long>(128, ((chunk + 63) / 64) * 64));
+  long nw = 0;
+  for (int i = 0; i < ntasks; ++i) {
+    t.blk[i] = nw;
+    nw += (n[i] + chunk - 1) / chunk;
+  }
+  t.blk[ntasks] = nw;
+  const float scale = ldexpf(1.0f, fx_shift);
+  if (nw > 0) {
+    const long blocks = (nw + 3) / 4;
+    switch (dp) {
+#define HBMR_GS(DD)                                                                         \
+  case DD:                                                                                  \
+    hipLaunchKernelGGL((kmeans_segsum_grouped_kernel<DD, 8>), dim3((unsigned)blocks),       \
+                       dim3(256), 0, st, t, perm, offsets, chunk, sums, scale);             \
+    break;
+      HBMR_GS(64)
+      HBMR_GS(128)
+      HBMR_GS(256)
+#undef HBMR_GS
+    }
+  }
+  return (int)hipGetLastError();
+}
+
 int hbmr_kmeans_map_batch(int ntasks, const void* const* X, const long* n, int dp,
                           const void* C, const float* chalf, int k_pad, int k, int32_t* labels,
                           void* ws, long ws_bytes, long long* sums, long long* counts,
@@ -789,6 +1094,15 @@ int hbmr_kmeans_map_batch(int ntasks, const void* const* X, const long* n, int d
   if (zero_outputs) {
     HBMR_RETURN_IF_ERROR(hipMemsetAsync(sums, 0, (size_t)ntasks * k * dp * 8, st));
     HBMR_RETURN_IF_ERROR(hipMemsetAsync(counts, 0, (size_t)ntasks * k * 8, st));
+  }
+  long total = 0;
+  for (int t = 0; t < ntasks; ++t) total += n[t];
+  const bool small = ((size_t)k * AccCfg<128>::RS * 8 + (size_t)k * 4) <= 76 * 1024 && dp <= 128;
+  if (!small && ntasks <= kMaxGroup && k <= 8192 &&
+      ws_bytes >= hbmr_kmeans_batch_workspace_bytes(total, ntasks, k)) {
+    set_lds_limits();
+    return map_batch_grouped(ntasks, X, n, dp, C, chalf, k_pad, k, labels, ws, sums, counts,
+                             fx_shift, st, cu_count());
   }
   for (int t = 0; t < ntasks; ++t) {
     int rc = hbmr_kmeans_assign_bf16(X[t], n[t], dp, C, chalf, k_pad, labels, nullptr, st);

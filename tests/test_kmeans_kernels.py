@@ -111,3 +111,29 @@ def test_cpu_map_matches_reference():
     assert (sums - ref_s).abs().max().item() <= 2
     assert torch.equal(counts, torch.bincount(labels.long(), minlength=k))
     assert abs(cost - dist.min(1).values.sum().item()) / dist.min(1).values.sum().item() < 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,dp,sizes", [(1024, 128, [5000, 1, 70000, 4096, 12345]),
+                                        (64, 128, [3000, 9000]),
+                                        (300, 64, [777, 20000, 5])])
+def test_map_batch_matches_per_split(k, dp, sizes):
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(3)
+    splits = [torch.randn(n, dp, generator=g).to(dev, torch.bfloat16) for n in sizes]
+    img = km.CentroidImage(torch.randn(k, dp, generator=g).to(dev), dev)
+    B = len(splits)
+    sums = torch.full((B, k, dp), 7, dtype=torch.int64, device=dev)   # poisoned: must be zeroed
+    counts = torch.full((B, k), 7, dtype=torch.int64, device=dev)
+    nlab, nws = km.batch_scratch_sizes(sizes, k)
+    labels = torch.empty(nlab, dtype=torch.int32, device=dev)
+    ws = torch.empty(nws, dtype=torch.uint8, device=dev)
+    km.map_batch_gpu(splits, img, sums, counts, labels, ws)
+    torch.cuda.synchronize()
+    for t, x in enumerate(splits):
+        lab = km.assign(x, img)
+        fx = torch.round(x.double() * (1 << km.FX_SHIFT)).long()
+        ref_s = torch.zeros(k, dp, dtype=torch.int64, device=dev).index_add_(0, lab.long(), fx)
+        ref_c = torch.bincount(lab.long(), minlength=k)
+        assert torch.equal(counts[t], ref_c), t
+        assert torch.equal(sums[t], ref_s), t
