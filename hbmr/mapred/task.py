@@ -384,7 +384,13 @@ class MapTask(Task):
             collector = _DirectCollector(outfmt.getRecordWriter(None, job, name, rep), rep)
         else:
             collector = MapOutputBuffer(self, job, rep, os.path.join(local_dir, "output"))
-        runner_cls = job.get_map_runner_class()
+        # the fork's GPU branch (MapTask.java:432-438): a GPU attempt runs the
+        # job's GPU map runner, told its device
+        if self.run_on_gpu:
+            job.set_int("hbmr.task.gpu.device", self.gpu_device_id)
+            runner_cls = job.get_gpu_map_runner_class()
+        else:
+            runner_cls = job.get_map_runner_class()
         runner = new_instance(runner_cls, job)
         try:
             runner.run(_ProgressReader(reader, rep, self), collector, rep)

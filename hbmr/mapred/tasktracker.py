@@ -140,6 +140,9 @@ class TaskTracker:
         self.cpu_pool = cf.ThreadPoolExecutor(max(1, self.cpu_slots), thread_name_prefix=f"{self.name}-cpu")
         self.reduce_pool = cf.ThreadPoolExecutor(max(1, self.reduce_slots),
                                                  thread_name_prefix=f"{self.name}-red")
+        self.gpu_pipes_pool = cf.ThreadPoolExecutor(
+            max(1, len(self.gpu_devices) * max(1, self.gpu_slots_per_device)),
+            thread_name_prefix=f"{self.name}-gpupipes")
         self.gpu_runtime = None
         if self.gpu_devices:
             from ..gpu.runtime import GpuRuntime
@@ -308,7 +311,12 @@ class TaskTracker:
         with self._lock:
             self.running[spec.attempt_id] = run
         if spec.is_map and spec.run_on_gpu:
-            self.gpu_runtime.submit(run)
+            if js.split_job is None:
+                # classic job with a GPU Pipes executable: a child process per
+                # attempt, told its device (the fork's model, B1 fixed)
+                self.gpu_pipes_pool.submit(self._run_cpu_map, run)
+            else:
+                self.gpu_runtime.submit(run)
         elif spec.is_map:
             self.cpu_pool.submit(self._run_cpu_map, run)
         else:
@@ -345,6 +353,8 @@ class TaskTracker:
             split = _split_from_dict(spec.split)
             aid = TaskAttemptID.for_name(spec.attempt_id)
             task = MapTask(js.conf, aid, spec.partition, split)
+            task.setRunOnGPU(spec.run_on_gpu)
+            task.setGPUDeviceId(spec.gpu_device_id)
             task.kill_event = run.kill
             run.task = task
             path = task.run(os.path.join(self.local_dir, spec.job_id, spec.attempt_id))

@@ -1,0 +1,217 @@
+"""Pipes binary protocol, parent side.
+
+Message codes and framing are the Hadoop Pipes ones (hadoop-1.0.3/src/mapred/
+org/apache/hadoop/mapred/pipes/BinaryProtocol.java:66-85): Hadoop VInts and
+VInt-length-prefixed byte strings over a loopback TCP socket, 128 KB buffers.
+Down (parent → child): START, SET_JOB_CONF, SET_INPUT_TYPES, RUN_MAP, MAP_ITEM,
+RUN_REDUCE, REDUCE_KEY, REDUCE_VALUE, CLOSE, ABORT, AUTHENTICATION_REQ.
+Up (child → parent): OUTPUT, PARTITIONED_OUTPUT, STATUS, PROGRESS, DONE,
+REGISTER_COUNTER, INCREMENT_COUNTER, AUTHENTICATION_RESP — parsed by
+:class:`UplinkReader` on its own thread and dispatched to an OutputHandler.
+Authentication: HMAC-SHA1(job token, challenge), base64 (Application.java:197-211).
+"""
+from __future__ import annotations
+
+import base64
+import hashlib
+import hmac
+import io
+import logging
+import struct
+import threading
+
+from ..io.vint import encode_vint, read_vint
+from ..io.writable import BytesWritable, Text, Writable
+
+log = logging.getLogger("hbmr.pipes")
+
+CURRENT_PROTOCOL_VERSION = 0
+
+START, SET_JOB_CONF, SET_INPUT_TYPES, RUN_MAP, MAP_ITEM, RUN_REDUCE, REDUCE_KEY, REDUCE_VALUE, \
+    CLOSE, ABORT, AUTHENTICATION_REQ = range(11)
+OUTPUT, PARTITIONED_OUTPUT, STATUS, PROGRESS, DONE, REGISTER_COUNTER, INCREMENT_COUNTER, \
+    AUTHENTICATION_RESP = range(50, 58)
+
+BUFFER_SIZE = 128 * 1024
+
+
+def create_digest(password: bytes, msg: str) -> str:
+    return base64.b64encode(hmac.new(password, msg.encode(), hashlib.sha1).digest()).decode()
+
+
+def to_wire(obj) -> bytes:
+    """Text/BytesWritable go as their raw bytes, other Writables serialised
+    (BinaryProtocol.writeObject, BinaryProtocol.java:349-369)."""
+    if isinstance(obj, Text):
+        return obj.bytes
+    if isinstance(obj, BytesWritable):
+        return obj.bytes
+    if isinstance(obj, Writable):
+        return obj.serialize()
+    if isinstance(obj, str):
+        return obj.encode()
+    return bytes(obj)
+
+
+def from_wire(raw: bytes, cls):
+    if cls is Text:
+        return Text(raw)
+    if cls is BytesWritable:
+        return BytesWritable(raw)
+    return cls.deserialize(raw)
+
+
+class DownwardProtocol:
+    def __init__(self, sock):
+        self.sock = sock
+        self.out = sock.makefile("wb", buffering=BUFFER_SIZE)
+        self._lock = threading.Lock()
+
+    def _int(self, v):
+        self.out.write(encode_vint(int(v)))
+
+    def _bytes(self, b):
+        b = b if isinstance(b, (bytes, bytearray)) else str(b).encode()
+        self.out.write(encode_vint(len(b)))
+        self.out.write(b)
+
+    def authenticate(self, digest, challenge):
+        with self._lock:
+            self._int(AUTHENTICATION_REQ)
+            self._bytes(digest.encode())
+            self._bytes(challenge.encode())
+            self.out.flush()
+
+    def start(self):
+        with self._lock:
+            self._int(START)
+            self._int(CURRENT_PROTOCOL_VERSION)
+
+    def set_job_conf(self, conf):
+        items = list(conf) if not isinstance(conf, dict) else list(conf.items())
+        with self._lock:
+            self._int(SET_JOB_CONF)
+            self._int(2 * len(items))
+            for k, v in items:
+                self._bytes(str(k).encode())
+                self._bytes(("" if v is None else str(v)).encode())
+
+    def set_input_types(self, key_type, value_type):
+        with self._lock:
+            self._int(SET_INPUT_TYPES)
+            self._bytes(key_type.encode())
+            self._bytes(value_type.encode())
+
+    def run_map(self, split_bytes: bytes, num_reduces: int, piped_input: bool):
+        with self._lock:
+            self._int(RUN_MAP)
+            self._bytes(split_bytes)
+            self._int(num_reduces)
+            self._int(1 if piped_input else 0)
+            self.out.flush()
+
+    def map_item(self, key, value):
+        with self._lock:
+            self._int(MAP_ITEM)
+            self._bytes(to_wire(key))
+            self._bytes(to_wire(value))
+
+    def run_reduce(self, partition: int, piped_output: bool):
+        with self._lock:
+            self._int(RUN_REDUCE)
+            self._int(partition)
+            self._int(1 if piped_output else 0)
+
+    def reduce_key(self, key):
+        with self._lock:
+            self._int(REDUCE_KEY)
+            self._bytes(to_wire(key))
+
+    def reduce_value(self, value):
+        with self._lock:
+            self._int(REDUCE_VALUE)
+            self._bytes(to_wire(value))
+
+    def end_of_input(self):
+        with self._lock:
+            self._int(CLOSE)
+            self.out.flush()
+
+    def abort(self):
+        with self._lock:
+            try:
+                self._int(ABORT)
+                self.out.flush()
+            except OSError:
+                pass
+
+    def flush(self):
+        with self._lock:
+            self.out.flush()
+
+    def close(self):
+        try:
+            self.out.close()
+        except OSError:
+            pass
+
+
+class UplinkReader(threading.Thread):
+    """Reads child → parent messages and dispatches them to ``handler``."""
+
+    def __init__(self, sock, handler):
+        super().__init__(daemon=True, name="pipes-uplink")
+        self.inp = sock.makefile("rb", buffering=BUFFER_SIZE)
+        self.handler = handler
+
+    def _bytes(self):
+        n = read_vint(self.inp)
+        return self.inp.read(n) if n else b""
+
+    def run(self):
+        h = self.handler
+        try:
+            while True:
+                cmd = read_vint(self.inp)
+                if cmd == OUTPUT:
+                    k = self._bytes()
+                    v = self._bytes()
+                    h.output(k, v)
+                elif cmd == PARTITIONED_OUTPUT:
+                    part = read_vint(self.inp)
+                    k = self._bytes()
+                    v = self._bytes()
+                    h.partitioned_output(part, k, v)
+                elif cmd == STATUS:
+                    h.status(self._bytes().decode(errors="replace"))
+                elif cmd == PROGRESS:
+                    h.progress(struct.unpack(">f", self.inp.read(4))[0])
+                elif cmd == DONE:
+                    h.done()
+                    return
+                elif cmd == REGISTER_COUNTER:
+                    cid = read_vint(self.inp)
+                    grp = self._bytes().decode()
+                    name = self._bytes().decode()
+                    h.register_counter(cid, grp, name)
+                elif cmd == INCREMENT_COUNTER:
+                    cid = read_vint(self.inp)
+                    amount = read_vint(self.inp)
+                    h.increment_counter(cid, amount)
+                elif cmd == AUTHENTICATION_RESP:
+                    h.authenticate(self._bytes().decode())
+                else:
+                    raise IOError(f"Bad command code: {cmd}")
+        except EOFError:
+            h.failed(IOError("pipe child exited before DONE"))
+        except BaseException as e:  # noqa: BLE001
+            h.failed(e)
+
+
+def read_all(data: bytes):
+    """Decode a recorded downlink stream (debugging aid, cf. downlink.data tee)."""
+    b = io.BytesIO(data)
+    out = []
+    while b.tell() < len(data):
+        out.append(read_vint(b))
+    return out

@@ -330,6 +330,7 @@ class TaskContextImpl : public MapContext, public ReduceContext {
   bool nextReduceKey() {
     if (pendingKey) {
       pendingKey = false;
+      key.swap(nextKey);
       return true;
     }
     while (true) {
@@ -356,7 +357,8 @@ class TaskContextImpl : public MapContext, public ReduceContext {
       return true;
     }
     if (cmd == REDUCE_KEY) {
-      deserializeString(key, *down);
+      // the current key stays visible to the reducer until it returns
+      deserializeString(nextKey, *down);
       pendingKey = true;
       return false;
     }
@@ -473,7 +475,7 @@ class TaskContextImpl : public MapContext, public ReduceContext {
   HadoopUtils::InStream* down;
   Uplink* up;
   JobConfImpl conf;
-  string key, value, inputSplit, inputKeyClass, inputValueClass;
+  string key, nextKey, value, inputSplit, inputKeyClass, inputValueClass;
   int numReduces = 0, reducePartition = 0;
   bool pipedInput = true, pipedOutput = true;
   bool hasTask = false, isMap = true, done = false, closed = false, pendingKey = false;
