@@ -94,15 +94,28 @@ class Configuration:
 
     addResource = add_resource  # noqa: N815
 
+    _parsed: dict = {}   # path -> (mtime_ns, [(name, value, final), ...])
+
     def _load_file(self, path: Path):
-        root = ET.parse(str(path)).getroot()
-        for prop in root.iter("property"):
-            name = prop.findtext("name")
-            if not name:
-                continue
-            value = prop.findtext("value") or ""
-            final = (prop.findtext("final") or "").strip().lower() == "true"
-            self._put(name.strip(), value, final)
+        # parsed XML is cached per (path, mtime): every JobConf() re-layers the
+        # default resources, and re-parsing them cost ~1 ms per job
+        key = str(path)
+        mt = os.stat(key).st_mtime_ns
+        hit = Configuration._parsed.get(key)
+        if hit is None or hit[0] != mt:
+            props = []
+            root = ET.parse(key).getroot()
+            for prop in root.iter("property"):
+                name = prop.findtext("name")
+                if not name:
+                    continue
+                value = prop.findtext("value") or ""
+                final = (prop.findtext("final") or "").strip().lower() == "true"
+                props.append((name.strip(), value, final))
+            hit = (mt, props)
+            Configuration._parsed[key] = hit
+        for name, value, final in hit[1]:
+            self._put(name, value, final)
 
     def _put(self, name, value, final):
         name = DEPRECATED_KEYS.get(name, name)

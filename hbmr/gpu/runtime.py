@@ -23,6 +23,7 @@ import torch
 
 from ..mapred import protocol as P
 from ..mapred.task import TaskReporter
+from ..utils.trace import TRACE
 
 log = logging.getLogger("hbmr.gpu")
 
@@ -184,6 +185,8 @@ class GpuRuntime:
                     outs = [sj.map_gpu(c, d) for c, d in zip(ctxs, datas)]
                 ev1.record(slot.stream)
             slot.inflight += len(live)
+            if TRACE.on:
+                TRACE.instant("gpu.launch", n=len(live), slot=slot.index)
             slot.done_q.put((live, ev0, ev1, outs))
         except BaseException as e:  # noqa: BLE001
             for r in (live or runs):
@@ -202,6 +205,8 @@ class GpuRuntime:
             runs, ev0, ev1, outs = item
             try:
                 ev1.synchronize()
+                if TRACE.on:
+                    TRACE.instant("gpu.complete", n=len(runs), slot=slot.index)
                 # a batch completes together; its device time is shared evenly
                 dt = ev0.elapsed_time(ev1) / 1000.0 / max(1, len(runs))
                 js = runs[0].job

@@ -22,7 +22,7 @@ Subclasses implement:
 """
 from __future__ import annotations
 
-from dataclasses import asdict, dataclass, field
+from dataclasses import dataclass, field
 
 
 @dataclass
@@ -35,7 +35,9 @@ class SplitSpec:
     length: int = 0               # bytes (for split-size bookkeeping)
 
     def to_dict(self):
-        return asdict(self)
+        # shallow (dataclasses.asdict deep-copies: ~25 µs per split per job)
+        return {"index": self.index, "key": self.key, "kind": self.kind, "params": self.params,
+                "locations": self.locations, "length": self.length}
 
     @classmethod
     def from_dict(cls, d):

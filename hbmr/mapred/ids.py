@@ -16,8 +16,11 @@ class JobID:
     jt: str
     id: int
 
+    def __post_init__(self):
+        object.__setattr__(self, "_s", f"job_{self.jt}_{self.id:04d}")
+
     def __str__(self):
-        return f"job_{self.jt}_{self.id:04d}"
+        return self._s
 
     @classmethod
     def for_name(cls, s: str) -> "JobID":
@@ -35,8 +38,12 @@ class TaskID:
     is_map: bool
     id: int
 
+    def __post_init__(self):
+        object.__setattr__(self, "_s", f"task_{self.job.jt}_{self.job.id:04d}_"
+                                       f"{'m' if self.is_map else 'r'}_{self.id:06d}")
+
     def __str__(self):
-        return f"task_{self.job.jt}_{self.job.id:04d}_{'m' if self.is_map else 'r'}_{self.id:06d}"
+        return self._s
 
     @classmethod
     def for_name(cls, s: str) -> "TaskID":
@@ -54,10 +61,11 @@ class TaskAttemptID:
     task: TaskID
     id: int
 
+    def __post_init__(self):
+        object.__setattr__(self, "_s", "attempt" + str(self.task)[4:] + f"_{self.id}")
+
     def __str__(self):
-        t = self.task
-        return (f"attempt_{t.job.jt}_{t.job.id:04d}_{'m' if t.is_map else 'r'}_"
-                f"{t.id:06d}_{self.id}")
+        return self._s
 
     @property
     def job(self):

@@ -20,6 +20,19 @@ Configuration.add_default_resource("mapred-default.xml")
 Configuration.add_default_resource("mapred-site.xml")
 
 
+_USER = None
+
+
+def _login_user():
+    global _USER
+    if _USER is None:
+        try:
+            _USER = getpass.getuser()
+        except Exception:  # noqa: BLE001
+            _USER = "unknown"
+    return _USER
+
+
 class JobConf(Configuration):
     def __init__(self, conf=None, job_class=None):
         if isinstance(conf, Configuration):
@@ -39,7 +52,7 @@ class JobConf(Configuration):
     getJobName, setJobName = get_job_name, set_job_name  # noqa: N815
 
     def get_user(self):
-        return self.get("user.name") or os.environ.get("USER") or getpass.getuser()
+        return self.get("user.name") or os.environ.get("USER") or _login_user()
 
     def set_user(self, u):
         self.set("user.name", u)

@@ -30,6 +30,7 @@ from .counters import Counters
 from .ids import JobID, TaskAttemptID, TaskID
 from .jobclient import FAILED, KILLED, PREP, RUNNING, SUCCEEDED, JobStatus, RunningJob
 from .scheduler.costmodel import CostModel
+from ..utils.trace import TRACE
 
 log = logging.getLogger("hbmr.jobtracker")
 
@@ -48,6 +49,7 @@ class TrackerInfo:
         self.blacklisted = False
         self.jobs_seen: set[str] = set()
         self.wake = False
+        self.more = False    # the last assignment stopped at the per-heartbeat cap
 
     def gpu_devices(self):
         return [g["device"] for g in self.status.gpus]
@@ -189,6 +191,9 @@ class JobInProgress:
             self.split_job = new_instance(sj_cls, conf)
             splits = self.split_job.get_splits(conf, trackers)
             self.collective_reduce = bool(getattr(self.split_job, "collective_reduce", True))
+            from ..gpu.splitjob import SplitJob
+            if type(self.split_job).map_gpu is not SplitJob.map_gpu:
+                self.gpu_capable = True   # the split job has a device map
             split_dicts = [s.to_dict() for s in splits]
         else:
             informat = new_instance(conf.get_input_format(), conf)
@@ -319,14 +324,14 @@ class JobHistory:
         self.max_events = 200_000
 
     def log(self, event, **kw):
-        rec = {"ts": time.time(), "event": event, **kw}
-        with self._lock:
-            if len(self.events) < self.max_events:
-                self.events.append(rec)
-            if self.path:
-                import json
-                with open(self.path, "a") as f:
-                    f.write(json.dumps(rec) + "\n")
+        kw["ts"] = time.time()
+        kw["event"] = event
+        if len(self.events) < self.max_events:
+            self.events.append(kw)     # list.append is atomic under the GIL
+        if self.path:
+            import json
+            with self._lock, open(self.path, "a") as f:
+                f.write(json.dumps(kw) + "\n")
 
 
 class _JTJobHandle:
@@ -429,6 +434,8 @@ class JobTracker:
                     if a is not None and a.tracker == name and jip.reduces:
                         # its map output is gone with the tracker
                         tip.successful = None
+                        jip.maps_done -= 1
+                        jip.t_maps_done = 0.0
                         if a.run_on_gpu:
                             jip.finished_gpu_maps -= 1
                         else:
@@ -440,6 +447,8 @@ class JobTracker:
         return JobID(self.name, next(self._seq))
 
     def submit_job(self, conf) -> RunningJob:
+        if TRACE.on:
+            TRACE.instant("jt.submit")
         jid = self.new_job_id()
         jip = JobInProgress(self, jid, conf)
         with self.lock:
@@ -492,6 +501,8 @@ class JobTracker:
                 jip.split_job.job_succeeded(jip)
             except Exception:  # noqa: BLE001
                 log.exception("job_succeeded hook failed")
+        if TRACE.on:
+            TRACE.instant("jt.job_finished", job=str(jip.job_id), state=state)
         jip.done.set()
         for cb in self.listeners:
             cb("finished", jip)
@@ -517,7 +528,11 @@ class JobTracker:
         ``block`` seconds) until new work exists or the tracker calls wakeup(),
         so idle trackers learn about new tasks immediately instead of on their
         next periodic heartbeat (the reference's 3 s floor, B13)."""
-        resp = self._heartbeat(status, initial, accept_new_tasks)
+        if TRACE.on:
+            with TRACE.span("jt.heartbeat", block=block):
+                resp = self._heartbeat(status, initial, accept_new_tasks)
+        else:
+            resp = self._heartbeat(status, initial, accept_new_tasks)
         if getattr(self, "_shutdown_trackers", False):
             resp["actions"].append(P.shutdown_action())
             return resp
@@ -538,11 +553,14 @@ class JobTracker:
                     resp["actions"].append(P.shutdown_action())
                     break
                 self.cv.wait(left)
+                if TRACE.on:
+                    TRACE.instant("jt.longpoll.wake", wake=tr.wake)
                 if tr.wake or self.trackers.get(name) is not tr:
                     break
                 if tr.status.healthy and not tr.blacklisted:
                     resp["actions"] += self.scheduler.assign_tasks(tr)
             tr.wake = False
+            resp["more"] = tr.more
         return resp
 
     def _heartbeat(self, status, initial, accept_new_tasks):
@@ -567,6 +585,7 @@ class JobTracker:
                 tr.cached.discard(tuple(k))
             for rep in st.task_reports:
                 self._update_task_status(tr, P.TaskStatus.from_dict(rep), actions)
+            tr.more = False
             if accept_new_tasks and st.healthy and not tr.blacklisted:
                 actions += self.scheduler.assign_tasks(tr)
             # kill attempts of jobs that are done / tasks already completed
@@ -575,7 +594,7 @@ class JobTracker:
                 if a is not None and (a.tip.job.completed() or
                                       (a.tip.successful is not None and a.tip.successful is not a)):
                     actions.append(P.kill_task_action(aid))
-        return {"actions": actions, "interval": self.heartbeat_interval}
+        return {"actions": actions, "interval": self.heartbeat_interval, "more": tr.more}
 
     def _update_task_status(self, tr: TrackerInfo, ts: P.TaskStatus, actions):
         a = self.attempt_index.get(ts.attempt_id)
@@ -719,6 +738,9 @@ class JobTracker:
             jip.status.reduce_progress = jip.reduces_done / len(jip.reduces)
 
     def _check_job_done(self, jip: JobInProgress):
+        # O(1) on the counters; the TIP scan only confirms the rare final case
+        if jip.maps_done < len(jip.maps) or jip.reduces_done < len(jip.reduces):
+            return
         if all(t.is_complete() for t in jip.maps) and all(t.is_complete() for t in jip.reduces):
             self._finish_job(jip, SUCCEEDED)
 

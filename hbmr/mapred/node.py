@@ -61,7 +61,8 @@ class Node:
         else:
             addr = self.store.get("hbmr/jobtracker").decode()
             jt_handle = JobTrackerProxy(addr)
-        gpus = [self.local_rank] if self.use_gpu else []
+        simulate = self.conf.get_boolean("hbmr.gpu.simulate", False)
+        gpus = [self.local_rank] if (self.use_gpu or simulate) else []
         self.tt = TaskTracker(self.conf, jt_handle,
                               name=f"tracker_{socket.gethostname()}_r{self.rank}", rank=self.rank,
                               world_size=self.world, gpu_devices=gpus, comm=self.comm)

@@ -55,6 +55,10 @@ class HybridTaskScheduler(TaskScheduler):
         self.locality_wait = conf.get_int("hbmr.locality.wait.ms", 500) / 1000.0
         self.max_reduces_per_hb = conf.get_int("hbmr.scheduler.max.reduces.per.heartbeat", 4)
         self.speculate_after = conf.get_float("hbmr.speculative.slowdown", 3.0)
+        # cap map launches per heartbeat response so a tracker can start the
+        # first tasks while the rest are still being assigned (the response
+        # says "more" and the tracker calls right back)
+        self.max_maps_per_hb = max(1, conf.get_int("hbmr.scheduler.max.maps.per.heartbeat", 16))
         self._skips: dict = {}
         self.decisions = 0
 
@@ -107,6 +111,8 @@ class HybridTaskScheduler(TaskScheduler):
         reduce_free = tr.status.max_reduce_slots - tr.running_reduce
         gpu_free = {g["device"]: g["max_slots"] * self.queue_depth - tr.running_gpu.get(
             g["device"], 0) for g in tr.status.gpus}
+        budget = self.max_maps_per_hb
+        tr.more = False
         for jip in sorted(jt.job_queue, key=lambda j: (_prio(j.priority), j.submit_time)):
             if jip.completed():
                 continue
@@ -131,6 +137,9 @@ class HybridTaskScheduler(TaskScheduler):
             if jip.gpu_capable:
                 for dev in sorted(gpu_free):
                     while gpu_free[dev] > 0 and jip.pending_maps:
+                        if budget <= 0:
+                            tr.more = True
+                            break
                         # delay scheduling: a GPU waits up to locality_wait for a
                         # split it holds in HBM / that names it before it steals a
                         # non-local one (a non-local split must be re-materialised)
@@ -148,11 +157,15 @@ class HybridTaskScheduler(TaskScheduler):
                             self._skips.pop(key, None)
                         actions.append(jt.launch(tr, tip, on_gpu=True, device=dev))
                         gpu_free[dev] -= 1
+                        budget -= 1
                         self.decisions += 1
             # ---- CPU maps
             if cpu_free > 0 and jip.pending_maps:
                 allowed = self._cpu_allowed(jip, total_cpu, total_gpu, now)
                 while cpu_free > 0 and allowed > 0 and jip.pending_maps:
+                    if budget <= 0:
+                        tr.more = True
+                        break
                     got = jip.obtain_map(tr, False, -1, allow_nonlocal=True)
                     if got is None:
                         break
@@ -160,6 +173,7 @@ class HybridTaskScheduler(TaskScheduler):
                     actions.append(jt.launch(tr, tip, on_gpu=False))
                     cpu_free -= 1
                     allowed -= 1
+                    budget -= 1
                     self.decisions += 1
             # ---- speculative backups of stragglers onto idle GPUs
             if jip.speculative and jip.gpu_capable and not jip.pending_maps:

@@ -25,6 +25,7 @@ import os
 import queue
 import random
 import socket
+import sys
 import threading
 import time
 import traceback
@@ -35,6 +36,8 @@ from . import protocol as P
 from .ids import TaskAttemptID
 from .jobconf import JobConf
 from .task import MapOutputLocation, MapTask, ReduceTask, TaskReporter
+
+from ..utils.trace import TRACE
 
 log = logging.getLogger("hbmr.tasktracker")
 
@@ -101,6 +104,13 @@ class TaskTracker:
                  local_dir=None):
         self.conf = conf
         self.jt = jobtracker
+        # The launcher, completion and heartbeat threads hand work to each
+        # other; with CPython's default 5 ms GIL switch interval a woken
+        # thread can wait that long for the interpreter while another one
+        # runs bookkeeping, idling the GPU.  0.2 ms keeps hand-offs prompt.
+        si = conf.get_float("hbmr.python.switchinterval.ms", 0.2)
+        if si > 0:
+            sys.setswitchinterval(si / 1000.0)
         self.host = socket.gethostname()
         self.rank = rank
         self.world_size = world_size
@@ -145,8 +155,11 @@ class TaskTracker:
             thread_name_prefix=f"{self.name}-gpupipes")
         self.gpu_runtime = None
         if self.gpu_devices:
-            from ..gpu.runtime import GpuRuntime
-            self.gpu_runtime = GpuRuntime(self, self.gpu_devices, self.gpu_slots_per_device)
+            if conf.get_boolean("hbmr.gpu.simulate", False):
+                from ..gpu.simulated import SimulatedGpuRuntime as _Rt
+            else:
+                from ..gpu.runtime import GpuRuntime as _Rt
+            self.gpu_runtime = _Rt(self, self.gpu_devices, self.gpu_slots_per_device)
         self.heartbeats = 0
         self.tasks_done = 0
 
@@ -190,6 +203,9 @@ class TaskTracker:
 
     def _finish(self, run: _Running, state, diag="", output=None, device_time=0.0, wake=True):
         st = run.status
+        if TRACE.on:
+            TRACE.instant("tt.finish", attempt=st.attempt_id, state=state,
+                          where=(output or {}).get("where") if isinstance(output, dict) else None)
         st.state = state
         st.finish_time = time.time()
         st.diagnostic = diag
@@ -233,18 +249,24 @@ class TaskTracker:
 
     def _hb_loop(self):
         initial = True
+        more = False
         while not self._stop.is_set():
             try:
                 self._news.clear()
                 st = self.status()
-                block = 0.0 if (st.task_reports or initial) else self.interval
+                block = 0.0 if (st.task_reports or initial or more) else self.interval
+                if TRACE.on:
+                    TRACE.instant("tt.heartbeat.send", reports=len(st.task_reports), block=block)
                 resp = self.jt.heartbeat(st.to_dict(), initial=initial,
                                          accept_new_tasks=True, block=block)
+                if TRACE.on:
+                    TRACE.instant("tt.heartbeat.recv", actions=len(resp.get("actions", [])))
                 self.heartbeats += 1
                 initial = False
+                more = bool(resp.get("more"))
                 for act in resp.get("actions", []):
                     self._handle(act)
-                if not resp.get("actions") and not st.task_reports and block == 0.0:
+                if not resp.get("actions") and not st.task_reports and block == 0.0 and not more:
                     self._news.wait(self.interval)
                 self._check_timeouts()
             except Exception as e:  # noqa: BLE001
@@ -367,6 +389,8 @@ class TaskTracker:
     def _run_reduce(self, run: _Running):
         spec, js = run.spec, run.job
         run.status.start_time = time.time()
+        if TRACE.on:
+            TRACE.instant("tt.reduce.start", attempt=spec.attempt_id)
         try:
             self._maybe_inject_fault(run) if not spec.collective else None
             if js.split_job is not None:
@@ -379,9 +403,11 @@ class TaskTracker:
                 missing = [a for _tid, a, _o in spec.map_outputs if a not in js.map_outputs]
                 if missing:
                     raise RuntimeError(f"map outputs lost on {self.name}: {missing[:4]}")
-                if self.gpu_runtime is not None:
+                dev = None if self.gpu_runtime is None else \
+                    self.gpu_runtime.torch_device(self.gpu_devices[0])
+                if dev is not None and dev.type == "cuda":
                     import torch
-                    ctx.device = self.gpu_runtime.torch_device(self.gpu_devices[0])
+                    ctx.device = dev
                     with torch.cuda.device(ctx.device):
                         combined = js.split_job.combine(ctx, outs)
                         js.result = js.split_job.reduce(ctx, combined)

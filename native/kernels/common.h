@@ -41,6 +41,27 @@ __device__ __forceinline__ void hbmr_unpack8(const uint4 v, float f[8]) {
   f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
 }
 
+// acc[j] += round_half_even(f[j] * scale) for the int64 fixed-point combiner.
+// __float2ll_rn is a ~15-op sequence; when every scaled value fits in int32
+// (|x| < 128 at scale 2^24 — the normal case) v_rndne + v_cvt_i32 is exact
+// and 3 ops.  The per-lane branch skips the slow path when no lane needs it.
+__device__ __forceinline__ void hbmr_fx_accum8(const float f[8], float scale, long long acc[8]) {
+  float y[8];
+  float m = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    y[j] = f[j] * scale;
+    m = fmaxf(m, fabsf(y[j]));
+  }
+  if (m < 2147483520.f) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += (long long)(int)__builtin_rintf(y[j]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += __float2ll_rn(y[j]);
+  }
+}
+
 // Bijective XCD-aware remap of a 1-D block id (cdna_hip_programming.md §5 T1):
 // consecutive logical tiles land on the same XCD (same L2).
 __device__ __forceinline__ uint32_t hbmr_xcd_remap(uint32_t bid, uint32_t nwg) {

@@ -276,11 +276,11 @@ __device__ __forceinline__ void lds_add_row(u64* s_rows, int r, int sub, const u
   float f[8];
   hbmr_unpack8(v, f);
   u64* dst = s_rows + r * AccCfg<D>::RS + sub * 9;
+  long long q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  hbmr_fx_accum8(f, scale, q);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const long long q = __float2ll_rn(f[j] * scale);
-    if (q) atomicAdd(dst + j, (u64)q);
-  }
+  for (int j = 0; j < 8; ++j)
+    if (q[j]) atomicAdd(dst + j, (u64)q[j]);
 }
 
 template <int D>
@@ -522,84 +522,84 @@ __global__ __launch_bounds__(256) void kmeans_scatter_kernel(const int32_t* __re
     if (lab[j] >= 0) perm[s_base[lab[j]] + rank[j]] = (uint32_t)(p0 + j);
 }
 
+// Segmented row sum of the rows perm[s0:e) (sorted by cluster; cluster c owns
+// perm[offsets[c]:offsets[c+1])) into out[c] (int64 fixed point).  The wave
+// walks its range one cluster segment at a time: the GPW row groups split a
+// segment's rows, U rows per group in flight (index load → row gather), and
+// at the segment end the groups are reduced with xor-shuffles so each cluster
+// costs one 128-value atomic flush per wave — spread over all groups — rather
+// than one per group.  Segment bounds are wave-uniform (scalar loads).
+template <int D, int U>
+__device__ __forceinline__ void segsum_range(const __bf16* __restrict__ X,
+                                             const uint32_t* __restrict__ pm,
+                                             const uint32_t* __restrict__ of, int k, long s0,
+                                             long e, u64* __restrict__ out, float scale) {
+  constexpr int TPP = D / 8;            // lanes per row
+  constexpr int GPW = HBMR_WAVE / TPP;  // row groups per wave
+  const int lane = threadIdx.x & 63;
+  const int grp = lane / TPP, sub = lane % TPP;
+  // first cluster whose segment contains s0: upper_bound(of, s0) - 1
+  int lo = 0, hi = k;  // invariant of[lo] <= s0 < of[hi] (of[k] = n)
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if ((long)of[mid] <= s0) lo = mid; else hi = mid;
+  }
+  int cur = __builtin_amdgcn_readfirstlane(lo);
+  long p = s0;
+  while (p < e) {
+    const long segE = min(e, (long)(uint32_t)__builtin_amdgcn_readfirstlane(of[cur + 1]));
+    if (segE > p) {
+      long long acc[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = 0;
+      for (long base = p + grp; base < segE; base += (long)U * GPW) {
+        uint32_t idx[U];
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long q = base + (long)u * GPW;
+          idx[u] = q < segE ? pm[q] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long q = base + (long)u * GPW;
+          if (q < segE) v[u] = reinterpret_cast<const uint4*>(X + (size_t)idx[u] * D)[sub];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const long q = base + (long)u * GPW;
+          if (q < segE) {
+            float f[8];
+            hbmr_unpack8(v[u], f);
+            hbmr_fx_accum8(f, scale, acc);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int off = TPP; off < HBMR_WAVE; off <<= 1) acc[j] += __shfl_xor(acc[j], off);
+      }
+      u64* dst = out + (size_t)cur * D + sub * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j % GPW == grp % 8 && acc[j]) atomicAdd(dst + j, (u64)acc[j]);
+      p = segE;
+    }
+    ++cur;
+  }
+}
+
 template <int D, int U>
 __global__ __launch_bounds__(256) void kmeans_segsum_kernel(
     const __bf16* __restrict__ X, long n, const uint32_t* __restrict__ perm,
     const uint32_t* __restrict__ offsets, int k, long chunk, long long* __restrict__ sums,
     float scale) {
-  constexpr int TPP = D / 8;              // lanes per row
-  constexpr int GPW = HBMR_WAVE / TPP;    // row groups per wave
-  const int lane = threadIdx.x & 63;
-  const int grp = lane / TPP, sub = lane % TPP;
   const long wid = (long)blockIdx.x * (blockDim.x / HBMR_WAVE) + threadIdx.x / HBMR_WAVE;
   const long s = wid * chunk;
   if (s >= n) return;
-  const long e = min(n, s + chunk);
-  // first cluster whose segment contains position s: upper_bound(offsets, s) - 1
-  int lo = 0, hi = k;  // invariant offsets[lo] <= s < offsets[hi] (offsets[k] = n)
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if ((long)offsets[mid] <= s) lo = mid; else hi = mid;
-  }
-  int cur = lo;
-  long bound = offsets[cur + 1];
-  long long acc[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] = 0;
-  auto flush = [&]() {
-    u64* dst = reinterpret_cast<u64*>(sums) + (size_t)cur * D + sub * 8;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (acc[j]) atomicAdd(dst + j, (u64)acc[j]);
-      acc[j] = 0;
-    }
-  };
-  for (long base = s + grp; base < e; base += (long)U * GPW) {
-    uint32_t idx[U];
-    uint4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long p = base + (long)u * GPW;
-      idx[u] = p < e ? perm[p] : 0u;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long p = base + (long)u * GPW;
-      if (p < e) v[u] = reinterpret_cast<const uint4*>(X + (size_t)idx[u] * D)[sub];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long p = base + (long)u * GPW;
-      if (p < e) {
-        while (p >= bound) {
-          flush();
-          ++cur;
-          bound = offsets[cur + 1];
-        }
-        float f[8];
-        hbmr_unpack8(v[u], f);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += __float2ll_rn(f[j] * scale);
-      }
-    }
-  }
-  // Final flush: when every group of the wave ended in the same cluster (the
-  // common case), reduce across groups in registers first so one group issues
-  // the atomics.
-  const int c0 = __shfl(cur, 0);
-  if (__all(cur == c0)) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-#pragma unroll
-      for (int off = TPP; off < HBMR_WAVE; off <<= 1) {
-        const long long o = __shfl_xor(acc[j], off);
-        acc[j] += o;
-      }
-    }
-    if (grp == 0) flush();
-  } else {
-    flush();
-  }
+  segsum_range<D, U>(X, perm, offsets, k, s, min(n, s + chunk), reinterpret_cast<u64*>(sums),
+                     scale);
 }
 
 // ---- grouped sorted combiner ------------------------------------------------------
@@ -635,6 +635,28 @@ __device__ void block_exclusive_scan(const uint32_t* __restrict__ in, int k, uin
   }
   if (t == 255) *total = wbase + v;
   __syncthreads();
+}
+
+// Per-split label histogram from the labels array (alternative to the fused
+// histogram atomics in the assign epilogue): LDS bins, one flush per block.
+constexpr long kHistPts = 16384;
+__global__ __launch_bounds__(256) void kmeans_hist_grouped_kernel(const SplitTable tbl,
+                                                                  const int32_t* __restrict__ labels,
+                                                                  uint32_t* __restrict__ hist) {
+  extern __shared__ uint32_t s_bins[];
+  const int k = tbl.k;
+  const int s = __builtin_amdgcn_readfirstlane(find_split(tbl, blockIdx.x));
+  const long local = blockIdx.x - tbl.blk[s];
+  const long n = tbl.n[s];
+  for (int i = threadIdx.x; i < k; i += 256) s_bins[i] = 0u;
+  __syncthreads();
+  const int32_t* lab = labels + tbl.off[s];
+  const long p1 = min(n, (local + 1) * kHistPts);
+  for (long p = local * kHistPts + threadIdx.x; p < p1; p += 256) atomicAdd(s_bins + lab[p], 1u);
+  __syncthreads();
+  uint32_t* hs = hist + (size_t)s * k;
+  for (int i = threadIdx.x; i < k; i += 256)
+    if (s_bins[i]) atomicAdd(hs + i, s_bins[i]);
 }
 
 __global__ __launch_bounds__(256) void kmeans_scatter_grouped_kernel(
@@ -688,80 +710,16 @@ template <int D, int U>
 __global__ __launch_bounds__(256) void kmeans_segsum_grouped_kernel(
     const SplitTable tbl, const uint32_t* __restrict__ perm, const uint32_t* __restrict__ offsets,
     long chunk, long long* __restrict__ sums, float scale) {
-  constexpr int TPP = D / 8;
-  constexpr int GPW = HBMR_WAVE / TPP;
   const int k = tbl.k;
-  const int lane = threadIdx.x & 63;
-  const int grp = lane / TPP, sub = lane % TPP;
   const long wid = (long)blockIdx.x * (blockDim.x / HBMR_WAVE) + threadIdx.x / HBMR_WAVE;
   // tbl.blk holds the prefix sum of WAVES (chunks) per split for this launch
   if (wid >= tbl.blk[tbl.nsplit]) return;
-  const int sidx = find_split(tbl, wid);
+  const int sidx = __builtin_amdgcn_readfirstlane(find_split(tbl, wid));
   const long n = tbl.n[sidx];
   const long s0 = (wid - tbl.blk[sidx]) * chunk;
-  const long e = min(n, s0 + chunk);
-  const __bf16* X = tbl.X[sidx];
-  const uint32_t* pm = perm + tbl.off[sidx];
-  const uint32_t* of = offsets + (size_t)sidx * (k + 1);
-  u64* out = reinterpret_cast<u64*>(sums) + (size_t)sidx * k * D;
-  int lo = 0, hi = k;
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if ((long)of[mid] <= s0) lo = mid; else hi = mid;
-  }
-  int cur = lo;
-  long bound = of[cur + 1];
-  long long acc[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] = 0;
-  auto flush = [&]() {
-    u64* dst = out + (size_t)cur * D + sub * 8;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (acc[j]) atomicAdd(dst + j, (u64)acc[j]);
-      acc[j] = 0;
-    }
-  };
-  for (long base = s0 + grp; base < e; base += (long)U * GPW) {
-    uint32_t idx[U];
-    uint4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long p = base + (long)u * GPW;
-      idx[u] = p < e ? pm[p] : 0u;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long p = base + (long)u * GPW;
-      if (p < e) v[u] = reinterpret_cast<const uint4*>(X + (size_t)idx[u] * D)[sub];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long p = base + (long)u * GPW;
-      if (p < e) {
-        while (p >= bound) {
-          flush();
-          ++cur;
-          bound = of[cur + 1];
-        }
-        float f[8];
-        hbmr_unpack8(v[u], f);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += __float2ll_rn(f[j] * scale);
-      }
-    }
-  }
-  const int c0 = __shfl(cur, 0);
-  if (__all(cur == c0)) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-#pragma unroll
-      for (int off = TPP; off < HBMR_WAVE; off <<= 1) acc[j] += __shfl_xor(acc[j], off);
-    }
-    if (grp == 0) flush();
-  } else {
-    flush();
-  }
+  segsum_range<D, U>(tbl.X[sidx], perm + tbl.off[sidx], offsets + (size_t)sidx * (k + 1), k, s0,
+                     min(n, s0 + chunk), reinterpret_cast<u64*>(sums) + (size_t)sidx * k * D,
+                     scale);
 }
 
 // Reduce side + next-iteration prep.  One workgroup per cluster.
@@ -875,9 +833,20 @@ int cu_count() {
 
 bool set_lds_limits() {
   // Opt every kernel that asks for >64 KiB of dynamic LDS into the full 160 KiB.
+  // The limit is static + dynamic, so a kernel with static __shared__ arrays
+  // may ask for less; a refused opt-in must not leave a sticky error behind
+  // for the next launch's hipGetLastError.
   static bool done = false;
   if (!done) {
-#define HBMR_LDS_OPTIN(fn) hipFuncSetAttribute((const void*)(fn), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)
+    auto optin = [](const void* fn) {
+      hipFuncAttributes at{};
+      size_t stat = 0;
+      if (hipFuncGetAttributes(&at, fn) == hipSuccess) stat = at.sharedSizeBytes;
+      if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(160 * 1024 - stat)) != hipSuccess)
+        (void)hipGetLastError();
+    };
+#define HBMR_LDS_OPTIN(fn) optin((const void*)(fn))
     HBMR_LDS_OPTIN((kmeans_accum_lds_kernel<64, 8>));
     HBMR_LDS_OPTIN((kmeans_accum_lds_kernel<128, 8>));
     HBMR_LDS_OPTIN((kmeans_accum_lds_kernel<256, 8>));
@@ -1020,7 +989,12 @@ static int map_batch_grouped(int ntasks, const void* const* X, const long* n, in
   uint32_t* offsets = reinterpret_cast<uint32_t*>(w + 2 * hb);
   uint32_t* perm = reinterpret_cast<uint32_t*>(w + 2 * hb + ws_align((size_t)ntasks * (k + 1) * 4));
   HBMR_RETURN_IF_ERROR(hipMemsetAsync(hist, 0, 2 * hb, st));  // hist + cursor
-  // 1. assign (+ fused histogram)
+  // 1. assign (+ histogram: fused atomics in the assign epilogue, or a separate
+  //    LDS-binned pass over the labels; HBMR_KMEANS_FUSED_HIST=1 selects fused)
+  static const bool fused = [] {
+    const char* e = getenv("HBMR_KMEANS_FUSED_HIST");
+    return e != nullptr && e[0] == '1';
+  }();
   long nb = 0;
   int pts = 0;
   switch (dp) {
@@ -1040,7 +1014,7 @@ static int map_batch_grouped(int ntasks, const void* const* X, const long* n, in
   case DD:                                                                                   \
     hipLaunchKernelGGL(kmeans_assign_grouped_kernel<DD>, dim3((unsigned)nb), dim3(kThreads),  \
                        AssignCfg<DD>::LDS_BYTES, st, t, reinterpret_cast<const __bf16*>(C),  \
-                       chalf, k_pad / kCK, labels, hist);                                    \
+                       chalf, k_pad / kCK, labels, fused ? hist : nullptr);                  \
     break;
       HBMR_GA(64)
       HBMR_GA(128)
@@ -1048,6 +1022,19 @@ static int map_batch_grouped(int ntasks, const void* const* X, const long* n, in
 #undef HBMR_GA
     }
     HBMR_RETURN_IF_ERROR(hipGetLastError());
+  }
+  if (!fused) {
+    long hb_blocks = 0;
+    for (int i = 0; i < ntasks; ++i) {
+      t.blk[i] = hb_blocks;
+      hb_blocks += (n[i] + kHistPts - 1) / kHistPts;
+    }
+    t.blk[ntasks] = hb_blocks;
+    if (hb_blocks > 0) {
+      hipLaunchKernelGGL(kmeans_hist_grouped_kernel, dim3((unsigned)hb_blocks), dim3(256),
+                         (size_t)k * 4, st, t, labels, hist);
+      HBMR_RETURN_IF_ERROR(hipGetLastError());
+    }
   }
   // 2. scan + scatter (+ counts, offsets)
   nb = 0;

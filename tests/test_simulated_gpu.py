@@ -1,0 +1,109 @@
+"""GPU-slot scheduling paths without a GPU (hbmr.gpu.simulate), SleepJob, and
+the event tracer.
+
+The reference exercised its GPU scheduler with fake trackers that advertise
+GPU devices (src/test/org/apache/hadoop/mapred/TestJobQueueTaskScheduler.java:
+183-201); here whole trackers run with simulated GPU slots.
+"""
+import json
+
+import torch
+
+from hbmr.examples.sleepjob import sleep_job_conf, split_sleep_conf
+from hbmr.mapred.cluster import LocalCluster
+from hbmr.mapred.jobclient import JobClient
+from hbmr.mapred.jobconf import JobConf
+from hbmr.models import kmeans as K
+from hbmr.utils.trace import TRACE
+
+JIP = "org.apache.hadoop.mapred.JobInProgress$Counter"
+
+
+def _sim_conf(**kw):
+    conf = JobConf()
+    conf.set_boolean("hbmr.gpu.simulate", True)
+    conf.set_int("mapred.tasktracker.map.gpu.tasks.maximum", 1)
+    conf.set_int("mapred.task.timeout", 0)
+    for k, v in kw.items():
+        conf.set(k, str(v))
+    return conf
+
+
+def _kmeans(cl, conf, iters=3, n=12000, k=6, d=16):
+    drv = K.KMeansDriver(cl.submit_job, lambda rj: rj._impl.jip.result[0], conf=conf, k=k, d=d,
+                         inp=f"synthetic:{n}:5", split_points=2000)
+    for _ in range(iters):
+        assert drv.step()["points"] == n
+    return drv
+
+
+def test_simulated_gpu_slots_take_every_map_and_match_cpu_bits():
+    conf = _sim_conf()
+    with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=0) as cl:
+        drv = _kmeans(cl, conf)
+        cs = drv.history[-1]["counters"]
+        assert cs.get(JIP, "GPU_MAP_TASKS") == 6 and cs.get(JIP, "CPU_MAP_TASKS") == 0
+        c_gpu = drv.centroids()
+    plain = JobConf()
+    with LocalCluster(plain, num_trackers=1, cpu_slots=2) as cl:
+        c_cpu = _kmeans(cl, plain).centroids()
+    # int64 fixed-point partials: identical regardless of where maps ran
+    assert torch.equal(c_gpu, c_cpu)
+
+
+def test_hybrid_policy_keeps_slow_cpu_slots_idle():
+    # GPU tasks 1 ms, CPU tasks 40 ms: after the CPU probe, min-makespan gives
+    # the CPU slots nothing while the GPU queue can absorb the job
+    conf = _sim_conf(**{"hbmr.scheduler.policy": "hybrid", "hbmr.gpu.simulate.task.ms": 1,
+                        "hbmr.gpu.queue.depth": 8})
+    with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=2) as cl:
+        for _ in range(3):
+            rj = cl.submit_job(split_sleep_conf(32, map_ms=40, base=conf))
+            rj.waitForCompletion(60)
+            assert rj.isSuccessful(), rj.getFailureInfo()
+        cs = rj.getCounters()
+        assert cs.get(JIP, "GPU_MAP_TASKS") >= 31
+        assert cs.get(JIP, "CPU_MAP_TASKS") <= 1
+        assert rj._impl.jip.result[0]["maps"] == 32
+
+
+def test_stock_policy_uses_cpu_slots_too():
+    conf = _sim_conf(**{"hbmr.scheduler.policy": "stock", "hbmr.gpu.simulate.task.ms": 5,
+                        "hbmr.gpu.queue.depth": 1})
+    with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=2) as cl:
+        rj = cl.submit_job(split_sleep_conf(24, map_ms=5, base=conf))
+        rj.waitForCompletion(60)
+        assert rj.isSuccessful(), rj.getFailureInfo()
+        cs = rj.getCounters()
+        assert cs.get(JIP, "CPU_MAP_TASKS") > 0 and cs.get(JIP, "GPU_MAP_TASKS") > 0
+        assert cs.get(JIP, "CPU_MAP_TASKS") + cs.get(JIP, "GPU_MAP_TASKS") == 24
+
+
+def test_classic_sleep_job_runs_on_cluster():
+    with LocalCluster(JobConf(), num_trackers=2, cpu_slots=2) as cl:
+        rj = JobClient.runJob(sleep_job_conf(maps=4, reduces=2, map_ms=5, reduce_ms=5,
+                                             reduce_count=3), cluster=cl, verbose=False)
+        assert rj.isSuccessful(), rj.getFailureInfo()
+        cs = rj.getCounters()
+        assert cs.get("org.apache.hadoop.mapred.Task$Counter", "REDUCE_INPUT_GROUPS") == 6
+
+
+def test_tracer_records_task_flow_and_exports_chrome(tmp_path):
+    conf = _sim_conf()
+    with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=0) as cl:
+        TRACE.clear()
+        TRACE.enable()
+        try:
+            rj = cl.submit_job(split_sleep_conf(8, base=conf))
+            rj.waitForCompletion(30)
+        finally:
+            TRACE.disable()
+    names = {e[3] for e in TRACE.events}
+    assert {"jt.submit", "gpu.launch", "gpu.complete", "tt.finish", "jt.job_finished"} <= names
+    out = tmp_path / "trace.json"
+    TRACE.to_chrome(str(out))
+    doc = json.loads(out.read_text())
+    assert any(e.get("cname") == "good" for e in doc["traceEvents"])   # GPU-coloured tasks
+    TRACE.to_jsonl(str(tmp_path / "trace.jsonl"))
+    assert (tmp_path / "trace.jsonl").read_text().count("\n") == len(TRACE.events)
+    TRACE.clear()

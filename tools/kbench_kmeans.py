@@ -68,6 +68,24 @@ def main():
             t_sp, t_sp_min = timeit(per_split, max(2, a.reps // 2))
             r.update(split=ns, per_split_ms=t_sp, per_split_min_ms=t_sp_min,
                      per_split_points_per_s=n / (t_sp * 1e-3))
+            # grouped batches of up to 64 splits (the GPU runtime's launch unit)
+            views = [x[s0:s0 + ns] for s0 in range(0, n, ns)]
+            batches = [views[i:i + 64] for i in range(0, len(views), 64)]
+            scratch = []
+            for b in batches:
+                nl, nw = km.batch_scratch_sizes([v.shape[0] for v in b], k)
+                scratch.append((torch.empty(nl, dtype=torch.int32, device=dev),
+                                torch.empty(nw, dtype=torch.uint8, device=dev),
+                                torch.empty(len(b), k, dp, dtype=torch.int64, device=dev),
+                                torch.empty(len(b), k, dtype=torch.int64, device=dev)))
+
+            def grouped():
+                for b, (bl, bw, bs, bc) in zip(batches, scratch):
+                    km.map_batch_gpu(b, img, bs, bc, bl, bw)
+            t_gr, t_gr_min = timeit(grouped, max(2, a.reps // 2))
+            r.update(grouped_ms=t_gr, grouped_min_ms=t_gr_min,
+                     grouped_points_per_s=n / (t_gr * 1e-3))
+            del scratch
         print(json.dumps(r), flush=True)
         out.append(r)
         del x, lab

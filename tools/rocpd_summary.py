@@ -1,0 +1,62 @@
+"""Summarise a rocprofv3 rocpd SQLite result (``--kernel-trace --stats`` run).
+
+usage: python tools/rocpd_summary.py <results.db> [--top N] [--timeline PATTERN]
+
+Prints per-kernel call count / total / mean / min (µs), sorted by total, as a
+markdown table (the form committed under ``profiles/``).  ``--timeline``
+additionally lists each dispatch whose name matches PATTERN with its start
+offset, so gaps between launches are visible.
+"""
+import argparse
+import re
+import sqlite3
+
+
+def load(db):
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, start, end, grid_x, workgroup_x from kernels "
+                     "order by start").fetchall()
+    return rows
+
+
+def short(name, width=70):
+    name = name.replace("(anonymous namespace)::", "")
+    name = re.sub(r"^void ", "", name)
+    name = re.sub(r"\(.*$", "", name)
+    return name if len(name) <= width else name[:width - 3] + "..."
+
+
+def summary(rows, top):
+    agg = {}
+    for name, s, e, *_ in rows:
+        a = agg.setdefault(short(name), [0, 0.0, float("inf")])
+        d = (e - s) / 1e3
+        a[0] += 1
+        a[1] += d
+        a[2] = min(a[2], d)
+    tot = sum(v[1] for v in agg.values())
+    lines = ["| kernel | calls | total µs | mean µs | min µs | % |", "|---|---|---|---|---|---|"]
+    for k, (n, t, mn) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
+        lines.append(f"| `{k}` | {n} | {t:.1f} | {t / n:.1f} | {mn:.1f} | {100 * t / tot:.1f} |")
+    return "\n".join(lines)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("db")
+    ap.add_argument("--top", type=int, default=25)
+    ap.add_argument("--timeline")
+    a = ap.parse_args()
+    rows = load(a.db)
+    print(summary(rows, a.top))
+    if a.timeline:
+        t0 = None
+        rx = re.compile(a.timeline)
+        for name, s, e, g, w in rows:
+            if rx.search(name):
+                t0 = s if t0 is None else t0
+                print(f"{(s - t0) / 1e3:12.1f} {(e - s) / 1e3:10.1f}  grid={g} wg={w}  {short(name)}")
+
+
+if __name__ == "__main__":
+    main()
