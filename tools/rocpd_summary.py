@@ -46,8 +46,18 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--timeline")
+    ap.add_argument("--from-last", nargs=2, metavar=("PATTERN", "N"),
+                    help="summarise only from the N-th last dispatch matching PATTERN on "
+                         "(e.g. the timed iterations of a benchmark after its warmup)")
     a = ap.parse_args()
     rows = load(a.db)
+    if a.from_last:
+        rx, n = re.compile(a.from_last[0]), int(a.from_last[1])
+        idx = [i for i, r in enumerate(rows) if rx.search(r[0])]
+        if len(idx) >= n:
+            rows = rows[idx[-n]:]
+        span = (rows[-1][2] - rows[0][1]) / 1e3 if rows else 0.0
+        print(f"window: {len(rows)} dispatches over {span:.1f} µs (first to last end)\n")
     print(summary(rows, a.top))
     if a.timeline:
         t0 = None
