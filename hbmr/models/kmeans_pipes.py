@@ -1,0 +1,147 @@
+"""K-Means through Pipes task binaries — BASELINE config 2 (and the paper's setup).
+
+The fork's users ran K-Means as a Hadoop Pipes job with two executables: a
+CPU binary for CPU map slots and a GPU binary for GPU map slots
+(`-cpubin`/`-gpubin`, Submitter.java:419-420, 523-529), one Lloyd iteration
+per job with the centroids side-loaded from a file.  This module drives the
+same shape against hbmr's binaries (native/apps/kmeans_cpu.cc,
+native/apps/kmeans_gpu.hip):
+
+* input: SequenceFile<LongWritable, FloatVectorWritable> points
+  (:func:`write_points`), split by FileInputFormat;
+* the C++ record reader hands each map its whole split; maps emit exact
+  int64 fixed-point (count, sums) partials per cluster;
+* reducers (CPU, C++) emit ``cluster \\t c0,c1,...``; :func:`read_centroids`
+  folds the part files into the next centroid file (clusters that received
+  no point keep their previous centroid).
+
+The in-process split-level job (hbmr.models.kmeans) is the fast path; this is
+the compatibility path for Pipes users, and both produce bit-identical
+centroids from the same inputs (same fixed-point partials, same update rule).
+"""
+from __future__ import annotations
+
+import os
+import struct
+
+import numpy as np
+import torch
+
+from ..io import sequencefile as seqf
+from ..io.writable import FloatVectorWritable, IntWritable, LongWritable
+from ..mapred import FileInputFormat, FileOutputFormat, JobConf
+from . import kmeans as K
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+BIN = os.path.join(ROOT, "hbmr", "bin")
+
+
+def write_points(path, n, d, seed=1, centers=8, files=1, bf16_exact=True, chunk=1 << 16,
+                 compression="NONE", codec=None):
+    """Synthetic Gaussian-mixture points (hbmr.models.kmeans.synthetic_points) as
+    ``files`` SequenceFiles under directory ``path``.  ``bf16_exact`` rounds the
+    values to bf16 first, so CPU fp32 and GPU bf16 maps see identical data."""
+    os.makedirs(path, exist_ok=True)
+    per = -(-n // files)
+    out = []
+    for fi in range(files):
+        a, b = fi * per, min(n, (fi + 1) * per)
+        fn = os.path.join(path, f"points-{fi:05d}.seq")
+        with seqf.Writer(fn, LongWritable, FloatVectorWritable, compression=compression,
+                         codec=codec) as w:
+            for c0 in range(a, b, chunk):
+                c1 = min(b, c0 + chunk)
+                x = K.synthetic_points(seed, c0, c1 - c0, d, centers, "cpu")
+                if bf16_exact:
+                    x = x.to(torch.bfloat16).to(torch.float32)
+                xb = x.numpy().astype(">f4")
+                hdr = struct.pack(">i", d)
+                for i in range(c1 - c0):
+                    w.append_raw(struct.pack(">q", c0 + i), hdr + xb[i].tobytes())
+        out.append(fn)
+    return out
+
+
+def write_centroids(path, cen: torch.Tensor):
+    cen = cen.detach().to("cpu", torch.float32)
+    with seqf.Writer(path, IntWritable, FloatVectorWritable) as w:
+        for j in range(cen.shape[0]):
+            w.append(IntWritable(j), FloatVectorWritable(cen[j].numpy()))
+    return path
+
+
+def read_centroids(outdir, old: torch.Tensor) -> torch.Tensor:
+    new = old.detach().to("cpu", torch.float32).clone()
+    for fn in sorted(os.listdir(outdir)):
+        if not fn.startswith("part-"):
+            continue
+        with open(os.path.join(outdir, fn)) as f:
+            for line in f:
+                line = line.rstrip("\n")
+                if not line:
+                    continue
+                k, v = line.split("\t", 1)
+                new[int(k)] = torch.from_numpy(np.array([float(t) for t in v.split(",")],
+                                                        dtype=np.float32))
+    return new
+
+
+def iteration_conf(base, inp, out, cen_file, k, d, cpubin=None, gpubin=None, reduces=1,
+                   maps=None) -> JobConf:
+    from ..pipes import submitter
+    job = JobConf(base)
+    job.set_job_name(f"kmeans-pipes {os.path.basename(out)}")
+    FileInputFormat.setInputPaths(job, inp)
+    FileOutputFormat.setOutputPath(job, out)
+    job.set("mapred.input.format.class", "hbmr.mapred.formats:SequenceFileInputFormat")
+    job.set_boolean("hadoop.pipes.java.recordreader", False)
+    job.set_boolean("hadoop.pipes.java.recordwriter", True)
+    job.set_int("hbmr.kmeans.k", k)
+    job.set_int("hbmr.kmeans.dims", d)
+    job.set("hbmr.kmeans.centroids.file", os.path.abspath(cen_file))
+    job.set_num_reduce_tasks(reduces)
+    if maps:
+        job.set_num_map_tasks(maps)
+    if cpubin:
+        submitter.set_executable(job, cpubin)
+    if gpubin:
+        submitter.set_gpu_executable(job, gpubin)
+    return job
+
+
+class KMeansPipesDriver:
+    """Chains Pipes K-Means iterations (one job each)."""
+
+    def __init__(self, workdir, inp, k, d, init: torch.Tensor, base=None, cluster=None,
+                 cpubin=os.path.join(BIN, "kmeans_cpu"), gpubin=os.path.join(BIN, "kmeans_gpu"),
+                 reduces=1, maps=None):
+        self.workdir, self.inp, self.k, self.d = workdir, inp, k, d
+        self.base, self.cluster = base, cluster
+        self.cpubin, self.gpubin, self.reduces, self.maps = cpubin, gpubin, reduces, maps
+        self.centroids = init.detach().to("cpu", torch.float32)
+        self.iteration = 0
+        self.history = []
+        os.makedirs(workdir, exist_ok=True)
+
+    def step(self):
+        from ..pipes import submitter
+        i = self.iteration
+        cen_file = write_centroids(os.path.join(self.workdir, f"centroids-{i:03d}.seq"),
+                                   self.centroids)
+        out = os.path.join(self.workdir, f"iter-{i:03d}")
+        job = iteration_conf(self.base, self.inp, out, cen_file, self.k, self.d, self.cpubin,
+                             self.gpubin, self.reduces, self.maps)
+        rj = submitter.run_job(job, cluster=self.cluster, verbose=False)
+        if not rj.isSuccessful():
+            raise RuntimeError(f"K-Means Pipes iteration {i} failed: {rj.getFailureInfo()}")
+        new = read_centroids(out, self.centroids)
+        shift = float((new - self.centroids).norm(dim=1).max())
+        self.centroids = new
+        self.history.append({"iteration": i, "shift": shift, "counters": rj.getCounters()})
+        self.iteration += 1
+        return self.history[-1]
+
+    def run(self, iters):
+        for _ in range(iters):
+            self.step()
+        return self.centroids

@@ -6,6 +6,8 @@ Produces (all in-tree so they travel to the GPU box with the repo snapshot):
                                   and native I/O (native/cpu/*.cc), C ABI, loaded
                                   by ``hbmr.ops`` via ctypes next to PyTorch.
 * ``hbmr/lib/libhbmr_pipes.a`` – the Pipes child-side runtime (native/pipes).
+* ``hbmr/lib/libhbmr_host.a``  – host-only objects (native/cpu + native/io:
+                                  CPU K-Means, SequenceFile) for CPU task binaries.
 * ``hbmr/bin/*``               – Pipes task executables (native/apps), e.g. the
                                   HIP K-Means GPU map binary.
 
@@ -73,7 +75,7 @@ def build(verbose: bool = False, jobs: int | None = None) -> dict:
     BINDIR.mkdir(parents=True, exist_ok=True)
     hdrs = _headers(NATIVE)
     hip_srcs = sorted((NATIVE / "kernels").glob("*.hip"))
-    cpu_srcs = sorted((NATIVE / "cpu").glob("*.cc"))
+    cpu_srcs = sorted((NATIVE / "cpu").glob("*.cc")) + sorted((NATIVE / "io").glob("*.cc"))
     pipes_srcs = sorted((NATIVE / "pipes").rglob("*.cc"))
 
     work = []
@@ -92,9 +94,15 @@ def build(verbose: bool = False, jobs: int | None = None) -> dict:
     lib_objs = [objs[s] for s in hip_srcs + cpu_srcs]
     if _stale(lib, lib_objs):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *lib_objs,
-              "-pthread"], verbose)
+              "-pthread", "-lz"], verbose)
+    hostlib = LIBDIR / "libhbmr_host.a"
+    host_objs = [objs[s] for s in cpu_srcs]
+    if _stale(hostlib, host_objs):
+        if hostlib.exists():
+            hostlib.unlink()
+        _run(["ar", "rcs", hostlib, *host_objs], verbose)
 
-    out = {"libhbmr": str(lib)}
+    out = {"libhbmr": str(lib), "libhbmr_host": str(hostlib)}
     if pipes_srcs:
         alib = LIBDIR / "libhbmr_pipes.a"
         pobjs = [objs[s] for s in pipes_srcs]
@@ -103,11 +111,11 @@ def build(verbose: bool = False, jobs: int | None = None) -> dict:
                 alib.unlink()
             _run(["ar", "rcs", alib, *pobjs], verbose)
         out["libhbmr_pipes"] = str(alib)
-        out.update(_build_apps(verbose, lib, alib, hdrs))
+        out.update(_build_apps(verbose, lib, alib, hostlib, hdrs))
     return out
 
 
-def _build_apps(verbose, lib, alib, hdrs):
+def _build_apps(verbose, lib, alib, hostlib, hdrs):
     """Each native/apps/<name>.cc (CPU) or .hip (GPU) becomes hbmr/bin/<name>."""
     apps = {}
     srcs = sorted((NATIVE / "apps").glob("*.cc")) + sorted((NATIVE / "apps").glob("*.hip"))
@@ -115,19 +123,22 @@ def _build_apps(verbose, lib, alib, hdrs):
     cmds = []
     for s in srcs:
         exe = BINDIR / s.stem
-        deps = [s, alib, *hdrs]
+        deps = [s, alib, hostlib, *hdrs]
         if s.suffix == ".hip":
             deps.append(lib)
-            cmd = [HIPCC, *HIP_FLAGS, *inc, s, "-o", exe, alib, f"-L{LIBDIR}", "-lhbmr",
-                   f"-Wl,-rpath,$ORIGIN/../lib", "-pthread"]
+            # compile, then link: hipcc's implicit "-x hip" would apply to the archives
+            obj = BUILD / f"app__{s.stem}.o"
+            cmd = [[HIPCC, *HIP_FLAGS, *inc, "-c", s, "-o", obj],
+                   [HIPCC, f"--offload-arch={ARCH}", obj, "-o", exe, alib, hostlib,
+                    f"-L{LIBDIR}", "-lhbmr", "-Wl,-rpath,$ORIGIN/../lib", "-pthread", "-lz"]]
         else:
-            cmd = [CXX, *CXX_FLAGS, *inc, s, "-o", exe, alib, "-pthread"]
+            cmd = [[CXX, *CXX_FLAGS, *inc, s, "-o", exe, alib, hostlib, "-pthread", "-lz"]]
         apps[s.stem] = str(exe)
         if _stale(exe, deps):
             cmds.append(cmd)
     n = min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=n) as ex:
-        list(ex.map(lambda c: _run(c, verbose), cmds))
+        list(ex.map(lambda cs: [_run(c, verbose) for c in cs], cmds))
     return {"apps": apps}
 
 

@@ -32,7 +32,10 @@ int hbmr_kmeans_map_batch(int ntasks, const void* const* X, const long* n, int d
                           const void* C, const float* chalf, int k_pad, int k, int32_t* labels,
                           void* ws, long ws_bytes, long long* sums, long long* counts,
                           int fx_shift, int zero_outputs, hipStream_t st);
+// fp32 [n, d] row-major → bf16 [n, dp] (round-to-nearest-even, columns d..dp zero)
+int hbmr_f32_to_bf16_pad(const float* src, long n, int d, int dp, void* dst, hipStream_t st);
 #endif
+int hbmr_kmeans_padded_dim(int d);
 int hbmr_kmeans_padded_k(int k);
 long hbmr_kmeans_accum_workspace_bytes(long n, int k);
 long hbmr_kmeans_batch_workspace_bytes(long total_n, int ntasks, int k);

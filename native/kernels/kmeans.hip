@@ -764,6 +764,17 @@ __global__ __launch_bounds__(128) void kmeans_update_kernel(
   }
 }
 
+__global__ __launch_bounds__(256) void f32_to_bf16_pad_kernel(const float* __restrict__ src,
+                                                              long n, int d, int dp,
+                                                              uint16_t* __restrict__ dst) {
+  const long total = n * dp;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const long r = e / dp;
+    const int c = (int)(e - r * dp);
+    dst[e] = c < d ? hbmr_f32_to_bf16(src[r * d + c]) : (uint16_t)0;
+  }
+}
+
 __global__ void kmeans_pad_clusters_kernel(__bf16* cbf, float* chalf, int k, int k_pad, int dp) {
   const int j = k + blockIdx.x;
   if (j >= k_pad) return;
@@ -955,6 +966,22 @@ int hbmr_kmeans_update(const long long* sums, const long long* counts, int fx_sh
 }
 
 int hbmr_kmeans_padded_k(int k) { return ((k + kCK - 1) / kCK) * kCK; }
+
+int hbmr_kmeans_padded_dim(int d) {
+  for (int dp : {64, 128, 256})
+    if (d <= dp) return dp;
+  return -1;
+}
+
+int hbmr_f32_to_bf16_pad(const float* src, long n, int d, int dp, void* dst, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (d > dp) return (int)hipErrorInvalidValue;
+  const long total = n * dp;
+  const long grid = std::min<long>((total + 255) / 256, 1L << 20);
+  hipLaunchKernelGGL(f32_to_bf16_pad_kernel, dim3((unsigned)grid), dim3(256), 0, st, src, n, d,
+                     dp, reinterpret_cast<uint16_t*>(dst));
+  return (int)hipGetLastError();
+}
 
 // A batch of K-Means map tasks (one per split) launched from C++ in one call:
 // assign + combine per split into its own output slab sums[t] / counts[t]
