@@ -1,0 +1,273 @@
+"""TeraGen / TeraSort / TeraValidate — BASELINE config 5, as a split-level job.
+
+Behaviour of the reference's examples (src/examples/org/apache/hadoop/examples/
+terasort): TeraGen writes 100-byte records (10-byte printable key from an LCG,
+10-char row id, 78 filler letters, "\\r\\n"; TeraGen.java), TeraSort samples
+up to 100,000 keys from ≤10 input splits to pick R-1 split points
+(TeraInputFormat.java:101-141, createPartitions :80-99) and range-partitions
+into R sorted part files (TeraSort.java:57-211), TeraValidate checks order
+within and across parts (TeraValidate.java).
+
+MI355X design:
+
+* map (per split, on its GPU slot): records are generated straight into HBM
+  (``teragen:<rows>`` input; the LCG jumps ahead in O(log n), bit-identical to
+  TeraGen) or read from TeraGen files; keys are radix-sorted (10 passes of the
+  native LSD sort), the 100-byte records gathered once, and the splitters
+  cut the sorted split into R runs (offsets only — no per-record partition
+  calls);
+* shuffle: one all-to-all-v per tracker over RCCL/xGMI (each GPU owns a
+  contiguous range of partitions) — the HTTP shuffle + merge of the
+  reference (ReduceTask.java:1231-2514) disappears;
+* reduce (collective, one per tracker): radix-sort the received runs, verify
+  order locally and against the neighbouring ranks' boundary keys
+  (TeraValidate), write ``part-NNNNN`` files if an output directory is set.
+
+CPU slots run the same steps with numpy (hbmr.ops.sort CPU twins).
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import numpy as np
+import torch
+
+from ..gpu.splitjob import SplitJob, SplitSpec
+from ..mapred import counters as C
+from ..ops import sort as S
+
+INPUT_KEY = "hbmr.terasort.input"            # "teragen:<rows>" or a directory of TeraGen files
+SPLIT_ROWS_KEY = "hbmr.terasort.split.rows"
+PARTS_KEY = "hbmr.terasort.partitions"       # R (default: one per tracker)
+SAMPLE_KEY = "terasort.partitions.sample"    # the reference's key (default 100000)
+
+
+def _hex_keys(hi: np.ndarray, lo: np.ndarray) -> list:
+    return [f"{int(h):016x}{int(lo_):04x}" for h, lo_ in zip(hi, lo)]
+
+
+def _parse_keys(hexes: list):
+    hi = np.array([int(h[:16], 16) for h in hexes], dtype=np.uint64)
+    lo = np.array([int(h[16:], 16) for h in hexes], dtype=np.uint64)
+    return torch.from_numpy(hi.view(np.int64)), torch.from_numpy(lo.view(np.int64))
+
+
+def create_partitions(sample_keys: np.ndarray, nparts: int) -> np.ndarray:
+    """TeraInputFormat.createPartitions: sort the sample, take keys at
+    Math.round(stepSize * i), i = 1..R-1 (sample_keys: uint8 [m, 10])."""
+    m = sample_keys.shape[0]
+    if nparts > m:
+        raise ValueError(f"Requested more partitions than input keys ({nparts} > {m})")
+    order = np.lexsort([sample_keys[:, j] for j in range(9, -1, -1)])
+    srt = sample_keys[order]
+    step = np.float32(m) / np.float32(nparts)
+    idx = [int(math.floor(float(np.float32(step * np.float32(i))) + 0.5)) for i in range(1, nparts)]
+    return srt[idx]
+
+
+def _key_words(keys10: np.ndarray):
+    hi = np.zeros(keys10.shape[0], dtype=np.uint64)
+    for j in range(8):
+        hi = (hi << np.uint64(8)) | keys10[:, j].astype(np.uint64)
+    lo = (keys10[:, 8].astype(np.uint64) << np.uint64(8)) | keys10[:, 9].astype(np.uint64)
+    return hi, lo
+
+
+def _s64(x: int) -> int:
+    """Wrap to the signed 64-bit range (checksums are sums mod 2^64)."""
+    return ((x + (1 << 63)) % (1 << 64)) - (1 << 63)
+
+
+def _file_records(path):
+    n = os.path.getsize(path) // S.RECORD
+    return n
+
+
+class TeraSortSplitJob(SplitJob):
+    collective_reduce = True
+    needs_reduce = True
+
+    def configure(self, conf):
+        self.conf = conf
+        self.input = conf.get(INPUT_KEY, "teragen:1000000")
+        self.split_rows = conf.get_long(SPLIT_ROWS_KEY, 10_000_000)
+        self.nparts_conf = conf.get_int(PARTS_KEY, 0)
+        self.sample = conf.get_long(SAMPLE_KEY, 100000)
+        self.out = conf.get("mapred.output.dir")
+
+    # -- splits + sampling (JobTracker side) -----------------------------------------
+    def _ranges(self):
+        """[(kind, params, rows)] covering the input."""
+        if self.input.startswith("teragen:"):
+            rows = int(self.input.split(":")[1])
+            out = []
+            for a in range(0, rows, self.split_rows):
+                n = min(self.split_rows, rows - a)
+                out.append(("teragen", {"first": a, "rows": n}, n))
+            return out
+        files = sorted(os.path.join(self.input, f) for f in os.listdir(self.input)
+                       if not f.startswith(("_", ".")))
+        out = []
+        for f in files:
+            n = _file_records(f)
+            for a in range(0, n, self.split_rows):
+                m = min(self.split_rows, n - a)
+                out.append(("file", {"path": f, "first": a, "rows": m}, m))
+        return out
+
+    def _sample_keys(self, ranges):
+        samples = min(10, len(ranges))
+        if samples == 0:
+            return np.zeros((0, 10), dtype=np.uint8)
+        per = max(1, self.sample // samples)
+        step = len(ranges) // samples
+        keys = []
+        for i in range(samples):
+            kind, p, rows = ranges[step * i]
+            m = min(per, rows)
+            if kind == "teragen":
+                recs = S.teragen_cpu(p["first"], m)
+            else:
+                recs = np.fromfile(p["path"], dtype=np.uint8, count=m * S.RECORD,
+                                   offset=p["first"] * S.RECORD).reshape(m, S.RECORD)
+            keys.append(recs[:, :10])
+        return np.concatenate(keys)
+
+    def get_splits(self, conf, trackers):
+        ranges = self._ranges()
+        nparts = self.nparts_conf or max(1, len(trackers))
+        split_keys = create_partitions(self._sample_keys(ranges), nparts) if nparts > 1 else \
+            np.zeros((0, 10), dtype=np.uint8)
+        hi, lo = _key_words(split_keys)
+        splitters = _hex_keys(hi, lo)
+        out = []
+        for i, (kind, p, rows) in enumerate(ranges):
+            loc = [trackers[i * len(trackers) // len(ranges)]] if trackers else []
+            key = f"tera:{kind}:{p.get('path', '')}:{p['first']}:{rows}"
+            out.append(SplitSpec(i, key, kind, {**p, "splitters": splitters, "nparts": nparts},
+                                 loc, rows * S.RECORD))
+        return out
+
+    # -- map ---------------------------------------------------------------------------
+    def load_split(self, spec: SplitSpec, device):
+        p = spec.params
+        if spec.kind == "teragen":
+            recs = S.teragen(p["first"], p["rows"], device=device)
+        else:
+            a = np.fromfile(p["path"], dtype=np.uint8, count=p["rows"] * S.RECORD,
+                            offset=p["first"] * S.RECORD).reshape(p["rows"], S.RECORD)
+            recs = torch.from_numpy(a).to(device)
+        return {"records": recs, "splitters": p["splitters"], "nparts": p["nparts"]}
+
+    def split_nbytes(self, data):
+        return int(data["records"].numel())
+
+    def _map(self, ctx, data):
+        recs = data["records"]
+        hi, lo = S.tera_keys(recs, stream=getattr(ctx, "stream", None))
+        perm, hs, ls = S.sort_keys(hi, lo)
+        srt = S.gather_records(recs, perm)
+        nparts = data["nparts"]
+        if nparts > 1:
+            shi, slo = _parse_keys(data["splitters"])
+            offs = S.split_offsets(hs, ls, shi.to(hs.device), slo.to(hs.device))
+        else:
+            offs = torch.tensor([0, recs.shape[0]], dtype=torch.int64)
+        # checksum of the input keys (order independent) for end-to-end validation
+        csum = int((hi.sum() + lo.sum()).item()) if recs.shape[0] else 0
+        ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, recs.shape[0])
+        ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_OUTPUT_RECORDS, recs.shape[0])
+        return {"records": srt, "offsets": offs.to("cpu").tolist(), "checksum": csum}
+
+    def map_gpu(self, ctx, data):
+        return self._map(ctx, data)
+
+    def map_cpu(self, ctx, data):
+        return self._map(ctx, data)
+
+    def map_gpu_batch(self, ctxs, datas):
+        return [self._map(c, d) for c, d in zip(ctxs, datas)]
+
+    # -- shuffle + reduce -------------------------------------------------------------
+    @staticmethod
+    def owner_range(rank, world, nparts):
+        return rank * nparts // world, (rank + 1) * nparts // world
+
+    def combine(self, ctx, outputs):
+        dev = ctx.device if ctx.device is not None else torch.device("cpu")
+        W = ctx.world_size
+        nparts = None
+        pieces, counts = [], [0] * W
+        csum = 0
+        for o in outputs:
+            csum += o["checksum"]
+        for d in range(W):
+            for o in outputs:
+                offs = o["offsets"]
+                nparts = len(offs) - 1
+                a, b = self.owner_range(d, W, nparts)
+                lo_, hi_ = offs[a], offs[b]
+                if hi_ > lo_:
+                    pieces.append(o["records"][lo_:hi_].to(dev))
+                    counts[d] += hi_ - lo_
+        send = torch.cat(pieces) if pieces else torch.empty(0, S.RECORD, dtype=torch.uint8,
+                                                            device=dev)
+        return {"send": send, "counts": counts, "checksum": csum, "nparts": nparts}
+
+    def reduce(self, ctx, combined):
+        comm = ctx.comm
+        recv, _ = comm.all_to_all_v(combined["send"], combined["counts"])
+        srt, hs, ls = S.sort_records(recv) if recv.shape[0] else (recv, recv[:0, 0].long(),
+                                                                  recv[:0, 0].long())
+        bad = S.count_unsorted(hs, ls)
+        # boundary check against the neighbours + global record/checksum totals
+        n = int(srt.shape[0])
+        first = (int(hs[0].item()), int(ls[0].item())) if n else (-1, -1)
+        last = (int(hs[-1].item()), int(ls[-1].item())) if n else (-1, -1)
+        csum_here = int(hs.sum().item()) + int(ls.sum().item()) if n else 0
+        meta = torch.tensor([n, _s64(combined["checksum"]), _s64(csum_here), bad, first[0],
+                             first[1], last[0], last[1]], dtype=torch.int64)
+        gathered = comm.all_gather(meta)
+        total = sum(int(g[0]) for g in gathered)
+        csum_in = sum(int(g[1]) for g in gathered)
+        csum_out = sum(int(g[2]) for g in gathered)
+        cross_bad = 0
+        prev_last = None
+        for g in gathered:
+            if int(g[0]) == 0:
+                continue
+            f = (int(g[4]) & 0xFFFFFFFFFFFFFFFF, int(g[5]))
+            if prev_last is not None and f < prev_last:
+                cross_bad += 1
+            prev_last = (int(g[6]) & 0xFFFFFFFFFFFFFFFF, int(g[7]))
+        if self.out:
+            self._write(ctx, srt, hs, ls, combined["nparts"] or 1)
+        return {"records": n, "total_records": total, "unsorted": bad + cross_bad,
+                "checksum_ok": (csum_in - csum_out) % (1 << 64) == 0}
+
+    def _write(self, ctx, srt, hs, ls, nparts):
+        os.makedirs(self.out, exist_ok=True)
+        a, b = self.owner_range(ctx.rank, ctx.world_size, nparts)
+        host = srt.to("cpu").numpy()
+        if b - a <= 1:
+            host.tofile(os.path.join(self.out, f"part-{a:05d}"))
+            return
+        # several partitions on this rank: cut by the job's splitters
+        raise NotImplementedError("more partitions than trackers: set hbmr.terasort.partitions")
+
+
+def terasort_conf(base=None, rows=1_000_000, split_rows=None, output=None, inp=None,
+                  partitions=0):
+    from ..mapred.jobconf import JobConf
+    job = JobConf(base)
+    job.set_job_name(f"TeraSort {inp or rows}")
+    job.set("hbmr.splitjob.class", "hbmr.models.terasort:TeraSortSplitJob")
+    job.set(INPUT_KEY, inp or f"teragen:{rows}")
+    if split_rows:
+        job.set_long(SPLIT_ROWS_KEY, split_rows)
+    if partitions:
+        job.set_int(PARTS_KEY, partitions)
+    if output:
+        job.set("mapred.output.dir", output)
+    return job

@@ -40,6 +40,19 @@ _SIGS = {
     "hbmr_kmeans_padded_k": (c_int, [c_int]),
     "hbmr_kmeans_map_cpu_f32": (c_int, [c_void_p, c_long, c_int, c_void_p, c_int, c_void_p,
                                         c_void_p, c_void_p, c_double_p, c_int, c_int]),
+    "hbmr_kmeans_padded_dim": (c_int, [c_int]),
+    "hbmr_f32_to_bf16_pad": (c_int, [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p]),
+    # sort / shuffle (native/kernels/sort.hip)
+    "hbmr_radix_sort_workspace_bytes": (c_long, [c_long]),
+    "hbmr_radix_sort_pairs_u64": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int,
+                                          c_int, c_void_p, c_long, c_void_p]),
+    "hbmr_teragen": (c_int, [c_long, c_long, c_void_p, c_void_p]),
+    "hbmr_tera_keys": (c_int, [c_void_p, c_long, c_int, c_void_p, c_void_p, c_void_p]),
+    "hbmr_gather_u64": (c_int, [c_void_p, c_void_p, c_long, c_void_p, c_void_p]),
+    "hbmr_gather_records": (c_int, [c_void_p, c_void_p, c_long, c_int, c_void_p, c_void_p]),
+    "hbmr_split_offsets": (c_int, [c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_int,
+                                   c_void_p, c_void_p]),
+    "hbmr_check_sorted": (c_int, [c_void_p, c_void_p, c_long, c_void_p, c_void_p]),
 }
 
 

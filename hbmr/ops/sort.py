@@ -1,0 +1,239 @@
+"""GPU sort / shuffle primitives (native/kernels/sort.hip) and their CPU twins.
+
+* :func:`radix_sort_pairs` — stable LSD radix sort of uint64 keys (held in
+  int64 tensors, compared unsigned) carrying uint32 values.
+* TeraSort record ops: :func:`teragen` (Hadoop 1.0.3 TeraGen records bit for
+  bit, on the device), :func:`tera_keys`, :func:`sort_records`,
+  :func:`gather_records`, :func:`split_offsets`, :func:`count_unsorted`.
+
+CPU versions (numpy) back CPU map slots and the tests' references; on a GPU
+the native library must load (no silent fallback).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+
+RECORD = 100
+KEY = 10
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _on_gpu(t):
+    return t.device.type == "cuda"
+
+
+# --------------------------------------------------------------------------- radix sort
+def radix_sort_pairs(keys: torch.Tensor, vals: torch.Tensor, begin_bit: int = 0,
+                     end_bit: int = 64, stream=None) -> None:
+    """In place: sort ``keys`` (int64 storage of uint64) and permute ``vals`` (int32)
+    by key bits [begin_bit, end_bit).  Stable."""
+    n = keys.numel()
+    if vals.numel() != n or keys.dtype != torch.int64 or vals.dtype != torch.int32:
+        raise ValueError("keys int64[n], vals int32[n] required")
+    if n <= 1:
+        return
+    if not _on_gpu(keys):
+        k = keys.numpy().view(np.uint64)
+        mask = np.uint64(((1 << (end_bit - begin_bit)) - 1) if end_bit - begin_bit < 64
+                         else 0xFFFFFFFFFFFFFFFF)
+        dig = (k >> np.uint64(begin_bit)) & mask
+        order = np.argsort(dig, kind="stable")
+        keys.copy_(torch.from_numpy(k[order].view(np.int64).copy()))
+        vals.copy_(vals[torch.from_numpy(order)])
+        return
+    lib = _lib.load()
+    tk = torch.empty_like(keys)
+    tv = torch.empty_like(vals)
+    wsb = int(lib.hbmr_radix_sort_workspace_bytes(n))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=keys.device)
+    rc = lib.hbmr_radix_sort_pairs_u64(_ptr(keys), _ptr(vals), _ptr(tk), _ptr(tv), n, begin_bit,
+                                       end_bit, _ptr(ws), wsb, _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_radix_sort_pairs_u64")
+
+
+def argsort_u64(keys: torch.Tensor, stream=None):
+    """(sorted keys, int32 permutation) without modifying ``keys``."""
+    k = keys.clone()
+    v = torch.arange(keys.numel(), dtype=torch.int32, device=keys.device)
+    radix_sort_pairs(k, v, stream=stream)
+    return k, v
+
+
+# --------------------------------------------------------------------------- TeraGen
+_A, _C, _M = 3141592621, 663896637, 0xFFFFFFFF
+
+
+def _lcg_jump_np(steps: np.ndarray) -> np.ndarray:
+    """State after ``steps`` LCG iterations from 0 (vectorised affine powering)."""
+    steps = steps.astype(np.uint64)
+    ra = np.ones_like(steps)
+    rc = np.zeros_like(steps)
+    ma = np.uint64(_A)
+    mc = np.uint64(_C)
+    m = np.uint64(_M)
+    s = steps.copy()
+    while s.any():
+        bit = (s & np.uint64(1)).astype(bool)
+        rc = np.where(bit, (ma * rc + mc) & m, rc)
+        ra = np.where(bit, (ma * ra) & m, ra)
+        mc = (ma * mc + mc) & m
+        ma = (ma * ma) & m
+        s >>= np.uint64(1)
+    return rc  # x0 = 0
+
+
+def teragen_cpu(first_row: int, nrows: int) -> np.ndarray:
+    """Reference TeraGen (TeraGen.java RandomGenerator / SortGenMapper) → uint8 [n, 100]."""
+    rows = np.arange(first_row, first_row + nrows, dtype=np.int64)
+    out = np.empty((nrows, RECORD), dtype=np.uint8)
+    s = _lcg_jump_np(rows.astype(np.uint64) * np.uint64(3))
+    kb = np.empty((nrows, 12), dtype=np.uint8)
+    for q in range(3):
+        s = (np.uint64(_A) * s + np.uint64(_C)) & np.uint64(_M)
+        temp = s // np.uint64(52)
+        for pos in (3, 2, 1, 0):
+            kb[:, pos + 4 * q] = (32 + temp % np.uint64(95)).astype(np.uint8)
+            temp = temp // np.uint64(95)
+    out[:, :10] = kb[:, :10]
+    rid = rows.astype(np.int32)   # Java (int) rowId
+    for i in range(nrows):
+        t = str(int(rid[i])).encode()[:10]
+        out[i, 10:20] = np.frombuffer(b" " * (10 - len(t)) + t, dtype=np.uint8)
+    fb = (rows * 8) % 26
+    for q in range(7):
+        out[:, 20 + 10 * q:30 + 10 * q] = (65 + (fb + q) % 26).astype(np.uint8)[:, None]
+    out[:, 90:98] = (65 + (fb + 7) % 26).astype(np.uint8)[:, None]
+    out[:, 98] = 13
+    out[:, 99] = 10
+    return out
+
+
+def teragen(first_row: int, nrows: int, device="cuda", stream=None) -> torch.Tensor:
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        return torch.from_numpy(teragen_cpu(first_row, nrows))
+    out = torch.empty(nrows, RECORD, dtype=torch.uint8, device=dev)
+    rc = _lib.load().hbmr_teragen(first_row, nrows, _ptr(out), _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_teragen")
+    return out
+
+
+# --------------------------------------------------------------------------- records
+def tera_keys(records: torch.Tensor, stream=None):
+    """(hi, lo) int64 tensors: key bytes 0-7 and 8-9 as big-endian unsigned ints."""
+    n, stride = records.shape
+    if _on_gpu(records):
+        hi = torch.empty(n, dtype=torch.int64, device=records.device)
+        lo = torch.empty(n, dtype=torch.int64, device=records.device)
+        rc = _lib.load().hbmr_tera_keys(_ptr(records), n, stride, _ptr(hi), _ptr(lo),
+                                         _lib.stream_handle(stream))
+        _lib.check(rc, "hbmr_tera_keys")
+        return hi, lo
+    r = records.numpy()
+    hi = np.zeros(n, dtype=np.uint64)
+    for j in range(8):
+        hi = (hi << np.uint64(8)) | r[:, j].astype(np.uint64)
+    lo = (r[:, 8].astype(np.uint64) << np.uint64(8)) | r[:, 9].astype(np.uint64)
+    return torch.from_numpy(hi.view(np.int64)), torch.from_numpy(lo.view(np.int64))
+
+
+def gather_records(records: torch.Tensor, perm: torch.Tensor, stream=None) -> torch.Tensor:
+    n, rb = records.shape
+    if not _on_gpu(records):
+        return records[perm.long()]
+    out = torch.empty_like(records)
+    rc = _lib.load().hbmr_gather_records(_ptr(records), _ptr(perm), n, rb, _ptr(out),
+                                          _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_gather_records")
+    return out
+
+
+def sort_keys(hi: torch.Tensor, lo: torch.Tensor, stream=None):
+    """Permutation ordering records by (hi, lo) unsigned; returns (perm, hi_sorted, lo_sorted)."""
+    n = hi.numel()
+    if not _on_gpu(hi):
+        h = hi.numpy().view(np.uint64)
+        lw = lo.numpy().view(np.uint64)
+        order = np.lexsort((lw, h)).astype(np.int32)
+        return (torch.from_numpy(order), torch.from_numpy(h[order].view(np.int64).copy()),
+                torch.from_numpy(lw[order].view(np.int64).copy()))
+    lib = _lib.load()
+    # LSD: 2 passes over the low 16 bits, then 8 over the high 64 (stable)
+    lo_k = lo.clone()
+    perm = torch.arange(n, dtype=torch.int32, device=hi.device)
+    radix_sort_pairs(lo_k, perm, 0, 16, stream=stream)
+    hi_k = torch.empty_like(hi)
+    rc = lib.hbmr_gather_u64(_ptr(hi), _ptr(perm), n, _ptr(hi_k), _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_gather_u64")
+    radix_sort_pairs(hi_k, perm, 0, 64, stream=stream)
+    lo_s = torch.empty_like(lo)
+    rc = lib.hbmr_gather_u64(_ptr(lo), _ptr(perm), n, _ptr(lo_s), _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_gather_u64")
+    return perm, hi_k, lo_s
+
+
+def sort_records(records: torch.Tensor, stream=None):
+    """Sort 100-byte records by their 10-byte key → (sorted records, hi, lo)."""
+    hi, lo = tera_keys(records, stream=stream)
+    perm, hs, ls = sort_keys(hi, lo, stream=stream)
+    return gather_records(records, perm, stream=stream), hs, ls
+
+
+def split_offsets(hi: torch.Tensor, lo: torch.Tensor, split_hi: torch.Tensor,
+                  split_lo: torch.Tensor, stream=None) -> torch.Tensor:
+    """For sorted (hi, lo): offsets[R+1] of the R range partitions defined by the
+    R-1 splitters (partition p holds keys in [split[p-1], split[p]))."""
+    n = hi.numel()
+    nparts = split_hi.numel() + 1
+    if not _on_gpu(hi):
+        h = hi.numpy().view(np.uint64)
+        lw = lo.numpy().view(np.uint64)
+        sh = split_hi.numpy().view(np.uint64)
+        sl = split_lo.numpy().view(np.uint64)
+        out = np.zeros(nparts + 1, dtype=np.int64)
+        out[nparts] = n
+        for p in range(1, nparts):
+            a, b = 0, n
+            while a < b:
+                m = (a + b) // 2
+                if h[m] < sh[p - 1] or (h[m] == sh[p - 1] and lw[m] < sl[p - 1]):
+                    a = m + 1
+                else:
+                    b = m
+            out[p] = a
+        return torch.from_numpy(out)
+    out = torch.empty(nparts + 1, dtype=torch.int64, device=hi.device)
+    rc = _lib.load().hbmr_split_offsets(_ptr(hi), _ptr(lo), n, _ptr(split_hi), _ptr(split_lo),
+                                         nparts, _ptr(out), _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_split_offsets")
+    return out
+
+
+def count_unsorted(hi: torch.Tensor, lo: torch.Tensor, stream=None) -> int:
+    """Number of adjacent out-of-order key pairs (TeraValidate's check)."""
+    n = hi.numel()
+    if n <= 1:
+        return 0
+    if not _on_gpu(hi):
+        h = hi.numpy().view(np.uint64)
+        lw = lo.numpy().view(np.uint64)
+        bad = (h[:-1] > h[1:]) | ((h[:-1] == h[1:]) & (lw[:-1] > lw[1:]))
+        return int(bad.sum())
+    bad = torch.zeros(1, dtype=torch.int64, device=hi.device)
+    rc = _lib.load().hbmr_check_sorted(_ptr(hi), _ptr(lo), n, _ptr(bad),
+                                        _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_check_sorted")
+    return int(bad.item())
+
+
+def keys_from_bytes(keys: list) -> tuple[torch.Tensor, torch.Tensor]:
+    """10-byte keys (bytes) → (hi, lo) int64 tensors (host)."""
+    hi = np.array([int.from_bytes(k[:8].ljust(8, b"\0"), "big") for k in keys], dtype=np.uint64)
+    lo = np.array([int.from_bytes(k[8:10].ljust(2, b"\0"), "big") for k in keys], dtype=np.uint64)
+    return torch.from_numpy(hi.view(np.int64)), torch.from_numpy(lo.view(np.int64))

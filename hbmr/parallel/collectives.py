@@ -42,6 +42,13 @@ class Comm:
     def barrier(self):
         raise NotImplementedError
 
+    def all_to_all_v(self, send: torch.Tensor, counts: list):
+        """Variable all-to-all of one buffer: rows [sum(counts[:j]), +counts[j]) of
+        ``send`` go to rank j.  Returns (recv, recv_counts), recv ordered by source."""
+        outs = list(torch.split(send, [int(c) for c in counts]))
+        ins = self.all_to_all(outs)
+        return (torch.cat(ins) if ins else send[:0]), [int(t.shape[0]) for t in ins]
+
     def reduce_scatter(self, t: torch.Tensor) -> torch.Tensor:
         """Sum over ranks, rank r keeps rows [r*n/W, (r+1)*n/W) (dim 0 padded by caller)."""
         full = self.all_reduce(t)
@@ -160,6 +167,20 @@ class TorchComm(Comm):
     def broadcast(self, t, src=0):
         self.dist.broadcast(t, src, group=self._grp(t))
         return t
+
+    def all_to_all_v(self, send, counts):
+        # one all_to_all_single with split sizes: a single RCCL alltoallv (grouped
+        # point-to-point over the xGMI mesh) instead of per-peer tensors
+        dev = send.device
+        sc = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=dev)
+        rc = torch.empty_like(sc)
+        self.dist.all_to_all_single(rc, sc, group=self._grp(send))
+        rcounts = [int(x) for x in rc.tolist()]
+        recv = torch.empty((sum(rcounts),) + tuple(send.shape[1:]), dtype=send.dtype, device=dev)
+        self.dist.all_to_all_single(recv, send.contiguous(), output_split_sizes=rcounts,
+                                    input_split_sizes=[int(c) for c in counts],
+                                    group=self._grp(send))
+        return recv, rcounts
 
     def barrier(self):
         self.dist.barrier(group=self.cpu_group or self.group)

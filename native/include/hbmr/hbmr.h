@@ -36,6 +36,28 @@ int hbmr_kmeans_map_batch(int ntasks, const void* const* X, const long* n, int d
 int hbmr_f32_to_bf16_pad(const float* src, long n, int d, int dp, void* dst, hipStream_t st);
 #endif
 int hbmr_kmeans_padded_dim(int d);
+
+// ---- sort / shuffle (native/kernels/sort.hip) ----------------------------------
+#ifndef HBMR_NO_HIP_DECLS
+// LSD radix sort of (uint64 key, uint32 value) by key bits [begin_bit, end_bit),
+// stable; keys/vals in and out, tkeys/tvals scratch of the same size.
+int hbmr_radix_sort_pairs_u64(uint64_t* keys, uint32_t* vals, uint64_t* tkeys, uint32_t* tvals,
+                              long n, int begin_bit, int end_bit, void* ws, long ws_bytes,
+                              hipStream_t st);
+// Hadoop TeraGen records [first_row, first_row + nrows) (100 B each)
+int hbmr_teragen(long first_row, long nrows, void* out, hipStream_t st);
+int hbmr_tera_keys(const void* records, long n, int stride, uint64_t* hi, uint64_t* lo,
+                   hipStream_t st);
+int hbmr_gather_u64(const uint64_t* src, const uint32_t* perm, long n, uint64_t* dst,
+                    hipStream_t st);
+int hbmr_gather_records(const void* src, const uint32_t* perm, long n, int record_bytes, void* dst,
+                        hipStream_t st);
+int hbmr_split_offsets(const uint64_t* hi, const uint64_t* lo, long n, const uint64_t* shi,
+                       const uint64_t* slo, int nparts, long* offsets, hipStream_t st);
+int hbmr_check_sorted(const uint64_t* hi, const uint64_t* lo, long n, unsigned long long* bad,
+                      hipStream_t st);
+#endif
+long hbmr_radix_sort_workspace_bytes(long n);
 int hbmr_kmeans_padded_k(int k);
 long hbmr_kmeans_accum_workspace_bytes(long n, int k);
 long hbmr_kmeans_batch_workspace_bytes(long total_n, int ntasks, int k);
