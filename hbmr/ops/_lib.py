@@ -53,6 +53,9 @@ _SIGS = {
     "hbmr_split_offsets": (c_int, [c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_int,
                                    c_void_p, c_void_p]),
     "hbmr_check_sorted": (c_int, [c_void_p, c_void_p, c_long, c_void_p, c_void_p]),
+    # GEMM (native/kernels/gemm.hip)
+    "hbmr_gemm_bf16_tn": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_long, c_long,
+                                  ctypes.c_float, c_int, c_void_p]),
 }
 
 

@@ -1,0 +1,51 @@
+"""bf16 MFMA GEMM (native/kernels/gemm.hip) — the Mars-style matmul map kernel.
+
+:func:`matmul_tn` computes ``alpha · A · Btᵀ`` for bf16 ``A[M, K]`` and
+``Bt[N, K]`` (K-contiguous operands) with fp32 accumulation on the CDNA4
+matrix cores; other shapes are zero-padded to the 256×256×64 tile.  On CPU it
+falls back to a float32 torch matmul (CPU map slots).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+TM, TN, TK = 256, 256, 64
+
+
+def _pad(x: torch.Tensor, rows: int, cols: int) -> torch.Tensor:
+    r, c = x.shape
+    if r == rows and c == cols:
+        return x.contiguous()
+    out = torch.zeros(rows, cols, dtype=x.dtype, device=x.device)
+    out[:r, :c] = x
+    return out
+
+
+def matmul_tn(a: torch.Tensor, bt: torch.Tensor, alpha: float = 1.0,
+              out_dtype=torch.float32, stream=None) -> torch.Tensor:
+    if a.dim() != 2 or bt.dim() != 2 or a.shape[1] != bt.shape[1]:
+        raise ValueError("A[M,K], Bt[N,K] required")
+    M, K = a.shape
+    N = bt.shape[0]
+    if a.device.type != "cuda":
+        c = (a.float() @ bt.float().t()) * alpha
+        return c.to(out_dtype)
+    if a.dtype != torch.bfloat16 or bt.dtype != torch.bfloat16:
+        raise ValueError("bf16 operands required on the GPU")
+    Mp, Np, Kp = -(-M // TM) * TM, -(-N // TN) * TN, -(-K // TK) * TK
+    ap, bp = _pad(a, Mp, Kp), _pad(bt, Np, Kp)
+    if out_dtype not in (torch.float32, torch.bfloat16):
+        raise ValueError("C must be fp32 or bf16")
+    c = torch.empty(Mp, Np, dtype=out_dtype, device=a.device)
+    rc = _lib.load().hbmr_gemm_bf16_tn(ap.data_ptr(), bp.data_ptr(), c.data_ptr(), Mp, Np, Kp,
+                                        float(alpha), int(out_dtype == torch.bfloat16),
+                                        _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_gemm_bf16_tn")
+    return c if (Mp == M and Np == N) else c[:M, :N]
+
+
+def matmul(a: torch.Tensor, b: torch.Tensor, **kw) -> torch.Tensor:
+    """A[M,K] · B[K,N] (transposes B once into the K-contiguous layout)."""
+    return matmul_tn(a, b.t().contiguous(), **kw)

@@ -58,6 +58,14 @@ int hbmr_check_sorted(const uint64_t* hi, const uint64_t* lo, long n, unsigned l
                       hipStream_t st);
 #endif
 long hbmr_radix_sort_workspace_bytes(long n);
+
+// ---- GEMM (native/kernels/gemm.hip) -------------------------------------------
+#ifndef HBMR_NO_HIP_DECLS
+// C[M,N] = alpha · A[M,K] · Bt[N,K]ᵀ (bf16 in, fp32 accumulate; C fp32 or bf16).
+// M, N multiples of 256, K of 64.
+int hbmr_gemm_bf16_tn(const void* A, const void* Bt, void* C, long M, long N, long K, float alpha,
+                      int out_bf16, hipStream_t st);
+#endif
 int hbmr_kmeans_padded_k(int k);
 long hbmr_kmeans_accum_workspace_bytes(long n, int k);
 long hbmr_kmeans_batch_workspace_bytes(long total_n, int ntasks, int k);

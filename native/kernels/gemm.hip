@@ -1,0 +1,158 @@
+// bf16 GEMM on the MFMA matrix cores (the Mars-style
+// matmul map task of BASELINE config 4).
+//
+//   C[M, N] (fp32 or bf16) = A[M, K] · B[K, N],   A row-major, B given as
+//   Bt[N, K] row-major (both operands K-contiguous), fp32 accumulation.
+//
+// Structure (cdna_hip_programming.md §5, CDNA4):
+// * 256×256 output tile per 512-thread workgroup (8 waves as 2 (M) × 4 (N),
+//   each wave 128×64 = 8×4 tiles of v_mfma_f32_16x16x32_bf16);
+// * K-steps of 64: the next step's A and B tiles (2 × 32 KiB) are staged with
+//   global_load_lds (16-B LDS-DMA, no VGPR round trip) into the other half of a
+//   double-buffered 128 KiB LDS image while the current step computes;
+// * LDS rows are 128 B; 16-B chunk c of row r is stored at chunk c ^ (r & 7)
+//   (XOR applied to the DMA's SOURCE address, since the DMA writes lane-linear)
+//   so the 16 rows a ds_read_b128 fragment load touches spread over the banks;
+// * one barrier per K-step; bijective XCD-aware tile order (each XCD's L2
+//   serves neighbouring tiles of the same A row-panel).
+// Shapes must be multiples of the tile (M, N % 256 == 0, K % 64 == 0); the
+// host wrapper (hbmr/ops/gemm.py) pads other shapes.
+#include "common.h"
+#include "../include/hbmr/hbmr.h"
+
+namespace {
+
+constexpr int kBM = 256, kBN = 256, kBK = 64;
+constexpr int kGemmThreads = 512;
+constexpr int kTileBytes = kBM * kBK * 2;            // one operand tile: 32 KiB
+constexpr int kStageBytes = 2 * kTileBytes;          // A + B
+constexpr int kGemmLds = 2 * kStageBytes;            // double buffered: 128 KiB
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+
+// Stage one 256×64 bf16 tile (rows row0.., cols k0..) of a K-contiguous
+// operand into LDS.  512 threads × 4 rounds × 16 B = 32 KiB.
+__device__ __forceinline__ void stage_tile(char* lds, const __bf16* __restrict__ G, long ld,
+                                           long row0, long k0, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int p = i * kGemmThreads + tid;  // 16-B piece index in the tile image
+    const int r = p >> 3, c = p & 7;
+    const int src_c = c ^ (r & 7);
+    const __bf16* g = G + (row0 + r) * ld + k0 + src_c * 8;
+    // each wave's 64 lanes land in one contiguous KiB: base for lane 0 of the wave
+    char* dst = lds + (size_t)(i * kGemmThreads + (tid & ~63)) * 16;
+    __builtin_amdgcn_global_load_lds((const void*)g, (void*)dst, 16, 0, 0);
+  }
+}
+
+template <bool OUT_BF16>
+__global__ __launch_bounds__(kGemmThreads, 1) void gemm_bf16_tn_kernel(
+    const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void* __restrict__ Cv, long M,
+    long N, long K, float alpha) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;  // 2 × 4 waves
+  const long tiles_n = N / kBN;
+  const uint32_t t = hbmr_xcd_remap(blockIdx.x, gridDim.x);
+  const long bm = t / tiles_n, bn = t % tiles_n;
+  const long m0 = bm * kBM, n0 = bn * kBN;
+  const int nk = (int)(K / kBK);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage_tile(smem, A, K, m0, 0, tid);
+  stage_tile(smem + kTileBytes, Bt, K, n0, 0, tid);
+
+  const int fr = lane & 15;    // fragment row (A) / column (B) within a 16-tile
+  const int fq = lane >> 4;    // k-group: elements k = 8 fq .. 8 fq + 7 of a 32-wide k-step
+
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * kStageBytes;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < nk) {
+      char* nxt = smem + ((kt + 1) & 1) * kStageBytes;
+      stage_tile(nxt, A, K, m0, (long)(kt + 1) * kBK, tid);
+      stage_tile(nxt + kTileBytes, Bt, K, n0, (long)(kt + 1) * kBK, tid);
+    }
+    const char* la = cur;
+    const char* lb = cur + kTileBytes;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int c = kk * 4 + fq;  // logical 16-B chunk of the row
+      bf16x8_t a[8], b[4];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = wm * 128 + i * 16 + fr;
+        a[i] = *reinterpret_cast<const bf16x8_t*>(la + r * 128 + ((c ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = wn * 64 + j * 16 + fr;
+        b[j] = *reinterpret_cast<const bf16x8_t*>(lb + r * 128 + ((c ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // C/D map of 16x16x32: col = lane & 15, row = 4 (lane >> 4) + reg
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long col = n0 + wn * 64 + j * 16 + fr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const long row = m0 + wm * 128 + i * 16 + fq * 4 + r;
+        const float v = acc[i][j][r] * alpha;
+        if (OUT_BF16)
+          reinterpret_cast<uint16_t*>(Cv)[row * N + col] = hbmr_f32_to_bf16(v);
+        else
+          reinterpret_cast<float*>(Cv)[row * N + col] = v;
+      }
+    }
+  }
+}
+
+bool g_gemm_lds_set = false;
+
+}  // namespace
+
+extern "C" {
+
+// C = alpha · A · Btᵀ; out_bf16 selects a bf16 C (else fp32).
+int hbmr_gemm_bf16_tn(const void* A, const void* Bt, void* C, long M, long N, long K, float alpha,
+                      int out_bf16, hipStream_t st) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  if (M % kBM || N % kBN || K % kBK) return (int)hipErrorInvalidValue;
+  if (!g_gemm_lds_set) {
+    HBMR_RETURN_IF_ERROR(hipFuncSetAttribute((const void*)gemm_bf16_tn_kernel<false>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLds));
+    HBMR_RETURN_IF_ERROR(hipFuncSetAttribute((const void*)gemm_bf16_tn_kernel<true>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLds));
+    g_gemm_lds_set = true;
+  }
+  const long tiles = (M / kBM) * (N / kBN);
+  if (tiles > 0x7fffffffL) return (int)hipErrorInvalidValue;
+  if (out_bf16)
+    hipLaunchKernelGGL(gemm_bf16_tn_kernel<true>, dim3((unsigned)tiles), dim3(kGemmThreads),
+                       kGemmLds, st, reinterpret_cast<const __bf16*>(A),
+                       reinterpret_cast<const __bf16*>(Bt), C, M, N, K, alpha);
+  else
+    hipLaunchKernelGGL(gemm_bf16_tn_kernel<false>, dim3((unsigned)tiles), dim3(kGemmThreads),
+                       kGemmLds, st, reinterpret_cast<const __bf16*>(A),
+                       reinterpret_cast<const __bf16*>(Bt), C, M, N, K, alpha);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,72 @@
+"""Mars-style matmul map tasks (BASELINE config 4) and the bf16 MFMA GEMM kernel."""
+import pytest
+import torch
+
+from hbmr.mapred.cluster import LocalCluster
+from hbmr.mapred.jobconf import JobConf
+from hbmr.models import matmul as MM
+from hbmr.ops import gemm as G
+
+
+def _ref(m, k, n, seed=1):
+    a = MM.synthetic_matrix(seed, 0, m, k, "cpu").float()
+    b = MM.synthetic_matrix(seed + 1, 0, k, n, "cpu").float()
+    return a @ b
+
+
+def test_synthetic_matrix_panels_are_consistent():
+    full = MM.synthetic_matrix(3, 0, 50, 17, "cpu")
+    assert torch.equal(full[20:35], MM.synthetic_matrix(3, 20, 15, 17, "cpu"))
+    assert full.float().abs().max() <= 1.0 and full.float().std() > 0.4
+
+
+@pytest.mark.parametrize("trackers", [1, 2])
+def test_matmul_job_cpu_checksum(trackers):
+    m, k, n = 1000, 96, 80
+    with LocalCluster(JobConf(), num_trackers=trackers, cpu_slots=2) as cl:
+        rj = cl.submit_job(MM.matmul_conf(m=m, k=k, n=n, split_rows=256))
+        rj.waitForCompletion(120)
+        assert rj.isSuccessful(), rj.getFailureInfo()
+        res = rj._impl.jip.result
+    ref = _ref(m, k, n).double().sum().item()
+    for r in res.values():
+        assert abs(r["checksum"] - ref) < 1e-6 * max(1.0, abs(ref)) + 1e-3
+    assert sum(r["rows"] for r in res.values()) == m
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,k,n", [(256, 64, 256), (512, 192, 768), (1000, 300, 100),
+                                   (2048, 1024, 1536)])
+def test_gemm_kernel_matches_fp32_reference(m, k, n):
+    g = torch.Generator().manual_seed(m + k + n)
+    a = torch.randn(m, k, generator=g).to(torch.bfloat16)
+    bt = torch.randn(n, k, generator=g).to(torch.bfloat16)
+    ref = a.float() @ bt.float().t()
+    c = G.matmul_tn(a.cuda(), bt.cuda()).cpu()
+    assert torch.allclose(c, ref, atol=2e-3 * k ** 0.5, rtol=1e-3), (c - ref).abs().max()
+    cb = G.matmul_tn(a.cuda(), bt.cuda(), out_dtype=torch.bfloat16).cpu().float()
+    assert torch.allclose(cb, ref, atol=0.05 * k ** 0.5, rtol=2e-2)
+
+
+@pytest.mark.gpu
+def test_gemm_layout_identity_with_asymmetric_b():
+    # A = I catches a transposed C write that a symmetric B would hide
+    n = 256
+    a = torch.eye(n, dtype=torch.bfloat16)
+    b = (torch.arange(n * n).reshape(n, n) % 97).to(torch.bfloat16)   # asymmetric
+    c = G.matmul(a.cuda(), b.cuda()).cpu()
+    assert torch.equal(c, b.float())
+
+
+@pytest.mark.gpu
+def test_matmul_job_gpu():
+    m, k, n = 4096, 512, 1024
+    with LocalCluster(JobConf(), num_trackers=1, gpus=[[0]], cpu_slots=0) as cl:
+        rj = cl.submit_job(MM.matmul_conf(m=m, k=k, n=n, split_rows=1024))
+        rj.waitForCompletion(120)
+        assert rj.isSuccessful(), rj.getFailureInfo()
+        res = rj._impl.jip.result[0]
+    ref = _ref(m, k, n).double().sum().item()
+    assert abs(res["checksum"] - ref) < 1e-4 * (abs(ref) + m * n ** 0.5)
+    cs = rj.getCounters()
+    assert cs.get("org.apache.hadoop.mapred.JobInProgress$Counter", "GPU_MAP_TASKS") == 4
