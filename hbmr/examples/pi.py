@@ -1,0 +1,93 @@
+"""PiEstimator: quasi-Monte Carlo estimate of pi
+(src/examples/org/apache/hadoop/examples/PiEstimator.java).
+
+Each map takes (offset, size), walks ``size`` points of the 2-D Halton sequence
+(bases 2 and 3) from index ``offset``, and counts points inside / outside the
+inscribed circle; one reducer sums the counts.  pi ≈ 4 · inside / total.
+The map's inner loop is vectorised over numpy (the reference's Java loop)."""
+from __future__ import annotations
+
+import argparse
+import os
+import tempfile
+from decimal import Decimal
+
+import numpy as np
+
+from ..io import sequencefile as seqf
+from ..io.writable import BooleanWritable, LongWritable
+from ..mapred import FileInputFormat, FileOutputFormat, JobClient, JobConf, Mapper, Reducer
+from ..mapred.formats import SequenceFileInputFormat, SequenceFileOutputFormat
+
+
+def halton(index: np.ndarray, base: int) -> np.ndarray:
+    """Radical inverse of ``index + 1`` in ``base`` (vectorised)."""
+    i = index.astype(np.int64) + 1
+    f = np.ones(i.shape, dtype=np.float64) / base
+    r = np.zeros(i.shape, dtype=np.float64)
+    while np.any(i > 0):
+        r += f * (i % base)
+        i //= base
+        f /= base
+    return r
+
+
+class PiMapper(Mapper):
+    def map(self, key, value, output, reporter):
+        offset, size = key.get(), value.get()
+        inside = 0
+        chunk = 1 << 20
+        for a in range(0, size, chunk):
+            idx = np.arange(offset + a, offset + min(size, a + chunk), dtype=np.int64)
+            x = halton(idx, 2) - 0.5
+            y = halton(idx, 3) - 0.5
+            inside += int(np.count_nonzero(x * x + y * y <= 0.25))
+            reporter.progress()
+        output.collect(BooleanWritable(True), LongWritable(inside))
+        output.collect(BooleanWritable(False), LongWritable(size - inside))
+
+
+class PiReducer(Reducer):
+    def reduce(self, key, values, output, reporter):
+        output.collect(key, LongWritable(sum(v.get() for v in values)))
+
+
+def estimate(maps, samples, conf=None, cluster=None, verbose=False):
+    tmp = tempfile.mkdtemp(prefix="pi-")
+    inp, out = os.path.join(tmp, "in"), os.path.join(tmp, "out")
+    os.makedirs(inp)
+    for i in range(maps):
+        with seqf.Writer(os.path.join(inp, f"part{i}"), LongWritable, LongWritable) as w:
+            w.append(LongWritable(i * samples), LongWritable(samples))
+    job = JobConf(conf)
+    job.set_job_name("PiEstimator")
+    job.set_input_format(SequenceFileInputFormat)
+    job.set_output_format(SequenceFileOutputFormat)
+    job.set_output_key_class(BooleanWritable)
+    job.set_output_value_class(LongWritable)
+    job.set_mapper_class(PiMapper)
+    job.set_reducer_class(PiReducer)
+    job.set_num_reduce_tasks(1)
+    job.set_speculative_execution(False)
+    FileInputFormat.setInputPaths(job, inp)
+    FileOutputFormat.setOutputPath(job, out)
+    JobClient.runJob(job, cluster=cluster, verbose=verbose)
+    counts = {}
+    for fn in os.listdir(out):
+        if fn.startswith("part-"):
+            with seqf.Reader(os.path.join(out, fn)) as r:
+                for k, v in r:
+                    counts[bool(k.get())] = v.get()
+    inside, outside = counts.get(True, 0), counts.get(False, 0)
+    return Decimal(4) * Decimal(inside) / Decimal(inside + outside)
+
+
+def main(argv=None, cluster=None):
+    ap = argparse.ArgumentParser(prog="hbmr pi")
+    ap.add_argument("maps", type=int)
+    ap.add_argument("samples", type=int)
+    a = ap.parse_args(argv)
+    print(f"Number of Maps  = {a.maps}\nSamples per Map = {a.samples}")
+    pi = estimate(a.maps, a.samples, cluster=cluster, verbose=True)
+    print(f"Estimated value of Pi is {pi}")
+    return 0

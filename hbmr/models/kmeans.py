@@ -454,3 +454,36 @@ class KMeansDriver:
 
     def centroids(self):
         return STORE.host_centroids(self.key(self.iteration))
+
+
+def main(argv=None, cluster=None):
+    """``hbmr examples kmeans --points N --k K --dims D --iters I``."""
+    import argparse
+    ap = argparse.ArgumentParser(prog="hbmr kmeans")
+    ap.add_argument("--input", default=None, help="SequenceFile dir (default: synthetic)")
+    ap.add_argument("--points", type=int, default=1_000_000)
+    ap.add_argument("--k", type=int, default=64)
+    ap.add_argument("--dims", type=int, default=128)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--split-points", type=int, default=500_000)
+    ap.add_argument("--seed", type=int, default=7)
+    a = ap.parse_args(argv)
+    from ..mapred.cluster import LocalCluster
+    from ..mapred.jobconf import JobConf
+    own = cluster is None
+    conf = JobConf()
+    if own:
+        gpus = [[0]] if torch.cuda.is_available() else None
+        cluster = LocalCluster(conf, num_trackers=1, gpus=gpus)
+    try:
+        drv = KMeansDriver(cluster.submit_job, lambda rj: rj._impl.jip.result[0], conf=conf,
+                           k=a.k, d=a.dims, inp=a.input or f"synthetic:{a.points}:{a.seed}",
+                           split_points=a.split_points)
+        for _ in range(a.iters):
+            r = drv.step()
+            print(f"iteration {r['iteration']}: shift {r['shift']:.6f} "
+                  f"({r['seconds'] * 1e3:.1f} ms)")
+        return 0
+    finally:
+        if own:
+            cluster.shutdown()

@@ -145,3 +145,23 @@ class KMeansPipesDriver:
         for _ in range(iters):
             self.step()
         return self.centroids
+
+
+def main(argv=None, cluster=None):
+    """``hbmr examples kmeans-pipes <points-dir> <workdir> --k K --dims D --iters I``."""
+    import argparse
+    ap = argparse.ArgumentParser(prog="hbmr kmeans-pipes")
+    ap.add_argument("input")
+    ap.add_argument("workdir")
+    ap.add_argument("--k", type=int, default=64)
+    ap.add_argument("--dims", type=int, default=128)
+    ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--reduces", type=int, default=1)
+    a = ap.parse_args(argv)
+    init = K.initial_centroids(a.input, a.k, a.dims)
+    drv = KMeansPipesDriver(a.workdir, a.input, a.k, a.dims, init, cluster=cluster,
+                            reduces=a.reduces)
+    for _ in range(a.iters):
+        r = drv.step()
+        print(f"iteration {r['iteration']}: shift {r['shift']:.6f}")
+    return 0

@@ -162,3 +162,30 @@ def matmul_conf(base=None, m=8192, k=8192, n=8192, split_rows=8192, seed=1, outp
     if output:
         job.set("mapred.output.dir", output)
     return job
+
+
+def main(argv=None, cluster=None):
+    """``hbmr examples matmul --m M --k K --n N --split-rows R``."""
+    import argparse
+    ap = argparse.ArgumentParser(prog="hbmr matmul")
+    ap.add_argument("--m", type=int, default=8192)
+    ap.add_argument("--k", type=int, default=8192)
+    ap.add_argument("--n", type=int, default=8192)
+    ap.add_argument("--split-rows", type=int, default=2048)
+    ap.add_argument("--output", default=None)
+    a = ap.parse_args(argv)
+    from ..mapred.cluster import LocalCluster
+    from ..mapred.jobconf import JobConf
+    own = cluster is None
+    if own:
+        gpus = [[0]] if torch.cuda.is_available() else None
+        cluster = LocalCluster(JobConf(), num_trackers=1, gpus=gpus)
+    try:
+        rj = cluster.submit_job(matmul_conf(m=a.m, k=a.k, n=a.n, split_rows=a.split_rows,
+                                            output=a.output))
+        rj.waitForCompletion()
+        print(rj._impl.jip.result)
+        return 0 if rj.isSuccessful() else 1
+    finally:
+        if own:
+            cluster.shutdown()

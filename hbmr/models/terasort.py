@@ -271,3 +271,150 @@ def terasort_conf(base=None, rows=1_000_000, split_rows=None, output=None, inp=N
     if output:
         job.set("mapred.output.dir", output)
     return job
+
+
+# --------------------------------------------------------------------------- TeraGen job
+class TeraGenSplitJob(SplitJob):
+    """Map-only TeraGen: each map writes ``part-NNNNN`` with its rows (generated
+    on its GPU, or with the CPU twin on CPU slots) — TeraGen.java's output."""
+
+    collective_reduce = True
+    needs_reduce = False
+
+    def configure(self, conf):
+        self.conf = conf
+        self.rows = conf.get_long("terasort.num-rows", 1000)
+        self.split_rows = conf.get_long(SPLIT_ROWS_KEY, 10_000_000)
+        self.out = conf.get("mapred.output.dir")
+
+    def get_splits(self, conf, trackers):
+        out = []
+        nsplit = max(1, -(-self.rows // self.split_rows))
+        for i in range(nsplit):
+            a = i * self.split_rows
+            n = min(self.split_rows, self.rows - a)
+            loc = [trackers[i * len(trackers) // nsplit]] if trackers else []
+            out.append(SplitSpec(i, f"teragen-out:{a}:{n}", "teragen", {"first": a, "rows": n},
+                                 loc, n * S.RECORD))
+        return out
+
+    def load_split(self, spec, device):
+        return spec
+
+    def split_nbytes(self, data):
+        return 0
+
+    def _map(self, ctx, spec):
+        p = spec.params
+        dev = ctx.device if ctx.device is not None else "cpu"
+        recs = S.teragen(p["first"], p["rows"], device=dev)
+        os.makedirs(self.out, exist_ok=True)
+        recs.to("cpu").numpy().tofile(os.path.join(self.out, f"part-{spec.index:05d}"))
+        ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_OUTPUT_RECORDS, p["rows"])
+        return p["rows"]
+
+    def map_gpu(self, ctx, data):
+        return self._map(ctx, data)
+
+    def map_cpu(self, ctx, data):
+        return self._map(ctx, data)
+
+    def map_gpu_batch(self, ctxs, datas):
+        return [self._map(c, d) for c, d in zip(ctxs, datas)]
+
+
+def teragen_conf(base=None, rows=1000, output=None, split_rows=None):
+    from ..mapred.jobconf import JobConf
+    job = JobConf(base)
+    job.set_job_name(f"TeraGen {rows}")
+    job.set("hbmr.splitjob.class", "hbmr.models.terasort:TeraGenSplitJob")
+    job.set_long("terasort.num-rows", rows)
+    if split_rows:
+        job.set_long(SPLIT_ROWS_KEY, split_rows)
+    job.set("mapred.output.dir", output)
+    return job
+
+
+def teravalidate(path) -> dict:
+    """TeraValidate over the part files of ``path`` in name order: records out of
+    order within a file or across file boundaries, total records and an
+    order-independent key checksum (sum of the 10-byte keys mod 2^64)."""
+    files = sorted(f for f in os.listdir(path) if f.startswith("part-"))
+    bad = 0
+    total = 0
+    csum = 0
+    prev_last = None
+    for fn in files:
+        recs = np.fromfile(os.path.join(path, fn), dtype=np.uint8)
+        if recs.size % S.RECORD:
+            raise ValueError(f"{fn}: not a whole number of 100-byte records")
+        recs = recs.reshape(-1, S.RECORD)
+        if not recs.shape[0]:
+            continue
+        hi, lo = _key_words(recs[:, :10])
+        h = torch.from_numpy(hi.view(np.int64))
+        lw = torch.from_numpy(lo.view(np.int64))
+        bad += S.count_unsorted(h, lw)
+        first = (int(hi[0]), int(lo[0]))
+        if prev_last is not None and first < prev_last:
+            bad += 1
+        prev_last = (int(hi[-1]), int(lo[-1]))
+        total += recs.shape[0]
+        csum = (csum + int(hi.sum(dtype=np.uint64)) + int(lo.sum(dtype=np.uint64))) % (1 << 64)
+    return {"files": len(files), "records": total, "misordered": bad, "checksum": csum}
+
+
+def _cli_cluster(cluster):
+    if cluster is not None:
+        return cluster, False
+    from ..mapred.cluster import LocalCluster
+    from ..mapred.jobconf import JobConf
+    gpus = [[0]] if torch.cuda.is_available() else None
+    return LocalCluster(JobConf(), num_trackers=1, gpus=gpus), True
+
+
+def main_teragen(argv=None, cluster=None):
+    import argparse
+    ap = argparse.ArgumentParser(prog="hbmr teragen")
+    ap.add_argument("rows", type=int)
+    ap.add_argument("output")
+    ap.add_argument("--split-rows", type=int, default=10_000_000)
+    a = ap.parse_args(argv)
+    cl, own = _cli_cluster(cluster)
+    try:
+        rj = cl.submit_job(teragen_conf(rows=a.rows, output=a.output, split_rows=a.split_rows))
+        rj.waitForCompletion()
+        return 0 if rj.isSuccessful() else 1
+    finally:
+        if own:
+            cl.shutdown()
+
+
+def main_terasort(argv=None, cluster=None):
+    import argparse
+    ap = argparse.ArgumentParser(prog="hbmr terasort")
+    ap.add_argument("input", help="directory of TeraGen files, or teragen:<rows>")
+    ap.add_argument("output")
+    ap.add_argument("--split-rows", type=int, default=10_000_000)
+    a = ap.parse_args(argv)
+    cl, own = _cli_cluster(cluster)
+    try:
+        inp = a.input if a.input.startswith("teragen:") else os.path.abspath(a.input)
+        rj = cl.submit_job(terasort_conf(inp=inp, output=a.output, split_rows=a.split_rows))
+        rj.waitForCompletion()
+        if rj.isSuccessful():
+            print(rj._impl.jip.result)
+        return 0 if rj.isSuccessful() else 1
+    finally:
+        if own:
+            cl.shutdown()
+
+
+def main_teravalidate(argv=None, cluster=None):
+    import argparse
+    ap = argparse.ArgumentParser(prog="hbmr teravalidate")
+    ap.add_argument("output")
+    a = ap.parse_args(argv)
+    r = teravalidate(a.output)
+    print(r)
+    return 0 if r["misordered"] == 0 else 1
