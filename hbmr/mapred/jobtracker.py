@@ -30,6 +30,7 @@ from .counters import Counters
 from .ids import JobID, TaskAttemptID, TaskID
 from .jobclient import FAILED, KILLED, PREP, RUNNING, SUCCEEDED, JobStatus, RunningJob
 from .scheduler.costmodel import CostModel
+from ..utils.metrics import METRICS
 from ..utils.trace import TRACE
 
 log = logging.getLogger("hbmr.jobtracker")
@@ -384,7 +385,22 @@ class JobTracker:
         self._stop = threading.Event()
         self.listeners = []
         self.start_time = time.time()
+        METRICS.register_gauges(self._gauges)
 
+    def _gauges(self):
+        """Sampled at scrape time (JobTrackerMetricsSource's gauges)."""
+        with self.lock:
+            trs = list(self.trackers.values())
+            yield "hbmr_trackers", {}, len(trs)
+            yield "hbmr_trackers_blacklisted", {}, sum(1 for t in trs if t.blacklisted)
+            yield "hbmr_running_maps", {"where": "cpu"}, sum(t.running_cpu for t in trs)
+            yield "hbmr_running_maps", {"where": "gpu"}, sum(sum(t.running_gpu.values())
+                                                             for t in trs)
+            yield "hbmr_running_reduces", {}, sum(t.running_reduce for t in trs)
+            yield "hbmr_cpu_map_slots", {}, sum(t.status.max_cpu_map_slots for t in trs)
+            yield "hbmr_gpu_slots", {}, sum(g["max_slots"] for t in trs for g in t.status.gpus)
+            yield "hbmr_jobs_running", {}, len(self.job_queue)
+            yield "hbmr_hbm_resident_splits", {}, sum(len(t.cached) for t in trs)
     # -- trackers -------------------------------------------------------------------
     def tracker_names(self):
         with self.lock:
@@ -449,6 +465,7 @@ class JobTracker:
     def submit_job(self, conf) -> RunningJob:
         if TRACE.on:
             TRACE.instant("jt.submit")
+        METRICS.inc("hbmr_jobs_submitted_total", help="jobs submitted")
         jid = self.new_job_id()
         jip = JobInProgress(self, jid, conf)
         with self.lock:
@@ -503,6 +520,15 @@ class JobTracker:
                 log.exception("job_succeeded hook failed")
         if TRACE.on:
             TRACE.instant("jt.job_finished", job=str(jip.job_id), state=state)
+        METRICS.inc("hbmr_jobs_completed_total", help="jobs finished, by final state",
+                    state=state)
+        hdir = _history_dir(self.conf) or _history_dir(jip.conf)
+        if hdir:
+            try:
+                from ..webui.history import write_job_history
+                jip.history_file = write_job_history(jip, hdir)
+            except Exception:  # noqa: BLE001
+                log.exception("writing job history failed")
         jip.done.set()
         for cb in self.listeners:
             cb("finished", jip)
@@ -685,6 +711,8 @@ class JobTracker:
         self.history.log("TASK_FINISHED", attempt=a.aid, tracker=a.tracker,
                          gpu=a.run_on_gpu, device=a.device, start=a.start, finish=a.finish,
                          device_time=a.device_time)
+        METRICS.inc("hbmr_tasks_succeeded_total", help="successful task attempts",
+                    type="map" if tip.is_map else "reduce", where="gpu" if a.run_on_gpu else "cpu")
         if tip.is_map and jip.maps_complete():
             jip.t_maps_done = time.time()
         self._check_job_done(jip)
@@ -704,6 +732,8 @@ class JobTracker:
                                           time.time(), succeeded=False)
         self.history.log("TASK_FAILED" if not killed else "TASK_KILLED", attempt=a.aid,
                          tracker=a.tracker, gpu=a.run_on_gpu, diag=diag[:500])
+        METRICS.inc("hbmr_tasks_failed_total", help="failed or killed task attempts",
+                    state="killed" if killed else "failed", where="gpu" if a.run_on_gpu else "cpu")
         if tip.commit_granted == a.aid:
             tip.commit_granted = None
         if jip.completed() or tip.successful is not None:
@@ -781,6 +811,8 @@ class JobTracker:
             tr.jobs_seen.add(str(jip.job_id))
         self.history.log("TASK_LAUNCHED", attempt=a.aid, tracker=tr.name, gpu=on_gpu,
                          device=device, speculative=speculative)
+        METRICS.inc("hbmr_tasks_launched_total", help="task attempts launched",
+                    type="map" if tip.is_map else "reduce", where="gpu" if on_gpu else "cpu")
         return P.launch_action(spec)
 
     def reduce_inputs(self, jip: JobInProgress, tracker_name=None):
@@ -814,6 +846,31 @@ class JobTracker:
     def rpc_job_result(self, jid):
         return self.jobs[str(jid)].result
 
+    def rpc_list_jobs(self, all_jobs=False):
+        """JobSubmissionProtocol.jobsToComplete / getAllJobs."""
+        with self.lock:
+            out = []
+            for jid, jip in self.jobs.items():
+                st = jip.status
+                if all_jobs or not jip.completed():
+                    out.append({"id": jid, "name": jip.conf.get_job_name(), "state": st.state,
+                                "user": jip.conf.get_user(), "start": jip.submit_time,
+                                "maps": len(jip.maps), "reduces": len(jip.reduces),
+                                "map_progress": st.map_progress,
+                                "reduce_progress": st.reduce_progress,
+                                "cpu_maps": jip.finished_cpu_maps,
+                                "gpu_maps": jip.finished_gpu_maps})
+            return out
+
+    def rpc_task_reports(self, jid, is_map=True):
+        jip = self.jobs[str(jid)]
+        with self.lock:
+            return [{"task": str(r.getTaskID()), "state": r.state, "progress": r.progress,
+                     "start": r.getStartTime(), "finish": r.getFinishTime(),
+                     "gpu": r.getRunOnGPU(), "device": r.getGPUDeviceId(),
+                     "tracker": getattr(r, "tracker", None)}
+                    for r in (t.report() for t in (jip.maps if is_map else jip.reduces))]
+
     def rpc_cluster_status(self):
         with self.lock:
             return {"trackers": {n: {"cpu_slots": t.status.max_cpu_map_slots,
@@ -838,3 +895,7 @@ class JobTracker:
 def job_result(rj: RunningJob):
     impl = rj._impl
     return getattr(impl, "result", None)
+
+
+def _history_dir(conf):
+    return conf.get("hbmr.history.dir") or conf.get("hadoop.job.history.location")

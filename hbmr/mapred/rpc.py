@@ -139,7 +139,7 @@ class RpcClient:
 
 
 JT_METHODS = ("heartbeat", "wakeup", "rpc_submit_job", "rpc_job_status", "rpc_kill_job",
-              "rpc_job_result", "rpc_cluster_status")
+              "rpc_job_result", "rpc_cluster_status", "rpc_list_jobs", "rpc_task_reports")
 
 
 class JobTrackerProxy:

@@ -1,0 +1,154 @@
+"""Job history files, their summary, and rule-based diagnosis.
+
+* :func:`write_job_history` — at job completion the JobTracker writes
+  ``<history dir>/<jobid>.jsonl``: a JOB line, then one line per task attempt
+  with its placement (CPU/GPU + device — which the fork's JobHistory never
+  recorded), times, device time and counters
+  (hadoop-1.0.3 JobHistory.java:94, 1485; keys ``hadoop.job.history.location``
+  / ``hbmr.history.dir``).
+* :func:`summarize_history` — the Rumen-style digest of one file: makespan,
+  phase times, CPU vs GPU map counts and mean times, per-tracker load.
+* :func:`diagnose` — Vaidya-style rules over the digest (contrib/vaidya):
+  CPU stragglers extending the makespan, idle GPU capacity, map-time skew,
+  failed attempts, slow reduce tail.
+"""
+from __future__ import annotations
+
+import json
+import os
+import statistics
+
+
+def history_dir(conf):
+    return conf.get("hbmr.history.dir") or conf.get("hadoop.job.history.location")
+
+
+def job_record(jip) -> dict:
+    st = jip.status
+    return {"type": "JOB", "job": str(jip.job_id), "name": jip.conf.get_job_name(),
+            "user": jip.conf.get_user(), "state": st.state, "submit": jip.submit_time,
+            "launch": jip.launch_time, "finish": st.finish_time,
+            "maps": len(jip.maps), "reduces": len(jip.reduces),
+            "cpu_maps": jip.finished_cpu_maps, "gpu_maps": jip.finished_gpu_maps,
+            "failure": st.failure_info, "timeline": jip.timeline(),
+            "counters": jip.counters.to_dict()}
+
+
+def attempt_records(jip):
+    for tip in list(jip.maps) + list(jip.reduces):
+        for a in list(tip.attempts.values()):
+            yield {"type": "MAP" if tip.is_map else "REDUCE", "task": str(tip.tid),
+                   "attempt": a.aid, "state": a.state, "tracker": a.tracker,
+                   "gpu": bool(a.run_on_gpu), "device": a.device, "start": a.start,
+                   "finish": a.finish, "device_time": a.device_time,
+                   "speculative": bool(a.speculative), "successful": tip.successful is a,
+                   "diagnostic": (a.diagnostic or "")[:500]}
+
+
+def write_job_history(jip, directory) -> str:
+    os.makedirs(directory, exist_ok=True)
+    path = os.path.join(directory, f"{jip.job_id}.jsonl")
+    with open(path, "w") as f:
+        f.write(json.dumps(job_record(jip), default=str) + "\n")
+        for rec in attempt_records(jip):
+            f.write(json.dumps(rec, default=str) + "\n")
+    return path
+
+
+def load_history(path):
+    job, attempts = None, []
+    with open(path) as f:
+        for line in f:
+            rec = json.loads(line)
+            if rec.get("type") == "JOB":
+                job = rec
+            else:
+                attempts.append(rec)
+    return job, attempts
+
+
+def _stats(xs):
+    if not xs:
+        return None
+    return {"n": len(xs), "mean": statistics.fmean(xs), "min": min(xs), "max": max(xs),
+            "p50": statistics.median(xs)}
+
+
+def summarize_history(path_or_records) -> dict:
+    if isinstance(path_or_records, str):
+        job, attempts = load_history(path_or_records)
+    else:
+        job, attempts = path_or_records
+    ok = [a for a in attempts if a["successful"]]
+    maps = [a for a in ok if a["type"] == "MAP"]
+
+    def dur(a):
+        return (a["finish"] or a["start"]) - a["start"]
+    cpu = [dur(a) for a in maps if not a["gpu"]]
+    gpu = [a["device_time"] or dur(a) for a in maps if a["gpu"]]
+    reds = [dur(a) for a in ok if a["type"] == "REDUCE"]
+    per_tracker: dict = {}
+    for a in ok:
+        t = per_tracker.setdefault(a["tracker"], {"maps_cpu": 0, "maps_gpu": 0, "reduces": 0})
+        if a["type"] == "REDUCE":
+            t["reduces"] += 1
+        else:
+            t["maps_gpu" if a["gpu"] else "maps_cpu"] += 1
+    failed = [a for a in attempts if a["state"] in ("FAILED", "FAILED_UNCLEAN")]
+    killed = [a for a in attempts if a["state"] == "KILLED"]
+    last_map = max((a["finish"] for a in maps), default=None)
+    return {"job": job["job"] if job else None, "name": job and job["name"],
+            "state": job and job["state"],
+            "makespan": (job["finish"] - job["submit"]) if job and job["finish"] else None,
+            "timeline": job and job.get("timeline"),
+            "maps": len(maps), "cpu_map_time": _stats(cpu), "gpu_map_time": _stats(gpu),
+            "reduce_time": _stats(reds), "failed_attempts": len(failed),
+            "killed_attempts": len(killed),
+            "speculative_attempts": sum(1 for a in attempts if a["speculative"]),
+            "last_map_finish": last_map, "per_tracker": per_tracker,
+            "diagnosis": diagnose(job, attempts)}
+
+
+def diagnose(job, attempts) -> list:
+    """Rule-based findings, most important first."""
+    out = []
+    ok = [a for a in attempts if a["successful"] and a["type"] == "MAP"]
+    if not ok:
+        return out
+    cpu = [a for a in ok if not a["gpu"]]
+    gpu = [a for a in ok if a["gpu"]]
+    end = max(a["finish"] for a in ok)
+    if cpu and gpu:
+        t_cpu = statistics.fmean(a["finish"] - a["start"] for a in cpu)
+        t_gpu = statistics.fmean((a["device_time"] or (a["finish"] - a["start"])) for a in gpu)
+        accel = t_cpu / max(t_gpu, 1e-9)
+        gpu_end = max(a["finish"] for a in gpu)
+        if max(a["finish"] for a in cpu) > gpu_end and accel > 1.5:
+            tail = max(a["finish"] for a in cpu) - gpu_end
+            out.append({"rule": "cpu-straggler", "severity": "high",
+                        "text": f"CPU map tasks ran {accel:.1f}x slower than GPU tasks and "
+                                f"finished {tail:.3f}s after the last GPU task; with the "
+                                f"hybrid policy the min-makespan split would leave them on GPU"})
+        out.append({"rule": "acceleration", "severity": "info",
+                    "text": f"GPU acceleration factor {accel:.1f}x "
+                            f"({len(gpu)} GPU / {len(cpu)} CPU map tasks)"})
+    durs = [a["finish"] - a["start"] for a in ok]
+    if len(durs) >= 8:
+        med = statistics.median(durs)
+        slow = [d for d in durs if d > 3 * med and d - med > 0.05]
+        if slow:
+            out.append({"rule": "map-skew", "severity": "medium",
+                        "text": f"{len(slow)} map tasks took >3x the median "
+                                f"({med:.3f}s): check input split sizes"})
+    fails = [a for a in attempts if a["state"] in ("FAILED", "FAILED_UNCLEAN")]
+    if fails:
+        out.append({"rule": "failures", "severity": "high",
+                    "text": f"{len(fails)} failed attempts, e.g. {fails[0]['diagnostic'][:160]}"})
+    reds = [a for a in attempts if a["successful"] and a["type"] == "REDUCE"]
+    if job and job.get("finish") and reds:
+        tail = job["finish"] - end
+        span = job["finish"] - job["submit"]
+        if span > 0 and tail / span > 0.5:
+            out.append({"rule": "reduce-tail", "severity": "medium",
+                        "text": f"reduce phase is {100 * tail / span:.0f}% of the makespan"})
+    return out
