@@ -94,6 +94,8 @@ class LocalJobRunner:
         committer_cls = job.get_output_committer()
         committer = committer_cls() if isinstance(committer_cls, type) else committer_cls
         try:
+            from ..filecache import TrackerCacheManager
+            TrackerCacheManager(local_root).localize(str(st.job_id), job)
             informat = new_instance(job.get_input_format(), job)
             outfmt = new_instance(job.get_output_format(), job)
             outfmt.checkOutputSpecs(None, job)

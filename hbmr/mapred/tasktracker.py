@@ -133,6 +133,10 @@ class TaskTracker:
         self._rng = random.Random(rank * 7919 + 17)
         from ..gpu.split_cache import SplitCache
         self.split_cache = SplitCache()
+        from ..filecache import TrackerCacheManager
+        self.cache_manager = TrackerCacheManager(
+            local_dir or os.path.join(conf.get("mapred.local.dir", "/tmp/hbmr-local"),
+                                      self.name))
         if comm is None:
             from ..parallel.collectives import SoloComm
             comm = SoloComm()
@@ -316,10 +320,12 @@ class TaskTracker:
     def _job(self, spec: P.TaskSpec) -> JobState:
         js = self.jobs.get(spec.job_id)
         if js is None:
-            conf = JobConf(load_defaults=False) if False else JobConf()
+            conf = JobConf()
             if spec.conf:
                 for k, v in spec.conf.items():
                     conf.set(k, v)
+            # DistributedCache: localize the job's side files once per tracker
+            self.cache_manager.localize(spec.job_id, conf)
             js = JobState(spec.job_id, conf)
             self.jobs[spec.job_id] = js
         return js
