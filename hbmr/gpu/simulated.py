@@ -184,10 +184,9 @@ class SimulatedGpuRuntime:
             slot, runs, outs = item
             if TRACE.on:
                 TRACE.instant("gpu.complete", n=len(runs))
-            js = runs[0].job
-            with js.lock:
-                for r, out in zip(runs, outs):
-                    js.map_outputs[r.spec.attempt_id] = out
+            for r, out in zip(runs, outs):   # a batch may mix jobs
+                with r.job.lock:
+                    r.job.map_outputs[r.spec.attempt_id] = out
             for r in runs:
                 tracker._finish(r, P.SUCCEEDED, output={"tracker": tracker.name, "where": "simgpu"},
                                 device_time=self.task_s, wake=False)

@@ -113,7 +113,8 @@ class HybridTaskScheduler(TaskScheduler):
             g["device"], 0) for g in tr.status.gpus}
         budget = self.max_maps_per_hb
         tr.more = False
-        for jip in sorted(jt.job_queue, key=lambda j: (_prio(j.priority), j.submit_time)):
+        self.begin_round(tr, total_cpu, total_gpu)
+        for jip in self.job_order(tr):
             if jip.completed():
                 continue
             # ---- reduces
@@ -125,7 +126,8 @@ class HybridTaskScheduler(TaskScheduler):
                     if jip.collective_reduce:
                         if tip.pinned_tracker != tr.name:
                             continue
-                    elif reduce_free <= 0 or n_red >= self.max_reduces_per_hb:
+                    elif reduce_free <= 0 or n_red >= self.max_reduces_per_hb or \
+                            n_red >= self.job_limit(jip, "reduce"):
                         break
                     extra = {"map_outputs": jt.reduce_inputs(jip, tr.name)}
                     actions.append(jt.launch(tr, tip, extra=extra))
@@ -135,8 +137,9 @@ class HybridTaskScheduler(TaskScheduler):
                 continue
             # ---- GPU maps
             if jip.gpu_capable:
+                glim = self.job_limit(jip, "gpu")
                 for dev in sorted(gpu_free):
-                    while gpu_free[dev] > 0 and jip.pending_maps:
+                    while gpu_free[dev] > 0 and jip.pending_maps and glim > 0:
                         if budget <= 0:
                             tr.more = True
                             break
@@ -158,10 +161,12 @@ class HybridTaskScheduler(TaskScheduler):
                         actions.append(jt.launch(tr, tip, on_gpu=True, device=dev))
                         gpu_free[dev] -= 1
                         budget -= 1
+                        glim -= 1
                         self.decisions += 1
             # ---- CPU maps
             if cpu_free > 0 and jip.pending_maps:
-                allowed = self._cpu_allowed(jip, total_cpu, total_gpu, now)
+                allowed = min(self._cpu_allowed(jip, total_cpu, total_gpu, now),
+                              self.job_limit(jip, "cpu"))
                 while cpu_free > 0 and allowed > 0 and jip.pending_maps:
                     if budget <= 0:
                         tr.more = True
@@ -186,6 +191,17 @@ class HybridTaskScheduler(TaskScheduler):
                     actions.append(jt.launch(tr, tip, on_gpu=True, device=dev, speculative=True))
                     gpu_free[dev] -= 1
         return actions
+
+    # -- policy hooks (FIFO by priority here; fair/capacity override) --------------------
+    def begin_round(self, tr, total_cpu, total_gpu):
+        pass
+
+    def job_order(self, tr):
+        return sorted(self.jt.job_queue, key=lambda j: (_prio(j.priority), j.submit_time))
+
+    def job_limit(self, jip, kind) -> int:
+        """Most new tasks of ``kind`` (gpu/cpu/reduce) this job may take now."""
+        return 1 << 30
 
     def _straggler(self, jip, now):
         """A running map whose only attempt is on a CPU (or has run > slowdown ×
