@@ -134,6 +134,9 @@ class HybridTaskScheduler(TaskScheduler):
                     n_red += 1
                     reduce_free -= 1
             if not jip.pending_maps:
+                # ---- speculative backups of stragglers onto idle GPUs
+                if jip.speculative and jip.gpu_capable and not jip.maps_complete():
+                    self._speculate(tr, jip, gpu_free, now, actions)
                 continue
             # ---- GPU maps
             if jip.gpu_capable:
@@ -180,17 +183,21 @@ class HybridTaskScheduler(TaskScheduler):
                     allowed -= 1
                     budget -= 1
                     self.decisions += 1
-            # ---- speculative backups of stragglers onto idle GPUs
             if jip.speculative and jip.gpu_capable and not jip.pending_maps:
-                for dev in sorted(gpu_free):
-                    if gpu_free[dev] < tr.gpu_capacity(dev) * self.queue_depth:
-                        continue  # only fully idle devices back up stragglers
-                    tip = self._straggler(jip, now)
-                    if tip is None:
-                        break
-                    actions.append(jt.launch(tr, tip, on_gpu=True, device=dev, speculative=True))
-                    gpu_free[dev] -= 1
+                self._speculate(tr, jip, gpu_free, now, actions)
         return actions
+
+    def _speculate(self, tr, jip, gpu_free, now, actions):
+        """Back up stragglers on fully idle GPUs (JobInProgress.java:2312's
+        speculation, aimed at the slow CPU attempts of a hybrid job)."""
+        for dev in sorted(gpu_free):
+            if gpu_free[dev] < tr.gpu_capacity(dev) * self.queue_depth:
+                continue  # only fully idle devices back up stragglers
+            tip = self._straggler(jip, now)
+            if tip is None:
+                break
+            actions.append(self.jt.launch(tr, tip, on_gpu=True, device=dev, speculative=True))
+            gpu_free[dev] -= 1
 
     # -- policy hooks (FIFO by priority here; fair/capacity override) --------------------
     def begin_round(self, tr, total_cpu, total_gpu):

@@ -281,17 +281,19 @@ class TaskTracker:
 
     def _check_timeouts(self):
         """markUnresponsiveTasks: fail attempts without progress for mapred.task.timeout."""
-        if self.task_timeout <= 0:
-            return
         now = time.time()
         with self._lock:
             runs = list(self.running.values())
         for r in runs:
-            if r.status.state == P.RUNNING and r.task is not None and \
-                    now - r.task.reporter.last_progress > self.task_timeout:
+            if r.status.state != P.RUNNING or r.task is None:
+                continue
+            # the job's mapred.task.timeout (TaskTracker.java:2834), else the tracker's
+            limit = r.job.conf.get_int("mapred.task.timeout", -1) / 1000.0 \
+                if r.job.conf.get("mapred.task.timeout") is not None else self.task_timeout
+            if limit > 0 and now - r.task.reporter.last_progress > limit:
                 r.kill.set()
                 self._finish(r, P.FAILED, f"Task {r.spec.attempt_id} failed to report status "
-                                          f"for {int(self.task_timeout)} seconds. Killing!")
+                                          f"for {limit:g} seconds. Killing!")
 
     # -- actions -------------------------------------------------------------------------
     def _handle(self, act):
