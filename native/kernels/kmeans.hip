@@ -75,6 +75,68 @@ __device__ __forceinline__ void stage_chunk(char* buf, const __bf16* __restrict_
   }
 }
 
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// Packed running arg-max of one lane over 32-row MFMA tiles (points on lanes,
+// clusters on the 16 accumulator registers).  The low lb = 4 + log2(tiles)
+// mantissa bits of every score are overwritten with a (tile, register) code,
+// so the running maximum needs no index registers: per tile and 32-point block
+// it costs 16 v_and_or_b32 + 8 v_max3_f32 into two partial maxima.  lb ≤ 12,
+// i.e. ≤ 2^-12 relative perturbation — below the bf16 operand rounding (2^-9).
+// v_max3_f32 goes through asm because __builtin_fmaxf canonicalises both
+// operands in IEEE mode (an extra v_max_f32 x,x,x per input, which made the
+// epilogue as long as the MFMA chain); the and_or stays compiler-visible so
+// MFMA→VALU read hazards are still padded.
+struct PackedArgMax {
+  uint32_t vmask;  // VGPR copy of ~((1 << lb) - 1): VOP3 reads only one SGPR
+  uint32_t top;    // (2^tb - 1) << 4
+  float b0, b1;
+
+  __device__ __forceinline__ void init(int ntiles) {
+    int tb = 0;
+    while ((1 << tb) < ntiles) ++tb;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(vmask) : "s"(~((1u << (tb + 4)) - 1u)));
+    top = ((1u << tb) - 1u) << 4;
+    b0 = b1 = -3.0e38f;
+  }
+  __device__ __forceinline__ void update(const f32x16& acc, int t) {
+    const uint32_t base = top - ((uint32_t)t << 4);
+    // per-register codes laundered into opaque SGPRs, else the or-constant is
+    // folded into a v_and + v_or3 pair instead of one v_and_or_b32.  (The asm
+    // is empty: a real s_or_b32 in it would clobber SCC under the loop branch.)
+    uint32_t code[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      code[r] = base | (15u - r);
+      asm("" : "+s"(code[r]));
+    }
+#pragma unroll
+    for (int r = 0; r < 16; r += 4) {
+      const float u0 = __uint_as_float((__float_as_uint(acc[r + 0]) & vmask) | code[r + 0]);
+      const float u1 = __uint_as_float((__float_as_uint(acc[r + 1]) & vmask) | code[r + 1]);
+      const float u2 = __uint_as_float((__float_as_uint(acc[r + 2]) & vmask) | code[r + 2]);
+      const float u3 = __uint_as_float((__float_as_uint(acc[r + 3]) & vmask) | code[r + 3]);
+      b0 = vmax3(b0, u0, u1);
+      b1 = vmax3(b1, u2, u3);
+    }
+  }
+  // best packed score of this lane and its cluster (lane half h)
+  __device__ __forceinline__ float best() const { return fmaxf(b0, b1); }
+  __device__ __forceinline__ int cluster(float bv, int h) const {
+    const uint32_t code = __float_as_uint(bv) & ~vmask;
+    const int tile = (int)(top >> 4) - (int)(code >> 4);
+    const int r = 15 - (int)(code & 15u);
+    return tile * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+  }
+  __device__ __forceinline__ float score(float bv) const {
+    return __uint_as_float(__float_as_uint(bv) & vmask);
+  }
+};
+
 // One workgroup's tile of points [blk*PTS, (blk+1)*PTS) of one split.
 template <int D>
 __device__ __forceinline__ void assign_tile(const __bf16* __restrict__ X, long n,
@@ -110,19 +172,15 @@ __device__ __forceinline__ void assign_tile(const __bf16* __restrict__ X, long n
     }
   }
 
-  float best[PB][16];
+  PackedArgMax am[PB];
 #pragma unroll
-  for (int pb = 0; pb < PB; ++pb)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) best[pb][r] = -3.0e38f;
+  for (int pb = 0; pb < PB; ++pb) am[pb].init(nchunks * (kCK / 32));
 
   // Retire the fragment loads here and launder the registers through an asm
   // so hipcc's waitcnt pass does not see them as pending inside the chunk loop
   // (it would otherwise emit vmcnt(0) at the first MFMA and drain the next
   // chunk's global_load_lds prefetch every iteration).
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  uint32_t vmask;
-  asm volatile("v_mov_b32 %0, 0xffffff00" : "=v"(vmask));
 #pragma unroll
   for (int pb = 0; pb < PB; ++pb)
 #pragma unroll
@@ -161,44 +219,219 @@ __device__ __forceinline__ void assign_tile(const __bf16* __restrict__ X, long n
         for (int pb = 0; pb < PB; ++pb)
           acc[pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfrag[pb][s], acc[pb], 0, 0, 0);
       }
-      // Running arg-max per register slot: the 32-cluster tile index is packed
-      // into the low 8 mantissa bits (2^-15 relative, far below the bf16
-      // operand rounding of 2^-9), so one v_and_or + one v_max per element.
-      const uint32_t tcode = 255u - (uint32_t)(c * (kCK / 32) + cb);
 #pragma unroll
-      for (int pb = 0; pb < PB; ++pb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          // hi_mask lives in a VGPR (vmask) so the selector can form one
-          // v_and_or_b32 (VOP3 may read only one SGPR on gfx950); the op itself
-          // stays compiler-visible so MFMA->VALU hazards are padded.
-          const uint32_t u = (__float_as_uint(acc[pb][r]) & vmask) | tcode;
-          best[pb][r] = __builtin_fmaxf(best[pb][r], __uint_as_float(u));
-        }
+      for (int pb = 0; pb < PB; ++pb) am[pb].update(acc[pb], c * (kCK / 32) + cb);
     }
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
   }
 
-  // Finish: arg-max over the 16 register slots, then across the lane halves.
+  // Finish: lane-local packed arg-max, then across the lane halves.
 #pragma unroll
   for (int pb = 0; pb < PB; ++pb) {
-    float bv = best[pb][0];
-    int br = 0;
-#pragma unroll
-    for (int r = 1; r < 16; ++r)
-      if (best[pb][r] > bv) { bv = best[pb][r]; br = r; }
-    const uint32_t bu = __float_as_uint(bv);
-    const int tile = 255 - (int)(bu & 0xffu);
-    int cluster = tile * 32 + (br & 3) + 8 * (br >> 2) + 4 * h;
+    float bv = am[pb].best();
+    int cluster = am[pb].cluster(bv, h);
     float ov = __shfl_xor(bv, 32);
     int oc = __shfl_xor(cluster, 32);
     if (ov > bv || (ov == bv && oc < cluster)) { bv = ov; cluster = oc; }
     const long p = p0 + pb * 32 + col;
     if (h == 0 && p < n) {
       labels[p] = cluster;
-      if (scores) scores[p] = __uint_as_float(__float_as_uint(bv) & 0xffffff00u);
+      if (scores) scores[p] = am[pb].score(bv);
       if (hist) atomicAdd(hist + cluster, 1u);  // fused histogram for the sorted combiner
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// v2: software-pipelined variant for D ≤ 128 (PB = 2).
+// The centroid stream advances in 32-cluster tiles through an NS-deep LDS
+// ring; the A fragments (and -|c|²/2) of tile t+1 are read into registers
+// while tile t's 16 MFMAs run, so the MFMA chain never waits on an LDS read,
+// and there is ONE barrier per tile:
+//   wait own DMA(t+1) + lgkmcnt(0) → barrier → DMA(t+NS) into tile t's slot
+//   (its LDS→register reads retired by the lgkmcnt) → ds_read tile t+1 →
+//   MFMAs + arg-max epilogue of tile t.
+// A DMA thus has NS-1 tiles (≈(NS-1)·512 MFMA cycles) to land: with NS = 2 the
+// L2 latency under full-chip load was exposed every tile.
+template <int D> struct AssignV2 {
+  static constexpr int KS = D / 16;
+  static constexpr int NS = 4;                           // ring depth
+  static constexpr int TILE_BYTES = 32 * D * 2;          // 32 clusters
+  static constexpr int BUF = TILE_BYTES + 32 * 4;        // + -|c|²/2
+  static constexpr int LDS_BYTES = NS * BUF;
+  static constexpr int PIECES = 32 * (D / 8);            // 16-B pieces per tile
+  // waves per workgroup sharing one centroid stream; 8 (2 per SIMD, half the
+  // L2→LDS traffic per FLOP) measured 16–19 % slower than 4 at 100M×1024×128
+  // (profiles/kmeans_assign_tuning.md); HBMR_KMEANS_V2_WAVES picks at build time
+#ifndef HBMR_KMEANS_V2_WAVES
+#define HBMR_KMEANS_V2_WAVES 4
+#endif
+  static constexpr int WAVES = PIECES >= HBMR_KMEANS_V2_WAVES * HBMR_WAVE ? HBMR_KMEANS_V2_WAVES : 4;
+  static constexpr int THREADS = WAVES * HBMR_WAVE;
+  static constexpr int MINB = WAVES == 8 ? 1 : 2;        // → ≤ 256 VGPRs either way
+  static constexpr int P = PIECES / THREADS;             // DMAs per lane per tile
+};
+
+template <int N> __device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Wait until at most `y` tile-DMAs of this wave are outstanding (wave 0 issues
+// one extra DMA per tile for -|c|²/2).  y is wave-uniform, ≤ Y.
+template <int P, int Y>
+__device__ __forceinline__ void wait_tile_dmas(int y, bool w0) {
+  if constexpr (Y > 0) {
+    if (y == Y) {
+      if (w0) vm_wait<Y * (P + 1)>(); else vm_wait<Y * P>();
+      return;
+    }
+    wait_tile_dmas<P, Y - 1>(y, w0);
+  } else {
+    vm_wait<0>();
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void stage_tile32(char* buf, const __bf16* __restrict__ C,
+                                             const float* __restrict__ chalf, int tile, int wave,
+                                             int lane) {
+  using V = AssignV2<D>;
+  constexpr int CPR = D / 8;
+  constexpr int SWZ = AssignCfg<D>::SWZ;
+  const char* gbase = reinterpret_cast<const char*>(C) + (size_t)tile * V::TILE_BYTES;
+#pragma unroll
+  for (int i = 0; i < V::P; ++i) {
+    const int base = (i * V::WAVES + wave) * HBMR_WAVE;
+    const int p = base + lane;
+    const int row = p / CPR, cpos = p % CPR;
+    const char* g = gbase + row * (D * 2) + ((cpos ^ (row & SWZ)) * 16);
+    __builtin_amdgcn_global_load_lds((const void*)g, (void*)(buf + base * 16), 16, 0, 0);
+  }
+  if (wave == 0 && lane < 32) {
+    const float* g = chalf + (size_t)tile * 32 + lane;
+    __builtin_amdgcn_global_load_lds((const void*)g, (void*)(buf + V::TILE_BYTES), 4, 0, 0);
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void read_tile32(const char* buf, int col, int h, bf16x8 (&a)[D / 16],
+                                            f32x16& bias) {
+  constexpr int SWZ = AssignCfg<D>::SWZ;
+  const char* abase = buf + col * (D * 2);
+  const int aswz = col & SWZ;
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s)
+    a[s] = *reinterpret_cast<const bf16x8*>(abase + (((2 * s + h) ^ aswz) << 4));
+  const float* ch = reinterpret_cast<const float*>(buf + AssignV2<D>::TILE_BYTES);
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(ch + 8 * g + 4 * h);
+    bias[4 * g + 0] = v[0];
+    bias[4 * g + 1] = v[1];
+    bias[4 * g + 2] = v[2];
+    bias[4 * g + 3] = v[3];
+  }
+}
+
+template <int D, int PB>
+__device__ __forceinline__ void assign_tile_v2(const __bf16* __restrict__ X, long n,
+                                               const __bf16* __restrict__ C,
+                                               const float* __restrict__ chalf, int ntiles,
+                                               int32_t* __restrict__ labels,
+                                               float* __restrict__ scores, long blk, char* smem) {
+  static_assert(D <= 128, "v2 keeps PB point blocks of D ≤ 128 in registers");
+  using V = AssignV2<D>;
+  constexpr int KS = V::KS;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / HBMR_WAVE);
+  const int lane = tid & (HBMR_WAVE - 1);
+  const int h = lane >> 5;
+  const int col = lane & 31;
+  const long p0 = blk * (V::WAVES * PB * 32) + (long)wave * PB * 32;
+
+#pragma unroll
+  for (int i = 0; i < V::NS; ++i)
+    if (i < ntiles) stage_tile32<D>(smem + i * V::BUF, C, chalf, i, wave, lane);
+
+  bf16x8 bfrag[PB][KS];
+#pragma unroll
+  for (int pb = 0; pb < PB; ++pb) {
+    long p = p0 + pb * 32 + col;
+    if (p >= n) p = n - 1;
+    const uint4* row = reinterpret_cast<const uint4*>(X + p * D);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) bfrag[pb][s] = __builtin_bit_cast(bf16x8, row[2 * s + h]);
+  }
+  PackedArgMax am[PB];
+#pragma unroll
+  for (int pb = 0; pb < PB; ++pb) am[pb].init(ntiles);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int pb = 0; pb < PB; ++pb)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(bfrag[pb][s]));
+  __syncthreads();
+
+  // Rolling register prefetch: right after the two MFMAs that consume k-step s
+  // of tile t, fragment s of tile t+1 is read into the same registers, so each
+  // LDS read has the rest of the tile's MFMAs to land and only one register
+  // set of A (and of -|c|²/2) is live.
+  bf16x8 a[KS];
+  f32x16 bias;
+  read_tile32<D>(smem, col, h, a, bias);
+  constexpr int SWZ = AssignCfg<D>::SWZ;
+  const int aswz = col & SWZ;
+
+  const bool w0 = wave == 0;
+  int slot = 0;  // t % NS
+  for (int t = 0; t < ntiles; ++t) {
+    // tile t+1's DMA has landed for every wave (younger DMAs in flight: tiles
+    // t+2 .. min(t+NS-1, ntiles-1)), and this wave's reads of tile t have
+    // retired → tile t's slot is free
+    wait_tile_dmas<V::P, V::NS - 2>(max(0, min(V::NS - 2, ntiles - 2 - t)), w0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + V::NS < ntiles) stage_tile32<D>(smem + slot * V::BUF, C, chalf, t + V::NS, wave, lane);
+    slot = slot + 1 == V::NS ? 0 : slot + 1;
+    // (past the last tile the reads hit a stale slot: harmless and branch-free)
+    const char* nbuf = smem + slot * V::BUF;
+    const char* nrow = nbuf + col * (D * 2);
+    f32x16 acc[PB];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+#pragma unroll
+      for (int pb = 0; pb < PB; ++pb)
+        acc[pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[s], bfrag[pb][s],
+                                                          s == 0 ? bias : acc[pb], 0, 0, 0);
+      a[s] = *reinterpret_cast<const bf16x8*>(nrow + (((2 * s + h) ^ aswz) << 4));
+    }
+    {
+      const float* ch = reinterpret_cast<const float*>(nbuf + V::TILE_BYTES);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(ch + 8 * g + 4 * h);
+        bias[4 * g + 0] = v[0];
+        bias[4 * g + 1] = v[1];
+        bias[4 * g + 2] = v[2];
+        bias[4 * g + 3] = v[3];
+      }
+    }
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb) am[pb].update(acc[pb], t);
+  }
+
+#pragma unroll
+  for (int pb = 0; pb < PB; ++pb) {
+    float bv = am[pb].best();
+    int cluster = am[pb].cluster(bv, h);
+    const float ov = __shfl_xor(bv, 32);
+    const int oc = __shfl_xor(cluster, 32);
+    if (ov > bv || (ov == bv && oc < cluster)) { bv = ov; cluster = oc; }
+    const long p = p0 + pb * 32 + col;
+    if (h == 0 && p < n) {
+      labels[p] = cluster;
+      if (scores) scores[p] = am[pb].score(bv);
     }
   }
 }
@@ -211,6 +444,41 @@ __global__ __launch_bounds__(kThreads, 2) void kmeans_assign_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   assign_tile<D>(X, n, C, chalf, nchunks, labels, scores, nullptr,
                  hbmr_xcd_remap(blockIdx.x, gridDim.x), smem);
+}
+
+template <int D, int PB>
+__global__ __launch_bounds__(AssignV2<D>::THREADS, AssignV2<D>::MINB) void kmeans_assign_v2_kernel(
+    const __bf16* __restrict__ X, long n, const __bf16* __restrict__ C,
+    const float* __restrict__ chalf, int ntiles, int32_t* __restrict__ labels,
+    float* __restrict__ scores) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  assign_tile_v2<D, PB>(X, n, C, chalf, ntiles, labels, scores,
+                    hbmr_xcd_remap(blockIdx.x, gridDim.x), smem);
+}
+
+// 1 = the chunked kernel above, 2 = the pipelined v2 (D ≤ 128); HBMR_KMEANS_ASSIGN
+inline int assign_version(int D) {
+  static const int v = [] {
+    const char* e = getenv("HBMR_KMEANS_ASSIGN");
+    return e && e[0] == '1' ? 1 : 2;
+  }();
+  return D <= 128 ? v : 1;
+}
+
+// v2 point blocks (32 points) per wave: 2 or 3; HBMR_KMEANS_PB
+inline int v2_pb() {
+  static const int pb = [] {
+    const char* e = getenv("HBMR_KMEANS_PB");
+    return e && e[0] == '3' ? 3 : 2;
+  }();
+  return pb;
+}
+
+// points per workgroup of the assign kernel launch_*assign picks
+template <int D> int assign_pts(bool hist) {
+  if constexpr (D <= 128)
+    if (assign_version(D) == 2 && !hist) return AssignV2<D>::WAVES * v2_pb() * 32;
+  return AssignCfg<D>::PTS;
 }
 
 // ---------------------------------------------------------------------------
@@ -245,6 +513,17 @@ __global__ __launch_bounds__(kThreads, 2) void kmeans_assign_grouped_kernel(
   const int s = __builtin_amdgcn_readfirstlane(find_split(tbl, b));
   assign_tile<D>(tbl.X[s], tbl.n[s], C, chalf, nchunks, labels + tbl.off[s], nullptr,
                  hist + (size_t)s * tbl.k, b - tbl.blk[s], smem);
+}
+
+template <int D, int PB>
+__global__ __launch_bounds__(AssignV2<D>::THREADS, AssignV2<D>::MINB) void kmeans_assign_grouped_v2_kernel(
+    const SplitTable tbl, const __bf16* __restrict__ C, const float* __restrict__ chalf,
+    int ntiles, int32_t* __restrict__ labels) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const long b = hbmr_xcd_remap(blockIdx.x, gridDim.x);
+  const int s = __builtin_amdgcn_readfirstlane(find_split(tbl, b));
+  assign_tile_v2<D, PB>(tbl.X[s], tbl.n[s], C, chalf, ntiles, labels + tbl.off[s], nullptr,
+                    b - tbl.blk[s], smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -789,12 +1068,40 @@ int launch_assign(const void* X, long n, const void* C, const float* chalf, int 
   using Cfg = AssignCfg<D>;
   if (n <= 0) return 0;
   if (k_pad % kCK) return (int)hipErrorInvalidValue;
-  const long nblk = (n + Cfg::PTS - 1) / Cfg::PTS;
+  const int pts = assign_pts<D>(false);
+  const long nblk = (n + pts - 1) / pts;
   if (nblk > 0x7fffffffL) return (int)hipErrorInvalidValue;
+  if constexpr (D <= 128) {
+    if (assign_version(D) == 2) {
+      auto kern = v2_pb() == 3 ? kmeans_assign_v2_kernel<D, 3> : kmeans_assign_v2_kernel<D, 2>;
+      hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(AssignV2<D>::THREADS),
+                         AssignV2<D>::LDS_BYTES, st, reinterpret_cast<const __bf16*>(X), n,
+                         reinterpret_cast<const __bf16*>(C), chalf, k_pad / 32, labels, scores);
+      return (int)hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL(kmeans_assign_kernel<D>, dim3((unsigned)nblk), dim3(kThreads),
                      Cfg::LDS_BYTES, st, reinterpret_cast<const __bf16*>(X), n,
                      reinterpret_cast<const __bf16*>(C), chalf, k_pad / kCK, labels, scores);
   return (int)hipGetLastError();
+}
+
+template <int D>
+void launch_grouped_assign(long nb, const SplitTable& t, const void* C, const float* chalf,
+                           int k_pad, int32_t* labels, uint32_t* hist, hipStream_t st) {
+  if constexpr (D <= 128) {
+    if (assign_version(D) == 2 && hist == nullptr) {
+      auto kern = v2_pb() == 3 ? kmeans_assign_grouped_v2_kernel<D, 3>
+                               : kmeans_assign_grouped_v2_kernel<D, 2>;
+      hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(AssignV2<D>::THREADS),
+                         AssignV2<D>::LDS_BYTES, st, t, reinterpret_cast<const __bf16*>(C),
+                         chalf, k_pad / 32, labels);
+      return;
+    }
+  }
+  hipLaunchKernelGGL(kmeans_assign_grouped_kernel<D>, dim3((unsigned)nb), dim3(kThreads),
+                     AssignCfg<D>::LDS_BYTES, st, t, reinterpret_cast<const __bf16*>(C), chalf,
+                     k_pad / kCK, labels, hist);
 }
 
 template <int D>
@@ -1025,9 +1332,9 @@ static int map_batch_grouped(int ntasks, const void* const* X, const long* n, in
   long nb = 0;
   int pts = 0;
   switch (dp) {
-    case 64: pts = AssignCfg<64>::PTS; break;
-    case 128: pts = AssignCfg<128>::PTS; break;
-    case 256: pts = AssignCfg<256>::PTS; break;
+    case 64: pts = assign_pts<64>(fused); break;
+    case 128: pts = assign_pts<128>(fused); break;
+    case 256: pts = assign_pts<256>(fused); break;
     default: return (int)hipErrorInvalidValue;
   }
   for (int i = 0; i < ntasks; ++i) {
@@ -1039,9 +1346,7 @@ static int map_batch_grouped(int ntasks, const void* const* X, const long* n, in
     switch (dp) {
 #define HBMR_GA(DD)                                                                          \
   case DD:                                                                                   \
-    hipLaunchKernelGGL(kmeans_assign_grouped_kernel<DD>, dim3((unsigned)nb), dim3(kThreads),  \
-                       AssignCfg<DD>::LDS_BYTES, st, t, reinterpret_cast<const __bf16*>(C),  \
-                       chalf, k_pad / kCK, labels, fused ? hist : nullptr);                  \
+    launch_grouped_assign<DD>(nb, t, C, chalf, k_pad, labels, fused ? hist : nullptr, st);   \
     break;
       HBMR_GA(64)
       HBMR_GA(128)
