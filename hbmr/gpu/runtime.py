@@ -50,6 +50,8 @@ class _Device:
         props = torch.cuda.get_device_properties(index)
         self.name = props.name
         self.total_mem = props.total_memory
+        self.device_errors = 0      # consecutive failed batches with a device-level error
+        self.last_error = ""
 
 
 class GpuRuntime:
@@ -189,6 +191,7 @@ class GpuRuntime:
                 TRACE.instant("gpu.launch", n=len(live), slot=slot.index)
             slot.done_q.put((live, ev0, ev1, outs))
         except BaseException as e:  # noqa: BLE001
+            self._note_error(dev.index, e)
             for r in (live or runs):
                 if r.status.state not in P.TERMINAL:
                     tracker._finish(r, P.FAILED,
@@ -209,10 +212,10 @@ class GpuRuntime:
                     TRACE.instant("gpu.complete", n=len(runs), slot=slot.index)
                 # a batch completes together; its device time is shared evenly
                 dt = ev0.elapsed_time(ev1) / 1000.0 / max(1, len(runs))
-                js = runs[0].job
-                with js.lock:
-                    for r, out in zip(runs, outs):
-                        js.map_outputs[r.spec.attempt_id] = out
+                for r, out in zip(runs, outs):   # a batch may mix jobs
+                    with r.job.lock:
+                        r.job.map_outputs[r.spec.attempt_id] = out
+                self.devices[slot.device.index].device_errors = 0
                 for r in runs:
                     r.task.reporter.incrCounter("hbmr.GpuCounters", "GPU_KERNEL_US", int(dt * 1e6))
                     tracker._finish(r, P.SUCCEEDED, output={"tracker": tracker.name,
@@ -220,11 +223,38 @@ class GpuRuntime:
                                     device_time=dt, wake=False)
                 tracker.notify_jobtracker()
             except BaseException as e:  # noqa: BLE001
+                self._note_error(slot.device.index, e)
                 for r in runs:
                     tracker._finish(r, P.FAILED,
                                     f"{type(e).__name__}: {e}\n{traceback.format_exc()[-2000:]}")
             finally:
                 slot.inflight -= len(runs)
+
+    # -- device health (NodeHealthChecker probes) --------------------------------------
+    def _note_error(self, d, exc):
+        """Count consecutive device-level failures (HIP runtime errors surface as
+        RuntimeError/AcceleratorError from torch or 'native error' from ops)."""
+        msg = f"{type(exc).__name__}: {exc}"
+        if any(s in msg for s in ("HIP", "hip", "CUDA", "Accelerator", "native error",
+                                  "device-side")):
+            dev = self.devices.get(d)
+            if dev is not None:
+                dev.device_errors += 1
+                dev.last_error = msg[:500]
+
+    def probe(self, d):
+        """None if device d looks usable, else a reason (for NodeHealthChecker)."""
+        dev = self.devices.get(d)
+        if dev is None:
+            return "unknown device"
+        limit = self.tracker.conf.get_int("hbmr.gpu.max.consecutive.errors", 3)
+        if dev.device_errors >= limit:
+            return f"{dev.device_errors} consecutive device errors; last: {dev.last_error}"
+        try:
+            torch.cuda.mem_get_info(d)
+        except Exception as e:  # noqa: BLE001
+            return f"device query failed: {e}"
+        return None
 
 
 class _Shim:

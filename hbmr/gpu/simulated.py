@@ -80,6 +80,12 @@ class SimulatedGpuRuntime:
     def has_capacity(self):
         return True
 
+    def probe(self, d):
+        """Device health for NodeHealthChecker: ``hbmr.gpu.simulate.bad.devices``
+        lists devices that report a fault (tests the unhealthy-GPU path)."""
+        bad = self.tracker.conf.get("hbmr.gpu.simulate.bad.devices", "") or ""
+        return "simulated device fault" if str(d) in [x.strip() for x in bad.split(",")] else None
+
     def start(self):
         for dev in self.devices.values():
             dev.thread = threading.Thread(target=self._worker, args=(dev,), daemon=True,

@@ -25,8 +25,9 @@ _default = None
 
 class LocalCluster:
     def __init__(self, conf=None, num_trackers=1, gpus=None, cpu_slots=None, reduce_slots=None,
-                 gpu_slots_per_device=None, local_dir=None):
-        """gpus: list per tracker of device ids, e.g. [[0], [1]]; None = CPU only."""
+                 gpu_slots_per_device=None, local_dir=None, hosts=None):
+        """gpus: list per tracker of device ids, e.g. [[0], [1]]; None = CPU only.
+        hosts: optional fake host name per tracker (rack-awareness tests)."""
         self.conf = as_jobconf(conf or JobConf())
         self.jt = JobTracker(self.conf)
         self.local_dir = local_dir or tempfile.mkdtemp(prefix="hbmr-cluster-")
@@ -37,7 +38,8 @@ class LocalCluster:
             tt = TaskTracker(self.conf, self.jt, name=f"tracker_{i}", rank=i,
                              world_size=num_trackers, gpu_devices=gpus[i], cpu_slots=cpu_slots,
                              reduce_slots=reduce_slots, gpu_slots_per_device=gpu_slots_per_device,
-                             comm=comms[i], local_dir=f"{self.local_dir}/tt{i}")
+                             comm=comms[i], local_dir=f"{self.local_dir}/tt{i}",
+                             host=hosts[i] if hosts else None)
             self.trackers.append(tt)
         for tt in self.trackers:
             tt.start()

@@ -30,6 +30,7 @@ from .counters import Counters
 from .ids import JobID, TaskAttemptID, TaskID
 from .jobclient import FAILED, KILLED, PREP, RUNNING, SUCCEEDED, JobStatus, RunningJob
 from .scheduler.costmodel import CostModel
+from ..net.topology import DEFAULT_RACK, Topology
 from ..utils.metrics import METRICS
 from ..utils.trace import TRACE
 
@@ -51,6 +52,7 @@ class TrackerInfo:
         self.jobs_seen: set[str] = set()
         self.wake = False
         self.more = False    # the last assignment stopped at the per-heartbeat cap
+        self.rack = DEFAULT_RACK
 
     def gpu_devices(self):
         return [g["device"] for g in self.status.gpus]
@@ -251,43 +253,62 @@ class JobInProgress:
         assignment instead of the reference's scan of every TIP."""
         key = (tracker.name, device if on_gpu else None)
         idx = self._loc_index.get(key)
-        if idx is None or idx[3] != len(tracker.cached):
-            lv0, lv1, lv2 = [], [], []
+        if idx is None or idx[4] != len(tracker.cached):
+            lv0, lv1, lv2, lv3 = [], [], [], []
             cached_keys = {k for k, _ in tracker.cached}
+            host = tracker.status.host
+            topo = self.jt.topology
             for tip in self.pending_maps:
                 sk = tip.split_key()
+                locs = tip.locations()
                 if sk is not None and on_gpu and (sk, device) in tracker.cached:
                     lv0.append(tip)
                 elif sk is not None and sk in cached_keys:
                     lv1.append(tip)
-                elif tracker.name in tip.locations():
+                elif tracker.name in locs or host in locs:
                     lv2.append(tip)
-            idx = [lv0[::-1], lv1[::-1], lv2[::-1], len(tracker.cached)]
+                elif locs and tracker.rack in topo.resolve(locs):
+                    lv3.append(tip)
+            idx = [lv0[::-1], lv1[::-1], lv2[::-1], lv3[::-1], len(tracker.cached)]
             self._loc_index[key] = idx
         return idx
 
     def obtain_map(self, tracker: TrackerInfo, on_gpu: bool, device: int, allow_nonlocal=True):
-        """findNewMapTask with locality levels: split cached in this device's HBM
-        > cached elsewhere on this tracker > node-local (split locations) > any."""
+        """findNewMapTask with locality levels: 0 split cached in this device's
+        HBM > 1 cached elsewhere on this tracker > 2 node-local (split locations)
+        > 3 rack-local > 4 any.  Levels ≥ 3 need ``allow_nonlocal`` (delay
+        scheduling): for a GPU the split must be re-materialised either way."""
         if not self.pending_maps:
             return None
         multi = len(self.jt.trackers) > 1
         idx = self._index(tracker, on_gpu, device)
-        for level in (0, 1, 2):
+        for level in (0, 1, 2, 3):
+            if level == 3 and not allow_nonlocal:
+                return None
             stack = idx[level]
             while stack:
                 tip = stack.pop()
                 if tip in self.pending_maps and not (multi and tracker.name in tip.failed_trackers):
                     self._take(tip)
+                    self._count_locality(level)
                     return tip, level
-        if not allow_nonlocal:
-            return None
         for tip in self.pending_maps:
             if multi and tracker.name in tip.failed_trackers:
                 continue
             self._take(tip)
-            return tip, 3
+            self._count_locality(4)
+            return tip, 4
         return None
+
+    def _count_locality(self, level):
+        # JobInProgress.Counter DATA_LOCAL_MAPS / RACK_LOCAL_MAPS (+ hbmr's
+        # HBM-resident level)
+        if level == 0:
+            self.counters.incr(C.JOB_GROUP, "HBM_LOCAL_MAPS")
+        if level <= 2:
+            self.counters.incr(C.JOB_GROUP, "DATA_LOCAL_MAPS")
+        elif level == 3:
+            self.counters.incr(C.JOB_GROUP, "RACK_LOCAL_MAPS")
 
     def _take(self, tip):
         del self.pending_maps[tip]
@@ -373,6 +394,7 @@ class JobTracker:
         self.trackers: dict[str, TrackerInfo] = {}
         self.attempt_index: dict[str, Attempt] = {}
         self.cost_model = CostModel(conf.get_float("hbmr.costmodel.ewma.alpha", 0.3))
+        self.topology = Topology(conf)
         sched_cls = conf.get("mapred.jobtracker.taskScheduler",
                              "hbmr.mapred.scheduler.hybrid:HybridTaskScheduler")
         self.scheduler = load_class(sched_cls)(self, conf)
@@ -600,7 +622,9 @@ class JobTracker:
                     # unknown tracker (e.g. after JT restart / expiry): re-initialise
                     return {"actions": [P.reinit_action()], "interval": self.heartbeat_interval}
                 tr = self.trackers[st.tracker_name] = TrackerInfo(st, now)
+                tr.rack = self.topology.rack(st.host)
                 self.history.log("TRACKER_JOINED", tracker=st.tracker_name, host=st.host,
+                                 rack=tr.rack,
                                  cpu_slots=st.max_cpu_map_slots,
                                  gpus=[g["device"] for g in st.gpus])
             tr.status = st

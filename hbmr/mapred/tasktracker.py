@@ -101,7 +101,7 @@ class _Running:
 class TaskTracker:
     def __init__(self, conf, jobtracker, name=None, rank=0, world_size=1, gpu_devices=(),
                  cpu_slots=None, reduce_slots=None, gpu_slots_per_device=None, comm=None,
-                 local_dir=None):
+                 local_dir=None, host=None):
         self.conf = conf
         self.jt = jobtracker
         # The launcher, completion and heartbeat threads hand work to each
@@ -111,7 +111,8 @@ class TaskTracker:
         si = conf.get_float("hbmr.python.switchinterval.ms", 0.2)
         if si > 0:
             sys.setswitchinterval(si / 1000.0)
-        self.host = socket.gethostname()
+        # slave.host.name: MiniMRCluster's per-tracker fake host (MiniMRCluster.java:151-188)
+        self.host = host or conf.get("slave.host.name") or socket.gethostname()
         self.rank = rank
         self.world_size = world_size
         self.name = name or f"tracker_{self.host}_r{rank}"
@@ -164,6 +165,8 @@ class TaskTracker:
             else:
                 from ..gpu.runtime import GpuRuntime as _Rt
             self.gpu_runtime = _Rt(self, self.gpu_devices, self.gpu_slots_per_device)
+        from .health import NodeHealthChecker
+        self.health = NodeHealthChecker(conf, self.gpu_runtime)
         self.heartbeats = 0
         self.tasks_done = 0
 
@@ -171,7 +174,9 @@ class TaskTracker:
     def status(self) -> P.TaskTrackerStatus:
         gpus = []
         if self.gpu_runtime is not None:
-            gpus = [g.__dict__ for g in self.gpu_runtime.device_status()]
+            gpus = self.health.filter_gpus(
+                [g.__dict__ for g in self.gpu_runtime.device_status()])
+        healthy, report = self.health.health_report()
         added, removed = self.split_cache.drain_changes()
         with self._lock:
             ids = list(self._changed)
@@ -188,7 +193,8 @@ class TaskTracker:
                                    max_reduce_slots=self.reduce_slots, gpus=gpus,
                                    task_reports=reports, cached_splits_added=added,
                                    cached_splits_removed=removed, rank=self.rank,
-                                   world_size=self.world_size, cpu_threads=self.cpu_threads)
+                                   world_size=self.world_size, cpu_threads=self.cpu_threads,
+                                   healthy=healthy, health_report=report)
 
     def _has_capacity(self):
         with self._lock:
@@ -234,6 +240,8 @@ class TaskTracker:
 
     # -- lifecycle -----------------------------------------------------------------------
     def start(self):
+        if self.health.enabled:
+            self.health.check_now()   # before the first heartbeat advertises slots
         t = threading.Thread(target=self._hb_loop, name=f"{self.name}-hb", daemon=True)
         t.start()
         self._threads.append(t)
@@ -273,6 +281,7 @@ class TaskTracker:
                 if not resp.get("actions") and not st.task_reports and block == 0.0 and not more:
                     self._news.wait(self.interval)
                 self._check_timeouts()
+                self.health.maybe_check()
             except Exception as e:  # noqa: BLE001
                 if self._stop.is_set():
                     break
