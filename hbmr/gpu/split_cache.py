@@ -68,6 +68,13 @@ class SplitCache:
             self.added, self.removed = [], []
             return a, r
 
+    def readvertise(self):
+        """After re-registering with a (restarted) JobTracker: report every
+        resident split as newly added."""
+        with self._lock:
+            self.added = [list(k) for k in self._entries]
+            self.removed = []
+
     def resident(self):
         with self._lock:
             return [list(k) for k in self._entries]

@@ -54,6 +54,20 @@ class LocalCluster:
     def job_result(self, rj: RunningJob, tracker=0):
         return self.trackers[tracker].job_result(rj.getID())
 
+    def restart_jobtracker(self, conf=None):
+        """Replace the JobTracker with a fresh one (MiniMRCluster.stopJobTracker +
+        startJobTracker, as TestJobTrackerRestart does); the trackers keep running,
+        are told to re-initialise and register again.  With
+        mapred.jobtracker.restart.recover the new JT re-submits unfinished jobs."""
+        old = self.jt
+        old.shutdown()
+        self.jt = JobTracker(as_jobconf(conf or self.conf))
+        for tt in self.trackers:
+            tt.jt = self.jt
+            tt.notify_jobtracker()
+        self.jt.start_expiry_thread()
+        return self.jt
+
     def shutdown(self):
         for tt in self.trackers:
             tt.stop()

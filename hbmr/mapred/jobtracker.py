@@ -19,7 +19,10 @@ Differences by design (SURVEY.md §2.1 bugs B1-B13):
 from __future__ import annotations
 
 import itertools
+import json
 import logging
+import os
+import shutil
 import threading
 import time
 
@@ -35,6 +38,13 @@ from ..utils.metrics import METRICS
 from ..utils.trace import TRACE
 
 log = logging.getLogger("hbmr.jobtracker")
+
+
+def _listdir(d):
+    try:
+        return os.listdir(d)
+    except OSError:
+        return []
 
 
 class TrackerInfo:
@@ -407,6 +417,27 @@ class JobTracker:
         self._stop = threading.Event()
         self.listeners = []
         self.start_time = time.time()
+        self.system_dir = conf.get("mapred.system.dir")
+        self.restart_count = 0
+        self._to_recover: list[str] = []
+        self._recover_trackers = 0
+        self._recover_deadline = 0.0
+        if self.system_dir:
+            info = self._load_info()
+            if info or any(n.startswith("job_") for n in _listdir(self.system_dir)):
+                self.restart_count = int(info.get("restart_count", 0)) + 1
+            if conf.get_boolean("mapred.jobtracker.restart.recover", False):
+                self._to_recover = sorted(n for n in _listdir(self.system_dir)
+                                          if n.startswith("job_") and os.path.exists(
+                                              os.path.join(self.system_dir, n, "job.json")))
+                self._recover_trackers = int(info.get("trackers", 0))
+                self._recover_deadline = self.start_time + conf.get_int(
+                    "hbmr.jobtracker.recovery.grace.ms", 3000) / 1000.0
+            else:
+                for n in _listdir(self.system_dir):   # stale job files of a previous run
+                    if n.startswith("job_"):
+                        shutil.rmtree(os.path.join(self.system_dir, n), ignore_errors=True)
+            self._save_info()
         METRICS.register_gauges(self._gauges)
 
     def _gauges(self):
@@ -482,13 +513,86 @@ class JobTracker:
 
     # -- jobs -----------------------------------------------------------------------
     def new_job_id(self):
-        return JobID(self.name, next(self._seq))
+        while True:
+            jid = JobID(self.name, next(self._seq))
+            if str(jid) not in self.jobs:   # recovered jobs keep their ids
+                return jid
 
-    def submit_job(self, conf) -> RunningJob:
+    # -- restart recovery ---------------------------------------------------------------
+    # RecoveryManager (JobTracker.java:1203, mapred.jobtracker.restart.recover :2394):
+    # every submitted job's conf is kept in mapred.system.dir/<jobid>/job.json until
+    # the job finishes (JobInProgress.garbageCollect deletes it).  A JobTracker that
+    # starts with recovery on re-submits each job it finds there, under its old id,
+    # once the trackers that were registered before the restart have re-joined (or
+    # after hbmr.jobtracker.recovery.grace.ms).  Recovery is job-level: the attempts
+    # of a recovered job re-run (a restarted tracker has dropped its in-flight
+    # attempts and map outputs anyway; committed outputs are idempotent renames).
+    def _sysdir(self, jid=None):
+        if not self.system_dir:
+            return None
+        return os.path.join(self.system_dir, str(jid)) if jid is not None else self.system_dir
+
+    def _persist_job(self, jid, conf):
+        d = self._sysdir(jid)
+        if d is None:
+            return
+        os.makedirs(d, exist_ok=True)
+        tmp = os.path.join(d, "job.json.tmp")
+        with open(tmp, "w") as f:
+            json.dump({"conf": conf.to_dict(), "submit_time": time.time()}, f)
+        os.replace(tmp, os.path.join(d, "job.json"))
+
+    def _forget_job(self, jid):
+        d = self._sysdir(jid)
+        if d is not None:
+            shutil.rmtree(d, ignore_errors=True)
+
+    def _save_info(self):
+        d = self._sysdir()
+        if d is None:
+            return
+        os.makedirs(d, exist_ok=True)
+        tmp = os.path.join(d, "jobtracker.json.tmp")
+        with open(tmp, "w") as f:
+            json.dump({"restart_count": self.restart_count, "trackers": len(self.trackers)}, f)
+        os.replace(tmp, os.path.join(d, "jobtracker.json"))
+
+    def _load_info(self):
+        d = self._sysdir()
+        try:
+            with open(os.path.join(d, "jobtracker.json")) as f:
+                return json.load(f)
+        except (OSError, ValueError, TypeError):
+            return {}
+
+    def _maybe_recover(self, now):
+        if not self._to_recover:
+            return
+        if len(self.trackers) < self._recover_trackers and now < self._recover_deadline:
+            return
+        todo, self._to_recover = self._to_recover, []
+        for jid_s in todo:
+            try:
+                with open(os.path.join(self._sysdir(jid_s), "job.json")) as f:
+                    doc = json.load(f)
+            except (OSError, ValueError) as e:
+                log.warning("cannot recover %s: %s", jid_s, e)
+                continue
+            from .jobconf import JobConf
+            conf = JobConf()
+            for k, v in doc["conf"].items():
+                conf.set(k, v)
+            self.history.log("JOB_RECOVERED", job=jid_s, restart=self.restart_count)
+            METRICS.inc("hbmr_jobs_recovered_total", help="jobs re-submitted after a JT restart")
+            self.submit_job(conf, job_id=JobID.for_name(jid_s))
+        log.info("recovered %d job(s) after restart %d", len(todo), self.restart_count)
+
+    def submit_job(self, conf, job_id=None) -> RunningJob:
         if TRACE.on:
             TRACE.instant("jt.submit")
         METRICS.inc("hbmr_jobs_submitted_total", help="jobs submitted")
-        jid = self.new_job_id()
+        jid = job_id or self.new_job_id()
+        self._persist_job(jid, conf)
         jip = JobInProgress(self, jid, conf)
         with self.lock:
             self.jobs[str(jid)] = jip
@@ -507,6 +611,12 @@ class JobTracker:
         for cb in self.listeners:
             cb("submitted", jip)
         return RunningJob(jid, _JTJobHandle(jip), conf)
+
+    def get_job(self, job_id) -> RunningJob | None:
+        """JobClient.getJob: a handle on a known (e.g. recovered) job."""
+        with self.lock:
+            jip = self.jobs.get(str(job_id))
+        return None if jip is None else RunningJob(jip.job_id, _JTJobHandle(jip), jip.conf)
 
     def kill_job(self, job_id):
         with self.lock:
@@ -551,6 +661,7 @@ class JobTracker:
                 jip.history_file = write_job_history(jip, hdir)
             except Exception:  # noqa: BLE001
                 log.exception("writing job history failed")
+        self._forget_job(jip.job_id)
         jip.done.set()
         for cb in self.listeners:
             cb("finished", jip)
@@ -623,6 +734,8 @@ class JobTracker:
                     return {"actions": [P.reinit_action()], "interval": self.heartbeat_interval}
                 tr = self.trackers[st.tracker_name] = TrackerInfo(st, now)
                 tr.rack = self.topology.rack(st.host)
+                if self.system_dir:
+                    self._save_info()
                 self.history.log("TRACKER_JOINED", tracker=st.tracker_name, host=st.host,
                                  rack=tr.rack,
                                  cpu_slots=st.max_cpu_map_slots,
@@ -635,6 +748,8 @@ class JobTracker:
                 tr.cached.discard(tuple(k))
             for rep in st.task_reports:
                 self._update_task_status(tr, P.TaskStatus.from_dict(rep), actions)
+            if self._to_recover:
+                self._maybe_recover(now)
             tr.more = False
             if accept_new_tasks and st.healthy and not tr.blacklisted:
                 actions += self.scheduler.assign_tasks(tr)

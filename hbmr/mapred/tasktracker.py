@@ -169,6 +169,7 @@ class TaskTracker:
         self.health = NodeHealthChecker(conf, self.gpu_runtime)
         self.heartbeats = 0
         self.tasks_done = 0
+        self._reinit = False
 
     # -- status -----------------------------------------------------------------------
     def status(self) -> P.TaskTrackerStatus:
@@ -278,6 +279,10 @@ class TaskTracker:
                 more = bool(resp.get("more"))
                 for act in resp.get("actions", []):
                     self._handle(act)
+                if self._reinit:
+                    self._reinit = False
+                    initial = True
+                    continue
                 if not resp.get("actions") and not st.task_reports and block == 0.0 and not more:
                     self._news.wait(self.interval)
                 self._check_timeouts()
@@ -324,7 +329,21 @@ class TaskTracker:
         elif typ == "kill_job":
             self.jobs.pop(act["job_id"], None)
         elif typ == "reinit":
+            # the JobTracker does not know us (it restarted, or expired us):
+            # drop every attempt and job, re-advertise the HBM-resident splits
+            # and register again (TaskTracker.java:1705 ReinitTrackerAction)
             log.warning("%s asked to reinitialise", self.name)
+            with self._lock:
+                runs = list(self.running.values())
+                self.running.clear()
+                self._changed.clear()
+            for r in runs:
+                r.kill.set()
+                if r.task is not None and getattr(r.task, "kill_event", None) is not None:
+                    r.task.kill_event.set()
+            self.jobs.clear()
+            self.split_cache.readvertise()
+            self._reinit = True
         elif typ == "shutdown":
             self._stop.set()
 
