@@ -3,7 +3,7 @@ from .api import (GpuMapper, InputFormat, InputSplit, MapRunnable, Mapper, Outpu
                   OutputFormat, Partitioner, RecordReader, RecordWriter, Reducer, Reporter)
 from .counters import Counters  # noqa: F401
 from .formats import (FileInputFormat, FileOutputFormat, FileSplit, KeyValueTextInputFormat,  # noqa: F401
-                      NLineInputFormat, NullOutputFormat, SequenceFileAsTextInputFormat,
+                      MapFileOutputFormat, NLineInputFormat, NullOutputFormat, SequenceFileAsTextInputFormat,
                       SequenceFileInputFormat, SequenceFileOutputFormat, TextInputFormat,
                       TextOutputFormat)
 from .jobclient import JobClient, RunningJob  # noqa: F401

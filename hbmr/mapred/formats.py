@@ -449,6 +449,40 @@ class SequenceFileOutputFormat(FileOutputFormat):
         return [seqf.Reader(os.path.join(path, p)) for p in files]
 
 
+class MapFileOutputFormat(FileOutputFormat):
+    """Reduce output as one MapFile per partition (MapFileOutputFormat.java):
+    reduce keys arrive sorted, so each part-NNNNN is a directly indexable map;
+    ``get_entry`` routes a lookup to the right part with the job's partitioner."""
+
+    def getRecordWriter(self, fs, job, name, progress=None):  # noqa: N802
+        from ..io.mapfile import MapFile
+        path = get_task_output_path(job, name)
+        comp = seqf.NONE
+        codec = None
+        if self.get_compress_output(job):
+            comp = job.get("mapred.output.compression.type", "RECORD").upper()
+            codec = job.get("mapred.output.compression.codec",
+                            "org.apache.hadoop.io.compress.DefaultCodec")
+        w = MapFile.Writer(path, job.get_output_key_class(), job.get_output_value_class(),
+                           comp, codec, conf=job)
+        return _SeqRecordWriter(w)
+
+    @staticmethod
+    def get_readers(path, conf=None):
+        from ..io.mapfile import MapFile
+        parts = sorted(p for p in os.listdir(path) if p.startswith("part-"))
+        return [MapFile.Reader(os.path.join(path, p), conf) for p in parts]
+
+    getReaders = get_readers  # noqa: N815
+
+    @staticmethod
+    def get_entry(readers, partitioner, key, value=None):
+        part = partitioner.getPartition(key, value, len(readers))
+        return readers[part].get(key, value)
+
+    getEntry = get_entry  # noqa: N815
+
+
 class NullOutputFormat(OutputFormat):
     def getRecordWriter(self, fs, job, name, progress=None):  # noqa: N802
         class _Null(RecordWriter):
