@@ -241,6 +241,9 @@ class Configuration:
     getClass = get_class  # noqa: N815
 
     def set_class(self, name, cls):
+        if cls is None:
+            self.unset(name)
+            return
         self.set(name, class_name(cls))
 
     setClass = set_class  # noqa: N815

@@ -16,19 +16,39 @@ class MapRunner(MapRunnable):
         self.mapper = new_instance(job.get_mapper_class(), job)
 
     def run(self, reader, output, reporter):
+        from .skipbadrecords import SkipLog, record_skip, skipping_limit
         m = self.mapper
         n = 0
+        skip_max = skipping_limit(self.job, True)
+        skipped = 0
+        skiplog = None
         try:
             while True:
                 kv = reader.next()
                 if kv is None:
                     break
                 n += 1
-                m.map(kv[0], kv[1], output, reporter)
+                if skip_max:
+                    # skipping mode (SkipBadRecords): a record whose map() fails
+                    # is logged and skipped instead of failing the attempt
+                    try:
+                        m.map(kv[0], kv[1], output, reporter)
+                    except Exception:  # noqa: BLE001
+                        skipped += 1
+                        if skipped > skip_max:
+                            raise
+                        record_skip(reporter, True)
+                        if skiplog is None:
+                            skiplog = SkipLog(self.job, type(kv[0]), type(kv[1]))
+                        skiplog.add(kv[0], kv[1])
+                else:
+                    m.map(kv[0], kv[1], output, reporter)
                 if (n & 1023) == 0:
                     reporter.progress()
         finally:
             reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, n)
+            if skiplog is not None:
+                skiplog.close()
             m.close()
 
 

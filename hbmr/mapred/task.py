@@ -510,13 +510,37 @@ class ReduceTask(Task):
 
         counted = ((next(n_in), r)[1] for r in merged)
         out = _Out()
+        from .skipbadrecords import SkipLog, record_skip, skipping_limit
+        skip_max = skipping_limit(job, False)
+        skipped = 0
+        skiplog = None
         try:
             for kb, vals in group_sorted(counted, group_key, vcls):
                 n_groups += 1
                 if (n_groups & 1023) == 0:
                     self.check_killed()
-                reducer.reduce(kcls.deserialize(kb), vals, out, rep)
+                if not skip_max:
+                    reducer.reduce(kcls.deserialize(kb), vals, out, rep)
+                    continue
+                # skipping mode: a key group whose reduce() fails is skipped
+                key = kcls.deserialize(kb)
+                seen = []
+                tracked = (seen.append(v) or v for v in vals)
+                try:
+                    reducer.reduce(key, tracked, out, rep)
+                except Exception:  # noqa: BLE001
+                    skipped += 1
+                    if skipped > skip_max:
+                        raise
+                    rest = list(vals)
+                    record_skip(rep, False, len(seen) + len(rest))
+                    if skiplog is None:
+                        skiplog = SkipLog(job, kcls, vcls)
+                    for v in seen + rest:
+                        skiplog.add(key, v)
         finally:
+            if skiplog is not None:
+                skiplog.close()
             reducer.close()
             writer.close(rep)
         rep.incrCounter(C.TASK_GROUP, C.REDUCE_INPUT_GROUPS, n_groups)

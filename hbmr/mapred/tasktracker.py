@@ -35,6 +35,7 @@ from . import counters as C
 from . import protocol as P
 from .ids import TaskAttemptID
 from .jobconf import JobConf
+from .profiling import run_profiled
 from .task import MapOutputLocation, MapTask, ReduceTask, TaskReporter
 
 from ..utils.trace import TRACE
@@ -415,7 +416,8 @@ class TaskTracker:
             task.setGPUDeviceId(spec.gpu_device_id)
             task.kill_event = run.kill
             run.task = task
-            path = task.run(os.path.join(self.local_dir, spec.job_id, spec.attempt_id))
+            path = run_profiled(js.conf, spec.attempt_id, True, spec.partition, task.run,
+                                os.path.join(self.local_dir, spec.job_id, spec.attempt_id))
             self._finish(run, P.SUCCEEDED, output={"tracker": self.name, "path": path})
         except BaseException as e:  # noqa: BLE001
             state = P.KILLED if run.kill.is_set() else P.FAILED
@@ -463,7 +465,8 @@ class TaskTracker:
             run.task = task
             for _tid, map_aid, out in spec.map_outputs:
                 task.add_map_output(MapOutputLocation(map_aid, out["path"]))
-            task.run(os.path.join(self.local_dir, spec.job_id, spec.attempt_id))
+            run_profiled(js.conf, spec.attempt_id, False, spec.partition, task.run,
+                         os.path.join(self.local_dir, spec.job_id, spec.attempt_id))
             self._finish(run, P.SUCCEEDED, output={"tracker": self.name})
         except BaseException as e:  # noqa: BLE001
             state = P.KILLED if run.kill.is_set() else P.FAILED
