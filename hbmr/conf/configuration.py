@@ -15,6 +15,7 @@ SURVEY.md B2) — here both spellings address one key.
 """
 from __future__ import annotations
 
+import getpass
 import os
 import re
 import threading
@@ -137,6 +138,8 @@ class Configuration:
             rep = os.environ.get(var)
             if rep is None:
                 rep = self.get_raw(var)
+            if rep is None and var in ("USER", "user.name"):
+                rep = getpass.getuser()
             if rep is None:
                 return value
             value = value[:m.start()] + rep + value[m.end():]

@@ -29,8 +29,13 @@ class LocalCluster:
         """gpus: list per tracker of device ids, e.g. [[0], [1]]; None = CPU only.
         hosts: optional fake host name per tracker (rack-awareness tests)."""
         self.conf = as_jobconf(conf or JobConf())
-        self.jt = JobTracker(self.conf)
         self.local_dir = local_dir or tempfile.mkdtemp(prefix="hbmr-cluster-")
+        # like MiniMRCluster, each cluster gets its own mapred.system.dir unless the
+        # caller named one: the stale-job sweep of a starting JobTracker must never
+        # see another live cluster's job files
+        if self.conf.get_raw("mapred.system.dir") == "${hadoop.tmp.dir}/mapred/system":
+            self.conf.set("mapred.system.dir", f"{self.local_dir}/system")
+        self.jt = JobTracker(self.conf)
         comms = InProcessComm.group(num_trackers) if num_trackers > 1 else [SoloComm()]
         gpus = gpus or [[] for _ in range(num_trackers)]
         self.trackers = []
