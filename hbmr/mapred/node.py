@@ -33,6 +33,12 @@ class Node:
         self.rank = int(os.environ.get("RANK", "0"))
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        # rehearsal of the multi-process path on a 1-GPU box: every rank drives
+        # device 0 and collectives go over gloo (RCCL refuses two ranks on one GPU)
+        shared = os.environ.get("HBMR_SHARED_DEVICE")
+        if shared is not None:
+            self.local_rank = int(shared)
+            backend = backend or "gloo"
         self.use_gpu = torch.cuda.is_available() if use_gpu is None else use_gpu
         self.jt = None
         self.server = None

@@ -35,6 +35,7 @@ from . import counters as C
 from . import protocol as P
 from .ids import TaskAttemptID
 from .jobconf import JobConf
+from .child import use_child_process
 from .profiling import run_profiled
 from .task import MapOutputLocation, MapTask, ReduceTask, TaskReporter
 
@@ -168,6 +169,7 @@ class TaskTracker:
             self.gpu_runtime = _Rt(self, self.gpu_devices, self.gpu_slots_per_device)
         from .health import NodeHealthChecker
         self.health = NodeHealthChecker(conf, self.gpu_runtime)
+        self.child_manager = None     # JvmManager analogue, created on first use
         self.heartbeats = 0
         self.tasks_done = 0
         self._reinit = False
@@ -260,6 +262,8 @@ class TaskTracker:
             t.join(timeout=5)
         self.cpu_pool.shutdown(wait=False, cancel_futures=True)
         self.reduce_pool.shutdown(wait=False, cancel_futures=True)
+        if self.child_manager is not None:
+            self.child_manager.shutdown()
 
     def _hb_loop(self):
         initial = True
@@ -329,6 +333,8 @@ class TaskTracker:
                 r.status.commit_granted = True  # picked up by the waiting task
         elif typ == "kill_job":
             self.jobs.pop(act["job_id"], None)
+            if self.child_manager is not None:
+                self.child_manager.job_done(act["job_id"])
         elif typ == "reinit":
             # the JobTracker does not know us (it restarted, or expired us):
             # drop every attempt and job, re-advertise the HBM-resident splits
@@ -409,6 +415,10 @@ class TaskTracker:
                 rep.incrCounter(C.JOB_GROUP, C.CPU_MAP_TASKS, 0)
                 self._finish(run, P.SUCCEEDED, output={"tracker": self.name, "where": "cpu"})
                 return
+            if use_child_process(js.conf):
+                path = self._run_in_child(run, is_map=True)
+                self._finish(run, P.SUCCEEDED, output={"tracker": self.name, "path": path})
+                return
             split = _split_from_dict(spec.split)
             aid = TaskAttemptID.for_name(spec.attempt_id)
             task = MapTask(js.conf, aid, spec.partition, split)
@@ -459,6 +469,10 @@ class TaskTracker:
                 small = js.result if isinstance(js.result, dict) else None
                 self._finish(run, P.SUCCEEDED, output={"tracker": self.name, "result": small})
                 return
+            if use_child_process(js.conf):
+                self._run_in_child(run, is_map=False)
+                self._finish(run, P.SUCCEEDED, output={"tracker": self.name})
+                return
             aid = TaskAttemptID.for_name(spec.attempt_id)
             task = ReduceTask(js.conf, aid, spec.partition, spec.num_maps)
             task.kill_event = run.kill
@@ -471,6 +485,37 @@ class TaskTracker:
         except BaseException as e:  # noqa: BLE001
             state = P.KILLED if run.kill.is_set() else P.FAILED
             self._finish(run, state, f"{type(e).__name__}: {e}\n{traceback.format_exc()[-2000:]}")
+
+    # -- child processes (TaskRunner / JvmManager) --------------------------------------------
+    def _children(self):
+        with self._lock:
+            if self.child_manager is None:
+                from .child import ChildManager
+                self.child_manager = ChildManager(self.name, self.local_dir, self.conf)
+            return self.child_manager
+
+    def _run_in_child(self, run: _Running, is_map: bool):
+        spec, js = run.spec, run.job
+        rep = TaskReporter()
+        shim = _SplitTaskShim(rep)
+        shim.kill_event = run.kill
+        run.task = shim
+        work = os.path.join(self.local_dir, spec.job_id, spec.attempt_id)
+        payload = {
+            "attempt_id": spec.attempt_id, "is_map": is_map, "partition": spec.partition,
+            "split": spec.split, "run_on_gpu": spec.run_on_gpu,
+            "gpu_device_id": spec.gpu_device_id, "num_maps": spec.num_maps,
+            "map_outputs": [(a, o["path"]) for _tid, a, o in spec.map_outputs] if not is_map
+            else [],
+            "conf": js.conf.to_dict(), "work_dir": work,
+            "log_dir": os.path.join(self.local_dir, "userlogs", spec.attempt_id),
+            "progress_interval": js.conf.get_int("hbmr.task.progress.interval.ms", 1000) / 1e3,
+        }
+
+        def _progress(p):
+            run.status.progress = float(p)
+        return self._children().run_task(spec.job_id, js.conf, payload, rep, run.kill,
+                                         progress_cb=_progress)
 
     def job_result(self, job_id):
         js = self.jobs.get(str(job_id))

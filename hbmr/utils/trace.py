@@ -135,7 +135,8 @@ TRACE = Tracer()
 
 _env = os.environ.get("HBMR_TRACE", "")
 if _env and _env != "0":
-    TRACE.enable(None if _env == "1" else _env)
+    # "{rank}" in the path keeps the dumps of a multi-process node apart
+    TRACE.enable(None if _env == "1" else _env.replace("{rank}", os.environ.get("RANK", "0")))
 
 
 def configure(conf):
