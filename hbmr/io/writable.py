@@ -21,6 +21,9 @@ import numpy as np
 
 from .vint import decode_vint, encode_vint, read_vint
 
+# one-byte VInt encodings of 0..127 (the common Text length), for serialize()
+_VINT1 = [bytes((i,)) for i in range(128)]
+
 _JAVA_NAME_TO_CLASS: dict[str, type] = {}
 
 
@@ -117,11 +120,19 @@ class Text(WritableComparable):
         return len(self.bytes)
 
     def serialize(self) -> bytes:
-        return encode_vint(len(self.bytes)) + self.bytes
+        b = self.bytes
+        n = len(b)
+        return (_VINT1[n] if n < 128 else encode_vint(n)) + b
 
     def readFields(self, inp):  # noqa: N802
         n = read_vint(inp)
         self.bytes = inp.read(n)
+
+    @classmethod
+    def deserialize(cls, raw: bytes):
+        obj = cls.__new__(cls)
+        obj.bytes = raw[1:] if raw[0] < 128 else raw[decode_vint(raw, 0)[1]:]
+        return obj
 
     @classmethod
     def raw_sort_key(cls, raw: bytes):
@@ -146,6 +157,10 @@ class _FixedNum(WritableComparable):
     FMT = ">i"
     __slots__ = ("value",)
 
+    def __init_subclass__(cls, **kw):
+        super().__init_subclass__(**kw)
+        cls._ST = struct.Struct(cls.FMT)
+
     def __init__(self, value=0):
         self.value = value
 
@@ -156,7 +171,15 @@ class _FixedNum(WritableComparable):
         self.value = v
 
     def serialize(self) -> bytes:
-        return struct.pack(self.FMT, self.value)
+        return self._ST.pack(self.value)
+
+    @classmethod
+    def deserialize(cls, raw: bytes):
+        if cls.readFields is not _FixedNum.readFields:
+            return super().deserialize(raw)
+        obj = cls.__new__(cls)
+        obj.value = cls._ST.unpack(raw)[0]
+        return obj
 
     def readFields(self, inp):  # noqa: N802
         sz = struct.calcsize(self.FMT)

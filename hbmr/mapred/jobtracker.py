@@ -63,6 +63,7 @@ class TrackerInfo:
         self.wake = False
         self.more = False    # the last assignment stopped at the per-heartbeat cap
         self.rack = DEFAULT_RACK
+        self.kills: set[str] = set()   # attempts to kill on the next heartbeat
 
     def gpu_devices(self):
         return [g["device"] for g in self.status.gpus]
@@ -77,7 +78,7 @@ class TrackerInfo:
 class Attempt:
     __slots__ = ("aid", "tip", "tracker", "run_on_gpu", "device", "state", "progress",
                  "start", "finish", "counters", "output", "diagnostic", "speculative",
-                 "device_time", "_released")
+                 "device_time", "_released", "profile_only")
 
     def __init__(self, aid, tip, tracker, run_on_gpu, device, speculative=False):
         self.aid = aid
@@ -94,6 +95,7 @@ class Attempt:
         self.diagnostic = ""
         self.speculative = speculative
         self.device_time = 0.0
+        self.profile_only = False   # a CPU profiling probe left running after its TIP won
 
 
 class TaskInProgress:
@@ -754,11 +756,16 @@ class JobTracker:
             if accept_new_tasks and st.healthy and not tr.blacklisted:
                 actions += self.scheduler.assign_tasks(tr)
             # kill attempts of jobs that are done / tasks already completed
+            # (detached CPU profiling probes excepted)
             for aid in list(tr.running):
                 a = self.attempt_index.get(aid)
-                if a is not None and (a.tip.job.completed() or
-                                      (a.tip.successful is not None and a.tip.successful is not a)):
-                    actions.append(P.kill_task_action(aid))
+                if a is not None and not a.profile_only and (
+                        a.tip.job.completed() or
+                        (a.tip.successful is not None and a.tip.successful is not a)):
+                    tr.kills.add(aid)
+            if tr.kills:
+                actions += [P.kill_task_action(aid) for aid in sorted(tr.kills)]
+                tr.kills.clear()
         return {"actions": actions, "interval": self.heartbeat_interval, "more": tr.more}
 
     def _update_task_status(self, tr: TrackerInfo, ts: P.TaskStatus, actions):
@@ -842,8 +849,19 @@ class JobTracker:
         # kill other running attempts of this TIP
         for other in tip.running_attempts():
             if other is not a:
+                if tip.is_map and not other.run_on_gpu and \
+                        self.cost_model.stats(jip.signature, False).n == 0:
+                    # the signature's CPU profiling probe lost to its GPU backup:
+                    # let it finish detached (output ignored, slot held) so the
+                    # cost model learns the real CPU time instead of a censored
+                    # bound that would invite more doomed CPU attempts
+                    other.profile_only = True
+                    continue
                 other.state = P.KILLED
                 self._release(other)
+                tr_o = self.trackers.get(other.tracker)
+                if tr_o is not None:
+                    tr_o.kills.add(other.aid)
                 if tip.is_map:
                     self.cost_model.task_finished(jip.signature, other.aid, other.run_on_gpu,
                                                   other.start, time.time(), succeeded=False)

@@ -55,6 +55,10 @@ class HybridTaskScheduler(TaskScheduler):
         self.locality_wait = conf.get_int("hbmr.locality.wait.ms", 500) / 1000.0
         self.max_reduces_per_hb = conf.get_int("hbmr.scheduler.max.reduces.per.heartbeat", 4)
         self.speculate_after = conf.get_float("hbmr.speculative.slowdown", 3.0)
+        # stock Hadoop only backs up attempts that ran > SPECULATIVE_LAG (60 s,
+        # TaskInProgress.java) and lag in progress; the GPU-aware early backup
+        # of CPU stragglers is part of the hybrid design
+        self.stock_lag = conf.get_int("hbmr.speculative.stock.lag.ms", 60000) / 1000.0
         # cap map launches per heartbeat response so a tracker can start the
         # first tasks while the rest are still being assigned (the response
         # says "more" and the tracker calls right back)
@@ -109,7 +113,9 @@ class HybridTaskScheduler(TaskScheduler):
         total_cpu, total_gpu = self._totals()
         cpu_free = tr.status.max_cpu_map_slots - tr.running_cpu
         reduce_free = tr.status.max_reduce_slots - tr.running_reduce
-        gpu_free = {g["device"]: g["max_slots"] * self.queue_depth - tr.running_gpu.get(
+        # stock Hadoop knows no queue behind a slot: one task per GPU slot
+        depth = 1 if self.policy == "stock" else self.queue_depth
+        gpu_free = {g["device"]: g["max_slots"] * depth - tr.running_gpu.get(
             g["device"], 0) for g in tr.status.gpus}
         budget = self.max_maps_per_hb
         tr.more = False
@@ -138,6 +144,25 @@ class HybridTaskScheduler(TaskScheduler):
                 if jip.speculative and jip.gpu_capable and not jip.maps_complete():
                     self._speculate(tr, jip, gpu_free, now, actions)
                 continue
+            # ---- CPU maps (first, as the fork's loop order, JobQueueTaskScheduler.java
+            # :295-387: the cost model decides how many; a CPU profile probe must
+            # not be starved by the GPUs' much larger queue budget)
+            if cpu_free > 0 and jip.pending_maps:
+                allowed = min(self._cpu_allowed(jip, total_cpu, total_gpu, now),
+                              self.job_limit(jip, "cpu"))
+                while cpu_free > 0 and allowed > 0 and jip.pending_maps:
+                    if budget <= 0:
+                        tr.more = True
+                        break
+                    got = jip.obtain_map(tr, False, -1, allow_nonlocal=True)
+                    if got is None:
+                        break
+                    tip, _ = got
+                    actions.append(jt.launch(tr, tip, on_gpu=False))
+                    cpu_free -= 1
+                    allowed -= 1
+                    budget -= 1
+                    self.decisions += 1
             # ---- GPU maps
             if jip.gpu_capable:
                 glim = self.job_limit(jip, "gpu")
@@ -166,23 +191,6 @@ class HybridTaskScheduler(TaskScheduler):
                         budget -= 1
                         glim -= 1
                         self.decisions += 1
-            # ---- CPU maps
-            if cpu_free > 0 and jip.pending_maps:
-                allowed = min(self._cpu_allowed(jip, total_cpu, total_gpu, now),
-                              self.job_limit(jip, "cpu"))
-                while cpu_free > 0 and allowed > 0 and jip.pending_maps:
-                    if budget <= 0:
-                        tr.more = True
-                        break
-                    got = jip.obtain_map(tr, False, -1, allow_nonlocal=True)
-                    if got is None:
-                        break
-                    tip, _ = got
-                    actions.append(jt.launch(tr, tip, on_gpu=False))
-                    cpu_free -= 1
-                    allowed -= 1
-                    budget -= 1
-                    self.decisions += 1
             if jip.speculative and jip.gpu_capable and not jip.pending_maps:
                 self._speculate(tr, jip, gpu_free, now, actions)
         return actions
@@ -223,6 +231,10 @@ class HybridTaskScheduler(TaskScheduler):
                 continue
             a = run[0]
             elapsed = now - a.start
+            if self.policy == "stock":
+                if elapsed > self.stock_lag:
+                    return tip
+                continue
             if not a.run_on_gpu and t_gpu is not None and elapsed > t_gpu * 2:
                 return tip
             if a.run_on_gpu and t_gpu is not None and elapsed > self.speculate_after * t_gpu + 1.0:

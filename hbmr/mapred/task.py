@@ -26,10 +26,13 @@ import os
 import threading
 import time
 
+import numpy as np
+
 from ..io.compress import get_codec
 from ..io.ifile import IFileWriter, SpillRecord, read_segment
 from ..utils.reflection import new_instance
 from . import counters as C
+from . import sortbuf
 from .api import OutputCollector, Reporter
 from .committer import FileOutputCommitter
 from .formats import FileSplit
@@ -230,7 +233,16 @@ class MapOutputBuffer(OutputCollector):
             if job.get_compress_map_output() else None
         self.out_dir = out_dir
         os.makedirs(out_dir, exist_ok=True)
+        # native sort path (hbmr/mapred/sortbuf.py): serialised records only,
+        # partition + sort + group + IFile encode per spill in C++
+        self.kind = sortbuf.key_kind(job)
+        self.native_hash = self.kind is not None and sortbuf.hash_partitioned(job)
+        self.keys: list = []
+        self.vals: list = []
+        self.parts: list = []
         self.buf: list = []
+        if self.native_hash:
+            self.collect = self._collect_native
         self.buf_bytes = 0
         self.spills: list[tuple[str, SpillRecord]] = []
         self.n_out = 0
@@ -243,16 +255,45 @@ class MapOutputBuffer(OutputCollector):
         if not isinstance(value, self.vcls):
             raise TypeError(f"Type mismatch in value from map: expected {self.vcls.__name__}, "
                             f"received {type(value).__name__}")
-        part = self.partitioner.getPartition(key, value, self.R)
-        if not 0 <= part < self.R:
-            raise ValueError(f"Illegal partition for {key!r} ({part})")
         kb = key.serialize()
         vb = value.serialize()
-        self.buf.append((part, self.sort_key(kb), kb, vb))
+        if self.native_hash:
+            self.keys.append(kb)
+            self.vals.append(vb)
+        else:
+            part = self.partitioner.getPartition(key, value, self.R)
+            if not 0 <= part < self.R:
+                raise ValueError(f"Illegal partition for {key!r} ({part})")
+            if self.kind is not None:
+                self.keys.append(kb)
+                self.vals.append(vb)
+                self.parts.append(part)
+            else:
+                self.buf.append((part, self.sort_key(kb), kb, vb))
         sz = len(kb) + len(vb) + 16  # 16 B accounting per record (MapTask.java:890-903)
         self.buf_bytes += sz
         self.n_out += 1
         self.bytes_out += len(kb) + len(vb)
+        if self.buf_bytes >= self.soft_limit:
+            self.sort_and_spill()
+
+    def _collect_native(self, key, value):
+        """collect() when partitioning is batched in C++: serialise and append."""
+        kc = self.kcls
+        if key.__class__ is not kc and not isinstance(key, kc):
+            raise TypeError(f"Type mismatch in key from map: expected {kc.__name__}, "
+                            f"received {type(key).__name__}")
+        vc = self.vcls
+        if value.__class__ is not vc and not isinstance(value, vc):
+            raise TypeError(f"Type mismatch in value from map: expected {vc.__name__}, "
+                            f"received {type(value).__name__}")
+        kb = key.serialize()
+        vb = value.serialize()
+        self.keys.append(kb)
+        self.vals.append(vb)
+        n = len(kb) + len(vb)
+        self.bytes_out += n
+        self.buf_bytes += n + 16   # 16 B accounting per record (MapTask.java:890-903)
         if self.buf_bytes >= self.soft_limit:
             self.sort_and_spill()
 
@@ -264,6 +305,8 @@ class MapOutputBuffer(OutputCollector):
         return parts
 
     def sort_and_spill(self):
+        if self.kind is not None:
+            return self._sort_and_spill_native()
         if not self.buf and self.spills:
             return
         self.task.check_killed()
@@ -289,6 +332,89 @@ class MapOutputBuffer(OutputCollector):
         self.spills.append((path, rec))
         self.reporter.incrCounter(C.TASK_GROUP, C.SPILLED_RECORDS, spilled)
 
+    # -- native path ------------------------------------------------------------------------
+    def _combine_native(self, b, perm, lo, hi):
+        """Run the combiner over the key groups of perm[lo:hi]; returns the IFile
+        body of its (re-sorted) output and the record count."""
+        ends = b.group_ends(self.kind, perm, lo, hi)
+        comb = new_instance(self.combiner_cls, self.job)
+        col = _ListCollector()
+        kdes, vdes = self.kcls.deserialize, self.vcls.deserialize
+        pl = perm.tolist()
+        a = lo
+        for e in ends.tolist():
+            comb.reduce(kdes(b.key(pl[a])), (vdes(b.value(r)) for r in pl[a:e]), col,
+                        self.reporter)
+            a = e
+        comb.close()
+        self.reporter.incrCounter(C.TASK_GROUP, C.COMBINE_INPUT_RECORDS, hi - lo)
+        self.reporter.incrCounter(C.TASK_GROUP, C.COMBINE_OUTPUT_RECORDS, len(col.out))
+        ob = sortbuf.Batch.from_lists([k.serialize() for k, _ in col.out],
+                                      [v.serialize() for _, v in col.out])
+        operm = ob.sort(self.kind, np.zeros(ob.n, np.int32))
+        return ob.ifile_body(operm, 0, ob.n), ob.n
+
+    def _sort_and_spill_native(self):
+        if not self.keys and self.spills:
+            return
+        self.task.check_killed()
+        b = sortbuf.Batch.from_lists(self.keys, self.vals)
+        if self.native_hash:
+            self.n_out += b.n
+        part = b.hash_partition(self.kind, self.R) if self.native_hash else \
+            np.asarray(self.parts, dtype=np.int32)
+        self.keys, self.vals, self.parts = [], [], []
+        self.buf_bytes = 0
+        perm = b.sort(self.kind, part)
+        starts = np.zeros(self.R + 1, np.int64)
+        np.cumsum(np.bincount(part, minlength=self.R), out=starts[1:])
+        idx = len(self.spills)
+        path = os.path.join(self.out_dir, f"spill{idx}.out")
+        rec = SpillRecord(self.R)
+        spilled = 0
+        with open(path, "wb") as f:
+            for p in range(self.R):
+                lo, hi = int(starts[p]), int(starts[p + 1])
+                if self.combiner_cls is not None and hi > lo:
+                    body, nrec = self._combine_native(b, perm, lo, hi)
+                else:
+                    body, nrec = b.ifile_body(perm, lo, hi), hi - lo
+                spilled += nrec
+                rec.put(p, *sortbuf.write_segment(f, body, self.codec))
+        rec.write(path + ".index")
+        self.spills.append((path, rec))
+        self.reporter.incrCounter(C.TASK_GROUP, C.SPILLED_RECORDS, spilled)
+
+    def _merge_parts_native(self, final):
+        rec_out = SpillRecord(self.R)
+        spilled = 0
+        combine = self.combiner_cls is not None and \
+            len(self.spills) >= self.min_spills_for_combine
+        with open(final, "wb") as f:
+            for p in range(self.R):
+                bodies = []
+                for path, rec in self.spills:
+                    start, _raw, plen = rec.get(p)
+                    with open(path, "rb") as sf:
+                        sf.seek(start)
+                        bodies.append(sortbuf.segment_body(sf.read(plen), self.codec))
+                b = sortbuf.Batch.from_ifile_bodies(bodies)
+                # a stable sort of the concatenated runs == the k-way merge
+                # (earlier spills win ties, Merger.MergeQueue)
+                perm = b.sort(self.kind, np.zeros(b.n, np.int32))
+                if combine and b.n:
+                    body, nrec = self._combine_native(b, perm, 0, b.n)
+                else:
+                    body, nrec = b.ifile_body(perm, 0, b.n), b.n
+                spilled += nrec
+                rec_out.put(p, *sortbuf.write_segment(f, body, self.codec))
+        rec_out.write(final + ".index")
+        for path, _ in self.spills:
+            for q in (path, path + ".index"):
+                if os.path.exists(q):
+                    os.remove(q)
+        self.reporter.incrCounter(C.TASK_GROUP, C.SPILLED_RECORDS, spilled)
+
     def flush(self):
         """Final spill + merge into file.out / file.out.index."""
         self.sort_and_spill()
@@ -297,6 +423,8 @@ class MapOutputBuffer(OutputCollector):
             path, rec = self.spills[0]
             os.replace(path, final)
             os.replace(path + ".index", final + ".index")
+        elif self.kind is not None:
+            self._merge_parts_native(final)
         else:
             self._merge_parts(final)
         self.reporter.incrCounter(C.TASK_GROUP, C.MAP_OUTPUT_RECORDS, self.n_out)
@@ -480,6 +608,9 @@ class ReduceTask(Task):
         vcls = job.get_map_output_value_class()
         sort_key = job.get_output_key_comparator()
         group_key = job.get_output_value_grouping_comparator()
+        from .skipbadrecords import SkipLog, record_skip, skipping_limit
+        skip_max = skipping_limit(job, False)
+        kind = sortbuf.key_kind(job) if not skip_max else None
         # copy phase
         segs = []
         shuffled = 0
@@ -487,10 +618,18 @@ class ReduceTask(Task):
             self.check_killed()
             data = loc.read_partition(self.partition)
             shuffled += len(data)
-            segs.append([(sort_key(kb), kb, vb) for kb, vb in read_segment(data, codec)])
+            if kind is not None:
+                segs.append(sortbuf.segment_body(data, codec))
+            else:
+                segs.append([(sort_key(kb), kb, vb) for kb, vb in read_segment(data, codec)])
         rep.incrCounter(C.TASK_GROUP, C.REDUCE_SHUFFLE_BYTES, shuffled)
         rep.set_progress(1 / 3)
         # sort phase (merge)
+        if kind is not None:
+            # stable sort of the concatenated map outputs == Merger's k-way merge
+            b = sortbuf.Batch.from_ifile_bodies(segs)
+            perm = b.sort(kind, np.zeros(b.n, np.int32))
+            return self._reduce_native(job, b, perm, kind, kcls, vcls)
         merged = merge_segments(segs, job.get_int("io.sort.factor", 10))
         rep.set_progress(2 / 3)
         # reduce phase
@@ -510,8 +649,6 @@ class ReduceTask(Task):
 
         counted = ((next(n_in), r)[1] for r in merged)
         out = _Out()
-        from .skipbadrecords import SkipLog, record_skip, skipping_limit
-        skip_max = skipping_limit(job, False)
         skipped = 0
         skiplog = None
         try:
@@ -545,6 +682,44 @@ class ReduceTask(Task):
             writer.close(rep)
         rep.incrCounter(C.TASK_GROUP, C.REDUCE_INPUT_GROUPS, n_groups)
         rep.incrCounter(C.TASK_GROUP, C.REDUCE_INPUT_RECORDS, next(n_in))
+        rep.incrCounter(C.TASK_GROUP, C.REDUCE_OUTPUT_RECORDS, n_out[0])
+        if committer.needs_task_commit(job, self.attempt_id):
+            committer.commit_task(job, self.attempt_id)
+        rep.set_progress(1.0)
+        self.finish_time = time.time()
+
+    def _reduce_native(self, job, b, perm, kind, kcls, vcls):
+        """Reduce phase over a natively merged partition (no skipping mode)."""
+        rep = self.reporter
+        rep.set_progress(2 / 3)
+        committer = self.committer()
+        committer.setup_task(job, self.attempt_id)
+        outfmt = new_instance(job.get_output_format(), job)
+        writer = outfmt.getRecordWriter(None, job, f"part-{self.partition:05d}", rep)
+        reducer = new_instance(job.get_reducer_class(), job)
+        n_out = [0]
+
+        class _Out(OutputCollector):
+            def collect(self_inner, k, v):
+                writer.write(k, v)
+                n_out[0] += 1
+
+        out = _Out()
+        ends = b.group_ends(kind, perm, 0, b.n).tolist()
+        pl = perm.tolist()
+        kdes, vdes = kcls.deserialize, vcls.deserialize
+        try:
+            a = 0
+            for g, e in enumerate(ends):
+                if (g & 1023) == 1023:
+                    self.check_killed()
+                reducer.reduce(kdes(b.key(pl[a])), (vdes(b.value(r)) for r in pl[a:e]), out, rep)
+                a = e
+        finally:
+            reducer.close()
+            writer.close(rep)
+        rep.incrCounter(C.TASK_GROUP, C.REDUCE_INPUT_GROUPS, len(ends))
+        rep.incrCounter(C.TASK_GROUP, C.REDUCE_INPUT_RECORDS, b.n)
         rep.incrCounter(C.TASK_GROUP, C.REDUCE_OUTPUT_RECORDS, n_out[0])
         if committer.needs_task_commit(job, self.attempt_id):
             committer.commit_task(job, self.attempt_id)

@@ -6,6 +6,8 @@ Produces (all in-tree so they travel to the GPU box with the repo snapshot):
                                   and native I/O (native/cpu/*.cc), C ABI, loaded
                                   by ``hbmr.ops`` via ctypes next to PyTorch.
 * ``hbmr/lib/libhbmr_pipes.a`` – the Pipes child-side runtime (native/pipes).
+* ``hbmr/lib/libhbmr_cpu.so``  – the same host-only objects as a shared library
+                                  (CPU task data path: map-output sort/IFile).
 * ``hbmr/lib/libhbmr_host.a``  – host-only objects (native/cpu + native/io:
                                   CPU K-Means, SequenceFile) for CPU task binaries.
 * ``hbmr/bin/*``               – Pipes task executables (native/apps), e.g. the
@@ -102,7 +104,13 @@ def build(verbose: bool = False, jobs: int | None = None) -> dict:
             hostlib.unlink()
         _run(["ar", "rcs", hostlib, *host_objs], verbose)
 
-    out = {"libhbmr": str(lib), "libhbmr_host": str(hostlib)}
+    # host-only shared library for CPU tasks (map-output buffer, CPU K-Means,
+    # SequenceFile): loadable without the HIP runtime
+    cpulib = LIBDIR / "libhbmr_cpu.so"
+    if _stale(cpulib, host_objs):
+        _run([CXX, "-shared", "-fPIC", "-o", cpulib, *host_objs, "-pthread", "-lz"], verbose)
+
+    out = {"libhbmr": str(lib), "libhbmr_host": str(hostlib), "libhbmr_cpu": str(cpulib)}
     if pipes_srcs:
         alib = LIBDIR / "libhbmr_pipes.a"
         pobjs = [objs[s] for s in pipes_srcs]

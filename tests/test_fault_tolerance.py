@@ -134,7 +134,6 @@ def test_speculative_gpu_backup_of_cpu_straggler():
     conf.set_boolean("hbmr.gpu.simulate", True)
     conf.set_int("mapred.tasktracker.map.gpu.tasks.maximum", 1)
     conf.set_float("hbmr.gpu.simulate.task.ms", 5)
-    conf.set("hbmr.scheduler.policy", "stock")
     conf.set_int("hbmr.gpu.queue.depth", 1)
     with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=1) as cl:
         job = split_sleep_conf(6, map_ms=1500, base=conf)     # CPU map tasks sleep 1.5 s
@@ -145,6 +144,34 @@ def test_speculative_gpu_backup_of_cpu_straggler():
         took = time.time() - t0
         jip = rj._impl.jip
         spec = [a for t in jip.maps for a in t.attempts.values() if a.speculative]
+        cpu = [a for t in jip.maps for a in t.attempts.values() if not a.run_on_gpu]
+        # the overtaken CPU attempt was the signature's profiling probe: it runs
+        # on detached and its real duration lands in the cost model
+        deadline = time.time() + 5
+        while cl.jt.cost_model.stats(jip.signature, False).n == 0 and time.time() < deadline:
+            time.sleep(0.05)
+        t_cpu = cl.jt.cost_model.stats(jip.signature, False).mean
     # the CPU straggler got a GPU backup that won; the job did not wait 1.5 s
     assert spec and any(a.run_on_gpu for a in spec)
     assert took < 1.4
+    assert len(cpu) == 1 and cpu[0].profile_only
+    assert t_cpu >= 1.4
+
+
+def test_stock_policy_waits_for_cpu_stragglers():
+    """GPU-unaware stock scheduling: CPU slots take tasks like any slot, and
+    backups only come after Hadoop's 60 s speculative lag."""
+    conf = JobConf()
+    conf.set_boolean("hbmr.gpu.simulate", True)
+    conf.set_int("mapred.tasktracker.map.gpu.tasks.maximum", 1)
+    conf.set_float("hbmr.gpu.simulate.task.ms", 5)
+    conf.set("hbmr.scheduler.policy", "stock")
+    with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=1) as cl:
+        job = split_sleep_conf(6, map_ms=600, base=conf)
+        t0 = time.time()
+        rj = cl.submit_job(job)
+        assert rj.waitForCompletion(30) and rj.isSuccessful()
+        took = time.time() - t0
+        cs = rj.getCounters()
+    assert cs.get(JIP, "CPU_MAP_TASKS") >= 1
+    assert took >= 0.55
