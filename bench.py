@@ -145,7 +145,11 @@ def main():
             "maps_launched": n_maps, "gpu_maps": gpu_maps, "cpu_maps": cpu_maps,
             "warmup_seconds": round(t_warm, 2),
             "final_shift": hist[-1].get("shift") if hist else None,
-            "cost_model": {k: {s: round(v["mean"], 6) for s, v in d.items()} for k, d in cm.items()},
+            # per job signature: completed-task mean seconds on each slot type and the
+            # number of tasks behind it (the CPU probe may still be running)
+            "cost_model": {k: {s: {"mean_s": round(v["mean"], 6), "n": v["n"],
+                                   "running": v["running"]} for s, v in d.items()}
+                           for k, d in cm.items()},
             "baseline_note": "BASELINE.md publishes only a ratio (hybrid 1.93x faster than stock "
                              "Hadoop scheduling on 2010 hardware); no absolute number to divide by",
         }

@@ -850,7 +850,8 @@ class JobTracker:
         for other in tip.running_attempts():
             if other is not a:
                 if tip.is_map and not other.run_on_gpu and \
-                        self.cost_model.stats(jip.signature, False).n == 0:
+                        self.cost_model.stats(jip.signature, False).n == 0 and \
+                        self.cost_model.is_probe(jip.signature, other.aid, False):
                     # the signature's CPU profiling probe lost to its GPU backup:
                     # let it finish detached (output ignored, slot held) so the
                     # cost model learns the real CPU time instead of a censored

@@ -21,6 +21,7 @@ from ..utils.reflection import new_instance
 from . import counters as C
 from .ids import JobID, TaskAttemptID, TaskID
 from .jobclient import FAILED, RUNNING, SUCCEEDED, RunningJob, _Waitable
+from .child import use_child_process
 from .task import MapOutputLocation, MapTask, ReduceTask
 
 log = logging.getLogger("hbmr.local")
@@ -110,12 +111,31 @@ class LocalJobRunner:
                 aid = TaskAttemptID(TaskID(jid, True, i), 0)
                 maps.append(MapTask(job, aid, i, sp))
             nthreads = max(1, job.get_int("mapred.local.map.tasks.maximum", 1))
+            # parallel local maps in child processes (past the GIL) when asked for
+            children = None
+            if nthreads > 1 and use_child_process(job):
+                from .child import ChildManager
+                children = ChildManager(f"local-{jid}", local_root, job)
+                conf_dict = job.to_dict()
 
             def run_map(i):
                 if lj.killed.is_set():
                     raise RuntimeError("job killed")
                 t = maps[i]
-                outputs[i] = t.run(os.path.join(local_root, str(t.attempt_id)))
+                work = os.path.join(local_root, str(t.attempt_id))
+                if children is not None:
+                    sp = t.split
+                    payload = {"attempt_id": str(t.attempt_id), "is_map": True, "partition": i,
+                               "split": {"kind": "class",
+                                         "cls": f"{type(sp).__module__}:{type(sp).__qualname__}",
+                                         "data": sp.serialize().hex()},
+                               "conf": conf_dict, "work_dir": work, "progress_interval": 1.0}
+                    t.start_time = time.time()
+                    outputs[i] = children.run_task(str(jid), job, payload, t.reporter,
+                                                   threading.Event())
+                    t.finish_time = time.time()
+                else:
+                    outputs[i] = t.run(work)
                 lj.map_reports.append(TaskReport(t.attempt_id.task, 1.0, SUCCEEDED, t.start_time,
                                                  t.finish_time, t.reporter.counters))
                 lj._counters.incr_all(t.reporter.counters)
@@ -125,8 +145,12 @@ class LocalJobRunner:
                 for i in range(len(maps)):
                     run_map(i)
             else:
-                with cf.ThreadPoolExecutor(nthreads) as ex:
-                    list(ex.map(run_map, range(len(maps))))
+                try:
+                    with cf.ThreadPoolExecutor(nthreads) as ex:
+                        list(ex.map(run_map, range(len(maps))))
+                finally:
+                    if children is not None:
+                        children.shutdown()
             lj._counters.incr(C.JOB_GROUP, C.TOTAL_LAUNCHED_MAPS, len(maps))
             lj._counters.incr(C.JOB_GROUP, C.CPU_MAP_TASKS, len(maps))
             st.map_progress = 1.0

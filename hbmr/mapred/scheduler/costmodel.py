@@ -32,6 +32,7 @@ class TimeStats:
     max: float = 0.0
     running: dict = field(default_factory=dict)   # attempt -> start time
     lower_bound: float = 0.0   # censored: killed/failed attempts ran at least this long
+    probe: str | None = None   # the first attempt on this slot type (profiling probe)
 
     def add(self, dt: float, alpha: float):
         self.n += 1
@@ -71,9 +72,16 @@ class CostModel:
             d = self._stats[sig] = {"cpu": TimeStats(), "gpu": TimeStats()}
         return d
 
+    def is_probe(self, sig, attempt, on_gpu) -> bool:
+        with self._lock:
+            return self._get(sig)["gpu" if on_gpu else "cpu"].probe == attempt
+
     def task_started(self, sig, attempt, on_gpu, t):
         with self._lock:
-            self._get(sig)["gpu" if on_gpu else "cpu"].running[attempt] = t
+            st = self._get(sig)["gpu" if on_gpu else "cpu"]
+            st.running[attempt] = t
+            if st.probe is None and st.n == 0:
+                st.probe = attempt
 
     def task_finished(self, sig, attempt, on_gpu, start, finish, succeeded=True):
         with self._lock:
@@ -114,8 +122,9 @@ class CostModel:
 
     def snapshot(self):
         with self._lock:
-            return {sig: {k: {"n": v.n, "mean": v.mean, "ewma": v.ewma, "running": len(v.running)}
-                          for k, v in d.items()} for sig, d in self._stats.items()}
+            return {sig: {k: {"n": v.n, "mean": v.mean, "ewma": v.ewma, "running": len(v.running),
+                              "lower_bound": v.lower_bound} for k, v in d.items()}
+                    for sig, d in self._stats.items()}
 
 
 def min_makespan_cpu_tasks(pending: int, cpu_slots: int, gpu_slots: int, t_cpu: float,

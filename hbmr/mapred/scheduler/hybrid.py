@@ -95,11 +95,15 @@ class HybridTaskScheduler(TaskScheduler):
             return pending if not (pending < accel * total_gpu) else 0
         # hybrid (min-makespan)
         cs, gs = cm.stats(sig, False), cm.stats(sig, True)
-        t_cpu, _ = cs.estimate(now)
+        t_cpu, cpu_lb = cs.estimate(now)
         t_gpu, _ = gs.estimate(now)
         if t_cpu is None:
             # profile: one CPU probe per signature (if none is running)
             return 1 if running_cpu == 0 and not cs.running else 0
+        if cs.n == 0 and cpu_lb and cs.probe in cs.running:
+            # only a censored bound while the probe still runs: wait for it
+            # rather than betting more slots on a still-growing estimate
+            return 0
         if t_gpu is None:
             return 0 if running_cpu else min(1, pending)
         x = min_makespan_cpu_tasks(pending + running_cpu, total_cpu, total_gpu, t_cpu, t_gpu)

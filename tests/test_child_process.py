@@ -174,3 +174,16 @@ def test_timeout_kills_child(tmp_path):
     assert not rj.isSuccessful()
     assert "failed to report status" in (rj.getFailureInfo() or "")
     assert not pids                    # the hung child was SIGKILLed
+
+
+def test_local_runner_parallel_child_maps(tmp_path):
+    inp, cnt = _words(tmp_path)
+    conf = JobConf()
+    conf.set("mapred.job.tracker", "local")
+    conf.set_int("mapred.local.map.tasks.maximum", 3)
+    conf.set("mapred.task.isolation", "process")
+    job = wordcount.make_job(str(inp), str(tmp_path / "out"), reduces=1, conf=conf)
+    rj = JobClient.runJob(job, verbose=False)
+    assert {k: int(v) for k, v in _read(tmp_path / "out").items()} == dict(cnt)
+    assert rj.getCounters().get("org.apache.hadoop.mapred.Task$Counter",
+                                "MAP_INPUT_RECORDS") == 240

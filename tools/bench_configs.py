@@ -56,6 +56,10 @@ def wordcount(a):
         words = _text(inp, a.mb)
         conf = JobConf()
         conf.set("mapred.job.tracker", "local")
+        if a.procs > 1:
+            # LocalJobRunner maps on child processes (the reference's runner is serial)
+            conf.set_int("mapred.local.map.tasks.maximum", a.procs)
+            conf.set("mapred.task.isolation", "process")
         times = []
         for i in range(a.steps):
             job = W.make_job(inp, os.path.join(tmp, f"out{i}"), reduces=1, conf=conf)
@@ -66,7 +70,8 @@ def wordcount(a):
         best = min(times)
         print(json.dumps({
             "config": "WordCount on LocalJobRunner, CPU-only mappers (BASELINE config 1)",
-            "input_mb": a.mb, "words": words, "job_seconds": [round(t, 3) for t in times],
+            "input_mb": a.mb, "words": words, "map_processes": a.procs,
+            "job_seconds": [round(t, 3) for t in times],
             "mb_per_s": round(a.mb / best, 2), "words_per_s": round(words / best, 1),
             "map_input_records": cs.get("org.apache.hadoop.mapred.Task$Counter",
                                         "MAP_INPUT_RECORDS"),
@@ -184,6 +189,7 @@ def main():
     ap.add_argument("--jobs", type=int, default=20)
     ap.add_argument("--maps", type=int, default=1)
     ap.add_argument("--lines", type=int, default=100)
+    ap.add_argument("--procs", type=int, default=1, help="wordcount: parallel map processes")
     a = ap.parse_args()
     {"wordcount": wordcount, "kmeans-pipes": kmeans_pipes, "mrbench": mrbench}[a.which](a)
 
