@@ -144,9 +144,13 @@ class SplitSleepJob(SplitJob):
     def split_nbytes(self, data):
         return 0
 
+    def load_split_sample(self, spec, device, fraction):
+        return ("sample", fraction)
+
     def map_cpu(self, ctx, data):
+        frac = data[1] if isinstance(data, tuple) else 1.0   # a sampled probe sleeps pro rata
         if self.map_ms > 0:
-            time.sleep(self.map_ms / 1000.0)
+            time.sleep(self.map_ms * frac / 1000.0)
         return 1
 
     def map_gpu(self, ctx, data):

@@ -16,6 +16,7 @@ Subclasses implement:
 * ``load_split(spec, device)``     -> split data on ``device`` ("cpu" for CPU slots)
 * ``map_gpu(ctx, data)``           -> map output (device tensors), kernels on ctx.stream
 * ``map_cpu(ctx, data)``           -> map output (host tensors)
+* ``load_split_sample(spec, dev, f)`` -> first fraction f of a split (profiling probes)
 * ``combine(ctx, outputs)``        -> one combined output on this tracker
 * ``reduce(ctx, combined)``        -> result (collectives via ctx.comm)
 * ``job_succeeded(jip)``           -> optional hook on the JobTracker
@@ -58,6 +59,13 @@ class SplitJob:
 
     def load_split(self, spec: SplitSpec, device):
         raise NotImplementedError
+
+    def load_split_sample(self, spec: SplitSpec, device, fraction: float):
+        """The first ``fraction`` of a split (a sampled CPU profiling probe times
+        the map on it and scales up).  Default: load and slice along dim 0."""
+        data = self.load_split(spec, device)
+        n = max(1, int(data.shape[0] * fraction))
+        return data[:n]
 
     def split_nbytes(self, data) -> int:
         try:

@@ -78,7 +78,7 @@ class TrackerInfo:
 class Attempt:
     __slots__ = ("aid", "tip", "tracker", "run_on_gpu", "device", "state", "progress",
                  "start", "finish", "counters", "output", "diagnostic", "speculative",
-                 "device_time", "_released", "profile_only")
+                 "device_time", "_released", "profile_only", "profile_fraction")
 
     def __init__(self, aid, tip, tracker, run_on_gpu, device, speculative=False):
         self.aid = aid
@@ -96,6 +96,7 @@ class Attempt:
         self.speculative = speculative
         self.device_time = 0.0
         self.profile_only = False   # a CPU profiling probe left running after its TIP won
+        self.profile_fraction = 0.0  # >0: sampled probe, timed on this fraction of a split
 
 
 class TaskInProgress:
@@ -819,6 +820,14 @@ class JobTracker:
         jip = tip.job
         a.state = P.SUCCEEDED
         self._release(a)
+        if a.profile_fraction:
+            # sampled profiling probe: its only product is the CPU time estimate
+            # (measured on the sample, scaled to a whole split)
+            dt = max(0.0, a.finish - a.start) / a.profile_fraction
+            self.cost_model.task_finished(jip.signature, a.aid, False, a.start, a.start + dt)
+            self.history.log("PROFILE_FINISHED", attempt=a.aid, tracker=a.tracker,
+                             fraction=a.profile_fraction, est_seconds=dt)
+            return
         if tip.is_map:
             if a.run_on_gpu and a.device_time > 0:
                 # GPU attempts are timed by HIP events: device time, not queue time
@@ -888,6 +897,9 @@ class JobTracker:
         if tip.is_map:
             self.cost_model.task_finished(jip.signature, a.aid, a.run_on_gpu, a.start,
                                           time.time(), succeeded=False)
+        if a.profile_fraction:
+            self.history.log("PROFILE_FAILED", attempt=a.aid, tracker=a.tracker, diag=diag[:500])
+            return
         self.history.log("TASK_FAILED" if not killed else "TASK_KILLED", attempt=a.aid,
                          tracker=a.tracker, gpu=a.run_on_gpu, diag=diag[:500])
         METRICS.inc("hbmr_tasks_failed_total", help="failed or killed task attempts",
@@ -934,11 +946,18 @@ class JobTracker:
 
     # -- launching (called by the scheduler under the lock) -------------------------------
     def launch(self, tr: TrackerInfo, tip: TaskInProgress, on_gpu=False, device=-1,
-               speculative=False, extra=None):
+               speculative=False, extra=None, profile_fraction=0.0):
         jip = tip.job
         aid = tip.new_attempt_id()
         a = Attempt(str(aid), tip, tr.name, on_gpu, device, speculative)
-        tip.attempts[a.aid] = a
+        if profile_fraction:
+            # a sampled CPU probe rides on a TIP without being one of its attempts:
+            # the TIP stays pending for real execution
+            a.profile_fraction = profile_fraction
+            a.profile_only = True
+            jip.counters.incr(C.JOB_GROUP, "PROFILE_TASKS")
+        else:
+            tip.attempts[a.aid] = a
         self.attempt_index[a.aid] = a
         tr.running.add(a.aid)
         if tip.is_map:
@@ -951,7 +970,8 @@ class JobTracker:
                 tr.running_cpu += 1
                 jip.running_cpu += 1
             self.cost_model.task_started(jip.signature, a.aid, on_gpu, a.start)
-            jip.counters.incr(C.JOB_GROUP, C.TOTAL_LAUNCHED_MAPS)
+            if not profile_fraction:
+                jip.counters.incr(C.JOB_GROUP, C.TOTAL_LAUNCHED_MAPS)
         else:
             if not jip.t_first_reduce:
                 jip.t_first_reduce = a.start
@@ -960,7 +980,8 @@ class JobTracker:
         spec = P.TaskSpec(attempt_id=a.aid, job_id=str(jip.job_id), is_map=tip.is_map,
                           partition=tip.partition, run_on_gpu=on_gpu, gpu_device_id=device,
                           split=tip.split or {}, num_maps=len(jip.maps),
-                          num_reduces=len(jip.reduces), collective=jip.collective_reduce)
+                          num_reduces=len(jip.reduces), collective=jip.collective_reduce,
+                          profile_fraction=profile_fraction)
         if extra:
             for k, v in extra.items():
                 setattr(spec, k, v)

@@ -115,6 +115,7 @@ class TaskSpec:
     map_outputs: list = field(default_factory=list)
     collective: bool = False
     conf: dict | None = None                      # job conf (sent once per tracker per job)
+    profile_fraction: float = 0.0                 # >0: sampled CPU profiling probe
 
     def to_dict(self):
         return dict(self.__dict__)   # shallow: fields are plain values / dicts

@@ -59,6 +59,9 @@ class HybridTaskScheduler(TaskScheduler):
         # TaskInProgress.java) and lag in progress; the GPU-aware early backup
         # of CPU stragglers is part of the hybrid design
         self.stock_lag = conf.get_int("hbmr.speculative.stock.lag.ms", 60000) / 1000.0
+        # split jobs are CPU-profiled by a sampled probe: the map on the first
+        # 1/32 of one split, timed and scaled, while the GPUs run every real task
+        self.probe_fraction = conf.get_float("hbmr.costmodel.probe.fraction", 1 / 32)
         # cap map launches per heartbeat response so a tracker can start the
         # first tasks while the rest are still being assigned (the response
         # says "more" and the tracker calls right back)
@@ -98,6 +101,8 @@ class HybridTaskScheduler(TaskScheduler):
         t_cpu, cpu_lb = cs.estimate(now)
         t_gpu, _ = gs.estimate(now)
         if t_cpu is None:
+            if self._sampled_probing(jip):
+                return 0   # the sampled probe (assign_tasks) profiles the CPU
             # profile: one CPU probe per signature (if none is running)
             return 1 if running_cpu == 0 and not cs.running else 0
         if cs.n == 0 and cpu_lb and cs.probe in cs.running:
@@ -151,6 +156,11 @@ class HybridTaskScheduler(TaskScheduler):
             # ---- CPU maps (first, as the fork's loop order, JobQueueTaskScheduler.java
             # :295-387: the cost model decides how many; a CPU profile probe must
             # not be starved by the GPUs' much larger queue budget)
+            if cpu_free > 0 and total_gpu > 0 and self._needs_sampled_probe(jip):
+                actions.append(jt.launch(tr, jip.maps[0], on_gpu=False,
+                                         profile_fraction=self.probe_fraction))
+                cpu_free -= 1
+                budget -= 1
             if cpu_free > 0 and jip.pending_maps:
                 allowed = min(self._cpu_allowed(jip, total_cpu, total_gpu, now),
                               self.job_limit(jip, "cpu"))
@@ -210,6 +220,16 @@ class HybridTaskScheduler(TaskScheduler):
                 break
             actions.append(self.jt.launch(tr, tip, on_gpu=True, device=dev, speculative=True))
             gpu_free[dev] -= 1
+
+    def _sampled_probing(self, jip) -> bool:
+        return (self.policy in ("hybrid", "optional") and self.probe_fraction > 0 and
+                jip.split_job is not None and jip.cpu_capable and jip.gpu_capable)
+
+    def _needs_sampled_probe(self, jip) -> bool:
+        if not self._sampled_probing(jip):
+            return False
+        cs = self.jt.cost_model.stats(jip.signature, False)
+        return cs.n == 0 and not cs.running and cs.lower_bound == 0
 
     # -- policy hooks (FIFO by priority here; fair/capacity override) --------------------
     def begin_round(self, tr, total_cpu, total_gpu):

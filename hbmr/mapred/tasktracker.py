@@ -154,7 +154,13 @@ class TaskTracker:
         self._news = threading.Event()
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
-        self.cpu_pool = cf.ThreadPoolExecutor(max(1, self.cpu_slots), thread_name_prefix=f"{self.name}-cpu")
+        # CPU map slots run below the control plane's scheduling priority: a
+        # compute-bound CPU map must not delay heartbeats and GPU launches
+        # (threads it starts inherit the nice value)
+        nice = conf.get_int("hbmr.cpu.slot.nice", 10)
+        self.cpu_pool = cf.ThreadPoolExecutor(max(1, self.cpu_slots),
+                                              thread_name_prefix=f"{self.name}-cpu",
+                                              initializer=_lower_priority, initargs=(nice,))
         self.reduce_pool = cf.ThreadPoolExecutor(max(1, self.reduce_slots),
                                                  thread_name_prefix=f"{self.name}-red")
         self.gpu_pipes_pool = cf.ThreadPoolExecutor(
@@ -406,6 +412,16 @@ class TaskTracker:
                 ctx = TaskContext(self, js, spec, rep, device="cpu")
                 from ..gpu.splitjob import SplitSpec
                 sspec = SplitSpec.from_dict(spec.split)
+                if spec.profile_fraction:
+                    # sampled profiling probe: time the CPU map on a slice; the
+                    # output is dropped (the GPUs run the real task)
+                    sample = js.split_job.load_split_sample(sspec, "cpu", spec.profile_fraction)
+                    run.status.start_time = time.time()
+                    js.split_job.map_cpu(ctx, sample)
+                    run.task.reporter.counters = C.Counters()
+                    self._finish(run, P.SUCCEEDED, output={"tracker": self.name, "where": "cpu",
+                                                           "profile": True})
+                    return
                 data, hit = self.split_cache.get_or_load(
                     sspec.key, "cpu", lambda: js.split_job.load_split(sspec, "cpu"),
                     js.split_job.split_nbytes)
@@ -520,6 +536,14 @@ class TaskTracker:
     def job_result(self, job_id):
         js = self.jobs.get(str(job_id))
         return None if js is None else js.result
+
+
+def _lower_priority(nice):
+    if nice > 0 and hasattr(os, "setpriority"):
+        try:
+            os.setpriority(os.PRIO_PROCESS, threading.get_native_id(), nice)
+        except OSError:
+            pass
 
 
 class _SplitTaskShim:

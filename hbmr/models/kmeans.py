@@ -238,6 +238,15 @@ class KMeansSplitJob(SplitJob):
         # bf16 is the storage precision of the points on every slot type
         return x.to(torch.bfloat16)
 
+    def load_split_sample(self, spec: SplitSpec, device, fraction: float):
+        if spec.kind == "synthetic":
+            p = dict(spec.params)
+            p["n"] = max(1, int(p["n"] * fraction))
+            spec = SplitSpec(spec.index, spec.key + f":sample{fraction}", spec.kind, p,
+                             spec.locations, spec.length)
+            return self.load_split(spec, device)
+        return super().load_split_sample(spec, device, fraction)
+
     def load_split(self, spec: SplitSpec, device):
         from ..ops import kmeans as km
         xb = self._load_fp32(spec, device)

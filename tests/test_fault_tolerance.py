@@ -135,6 +135,7 @@ def test_speculative_gpu_backup_of_cpu_straggler():
     conf.set_int("mapred.tasktracker.map.gpu.tasks.maximum", 1)
     conf.set_float("hbmr.gpu.simulate.task.ms", 5)
     conf.set_int("hbmr.gpu.queue.depth", 1)
+    conf.set_float("hbmr.costmodel.probe.fraction", 0)   # whole-task CPU probe
     with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=1) as cl:
         job = split_sleep_conf(6, map_ms=1500, base=conf)     # CPU map tasks sleep 1.5 s
         job.set_boolean("mapred.map.tasks.speculative.execution", True)
@@ -175,3 +176,35 @@ def test_stock_policy_waits_for_cpu_stragglers():
         cs = rj.getCounters()
     assert cs.get(JIP, "CPU_MAP_TASKS") >= 1
     assert took >= 0.55
+
+
+def test_sampled_cpu_probe_profiles_without_straggling():
+    """Hybrid scheduling of a split job: the CPU is profiled by a probe that runs
+    the map on 1/8 of a split (output dropped) while the GPU slots run every
+    real task; the scaled probe time lands in the cost model."""
+    conf = JobConf()
+    conf.set_boolean("hbmr.gpu.simulate", True)
+    conf.set_int("mapred.tasktracker.map.gpu.tasks.maximum", 1)
+    conf.set_float("hbmr.gpu.simulate.task.ms", 5)
+    conf.set_float("hbmr.costmodel.probe.fraction", 0.125)
+    with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=2) as cl:
+        job = split_sleep_conf(8, map_ms=800, base=conf)
+        t0 = time.time()
+        rj = cl.submit_job(job)
+        assert rj.waitForCompletion(30) and rj.isSuccessful()
+        took = time.time() - t0
+        cs = rj.getCounters()
+        sig = rj._impl.jip.signature
+        deadline = time.time() + 5
+        while cl.jt.cost_model.stats(sig, False).n == 0 and time.time() < deadline:
+            time.sleep(0.02)
+        st = cl.jt.cost_model.stats(sig, False)
+        # a second job of the same signature starts profiled: no probe, no CPU maps
+        rj2 = cl.submit_job(split_sleep_conf(8, map_ms=800, base=conf))
+        assert rj2.waitForCompletion(30) and rj2.isSuccessful()
+        cs2 = rj2.getCounters()
+    assert cs.get(JIP, "PROFILE_TASKS") == 1
+    assert (cs.get(JIP, "CPU_MAP_TASKS") or 0) == 0
+    assert took < 0.5                      # nobody waited for the 800 ms CPU map
+    assert st.n == 1 and 0.7 < st.mean < 1.2   # 100 ms sample scaled by 8
+    assert not cs2.get(JIP, "PROFILE_TASKS") and not cs2.get(JIP, "CPU_MAP_TASKS")
