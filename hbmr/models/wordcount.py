@@ -46,3 +46,144 @@ def main(argv=None):
     job = make_job(a.input, a.output, a.reduces)
     rj = JobClient.runJob(job)
     return 0 if rj.isSuccessful() else 1
+
+
+# --------------------------------------------------------------------------- GPU WordCount
+# The same job as a split-level GPU job: a text split
+# is read into HBM with LineRecordReader's boundary rule, tokenized and counted
+# by native/kernels/text.hip (exact hash aggregation = the fused combiner), the
+# per-tracker tables are merged and hash-partitioned like HashPartitioner, the
+# shuffle is one all-to-all-v of "word\n" bytes + one of counts (RCCL over
+# xGMI), and each tracker writes its partition sorted by Text key order, in
+# TextOutputFormat's "word\tcount" lines — the classic job's output, byte for
+# byte.
+from ..gpu.splitjob import SplitJob, SplitSpec  # noqa: E402
+
+
+def read_text_split(path, start, length, chunk=1 << 16) -> bytes:
+    """Bytes of the lines a LineRecordReader over (path, start, length) returns,
+    newlines included: the first partial line is skipped unless start == 0, and
+    the line running through the split end is read to its end."""
+    from ..fs import strip_scheme
+    end = start + length
+    with open(strip_scheme(path), "rb") as f:
+        f.seek(start)
+        begin = start
+        if start != 0:
+            while True:
+                buf = f.read(chunk)
+                if not buf:
+                    return b""
+                i = buf.find(b"\n")
+                if i >= 0:
+                    begin += i + 1
+                    break
+                begin += len(buf)
+        if begin > end:
+            return b""
+        f.seek(begin)
+        body = f.read(end - begin)
+        # finish the line that contains offset `end` (it starts at or before end)
+        tail = []
+        while True:
+            buf = f.read(chunk)
+            if not buf:
+                break
+            i = buf.find(b"\n")
+            if i >= 0:
+                tail.append(buf[:i + 1])
+                break
+            tail.append(buf)
+        return body + b"".join(tail)
+
+
+class WordCountSplitJob(SplitJob):
+    collective_reduce = True
+    needs_reduce = True
+
+    def configure(self, conf):
+        self.conf = conf
+        self.out = conf.get("mapred.output.dir")
+
+    def get_splits(self, conf, trackers):
+        from ..mapred.formats import TextInputFormat
+        from ..mapred.jobconf import JobConf
+        splits = TextInputFormat().getSplits(JobConf(conf), max(1, conf.get_num_map_tasks()))
+        out = []
+        for i, s in enumerate(splits):
+            loc = [trackers[i * len(trackers) // len(splits)]] if trackers else []
+            key = f"wc:{s.path}:{s.start}:{s.length}"
+            out.append(SplitSpec(i, key, "file", {"path": s.path, "start": s.start,
+                                                  "length": s.length}, loc, s.length))
+        return out
+
+    def load_split(self, spec: SplitSpec, device):
+        import torch
+        p = spec.params
+        data = read_text_split(p["path"], p["start"], p["length"])
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8) if data else \
+            torch.empty(0, dtype=torch.uint8)
+        return t if str(device) == "cpu" else t.to(device)
+
+    def _count(self, ctx, data):
+        from ..mapred import counters as C
+        from ..ops import text
+        ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_BYTES, int(data.numel()))
+        return text.count_words(data, getattr(ctx, "stream", None))
+
+    def map_gpu(self, ctx, data):
+        return self._count(ctx, data)
+
+    def map_cpu(self, ctx, data):
+        return self._count(ctx, data)
+
+    def combine(self, ctx, outputs):
+        import torch
+        from ..ops import text
+        dev = ctx.device if ctx.device is not None else torch.device("cpu")
+        blobs = [b.to(dev) for b, _ in outputs]
+        counts = [c.to(dev) for _, c in outputs]
+        blob = torch.cat(blobs) if blobs else torch.empty(0, dtype=torch.uint8, device=dev)
+        cnt = torch.cat(counts) if counts else torch.empty(0, dtype=torch.int64, device=dev)
+        return text.merge_tables(blob, cnt, max(1, ctx.world_size))
+
+    def reduce(self, ctx, combined):
+        from ..mapred import counters as C
+        from ..ops import text
+        blob, counts, part_bytes, part_words = combined
+        rblob, _ = ctx.comm.all_to_all_v(blob, part_bytes)
+        rcounts, _ = ctx.comm.all_to_all_v(counts, part_words)
+        mblob, mcounts, _, _ = text.merge_tables(rblob, rcounts, 1)
+        items = text.sorted_items(mblob, mcounts)
+        total = sum(n for _, n in items)
+        ctx.reporter.incrCounter(C.TASK_GROUP, C.REDUCE_INPUT_GROUPS, len(items))
+        ctx.reporter.incrCounter(C.TASK_GROUP, C.REDUCE_OUTPUT_RECORDS, len(items))
+        if self.out:
+            import os
+            tmp = os.path.join(self.out, "_temporary")
+            os.makedirs(tmp, exist_ok=True)
+            name = f"part-{ctx.rank:05d}"
+            with open(os.path.join(tmp, name), "wb") as f:
+                f.write(b"".join(w + b"\t" + str(n).encode() + b"\n" for w, n in items))
+            os.replace(os.path.join(tmp, name), os.path.join(self.out, name))
+        return {"distinct": len(items), "words": total}
+
+    def job_succeeded(self, jip):
+        import os
+        import shutil
+        if self.out:
+            shutil.rmtree(os.path.join(self.out, "_temporary"), ignore_errors=True)
+            open(os.path.join(self.out, "_SUCCESS"), "wb").close()
+
+
+def gpu_job(inputs, output, base=None, maps=None) -> JobConf:
+    """WordCount as a split-level job (GPU map slots, CPU slots per the hybrid
+    cost model)."""
+    job = JobConf(base)
+    job.set_job_name("wordcount-gpu")
+    job.set("hbmr.splitjob.class", "hbmr.models.wordcount:WordCountSplitJob")
+    FileInputFormat.setInputPaths(job, *([inputs] if isinstance(inputs, str) else inputs))
+    FileOutputFormat.setOutputPath(job, output)
+    if maps:
+        job.set_num_map_tasks(maps)
+    return job

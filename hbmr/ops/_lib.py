@@ -53,6 +53,16 @@ _SIGS = {
     "hbmr_split_offsets": (c_int, [c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_int,
                                    c_void_p, c_void_p]),
     "hbmr_check_sorted": (c_int, [c_void_p, c_void_p, c_long, c_void_p, c_void_p]),
+    # text / WordCount (native/kernels/text.hip)
+    "hbmr_wc_tiles": (c_long, [c_long]),
+    "hbmr_wc_tokenize_count": (c_int, [c_void_p, c_long, c_void_p, c_void_p]),
+    "hbmr_wc_tokenize_write": (c_int, [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "hbmr_wc_insert": (c_int, [c_void_p, c_long, c_void_p, c_void_p, c_void_p, c_long, c_void_p,
+                               c_void_p, c_long, c_void_p, c_void_p]),
+    "hbmr_wc_compact": (c_int, [c_void_p, c_long, c_void_p, c_void_p, c_long, c_int, c_void_p,
+                                c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "hbmr_wc_pack": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p,
+                             c_void_p]),
     # GEMM (native/kernels/gemm.hip)
     "hbmr_gemm_bf16_tn": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_long, c_long,
                                   ctypes.c_float, c_int, c_void_p]),

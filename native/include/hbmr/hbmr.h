@@ -66,6 +66,22 @@ long hbmr_radix_sort_workspace_bytes(long n);
 int hbmr_gemm_bf16_tn(const void* A, const void* Bt, void* C, long M, long N, long K, float alpha,
                       int out_bf16, hipStream_t st);
 #endif
+// ---- text / WordCount (native/kernels/text.hip) ---------------------------------
+#ifndef HBMR_NO_HIP_DECLS
+long hbmr_wc_tiles(long n);
+int hbmr_wc_tokenize_count(const uint8_t* buf, long n, uint32_t* tile_counts, hipStream_t st);
+int hbmr_wc_tokenize_write(const uint8_t* buf, long n, const long* tile_base, uint32_t* starts,
+                           uint32_t* lens, hipStream_t st);
+int hbmr_wc_insert(const uint8_t* buf, long n, const uint32_t* starts, const uint32_t* lens,
+                   const int64_t* weights, long nwords, uint64_t* tkeys, uint64_t* tcounts,
+                   long cap, int* overflow, hipStream_t st);
+int hbmr_wc_compact(const uint8_t* buf, long n, const uint64_t* tkeys, const uint64_t* tcounts,
+                    long cap, int R, uint32_t* ustart, uint32_t* ulen, int64_t* ucount,
+                    int32_t* upart, unsigned int* counter, hipStream_t st);
+int hbmr_wc_pack(const uint8_t* buf, const uint32_t* ustart, const uint32_t* ulen,
+                 const int64_t* order, long nu, const int64_t* out_off, uint8_t* out,
+                 hipStream_t st);
+#endif
 int hbmr_kmeans_padded_k(int k);
 long hbmr_kmeans_accum_workspace_bytes(long n, int k);
 long hbmr_kmeans_batch_workspace_bytes(long total_n, int ntasks, int k);

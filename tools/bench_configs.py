@@ -3,6 +3,7 @@
   python tools/bench_configs.py wordcount    [--mb 64]                   # config 1
   python tools/bench_configs.py kmeans-pipes [--points 1000000 --k 64]   # config 2
   python tools/bench_configs.py mrbench      [--jobs 20]                 # job-launch latency
+  python tools/bench_configs.py wordcount-gpu [--mb 1024 --files 16]      # GPU WordCount
 
 config 1: WordCount through the LocalJobRunner (mapred.job.tracker=local,
 CPU-only mappers), synthetic RandomTextWriter-style text.
@@ -77,6 +78,55 @@ def wordcount(a):
                                         "MAP_INPUT_RECORDS"),
             "combine_output_records": cs.get("org.apache.hadoop.mapred.Task$Counter",
                                              "COMBINE_OUTPUT_RECORDS")}), flush=True)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def wordcount_gpu(a):
+    """WordCount as a split-level GPU job (text.hip): cold job (file → HBM) and
+    warm jobs (splits resident in HBM), output checked against a CPU count."""
+    import collections
+
+    import torch
+
+    from hbmr.mapred.cluster import LocalCluster
+    from hbmr.mapred.jobconf import JobConf
+    from hbmr.models import wordcount as W
+    tmp = tempfile.mkdtemp(prefix="hbmr-wcg-")
+    try:
+        inp = os.path.join(tmp, "in")
+        words = _text(inp, a.mb, files=a.files)
+        conf = JobConf()
+        conf.set_int("hbmr.gpu.queue.depth", 16)
+        with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=a.cpu_slots) as cl:
+            times = []
+            for i in range(a.steps + 1):
+                job = W.gpu_job(inp, os.path.join(tmp, f"out{i}"), base=conf, maps=a.files)
+                t = time.perf_counter()
+                rj = cl.submit_job(job)
+                rj.waitForCompletion()
+                torch.cuda.synchronize()
+                times.append(time.perf_counter() - t)
+                if not rj.isSuccessful():
+                    raise RuntimeError(rj.getFailureInfo())
+            cs = rj.getCounters()
+        got = {}
+        with open(os.path.join(tmp, f"out{a.steps}", "part-00000"), "rb") as f:
+            for line in f:
+                w, n = line.rstrip(b"\n").split(b"\t")
+                got[w] = int(n)
+        ref = collections.Counter()
+        for fn in os.listdir(inp):
+            with open(os.path.join(inp, fn), "rb") as f:
+                ref.update(f.read().split())
+        best = min(times[1:]) if len(times) > 1 else times[0]
+        print(json.dumps({
+            "config": "WordCount as a split-level GPU job (1 MI355X, text.hip kernels)",
+            "input_mb": a.mb, "words": words, "map_tasks": a.files, "cpu_slots": a.cpu_slots,
+            "cold_job_s": round(times[0], 3), "warm_job_ms": [round(1e3 * t, 2) for t in times[1:]],
+            "warm_gb_per_s": round(a.mb / 1024 / best, 2), "words_per_s": round(words / best, 1),
+            "gpu_maps": cs.get("org.apache.hadoop.mapred.JobInProgress$Counter", "GPU_MAP_TASKS"),
+            "output_matches_cpu_count": got == dict(ref)}), flush=True)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
@@ -179,7 +229,7 @@ def mrbench(a):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", choices=["wordcount", "kmeans-pipes", "mrbench"])
+    ap.add_argument("which", choices=["wordcount", "wordcount-gpu", "kmeans-pipes", "mrbench"])
     ap.add_argument("--mb", type=int, default=64)
     ap.add_argument("--points", type=int, default=1_000_000)
     ap.add_argument("--dims", type=int, default=128)
@@ -190,8 +240,10 @@ def main():
     ap.add_argument("--maps", type=int, default=1)
     ap.add_argument("--lines", type=int, default=100)
     ap.add_argument("--procs", type=int, default=1, help="wordcount: parallel map processes")
+    ap.add_argument("--cpu-slots", type=int, default=0)
     a = ap.parse_args()
-    {"wordcount": wordcount, "kmeans-pipes": kmeans_pipes, "mrbench": mrbench}[a.which](a)
+    {"wordcount": wordcount, "wordcount-gpu": wordcount_gpu, "kmeans-pipes": kmeans_pipes,
+     "mrbench": mrbench}[a.which](a)
 
 
 if __name__ == "__main__":
