@@ -31,21 +31,24 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def _text(path, mb, seed=3, files=8):
-    import random
-    rnd = random.Random(seed)
-    words = [f"w{i:04d}" for i in range(2000)] + ["the", "a", "of", "gpu", "map", "reduce"]
+    """RandomTextWriter-style text: words from a 2,000-word vocabulary (Zipf-ish
+    draw), space separated, ~10 words per line.  numpy-generated so GBs are quick."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    vocab = np.array([list(f"w{i:04d}".encode()) for i in range(2000)], dtype=np.uint8)
     os.makedirs(path, exist_ok=True)
-    per = mb * (1 << 20) // files
-    total_words = 0
+    per_words = mb * (1 << 20) // 6 // files
+    total = 0
     for f in range(files):
-        with open(os.path.join(path, f"part-{f:05d}"), "w") as fh:
-            n = 0
-            while n < per:
-                line = " ".join(rnd.choice(words) for _ in range(rnd.randint(5, 15)))
-                fh.write(line + "\n")
-                n += len(line) + 1
-                total_words += line.count(" ") + 1
-    return total_words
+        idx = np.minimum(rng.zipf(1.3, per_words) - 1, 1999)
+        rec = np.empty((per_words, 6), dtype=np.uint8)
+        rec[:, :5] = vocab[idx]
+        rec[:, 5] = ord(" ")
+        rec[9::10, 5] = ord("\n")
+        rec[-1, 5] = ord("\n")
+        rec.tofile(os.path.join(path, f"part-{f:05d}"))
+        total += per_words
+    return total
 
 
 def wordcount(a):
