@@ -11,12 +11,13 @@
 //     whitespace set of the CPU mapper) compacted in order by a per-tile count,
 //     a scan of tile counts and a per-tile rewrite.  Each lane owns 16
 //     consecutive bytes read as one 16-byte vector load.
-//  2. wc_insert: one lane per word inserts into an open-addressing table of
-//     64-bit keys (32-bit hash tag | representative start + 1) with a 64-bit
-//     CAS; a tag match is confirmed by comparing the bytes of the
-//     representative occurrence, so the aggregation is exact (no hash-only
-//     merging).  Counts are 64-bit atomics; an optional weight per word makes
-//     the same kernel merge partial (word, count) tables.
+//  2. wc_insert: open-addressing tables of 64-bit keys (32-bit hash tag |
+//     representative start + 1) claimed by 64-bit CAS; a tag match is
+//     confirmed by comparing the bytes of the representative occurrence, so
+//     the aggregation is exact (no hash-only merging).  Each workgroup folds
+//     its words into an LDS table first and inserts every distinct word once
+//     into the global (HBM) table.  Counts are 64-bit atomics; an optional
+//     weight per word makes the same kernel merge partial (word, count) tables.
 //  3. wc_compact: occupied slots → (start, len, count, partition), partition =
 //     (Text.hashCode() & INT_MAX) % R with hashCode = WritableComparator.
 //     hashBytes (31·h + signed byte, h0 = 1), i.e. Hadoop's HashPartitioner.
@@ -129,18 +130,22 @@ __device__ __forceinline__ uint64_t word_hash64(const uint8_t* p, uint32_t len) 
   return h;
 }
 
-__global__ __launch_bounds__(256) void wc_insert_kernel(
-    const uint8_t* __restrict__ buf, long n, const uint32_t* __restrict__ starts,
-    const uint32_t* __restrict__ lens, const int64_t* __restrict__ weights, long nwords,
-    unsigned long long* __restrict__ tkeys, unsigned long long* __restrict__ tcounts,
-    unsigned long long mask, int* __restrict__ overflow) {
-  const long w = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= nwords) return;
-  const uint32_t s = starts[w], len = lens[w];
+// bytes of the word at p (len) equal the whitespace-delimited word at rs?
+__device__ __forceinline__ bool same_word(const uint8_t* __restrict__ buf, long n, uint32_t rs,
+                                          const uint8_t* p, uint32_t len) {
+  for (uint32_t i = 0; i < len; ++i)
+    if ((long)rs + i >= n || buf[rs + i] != p[i]) return false;
+  return !((long)rs + len < n && !is_space(buf[rs + len]));
+}
+
+// insert (key = tag | start+1) with weight into the global table
+__device__ __forceinline__ bool global_insert(const uint8_t* __restrict__ buf, long n,
+                                              uint64_t h, unsigned long long key, uint32_t s,
+                                              uint32_t len, unsigned long long wt,
+                                              unsigned long long* __restrict__ tkeys,
+                                              unsigned long long* __restrict__ tcounts,
+                                              unsigned long long mask) {
   const uint8_t* p = buf + s;
-  const uint64_t h = word_hash64(p, len);
-  const unsigned long long key = ((h >> 32) << 32) | (unsigned long long)(s + 1u);
-  const unsigned long long wt = weights ? (unsigned long long)weights[w] : 1ull;
   unsigned long long slot = h & mask;
   for (unsigned long long probe = 0; probe <= mask; ++probe) {
     unsigned long long cur = tkeys[slot];
@@ -148,27 +153,87 @@ __global__ __launch_bounds__(256) void wc_insert_kernel(
       cur = atomicCAS(&tkeys[slot], 0ull, key);
       if (cur == 0ull) {
         atomicAdd(&tcounts[slot], wt);
-        return;
+        return true;
       }
     }
-    if ((cur >> 32) == (key >> 32)) {
-      const uint32_t rs = (uint32_t)(cur & 0xffffffffull) - 1u;
-      bool eq = true;
-      for (uint32_t i = 0; i < len; ++i) {
-        if ((long)rs + i >= n || buf[rs + i] != p[i]) {
-          eq = false;
-          break;
-        }
-      }
-      if (eq && ((long)rs + len < n) && !is_space(buf[rs + len])) eq = false;
-      if (eq) {
-        atomicAdd(&tcounts[slot], wt);
-        return;
-      }
+    if ((cur >> 32) == (key >> 32) &&
+        same_word(buf, n, (uint32_t)(cur & 0xffffffffull) - 1u, p, len)) {
+      atomicAdd(&tcounts[slot], wt);
+      return true;
     }
     slot = (slot + 1) & mask;
   }
-  atomicExch(overflow, 1);
+  return false;
+}
+
+constexpr int kInsThreads = 256;
+constexpr int kInsWordsPerThread = 16;
+constexpr int kInsWords = kInsThreads * kInsWordsPerThread;  // words per workgroup
+constexpr int kLdsSlots = 2048;                              // 32 KiB of LDS
+constexpr int kLdsProbes = 32;
+
+// Two-level aggregation: a workgroup first folds its 4096 words into an LDS
+// table (hot words — the Zipf head of natural text — collapse there instead
+// of hammering one global counter), then inserts each distinct word once into
+// the global table with its local count.  Words that find no LDS slot within
+// kLdsProbes go straight to the global table.
+__global__ __launch_bounds__(kInsThreads) void wc_insert_kernel(
+    const uint8_t* __restrict__ buf, long n, const uint32_t* __restrict__ starts,
+    const uint32_t* __restrict__ lens, const int64_t* __restrict__ weights, long nwords,
+    unsigned long long* __restrict__ tkeys, unsigned long long* __restrict__ tcounts,
+    unsigned long long mask, int* __restrict__ overflow) {
+  __shared__ unsigned long long s_keys[kLdsSlots];
+  __shared__ unsigned long long s_cnt[kLdsSlots];
+  for (int i = threadIdx.x; i < kLdsSlots; i += kInsThreads) {
+    s_keys[i] = 0ull;
+    s_cnt[i] = 0ull;
+  }
+  __syncthreads();
+  const long w0 = (long)blockIdx.x * kInsWords;
+  bool ovf = false;
+#pragma unroll 1
+  for (int j = 0; j < kInsWordsPerThread; ++j) {
+    const long w = w0 + (long)j * kInsThreads + threadIdx.x;
+    if (w >= nwords) break;
+    const uint32_t s = starts[w], len = lens[w];
+    const uint8_t* p = buf + s;
+    const uint64_t h = word_hash64(p, len);
+    const unsigned long long key = ((h >> 32) << 32) | (unsigned long long)(s + 1u);
+    const unsigned long long wt = weights ? (unsigned long long)weights[w] : 1ull;
+    uint32_t slot = (uint32_t)(h >> 7) & (kLdsSlots - 1);
+    bool done = false;
+    for (int probe = 0; probe < kLdsProbes && !done; ++probe) {
+      unsigned long long cur = s_keys[slot];
+      if (cur == 0ull) {
+        cur = atomicCAS(&s_keys[slot], 0ull, key);
+        if (cur == 0ull) {
+          atomicAdd(&s_cnt[slot], wt);
+          done = true;
+          break;
+        }
+      }
+      if ((cur >> 32) == (key >> 32) &&
+          same_word(buf, n, (uint32_t)(cur & 0xffffffffull) - 1u, p, len)) {
+        atomicAdd(&s_cnt[slot], wt);
+        done = true;
+        break;
+      }
+      slot = (slot + 1) & (kLdsSlots - 1);
+    }
+    if (!done && !global_insert(buf, n, h, key, s, len, wt, tkeys, tcounts, mask)) ovf = true;
+  }
+  __syncthreads();
+  // flush: each distinct word of this workgroup once into the global table
+  for (int i = threadIdx.x; i < kLdsSlots; i += kInsThreads) {
+    const unsigned long long key = s_keys[i];
+    if (key == 0ull) continue;
+    const uint32_t s = (uint32_t)(key & 0xffffffffull) - 1u;
+    uint32_t len = 0;
+    while ((long)s + len < n && !is_space(buf[s + len])) ++len;
+    const uint64_t h = word_hash64(buf + s, len);
+    if (!global_insert(buf, n, h, key, s, len, s_cnt[i], tkeys, tcounts, mask)) ovf = true;
+  }
+  if (ovf) atomicExch(overflow, 1);
 }
 
 __global__ __launch_bounds__(256) void wc_compact_kernel(
@@ -242,7 +307,8 @@ int hbmr_wc_insert(const uint8_t* buf, long n, const uint32_t* starts, const uin
                    long cap, int* overflow, hipStream_t stream) {
   if (nwords == 0) return 0;
   if (cap <= 0 || (cap & (cap - 1)) != 0 || n >= 0xffffffffl) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(wc_insert_kernel, dim3(grid_for(nwords, 256)), dim3(256), 0, stream, buf, n,
+  hipLaunchKernelGGL(wc_insert_kernel, dim3(grid_for(nwords, kInsWords)), dim3(kInsThreads), 0,
+                     stream, buf, n,
                      starts, lens, weights, nwords,
                      reinterpret_cast<unsigned long long*>(tkeys),
                      reinterpret_cast<unsigned long long*>(tcounts),

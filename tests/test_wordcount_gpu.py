@@ -106,6 +106,17 @@ def test_gpu_count_words_exact():
 
 
 @pytest.mark.gpu
+def test_gpu_count_words_hot_words():
+    """Zipf head: a few words are most of the text (LDS pre-aggregation path)."""
+    rnd = random.Random(2)
+    data = b" ".join(rnd.choice([b"the"] * 90 + [b"of"] * 9 + [b"w%d" % rnd.randint(0, 5000)])
+                     for _ in range(300_000)) + b"\n"
+    blob, counts = text.count_words(torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda())
+    got = dict(text.parse_table(bytes(blob.cpu().numpy()), counts.cpu()))
+    assert got == dict(collections.Counter(data.split()))
+
+
+@pytest.mark.gpu
 def test_gpu_count_words_empty_and_unaligned():
     buf = torch.frombuffer(bytearray(b"  x yy x "), dtype=torch.uint8).cuda()
     blob, counts = text.count_words(buf[1:])        # misaligned view
