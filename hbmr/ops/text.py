@@ -18,7 +18,8 @@ import torch
 from . import _lib
 from ..io.writable import hash_bytes
 
-_TABLE_MAX = 1 << 26
+_TABLE_MAX = 1 << 28
+INITIAL_TABLE = 1 << 21     # first word-table size tried (slots)
 
 
 def _ptr(t):
@@ -68,7 +69,10 @@ def aggregate(buf, starts, lens, weights=None, R=1, stream=None):
     dev = buf.device
     nw = starts.numel()
     n = buf.numel()
-    cap = min(_pow2(2 * max(nw, 1)), _TABLE_MAX)
+    # distinct words are usually far fewer than words: start at ≤ 2M slots
+    # (32 MiB of keys + counts) and grow on overflow (bounded probe runs)
+    full = min(_pow2(2 * max(nw, 1)), _TABLE_MAX)
+    cap = min(full, INITIAL_TABLE)
     while True:
         tkeys = torch.zeros(cap, dtype=torch.int64, device=dev)
         tcounts = torch.zeros(cap, dtype=torch.int64, device=dev)
@@ -78,9 +82,9 @@ def aggregate(buf, starts, lens, weights=None, R=1, stream=None):
                   _ptr(tkeys), _ptr(tcounts), cap, _ptr(ovf), _st(stream))
         if int(ovf) == 0:
             break
-        if cap >= 2 * _TABLE_MAX:
-            raise RuntimeError("word table overflow")
-        cap *= 2
+        if cap >= full:
+            raise RuntimeError(f"word table overflow at {cap} slots for {nw} words")
+        cap = min(cap * 4, full)
     ustart = torch.empty(min(cap, max(nw, 1)), dtype=torch.int32, device=dev)
     ulen = torch.empty_like(ustart)
     ucount = torch.empty(ustart.numel(), dtype=torch.int64, device=dev)

@@ -150,6 +150,52 @@ def _build_apps(verbose, lib, alib, hostlib, hdrs):
     return {"apps": apps}
 
 
+SANITIZERS = {
+    # host code only (GPU sanitizers are not available on the MI355X pool)
+    "asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=all"],
+    "tsan": ["-fsanitize=thread", "-fno-omit-frame-pointer"],
+}
+
+
+def build_sanitized(kind: str, verbose: bool = False) -> dict:
+    """Host-only sanitizer builds (SURVEY.md §5 race detection / sanitizers):
+    the Pipes runtime, CPU kernels, SequenceFile I/O and the CPU Pipes apps,
+    plus native/tests/selftest.cc, compiled with ASAN+UBSAN or TSAN into
+    build/sanitize/<kind>/.  Returns {name: executable}."""
+    flags = SANITIZERS[kind]
+    out_dir = ROOT / "build" / "sanitize" / kind
+    out_dir.mkdir(parents=True, exist_ok=True)
+    hdrs = _headers(NATIVE)
+    srcs = (sorted((NATIVE / "cpu").glob("*.cc")) + sorted((NATIVE / "io").glob("*.cc")) +
+            sorted((NATIVE / "pipes").rglob("*.cc")))
+    inc = [f"-I{NATIVE / 'include'}", f"-I{NATIVE / 'pipes' / 'api'}", f"-I{NATIVE / 'pipes'}"]
+    base = ["-O1", "-g", "-std=c++17", "-pthread", "-DHBMR_NO_HIP_DECLS", *inc, *flags]
+    work = []
+    for src in srcs:
+        o = out_dir / (src.relative_to(NATIVE).as_posix().replace("/", "__") + ".o")
+        if _stale(o, [src, *hdrs, Path(__file__)]):
+            work.append([CXX, *base, "-c", src, "-o", o])
+    n = min(8, os.cpu_count() or 4)
+    with cf.ThreadPoolExecutor(max_workers=n) as ex:
+        list(ex.map(lambda c: _run(c, verbose), work))
+    objs = [out_dir / (src.relative_to(NATIVE).as_posix().replace("/", "__") + ".o")
+            for src in srcs]
+    exes = {}
+    mains = sorted((NATIVE / "apps").glob("*.cc")) + sorted((NATIVE / "tests").glob("*.cc"))
+    cmds = []
+    for m in mains:
+        exe = out_dir / m.stem
+        exes[m.stem] = str(exe)
+        if _stale(exe, [m, *objs, *hdrs]):
+            cmds.append([CXX, *base, m, *objs, "-o", exe, "-lz"])
+    with cf.ThreadPoolExecutor(max_workers=n) as ex:
+        list(ex.map(lambda c: _run(c, verbose), cmds))
+    return exes
+
+
 if __name__ == "__main__":
-    res = build(verbose="-v" in sys.argv)
-    print(res)
+    if len(sys.argv) > 2 and sys.argv[1] == "sanitize":
+        print(build_sanitized(sys.argv[2], verbose="-v" in sys.argv))
+    else:
+        res = build(verbose="-v" in sys.argv)
+        print(res)

@@ -147,7 +147,10 @@ __device__ __forceinline__ bool global_insert(const uint8_t* __restrict__ buf, l
                                               unsigned long long mask) {
   const uint8_t* p = buf + s;
   unsigned long long slot = h & mask;
-  for (unsigned long long probe = 0; probe <= mask; ++probe) {
+  // a probe run this long means the table is too full: report overflow and let
+  // the host retry with a larger table instead of crawling
+  const unsigned long long max_probe = mask < 4096ull ? mask : 4096ull;
+  for (unsigned long long probe = 0; probe <= max_probe; ++probe) {
     unsigned long long cur = tkeys[slot];
     if (cur == 0ull) {
       cur = atomicCAS(&tkeys[slot], 0ull, key);

@@ -106,6 +106,17 @@ def test_gpu_count_words_exact():
 
 
 @pytest.mark.gpu
+def test_gpu_count_words_table_growth(monkeypatch):
+    """More distinct words than the first table holds: overflow → retry larger."""
+    monkeypatch.setattr(text, "INITIAL_TABLE", 1024)
+    words = [b"u%d" % i for i in range(50_000)] * 2
+    data = b" ".join(words)
+    blob, counts = text.count_words(torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda())
+    got = dict(text.parse_table(bytes(blob.cpu().numpy()), counts.cpu()))
+    assert len(got) == 50_000 and set(got.values()) == {2}
+
+
+@pytest.mark.gpu
 def test_gpu_count_words_hot_words():
     """Zipf head: a few words are most of the text (LDS pre-aggregation path)."""
     rnd = random.Random(2)
