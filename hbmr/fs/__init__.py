@@ -135,11 +135,90 @@ class LocalFileSystem:
     getDefaultBlockSize = get_default_block_size  # noqa: N815
 
 
-def get_fs(path=None, conf=None) -> LocalFileSystem:
+def is_dfs(path) -> bool:
+    return str(path).startswith("hdfs://")
+
+
+def get_fs(path=None, conf=None):
+    """FileSystem for a path: ``hdfs://authority/...`` → hbmr.dfs, else local."""
     p = str(path or "")
+    if is_dfs(p):
+        from ..dfs.client import DistributedFileSystem, split_uri
+        return DistributedFileSystem(split_uri(p)[0], conf)
     if "://" in p and not p.startswith("file://"):
-        raise ValueError(f"unsupported filesystem scheme in {p!r} (hbmr is single-node: use file://)")
+        raise ValueError(f"unsupported filesystem scheme in {p!r} (use file:// or hdfs://)")
     return LocalFileSystem(conf)
+
+
+# -- scheme-dispatching helpers for the MapReduce I/O paths ---------------------------------
+def fopen(path, mode="rb", buffering=-1, conf=None):
+    """open() for local paths and hdfs:// URIs (read or write, binary)."""
+    if is_dfs(path):
+        fs = get_fs(path, conf)
+        return fs.open(path) if "r" in mode else fs.create(path)
+    return open(strip_scheme(path), mode, buffering=buffering)
+
+
+def makedirs(path):
+    if is_dfs(path):
+        get_fs(path).mkdirs(path)
+    else:
+        os.makedirs(strip_scheme(path), exist_ok=True)
+
+
+def exists(path) -> bool:
+    return get_fs(path).exists(path) if is_dfs(path) else os.path.exists(strip_scheme(path))
+
+
+def isdir(path) -> bool:
+    return get_fs(path).is_dir(path) if is_dfs(path) else os.path.isdir(strip_scheme(path))
+
+
+def listdir(path) -> list:
+    return get_fs(path).listdir(path) if is_dfs(path) else os.listdir(strip_scheme(path))
+
+
+def rmtree(path):
+    if is_dfs(path):
+        get_fs(path).delete(path, recursive=True)
+    else:
+        shutil.rmtree(strip_scheme(path), ignore_errors=True)
+
+
+def replace(src, dst):
+    """Move src over dst (files)."""
+    if is_dfs(src):
+        fs = get_fs(src)
+        if fs.exists(dst):
+            fs.delete(dst)
+        fs.rename(src, dst)
+    else:
+        os.replace(strip_scheme(src), strip_scheme(dst))
+
+
+def walk_files(root) -> list:
+    """Relative paths of all files under root."""
+    if not is_dfs(root):
+        r = strip_scheme(root)
+        return [os.path.relpath(os.path.join(d, f), r) for d, _, fs in os.walk(r) for f in fs]
+    fs = get_fs(root)
+    out, todo = [], [""]
+    while todo:
+        rel = todo.pop()
+        for st in fs.list_status(os.path.join(root, rel) if rel else root, filter_hidden=False):
+            name = os.path.join(rel, os.path.basename(st.path.rstrip("/")))
+            (todo if st.is_dir else out).append(name)
+    return out
+
+
+def block_hosts(fs, path, start, length) -> list:
+    """Hosts of the block holding ``start`` (FileInputFormat.getBlockIndex)."""
+    if not hasattr(fs, "get_file_block_locations"):
+        return []
+    for off, blen, hosts in fs.get_file_block_locations(path, start, max(1, length)):
+        if off <= start < off + max(blen, 1):
+            return list(hosts)
+    return []
 
 
 FileSystem = LocalFileSystem

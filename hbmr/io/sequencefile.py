@@ -97,10 +97,11 @@ class Writer:
             raise ValueError(f"bad compression type {compression}")
         self.codec = get_codec(codec or "default") if self.compression != NONE else None
         self.block_size = block_size
+        from .. import fs as F
         d = os.path.dirname(self.path)
         if d:
-            os.makedirs(d, exist_ok=True)
-        self.out = _PosFile(open(self.path, "wb"))
+            F.makedirs(d)
+        self.out = _PosFile(F.fopen(self.path, "wb"))
         self.sync = hashlib.md5(f"{uuid.uuid4()}@{time.time_ns()}".encode()).digest()
         self.last_sync_pos = 0
         self._blk_keys = io.BytesIO()
@@ -194,9 +195,13 @@ class Writer:
 
 class Reader:
     def __init__(self, path, fs=None, buffer_size: int = 1 << 20):
+        from .. import fs as F
         self.path = str(path)
-        self.f = open(self.path, "rb", buffering=buffer_size)
-        self.file_len = os.fstat(self.f.fileno()).st_size
+        self.f = F.fopen(self.path, "rb", buffering=buffer_size)
+        if F.is_dfs(self.path):
+            self.file_len = F.get_fs(self.path).get_file_status(self.path).length
+        else:
+            self.file_len = os.fstat(self.f.fileno()).st_size
         magic = self.f.read(3)
         if magic != b"SEQ":
             raise IOError(f"{self.path} is not a SequenceFile")

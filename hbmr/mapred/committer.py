@@ -9,8 +9,8 @@ and drops the ``_SUCCESS`` marker.
 from __future__ import annotations
 
 import os
-import shutil
 
+from .. import fs as F
 from .formats import get_output_path
 
 TEMP_DIR = "_temporary"
@@ -53,44 +53,42 @@ class FileOutputCommitter(OutputCommitter):
     def setup_job(self, job):
         out = self._out(job)
         if out:
-            os.makedirs(os.path.join(out, TEMP_DIR), exist_ok=True)
+            F.makedirs(os.path.join(out, TEMP_DIR))
 
     def commit_job(self, job):
         out = self._out(job)
         if not out:
             return
-        shutil.rmtree(os.path.join(out, TEMP_DIR), ignore_errors=True)
+        F.rmtree(os.path.join(out, TEMP_DIR))
         if job.get_boolean("mapreduce.fileoutputcommitter.marksuccessfuljobs", True):
-            open(os.path.join(out, SUCCEEDED_FILE), "wb").close()
+            F.fopen(os.path.join(out, SUCCEEDED_FILE), "wb").close()
 
     def abort_job(self, job, state="FAILED"):
         out = self._out(job)
         if out:
-            shutil.rmtree(os.path.join(out, TEMP_DIR), ignore_errors=True)
+            F.rmtree(os.path.join(out, TEMP_DIR))
 
     def setup_task(self, job, attempt):
         wp = self.work_path(job, attempt)
         if wp:
-            os.makedirs(wp, exist_ok=True)
+            F.makedirs(wp)
 
     def needs_task_commit(self, job, attempt) -> bool:
         wp = self.work_path(job, attempt)
-        return bool(wp) and os.path.isdir(wp) and bool(os.listdir(wp))
+        return bool(wp) and F.isdir(wp) and bool(F.listdir(wp))
 
     def commit_task(self, job, attempt):
         wp = self.work_path(job, attempt)
         out = self._out(job)
-        if not wp or not os.path.isdir(wp):
+        if not wp or not F.isdir(wp):
             return
-        for root, _dirs, files in os.walk(wp):
-            rel = os.path.relpath(root, wp)
-            dst_dir = out if rel == "." else os.path.join(out, rel)
-            os.makedirs(dst_dir, exist_ok=True)
-            for f in files:
-                os.replace(os.path.join(root, f), os.path.join(dst_dir, f))
-        shutil.rmtree(wp, ignore_errors=True)
+        for rel in F.walk_files(wp):
+            dst = os.path.join(out, rel)
+            F.makedirs(os.path.dirname(dst))
+            F.replace(os.path.join(wp, rel), dst)
+        F.rmtree(wp)
 
     def abort_task(self, job, attempt):
         wp = self.work_path(job, attempt)
         if wp:
-            shutil.rmtree(wp, ignore_errors=True)
+            F.rmtree(wp)

@@ -19,6 +19,7 @@ import io
 import os
 import struct
 
+from .. import fs as F
 from ..fs import get_fs, hidden, strip_scheme
 from ..io import sequencefile as seqf
 from ..io.compress import codec_for_path, get_codec
@@ -105,9 +106,9 @@ class FileInputFormat(InputFormat):
         return codec_for_path(path) is None
 
     def list_status(self, job):
-        fs = get_fs(conf=job)
         out = []
         for p in get_input_paths(job):
+            fs = get_fs(p, job)
             matches = fs.glob_status(p) if any(ch in p for ch in "*?[") else \
                 [fs.get_file_status(p)]
             if not matches:
@@ -131,20 +132,26 @@ class FileInputFormat(InputFormat):
         total = sum(f.length for f in files)
         goal = total // (num_splits if num_splits > 0 else 1)
         min_size = max(job.get_long("mapred.min.split.size", 1), 1)
-        fs = get_fs(conf=job)
         splits = []
         for f in files:
+            fs = get_fs(f.path, job)
             length = f.length
+            # split hosts = the DataNodes holding the split's first block
+            # (FileInputFormat.getBlockIndex), for data-local scheduling
+            hosts = (lambda s, n: F.block_hosts(fs, f.path, s, n)) if F.is_dfs(f.path) else \
+                (lambda s, n: None)
             if length != 0 and self.is_splitable(fs, f.path):
                 split_size = self.compute_split_size(goal, min_size, f.block_size)
                 remaining = length
                 while remaining / split_size > SPLIT_SLOP:
-                    splits.append(FileSplit(f.path, length - remaining, split_size))
+                    st = length - remaining
+                    splits.append(FileSplit(f.path, st, split_size, hosts(st, split_size)))
                     remaining -= split_size
                 if remaining != 0:
-                    splits.append(FileSplit(f.path, length - remaining, remaining))
+                    st = length - remaining
+                    splits.append(FileSplit(f.path, st, remaining, hosts(st, remaining)))
             elif length != 0:
-                splits.append(FileSplit(f.path, 0, length))
+                splits.append(FileSplit(f.path, 0, length, hosts(0, length)))
             else:
                 splits.append(FileSplit(f.path, 0, 0))
         return splits
@@ -159,11 +166,11 @@ class LineRecordReader(RecordReader):
         self.path = split.path
         self.codec = codec_for_path(split.path)
         if self.codec is not None:
-            with open(strip_scheme(split.path), "rb") as f:
+            with F.fopen(split.path, "rb") as f:
                 self.f = io.BytesIO(self.codec.decompress(f.read()))
             self.end = 1 << 62
         else:
-            self.f = open(strip_scheme(split.path), "rb", buffering=1 << 20)
+            self.f = F.fopen(split.path, "rb", buffering=1 << 20)
         self.f.seek(self.start)
         self.pos = self.start
         if self.start != 0:
@@ -240,7 +247,7 @@ class NLineInputFormat(FileInputFormat):
             begin = 0
             length = 0
             count = 0
-            with open(st.path, "rb") as f:
+            with F.fopen(st.path, "rb") as f:
                 for line in f:
                     count += 1
                     length += len(line)
@@ -268,7 +275,7 @@ class NLineInputFormat(FileInputFormat):
 
 class SequenceFileRecordReader(RecordReader):
     def __init__(self, job, split: FileSplit):
-        self.reader = seqf.Reader(strip_scheme(split.path))
+        self.reader = seqf.Reader(split.path)
         self.start = split.start
         self.end = split.start + split.length
         if self.start > self.reader.get_position():
@@ -360,7 +367,7 @@ class FileOutputFormat(OutputFormat):
         out = get_output_path(job)
         if out is None and job.get_num_reduce_tasks() != 0:
             raise ValueError("Output directory not set in JobConf.")
-        if out is not None and os.path.exists(out) and os.listdir(out):
+        if out is not None and F.exists(out) and F.listdir(out):
             raise FileExistsError(f"Output directory {out} already exists")
 
     @staticmethod
@@ -416,8 +423,8 @@ class TextOutputFormat(FileOutputFormat):
             codec = get_codec(job.get("mapred.output.compression.codec",
                                       "org.apache.hadoop.io.compress.DefaultCodec"))
             path += codec.getDefaultExtension()
-        os.makedirs(os.path.dirname(path), exist_ok=True)
-        return _TextRecordWriter(open(path, "wb"), sep, codec)
+        F.makedirs(os.path.dirname(path))
+        return _TextRecordWriter(F.fopen(path, "wb"), sep, codec)
 
 
 class _SeqRecordWriter(RecordWriter):
@@ -445,7 +452,7 @@ class SequenceFileOutputFormat(FileOutputFormat):
 
     @staticmethod
     def get_readers(path):
-        files = sorted(p for p in os.listdir(path) if p.startswith("part-"))
+        files = sorted(p for p in F.listdir(path) if p.startswith("part-"))
         return [seqf.Reader(os.path.join(path, p)) for p in files]
 
 
