@@ -6,7 +6,10 @@ jar/pipes/job/fs/version/... dispatch).
   hbmr streaming -input I -output O -mapper CMD -reducer CMD ...
   hbmr job -jt host:port -list [all] | -status ID | -kill ID | -counter ID GROUP NAME
            | -tasks ID map|reduce | -history FILE
-  hbmr fs -ls|-cat|-text|-put|-get|-rm|-rmr|-mkdir|-du PATH...
+  hbmr fs -ls|-lsr|-cat|-text|-put|-get|-cp|-mv|-rm|-rmr|-mkdir|-du|-setrep PATH...
+                                      (local paths and hdfs://NAMENODE/... URIs)
+  hbmr namenode -dir D [-port P] | datanode -nn HOST:PORT -dir D [-host H]
+  hbmr fsck hdfs://NAMENODE/path | dfsadmin -nn NAMENODE -report|-safemode X|...
   hbmr node            start this process's TaskTracker (+ JobTracker on rank 0)
                        under torchrun: one process per GPU
   hbmr run module:function [args]     run a user program (the ``jar`` analogue)
@@ -75,67 +78,175 @@ def _job(argv):
 
 
 def _fs(argv):
+    """FsShell over the FileSystem layer: local paths and hdfs:// URIs."""
+    from . import fs as F
     from .io import sequencefile as seqf
     if not argv:
-        print("hbmr fs -ls|-cat|-text|-put|-get|-rm|-rmr|-mkdir|-du PATH...", file=sys.stderr)
+        print("hbmr fs -ls|-lsr|-cat|-text|-put|-get|-cp|-mv|-rm|-rmr|-mkdir|-du|-setrep PATH...",
+              file=sys.stderr)
         return 2
-    op, paths = argv[0], [p[5:] if p.startswith("file:") else p for p in argv[1:]]
+    op, paths = argv[0], [p[5:] if p.startswith("file:") and not p.startswith("file://") else p
+                          for p in argv[1:]]
+
+    def _walk(p):
+        fs = F.get_fs(p)
+        st = fs.get_file_status(p)
+        if not st.is_dir:
+            return [st]
+        out = []
+        for c in fs.list_status(p, filter_hidden=False):
+            out += _walk(c.path) if c.is_dir and op == "-lsr" else [c]
+        return out
+
+    def _copy(src, dst):
+        if F.isdir(dst):
+            dst = os.path.join(dst, os.path.basename(src.rstrip("/")))
+        if F.isdir(src):
+            F.makedirs(dst)
+            for name in F.listdir(src):
+                _copy(os.path.join(src, name), os.path.join(dst, name))
+            return
+        with F.fopen(src, "rb") as fi, F.fopen(dst, "wb") as fo:
+            shutil.copyfileobj(fi, fo, 1 << 20)
+
     if op in ("-ls", "-lsr"):
         for p in paths or ["."]:
-            entries = [p] if os.path.isfile(p) else sorted(
-                os.path.join(d, f) for d, _s, fs in os.walk(p) for f in fs) if op == "-lsr" \
-                else [os.path.join(p, f) for f in sorted(os.listdir(p))]
+            entries = _walk(p)
             print(f"Found {len(entries)} items")
-            for e in entries:
-                st = os.stat(e)
-                kind = "d" if os.path.isdir(e) else "-"
-                print(f"{kind}rw-r--r--   1 {st.st_size:>12} "
-                      f"{time.strftime('%Y-%m-%d %H:%M', time.localtime(st.st_mtime))} {e}")
+            for st in entries:
+                kind = "d" if st.is_dir else "-"
+                print(f"{kind}rw-r--r--   1 {st.length:>12} "
+                      f"{time.strftime('%Y-%m-%d %H:%M', time.localtime(st.modification_time))} "
+                      f"{st.path}")
     elif op == "-cat":
         for p in paths:
-            with open(p, "rb") as f:
+            with F.fopen(p, "rb") as f:
                 shutil.copyfileobj(f, sys.stdout.buffer)
     elif op == "-text":
         for p in paths:
-            with open(p, "rb") as f:
+            with F.fopen(p, "rb") as f:
                 magic = f.read(3)
             if magic == b"SEQ":
                 with seqf.Reader(p) as r:
                     for k, v in r:
                         print(f"{k}\t{v}")
             else:
-                with open(p, "rb") as f:
+                with F.fopen(p, "rb") as f:
                     shutil.copyfileobj(f, sys.stdout.buffer)
     elif op in ("-put", "-copyFromLocal", "-get", "-copyToLocal", "-cp"):
         *srcs, dst = paths
-        for s in srcs:
-            if os.path.isdir(s):
-                shutil.copytree(s, os.path.join(dst, os.path.basename(s)) if os.path.isdir(dst)
-                                else dst)
-            else:
-                shutil.copy(s, dst)
+        for src in srcs:
+            _copy(src, dst)
     elif op == "-mv":
-        shutil.move(paths[0], paths[1])
+        if not F.get_fs(paths[0]).rename(paths[0], paths[1]):
+            print(f"mv: cannot move {paths[0]}", file=sys.stderr)
+            return 1
     elif op in ("-rm", "-rmr"):
         for p in paths:
-            if os.path.isdir(p):
-                if op != "-rmr":
-                    print(f"rm: cannot remove {p}: Is a directory", file=sys.stderr)
-                    return 1
-                shutil.rmtree(p)
-            else:
-                os.remove(p)
+            if F.isdir(p) and op != "-rmr":
+                print(f"rm: cannot remove {p}: Is a directory", file=sys.stderr)
+                return 1
+            F.get_fs(p).delete(p, recursive=True)
             print(f"Deleted {p}")
     elif op == "-mkdir":
         for p in paths:
-            os.makedirs(p, exist_ok=True)
+            F.makedirs(p)
     elif op in ("-du", "-dus"):
         for p in paths:
-            tot = sum(os.path.getsize(os.path.join(d, f)) for d, _s, fs in os.walk(p) for f in fs) \
-                if os.path.isdir(p) else os.path.getsize(p)
+            op_ = op
+            op = "-lsr"
+            tot = sum(st.length for st in _walk(p) if not st.is_dir)
+            op = op_
             print(f"{tot}\t{p}")
+    elif op == "-setrep":
+        r, p = int(paths[0]), paths[1]
+        F.get_fs(p).set_replication(p, r)
+        print(f"Replication {r} set: {p}")
     else:
         print(f"{op}: Unknown command", file=sys.stderr)
+        return 2
+    return 0
+
+
+def _namenode(argv):
+    """hbmr namenode -dir NAME_DIR [-port P]: serve a NameNode over RPC."""
+    import argparse
+    from .dfs.namenode import NameNode
+    from .mapred.jobconf import JobConf
+    from .mapred.rpc import RpcServer
+    ap = argparse.ArgumentParser(prog="hbmr namenode")
+    ap.add_argument("-dir", required=True)
+    ap.add_argument("-port", type=int, default=8020)
+    a = ap.parse_args(argv)
+    nn = NameNode(JobConf(), a.dir)
+    srv = RpcServer(nn, NameNode.METHODS, port=a.port).start()
+    print(f"NameNode up: hdfs://127.0.0.1:{srv.port}", flush=True)
+    try:
+        while True:
+            time.sleep(1.0)
+    except KeyboardInterrupt:
+        nn.save_namespace()
+    return 0
+
+
+def _datanode(argv):
+    """hbmr datanode -nn HOST:PORT -dir DATA_DIR [-id ID] [-host H] [-rack R]."""
+    import argparse
+    import socket
+    from .dfs.client import RpcProxy
+    from .dfs.datanode import DataNode
+    from .mapred.jobconf import JobConf
+    ap = argparse.ArgumentParser(prog="hbmr datanode")
+    ap.add_argument("-nn", required=True)
+    ap.add_argument("-dir", required=True)
+    ap.add_argument("-id", default=None)
+    ap.add_argument("-host", default=socket.gethostname())
+    ap.add_argument("-rack", default="/default-rack")
+    a = ap.parse_args(argv)
+    dn = DataNode(JobConf(), RpcProxy(a.nn), a.id or f"dn-{a.host}-{os.getpid()}", a.host, a.dir,
+                  a.rack, serve_rpc=True)
+    print(f"DataNode {dn.id} up, serving {dn.server.port}", flush=True)
+    try:
+        while True:
+            time.sleep(1.0)
+    except KeyboardInterrupt:
+        dn.shutdown()
+    return 0
+
+
+def _fsck(argv):
+    from .dfs.client import namenode_for, split_uri
+    if not argv:
+        print("hbmr fsck hdfs://NAMENODE/path", file=sys.stderr)
+        return 2
+    auth, path = split_uri(argv[0])
+    rep = namenode_for(auth).fsck(path)
+    for line in rep.pop("problems", []):
+        print(line)
+    print(json.dumps(rep, indent=1))
+    return 0 if rep["status"] == "HEALTHY" else 1
+
+
+def _dfsadmin(argv):
+    """hbmr dfsadmin -nn AUTH -report | -safemode get|enter|leave | -saveNamespace
+    | -decommission DN_ID"""
+    from .dfs.client import namenode_for
+    if len(argv) < 3 or argv[0] != "-nn":
+        print(_dfsadmin.__doc__, file=sys.stderr)
+        return 2
+    nn = namenode_for(argv[1])
+    op, rest = argv[2], argv[3:]
+    if op == "-report":
+        for d in nn.datanode_report():
+            print(json.dumps(d))
+    elif op == "-safemode":
+        print("Safe mode is " + ("ON" if nn.safemode(rest[0] if rest else "get") else "OFF"))
+    elif op == "-saveNamespace":
+        print("Save namespace " + ("successful" if nn.save_namespace() else "failed"))
+    elif op == "-decommission":
+        print("Decommission " + ("started" if nn.decommission(rest[0]) else "failed"))
+    else:
+        print(_dfsadmin.__doc__, file=sys.stderr)
         return 2
     return 0
 
@@ -196,6 +307,14 @@ def main(argv=None):
         return _fs(rest)
     if cmd == "node":
         return _node(rest)
+    if cmd == "namenode":
+        return _namenode(rest)
+    if cmd == "datanode":
+        return _datanode(rest)
+    if cmd == "fsck":
+        return _fsck(rest)
+    if cmd == "dfsadmin":
+        return _dfsadmin(rest)
     if cmd in ("run", "jar"):
         return _run(rest)
     if cmd == "version":

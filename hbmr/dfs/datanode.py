@@ -150,6 +150,8 @@ class DataNode:
             except ChecksumError:
                 bad.append(bid)
                 self.nn.report_bad_block(bid, self.id)
+            except FileNotFoundError:
+                pass   # invalidated and deleted while we scanned
         return bad
 
     def ping(self):

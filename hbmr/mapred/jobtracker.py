@@ -198,6 +198,11 @@ class JobInProgress:
             "hbmr.splitjob.class", "mapred.mapper.class", "hadoop.pipes.executable",
             "hadoop.pipes.gpu.executable", "mapred.input.format.class", "hbmr.split.size"))
 
+    def committer(self):
+        cls = self.conf.get_output_committer()
+        from .committer import FileOutputCommitter
+        return cls() if isinstance(cls, type) else (cls or FileOutputCommitter())
+
     # -- init ---------------------------------------------------------------------
     def init_tasks(self):
         conf = self.conf
@@ -212,6 +217,8 @@ class JobInProgress:
                 self.gpu_capable = True   # the split job has a device map
             split_dicts = [s.to_dict() for s in splits]
         else:
+            # job setup (the reference's setup task: FileOutputCommitter.setupJob)
+            self.committer().setup_job(conf)
             informat = new_instance(conf.get_input_format(), conf)
             splits = informat.getSplits(conf, conf.get_num_map_tasks())
             split_dicts = [{"kind": "class", "cls": f"{type(s).__module__}:{type(s).__qualname__}",
@@ -653,6 +660,13 @@ class JobTracker:
                 jip.split_job.job_succeeded(jip)
             except Exception:  # noqa: BLE001
                 log.exception("job_succeeded hook failed")
+        elif jip.split_job is None and jip.maps is not None:
+            # job cleanup (the reference's cleanup task: commitJob / abortJob)
+            try:
+                com = jip.committer()
+                com.commit_job(jip.conf) if state == SUCCEEDED else com.abort_job(jip.conf)
+            except Exception:  # noqa: BLE001
+                log.exception("job cleanup failed")
         if TRACE.on:
             TRACE.instant("jt.job_finished", job=str(jip.job_id), state=state)
         METRICS.inc("hbmr_jobs_completed_total", help="jobs finished, by final state",
