@@ -71,7 +71,32 @@ def _compile_jobs(srcs, compiler, flags, objdir, hdrs):
     return jobs
 
 
+class _BuildLock:
+    """Inter-process lock so concurrent builders (pytest-xdist workers, a test and the
+    driver) never link against an object another process is still writing."""
+
+    def __init__(self, path: Path):
+        self.path = path
+
+    def __enter__(self):
+        import fcntl
+        self.path.parent.mkdir(parents=True, exist_ok=True)
+        self.fd = open(self.path, "w")
+        fcntl.flock(self.fd, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *exc):
+        import fcntl
+        fcntl.flock(self.fd, fcntl.LOCK_UN)
+        self.fd.close()
+
+
 def build(verbose: bool = False, jobs: int | None = None) -> dict:
+    with _BuildLock(ROOT / "build" / ".native.lock"):
+        return _build(verbose, jobs)
+
+
+def _build(verbose: bool, jobs: int | None) -> dict:
     BUILD.mkdir(parents=True, exist_ok=True)
     LIBDIR.mkdir(parents=True, exist_ok=True)
     BINDIR.mkdir(parents=True, exist_ok=True)
@@ -162,8 +187,13 @@ def build_sanitized(kind: str, verbose: bool = False) -> dict:
     the Pipes runtime, CPU kernels, SequenceFile I/O and the CPU Pipes apps,
     plus native/tests/selftest.cc, compiled with ASAN+UBSAN or TSAN into
     build/sanitize/<kind>/.  Returns {name: executable}."""
-    flags = SANITIZERS[kind]
     out_dir = ROOT / "build" / "sanitize" / kind
+    with _BuildLock(out_dir.parent / f".{kind}.lock"):
+        return _build_sanitized(kind, out_dir, verbose)
+
+
+def _build_sanitized(kind: str, out_dir: Path, verbose: bool) -> dict:
+    flags = SANITIZERS[kind]
     out_dir.mkdir(parents=True, exist_ok=True)
     hdrs = _headers(NATIVE)
     srcs = (sorted((NATIVE / "cpu").glob("*.cc")) + sorted((NATIVE / "io").glob("*.cc")) +
