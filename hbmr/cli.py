@@ -10,6 +10,10 @@ jar/pipes/job/fs/version/... dispatch).
                                       (local paths and hdfs://NAMENODE/... URIs)
   hbmr namenode -dir D [-port P] | datanode -nn HOST:PORT -dir D [-host H]
   hbmr fsck hdfs://NAMENODE/path | dfsadmin -nn NAMENODE -report|-safemode X|...
+  hbmr distcp [-update|-overwrite|-delete|-i|-p|-m N] SRC... DST   (file:// / hdfs://)
+  hbmr archive -archiveName NAME.har -p PARENT SRC... DEST        (read back as har://)
+  hbmr rumen TRACE_OUT TOPOLOGY_OUT HISTORY...                     (job-history traces)
+  hbmr gridmix [-generate BYTES] [-jobtype LOADJOB|SLEEPJOB] [-policy REPLAY|STRESS|SERIAL] IOPATH TRACE
   hbmr node            start this process's TaskTracker (+ JobTracker on rank 0)
                        under torchrun: one process per GPU
   hbmr run module:function [args]     run a user program (the ``jar`` analogue)
@@ -286,6 +290,14 @@ def _run(argv):
     return rc or 0
 
 
+TOOLS = {  # src/tools + contrib commands of bin/hadoop
+    "distcp": "hbmr.tools.distcp:main",
+    "archive": "hbmr.tools.har:main",
+    "rumen": "hbmr.tools.rumen:main",
+    "gridmix": "hbmr.tools.gridmix:main",
+}
+
+
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     if not argv or argv[0] in ("-h", "--help", "help"):
@@ -317,6 +329,8 @@ def main(argv=None):
         return _dfsadmin(rest)
     if cmd in ("run", "jar"):
         return _run(rest)
+    if cmd in TOOLS:
+        return _run([TOOLS[cmd], *rest])
     if cmd == "version":
         print(VERSION)
         return 0

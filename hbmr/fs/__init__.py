@@ -136,13 +136,25 @@ class LocalFileSystem:
 
 
 def is_dfs(path) -> bool:
-    return str(path).startswith("hdfs://")
+    """True for paths served by a non-local FileSystem (hdfs://, har://)."""
+    return str(path).startswith(("hdfs://", "har://"))
+
+
+_HAR_CACHE: dict = {}
 
 
 def get_fs(path=None, conf=None):
-    """FileSystem for a path: ``hdfs://authority/...`` → hbmr.dfs, else local."""
+    """FileSystem for a path: ``hdfs://authority/...`` → hbmr.dfs, ``har://...`` →
+    a read-only Hadoop archive, else local."""
     p = str(path or "")
-    if is_dfs(p):
+    if p.startswith("har://"):
+        from ..tools.har import HarFileSystem, split_har_uri
+        key = split_har_uri(p)[0]
+        fs = _HAR_CACHE.get(key)
+        if fs is None:
+            fs = _HAR_CACHE[key] = HarFileSystem(p, conf)
+        return fs
+    if p.startswith("hdfs://"):
         from ..dfs.client import DistributedFileSystem, split_uri
         return DistributedFileSystem(split_uri(p)[0], conf)
     if "://" in p and not p.startswith("file://"):
