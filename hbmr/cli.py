@@ -14,6 +14,7 @@ jar/pipes/job/fs/version/... dispatch).
   hbmr archive -archiveName NAME.har -p PARENT SRC... DEST        (read back as har://)
   hbmr rumen TRACE_OUT TOPOLOGY_OUT HISTORY...                     (job-history traces)
   hbmr gridmix [-generate BYTES] [-jobtype LOADJOB|SLEEPJOB] [-policy REPLAY|STRESS|SERIAL] IOPATH TRACE
+  hbmr test TestDFSIO|nnbench|mrbench|testbigmapoutput|threadedmapbench|sortvalidate ...
   hbmr node            start this process's TaskTracker (+ JobTracker on rank 0)
                        under torchrun: one process per GPU
   hbmr run module:function [args]     run a user program (the ``jar`` analogue)
@@ -329,6 +330,9 @@ def main(argv=None):
         return _dfsadmin(rest)
     if cmd in ("run", "jar"):
         return _run(rest)
+    if cmd == "test":
+        from .benchmarks import driver as bdriver
+        return bdriver.main(rest)
     if cmd in TOOLS:
         return _run([TOOLS[cmd], *rest])
     if cmd == "version":

@@ -502,6 +502,10 @@ class MapTask(Task):
         R = job.get_num_reduce_tasks()
         committer = self.committer()
         committer.setup_task(job, self.attempt_id)
+        if isinstance(self.split, FileSplit):  # MapTask.updateJobWithSplit
+            job.set("map.input.file", self.split.path)
+            job.set_long("map.input.start", self.split.start)
+            job.set_long("map.input.length", self.split.length)
         informat = new_instance(job.get_input_format(), job)
         reader = informat.getRecordReader(self.split, job, rep)
         if isinstance(self.split, FileSplit):
