@@ -6,10 +6,11 @@ jar/pipes/job/fs/version/... dispatch).
   hbmr streaming -input I -output O -mapper CMD -reducer CMD ...
   hbmr job -jt host:port -list [all] | -status ID | -kill ID | -counter ID GROUP NAME
            | -tasks ID map|reduce | -history FILE
-  hbmr fs -ls|-lsr|-cat|-text|-put|-get|-cp|-mv|-rm|-rmr|-mkdir|-du|-setrep PATH...
+  hbmr fs -ls|-lsr|-cat|-text|-put|-get|-cp|-mv|-rm|-rmr|-mkdir|-du|-count [-q]|-setrep PATH...
                                       (local paths and hdfs://NAMENODE/... URIs)
   hbmr namenode -dir D [-port P] | datanode -nn HOST:PORT -dir D [-host H]
   hbmr fsck hdfs://NAMENODE/path | dfsadmin -nn NAMENODE -report|-safemode X|...
+  hbmr balancer -nn NAMENODE [-threshold PCT] | secondarynamenode -nn NAMENODE -dir D
   hbmr distcp [-update|-overwrite|-delete|-i|-p|-m N] SRC... DST   (file:// / hdfs://)
   hbmr archive -archiveName NAME.har -p PARENT SRC... DEST        (read back as har://)
   hbmr rumen TRACE_OUT TOPOLOGY_OUT HISTORY...                     (job-history traces)
@@ -87,7 +88,7 @@ def _fs(argv):
     from . import fs as F
     from .io import sequencefile as seqf
     if not argv:
-        print("hbmr fs -ls|-lsr|-cat|-text|-put|-get|-cp|-mv|-rm|-rmr|-mkdir|-du|-setrep PATH...",
+        print("hbmr fs -ls|-lsr|-cat|-text|-put|-get|-cp|-mv|-rm|-rmr|-mkdir|-du|-count [-q]|-setrep PATH...",
               file=sys.stderr)
         return 2
     op, paths = argv[0], [p[5:] if p.startswith("file:") and not p.startswith("file://") else p
@@ -163,6 +164,26 @@ def _fs(argv):
             tot = sum(st.length for st in _walk(p) if not st.is_dir)
             op = op_
             print(f"{tot}\t{p}")
+    elif op == "-count":
+        quota = bool(paths) and paths[0] == "-q"
+        for p in paths[1:] if quota else paths:
+            fs = F.get_fs(p)
+            if hasattr(fs, "get_content_summary"):
+                c = fs.get_content_summary(p)
+            else:
+                sts = list(_walk(p))
+                c = {"directoryCount": 1 + sum(st.is_dir for st in sts),
+                     "fileCount": sum(not st.is_dir for st in sts),
+                     "length": sum(st.length for st in sts if not st.is_dir),
+                     "quota": -1, "spaceQuota": -1, "spaceConsumed": 0}
+            cols = [c["directoryCount"], c["fileCount"], c["length"]]
+            if quota:
+                qn = c["quota"]
+                qs = c["spaceQuota"]
+                rem_n = "inf" if qn < 0 else qn - c["directoryCount"] - c["fileCount"]
+                rem_s = "inf" if qs < 0 else qs - c["spaceConsumed"]
+                cols = ["none" if qn < 0 else qn, rem_n, "none" if qs < 0 else qs, rem_s] + cols
+            print("\t".join(str(x) for x in cols + [p]))
     elif op == "-setrep":
         r, p = int(paths[0]), paths[1]
         F.get_fs(p).set_replication(p, r)
@@ -234,7 +255,8 @@ def _fsck(argv):
 
 def _dfsadmin(argv):
     """hbmr dfsadmin -nn AUTH -report | -safemode get|enter|leave | -saveNamespace
-    | -decommission DN_ID"""
+    | -decommission DN_ID | -setQuota N PATH.. | -clrQuota PATH.. | -setSpaceQuota BYTES PATH..
+    | -clrSpaceQuota PATH.. | -rollEditLog"""
     from .dfs.client import namenode_for
     if len(argv) < 3 or argv[0] != "-nn":
         print(_dfsadmin.__doc__, file=sys.stderr)
@@ -250,9 +272,62 @@ def _dfsadmin(argv):
         print("Save namespace " + ("successful" if nn.save_namespace() else "failed"))
     elif op == "-decommission":
         print("Decommission " + ("started" if nn.decommission(rest[0]) else "failed"))
+    elif op in ("-setQuota", "-setSpaceQuota"):
+        n, paths = int(rest[0]), rest[1:]
+        for p in paths:
+            cur = nn.get_content_summary(p)
+            ns, ds = cur["quota"], cur["spaceQuota"]
+            nn.set_quota(p, n if op == "-setQuota" else ns, n if op == "-setSpaceQuota" else ds)
+    elif op in ("-clrQuota", "-clrSpaceQuota"):
+        for p in rest:
+            cur = nn.get_content_summary(p)
+            nn.set_quota(p, -1 if op == "-clrQuota" else cur["quota"],
+                         -1 if op == "-clrSpaceQuota" else cur["spaceQuota"])
+    elif op == "-rollEditLog":
+        print(json.dumps(nn.roll_edit_log()))
     else:
         print(_dfsadmin.__doc__, file=sys.stderr)
         return 2
+    return 0
+
+
+def _balancer(argv):
+    """hbmr balancer -nn AUTH [-threshold PCT]"""
+    import argparse
+    from .dfs.balancer import Balancer
+    from .dfs.client import namenode_for
+    ap = argparse.ArgumentParser(prog="hbmr balancer")
+    ap.add_argument("-nn", required=True)
+    ap.add_argument("-threshold", type=float, default=10.0)
+    a = ap.parse_args(argv)
+    b = Balancer(namenode_for(a.nn), a.threshold)
+    rc = b.run()
+    print(f"Balancing took effect: moved {b.moved_blocks} blocks ({b.moved_bytes} bytes); "
+          f"exit status {rc}")
+    return 0 if rc > 0 else 1
+
+
+def _secondarynamenode(argv):
+    """hbmr secondarynamenode -nn AUTH -dir CHECKPOINT_DIR [-period S] [-checkpoint]"""
+    import argparse
+    import time
+    from .dfs.client import namenode_for
+    from .dfs.secondary import SecondaryNameNode
+    ap = argparse.ArgumentParser(prog="hbmr secondarynamenode")
+    ap.add_argument("-nn", required=True)
+    ap.add_argument("-dir", required=True)
+    ap.add_argument("-period", type=float, default=3600.0)
+    ap.add_argument("-checkpoint", action="store_true", help="one checkpoint, then exit")
+    a = ap.parse_args(argv)
+    snn = SecondaryNameNode(namenode_for(a.nn), a.dir, period_s=a.period)
+    if a.checkpoint:
+        return 0 if snn.do_checkpoint() else 1
+    snn.start()
+    try:
+        while True:
+            time.sleep(1.0)
+    except KeyboardInterrupt:
+        snn.shutdown()
     return 0
 
 
@@ -328,6 +403,10 @@ def main(argv=None):
         return _fsck(rest)
     if cmd == "dfsadmin":
         return _dfsadmin(rest)
+    if cmd == "balancer":
+        return _balancer(rest)
+    if cmd == "secondarynamenode":
+        return _secondarynamenode(rest)
     if cmd in ("run", "jar"):
         return _run(rest)
     if cmd == "test":

@@ -275,6 +275,12 @@ class DistributedFileSystem:
     def set_replication(self, path, r):
         return self.nn.set_replication(self._p(path), r)
 
+    def set_quota(self, path, ns_quota=-1, ds_quota=-1):
+        return self.nn.set_quota(self._p(path), ns_quota, ds_quota)
+
+    def get_content_summary(self, path):
+        return self.nn.get_content_summary(self._p(path))
+
     def get_file_block_locations(self, path, start, length):
         """[(offset, length, [hosts])] of the blocks overlapping [start, start+length)."""
         return [(b["offset"], b["length"], b["hosts"])

@@ -53,6 +53,7 @@ class DataNode:
     def __init__(self, conf, namenode, dn_id, host, data_dir, rack="/default-rack",
                  serve_rpc=False):
         g = (lambda k, d: conf.get_int(k, d)) if conf is not None else (lambda k, d: d)
+        self.conf = conf
         self.bpc = g("io.bytes.per.checksum", 512)
         self.hb_interval = g("dfs.heartbeat.interval.ms", 3000) / 1000.0
         self.nn = namenode
@@ -80,9 +81,16 @@ class DataNode:
         return os.path.join(self.dir, f"blk_{bid}")
 
     def _capacity(self):
+        """Configured capacity (``dfs.datanode.capacity`` bytes, hbmr key) or the
+        volume size, minus ``dfs.datanode.du.reserved``."""
+        c = self.conf
+        fixed = c.get_long("dfs.datanode.capacity", 0) if c is not None else 0
+        reserved = c.get_long("dfs.datanode.du.reserved", 0) if c is not None else 0
+        if fixed > 0:
+            return max(0, fixed - reserved)
         try:
             st = os.statvfs(self.dir)
-            return st.f_blocks * st.f_frsize
+            return max(0, st.f_blocks * st.f_frsize - reserved)
         except OSError:
             return 0
 

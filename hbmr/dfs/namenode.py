@@ -53,14 +53,22 @@ def norm(path: str) -> str:
     return p
 
 
+class QuotaExceededException(IOError):
+    pass
+
+
 class NameNode:
     METHODS = ["mkdirs", "create", "add_block", "complete", "get_block_locations",
                "get_file_info", "list_status", "rename", "delete", "set_replication",
                "register_datanode", "dn_heartbeat", "block_received", "block_report",
                "report_bad_block", "fsck", "datanode_report", "save_namespace", "safemode",
-               "datanode_address", "decommission"]
+               "datanode_address", "decommission", "roll_edit_log", "get_checkpoint_files",
+               "install_checkpoint", "get_blocks", "move_block", "pending_moves",
+               "set_quota", "get_content_summary"]
 
-    def __init__(self, conf=None, name_dir=None):
+    def __init__(self, conf=None, name_dir=None, checkpoint_only=False):
+        """checkpoint_only: load image + edits for an offline merge (the
+        SecondaryNameNode's working copy): no monitor thread, no edit log."""
         g = (lambda k, d: conf.get_int(k, d)) if conf is not None else (lambda k, d: d)
         gl = (lambda k, d: conf.get_long(k, d)) if conf is not None else (lambda k, d: d)
         gf = (lambda k, d: conf.get_float(k, d)) if conf is not None else (lambda k, d: d)
@@ -77,6 +85,12 @@ class NameNode:
         self.invalidate: dict[str, set] = {}      # dn -> block ids to delete
         self.pending_repl: dict[int, float] = {}  # block -> deadline
         self.leases: dict[str, str] = {}
+        self.lease_time: dict[str, float] = {}
+        self.lease_hard_limit = g("dfs.lease.hard.limit.ms", 3600 * 1000) / 1000.0
+        self.moves: dict[int, tuple] = {}          # block -> (src, dst, deadline) (Balancer)
+        self.quotas: dict[str, dict] = {}          # dir -> {"ns": n, "ds": bytes}; -1 = none
+        self.segment = 0                           # id of the open edit-log segment
+        self.image_through = -1                    # last segment merged into fsimage
         self.next_block = 1
         self.safe_mode = False
         self.manual_safe_mode = False
@@ -85,7 +99,13 @@ class NameNode:
         if name_dir:
             os.makedirs(name_dir, exist_ok=True)
             self._load()
-            self._edits = open(os.path.join(name_dir, "edits"), "a", buffering=1)
+            if checkpoint_only:
+                return
+            ed = os.path.join(name_dir, "edits")
+            fresh = not os.path.exists(ed) or os.path.getsize(ed) == 0
+            self._edits = open(ed, "a", buffering=1)
+            if fresh:
+                self._log("segment", id=self.segment)
         self.safe_mode = bool(self.blocks)
         self._mon = threading.Thread(target=self._monitor, daemon=True, name="ReplicationMonitor")
         self._mon.start()
@@ -104,17 +124,27 @@ class NameNode:
                 d = json.load(f)
             self.inodes = d["inodes"]
             self.next_block = d["next_block"]
+            self.quotas = d.get("quotas", {})
+            self.image_through = d.get("through_segment", -1)
+            self.segment = self.image_through + 1
         for ino in self.inodes.values():
             if ino["type"] == "file":
                 for b in ino["blocks"]:
                     self.blocks[b["id"]] = {"len": b["len"], "locs": set(), "file": None}
-        ed = os.path.join(self.name_dir, "edits")
-        if os.path.exists(ed):
+        # edits.old = a rolled segment a checkpoint has not merged yet (a crash between
+        # roll and install); skipped when the image already went through it
+        for name in ("edits.old", "edits"):
+            ed = os.path.join(self.name_dir, name)
+            if not os.path.exists(ed):
+                continue
             with open(ed) as f:
-                for line in f:
-                    line = line.strip()
-                    if line:
-                        self._replay(json.loads(line))
+                lines = [json.loads(x) for x in f if x.strip()]
+            if lines and lines[0].get("op") == "segment":
+                if lines[0]["id"] <= self.image_through:
+                    continue
+                self.segment = max(self.segment, lines[0]["id"])
+            for e in lines:
+                self._replay(e)
         for path, ino in self.inodes.items():
             if ino["type"] == "file":
                 for b in ino["blocks"]:
@@ -122,6 +152,8 @@ class NameNode:
 
     def _replay(self, e):
         op = e["op"]
+        if op == "segment":
+            return
         if op == "mkdir":
             self.inodes[e["path"]] = {"type": "dir", "mtime": e["t"]}
         elif op == "create":
@@ -148,18 +180,84 @@ class NameNode:
             self._do_delete(e["path"])
         elif op == "set_repl":
             self.inodes[e["path"]]["repl"] = e["repl"]
+        elif op == "abandon_block":
+            ino = self.inodes[e["path"]]
+            ino["blocks"] = [b for b in ino["blocks"] if b["id"] != e["id"]]
+            self.blocks.pop(e["id"], None)
+        elif op == "set_quota":
+            self.quotas[e["path"]] = {"ns": e["ns"], "ds": e["ds"]}
+
+    def _image(self, through):
+        return {"inodes": self.inodes, "next_block": self.next_block, "quotas": self.quotas,
+                "through_segment": through}
 
     def save_namespace(self):
-        """Checkpoint: write fsimage.json, truncate the edit log."""
+        """Checkpoint in place (dfsadmin -saveNamespace): write fsimage.json, start a
+        new edit-log segment."""
         if not self.name_dir:
             return False
         with self.lock:
             tmp = os.path.join(self.name_dir, "fsimage.json.tmp")
             with open(tmp, "w") as f:
-                json.dump({"inodes": self.inodes, "next_block": self.next_block}, f)
+                json.dump(self._image(self.segment), f)
             os.replace(tmp, os.path.join(self.name_dir, "fsimage.json"))
-            self._edits.close()
+            self.image_through = self.segment
+            self.segment += 1
+            old = os.path.join(self.name_dir, "edits.old")
+            if os.path.exists(old):
+                os.remove(old)
+            if self._edits is not None:
+                self._edits.close()
             self._edits = open(os.path.join(self.name_dir, "edits"), "w", buffering=1)
+            self._log("segment", id=self.segment)
+        return True
+
+    # -- SecondaryNameNode protocol (rollEditLog / GetImageServlet / rollFsImage) ----------
+    def roll_edit_log(self):
+        """Close the current segment as edits.old and open a new one; the
+        SecondaryNameNode then merges fsimage + edits.old offline."""
+        if not self.name_dir:
+            raise IOError("NameNode has no name dir")
+        with self.lock:
+            old = os.path.join(self.name_dir, "edits.old")
+            if os.path.exists(old):
+                return {"segment": self._old_segment(old), "rolled": False}
+            self._edits.close()
+            os.replace(os.path.join(self.name_dir, "edits"), old)
+            rolled = self.segment
+            self.segment += 1
+            self._edits = open(os.path.join(self.name_dir, "edits"), "w", buffering=1)
+            self._log("segment", id=self.segment)
+        return {"segment": rolled, "rolled": True}
+
+    @staticmethod
+    def _old_segment(path):
+        with open(path) as f:
+            first = f.readline()
+        return json.loads(first)["id"] if first.strip() else -1
+
+    def get_checkpoint_files(self):
+        """(fsimage text, edits.old text) — what GetImageServlet serves."""
+        img = os.path.join(self.name_dir, "fsimage.json")
+        old = os.path.join(self.name_dir, "edits.old")
+        read = (lambda q: open(q).read() if os.path.exists(q) else "")
+        return {"image": read(img), "edits": read(old)}
+
+    def install_checkpoint(self, image_text, through_segment):
+        """Replace fsimage with the merged one and drop edits.old (rollFsImage)."""
+        with self.lock:
+            old = os.path.join(self.name_dir, "edits.old")
+            if not os.path.exists(old) or self._old_segment(old) != through_segment:
+                raise IOError("checkpoint does not match the rolled edit log")
+            d = json.loads(image_text)
+            if d.get("through_segment") != through_segment:
+                raise IOError("image was not merged through the rolled segment")
+            tmp = os.path.join(self.name_dir, "fsimage.json.ckpt")
+            with open(tmp, "w") as f:
+                f.write(image_text)
+            os.replace(tmp, os.path.join(self.name_dir, "fsimage.json"))
+            os.remove(old)
+            self.image_through = through_segment
         return True
 
     # -- namespace ----------------------------------------------------------------------
@@ -179,6 +277,9 @@ class NameNode:
         with self.lock:
             self._check_safe()
             t = time.time()
+            new = [q for q in [p] + self._parents(p) if q not in self.inodes]
+            if new:
+                self._check_ns_quota(p, len(new))
             for q in reversed([p] + self._parents(p)):
                 ino = self.inodes.get(q)
                 if ino is None:
@@ -204,6 +305,7 @@ class NameNode:
             parent = posixpath.dirname(p)
             if parent not in self.inodes:
                 self.mkdirs(parent)
+            self._check_ns_quota(p, 1)
             repl = int(replication or self.replication)
             bs = int(block_size or self.block_size)
             t = time.time()
@@ -211,6 +313,7 @@ class NameNode:
             self.inodes[p] = {"type": "file", "blocks": [], "repl": repl, "bs": bs, "len": 0,
                               "mtime": t, "uc": True}
             self.leases[p] = client
+            self.lease_time[p] = time.time()
         return {"block_size": bs, "replication": repl}
 
     def add_block(self, path, client="", prev_len=0, writer_host=None):
@@ -220,12 +323,14 @@ class NameNode:
             ino = self.inodes.get(p)
             if ino is None or ino["type"] != "file" or not ino.get("uc"):
                 raise FileNotFoundError(f"{p} is not open for writing")
-            bid = self.next_block
-            self.next_block += 1
-            self._log("add_block", path=p, id=bid, prev_len=prev_len)
             if ino["blocks"]:
                 ino["blocks"][-1]["len"] = prev_len
                 self.blocks[ino["blocks"][-1]["id"]]["len"] = prev_len
+            self._check_ds_quota(p, ino["bs"] * ino["repl"])
+            self.lease_time[p] = time.time()
+            bid = self.next_block
+            self.next_block += 1
+            self._log("add_block", path=p, id=bid, prev_len=prev_len)
             ino["blocks"].append({"id": bid, "len": 0})
             self.blocks[bid] = {"len": 0, "locs": set(), "file": p}
             targets = self.choose_targets(ino["repl"], writer_host)
@@ -247,7 +352,101 @@ class NameNode:
             ino["uc"] = False
             ino["mtime"] = time.time()
             self.leases.pop(p, None)
+            self.lease_time.pop(p, None)
         return True
+
+    # -- quotas (dfsadmin -setQuota/-setSpaceQuota, fs -count -q) ------------------------
+    def _usage(self, d):
+        pre = d.rstrip("/") + "/"
+        names = space = 0
+        dirs = files = length = 0
+        for q, ino in self.inodes.items():
+            if q == d or q.startswith(pre) or d == "/":
+                names += 1
+                if ino["type"] == "dir":
+                    dirs += 1
+                else:
+                    files += 1
+                    length += ino["len"]
+                    space += sum(max(b["len"], 0) for b in ino["blocks"]) * ino["repl"]
+                    if ino.get("uc") and ino["blocks"]:   # open last block: charged in full
+                        space += max(0, ino["bs"] - ino["blocks"][-1]["len"]) * ino["repl"]
+        return {"names": names, "space": space, "dirs": dirs, "files": files, "length": length}
+
+    def _quota_dirs(self, p):
+        return [q for q in [p] + self._parents(p) if q in self.quotas]
+
+    def _check_ns_quota(self, p, n_new):
+        for q in self._quota_dirs(p):
+            ns = self.quotas[q]["ns"]
+            if ns >= 0 and self._usage(q)["names"] + n_new > ns:
+                raise QuotaExceededException(f"The NameSpace quota (directories and files) "
+                                             f"of directory {q} is exceeded: quota={ns}")
+
+    def _check_ds_quota(self, p, nbytes):
+        for q in self._quota_dirs(p):
+            ds = self.quotas[q]["ds"]
+            if ds >= 0 and self._usage(q)["space"] + nbytes > ds:
+                raise QuotaExceededException(f"The DiskSpace quota of {q} is exceeded: "
+                                             f"quota={ds}")
+
+    def set_quota(self, path, ns_quota=-1, ds_quota=-1):
+        """ns_quota / ds_quota < 0 clears that quota (HdfsConstants.QUOTA_RESET)."""
+        p = norm(path)
+        with self.lock:
+            self._check_safe()
+            ino = self.inodes.get(p)
+            if ino is None or ino["type"] != "dir":
+                raise FileNotFoundError(f"{p} is not a directory")
+            self._log("set_quota", path=p, ns=int(ns_quota), ds=int(ds_quota))
+            if ns_quota < 0 and ds_quota < 0:
+                self.quotas.pop(p, None)
+            else:
+                self.quotas[p] = {"ns": int(ns_quota), "ds": int(ds_quota)}
+        return True
+
+    def get_content_summary(self, path):
+        p = norm(path)
+        with self.lock:
+            if p not in self.inodes:
+                raise FileNotFoundError(p)
+            u = self._usage(p)
+            q = self.quotas.get(p, {"ns": -1, "ds": -1})
+            return {"directoryCount": u["dirs"], "fileCount": u["files"], "length": u["length"],
+                    "spaceConsumed": u["space"], "quota": q["ns"], "spaceQuota": q["ds"]}
+
+    # -- Balancer support (NamenodeProtocol.getBlocks + replace-block) -----------------------
+    def get_blocks(self, dn_id, max_bytes=None):
+        with self.lock:
+            out, tot = [], 0
+            for bid, info in self.blocks.items():
+                if dn_id in info["locs"] and info.get("file") and bid not in self.moves:
+                    out.append({"block": bid, "len": info["len"], "locs": sorted(info["locs"])})
+                    tot += info["len"]
+                    if max_bytes is not None and tot >= max_bytes:
+                        break
+            return out
+
+    def move_block(self, block, src, dst):
+        """Copy a replica src → dst, then drop it from src (the Balancer's move)."""
+        with self.lock:
+            info = self.blocks.get(block)
+            if info is None or src not in info["locs"] or dst in info["locs"]:
+                return False
+            d = self.datanodes.get(dst)
+            if d is None or not d["alive"] or d["decommission"]:
+                return False
+            self.moves[block] = (src, dst, time.time() + 60.0)
+            self.datanodes[src].setdefault("repl_cmds", []).append(
+                {"cmd": "replicate", "block": block, "targets": [dst]})
+        return True
+
+    def pending_moves(self):
+        with self.lock:
+            now = time.time()
+            for b in [b for b, m in self.moves.items() if m[2] < now]:
+                self.moves.pop(b)
+            return len(self.moves)
 
     def _info(self, p, ino):
         if ino["type"] == "dir":
@@ -407,6 +606,12 @@ class NameNode:
             info["locs"].add(dn_id)
             info["len"] = max(info.get("len", 0), length)
             self.pending_repl.pop(block, None)
+            mv = self.moves.get(block)
+            if mv is not None and mv[1] == dn_id:   # balancer move landed: drop the source
+                self.moves.pop(block)
+                if mv[0] in info["locs"] and len(info["locs"]) > 1:
+                    info["locs"].discard(mv[0])
+                    self.invalidate.setdefault(mv[0], set()).add(block)
         return True
 
     def block_report(self, dn_id, blocks):
@@ -496,8 +701,34 @@ class NameNode:
             except Exception:  # noqa: BLE001
                 log.exception("replication monitor")
 
+    def recover_leases(self):
+        """Files whose writer vanished past the hard limit are closed with the
+        lengths the DataNodes hold (LeaseManager.Monitor → internalReleaseLease)."""
+        now = time.time()
+        with self.lock:
+            for p, t in list(self.lease_time.items()):
+                ino = self.inodes.get(p)
+                if ino is None or not ino.get("uc"):
+                    self.lease_time.pop(p, None)
+                    continue
+                if now - t < self.lease_hard_limit:
+                    continue
+                last = 0
+                if ino["blocks"]:
+                    info = self.blocks.get(ino["blocks"][-1]["id"], {})
+                    last = info.get("len", 0)
+                    if not info.get("locs"):   # last block never reached a DataNode
+                        dead = ino["blocks"].pop()
+                        self.blocks.pop(dead["id"], None)
+                        self._log("abandon_block", path=p, id=dead["id"])
+                        last = ino["blocks"][-1]["len"] if ino["blocks"] else 0
+                log.warning("lease of %s (holder %s) expired; closing the file", p,
+                            self.leases.get(p))
+                self.complete(p, self.leases.get(p, ""), last)
+
     def check_replication(self):
         now = time.time()
+        self.recover_leases()
         with self.lock:
             for d in self.datanodes.values():
                 if d["alive"] and now - d["last"] > self.dead_interval:
