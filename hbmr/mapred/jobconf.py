@@ -140,15 +140,18 @@ class JobConf(Configuration):
         self.set_class("mapred.output.value.class", c)
 
     def get_map_output_key_class(self):
+        """Writable class, or a serializer adapter for plain types (io.serializations)."""
+        from ..io.serializer import adapter_for
         c = self._cls("mapred.mapoutput.key.class", None)
-        return c if c is not None else self.get_output_key_class()
+        return adapter_for(c if c is not None else self.get_output_key_class(), self)
 
     def set_map_output_key_class(self, c):
         self.set_class("mapred.mapoutput.key.class", c)
 
     def get_map_output_value_class(self):
+        from ..io.serializer import adapter_for
         c = self._cls("mapred.mapoutput.value.class", None)
-        return c if c is not None else self.get_output_value_class()
+        return adapter_for(c if c is not None else self.get_output_value_class(), self)
 
     def set_map_output_value_class(self, c):
         self.set_class("mapred.mapoutput.value.class", c)

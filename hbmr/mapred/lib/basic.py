@@ -9,6 +9,7 @@ import bisect
 import random
 import re
 
+from ...io.serializer import hash_code as serializer_hash
 from ...io.writable import IntWritable, LongWritable, Text, hash_bytes
 from ..api import Mapper, Partitioner, Reducer
 
@@ -28,7 +29,8 @@ class HashPartitioner(Partitioner):
     """(key.hashCode() & Integer.MAX_VALUE) % numReduceTasks (HashPartitioner.java:31-34)."""
 
     def getPartition(self, key, value, num_partitions):  # noqa: N802
-        return (key.hash_code() & 0x7FFFFFFF) % num_partitions
+        h = key.hash_code() if hasattr(key, "hash_code") else serializer_hash(key)
+        return (h & 0x7FFFFFFF) % num_partitions
 
 
 class TokenCountMapper(Mapper):

@@ -30,6 +30,7 @@ import numpy as np
 
 from ..io.compress import get_codec
 from ..io.ifile import IFileWriter, SpillRecord, read_segment
+from ..io.serializer import to_bytes
 from ..utils.reflection import new_instance
 from . import counters as C
 from . import sortbuf
@@ -205,8 +206,8 @@ def run_combiner(combiner_cls, job, kcls, vcls, records, reporter):
     reporter.incrCounter(C.TASK_GROUP, C.COMBINE_OUTPUT_RECORDS, len(col.out))
     out = []
     for k, v in col.out:
-        kb = k.serialize()
-        out.append((sort_key(kb), kb, v.serialize()))
+        kb = to_bytes(k, kcls)
+        out.append((sort_key(kb), kb, to_bytes(v, vcls)))
     out.sort(key=lambda r: r[0])
     return out
 
@@ -255,8 +256,8 @@ class MapOutputBuffer(OutputCollector):
         if not isinstance(value, self.vcls):
             raise TypeError(f"Type mismatch in value from map: expected {self.vcls.__name__}, "
                             f"received {type(value).__name__}")
-        kb = key.serialize()
-        vb = value.serialize()
+        kb = to_bytes(key, self.kcls)
+        vb = to_bytes(value, self.vcls)
         if self.native_hash:
             self.keys.append(kb)
             self.vals.append(vb)
@@ -349,8 +350,8 @@ class MapOutputBuffer(OutputCollector):
         comb.close()
         self.reporter.incrCounter(C.TASK_GROUP, C.COMBINE_INPUT_RECORDS, hi - lo)
         self.reporter.incrCounter(C.TASK_GROUP, C.COMBINE_OUTPUT_RECORDS, len(col.out))
-        ob = sortbuf.Batch.from_lists([k.serialize() for k, _ in col.out],
-                                      [v.serialize() for _, v in col.out])
+        ob = sortbuf.Batch.from_lists([to_bytes(k, self.kcls) for k, _ in col.out],
+                                      [to_bytes(v, self.vcls) for _, v in col.out])
         operm = ob.sort(self.kind, np.zeros(ob.n, np.int32))
         return ob.ifile_body(operm, 0, ob.n), ob.n
 
