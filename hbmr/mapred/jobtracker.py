@@ -410,6 +410,8 @@ class JobTracker:
         self.lock = threading.RLock()
         self.cv = threading.Condition(self.lock)
         self.jobs: dict[str, JobInProgress] = {}
+        from ..security import JobTokenSecretManager
+        self.job_tokens = JobTokenSecretManager()
         self.job_queue: list[JobInProgress] = []
         self.trackers: dict[str, TrackerInfo] = {}
         self.attempt_index: dict[str, Attempt] = {}
@@ -601,7 +603,15 @@ class JobTracker:
         if TRACE.on:
             TRACE.instant("jt.submit")
         METRICS.inc("hbmr_jobs_submitted_total", help="jobs submitted")
+        from .. import security as SEC
+        if SEC.acls_enabled(self.conf) and job_id is None:
+            ugi = SEC.UserGroupInformation.get_current_user()
+            SEC.QueueManager(self.conf).check_submit(conf.get("mapred.job.queue.name",
+                                                              "default"), ugi)
+            conf.set("user.name", ugi.user)   # the authenticated submitter owns the job
         jid = job_id or self.new_job_id()
+        conf.set("mapred.job.id", str(jid))
+        self.job_tokens.add_job(jid)
         self._persist_job(jid, conf)
         jip = JobInProgress(self, jid, conf)
         with self.lock:
@@ -628,7 +638,20 @@ class JobTracker:
             jip = self.jobs.get(str(job_id))
         return None if jip is None else RunningJob(jip.job_id, _JTJobHandle(jip), jip.conf)
 
+    def check_access(self, job_id, op):
+        """JobACLsManager check for the current (RPC or doAs) user; raises
+        AccessControlException (mapred.acls.enabled)."""
+        from .. import security as SEC
+        jip = self.jobs.get(str(job_id))
+        if jip is None:
+            raise KeyError(f"unknown job {job_id}")
+        SEC.check_job_access(self.conf, jip.conf, SEC.UserGroupInformation.get_current_user(),
+                             SEC.MODIFY_JOB if op == "modify" else SEC.VIEW_JOB)
+        return jip
+
     def kill_job(self, job_id):
+        if str(job_id) in self.jobs:
+            self.check_access(job_id, "modify")
         with self.lock:
             jip = self.jobs.get(str(job_id))
             if jip is None or jip.completed():
@@ -1026,7 +1049,7 @@ class JobTracker:
         return str(self.submit_job(conf).getID())
 
     def rpc_job_status(self, jid):
-        jip = self.jobs[str(jid)]
+        jip = self.check_access(jid, "view")
         st = jip.status
         return {"state": st.state, "map_progress": st.map_progress,
                 "reduce_progress": st.reduce_progress, "start_time": st.start_time,
@@ -1037,7 +1060,7 @@ class JobTracker:
         self.kill_job(jid)
 
     def rpc_job_result(self, jid):
-        return self.jobs[str(jid)].result
+        return self.check_access(jid, "view").result
 
     def rpc_list_jobs(self, all_jobs=False):
         """JobSubmissionProtocol.jobsToComplete / getAllJobs."""
@@ -1056,7 +1079,7 @@ class JobTracker:
             return out
 
     def rpc_task_reports(self, jid, is_map=True):
-        jip = self.jobs[str(jid)]
+        jip = self.check_access(jid, "view")
         with self.lock:
             return [{"task": str(r.getTaskID()), "state": r.state, "progress": r.progress,
                      "start": r.getStartTime(), "finish": r.getFinishTime(),

@@ -20,6 +20,7 @@ import torch
 from ..parallel.collectives import SoloComm, TorchComm
 from .jobconf import JobConf
 from .jobtracker import JobTracker
+from ..security import rpc_secret
 from .rpc import JT_METHODS, JobTrackerProxy, RpcServer
 from .tasktracker import TaskTracker
 
@@ -60,13 +61,13 @@ class Node:
         if self.rank == 0:
             self.jt = JobTracker(self.conf)
             if self.world > 1:
-                self.server = RpcServer(self.jt, JT_METHODS).start()
+                self.server = RpcServer(self.jt, JT_METHODS, secret=rpc_secret(self.conf)).start()
                 host = os.environ.get("MASTER_ADDR", "127.0.0.1")
                 self.store.set("hbmr/jobtracker", f"{host}:{self.server.port}")
             jt_handle = self.jt
         else:
             addr = self.store.get("hbmr/jobtracker").decode()
-            jt_handle = JobTrackerProxy(addr)
+            jt_handle = JobTrackerProxy(addr, self.conf)
         simulate = self.conf.get_boolean("hbmr.gpu.simulate", False)
         gpus = [self.local_rank] if (self.use_gpu or simulate) else []
         self.tt = TaskTracker(self.conf, jt_handle,

@@ -8,10 +8,21 @@ InterTrackerProtocol (heartbeat / wakeup) and the JobSubmissionProtocol
 ``{"m": method, "a": args, "k": kwargs}`` → ``{"r": result}`` or ``{"e": error}``.
 Sockets use TCP_NODELAY; clients keep one connection per thread so a
 long-polling heartbeat never blocks a concurrent wakeup.
+
+Authentication (hbmr.security): every call carries the caller's user name
+(Hadoop "simple" auth), which the server installs as the current
+UserGroupInformation while the method runs (ACL checks use it).  A server
+given a cluster secret (``hbmr.rpc.secret`` / ``HBMR_RPC_SECRET``) first sends
+a random challenge and only serves connections that answer
+HMAC-SHA256(secret, challenge ‖ user); the user is then taken from the
+authenticated handshake, not from the calls.
 """
 from __future__ import annotations
 
+import contextlib
+import hmac
 import logging
+import secrets as _secrets
 import socket
 import socketserver
 import struct
@@ -44,26 +55,69 @@ def _recv(sock):
     return msgpack.unpackb(_recv_exact(sock, n), raw=False, strict_map_key=False)
 
 
+_ENV = object()
+
+
+def _conf_secret(conf):
+    from ..security import rpc_secret
+    return rpc_secret(conf)
+
+
+def _secret(v):
+    if v is _ENV:
+        from ..security import rpc_secret
+        return rpc_secret(None)
+    return v.encode() if isinstance(v, str) else v
+
+
 class RpcServer:
-    def __init__(self, target, methods, host="0.0.0.0", port=0):
+    def __init__(self, target, methods, host="0.0.0.0", port=0, secret=_ENV):
+        from ..security import UserGroupInformation, rpc_response
         self.target = target
         self.methods = set(methods)
+        self.secret = _secret(secret)
         outer = self
 
         class Handler(socketserver.BaseRequestHandler):
+            def _authenticate(self, s):
+                nonce = _secrets.token_bytes(16)
+                _send(s, {"challenge": nonce})
+                auth = _recv(s)
+                user = str(auth.get("user", "")) if isinstance(auth, dict) else ""
+                want = rpc_response(outer.secret, nonce, user)
+                if not (isinstance(auth, dict) and isinstance(auth.get("auth"), str) and
+                        hmac.compare_digest(auth["auth"], want)):
+                    _send(s, {"e": "AccessControlException: RPC authentication failed"})
+                    return None
+                _send(s, {"r": "ok"})
+                return user
+
             def handle(self):
                 s = self.request
                 s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                authed = None
+                if outer.secret:
+                    try:
+                        authed = self._authenticate(s)
+                    except (ConnectionError, OSError, ValueError):
+                        return
+                    if authed is None:
+                        return
                 while True:
                     try:
                         req = _recv(s)
                     except (ConnectionError, OSError):
                         return
                     m = req.get("m")
+                    user = authed or req.get("u")
+                    ctx = UserGroupInformation.create_remote_user(user).do_as() if user \
+                        else contextlib.nullcontext()
                     try:
                         if m not in outer.methods:
                             raise AttributeError(f"no RPC method {m!r}")
-                        res = getattr(outer.target, m)(*req.get("a", ()), **req.get("k", {}))
+                        with ctx:
+                            res = getattr(outer.target, m)(*req.get("a", ()),
+                                                           **req.get("k", {}))
                         _send(s, {"r": res})
                     except Exception as e:  # noqa: BLE001
                         log.debug("rpc %s failed", m, exc_info=True)
@@ -98,25 +152,48 @@ class RpcError(RuntimeError):
 
 
 class RpcClient:
-    def __init__(self, address: str, timeout: float = 600.0):
+    def __init__(self, address: str, timeout: float = 600.0, secret=_ENV):
         host, port = address.rsplit(":", 1)
         self.addr = (host, int(port))
         self.timeout = timeout
+        self.secret = _secret(secret)
         self._tl = threading.local()
 
     def _sock(self):
         s = getattr(self._tl, "sock", None)
+        if s is not None and self.secret:
+            from ..security import UserGroupInformation
+            if getattr(self._tl, "user", None) != UserGroupInformation.get_current_user().user:
+                s.close()   # the handshake bound another identity: reconnect
+                s = self._tl.sock = None
         if s is None:
             s = socket.create_connection(self.addr, timeout=self.timeout)
             s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            if self.secret:
+                self._handshake(s)
             self._tl.sock = s
         return s
 
+    def _handshake(self, s):
+        from ..security import UserGroupInformation, rpc_response
+        hello = _recv(s)
+        if "challenge" not in hello:
+            raise RpcError(f"server did not start the RPC handshake: {hello}")
+        user = UserGroupInformation.get_current_user().user
+        self._tl.user = user
+        _send(s, {"user": user, "auth": rpc_response(self.secret, hello["challenge"], user)})
+        resp = _recv(s)
+        if "e" in resp:
+            s.close()
+            raise RpcError(resp["e"])
+
     def call(self, method, *args, **kwargs):
+        from ..security import UserGroupInformation
+        user = UserGroupInformation.get_current_user().user
         for attempt in range(2):
             s = self._sock()
             try:
-                _send(s, {"m": method, "a": list(args), "k": kwargs})
+                _send(s, {"m": method, "a": list(args), "k": kwargs, "u": user})
                 resp = _recv(s)
                 break
             except (ConnectionError, OSError):
@@ -129,6 +206,9 @@ class RpcClient:
                     raise
         if "e" in resp:
             raise RpcError(resp["e"])
+        if "challenge" in resp:
+            self.close()
+            raise RpcError("server requires RPC authentication (set hbmr.rpc.secret)")
         return resp.get("r")
 
     def close(self):
@@ -145,8 +225,8 @@ JT_METHODS = ("heartbeat", "wakeup", "rpc_submit_job", "rpc_job_status", "rpc_ki
 class JobTrackerProxy:
     """TaskTracker/JobClient-side stub of a remote JobTracker."""
 
-    def __init__(self, address):
-        self.rpc = RpcClient(address)
+    def __init__(self, address, conf=None):
+        self.rpc = RpcClient(address, secret=_conf_secret(conf))
         self.address = address
 
     def heartbeat(self, status, initial=False, accept_new_tasks=True, block=0.0):
@@ -198,7 +278,7 @@ class JobTrackerClient:
     """JobClient runner for ``mapred.job.tracker=host:port``."""
 
     def __init__(self, address, conf=None):
-        self.rpc = RpcClient(address)
+        self.rpc = RpcClient(address, secret=_conf_secret(conf))
 
     def submit_job(self, job):
         from .jobclient import RunningJob
