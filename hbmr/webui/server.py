@@ -13,6 +13,19 @@
                             one track per tracker slot kind, CPU/GPU coloured
   /metrics                  Prometheus text exposition (hbmr.utils.metrics)
   /api/cluster, /api/jobs, /api/job?jobid=ID    JSON
+  /jobconf.jsp?jobid=ID     the job's configuration
+  /jobtasks.jsp?jobid=ID&type=map|reduce&pagenum=N&state=running|completed|killed|all
+  /taskdetails.jsp?tipid=ID every attempt of a task (tracker, CPU/GPU, times, diagnostics)
+  /jobfailures.jsp?jobid=ID failed and killed attempts, grouped by tracker
+  /machines.jsp[?type=active|blacklisted]   trackers with slots, failures, health
+  /jobqueue_details.jsp?queueName=Q         a queue's jobs (+ its ACLs)
+  /jobhistory.jsp           completed-job history files; ?logFile=F → summary +
+                            rule-based analysis (analysejobhistory.jsp / Vaidya)
+
+:class:`DFSWebUI` serves the NameNode pages (webapps/hdfs): ``/dfshealth.jsp``
+(capacity, safe mode, live/dead DataNodes), ``/dfsnodelist.jsp?whatNodes=LIVE|DEAD``
+and ``/browseDirectory.jsp?dir=/path`` (nn_browsedfscontent; ``?filename=`` shows
+the first 32 KB of a file).
 
 Enabled by ``hbmr.webui.port`` (default 50030, the reference's
 mapred.job.tracker.http.address port; 0 = any free port; -1 = off).
@@ -152,7 +165,135 @@ class WebUI:
             return "application/json", json.dumps(self.jobs(), default=str)
         if path == "/api/job":
             return "application/json", json.dumps(self.job(q["jobid"]), default=str)
+        extra = {"/jobconf.jsp": self.jobconf_html, "/jobtasks.jsp": self.jobtasks_html,
+                 "/taskdetails.jsp": self.taskdetails_html, "/jobfailures.jsp":
+                 self.jobfailures_html, "/machines.jsp": self.machines_html,
+                 "/jobqueue_details.jsp": self.queue_html, "/jobhistory.jsp": self.history_html}
+        if path in extra:
+            return "text/html", extra[path](q)
         raise KeyError(path)
+
+    # -- the remaining webapps/job pages ------------------------------------------------------
+    def _jip(self, q):
+        jid = q.get("jobid")
+        if jid not in self.jt.jobs:
+            raise KeyError(f"job {jid}")
+        return jid, self.jt.jobs[jid]
+
+    def jobconf_html(self, q):
+        jid, jip = self._jip(q)
+        rows = [[html.escape(k), html.escape(str(v))] for k, v in sorted(jip.conf.items())]
+        return _page(f"Job Configuration: {jid}", _table(["name", "value"], rows))
+
+    @staticmethod
+    def _attempt_row(a):
+        where = f"<span class=gpu>gpu{a.device}</span>" if a.run_on_gpu else \
+            "<span class=cpu>cpu</span>"
+        dur = f"{a.finish - a.start:.3f}s" if a.finish and a.start else "-"
+        return [html.escape(str(a.aid)), a.state, where, html.escape(a.tracker or ""),
+                _fmt_t(a.start), _fmt_t(a.finish), dur,
+                f"{100 * (a.progress or 0):.0f}%", html.escape((a.diagnostic or "")[:300])]
+
+    _ATTEMPT_HDR = ["attempt", "state", "ran on", "tracker", "start", "finish", "time",
+                    "progress", "diagnostics"]
+
+    def jobtasks_html(self, q):
+        jid, jip = self._jip(q)
+        typ = q.get("type", "map")
+        want = q.get("state", "all")
+        page, per = int(q.get("pagenum", 1)), 200
+        with self.jt.lock:
+            tips = jip.maps if typ == "map" else jip.reduces
+            rows = []
+            for tip in tips:
+                st = ("completed" if tip.successful else "killed" if tip.killed else
+                      "running" if tip.attempts else "pending")
+                if want not in ("all", st):
+                    continue
+                a = tip.successful or (max(tip.attempts.values(), key=lambda x: x.start or 0)
+                                       if tip.attempts else None)
+                rows.append([f"<a href='/taskdetails.jsp?jobid={jid}&tipid={tip.tid}'>"
+                             f"{tip.tid}</a>", st, len(tip.attempts), tip.failures]
+                            + (self._attempt_row(a)[2:8] if a else ["-"] * 6))
+        body = _table(["task", "status", "attempts", "failures", "ran on", "tracker", "start",
+                       "finish", "time", "progress"], rows[(page - 1) * per:page * per])
+        return _page(f"{typ} tasks of {jid} ({want})", body)
+
+    def _tip(self, q):
+        tipid = q.get("tipid")
+        jids = [q["jobid"]] if q.get("jobid") else list(self.jt.jobs)
+        for jid in jids:
+            jip = self.jt.jobs.get(jid)
+            for tip in (jip.maps + jip.reduces) if jip else []:
+                if str(tip.tid) == tipid:
+                    return jid, tip
+        raise KeyError(f"task {tipid}")
+
+    def taskdetails_html(self, q):
+        jid, tip = self._tip(q)
+        with self.jt.lock:
+            rows = [self._attempt_row(a) for a in sorted(tip.attempts.values(),
+                                                         key=lambda a: str(a.aid))]
+        split = html.escape(str(getattr(tip.split, "path", tip.split))[:200]) if tip.split else "-"
+        return _page(f"Task {tip.tid}", f"<p>job {jid}; input split: {split}</p>"
+                     + _table(self._ATTEMPT_HDR, rows))
+
+    def jobfailures_html(self, q):
+        jid, jip = self._jip(q)
+        by_tracker: dict = {}
+        with self.jt.lock:
+            for tip in jip.maps + jip.reduces:
+                for a in tip.attempts.values():
+                    if a.state in ("FAILED", "KILLED"):
+                        by_tracker.setdefault(a.tracker or "?", []).append(self._attempt_row(a))
+        body = "".join(f"<h2>{html.escape(t)}</h2>" + _table(self._ATTEMPT_HDR, rows)
+                       for t, rows in sorted(by_tracker.items())) or "<p>no failures</p>"
+        return _page(f"Failures of {jid}", body)
+
+    def machines_html(self, q):
+        typ = q.get("type", "active")
+        with self.jt.lock:
+            rows = [[html.escape(n), t.status.max_cpu_map_slots,
+                     ", ".join(f"gpu{g['device']}" for g in t.status.gpus) or "-",
+                     t.status.max_reduce_slots, t.failures,
+                     "yes" if t.status.healthy else f"no: {html.escape(str(t.status.health_report))}",
+                     f"{time.time() - t.last_seen:.1f}s ago"]
+                    for n, t in sorted(self.jt.trackers.items())
+                    if (typ == "blacklisted") == bool(t.blacklisted)]
+        return _page(f"{typ.capitalize()} Task Trackers",
+                     _table(["tracker", "CPU map slots", "GPUs", "reduce slots", "failures",
+                             "healthy", "last heartbeat"], rows))
+
+    def queue_html(self, q):
+        from ..security import QueueManager
+        name = q.get("queueName", "default")
+        qm = QueueManager(self.jt.conf)
+        acls = [[op, html.escape(str(qm.acl(name, op)))] for op in ("acl-submit-job",
+                                                                    "acl-administer-jobs")]
+        jobs = [[f"<a href='/jobdetails?jobid={j['id']}'>{j['id']}</a>", html.escape(j["name"]),
+                 html.escape(str(j["user"])), j["state"]]
+                for j in self.jobs()
+                if self.jt.jobs[j["id"]].conf.get("mapred.job.queue.name", "default") == name]
+        return _page(f"Queue {name}", _table(["acl", "value"], acls)
+                     + _table(["job", "name", "user", "state"], jobs))
+
+    def history_html(self, q):
+        import os
+        from .history import diagnose, history_dir, load_history, summarize_history
+        d = history_dir(self.jt.conf)
+        if q.get("logFile"):
+            path = os.path.join(d, os.path.basename(q["logFile"]))
+            job, attempts = load_history(path)
+            summ = summarize_history(path)
+            rules = diagnose(job, attempts)
+            return _page(f"Analysis of {os.path.basename(path)}",
+                         f"<pre>{html.escape(json.dumps(summ, indent=1, default=str))}</pre>"
+                         "<h2>Diagnosis</h2><ul>" + "".join(
+                             f"<li>{html.escape(str(r))}</li>" for r in rules) + "</ul>")
+        files = sorted(os.listdir(d)) if d and os.path.isdir(d) else []
+        rows = [[f"<a href='/jobhistory.jsp?logFile={f}'>{html.escape(f)}</a>"] for f in files
+                if f.endswith(".jsonl")]
+        return _page("Job History", _table(["history file"], rows))
 
     def index_html(self):
         c = self.cluster()
@@ -237,6 +378,81 @@ class WebUI:
             ev.append({"name": "thread_name", "ph": "M", "pid": 1, "tid": tid,
                        "args": {"name": track}})
         return {"traceEvents": ev, "displayTimeUnit": "ms"}
+
+
+class DFSWebUI(WebUI):
+    """NameNode web UI (webapps/hdfs): health, node lists, directory browser."""
+
+    def __init__(self, namenode, host="0.0.0.0", port=50070):
+        self.nn = namenode
+        super().__init__(None, host, port)
+
+    def route(self, path, q):
+        if path in ("/", "/dfshealth.jsp"):
+            return "text/html", self.health_html()
+        if path == "/dfsnodelist.jsp":
+            return "text/html", self.nodelist_html(q.get("whatNodes", "LIVE"))
+        if path in ("/browseDirectory.jsp", "/nn_browsedfscontent.jsp"):
+            return "text/html", self.browse_html(q)
+        if path == "/metrics":
+            return "text/plain; version=0.0.4", METRICS.prometheus_text()
+        raise KeyError(path)
+
+    def health_html(self):
+        nodes = self.nn.datanode_report()
+        cap = sum(d["capacity"] or 0 for d in nodes if d["alive"])
+        used = sum(d["used"] or 0 for d in nodes if d["alive"])
+        fsck = self.nn.fsck("/")
+        live = sum(1 for d in nodes if d["alive"])
+        rows = [["Configured Capacity", cap], ["DFS Used", used],
+                ["DFS Used%", f"{100 * used / cap:.2f}%" if cap else "-"],
+                ["Files", fsck["files"]], ["Blocks", fsck["blocks"]],
+                ["Missing blocks", fsck["missing_blocks"]],
+                ["Under-replicated blocks", fsck["under_replicated_blocks"]],
+                ["Safe mode", "ON" if self.nn.safemode("get") else "OFF"],
+                ["<a href='/dfsnodelist.jsp?whatNodes=LIVE'>Live Nodes</a>", live],
+                ["<a href='/dfsnodelist.jsp?whatNodes=DEAD'>Dead Nodes</a>", len(nodes) - live]]
+        return _page("NameNode", _table(["", ""], rows) +
+                     "<p><a href='/browseDirectory.jsp?dir=/'>Browse the filesystem</a></p>")
+
+    def nodelist_html(self, what):
+        alive = what.upper() == "LIVE"
+        rows = [[html.escape(d["id"]), html.escape(d["host"]), html.escape(d["rack"]),
+                 d["capacity"], d["used"], d["blocks"], d["decommission"] or "In Service"]
+                for d in self.nn.datanode_report() if bool(d["alive"]) == alive]
+        return _page(f"{what.capitalize()} Datanodes",
+                     _table(["node", "host", "rack", "capacity", "used", "blocks",
+                             "admin state"], rows))
+
+    def browse_html(self, q):
+        if q.get("filename"):
+            f = q["filename"]
+            locs = self.nn.get_block_locations(f, 0, 32768)
+            from ..dfs.datanode import resolve_datanode
+            data = b""
+            for b in locs:
+                if len(data) >= 32768:
+                    break
+                for dn in b["dns"]:
+                    try:
+                        data += resolve_datanode(self.nn, dn).read_block(b["block"], 0,
+                                                                          32768 - len(data))
+                        break
+                    except Exception:  # noqa: BLE001
+                        continue
+            return _page(f"File: {f}", "<pre>" + html.escape(data.decode("utf-8", "replace"))
+                         + "</pre>")
+        d = q.get("dir", "/")
+        rows = []
+        for e in self.nn.list_status(d):
+            name = html.escape(e["path"])
+            link = (f"<a href='/browseDirectory.jsp?dir={name}'>{name}/</a>" if e["is_dir"] else
+                    f"<a href='/browseDirectory.jsp?filename={name}'>{name}</a>")
+            rows.append([link, "dir" if e["is_dir"] else "file", e["length"],
+                         e.get("replication", 0), e.get("block_size", 0), _fmt_t(e["mtime"])])
+        return _page(f"Contents of directory {d}",
+                     _table(["name", "type", "size", "replication", "block size",
+                             "modification time"], rows))
 
 
 def maybe_start(jt, conf):
