@@ -14,6 +14,8 @@ jar/pipes/job/fs/version/... dispatch).
   hbmr distcp [-update|-overwrite|-delete|-i|-p|-m N] SRC... DST   (file:// / hdfs://)
   hbmr archive -archiveName NAME.har -p PARENT SRC... DEST        (read back as har://)
   hbmr rumen TRACE_OUT TOPOLOGY_OUT HISTORY...                     (job-history traces)
+  hbmr logalyzer [-archive -logs URLS] -archiveDir D [-analysis OUT -grep P -sort COLS]
+  hbmr distch [-i] PATH:OWNER:GROUP:PERM ...  |  hbmr failmon [--interval S] [--logs GLOB..]
   hbmr gridmix [-generate BYTES] [-jobtype LOADJOB|SLEEPJOB] [-policy REPLAY|STRESS|SERIAL] IOPATH TRACE
   hbmr test TestDFSIO|nnbench|mrbench|testbigmapoutput|threadedmapbench|sortvalidate ...
   hbmr node            start this process's TaskTracker (+ JobTracker on rank 0)
@@ -371,6 +373,9 @@ TOOLS = {  # src/tools + contrib commands of bin/hadoop
     "archive": "hbmr.tools.har:main",
     "rumen": "hbmr.tools.rumen:main",
     "gridmix": "hbmr.tools.gridmix:main",
+    "logalyzer": "hbmr.tools.logalyzer:main",
+    "distch": "hbmr.tools.distch:main",
+    "failmon": "hbmr.utils.failmon:main",
 }
 
 
