@@ -221,7 +221,53 @@ class TaskTracker:
             self._changed.add(aid)
         self._news.set()
 
+    def _run_debug_script(self, run: _Running, diag: str) -> str:
+        """Failed attempt + ``mapred.{map,reduce}.task.debug.script``: run the script
+        as ``script stdout stderr syslog jobconf [program]`` in the attempt's log dir,
+        keep its output as userlogs/<attempt>/debugout and return it for the
+        diagnostics (TaskTracker.TaskInProgress.runDebugScript in the reference;
+        Pipes jobs default to the gdb-style ``pipes-default-script`` when
+        ``hadoop.pipes.executable`` is set and ``mapred.*.task.debug.script`` is)."""
+        import shlex
+        import subprocess
+        js = run.job
+        if js is None or run.spec is None:
+            return ""
+        aid = run.spec.attempt_id
+        is_map = "_m_" in aid
+        script = js.conf.get("mapred.map.task.debug.script" if is_map
+                             else "mapred.reduce.task.debug.script")
+        if not script:
+            return ""
+        logd = os.path.join(self.local_dir, "userlogs", aid)
+        os.makedirs(logd, exist_ok=True)
+        files = [os.path.join(logd, n) for n in ("stdout", "stderr", "syslog")]
+        for f in files:
+            if not os.path.exists(f):
+                with open(f, "w") as fh:
+                    fh.write(diag if f.endswith("stderr") else "")
+        confp = os.path.join(logd, "job.xml")
+        with open(confp, "w") as fh:
+            js.conf.write_xml(fh)
+        args = shlex.split(script) + files + [confp]
+        prog = js.conf.get("hadoop.pipes.executable")
+        if prog:
+            args.append(prog)
+        try:
+            r = subprocess.run(args, cwd=logd, capture_output=True, text=True,
+                               timeout=js.conf.get_int("hbmr.task.debug.script.timeout.s", 60))
+            out = r.stdout + r.stderr
+        except (OSError, subprocess.TimeoutExpired) as e:
+            out = f"debug script failed: {e}"
+        with open(os.path.join(logd, "debugout"), "w") as fh:
+            fh.write(out)
+        return out
+
     def _finish(self, run: _Running, state, diag="", output=None, device_time=0.0, wake=True):
+        if state == P.FAILED:
+            dbg = self._run_debug_script(run, diag)
+            if dbg:
+                diag = f"{diag}\nDebug script output:\n{dbg[-4096:]}"
         st = run.status
         if TRACE.on:
             TRACE.instant("tt.finish", attempt=st.attempt_id, state=state,

@@ -208,3 +208,26 @@ def test_sampled_cpu_probe_profiles_without_straggling():
     assert took < 0.5                      # nobody waited for the 800 ms CPU map
     assert st.n == 1 and 0.7 < st.mean < 1.2   # 100 ms sample scaled by 8
     assert not cs2.get(JIP, "PROFILE_TASKS") and not cs2.get(JIP, "CPU_MAP_TASKS")
+
+
+def test_debug_script_runs_on_failed_attempts(tmp_path):
+    """mapred.map.task.debug.script (TestMiniMRMapRedDebugScript.java): the script
+    gets stdout/stderr/syslog/jobconf paths, its output lands in the diagnostics."""
+    inp, _ = _words(tmp_path, files=1)
+    script = tmp_path / "debug.sh"
+    script.write_text("#!/bin/sh\necho \"DEBUG-SCRIPT args=$#\"\nhead -c 200 \"$2\"\n"
+                      "grep -c mapred.job.name \"$4\"\n")
+    script.chmod(0o755)
+    conf = JobConf()
+    conf.set_float("hbmr.faultinject.probability", 1.0)
+    with LocalCluster(conf, num_trackers=1, cpu_slots=1) as cl:
+        job = wordcount.make_job(str(inp), str(tmp_path / "out"))
+        job.set_int("mapred.map.max.attempts", 1)
+        job.set("mapred.map.task.debug.script", str(script))
+        with pytest.raises(RuntimeError):
+            JobClient.runJob(job, cluster=cl, verbose=False)
+        logs = os.path.join(cl.local_dir, "tt0", "userlogs")
+        outs = [open(os.path.join(logs, a, "debugout")).read() for a in os.listdir(logs)
+                if os.path.exists(os.path.join(logs, a, "debugout"))]
+    assert outs and "DEBUG-SCRIPT args=4" in outs[0]
+    assert outs[0].rstrip().endswith("1")
