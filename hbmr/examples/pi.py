@@ -4,7 +4,12 @@
 Each map takes (offset, size), walks ``size`` points of the 2-D Halton sequence
 (bases 2 and 3) from index ``offset``, and counts points inside / outside the
 inscribed circle; one reducer sums the counts.  pi ≈ 4 · inside / total.
-The map's inner loop is vectorised over numpy (the reference's Java loop)."""
+The map's inner loop is vectorised over numpy (the reference's Java loop).
+
+:class:`PiSplitJob` is the GPU form: each map task is one launch of the fp64
+Halton kernel (native/kernels/pi.hip) on its GPU slot's stream — bit-exact with
+the numpy map, so CPU and GPU slots can share a job under the hybrid
+scheduler — and the reduce is a collective sum."""
 from __future__ import annotations
 
 import argparse
@@ -80,6 +85,68 @@ def estimate(maps, samples, conf=None, cluster=None, verbose=False):
                     counts[bool(k.get())] = v.get()
     inside, outside = counts.get(True, 0), counts.get(False, 0)
     return Decimal(4) * Decimal(inside) / Decimal(inside + outside)
+
+
+from ..gpu.splitjob import SplitJob, SplitSpec  # noqa: E402
+
+
+class PiSplitJob(SplitJob):
+    collective_reduce = True
+    needs_reduce = True
+
+    def configure(self, conf):
+        self.conf = conf
+        self.maps = conf.get_int("hbmr.pi.maps", 1)
+        self.samples = conf.get_long("hbmr.pi.samples", 1000)
+
+    def get_splits(self, conf, trackers):
+        out = []
+        for i in range(self.maps):
+            loc = [trackers[i * len(trackers) // self.maps]] if trackers else []
+            out.append(SplitSpec(i, f"pi:{i}:{self.samples}", "range",
+                                 {"offset": i * self.samples, "size": self.samples}, loc, 0))
+        return out
+
+    def load_split(self, spec, device):
+        return (spec.params["offset"], spec.params["size"])
+
+    def load_split_sample(self, spec, device, fraction):
+        return (spec.params["offset"], max(1, int(spec.params["size"] * fraction)))
+
+    def split_nbytes(self, data):
+        return 0
+
+    def map_gpu(self, ctx, data):
+        from ..ops import pi as P
+        return (P.count_inside_gpu(data[0], data[1], stream=getattr(ctx, "stream", None)),
+                data[1])
+
+    def map_cpu(self, ctx, data):
+        from ..ops import pi as P
+        return (P.count_inside_cpu(data[0], data[1]), data[1])
+
+    def combine(self, ctx, outputs):
+        import torch
+        inside = sum(int(o[0].item()) if hasattr(o[0], "item") else int(o[0]) for o in outputs)
+        return torch.tensor([inside, sum(o[1] for o in outputs)], dtype=torch.int64)
+
+    def reduce(self, ctx, combined):
+        t = combined
+        if ctx.device is not None and ctx.device.type == "cuda":
+            t = t.to(ctx.device)
+        ctx.comm.all_reduce(t)
+        inside, total = (int(x) for x in t.cpu().tolist())
+        return {"inside": inside, "total": total,
+                "pi": str(Decimal(4) * Decimal(inside) / Decimal(max(total, 1)))}
+
+
+def split_job_conf(maps, samples, base=None) -> JobConf:
+    job = JobConf(base)
+    job.set_job_name("PiEstimator (split job)")
+    job.set("hbmr.splitjob.class", "hbmr.examples.pi:PiSplitJob")
+    job.set_int("hbmr.pi.maps", maps)
+    job.set_long("hbmr.pi.samples", samples)
+    return job
 
 
 def main(argv=None, cluster=None):

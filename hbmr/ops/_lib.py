@@ -63,6 +63,8 @@ _SIGS = {
                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "hbmr_wc_pack": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p,
                              c_void_p]),
+    # PiEstimator (native/kernels/pi.hip)
+    "hbmr_pi_halton": (c_int, [ctypes.c_longlong, ctypes.c_longlong, c_void_p, c_void_p]),
     # GEMM (native/kernels/gemm.hip)
     "hbmr_gemm_bf16_tn": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_long, c_long,
                                   ctypes.c_float, c_int, c_void_p]),

@@ -92,3 +92,19 @@ def test_distch_permissions(tmp_path):
         distch.parse_op("hdfs://nn/x:::700")
     with pytest.raises(ValueError):
         distch.parse_op(f"{d}:::79")
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_gpu_parser_on_real_node():
+    """On the MI355X box: the amdgpu sysfs is read (skipped where the container
+    does not expose /sys/class/drm)."""
+    p = failmon.GPUParser()
+    if not p.cards():
+        pytest.skip("no amdgpu sysfs visible in this container")
+    recs = p.query()
+    assert recs and all(r["type"] == "GPU" for r in recs)
+    print([(r["properties"].get("card"), r["properties"].get("vram_total"),
+            r["logLevel"]) for r in recs])
