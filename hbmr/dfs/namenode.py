@@ -606,6 +606,8 @@ class NameNode:
             info["locs"].add(dn_id)
             info["len"] = max(info.get("len", 0), length)
             self.pending_repl.pop(block, None)
+            # a fresh good replica must not be hit by an older queued delete
+            self.invalidate.get(dn_id, set()).discard(block)
             mv = self.moves.get(block)
             if mv is not None and mv[1] == dn_id:   # balancer move landed: drop the source
                 self.moves.pop(block)
@@ -750,7 +752,8 @@ class NameNode:
                         continue
                     if self.pending_repl.get(b["id"], 0) > now:
                         continue
-                    targets = self.choose_targets(need, exclude=set(info["locs"]))
+                    doomed = {dn for dn, inv in self.invalidate.items() if b["id"] in inv}
+                    targets = self.choose_targets(need, exclude=set(info["locs"]) | doomed)
                     if not targets:
                         continue
                     src = random.choice(live)

@@ -530,7 +530,143 @@ static void* pingThread(void* arg) {
   return nullptr;
 }
 
+// ---------------------------------------------------------------------------
+// Text protocol (HadoopPipes.cc TextProtocol / TextUpwardProtocol): with neither
+// hadoop.pipes.command.port nor .file set, the child reads tab-separated text
+// commands on stdin ("mapItem\tK\tV", "runMap\tSPLIT\tR\tPIPED", ...) and writes
+// text replies on stdout ("output\tK\tV", "done", ...), for debugging a task
+// binary by hand.  Instead of a second protocol implementation the text is
+// translated to and from the binary stream by two bridge threads, so the task
+// context runs exactly the code path it runs under the parent.
+namespace {
+
+string unescapeText(const string& s) {
+  string o;
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '\\' && i + 1 < s.size()) {
+      const char c = s[++i];
+      o += c == 't' ? '\t' : c == 'n' ? '\n' : c;
+    } else {
+      o += s[i];
+    }
+  }
+  return o;
+}
+
+string escapeText(const string& s) {
+  string o;
+  for (char c : s) {
+    if (c == '\t') o += "\\t";
+    else if (c == '\n') o += "\\n";
+    else if (c == '\\') o += "\\\\";
+    else o += c;
+  }
+  return o;
+}
+
+struct BridgeFds { int text_in; int bin_out; int bin_in; FILE* text_out; };
+
+void* textDownThread(void* arg) {
+  BridgeFds* b = (BridgeFds*)arg;
+  FILE* in = fdopen(b->text_in, "r");
+  FILE* outf = fdopen(b->bin_out, "wb");
+  HadoopUtils::FileOutStream out;
+  out.open(outf);
+  serializeInt(AUTHENTICATION_REQ, out);   // no secret in text mode: auth is a no-op
+  serializeString("", out);
+  serializeString("", out);
+  char* line = nullptr;
+  size_t cap = 0;
+  ssize_t n;
+  while ((n = getline(&line, &cap, in)) > 0) {
+    string l(line, (size_t)n);
+    while (!l.empty() && (l.back() == '\n' || l.back() == '\r')) l.pop_back();
+    if (l.empty()) continue;
+    std::vector<string> f(1);
+    for (char ch : l) {   // keeps empty fields (an empty value is legal)
+      if (ch == '\t') f.emplace_back();
+      else f.back() += ch;
+    }
+    for (auto& x : f) x = unescapeText(x);
+    const string& c = f[0];
+    auto need = [&](size_t k) {
+      HADOOP_ASSERT(f.size() >= k, "Short text protocol command " + c);
+    };
+    if (c == "start") { need(2); serializeInt(START_MESSAGE, out); serializeInt(HadoopUtils::toInt(f[1]), out); }
+    else if (c == "setJobConf") {
+      serializeInt(SET_JOB_CONF, out);
+      serializeInt((int)f.size() - 1, out);
+      for (size_t i = 1; i < f.size(); ++i) serializeString(f[i], out);
+    } else if (c == "setInputTypes") { need(3); serializeInt(SET_INPUT_TYPES, out); serializeString(f[1], out); serializeString(f[2], out); }
+    else if (c == "runMap") { need(4); serializeInt(RUN_MAP, out); serializeString(f[1], out); serializeInt(HadoopUtils::toInt(f[2]), out); serializeInt(HadoopUtils::toInt(f[3]), out); }
+    else if (c == "mapItem") { need(3); serializeInt(MAP_ITEM, out); serializeString(f[1], out); serializeString(f[2], out); }
+    else if (c == "runReduce") { need(3); serializeInt(RUN_REDUCE, out); serializeInt(HadoopUtils::toInt(f[1]), out); serializeInt(HadoopUtils::toInt(f[2]), out); }
+    else if (c == "reduceKey") { need(2); serializeInt(REDUCE_KEY, out); serializeString(f[1], out); }
+    else if (c == "reduceValue") { need(2); serializeInt(REDUCE_VALUE, out); serializeString(f[1], out); }
+    else if (c == "close") { serializeInt(CLOSE, out); }
+    else if (c == "abort") { serializeInt(ABORT, out); }
+    else { std::cerr << "hbmr pipes: illegal text protocol command " << c << std::endl; }
+    out.flush();
+  }
+  free(line);
+  fclose(outf);
+  fclose(in);
+  return nullptr;
+}
+
+void* textUpThread(void* arg) {
+  BridgeFds* b = (BridgeFds*)arg;
+  FILE* inf = fdopen(b->bin_in, "rb");
+  HadoopUtils::FileInStream in;
+  in.open(inf);
+  FILE* o = b->text_out;
+  try {
+    for (;;) {
+      const int cmd = deserializeInt(in);
+      string k, v;
+      switch (cmd) {
+        case OUTPUT:
+          deserializeString(k, in); deserializeString(v, in);
+          fprintf(o, "output\t%s\t%s\n", escapeText(k).c_str(), escapeText(v).c_str());
+          break;
+        case PARTITIONED_OUTPUT: {
+          const int part = deserializeInt(in);
+          deserializeString(k, in); deserializeString(v, in);
+          fprintf(o, "partitionedOutput\t%d\t%s\t%s\n", part, escapeText(k).c_str(),
+                  escapeText(v).c_str());
+          break;
+        }
+        case STATUS: deserializeString(k, in); fprintf(o, "status\t%s\n", escapeText(k).c_str()); break;
+        case PROGRESS: fprintf(o, "progress\t%f\n", deserializeFloat(in)); break;
+        case DONE: fprintf(o, "done\n"); fflush(o); break;
+        case REGISTER_COUNTER: {
+          const int id = deserializeInt(in);
+          deserializeString(k, in); deserializeString(v, in);
+          fprintf(o, "registerCounter\t%d\t%s\t%s\n", id, escapeText(k).c_str(), escapeText(v).c_str());
+          break;
+        }
+        case INCREMENT_COUNTER: {
+          const int id = deserializeInt(in);
+          fprintf(o, "incrementCounter\t%d\t%lld\n", id, (long long)deserializeLong(in));
+          break;
+        }
+        case AUTHENTICATION_RESP: deserializeString(k, in); break;
+        default: fprintf(o, "unknown\t%d\n", cmd); break;
+      }
+    }
+  } catch (HadoopUtils::Error&) {
+    // end of the binary stream: the task closed its output
+  }
+  fflush(o);
+  fclose(inf);
+  return nullptr;
+}
+
+}  // namespace
+
 bool runTask(const Factory& factory) {
+  pthread_t textThreads[2];
+  bool textMode = false;
   try {
     FILE* in = nullptr;
     FILE* out = nullptr;
@@ -562,9 +698,16 @@ bool runTask(const Factory& factory) {
       const string outName = string(file) + ".out";
       out = fopen(outName.c_str(), "wb");
     } else {
-      std::cerr << "hbmr pipes: no hadoop.pipes.command.port / .file in the environment"
-                << std::endl;
-      return false;
+      // text protocol on stdin/stdout through the bridge threads
+      int down[2], up[2];
+      HADOOP_ASSERT(pipe(down) == 0 && pipe(up) == 0, "pipe() failed");
+      static BridgeFds fds;
+      fds = {dup(0), down[1], up[0], stdout};
+      in = fdopen(down[0], "rb");
+      out = fdopen(up[1], "wb");
+      pthread_create(&textThreads[0], nullptr, textDownThread, &fds);
+      pthread_create(&textThreads[1], nullptr, textUpThread, &fds);
+      textMode = true;
     }
     HadoopUtils::FileInStream inStream;
     inStream.open(in);
@@ -578,6 +721,10 @@ bool runTask(const Factory& factory) {
     outStream.flush();
     fclose(in);
     fclose(out);
+    if (textMode) {  // the up bridge drains and prints what is left; stdin may stay open
+      pthread_join(textThreads[1], nullptr);
+      pthread_detach(textThreads[0]);
+    }
     return true;
   } catch (HadoopUtils::Error& e) {
     std::cerr << "hbmr pipes error: " << e.getMessage() << std::endl;

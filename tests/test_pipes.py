@@ -121,3 +121,27 @@ def test_gpu_only_job_is_accepted_and_not_placed_on_cpu(tmp_path):
     submitter.setup_pipes_job(conf)   # the fork crashed here (B3)
     assert conf.get_boolean("hbmr.job.cpu.capable", True) is False
     assert conf.is_gpu_capable()
+
+
+def test_text_protocol_debug_mode():
+    """No command port/file in the environment: the C++ child speaks the text
+    protocol on stdin/stdout (HadoopPipes.cc TextProtocol), map and reduce."""
+    import subprocess
+    from pathlib import Path
+    exe = Path(__file__).resolve().parent.parent / "hbmr" / "bin" / "wordcount-simple"
+    env = {k: v for k, v in os.environ.items() if not k.startswith("hadoop.pipes.")}
+    m = subprocess.run([str(exe)], input="start\t0\nsetJobConf\tx\ty\nrunMap\ts\t1\t1\n"
+                       "mapItem\t0\ta b\\ta\nclose\n", capture_output=True, text=True,
+                       env=env, timeout=30)
+    assert m.returncode == 0, m.stderr
+    lines = m.stdout.splitlines()
+    assert lines[-1] == "done"
+    # one reduce → the in-child combiner folds the map output (escaped \t = a tab)
+    assert sorted(ln for ln in lines if ln.startswith("output")) == \
+        ["output\ta\t2", "output\tb\t1"]
+    r = subprocess.run([str(exe)], input="start\t0\nrunReduce\t0\t1\nreduceKey\ta\n"
+                       "reduceValue\t1\nreduceValue\t2\nreduceKey\tb\nreduceValue\t5\nclose\n",
+                       capture_output=True, text=True, env=env, timeout=30)
+    assert r.returncode == 0, r.stderr
+    assert [ln for ln in r.stdout.splitlines() if ln.startswith("output")] == \
+        ["output\ta\t3", "output\tb\t5"]
