@@ -153,8 +153,29 @@ def main(argv=None, cluster=None):
     ap = argparse.ArgumentParser(prog="hbmr pi")
     ap.add_argument("maps", type=int)
     ap.add_argument("samples", type=int)
+    ap.add_argument("-split", action="store_true",
+                    help="run as a split-level job (GPU slots when a GPU is present)")
     a = ap.parse_args(argv)
     print(f"Number of Maps  = {a.maps}\nSamples per Map = {a.samples}")
+    if a.split:
+        import torch
+        from ..mapred.cluster import LocalCluster
+        gpus = [[i for i in range(torch.cuda.device_count())]] if torch.cuda.is_available() \
+            else None
+        own = cluster is None
+        cl = cluster or LocalCluster(JobConf(), num_trackers=1, gpus=gpus)
+        try:
+            rj = cl.submit_job(split_job_conf(a.maps, a.samples))
+            rj.waitForCompletion()
+            if not rj.isSuccessful():
+                print(f"job failed: {rj.getFailureInfo()}")
+                return 1
+            pi = rj._impl.jip.result[0]["pi"]
+        finally:
+            if own:
+                cl.shutdown()
+        print(f"Estimated value of Pi is {pi}")
+        return 0
     pi = estimate(a.maps, a.samples, cluster=cluster, verbose=True)
     print(f"Estimated value of Pi is {pi}")
     return 0
