@@ -12,7 +12,17 @@ tasks per job.  Data: synthetic Gaussian mixture generated in HBM by the
 framework's own split loader; centroids initialised from the first k points.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
+  torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1, one rank per GPU)
+
+With ``--gpus N > 1`` and no torchrun environment, bench.py launches the N rank
+processes itself (same env contract as torchrun: RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT) before anything touches the
+GPU, forwards rank 0's JSON line and exits non-zero if any rank fails.
+
+``--simulate-ms T`` rehearses the same job on CPU: GPU slots are simulated
+(``hbmr.gpu.simulate``, T ms of device time per split, no split data) and the
+collectives run over gloo, so the control plane + reduce can be timed at
+world 1/2/4/8 without GPUs (profiles/scale_sim_cpu.json).
 
 Timing: W untimed iterations (the first one materialises the splits in HBM and
 profiles the CPU slot), then a barrier job (every tracker: RCCL barrier + device
@@ -46,18 +56,22 @@ def main():
     ap.add_argument("--cpu-slots", type=int, default=2)
     ap.add_argument("--gpu-slots", type=int, default=2, help="HIP streams (GPU map slots) per GPU")
     ap.add_argument("--queue-depth", type=int, default=64)
+    ap.add_argument("--simulate-ms", type=float, default=None,
+                    help="CPU rehearsal: simulated GPU slots with this device time per split")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args()
     logging.basicConfig(level=logging.INFO if a.verbose else logging.WARNING,
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if a.gpus > 1 and world == 1:
-        print("for --gpus > 1 launch with: python -m torch.distributed.run --nproc-per-node N "
-              "bench.py --gpus N", file=sys.stderr)
-        return 2
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(a.gpus)
 
     import torch
+    if a.simulate_ms is not None and world > 1:
+        # N rank processes share this host's cores: no intra-op thread pools
+        # spinning against each other (on a GPU node the ranks do no torch CPU work)
+        torch.set_num_threads(1)
 
     from hbmr.gpu.syncjob import sync_conf
     from hbmr.mapred.jobconf import JobConf
@@ -71,7 +85,12 @@ def main():
     conf.set_int("hbmr.gpu.queue.depth", a.queue_depth)
     conf.set_int("hbmr.heartbeat.interval.ms", 200)
     conf.set_int("mapred.task.timeout", 0)
-    node = Node(conf)
+    use_gpu = torch.cuda.is_available() and a.simulate_ms is None
+    if a.simulate_ms is not None:
+        conf.set("hbmr.gpu.simulate", "true")
+        conf.set("hbmr.gpu.simulate.nodata", "true")
+        conf.set("hbmr.gpu.simulate.task.ms", str(a.simulate_ms))
+    node = Node(conf, use_gpu=use_gpu)
     if not node.is_master:
         node.serve_until_shutdown()
         node.shutdown()
@@ -93,12 +112,14 @@ def main():
             drv.step()
         t_warm = time.time() - t_setup
         barrier()
-        torch.cuda.synchronize()
+        if use_gpu:
+            torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(a.steps):
             drv.step()
         barrier()
-        torch.cuda.synchronize()
+        if use_gpu:
+            torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         hist = drv.history[a.warmup:]
         n_maps = sum(h["counters"].get("org.apache.hadoop.mapred.JobInProgress$Counter",
@@ -131,7 +152,8 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic",
+            "data": "synthetic" if a.simulate_ms is None else
+                    f"simulated GPU slots ({a.simulate_ms} ms/split), CPU only",
             "config": {"model": "K-Means 100M pts x 128-d, k=1024 (hybrid CPU+GPU scheduling)"
                        if (a.points, a.dims, a.k) == (100_000_000, 128, 1024) else
                        f"K-Means {a.points} pts x {a.dims}-d, k={a.k}",
@@ -145,6 +167,7 @@ def main():
             "maps_launched": n_maps, "gpu_maps": gpu_maps, "cpu_maps": cpu_maps,
             "warmup_seconds": round(t_warm, 2),
             "final_shift": hist[-1].get("shift") if hist else None,
+            "maps_per_tracker_last_job": hist[-1].get("maps_per_tracker") if hist else None,
             # per job signature: completed-task mean seconds on each slot type and the
             # number of tasks behind it (the CPU probe may still be running)
             "cost_model": {k: {s: {"mean_s": round(v["mean"], 6), "n": v["n"],
@@ -157,6 +180,52 @@ def main():
     finally:
         node.shutdown()
     return 0
+
+
+def spawn_ranks(n):
+    """torchrun-equivalent launcher: N rank processes of this script on one node.
+    The parent never initialises HIP (it only spawns and waits)."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get(
+                       "HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env, start_new_session=True))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 1
+                    print(f"bench: rank {procs.index(p)} exited with {code}; stopping the others",
+                          file=sys.stderr)
+                    for q in live:
+                        try:
+                            os.killpg(q.pid, signal.SIGTERM)
+                        except ProcessLookupError:
+                            pass
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        for q in procs:
+            try:
+                os.killpg(q.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+        raise
+    return rc
 
 
 if __name__ == "__main__":

@@ -216,11 +216,11 @@ class GpuRuntime:
                     with r.job.lock:
                         r.job.map_outputs[r.spec.attempt_id] = out
                 self.devices[slot.device.index].device_errors = 0
-                for r in runs:
-                    r.task.reporter.incrCounter("hbmr.GpuCounters", "GPU_KERNEL_US", int(dt * 1e6))
-                    tracker._finish(r, P.SUCCEEDED, output={"tracker": tracker.name,
-                                                            "where": where},
-                                    device_time=dt, wake=False)
+                # one compact report for the batch (JobTracker._bulk_succeeded)
+                agg = _merge_counters(runs)
+                agg.incr("hbmr.GpuCounters", "GPU_KERNEL_US", int(dt * 1e6) * len(runs))
+                tracker.finish_bulk(runs, dt, {"tracker": tracker.name, "where": where},
+                                    agg.to_dict())
                 tracker.notify_jobtracker()
             except BaseException as e:  # noqa: BLE001
                 self._note_error(slot.device.index, e)
@@ -255,6 +255,15 @@ class GpuRuntime:
         except Exception as e:  # noqa: BLE001
             return f"device query failed: {e}"
         return None
+
+
+def _merge_counters(runs):
+    from ..mapred.counters import Counters
+    agg = Counters()
+    for r in runs:
+        if r.task is not None:
+            agg.incr_all(r.task.reporter.counters)
+    return agg
 
 
 class _Shim:

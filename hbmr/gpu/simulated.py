@@ -12,8 +12,13 @@ to fake trackers with ``availableGPUDevices`` set
 (src/test/org/apache/hadoop/mapred/TestJobQueueTaskScheduler.java:183-201).
 
 Keys:
-  hbmr.gpu.simulate.task.ms   simulated device time per map task (default 0)
+  hbmr.gpu.simulate.task.ms   simulated device time per map task (default 0); the
+                              device runs one task at a time whatever its slot count
   hbmr.gpu.simulate.hbm.gb    simulated HBM size per device (default 288)
+  hbmr.gpu.simulate.nodata    do not materialise splits and skip the map
+                              function (the job's ``map_sim`` hook, if any,
+                              still runs on a ``None`` split): control-plane
+                              and collective timing at full problem size
 """
 from __future__ import annotations
 
@@ -33,6 +38,9 @@ from ..utils.trace import TRACE
 log = logging.getLogger("hbmr.gpu.sim")
 
 
+_NO_DATA = ("simulated split",)   # cache placeholder of an unmaterialised split
+
+
 class _SimSlot:
     def __init__(self, index):
         self.index = index
@@ -49,6 +57,7 @@ class _SimDevice:
         self.thread = None
         self.total_mem = hbm
         self.name = "simulated-gfx950"
+        self.busy_until = 0.0     # the slots' streams share one device
 
 
 class SimulatedGpuRuntime:
@@ -59,6 +68,7 @@ class SimulatedGpuRuntime:
         self.devices = {d: _SimDevice(d, max(1, slots_per_device), hbm) for d in devices}
         self.task_s = conf.get_float("hbmr.gpu.simulate.task.ms", 0.0) / 1000.0
         self.max_batch = max(1, conf.get_int("hbmr.gpu.batch.max", 64))
+        self.nodata = conf.get_boolean("hbmr.gpu.simulate.nodata", False)
         self._stop = threading.Event()
         self._done: list = []          # heap of (ready_time, seq, item)
         self._done_cv = threading.Condition()
@@ -147,14 +157,21 @@ class SimulatedGpuRuntime:
                                            "GPU runner (hadoop.pipes.gpu.executable)")
                     tracker._maybe_inject_fault(r)
                     sspec = SplitSpec.from_dict(r.spec.split)
-                    data, hit = tracker.split_cache.get_or_load(
-                        sspec.key, dev.index, lambda s=sspec: sj.load_split(s, "cpu"),
-                        sj.split_nbytes)
+                    if self.nodata:
+                        data, hit = tracker.split_cache.get_or_load(
+                            sspec.key, dev.index, lambda: _NO_DATA, lambda _d, n=sspec.length: n)
+                        data = None
+                    else:
+                        data, hit = tracker.split_cache.get_or_load(
+                            sspec.key, dev.index, lambda s=sspec: sj.load_split(s, "cpu"),
+                            sj.split_nbytes)
                     rep.incrCounter("hbmr.GpuCounters",
                                     "GPU_SPLIT_CACHE_HITS" if hit else "GPU_SPLIT_CACHE_MISSES")
                     r.status.start_time = now
                     ctx = TaskContext(tracker, js, r.spec, rep, device="cpu")
-                    fn = getattr(sj, "map_sim", None) or sj.map_cpu
+                    fn = getattr(sj, "map_sim", None)
+                    if fn is None:
+                        fn = (lambda _c, _d: None) if self.nodata else sj.map_cpu
                     outs.append(fn(ctx, data))
                     live.append(r)
                 except BaseException as e:  # noqa: BLE001
@@ -162,9 +179,10 @@ class SimulatedGpuRuntime:
                                                  f"{traceback.format_exc()[-2000:]}")
             if not live:
                 continue
-            # in-order stream semantics: the batch starts when the slot is free
-            start = max(time.time(), slot.busy_until)
-            slot.busy_until = start + self.task_s * len(live)
+            # the slots are streams of ONE device: work on any slot queues behind
+            # the device's earlier work (task.ms is the device's time per task)
+            start = max(time.time(), dev.busy_until)
+            slot.busy_until = dev.busy_until = start + self.task_s * len(live)
             slot.inflight += len(live)
             if TRACE.on:
                 TRACE.instant("gpu.launch", n=len(live))
@@ -193,9 +211,14 @@ class SimulatedGpuRuntime:
             for r, out in zip(runs, outs):   # a batch may mix jobs
                 with r.job.lock:
                     r.job.map_outputs[r.spec.attempt_id] = out
-            for r in runs:
-                tracker._finish(r, P.SUCCEEDED, output={"tracker": tracker.name, "where": "simgpu"},
-                                device_time=self.task_s, wake=False)
+            finish_bulk = getattr(tracker, "finish_bulk", None)
+            if finish_bulk is not None:
+                finish_bulk(runs, self.task_s, {"tracker": tracker.name, "where": "simgpu"})
+            else:
+                for r in runs:
+                    tracker._finish(r, P.SUCCEEDED, output={"tracker": tracker.name,
+                                                            "where": "simgpu"},
+                                    device_time=self.task_s, wake=False)
             slot.inflight -= len(runs)
             tracker.notify_jobtracker()
 

@@ -61,6 +61,10 @@ class TrackerInfo:
         self.blacklisted = False
         self.jobs_seen: set[str] = set()
         self.wake = False
+        # long-poll doorbell: set by wakeup() (no JobTracker lock needed, so a
+        # tracker's completion thread never queues behind a heartbeat) and by
+        # _kick() when new work may exist for every tracker
+        self.bell = threading.Event()
         self.more = False    # the last assignment stopped at the per-heartbeat cap
         self.rack = DEFAULT_RACK
         self.kills: set[str] = set()   # attempts to kill on the next heartbeat
@@ -95,11 +99,16 @@ class Attempt:
         self.diagnostic = ""
         self.speculative = speculative
         self.device_time = 0.0
+        self._released = False
         self.profile_only = False   # a CPU profiling probe left running after its TIP won
         self.profile_fraction = 0.0  # >0: sampled probe, timed on this fraction of a split
 
 
 class TaskInProgress:
+    __slots__ = ("job", "tid", "split", "partition", "pinned_tracker", "attempts", "next_attempt",
+                 "failures", "failed_trackers", "successful", "commit_granted", "killed",
+                 "_aid_prefix", "__weakref__")
+
     def __init__(self, job, tid: TaskID, split=None, partition=0, pinned_tracker=None):
         self.job = job
         self.tid = tid
@@ -113,6 +122,7 @@ class TaskInProgress:
         self.successful: Attempt | None = None
         self.commit_granted: str | None = None
         self.killed = False
+        self._aid_prefix = "attempt" + str(tid)[4:] + "_"
 
     @property
     def is_map(self):
@@ -430,6 +440,9 @@ class JobTracker:
         self.listeners = []
         self.start_time = time.time()
         self.system_dir = conf.get("mapred.system.dir")
+        # job files exist for restart recovery only: without it a submit does
+        # no file-system work on the job's critical path
+        self.recover = conf.get_boolean("mapred.jobtracker.restart.recover", False)
         self.restart_count = 0
         self._to_recover: list[str] = []
         self._recover_trackers = 0
@@ -545,7 +558,7 @@ class JobTracker:
         return os.path.join(self.system_dir, str(jid)) if jid is not None else self.system_dir
 
     def _persist_job(self, jid, conf):
-        d = self._sysdir(jid)
+        d = self._sysdir(jid) if self.recover else None
         if d is None:
             return
         os.makedirs(d, exist_ok=True)
@@ -555,7 +568,7 @@ class JobTracker:
         os.replace(tmp, os.path.join(d, "job.json"))
 
     def _forget_job(self, jid):
-        d = self._sysdir(jid)
+        d = self._sysdir(jid) if self.recover else None
         if d is not None:
             shutil.rmtree(d, ignore_errors=True)
 
@@ -627,7 +640,7 @@ class JobTracker:
             self.job_queue.append(jip)
             if not jip.maps and not jip.reduces:
                 self._finish_job(jip, SUCCEEDED)
-            self.cv.notify_all()
+            self._kick()
         for cb in self.listeners:
             cb("submitted", jip)
         return RunningJob(jid, _JTJobHandle(jip), conf)
@@ -708,16 +721,20 @@ class JobTracker:
 
     # -- heartbeat ----------------------------------------------------------------------
     def wakeup(self, tracker_name: str):
-        """A tracker has news (a task finished): end its long-poll heartbeat now."""
-        with self.lock:
-            tr = self.trackers.get(tracker_name)
-            if tr is not None:
-                tr.wake = True
-            self.cv.notify_all()
+        """A tracker has news (a task finished): end its long-poll heartbeat now.
+        Lock-free: dict lookup + attribute store + Event.set."""
+        tr = self.trackers.get(tracker_name)
+        if tr is not None:
+            tr.wake = True
+            tr.bell.set()
+
+    def _kick(self):
+        """New work may be assignable: ring every long-polling tracker."""
+        for tr in list(self.trackers.values()):
+            tr.bell.set()
 
     def notify(self):
-        with self.lock:
-            self.cv.notify_all()
+        self._kick()
 
     def heartbeat(self, status: dict, initial: bool = False, accept_new_tasks: bool = True,
                   block: float = 0.0):
@@ -727,6 +744,12 @@ class JobTracker:
         ``block`` seconds) until new work exists or the tracker calls wakeup(),
         so idle trackers learn about new tasks immediately instead of on their
         next periodic heartbeat (the reference's 3 s floor, B13)."""
+        name = status["tracker_name"] if isinstance(status, dict) else status.tracker_name
+        tr0 = self.trackers.get(name)
+        if tr0 is not None:
+            # clear before this call's assignment: a ring from here on re-polls
+            tr0.bell.clear()
+            tr0.wake = False
         if TRACE.on:
             with TRACE.span("jt.heartbeat", block=block):
                 resp = self._heartbeat(status, initial, accept_new_tasks)
@@ -737,29 +760,30 @@ class JobTracker:
             return resp
         if resp["actions"] or block <= 0 or not accept_new_tasks:
             return resp
-        name = status["tracker_name"] if isinstance(status, dict) else status.tracker_name
         deadline = time.time() + block
-        with self.lock:
-            tr = self.trackers.get(name)
-            if tr is None:
-                return resp
-            tr.wake = False
-            while not resp["actions"]:
-                left = deadline - time.time()
-                if left <= 0 or tr.wake or self._stop.is_set():
-                    break
-                if getattr(self, "_shutdown_trackers", False):
-                    resp["actions"].append(P.shutdown_action())
-                    break
-                self.cv.wait(left)
-                if TRACE.on:
-                    TRACE.instant("jt.longpoll.wake", wake=tr.wake)
-                if tr.wake or self.trackers.get(name) is not tr:
-                    break
+        tr = self.trackers.get(name)
+        if tr is None:
+            return resp
+        while not resp["actions"]:
+            if tr.wake or self._stop.is_set():
+                break
+            left = deadline - time.time()
+            if left <= 0:
+                break
+            tr.bell.wait(left)
+            tr.bell.clear()
+            if TRACE.on:
+                TRACE.instant("jt.longpoll.wake", wake=tr.wake)
+            if tr.wake or self.trackers.get(name) is not tr:
+                break
+            if getattr(self, "_shutdown_trackers", False):
+                resp["actions"].append(P.shutdown_action())
+                break
+            with self.lock:
                 if tr.status.healthy and not tr.blacklisted:
                     resp["actions"] += self.scheduler.assign_tasks(tr)
-            tr.wake = False
-            resp["more"] = tr.more
+        tr.wake = False
+        resp["more"] = tr.more
         return resp
 
     def _heartbeat(self, status, initial, accept_new_tasks):
@@ -788,6 +812,10 @@ class JobTracker:
                 tr.cached.discard(tuple(k))
             for rep in st.task_reports:
                 self._update_task_status(tr, P.TaskStatus.from_dict(rep), actions)
+            for bulk in st.bulk_reports:
+                self._bulk_succeeded(tr, bulk)
+            if st.lost_outputs:
+                self._outputs_lost(tr, st.lost_outputs)
             if self._to_recover:
                 self._maybe_recover(now)
             tr.more = False
@@ -834,7 +862,7 @@ class JobTracker:
         self._update_progress(jip)
 
     def _release(self, a: Attempt):
-        if a.tip.is_map and not getattr(a, "_released", False):
+        if a.tip.is_map and not a._released:
             jip = a.tip.job
             if a.run_on_gpu:
                 jip.running_gpu = max(0, jip.running_gpu - 1)
@@ -921,7 +949,98 @@ class JobTracker:
             jip.t_maps_done = time.time()
         self._check_job_done(jip)
         if tip.is_map and jip.reduces and jip.maps_complete():
-            self.cv.notify_all()  # reduces became schedulable: wake long-polling trackers
+            self._kick()  # reduces became schedulable: wake long-polling trackers
+
+    def _bulk_succeeded(self, tr: TrackerInfo, rep: dict):
+        """A batch of GPU map attempts that completed together (one HIP event
+        pair): the lean path of _attempt_succeeded — per attempt only the TIP
+        bookkeeping; counters, cost model, history and metrics once per batch."""
+        aids = rep["attempts"]
+        dt = float(rep.get("device_time", 0.0))
+        fin = rep.get("finish_time") or time.time()
+        out = rep.get("output") or {}
+        index = self.attempt_index
+        done = []
+        odd = []
+        for aid in aids:
+            a = index.get(aid)
+            if a is None or a.state in P.TERMINAL:
+                continue
+            tip = a.tip
+            if a.profile_fraction or tip.successful is not None or tip.killed or \
+                    len(tip.attempts) > 1:
+                odd.append(a)        # speculative twins etc.: the general path
+                continue
+            a.progress = 1.0
+            a.finish = fin
+            a.output = out
+            a.device_time = dt
+            a.state = P.SUCCEEDED
+            done.append(a)
+        if done:
+            jip = done[0].tip.job
+            n = 0
+            for a in done:
+                tip = a.tip
+                jp = tip.job
+                if not a._released:
+                    a._released = True
+                    jp.running_gpu = max(0, jp.running_gpu - 1)
+                    tr.running.discard(a.aid)
+                    tr.running_gpu[a.device] = max(0, tr.running_gpu.get(a.device, 1) - 1)
+                tip.successful = a
+                jp.maps_done += 1
+                jp.finished_gpu_maps += 1
+                jp.completion_events.append({"map": str(tip.tid), "attempt": a.aid,
+                                             "tracker": a.tracker, "output": out, "gpu": True,
+                                             "device": a.device})
+                n += 1
+            self.cost_model.tasks_finished(jip.signature, [a.aid for a in done], True, dt)
+            if rep.get("counters"):
+                jip.pending_counters.append(rep["counters"])
+            self.history.log("TASKS_FINISHED", attempts=[a.aid for a in done], tracker=tr.name,
+                             gpu=True, device=done[0].device, finish=fin, device_time=dt)
+            METRICS.inc("hbmr_tasks_succeeded_total", n, help="successful task attempts",
+                        type="map", where="gpu")
+            jobs = {a.tip.job for a in done}
+            for jp in jobs:
+                self._update_progress(jp)
+                if jp.maps_complete():
+                    jp.t_maps_done = time.time()
+                self._check_job_done(jp)
+                if jp.reduces and jp.maps_complete():
+                    self._kick()
+        for a in odd:
+            self._update_task_status(tr, P.TaskStatus(
+                attempt_id=a.aid, is_map=True, state=P.SUCCEEDED, progress=1.0,
+                run_on_gpu=True, gpu_device_id=a.device, finish_time=fin, output=out,
+                device_time=dt), [])
+
+    def _outputs_lost(self, tr: TrackerInfo, aids):
+        """Map outputs held by a tracker's GPU worker are gone (the worker died):
+        re-execute those maps if their job still needs them (the per-attempt
+        analogue of lostTaskTracker's re-execution, JobInProgress.java:3140-3160)."""
+        for aid in aids:
+            a = self.attempt_index.get(aid)
+            if a is None:
+                continue
+            tip = a.tip
+            jip = tip.job
+            if jip.completed() or tip.successful is not a or not jip.reduces:
+                continue
+            if any(r.is_complete() for r in jip.reduces):
+                continue
+            tip.successful = None
+            a.state = P.KILLED
+            jip.maps_done -= 1
+            jip.t_maps_done = 0.0
+            if a.run_on_gpu:
+                jip.finished_gpu_maps -= 1
+            else:
+                jip.finished_cpu_maps -= 1
+            jip.add_pending(tip, front=True)
+            self.history.log("MAP_OUTPUT_LOST", attempt=aid, tracker=tr.name)
+        self._kick()
 
     def _attempt_failed(self, a: Attempt, diag, killed=False):
         tip = a.tip
@@ -1031,6 +1150,45 @@ class JobTracker:
                     type="map" if tip.is_map else "reduce", where="gpu" if on_gpu else "cpu")
         return P.launch_action(spec)
 
+    def launch_gpu_batch(self, tr: TrackerInfo, tips, device):
+        """One bulk LaunchTaskAction for GPU map attempts of one job on one device
+        (the per-task launch() costs ~50 µs of JobTracker time; this ~3 µs).
+        The tracker queues them on the device's slots as one batch."""
+        jip = tips[0].job
+        now = time.time()
+        tasks = []
+        aids = []
+        index = self.attempt_index
+        running = tr.running
+        for tip in tips:
+            aid = tip._aid_prefix + str(tip.next_attempt)
+            tip.next_attempt += 1
+            a = Attempt(aid, tip, tr.name, True, device)
+            a.start = now
+            tip.attempts[aid] = a
+            index[aid] = a
+            running.add(aid)
+            tasks.append([aid, tip.partition, tip.split])
+            aids.append(aid)
+        n = len(tips)
+        tr.running_gpu[device] = tr.running_gpu.get(device, 0) + n
+        jip.running_gpu += n
+        if not jip.t_first_map:
+            jip.t_first_map = now
+        self.cost_model.tasks_started(jip.signature, aids, True, now)
+        jip.counters.incr(C.JOB_GROUP, C.TOTAL_LAUNCHED_MAPS, n)
+        self.history.log("TASKS_LAUNCHED", attempts=aids, tracker=tr.name, gpu=True,
+                         device=device)
+        METRICS.inc("hbmr_tasks_launched_total", n, help="task attempts launched", type="map",
+                    where="gpu")
+        act = {"type": "launch_batch", "job_id": str(jip.job_id), "run_on_gpu": True,
+               "device": device, "num_maps": len(jip.maps), "num_reduces": len(jip.reduces),
+               "collective": jip.collective_reduce, "tasks": tasks}
+        if str(jip.job_id) not in tr.jobs_seen:
+            act["conf"] = jip.conf_dict
+            tr.jobs_seen.add(str(jip.job_id))
+        return act
+
     def reduce_inputs(self, jip: JobInProgress, tracker_name=None):
         """Map outputs a reduce needs: classic = every map's output location;
         collective = the committed map attempts that ran on ``tracker_name``."""
@@ -1100,12 +1258,12 @@ class JobTracker:
         """Tell every tracker to exit on its next heartbeat."""
         with self.lock:
             self._shutdown_trackers = True
-            self.cv.notify_all()
+            self._kick()
 
     def shutdown(self):
         self._stop.set()
         with self.lock:
-            self.cv.notify_all()
+            self._kick()
 
 
 def job_result(rj: RunningJob):

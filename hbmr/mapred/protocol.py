@@ -17,7 +17,7 @@ from __future__ import annotations
 
 from dataclasses import dataclass, field
 
-PROTOCOL_VERSION = 2
+PROTOCOL_VERSION = 3
 
 # task states (TaskStatus.State)
 UNASSIGNED = "UNASSIGNED"
@@ -86,6 +86,12 @@ class TaskTrackerStatus:
     rank: int = 0
     world_size: int = 1
     cpu_threads: int = 1
+    # GPU map attempts that completed as one batch (one HIP event pair):
+    # [{"attempts": [...], "device_time": s, "finish_time": t, "counters": {...},
+    #   "output": {...}}] — the compact form of len(attempts) SUCCEEDED reports
+    bulk_reports: list = field(default_factory=list)
+    # succeeded map attempts whose output was lost (their GPU worker died)
+    lost_outputs: list = field(default_factory=list)
 
     @property
     def max_gpu_map_slots(self):
@@ -128,6 +134,11 @@ class TaskSpec:
 # heartbeat response actions ---------------------------------------------------
 def launch_action(spec: TaskSpec):
     return {"type": "launch", "task": spec.to_dict()}
+
+
+# {"type": "launch_batch", "job_id", "run_on_gpu", "device", "num_maps",
+#  "num_reduces", "collective", "tasks": [[attempt_id, partition, split], ...],
+#  "conf"?} — built by JobTracker.launch_gpu_batch
 
 
 def kill_task_action(attempt_id: str):

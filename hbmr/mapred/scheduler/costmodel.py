@@ -83,6 +83,36 @@ class CostModel:
             if st.probe is None and st.n == 0:
                 st.probe = attempt
 
+    def tasks_started(self, sig, attempts, on_gpu, t):
+        with self._lock:
+            st = self._get(sig)["gpu" if on_gpu else "cpu"]
+            if st.probe is None and st.n == 0 and attempts:
+                st.probe = attempts[0]
+            run = st.running
+            for a in attempts:
+                run[a] = t
+
+    def tasks_finished(self, sig, attempts, on_gpu, dt_each):
+        """A batch of attempts that each took ``dt_each`` seconds (GPU tasks
+        completed by one event pair share its device time)."""
+        with self._lock:
+            st = self._get(sig)["gpu" if on_gpu else "cpu"]
+            pop = st.running.pop
+            for a in attempts:
+                pop(a, None)
+            if dt_each >= 0 and attempts:
+                # n EWMA steps with the same sample, in closed form
+                n = len(attempts)
+                if st.n == 0:
+                    st.ewma = dt_each
+                else:
+                    keep = (1 - self.alpha) ** n
+                    st.ewma = keep * st.ewma + (1 - keep) * dt_each
+                st.n += n
+                st.total += dt_each * n
+                st.min = min(st.min, dt_each)
+                st.max = max(st.max, dt_each)
+
     def task_finished(self, sig, attempt, on_gpu, start, finish, succeeded=True):
         with self._lock:
             st = self._get(sig)["gpu" if on_gpu else "cpu"]

@@ -65,7 +65,7 @@ class HybridTaskScheduler(TaskScheduler):
         # cap map launches per heartbeat response so a tracker can start the
         # first tasks while the rest are still being assigned (the response
         # says "more" and the tracker calls right back)
-        self.max_maps_per_hb = max(1, conf.get_int("hbmr.scheduler.max.maps.per.heartbeat", 16))
+        self.max_maps_per_hb = max(1, conf.get_int("hbmr.scheduler.max.maps.per.heartbeat", 256))
         self._skips: dict = {}
         self.decisions = 0
 
@@ -180,7 +180,9 @@ class HybridTaskScheduler(TaskScheduler):
             # ---- GPU maps
             if jip.gpu_capable:
                 glim = self.job_limit(jip, "gpu")
+                bulk = jip.split_job is not None   # split jobs: one bulk launch per device
                 for dev in sorted(gpu_free):
+                    batch = []
                     while gpu_free[dev] > 0 and jip.pending_maps and glim > 0:
                         if budget <= 0:
                             tr.more = True
@@ -200,11 +202,16 @@ class HybridTaskScheduler(TaskScheduler):
                         tip, level = got
                         if level < 3:
                             self._skips.pop(key, None)
-                        actions.append(jt.launch(tr, tip, on_gpu=True, device=dev))
+                        if bulk:
+                            batch.append(tip)
+                        else:
+                            actions.append(jt.launch(tr, tip, on_gpu=True, device=dev))
                         gpu_free[dev] -= 1
                         budget -= 1
                         glim -= 1
                         self.decisions += 1
+                    if batch:
+                        actions.append(jt.launch_gpu_batch(tr, batch, dev))
             if jip.speculative and jip.gpu_capable and not jip.pending_maps:
                 self._speculate(tr, jip, gpu_free, now, actions)
         return actions

@@ -89,14 +89,29 @@ class TaskContext:
         return self.comm.world_size
 
 
+class _Flag:
+    """Kill flag of a batched GPU attempt: nothing ever waits on it, so no
+    Event (whose Condition + Lock cost more than the rest of the launch)."""
+    __slots__ = ("v",)
+
+    def __init__(self):
+        self.v = False
+
+    def set(self):
+        self.v = True
+
+    def is_set(self):
+        return self.v
+
+
 class _Running:
     __slots__ = ("spec", "status", "task", "kill", "job")
 
-    def __init__(self, spec, status, job):
+    def __init__(self, spec, status, job, kill=None):
         self.spec = spec
         self.status = status
         self.task = None
-        self.kill = threading.Event()
+        self.kill = threading.Event() if kill is None else kill
         self.job = job
 
 
@@ -151,6 +166,8 @@ class TaskTracker:
         self.running: dict[str, _Running] = {}
         self._lock = threading.Lock()
         self._changed: set[str] = set()
+        self._bulk: list[dict] = []          # batched GPU completions not yet reported
+        self._lost: list[str] = []           # succeeded attempts whose output was lost
         self._news = threading.Event()
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
@@ -198,7 +215,10 @@ class TaskTracker:
                     reports.append(r.status.to_dict())
                     if r.status.state in P.TERMINAL:
                         self.running.pop(aid, None)
-        return P.TaskTrackerStatus(tracker_name=self.name, host=self.host,
+            bulk, self._bulk = self._bulk, []
+            lost, self._lost = self._lost, []
+        return P.TaskTrackerStatus(tracker_name=self.name, host=self.host, bulk_reports=bulk,
+                                   lost_outputs=lost,
                                    max_cpu_map_slots=self.cpu_slots,
                                    max_reduce_slots=self.reduce_slots, gpus=gpus,
                                    task_reports=reports, cached_splits_added=added,
@@ -286,6 +306,44 @@ class TaskTracker:
         if wake:
             self.notify_jobtracker()
 
+    def finish_bulk(self, runs, device_time, output, counters=None):
+        """A batch of GPU map attempts completed together: one compact report
+        (JobTracker._bulk_succeeded) instead of one status per attempt.
+        ``counters`` is the batch's merged counters dict (else each run's
+        reporter counters are merged here)."""
+        if not runs:
+            return
+        now = time.time()
+        if counters is None:
+            agg = C.Counters()
+            for r in runs:
+                if r.task is not None:
+                    agg.incr_all(r.task.reporter.counters)
+            counters = agg.to_dict()
+        aids = []
+        with self._lock:
+            for r in runs:
+                st = r.status
+                st.state = P.SUCCEEDED
+                st.finish_time = now
+                st.progress = 1.0
+                st.device_time = device_time
+                st.output = output
+                aids.append(st.attempt_id)
+                self.running.pop(st.attempt_id, None)
+            self._bulk.append({"attempts": aids, "device_time": device_time, "finish_time": now,
+                               "counters": counters, "output": output})
+        self.tasks_done += len(runs)
+        if TRACE.on:
+            TRACE.instant("tt.finish", n=len(runs), state=P.SUCCEEDED,
+                          where=(output or {}).get("where"))
+        self._news.set()
+
+    def outputs_lost(self, aids):
+        with self._lock:
+            self._lost.extend(aids)
+        self.notify_jobtracker()
+
     def notify_jobtracker(self):
         """Cut our long-polling heartbeat short so finished tasks are reported now."""
         self._news.set()
@@ -369,7 +427,9 @@ class TaskTracker:
     # -- actions -------------------------------------------------------------------------
     def _handle(self, act):
         typ = act["type"]
-        if typ == "launch":
+        if typ == "launch_batch":
+            self._launch_batch(act)
+        elif typ == "launch":
             self._launch(P.TaskSpec.from_dict(act["task"]))
         elif typ == "kill_task":
             with self._lock:
@@ -438,6 +498,36 @@ class TaskTracker:
             self.cpu_pool.submit(self._run_cpu_map, run)
         else:
             self.reduce_pool.submit(self._run_reduce, run)
+
+    def _launch_batch(self, act):
+        """Bulk LaunchTaskAction (JobTracker.launch_gpu_batch): GPU maps of one
+        split job on one device, handed to the device runtime as they are built."""
+        jid = act["job_id"]
+        js = self.jobs.get(jid)
+        if js is None:
+            js = self._job(P.TaskSpec(attempt_id="", job_id=jid, is_map=True, partition=0,
+                                      conf=act.get("conf")))
+        dev = act["device"]
+        nm, nr, coll = act["num_maps"], act["num_reduces"], act["collective"]
+        now = time.time()
+        runs = []
+        for aid, part, split in act["tasks"]:
+            spec = P.TaskSpec(aid, jid, True, part, True, dev, split, nm, nr, (), coll)
+            st = P.TaskStatus(aid, True, P.RUNNING, 0.0, True, dev, now)
+            runs.append(_Running(spec, st, js, _Flag()))
+        with self._lock:
+            for r in runs:
+                self.running[r.spec.attempt_id] = r
+        if js.split_job is None or self.gpu_runtime is None:
+            for r in runs:      # not a split job: the per-attempt GPU Pipes path
+                self.gpu_pipes_pool.submit(self._run_cpu_map, r)
+            return
+        submit_many = getattr(self.gpu_runtime, "submit_many", None)
+        if submit_many is not None:
+            submit_many(runs)
+        else:
+            for r in runs:
+                self.gpu_runtime.submit(r)
 
     def _maybe_inject_fault(self, run):
         if self.fault_p > 0 and self._rng.random() < self.fault_p:

@@ -187,21 +187,37 @@ class KMeansSplitJob(SplitJob):
             STORE.put_host(self.cin, decode_centroids(init))
 
     # -- splits -------------------------------------------------------------------
+    _split_memo: dict = {}
+
     def get_splits(self, conf, trackers):
         if self.input.startswith("synthetic:"):
-            _, n, seed = self.input.split(":")
-            n, seed = int(n), int(seed)
-            per = self.split_points
-            nsplits = max(1, math.ceil(n / per))
-            out = []
-            for i in range(nsplits):
-                a = i * per
-                m = min(per, n - a)
-                key = f"kmeans-syn:{seed}:{self.d}:{self.centers}:{a}:{m}"
-                loc = [trackers[i * len(trackers) // nsplits]] if trackers else []
-                out.append(SplitSpec(i, key, "synthetic",
-                                     {"seed": seed, "start": a, "n": m}, loc, m * self.d * 2))
+            # iteration jobs re-split the same input: reuse the split list
+            mk = (self.input, self.split_points, self.d, self.centers, tuple(trackers))
+            got = KMeansSplitJob._split_memo.get(mk)
+            if got is not None:
+                return got
+            if len(KMeansSplitJob._split_memo) > 16:
+                KMeansSplitJob._split_memo.clear()
+            out = KMeansSplitJob._split_memo[mk] = self._synthetic_splits(trackers)
             return out
+        return self._file_splits(conf, trackers)
+
+    def _synthetic_splits(self, trackers):
+        _, n, seed = self.input.split(":")
+        n, seed = int(n), int(seed)
+        per = self.split_points
+        nsplits = max(1, math.ceil(n / per))
+        out = []
+        for i in range(nsplits):
+            a = i * per
+            m = min(per, n - a)
+            key = f"kmeans-syn:{seed}:{self.d}:{self.centers}:{a}:{m}"
+            loc = [trackers[i * len(trackers) // nsplits]] if trackers else []
+            out.append(SplitSpec(i, key, "synthetic",
+                                 {"seed": seed, "start": a, "n": m}, loc, m * self.d * 2))
+        return out
+
+    def _file_splits(self, conf, trackers):
         from ..mapred.formats import FileInputFormat, SequenceFileInputFormat
         from ..mapred.jobconf import JobConf
         jc = JobConf(conf)
@@ -306,11 +322,21 @@ class KMeansSplitJob(SplitJob):
         ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, points.shape[0])
         return sums, counts
 
+    def map_sim(self, ctx, points):
+        """Simulated GPU slot (hbmr.gpu.simulate): no device, and with
+        ``hbmr.gpu.simulate.nodata`` no split either — contributes nothing to
+        the partials (the reduce still runs the full-size collective)."""
+        if points is None:
+            ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, 0)
+            return None
+        return self.map_cpu(ctx, points)
+
     # -- combine + reduce -------------------------------------------------------------------
     def combine(self, ctx, outputs):
         from ..ops import kmeans as km
         dev = ctx.device if ctx.device is not None else torch.device("cpu")
         dp = km.padded_dim(self.d) if dev.type == "cuda" else self.d
+        outputs = [o for o in outputs if o is not None]   # simulated no-data maps
         same = [(s, c) for s, c in outputs if s.device == dev and s.shape[1] == dp]
         other = [(s, c) for s, c in outputs if not (s.device == dev and s.shape[1] == dp)]
         if same:
@@ -327,10 +353,12 @@ class KMeansSplitJob(SplitJob):
 
     def reduce(self, ctx, combined):
         from ..ops import kmeans as km
+        from ..utils.trace import TRACE
         sums, counts = combined
         k, dp = sums.shape
         packed = torch.cat([sums.reshape(-1), counts])
-        ctx.comm.all_reduce(packed)        # exact: int64 over RCCL / gloo
+        with TRACE.span("kmeans.allreduce", nbytes=packed.numel() * 8):
+            ctx.comm.all_reduce(packed)        # exact: int64 over RCCL / gloo
         sums = packed[:k * dp].view(k, dp)
         counts = packed[k * dp:]
         if sums.device.type == "cuda":
@@ -448,6 +476,11 @@ class KMeansDriver:
         jip = getattr(rj._impl, "jip", None)
         if jip is not None:
             res["timeline"] = jip.timeline()
+            per = {}
+            for t in jip.maps:
+                if t.successful is not None:
+                    per[t.successful.tracker] = per.get(t.successful.tracker, 0) + 1
+            res["maps_per_tracker"] = per
         res.update(iteration=i, seconds=time.time() - t0, job=str(rj.getID()),
                    counters=rj.getCounters())
         self.history.append(res)
