@@ -158,23 +158,30 @@ class CostModel:
 
 
 def min_makespan_cpu_tasks(pending: int, cpu_slots: int, gpu_slots: int, t_cpu: float,
-                           t_gpu: float) -> int:
+                           t_gpu: float, gpu_backlog: int = 0) -> int:
     """Number of the ``pending`` tasks to give CPU slots so the makespan
-    max(ceil(x/C)·t_c, ceil((P-x)/G)·t_g) is minimal (Shirahata et al.'s
-    objective, made live).  Ties go to fewer CPU tasks."""
+    max(ceil(x/C)·t_c, ceil((B+P-x)/G)·t_g) is minimal (Shirahata et al.'s
+    objective, made live); B = tasks already queued on the GPUs (a deep GPU
+    queue is work the CPUs can shorten).  Ties go to fewer CPU tasks."""
     if pending <= 0:
         return 0
     if gpu_slots <= 0:
         return pending
     if cpu_slots <= 0 or t_cpu is None or t_gpu is None:
         return 0
-    best_x, best = 0, math.ceil(pending / gpu_slots) * t_gpu
+    b = max(0, gpu_backlog)
+    best_x, best = 0, math.ceil((pending + b) / gpu_slots) * t_gpu
     waves = math.ceil(pending / cpu_slots)
     for w in range(1, waves + 1):
         x = min(pending, w * cpu_slots)
-        cost = max(w * t_cpu, math.ceil((pending - x) / gpu_slots) * t_gpu)
-        if cost < best - 1e-12:
+        cost = max(w * t_cpu, math.ceil((pending + b - x) / gpu_slots) * t_gpu)
+        if cost < best * (1 - 1e-9):
             best, best_x = cost, x
+    if best_x:
+        # the optimum's CPU wave need not be full: the fewest CPU tasks that
+        # still let the GPUs finish the rest within ``best``
+        fit = math.floor(best / t_gpu * (1 + 1e-9)) * gpu_slots
+        best_x = min(best_x, max(1, pending + b - fit))
     return best_x
 
 

@@ -111,7 +111,8 @@ class HybridTaskScheduler(TaskScheduler):
             return 0
         if t_gpu is None:
             return 0 if running_cpu else min(1, pending)
-        x = min_makespan_cpu_tasks(pending + running_cpu, total_cpu, total_gpu, t_cpu, t_gpu)
+        x = min_makespan_cpu_tasks(pending + running_cpu, total_cpu, total_gpu, t_cpu, t_gpu,
+                                   gpu_backlog=jip.running_maps(on_gpu=True))
         return max(0, x - running_cpu)
 
     # -- main entry -----------------------------------------------------------------
@@ -161,6 +162,9 @@ class HybridTaskScheduler(TaskScheduler):
                                          profile_fraction=self.probe_fraction))
                 cpu_free -= 1
                 budget -= 1
+            reserve = 0     # pending maps the plan keeps for later CPU waves
+            if jip.pending_maps and self.policy == "hybrid" and total_gpu > 0:
+                reserve = self._cpu_allowed(jip, total_cpu, total_gpu, now)
             if cpu_free > 0 and jip.pending_maps:
                 allowed = min(self._cpu_allowed(jip, total_cpu, total_gpu, now),
                               self.job_limit(jip, "cpu"))
@@ -175,6 +179,7 @@ class HybridTaskScheduler(TaskScheduler):
                     actions.append(jt.launch(tr, tip, on_gpu=False))
                     cpu_free -= 1
                     allowed -= 1
+                    reserve -= 1
                     budget -= 1
                     self.decisions += 1
             # ---- GPU maps
@@ -183,7 +188,10 @@ class HybridTaskScheduler(TaskScheduler):
                 bulk = jip.split_job is not None   # split jobs: one bulk launch per device
                 for dev in sorted(gpu_free):
                     batch = []
-                    while gpu_free[dev] > 0 and jip.pending_maps and glim > 0:
+                    # the min-makespan plan's later CPU waves stay pending: a deep GPU
+                    # queue must not swallow them (they free the GPUs' tail)
+                    while gpu_free[dev] > 0 and len(jip.pending_maps) > max(0, reserve) and \
+                            glim > 0:
                         if budget <= 0:
                             tr.more = True
                             break

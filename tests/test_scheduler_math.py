@@ -1,0 +1,128 @@
+"""The scheduling maths of the GPU fork, tested the way the reference tested
+its scheduler (TestJobQueueTaskScheduler.java:283-340 drives assignTasks with
+fake trackers): the min-makespan split (JobQueueTaskScheduler.java:181-220,
+dead code in the fork, live here) against brute force, the optional-scheduling
+rule (:290-291), and whole simulated clusters where CPU slots are 10-20x
+slower than the GPU, so the hybrid policy must give them some work (x* > 0)."""
+import itertools
+import math
+import time
+
+import pytest
+
+from hbmr.examples.sleepjob import split_sleep_conf
+from hbmr.mapred.cluster import LocalCluster
+from hbmr.mapred.jobconf import JobConf
+from hbmr.mapred.scheduler.costmodel import (CostModel, makespan_estimates,
+                                             min_makespan_cpu_tasks)
+
+JIP = "org.apache.hadoop.mapred.JobInProgress$Counter"
+
+
+def _cost(x, p, c, g, tc, tg):
+    return max(math.ceil(x / c) * tc if x else 0.0, math.ceil((p - x) / g) * tg)
+
+
+@pytest.mark.parametrize("p,c,g", list(itertools.product([1, 2, 7, 16, 33, 128],
+                                                          [1, 2, 3, 8], [1, 2, 8])))
+def test_min_makespan_matches_brute_force(p, c, g):
+    for tc, tg in [(1.0, 1.0), (3.0, 1.0), (10.0, 1.0), (0.5, 1.0), (200.0, 1.0), (7.3, 0.9)]:
+        x = min_makespan_cpu_tasks(p, c, g, tc, tg)
+        assert 0 <= x <= p
+        costs = [_cost(y, p, c, g, tc, tg) for y in range(p + 1)]
+        best = min(costs)
+        assert _cost(x, p, c, g, tc, tg) <= best * (1 + 1e-9), (p, c, g, tc, tg, x)
+        # the fewest CPU tasks among the optima
+        assert x == min(y for y in range(p + 1) if costs[y] <= best * (1 + 1e-9)), (p, c, g, tc, tg)
+
+
+def test_min_makespan_counts_the_gpu_backlog():
+    # 6 pending, 30 already queued on the single GPU: the CPUs should take
+    # the pending ones rather than queue them behind 600 ms of GPU work
+    assert min_makespan_cpu_tasks(6, 4, 1, 0.2, 0.02) == 0
+    assert min_makespan_cpu_tasks(6, 4, 1, 0.2, 0.02, gpu_backlog=30) == 6
+    for p, b in itertools.product([1, 5, 17], [0, 3, 40]):
+        x = min_makespan_cpu_tasks(p, 3, 2, 0.1, 0.02, gpu_backlog=b)
+        costs = [max(math.ceil(y / 3) * 0.1 if y else 0.0, math.ceil((p + b - y) / 2) * 0.02)
+                 for y in range(p + 1)]
+        assert costs[x] <= min(costs) * (1 + 1e-9)
+
+
+def test_min_makespan_edge_cases():
+    assert min_makespan_cpu_tasks(0, 4, 1, 1.0, 1.0) == 0
+    assert min_makespan_cpu_tasks(10, 4, 0, 1.0, 1.0) == 10      # no GPUs: all on CPUs
+    assert min_makespan_cpu_tasks(10, 0, 1, 1.0, 1.0) == 0       # no CPUs
+    assert min_makespan_cpu_tasks(10, 4, 1, None, 1.0) == 0      # unprofiled CPU
+    # GPU 100x faster with few tasks: the CPUs get nothing (the fork's point)
+    assert min_makespan_cpu_tasks(64, 8, 8, 100.0, 1.0) == 0
+    # CPU only 2x slower and 4 CPUs vs 1 GPU: most work goes to CPUs
+    assert min_makespan_cpu_tasks(40, 4, 1, 2.0, 1.0) >= 20
+
+
+def test_makespan_estimates_are_consistent():
+    est = makespan_estimates(40, 4, 1, 20.0, 1.0)
+    assert est["optimal"] <= est["gpu_only"] and est["optimal"] <= est["cpu_only"]
+    assert est["optimal"] <= est["greedy"] + 1e-9
+    assert est["optimal_cpu_tasks"] == min_makespan_cpu_tasks(40, 4, 1, 20.0, 1.0)
+
+
+def test_cost_model_batch_updates_equal_single_updates():
+    a, b = CostModel(alpha=0.3), CostModel(alpha=0.3)
+    ids = [f"a{i}" for i in range(5)]
+    a.tasks_started("s", ids, True, 0.0)
+    a.tasks_finished("s", ids, True, 0.002)
+    for i in ids:
+        b.task_started("s", i, True, 0.0)
+        b.task_finished("s", i, True, 0.0, 0.002)
+    sa, sb = a.stats("s", True), b.stats("s", True)
+    assert sa.n == sb.n == 5 and not sa.running
+    assert sa.mean == pytest.approx(sb.mean) and sa.ewma == pytest.approx(sb.ewma)
+
+
+# ---------------------------------------------------------------- whole simulated clusters
+def _conf(policy, gpu_ms, depth=64, **kw):
+    conf = JobConf()
+    conf.set_boolean("hbmr.gpu.simulate", True)
+    conf.set("hbmr.scheduler.policy", policy)
+    conf.set_float("hbmr.gpu.simulate.task.ms", gpu_ms)
+    conf.set_int("hbmr.gpu.queue.depth", depth)
+    conf.set_int("mapred.tasktracker.map.gpu.tasks.maximum", 1)
+    conf.set_int("mapred.task.timeout", 0)
+    conf.set_int("hbmr.heartbeat.interval.ms", 20)
+    for k, v in kw.items():
+        conf.set(k, str(v))
+    return conf
+
+
+def run_policy(policy, maps, gpu_ms, cpu_ms, cpu_slots, jobs=2, cpu=True):
+    """Makespan (s) of the last of ``jobs`` identical split jobs (the first ones
+    profile the CPU) plus its CPU/GPU map counts."""
+    conf = _conf(policy, gpu_ms)
+    with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=cpu_slots) as cl:
+        for _ in range(jobs):
+            t0 = time.perf_counter()
+            rj = cl.submit_job(split_sleep_conf(maps, map_ms=cpu_ms, base=conf, cpu_capable=cpu))
+            rj.waitForCompletion(120)
+            dt = time.perf_counter() - t0
+            assert rj.isSuccessful(), rj.getFailureInfo()
+        cs = rj.getCounters()
+        return dt, cs.get(JIP, "CPU_MAP_TASKS"), cs.get(JIP, "GPU_MAP_TASKS")
+
+
+def test_hybrid_gives_cpu_slots_work_when_they_pay_and_beats_gpu_only():
+    # GPU 20 ms/task, CPU 200 ms/task (10x), 4 CPU slots, 40 maps:
+    # GPU-only 800 ms; optimum x*=10 -> max(3 waves*200, 30*20) = 600 ms
+    assert min_makespan_cpu_tasks(40, 4, 1, 0.2, 0.02) == 10
+    t_h, cpu_h, gpu_h = run_policy("hybrid", 40, 20.0, 200.0, 4)
+    t_g, cpu_g, _ = run_policy("hybrid", 40, 20.0, 200.0, 4, cpu=False)
+    assert cpu_g == 0
+    assert 4 <= cpu_h <= 14 and cpu_h + gpu_h == 40
+    assert t_h < t_g * 0.9, (t_h, t_g)
+
+
+def test_optional_rule_idles_cpus_only_when_gpus_can_drain_the_queue():
+    # accel = 200/20 = 10, one GPU slot: CPUs stay idle while pending < 10
+    t_small, cpu_small, _ = run_policy("optional", 8, 20.0, 200.0, 4)
+    assert cpu_small == 0
+    t_big, cpu_big, gpu_big = run_policy("optional", 40, 20.0, 200.0, 4)
+    assert cpu_big > 0 and cpu_big + gpu_big == 40
