@@ -58,6 +58,8 @@ def main():
     ap.add_argument("--queue-depth", type=int, default=64)
     ap.add_argument("--simulate-ms", type=float, default=None,
                     help="CPU rehearsal: simulated GPU slots with this device time per split")
+    ap.add_argument("--in-process", action="store_true",
+                    help="run the GPU slots inside the tracker process (no worker process)")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args()
     logging.basicConfig(level=logging.INFO if a.verbose else logging.WARNING,
@@ -85,12 +87,20 @@ def main():
     conf.set_int("hbmr.gpu.queue.depth", a.queue_depth)
     conf.set_int("hbmr.heartbeat.interval.ms", 200)
     conf.set_int("mapred.task.timeout", 0)
-    use_gpu = torch.cuda.is_available() and a.simulate_ms is None
+    # device_count() does not initialise HIP in this process: with the default
+    # per-rank GPU worker process (hbmr.gpu.worker.process) the device work and
+    # its synchronisation happen in the workers (the barrier job synchronises
+    # every worker's device), and this process never holds a HIP context
+    has_gpu = torch.cuda.device_count() > 0 and a.simulate_ms is None
+    in_process = a.in_process and has_gpu
+    conf.set_boolean("hbmr.gpu.worker.process", not in_process)
     if a.simulate_ms is not None:
+        if world > 1:
+            conf.set_int("hbmr.worker.torch.threads", 1)
         conf.set("hbmr.gpu.simulate", "true")
         conf.set("hbmr.gpu.simulate.nodata", "true")
         conf.set("hbmr.gpu.simulate.task.ms", str(a.simulate_ms))
-    node = Node(conf, use_gpu=use_gpu)
+    node = Node(conf, use_gpu=has_gpu)
     if not node.is_master:
         node.serve_until_shutdown()
         node.shutdown()
@@ -112,13 +122,13 @@ def main():
             drv.step()
         t_warm = time.time() - t_setup
         barrier()
-        if use_gpu:
+        if in_process:
             torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(a.steps):
             drv.step()
         barrier()
-        if use_gpu:
+        if in_process:
             torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         hist = drv.history[a.warmup:]
@@ -160,7 +170,8 @@ def main():
                        "global_batch": a.points, "seq_len": a.dims,
                        "parallelism": f"dp{world}", "k": a.k, "split_points": a.split_points,
                        "map_tasks_per_job": splits, "policy": a.policy,
-                       "cpu_slots_per_tracker": a.cpu_slots, "gpu_slots_per_gpu": a.gpu_slots},
+                       "cpu_slots_per_tracker": a.cpu_slots, "gpu_slots_per_gpu": a.gpu_slots,
+                       "gpu_worker_process": not in_process},
             "job_makespan_ms": round(ms, 3),
             "phases_ms": phases_ms,
             "points_per_sec": round(a.points * a.steps / dt, 1),

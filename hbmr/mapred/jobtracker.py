@@ -68,6 +68,7 @@ class TrackerInfo:
         self.more = False    # the last assignment stopped at the per-heartbeat cap
         self.rack = DEFAULT_RACK
         self.kills: set[str] = set()   # attempts to kill on the next heartbeat
+        self.extra_actions: list = []  # e.g. restart_gpu_worker, sent on the next heartbeat
 
     def gpu_devices(self):
         return [g["device"] for g in self.status.gpus]
@@ -443,6 +444,7 @@ class JobTracker:
         # job files exist for restart recovery only: without it a submit does
         # no file-system work on the job's critical path
         self.recover = conf.get_boolean("mapred.jobtracker.restart.recover", False)
+        self.worker_generation = 0     # GPU worker gang (communicator) generation
         self.restart_count = 0
         self._to_recover: list[str] = []
         self._recover_trackers = 0
@@ -780,6 +782,9 @@ class JobTracker:
                 resp["actions"].append(P.shutdown_action())
                 break
             with self.lock:
+                if tr.extra_actions:
+                    resp["actions"] += tr.extra_actions
+                    tr.extra_actions = []
                 if tr.status.healthy and not tr.blacklisted:
                     resp["actions"] += self.scheduler.assign_tasks(tr)
         tr.wake = False
@@ -832,6 +837,11 @@ class JobTracker:
             if tr.kills:
                 actions += [P.kill_task_action(aid) for aid in sorted(tr.kills)]
                 tr.kills.clear()
+            if st.gpu_worker_lost:
+                self._restart_gpu_gang(tr)
+            if tr.extra_actions:
+                actions += tr.extra_actions
+                tr.extra_actions = []
         return {"actions": actions, "interval": self.heartbeat_interval, "more": tr.more}
 
     def _update_task_status(self, tr: TrackerInfo, ts: P.TaskStatus, actions):
@@ -1016,6 +1026,53 @@ class JobTracker:
                 run_on_gpu=True, gpu_device_id=a.device, finish_time=fin, output=out,
                 device_time=dt), [])
 
+    def _restart_gpu_gang(self, origin: TrackerInfo):
+        """A GPU worker died while world > 1: its peers may be blocked in a
+        collective with it.  Every GPU tracker restarts its worker under a new
+        communicator generation (their held map outputs are reported lost and
+        re-executed)."""
+        self.worker_generation += 1
+        g = self.worker_generation
+        self.history.log("GPU_GANG_RESTART", origin=origin.name, generation=g)
+        log.warning("GPU worker of %s died: restarting every GPU worker (generation %d)",
+                    origin.name, g)
+        for t in self.trackers.values():
+            if t.status.gpus:
+                t.extra_actions.append(P.restart_gpu_worker_action(g))
+        self._kick()
+
+    def _restart_collective(self, jip: JobInProgress, diag):
+        """Re-run a split job's collective reduce gang: kill the running members,
+        forget finished ones and re-execute the maps (their outputs were consumed
+        by finished members or died with a worker)."""
+        self.history.log("COLLECTIVE_RESTART", job=str(jip.job_id), diag=diag[:500])
+        for r in jip.reduces:
+            for a in r.running_attempts():
+                a.state = P.KILLED
+                self._release(a)
+                t = self.trackers.get(a.tracker)
+                if t is not None:
+                    t.kills.add(a.aid)
+            if r.successful is not None:
+                r.successful = None
+                jip.reduces_done -= 1
+        jip.result = None
+        for tip in jip.maps:
+            a = tip.successful
+            if a is None:
+                continue
+            tip.successful = None
+            a.state = P.KILLED
+            jip.maps_done -= 1
+            if a.run_on_gpu:
+                jip.finished_gpu_maps -= 1
+            else:
+                jip.finished_cpu_maps -= 1
+            jip.add_pending(tip)
+        jip.t_maps_done = 0.0
+        self._update_progress(jip)
+        self._kick()
+
     def _outputs_lost(self, tr: TrackerInfo, aids):
         """Map outputs held by a tracker's GPU worker are gone (the worker died):
         re-execute those maps if their job still needs them (the per-attempt
@@ -1083,8 +1140,8 @@ class JobTracker:
             if tip.is_map:
                 jip.add_pending(tip, front=True)  # failed tasks first (findNewMapTask)
             elif jip.collective_reduce:
-                # a collective gang cannot restart one member: fail the job
-                self._finish_job(jip, FAILED, f"collective reduce {tip.tid} failed: {diag}")
+                # a collective gang cannot restart one member: the whole gang re-runs
+                self._restart_collective(jip, diag)
 
     def _update_progress(self, jip: JobInProgress):
         # O(1): completed fraction (the reference recomputed this from every TIP)

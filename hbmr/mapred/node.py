@@ -39,18 +39,29 @@ class Node:
         shared = os.environ.get("HBMR_SHARED_DEVICE")
         if shared is not None:
             self.local_rank = int(shared)
-            backend = backend or "gloo"
-        self.use_gpu = torch.cuda.is_available() if use_gpu is None else use_gpu
+        simulate = self.conf.get_boolean("hbmr.gpu.simulate", False)
+        # device_count() does not initialise HIP; is_available() would
+        self.use_gpu = (torch.cuda.device_count() > 0) if use_gpu is None else use_gpu
+        # default: device work in a per-rank GPU worker process, so this process
+        # (TaskTracker, and the JobTracker on rank 0) never holds a HIP context
+        self.worker_mode = self.conf.get_boolean("hbmr.gpu.worker.process",
+                                                 self.use_gpu or simulate)
+        if self.worker_mode:
+            self.conf.set("hbmr.gpu.worker.process", "true")
+        dev_backend = "gloo" if (shared is not None or not self.use_gpu) else "nccl"
         self.jt = None
         self.server = None
         self.dist = None
         self.comm = SoloComm()
-        if self.use_gpu:
+        worker_comm = None
+        if self.use_gpu and not self.worker_mode:
             torch.cuda.set_device(self.local_rank)
         if self.world > 1:
             import torch.distributed as dist
             self.dist = dist
-            be = backend or ("nccl" if self.use_gpu else "gloo")
+            # the rank processes only need host collectives when the device work
+            # lives in the workers (which form their own group, see below)
+            be = "gloo" if (self.worker_mode or not self.use_gpu) else (backend or dev_backend)
             kw = {}
             if be == "nccl":
                 kw["device_id"] = torch.device("cuda", self.local_rank)
@@ -58,6 +69,10 @@ class Node:
             cpu_group = dist.new_group(backend="gloo") if be != "gloo" else None
             self.comm = TorchComm(group=None, cpu_group=cpu_group)
             self.store = dist.distributed_c10d._get_default_store()
+            if self.worker_mode:
+                worker_comm = {"host": os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                               "port": int(os.environ["MASTER_PORT"]), "rank": self.rank,
+                               "world": self.world, "backend": backend or dev_backend}
         if self.rank == 0:
             self.jt = JobTracker(self.conf)
             if self.world > 1:
@@ -68,11 +83,11 @@ class Node:
         else:
             addr = self.store.get("hbmr/jobtracker").decode()
             jt_handle = JobTrackerProxy(addr, self.conf)
-        simulate = self.conf.get_boolean("hbmr.gpu.simulate", False)
         gpus = [self.local_rank] if (self.use_gpu or simulate) else []
         self.tt = TaskTracker(self.conf, jt_handle,
                               name=f"tracker_{socket.gethostname()}_r{self.rank}", rank=self.rank,
-                              world_size=self.world, gpu_devices=gpus, comm=self.comm)
+                              world_size=self.world, gpu_devices=gpus, comm=self.comm,
+                              worker_comm=worker_comm)
         self.tt.start()
         if self.jt is not None:
             if not self.jt.wait_for_trackers(self.world, timeout=300):

@@ -92,6 +92,9 @@ class TaskTrackerStatus:
     bulk_reports: list = field(default_factory=list)
     # succeeded map attempts whose output was lost (their GPU worker died)
     lost_outputs: list = field(default_factory=list)
+    # the tracker's GPU worker process died and its collective peers must be
+    # restarted with it (world > 1): the JobTracker answers restart_gpu_worker
+    gpu_worker_lost: bool = False
 
     @property
     def max_gpu_map_slots(self):
@@ -151,6 +154,10 @@ def kill_job_action(job_id: str):
 
 def commit_action(attempt_id: str):
     return {"type": "commit", "attempt_id": attempt_id}
+
+
+def restart_gpu_worker_action(generation: int):
+    return {"type": "restart_gpu_worker", "generation": generation}
 
 
 def reinit_action():

@@ -118,7 +118,7 @@ class _Running:
 class TaskTracker:
     def __init__(self, conf, jobtracker, name=None, rank=0, world_size=1, gpu_devices=(),
                  cpu_slots=None, reduce_slots=None, gpu_slots_per_device=None, comm=None,
-                 local_dir=None, host=None):
+                 local_dir=None, host=None, worker_comm=None):
         self.conf = conf
         self.jt = jobtracker
         # The launcher, completion and heartbeat threads hand work to each
@@ -168,6 +168,7 @@ class TaskTracker:
         self._changed: set[str] = set()
         self._bulk: list[dict] = []          # batched GPU completions not yet reported
         self._lost: list[str] = []           # succeeded attempts whose output was lost
+        self._worker_lost = False            # GPU worker died: the gang must restart
         self._news = threading.Event()
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
@@ -184,8 +185,13 @@ class TaskTracker:
             max(1, len(self.gpu_devices) * max(1, self.gpu_slots_per_device)),
             thread_name_prefix=f"{self.name}-gpupipes")
         self.gpu_runtime = None
+        self.worker_comm = worker_comm
         if self.gpu_devices:
-            if conf.get_boolean("hbmr.gpu.simulate", False):
+            if conf.get_boolean("hbmr.gpu.worker.process", False):
+                # device work in a persistent child process per tracker: a GPU
+                # fault fails attempts, not the tracker (hbmr/gpu/remote.py)
+                from ..gpu.remote import RemoteGpuRuntime as _Rt
+            elif conf.get_boolean("hbmr.gpu.simulate", False):
                 from ..gpu.simulated import SimulatedGpuRuntime as _Rt
             else:
                 from ..gpu.runtime import GpuRuntime as _Rt
@@ -217,8 +223,9 @@ class TaskTracker:
                         self.running.pop(aid, None)
             bulk, self._bulk = self._bulk, []
             lost, self._lost = self._lost, []
+            wlost, self._worker_lost = self._worker_lost, False
         return P.TaskTrackerStatus(tracker_name=self.name, host=self.host, bulk_reports=bulk,
-                                   lost_outputs=lost,
+                                   lost_outputs=lost, gpu_worker_lost=wlost,
                                    max_cpu_map_slots=self.cpu_slots,
                                    max_reduce_slots=self.reduce_slots, gpus=gpus,
                                    task_reports=reports, cached_splits_added=added,
@@ -339,9 +346,10 @@ class TaskTracker:
                           where=(output or {}).get("where"))
         self._news.set()
 
-    def outputs_lost(self, aids):
+    def outputs_lost(self, aids, worker_lost=False):
         with self._lock:
             self._lost.extend(aids)
+            self._worker_lost = self._worker_lost or worker_lost
         self.notify_jobtracker()
 
     def notify_jobtracker(self):
@@ -354,13 +362,13 @@ class TaskTracker:
 
     # -- lifecycle -----------------------------------------------------------------------
     def start(self):
+        if self.gpu_runtime is not None:
+            self.gpu_runtime.start()  # a GPU worker process must be up before the probe
         if self.health.enabled:
             self.health.check_now()   # before the first heartbeat advertises slots
         t = threading.Thread(target=self._hb_loop, name=f"{self.name}-hb", daemon=True)
         t.start()
         self._threads.append(t)
-        if self.gpu_runtime is not None:
-            self.gpu_runtime.start()
         return self
 
     def stop(self):
@@ -436,8 +444,13 @@ class TaskTracker:
                 r = self.running.get(act["attempt_id"])
             if r is not None:
                 r.kill.set()
-                if r.task is not None:
+                if r.task is not None and getattr(r.task, "kill_event", None) is not None:
                     r.task.kill_event.set()
+                if getattr(self.gpu_runtime, "remote", False):
+                    self.gpu_runtime.kill(act["attempt_id"])
+        elif typ == "restart_gpu_worker":
+            if getattr(self.gpu_runtime, "remote", False):
+                self.gpu_runtime.restart(act["generation"])
         elif typ == "commit":
             with self._lock:
                 r = self.running.get(act["attempt_id"])
@@ -462,6 +475,8 @@ class TaskTracker:
                     r.task.kill_event.set()
             self.jobs.clear()
             self.split_cache.readvertise()
+            if getattr(self.gpu_runtime, "remote", False):
+                self.gpu_runtime.readvertise()
             self._reinit = True
         elif typ == "shutdown":
             self._stop.set()
@@ -487,6 +502,7 @@ class TaskTracker:
         run = _Running(spec, st, js)
         with self._lock:
             self.running[spec.attempt_id] = run
+        remote = getattr(self.gpu_runtime, "remote", False) and js.split_job is not None
         if spec.is_map and spec.run_on_gpu:
             if js.split_job is None:
                 # classic job with a GPU Pipes executable: a child process per
@@ -494,6 +510,13 @@ class TaskTracker:
                 self.gpu_pipes_pool.submit(self._run_cpu_map, run)
             else:
                 self.gpu_runtime.submit(run)
+        elif remote:
+            # split-job CPU maps and reduces run where the job's map outputs
+            # live: in the GPU worker process
+            if spec.is_map:
+                self.gpu_runtime.submit_cpu(run)
+            else:
+                self.gpu_runtime.submit_reduce(run)
         elif spec.is_map:
             self.cpu_pool.submit(self._run_cpu_map, run)
         else:
@@ -543,29 +566,8 @@ class TaskTracker:
                 return
             self._maybe_inject_fault(run)
             if js.split_job is not None:
-                rep = TaskReporter()
-                run.task = _SplitTaskShim(rep)
-                ctx = TaskContext(self, js, spec, rep, device="cpu")
-                from ..gpu.splitjob import SplitSpec
-                sspec = SplitSpec.from_dict(spec.split)
-                if spec.profile_fraction:
-                    # sampled profiling probe: time the CPU map on a slice; the
-                    # output is dropped (the GPUs run the real task)
-                    sample = js.split_job.load_split_sample(sspec, "cpu", spec.profile_fraction)
-                    run.status.start_time = time.time()
-                    js.split_job.map_cpu(ctx, sample)
-                    run.task.reporter.counters = C.Counters()
-                    self._finish(run, P.SUCCEEDED, output={"tracker": self.name, "where": "cpu",
-                                                           "profile": True})
-                    return
-                data, hit = self.split_cache.get_or_load(
-                    sspec.key, "cpu", lambda: js.split_job.load_split(sspec, "cpu"),
-                    js.split_job.split_nbytes)
-                out = js.split_job.map_cpu(ctx, data)
-                with js.lock:
-                    js.map_outputs[spec.attempt_id] = out
-                rep.incrCounter(C.JOB_GROUP, C.CPU_MAP_TASKS, 0)
-                self._finish(run, P.SUCCEEDED, output={"tracker": self.name, "where": "cpu"})
+                from ..gpu.splitexec import run_split_cpu_map
+                run_split_cpu_map(self, run)
                 return
             if use_child_process(js.conf):
                 path = self._run_in_child(run, is_map=True)
@@ -594,32 +596,10 @@ class TaskTracker:
         try:
             self._maybe_inject_fault(run) if not spec.collective else None
             if js.split_job is not None:
-                rep = TaskReporter()
-                run.task = _SplitTaskShim(rep)
-                ctx = TaskContext(self, js, spec, rep)
-                with js.lock:
-                    outs = [js.map_outputs[a] for _tid, a, _o in spec.map_outputs
-                            if a in js.map_outputs]
-                missing = [a for _tid, a, _o in spec.map_outputs if a not in js.map_outputs]
-                if missing:
-                    raise RuntimeError(f"map outputs lost on {self.name}: {missing[:4]}")
+                from ..gpu.splitexec import run_split_reduce
                 dev = None if self.gpu_runtime is None else \
                     self.gpu_runtime.torch_device(self.gpu_devices[0])
-                if dev is not None and dev.type == "cuda":
-                    import torch
-                    ctx.device = dev
-                    with torch.cuda.device(ctx.device):
-                        combined = js.split_job.combine(ctx, outs)
-                        js.result = js.split_job.reduce(ctx, combined)
-                else:
-                    ctx.device = None
-                    combined = js.split_job.combine(ctx, outs)
-                    js.result = js.split_job.reduce(ctx, combined)
-                # map outputs are no longer needed
-                with js.lock:
-                    js.map_outputs.clear()
-                small = js.result if isinstance(js.result, dict) else None
-                self._finish(run, P.SUCCEEDED, output={"tracker": self.name, "result": small})
+                run_split_reduce(self, run, dev)
                 return
             if use_child_process(js.conf):
                 self._run_in_child(run, is_map=False)

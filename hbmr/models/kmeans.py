@@ -28,6 +28,7 @@ from __future__ import annotations
 import base64
 import logging
 import math
+import os
 import threading
 import time
 
@@ -47,6 +48,11 @@ CIN_KEY = "hbmr.kmeans.centroids.in"
 COUT_KEY = "hbmr.kmeans.centroids.out"
 INIT_KEY = "hbmr.kmeans.centroids.init"     # base64 fp32 [k, d] (first iteration only)
 NCENTERS_KEY = "hbmr.kmeans.synthetic.centers"
+RETURN_KEY = "hbmr.kmeans.return.centroids"   # reduce result carries the new centroids
+# rank 0's reduce also writes every centroid version here (in the background),
+# so a tracker whose GPU worker restarted can re-localise the input centroids of
+# the next iteration (the DistributedCache role; the fast path stays in memory)
+CDIR_KEY = "hbmr.kmeans.centroids.dir"
 
 # --------------------------------------------------------------------------- data
 _M32 = 0xFFFFFFFF
@@ -167,6 +173,42 @@ class CentroidStore:
 STORE = CentroidStore()
 
 
+def _centroid_file(cdir, key):
+    return os.path.join(cdir, key.replace("/", "_").replace(":", "_") + ".npy")
+
+
+def _save_centroids_async(cdir, key, prev, cen):
+    """Write centroid version ``key`` (and drop the one before ``prev``) off the
+    critical path: the device->host copy is queued on the current stream and the
+    file is written by a helper thread once it lands."""
+    host = torch.empty(cen.shape, dtype=torch.float32, pin_memory=cen.is_cuda)
+    host.copy_(cen, non_blocking=cen.is_cuda)
+    ev = None
+    if cen.is_cuda:
+        ev = torch.cuda.Event()
+        ev.record()
+
+    def _write():
+        if ev is not None:
+            ev.synchronize()
+        os.makedirs(cdir, exist_ok=True)
+        path = _centroid_file(cdir, key)
+        tmp = path + ".tmp.npy"
+        np.save(tmp, host.numpy())
+        os.replace(tmp, path)
+        old = _SAVED.setdefault(cdir, [])
+        old.append(path)
+        while len(old) > 3:
+            try:
+                os.remove(old.pop(0))
+            except OSError:
+                pass
+    threading.Thread(target=_write, daemon=True, name="kmeans-centroid-save").start()
+
+
+_SAVED: dict = {}
+
+
 # --------------------------------------------------------------------------- the job
 class KMeansSplitJob(SplitJob):
     collective_reduce = True
@@ -182,9 +224,14 @@ class KMeansSplitJob(SplitJob):
         self.cout = conf.get(COUT_KEY)
         self.centers = conf.get_int(NCENTERS_KEY, self.k)
         self.fx_shift = conf.get_int("hbmr.kmeans.fx.shift", 24)
+        self.cdir = conf.get(CDIR_KEY)
         init = conf.get(INIT_KEY)
         if init and self.cin and STORE.host_centroids(self.cin) is None:
             STORE.put_host(self.cin, decode_centroids(init))
+        if self.cin and self.cdir and STORE.host_centroids(self.cin) is None:
+            path = _centroid_file(self.cdir, self.cin)
+            if os.path.exists(path):
+                STORE.put_host(self.cin, torch.from_numpy(np.load(path)))
 
     # -- splits -------------------------------------------------------------------
     _split_memo: dict = {}
@@ -382,7 +429,16 @@ class KMeansSplitJob(SplitJob):
             shift = float((new_cen - old).norm(dim=1).max()) if self.k else 0.0
             STORE.put_host(self.cout, new_cen)
         self._write_output(ctx, counts, new_cen)
-        return {"shift": shift, "points": int(counts.sum().item()), "centroids_key": self.cout}
+        res = {"shift": shift, "points": int(counts.sum().item()), "centroids_key": self.cout}
+        if ctx.rank == 0 and self.cdir:
+            cen = new_cen if new_cen is not None else STORE.image(self.cout, sums.device).cen
+            _save_centroids_async(self.cdir, self.cout, self.cin, cen[:, :self.d])
+        if ctx.rank == 0 and self.conf.get_boolean(RETURN_KEY, False):
+            # the new centroids travel back with the result (the client may live
+            # in another process than the reduce, e.g. with GPU worker processes)
+            cen = new_cen if new_cen is not None else STORE.image(self.cout, sums.device).cen
+            res["centroids"] = encode_centroids(cen[:, :self.d])
+        return res
 
     def _write_output(self, ctx, counts, new_cen):
         out = self.conf.get("mapred.output.dir")
@@ -404,7 +460,8 @@ class KMeansSplitJob(SplitJob):
 
 
 # --------------------------------------------------------------------------- driver
-def make_iteration_conf(base, k, d, inp, split_points, cin, cout, init=None):
+def make_iteration_conf(base, k, d, inp, split_points, cin, cout, init=None,
+                        return_centroids=False):
     from ..mapred.jobconf import JobConf
     job = JobConf(base)
     job.set_job_name(f"kmeans {cin}->{cout}")
@@ -419,6 +476,8 @@ def make_iteration_conf(base, k, d, inp, split_points, cin, cout, init=None):
     job.set("hbmr.job.signature", f"kmeans|{inp}|{k}|{d}|{split_points}")
     if init is not None:
         job.set(INIT_KEY, encode_centroids(init))
+    if return_centroids:
+        job.set_boolean(RETURN_KEY, True)
     return job
 
 
@@ -448,7 +507,7 @@ class KMeansDriver:
     separate Hadoop jobs)."""
 
     def __init__(self, submit, result_of, conf=None, k=64, d=128, inp="synthetic:100000:1",
-                 split_points=500_000, run_id=None):
+                 split_points=500_000, run_id=None, return_centroids=None):
         self.submit = submit          # conf -> RunningJob
         self.result_of = result_of    # RunningJob -> reduce result dict
         self.base = conf
@@ -456,6 +515,11 @@ class KMeansDriver:
         self.run_id = run_id or f"km{int(time.time() * 1e3) & 0xFFFFFF:x}"
         self.iteration = 0
         self.history = []
+        # small models bring their centroids back with every result (cheap);
+        # the bench-sized one (k*d = 128K floats) only when asked
+        self.return_centroids = (k * d <= 65536) if return_centroids is None else return_centroids
+        base_dir = (conf.get("mapred.local.dir") if conf is not None else None) or "/tmp/hbmr-local"
+        self.centroid_dir = os.path.join(base_dir, "kmeans-centroids", self.run_id)
 
     def key(self, i):
         return f"{self.run_id}:{i}"
@@ -466,7 +530,9 @@ class KMeansDriver:
         if init is not None:
             STORE.put_host(self.key(0), init)
         job = make_iteration_conf(self.base, self.k, self.d, self.inp, self.split_points,
-                                  self.key(i), self.key(i + 1), init=init)
+                                  self.key(i), self.key(i + 1), init=init,
+                                  return_centroids=self.return_centroids)
+        job.set(CDIR_KEY, self.centroid_dir)
         t0 = time.time()
         rj = self.submit(job)
         rj.waitForCompletion()
@@ -495,7 +561,11 @@ class KMeansDriver:
         return self.centroids()
 
     def centroids(self):
-        return STORE.host_centroids(self.key(self.iteration))
+        c = STORE.host_centroids(self.key(self.iteration))
+        if c is None and self.history and self.history[-1].get("centroids"):
+            c = decode_centroids(self.history[-1]["centroids"])
+            STORE.put_host(self.key(self.iteration), c)
+        return c
 
 
 def main(argv=None, cluster=None):
