@@ -21,6 +21,7 @@ from __future__ import annotations
 import itertools
 import json
 import logging
+import math
 import os
 import shutil
 import threading
@@ -202,6 +203,10 @@ class JobInProgress:
         self.max_reduce_attempts = conf.get_max_reduce_attempts()
         self.result = None
         self.conf_dict = conf.to_dict()
+        from .child import use_child_process
+        self.reduce_in_child = use_child_process(conf)
+        self.slowstart = conf.get_float("mapred.reduce.slowstart.completed.maps", 0.05)
+        self.slowstart_maps = 0
 
     @staticmethod
     def _signature(conf):
@@ -253,6 +258,7 @@ class JobInProgress:
             for r in range(conf.get_num_reduce_tasks()):
                 self.reduces.append(TaskInProgress(self, TaskID(self.job_id, False, r),
                                                    partition=r))
+        self.slowstart_maps = math.ceil(min(1.0, max(0.0, self.slowstart)) * len(self.maps))
         self.status.state = RUNNING
         self.launch_time = time.time()
         self.jt.history.log("JOB_INITED", job=str(self.job_id), maps=len(self.maps),
@@ -958,7 +964,8 @@ class JobTracker:
         if tip.is_map and jip.maps_complete():
             jip.t_maps_done = time.time()
         self._check_job_done(jip)
-        if tip.is_map and jip.reduces and jip.maps_complete():
+        if tip.is_map and jip.reduces and (jip.maps_complete() or
+                                           jip.maps_done == jip.slowstart_maps):
             self._kick()  # reduces became schedulable: wake long-polling trackers
 
     def _bulk_succeeded(self, tr: TrackerInfo, rep: dict):
@@ -1254,6 +1261,18 @@ class JobTracker:
                     if t.successful is not None and t.successful.tracker == tracker_name]
         return [[str(t.tid), t.successful.aid, t.successful.output] for t in jip.maps
                 if t.successful is not None]
+
+    def map_completion_events(self, job_id, start=0):
+        """TaskUmbilicalProtocol.getMapCompletionEvents (TaskUmbilicalProtocol.java:
+        167): successful map outputs from index ``start`` on, for reduces that
+        started before every map finished (slow-start)."""
+        with self.lock:
+            jip = self.jobs.get(str(job_id))
+            if jip is None:
+                return {"events": [], "num_maps": 0, "state": "UNKNOWN"}
+            evs = jip.completion_events[start:]
+            return {"events": [[e["map"], e["attempt"], e["output"]] for e in evs],
+                    "num_maps": len(jip.maps), "state": jip.status.state}
 
     # -- RPC-facing job submission protocol (JobSubmissionProtocol) -------------------------
     def rpc_submit_job(self, conf_dict):

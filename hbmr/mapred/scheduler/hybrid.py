@@ -134,7 +134,7 @@ class HybridTaskScheduler(TaskScheduler):
             if jip.completed():
                 continue
             # ---- reduces
-            if jip.reduces and jip.maps_complete():
+            if jip.reduces and self._reduces_may_start(jip):
                 n_red = 0
                 for tip in jip.reduces:
                     if tip.is_complete() or tip.is_running():
@@ -162,8 +162,10 @@ class HybridTaskScheduler(TaskScheduler):
                                          profile_fraction=self.probe_fraction))
                 cpu_free -= 1
                 budget -= 1
-            reserve = 0     # pending maps the plan keeps for later CPU waves
-            if jip.pending_maps and self.policy == "hybrid" and total_gpu > 0:
+            reserve = 0     # pending maps the min-makespan plan keeps for later CPU waves
+            if jip.pending_maps and self.policy == "hybrid" and total_gpu > 0 and \
+                    total_cpu > 0 and jip.cpu_capable and \
+                    self.jt.cost_model.stats(jip.signature, False).n > 0:
                 reserve = self._cpu_allowed(jip, total_cpu, total_gpu, now)
             if cpu_free > 0 and jip.pending_maps:
                 allowed = min(self._cpu_allowed(jip, total_cpu, total_gpu, now),
@@ -223,6 +225,18 @@ class HybridTaskScheduler(TaskScheduler):
             if jip.speculative and jip.gpu_capable and not jip.pending_maps:
                 self._speculate(tr, jip, gpu_free, now, actions)
         return actions
+
+    def _reduces_may_start(self, jip) -> bool:
+        """Reduce slow-start (JobInProgress.java:879-881): classic reduces launch
+        once ``mapred.reduce.slowstart.completed.maps`` of the maps are done and
+        copy the rest as they complete (map ∥ shuffle); a collective reduce gang
+        needs every map, as do reduces in child processes (their inputs are fixed
+        at launch)."""
+        if jip.maps_complete():
+            return True
+        if jip.collective_reduce or jip.split_job is not None or jip.reduce_in_child:
+            return False
+        return jip.maps_done >= jip.slowstart_maps
 
     def _speculate(self, tr, jip, gpu_free, now, actions):
         """Back up stragglers on fully idle GPUs (JobInProgress.java:2312's

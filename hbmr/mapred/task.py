@@ -225,8 +225,8 @@ class MapOutputBuffer(OutputCollector):
         self.sort_key = job.get_output_key_comparator()
         self.partitioner = new_instance(job.get_partitioner_class(), job)
         self.combiner_cls = job.get_combiner_class()
-        sort_mb = job.get_int("io.sort.mb", 100)
-        self.soft_limit = int(sort_mb * (1 << 20) * job.get_float("io.sort.spill.percent", 0.8))
+        sort_bytes = job.get_int("hbmr.io.sort.bytes", job.get_int("io.sort.mb", 100) << 20)
+        self.soft_limit = int(sort_bytes * job.get_float("io.sort.spill.percent", 0.8))
         self.factor = max(2, job.get_int("io.sort.factor", 10))
         self.min_spills_for_combine = job.get_int("min.num.spills.for.combine", 3)
         self.codec = get_codec(job.get("mapred.map.output.compression.codec",
@@ -248,6 +248,12 @@ class MapOutputBuffer(OutputCollector):
         self.spills: list[tuple[str, SpillRecord]] = []
         self.n_out = 0
         self.bytes_out = 0
+        # SpillThread (MapTask.java:913-915, 1346): a full buffer is sorted and
+        # spilled in the background while map() keeps collecting into a fresh
+        # one; collect blocks only if that one fills while a spill is running
+        self.spill_async = job.get_boolean("hbmr.map.spill.async", True)
+        self._spill_thread = None
+        self._spill_error = None
 
     def collect(self, key, value):
         if not isinstance(key, self.kcls):
@@ -276,7 +282,7 @@ class MapOutputBuffer(OutputCollector):
         self.n_out += 1
         self.bytes_out += len(kb) + len(vb)
         if self.buf_bytes >= self.soft_limit:
-            self.sort_and_spill()
+            self._spill_full()
 
     def _collect_native(self, key, value):
         """collect() when partitioning is batched in C++: serialise and append."""
@@ -296,24 +302,60 @@ class MapOutputBuffer(OutputCollector):
         self.bytes_out += n
         self.buf_bytes += n + 16   # 16 B accounting per record (MapTask.java:890-903)
         if self.buf_bytes >= self.soft_limit:
-            self.sort_and_spill()
+            self._spill_full()
 
-    def _sorted_partitions(self):
-        self.buf.sort(key=lambda r: (r[0], r[1]))
-        parts = [[] for _ in range(self.R)]
-        for p, sk, kb, vb in self.buf:
+    def _spill_full(self):
+        """The buffer passed io.sort.spill.percent: hand it to the spill thread."""
+        if not self.spill_async:
+            self.sort_and_spill()
+            return
+        self._wait_spill()
+        taken = (self.keys, self.vals, self.parts, self.buf)
+        self.keys, self.vals, self.parts, self.buf = [], [], [], []
+        self.buf_bytes = 0
+
+        def run():
+            try:
+                self._spill(*taken)
+            except BaseException as e:  # noqa: BLE001
+                self._spill_error = e
+        self._spill_thread = threading.Thread(target=run, daemon=True,
+                                              name=f"SpillThread-{self.task.attempt_id}")
+        self._spill_thread.start()
+        self.reporter.incrCounter("hbmr.MapSpillCounters", "BACKGROUND_SPILLS", 1)
+
+    def _wait_spill(self):
+        t = self._spill_thread
+        if t is not None:
+            t.join()
+            self._spill_thread = None
+        if self._spill_error is not None:
+            e, self._spill_error = self._spill_error, None
+            raise e
+
+    @staticmethod
+    def _sorted_partitions(buf, R):
+        buf.sort(key=lambda r: (r[0], r[1]))
+        parts = [[] for _ in range(R)]
+        for p, sk, kb, vb in buf:
             parts[p].append((sk, kb, vb))
         return parts
 
     def sort_and_spill(self):
+        """Spill the current buffer now (in the caller's thread)."""
+        self._wait_spill()
+        taken = (self.keys, self.vals, self.parts, self.buf)
+        self.keys, self.vals, self.parts, self.buf = [], [], [], []
+        self.buf_bytes = 0
+        self._spill(*taken)
+
+    def _spill(self, keys, vals, parts_l, buf):
         if self.kind is not None:
-            return self._sort_and_spill_native()
-        if not self.buf and self.spills:
+            return self._sort_and_spill_native(keys, vals, parts_l)
+        if not buf and self.spills:
             return
         self.task.check_killed()
-        parts = self._sorted_partitions()
-        self.buf = []
-        self.buf_bytes = 0
+        parts = self._sorted_partitions(buf, self.R)
         idx = len(self.spills)
         path = os.path.join(self.out_dir, f"spill{idx}.out")
         rec = SpillRecord(self.R)
@@ -355,17 +397,15 @@ class MapOutputBuffer(OutputCollector):
         operm = ob.sort(self.kind, np.zeros(ob.n, np.int32))
         return ob.ifile_body(operm, 0, ob.n), ob.n
 
-    def _sort_and_spill_native(self):
-        if not self.keys and self.spills:
+    def _sort_and_spill_native(self, keys, vals, parts_l):
+        if not keys and self.spills:
             return
         self.task.check_killed()
-        b = sortbuf.Batch.from_lists(self.keys, self.vals)
+        b = sortbuf.Batch.from_lists(keys, vals)
         if self.native_hash:
             self.n_out += b.n
         part = b.hash_partition(self.kind, self.R) if self.native_hash else \
-            np.asarray(self.parts, dtype=np.int32)
-        self.keys, self.vals, self.parts = [], [], []
-        self.buf_bytes = 0
+            np.asarray(parts_l, dtype=np.int32)
         perm = b.sort(self.kind, part)
         starts = np.zeros(self.R + 1, np.int64)
         np.cumsum(np.bincount(part, minlength=self.R), out=starts[1:])
@@ -418,7 +458,7 @@ class MapOutputBuffer(OutputCollector):
 
     def flush(self):
         """Final spill + merge into file.out / file.out.index."""
-        self.sort_and_spill()
+        self.sort_and_spill()      # waits for a running background spill first
         final = os.path.join(self.out_dir, "file.out")
         if len(self.spills) == 1:
             path, rec = self.spills[0]
@@ -601,6 +641,44 @@ class ReduceTask(Task):
     def add_map_output(self, loc: MapOutputLocation):
         self.locations.append(loc)
 
+    #: reduce slow-start: callable(start) -> {"events": [[map tid, attempt, output]],
+    #: "num_maps": M, "state": job state} polled for map completions that happen
+    #: after the reduce started (GetMapEventsThread, ReduceTask.java:2793)
+    event_source = None
+
+    def _map_outputs(self):
+        """Yield every map's output location once: the ones known at launch, then
+        new completion events until all ``num_maps`` maps have been seen."""
+        seen = set()
+        for loc in self.locations:
+            seen.add(loc.map_attempt)
+            yield loc
+        if self.event_source is None:
+            return
+        got_maps = set()
+        start = 0
+        delay = 0.001
+        while len(seen) < self.num_maps:
+            self.check_killed()
+            r = self.event_source(start)
+            evs = r.get("events") or []
+            start += len(evs)
+            if r.get("state") not in (None, "RUNNING", "PREP"):
+                raise RuntimeError(f"job ended ({r.get('state')}) while the reduce was copying")
+            new = False
+            for tid, aid, out in evs:
+                if tid in got_maps or aid in seen:
+                    continue        # a re-executed map's second event: already fetched
+                got_maps.add(tid)
+                seen.add(aid)
+                new = True
+                yield MapOutputLocation(aid, (out or {}).get("path"))
+            if not new:
+                time.sleep(delay)
+                delay = min(0.05, delay * 2)
+            else:
+                delay = 0.001
+
     def run(self, local_dir: str):
         self.start_time = time.time()
         job = self._task_conf()
@@ -616,26 +694,25 @@ class ReduceTask(Task):
         from .skipbadrecords import SkipLog, record_skip, skipping_limit
         skip_max = skipping_limit(job, False)
         kind = sortbuf.key_kind(job) if not skip_max else None
-        # copy phase
-        segs = []
-        shuffled = 0
-        for loc in self.locations:
+        # copy phase: bounded shuffle buffer, big or overflowing segments go to
+        # disk as sorted runs (ReduceCopier, hbmr/mapred/shuffle.py)
+        from .shuffle import ShuffleMerger
+        merger = ShuffleMerger(job, local_dir, codec, sort_key, kind, rep, self.check_killed)
+        for loc in self._map_outputs():
             self.check_killed()
-            data = loc.read_partition(self.partition)
-            shuffled += len(data)
-            if kind is not None:
-                segs.append(sortbuf.segment_body(data, codec))
-            else:
-                segs.append([(sort_key(kb), kb, vb) for kb, vb in read_segment(data, codec)])
-        rep.incrCounter(C.TASK_GROUP, C.REDUCE_SHUFFLE_BYTES, shuffled)
+            merger.add(loc.read_partition(self.partition))
+        rep.incrCounter(C.TASK_GROUP, C.REDUCE_SHUFFLE_BYTES, merger.shuffled)
         rep.set_progress(1 / 3)
         # sort phase (merge)
-        if kind is not None:
-            # stable sort of the concatenated map outputs == Merger's k-way merge
-            b = sortbuf.Batch.from_ifile_bodies(segs)
-            perm = b.sort(kind, np.zeros(b.n, np.int32))
-            return self._reduce_native(job, b, perm, kind, kcls, vcls)
-        merged = merge_segments(segs, job.get_int("io.sort.factor", 10))
+        if not merger.on_disk:
+            if kind is not None:
+                # stable sort of the concatenated map outputs == Merger's k-way merge
+                b = sortbuf.Batch.from_ifile_bodies(merger.memory_bodies())
+                perm = b.sort(kind, np.zeros(b.n, np.int32))
+                return self._reduce_native(job, b, perm, kind, kcls, vcls)
+            merged = merge_segments(merger.memory_records(), job.get_int("io.sort.factor", 10))
+        else:
+            merged = merger.final_iter()
         rep.set_progress(2 / 3)
         # reduce phase
         committer = self.committer()
@@ -685,6 +762,7 @@ class ReduceTask(Task):
                 skiplog.close()
             reducer.close()
             writer.close(rep)
+        merger.cleanup()
         rep.incrCounter(C.TASK_GROUP, C.REDUCE_INPUT_GROUPS, n_groups)
         rep.incrCounter(C.TASK_GROUP, C.REDUCE_INPUT_RECORDS, next(n_in))
         rep.incrCounter(C.TASK_GROUP, C.REDUCE_OUTPUT_RECORDS, n_out[0])
