@@ -136,7 +136,10 @@ class TeraSortSplitJob(SplitJob):
 
     def get_splits(self, conf, trackers):
         ranges = self._ranges()
-        nparts = self.nparts_conf or max(1, len(trackers))
+        # default R: one per tracker, and at least one per ~2 GB of input so a
+        # single GPU sorts the output a partition at a time
+        total = sum(r[2] for r in ranges) * S.RECORD
+        nparts = self.nparts_conf or max(1, len(trackers), -(-total // (2 << 30)))
         split_keys = create_partitions(self._sample_keys(ranges), nparts) if nparts > 1 else \
             np.zeros((0, 10), dtype=np.uint8)
         hi, lo = _key_words(split_keys)
@@ -164,21 +167,35 @@ class TeraSortSplitJob(SplitJob):
         return int(data["records"].numel())
 
     def _map(self, ctx, data):
+        """Range-partition the split (TeraSort.java's TotalOrderPartitioner):
+        key words + partition of every record, then a stable counting sort by
+        partition.  The map output is 20 B per record — sorted-by-partition key
+        words and row numbers into the (HBM-resident) input split; the 100-byte
+        records themselves move once, in the reduce's final gather."""
         recs = data["records"]
-        hi, lo = S.tera_keys(recs, stream=getattr(ctx, "stream", None))
-        perm, hs, ls = S.sort_keys(hi, lo)
-        srt = S.gather_records(recs, perm)
+        stream = getattr(ctx, "stream", None)
         nparts = data["nparts"]
+        shi, slo = _parse_keys(data["splitters"]) if nparts > 1 else (
+            torch.zeros(0, dtype=torch.int64), torch.zeros(0, dtype=torch.int64))
+        hi, lo, pid = S.tera_keys_part(recs, shi, slo, stream=stream)
+        n = recs.shape[0]
+        row = torch.arange(n, dtype=torch.int32, device=recs.device)
         if nparts > 1:
-            shi, slo = _parse_keys(data["splitters"])
-            offs = S.split_offsets(hs, ls, shi.to(hs.device), slo.to(hs.device))
+            bits = max(1, int(math.ceil(math.log2(nparts))))
+            S.radix_sort_pairs(pid, row, 0, min(64, 8 * ((bits + 7) // 8)), stream=stream)
+            hp, lp = S.gather_u64(hi, row, stream=stream), S.gather_u64(lo, row, stream=stream)
         else:
-            offs = torch.tensor([0, recs.shape[0]], dtype=torch.int64)
-        # checksum of the input keys (order independent) for end-to-end validation
-        csum = int((hi.sum() + lo.sum()).item()) if recs.shape[0] else 0
-        ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, recs.shape[0])
-        ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_OUTPUT_RECORDS, recs.shape[0])
-        return {"records": srt, "offsets": offs.to("cpu").tolist(), "checksum": csum}
+            hp, lp = hi, lo
+        counts = torch.bincount(pid, minlength=nparts) if n else \
+            torch.zeros(nparts, dtype=torch.int64, device=recs.device)
+        offs = torch.zeros(nparts + 1, dtype=torch.int64, device=recs.device)
+        torch.cumsum(counts, 0, out=offs[1:])
+        # order-independent checksum of the input keys, kept on the device
+        csum = hi.sum() + lo.sum()
+        ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, n)
+        ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_OUTPUT_RECORDS, n)
+        return {"records": recs, "hi": hp, "lo": lp, "row": row, "offsets": offs,
+                "checksum": csum, "nparts": nparts, "splitters": data["splitters"]}
 
     def map_gpu(self, ctx, data):
         return self._map(ctx, data)
@@ -195,43 +212,32 @@ class TeraSortSplitJob(SplitJob):
         return rank * nparts // world, (rank + 1) * nparts // world
 
     def combine(self, ctx, outputs):
-        dev = ctx.device if ctx.device is not None else torch.device("cpu")
-        W = ctx.world_size
-        nparts = None
-        pieces, counts = [], [0] * W
-        csum = 0
-        for o in outputs:
-            csum += o["checksum"]
-        for d in range(W):
-            for o in outputs:
-                offs = o["offsets"]
-                nparts = len(offs) - 1
-                a, b = self.owner_range(d, W, nparts)
-                lo_, hi_ = offs[a], offs[b]
-                if hi_ > lo_:
-                    pieces.append(o["records"][lo_:hi_].to(dev))
-                    counts[d] += hi_ - lo_
-        send = torch.cat(pieces) if pieces else torch.empty(0, S.RECORD, dtype=torch.uint8,
-                                                            device=dev)
-        return {"send": send, "counts": counts, "checksum": csum, "nparts": nparts}
+        outs = [o for o in outputs if o is not None]
+        if not outs:
+            return {"outs": [], "offsets": None, "nparts": None, "checksum": 0}
+        # one device->host copy of every map's partition offsets
+        offs = torch.stack([o["offsets"] for o in outs]).to("cpu").numpy()
+        csum = torch.stack([o["checksum"].reshape(()) for o in outs]).sum()
+        return {"outs": outs, "offsets": offs, "nparts": outs[0]["nparts"], "checksum": csum}
 
     def reduce(self, ctx, combined):
         comm = ctx.comm
-        recv, _ = comm.all_to_all_v(combined["send"], combined["counts"])
-        srt, hs, ls = S.sort_records(recv) if recv.shape[0] else (recv, recv[:0, 0].long(),
-                                                                  recv[:0, 0].long())
-        bad = S.count_unsorted(hs, ls)
-        # boundary check against the neighbours + global record/checksum totals
-        n = int(srt.shape[0])
-        first = (int(hs[0].item()), int(ls[0].item())) if n else (-1, -1)
-        last = (int(hs[-1].item()), int(ls[-1].item())) if n else (-1, -1)
-        csum_here = int(hs.sum().item()) + int(ls.sum().item()) if n else 0
-        meta = torch.tensor([n, _s64(combined["checksum"]), _s64(csum_here), bad, first[0],
-                             first[1], last[0], last[1]], dtype=torch.int64)
+        outs = combined["outs"]
+        dev = ctx.device if ctx.device is not None else torch.device("cpu")
+        nparts = combined["nparts"]
+        csum_in = combined["checksum"]
+        csum_in = int(csum_in.item()) if torch.is_tensor(csum_in) else int(csum_in)
+        if comm.world_size == 1:
+            stats = self._reduce_local(ctx, outs, combined["offsets"], nparts or 1, dev)
+        else:
+            stats = self._reduce_shuffle(ctx, outs, combined["offsets"], nparts, dev)
+        n, bad, csum_here, first, last = stats
+        meta = torch.tensor([n, _s64(csum_in), _s64(csum_here), bad, first[0], first[1], last[0],
+                             last[1]], dtype=torch.int64)
         gathered = comm.all_gather(meta)
         total = sum(int(g[0]) for g in gathered)
-        csum_in = sum(int(g[1]) for g in gathered)
-        csum_out = sum(int(g[2]) for g in gathered)
+        c_in = sum(int(g[1]) for g in gathered)
+        c_out = sum(int(g[2]) for g in gathered)
         cross_bad = 0
         prev_last = None
         for g in gathered:
@@ -241,20 +247,119 @@ class TeraSortSplitJob(SplitJob):
             if prev_last is not None and f < prev_last:
                 cross_bad += 1
             prev_last = (int(g[6]) & 0xFFFFFFFFFFFFFFFF, int(g[7]))
-        if self.out:
-            self._write(ctx, srt, hs, ls, combined["nparts"] or 1)
+        peak = torch.cuda.max_memory_allocated(dev) if dev.type == "cuda" else 0
         return {"records": n, "total_records": total, "unsorted": bad + cross_bad,
-                "checksum_ok": (csum_in - csum_out) % (1 << 64) == 0}
+                "checksum_ok": (c_in - c_out) % (1 << 64) == 0, "partitions": nparts or 1,
+                "peak_hbm_bytes": int(peak)}
 
-    def _write(self, ctx, srt, hs, ls, nparts):
+    def _sorted_partition(self, his, los, rows, starts, lens, bases, dev, stream=None):
+        """Collect one partition's pieces from every map output, sort its keys,
+        gather its records: (records, sorted hi, sorted lo)."""
+        h, lw, split, row = S.tera_collect(his, los, rows, starts, lens, stream=stream)
+        perm, hs, ls = S.sort_keys(h, lw, stream=stream)
+        del h, lw
+        recs = S.gather_records_multi(bases, split, row, perm, stream=stream)
+        return recs, hs, ls
+
+    def _reduce_local(self, ctx, outs, offs, nparts, dev):
+        """One rank owns every partition: no record shuffle.  Partitions are
+        sorted one at a time (working set = one partition), so peak HBM is the
+        input splits + 20 B/record of map output + one partition."""
+        if not outs:
+            return 0, 0, 0, (-1, -1), (-1, -1)
+        his = [o["hi"] for o in outs]
+        los = [o["lo"] for o in outs]
+        rows = [o["row"] for o in outs]
+        bases = [o["records"] for o in outs]
+        zero = torch.zeros((), dtype=torch.int64, device=dev)
+        bad = zero.clone()
+        csum = zero.clone()
+        prev_last = None
+        first = last = None
+        n = 0
+        for p in range(nparts):
+            starts = offs[:, p]
+            lens = offs[:, p + 1] - offs[:, p]
+            m = int(lens.sum())
+            if m == 0:
+                continue
+            recs, hs, ls = self._sorted_partition(his, los, rows, starts, lens, bases, dev)
+            bad = bad + S.count_unsorted_dev(hs, ls)
+            if prev_last is not None:
+                bad = bad + S.pair_greater(prev_last, (hs[:1], ls[:1]))
+            prev_last = (hs[-1:], ls[-1:])
+            if first is None:
+                first = (hs[:1], ls[:1])
+            last = (hs[-1:], ls[-1:])
+            csum = csum + hs.sum() + ls.sum()
+            n += m
+            if self.out:
+                self._write_part(p, recs)
+            del recs, hs, ls
+        fl = torch.cat([first[0], first[1], last[0], last[1]]).to("cpu").tolist()
+        return n, int(bad.item()), int(csum.item()), (fl[0], fl[1]), (fl[2], fl[3])
+
+    def _reduce_shuffle(self, ctx, outs, offs, nparts, dev):
+        """world > 1: every rank gathers the records of each destination's
+        partition range from its splits (one pass), one all-to-all-v over
+        RCCL/xGMI, then sorts what it received (its contiguous key range)."""
+        comm = ctx.comm
+        W, me = comm.world_size, comm.rank
+        # a rank that ran no map learns R (and the splitters) from its peers
+        nparts = max(int(g[0]) for g in comm.all_gather(
+            torch.tensor([nparts or 0], dtype=torch.int64)))
+        counts = [0] * W
+        splits, rowsl = [], []
+        if outs:
+            rows = [o["row"] for o in outs]
+            bases = [o["records"] for o in outs]
+            for d in range(W):
+                a, b = self.owner_range(d, W, nparts)
+                starts = offs[:, a]
+                lens = offs[:, b] - offs[:, a]
+                counts[d] = int(lens.sum())
+                if counts[d]:
+                    _h, _l, sp, rw = S.tera_collect(None, None, rows, starts, lens, with_keys=False)
+                    splits.append(sp)
+                    rowsl.append(rw)
+            if splits:
+                send = S.gather_records_multi(bases, torch.cat(splits), torch.cat(rowsl))
+            else:
+                send = torch.empty(0, S.RECORD, dtype=torch.uint8, device=dev)
+            del splits, rowsl
+        else:
+            send = torch.empty(0, S.RECORD, dtype=torch.uint8, device=dev)
+        recv, _ = comm.all_to_all_v(send, counts)
+        del send
+        if recv.shape[0] == 0:
+            return 0, 0, 0, (-1, -1), (-1, -1)
+        srt, hs, ls = S.sort_records(recv)
+        del recv
+        bad = S.count_unsorted(hs, ls)
+        csum_here = int(hs.sum().item()) + int(ls.sum().item())
+        n = int(srt.shape[0])
+        if self.out:
+            a, b = self.owner_range(me, W, nparts)
+            if b - a > 1:
+                shi, slo = _parse_keys(self._splitters_of(outs))
+                cut = S.split_offsets(hs, ls, shi[a:b - 1].to(dev), slo[a:b - 1].to(dev)) \
+                    .to("cpu").tolist()
+                cut = [0] + cut[1:-1] + [n]
+            else:
+                cut = [0, n]
+            for i, p in enumerate(range(a, b)):
+                self._write_part(p, srt[cut[i]:cut[i + 1]])
+        fl = torch.stack([hs[0], ls[0], hs[-1], ls[-1]]).to("cpu").tolist()
+        return n, bad, csum_here, (fl[0], fl[1]), (fl[2], fl[3])
+
+    def _splitters_of(self, outs):
+        if not outs:
+            raise RuntimeError("writing several partitions needs the splitters of a local map")
+        return outs[0]["splitters"]
+
+    def _write_part(self, p, recs):
         os.makedirs(self.out, exist_ok=True)
-        a, b = self.owner_range(ctx.rank, ctx.world_size, nparts)
-        host = srt.to("cpu").numpy()
-        if b - a <= 1:
-            host.tofile(os.path.join(self.out, f"part-{a:05d}"))
-            return
-        # several partitions on this rank: cut by the job's splitters
-        raise NotImplementedError("more partitions than trackers: set hbmr.terasort.partitions")
+        recs.to("cpu").numpy().tofile(os.path.join(self.out, f"part-{p:05d}"))
 
 
 def terasort_conf(base=None, rows=1_000_000, split_rows=None, output=None, inp=None,

@@ -53,6 +53,12 @@ _SIGS = {
     "hbmr_split_offsets": (c_int, [c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_int,
                                    c_void_p, c_void_p]),
     "hbmr_check_sorted": (c_int, [c_void_p, c_void_p, c_long, c_void_p, c_void_p]),
+    "hbmr_tera_keys_part": (c_int, [c_void_p, c_long, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                    c_void_p, c_void_p, c_void_p]),
+    "hbmr_tera_collect": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_long,
+                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "hbmr_gather_records_multi": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int,
+                                          c_void_p, c_void_p]),
     # text / WordCount (native/kernels/text.hip)
     "hbmr_wc_tiles": (c_long, [c_long]),
     "hbmr_wc_tokenize_count": (c_int, [c_void_p, c_long, c_void_p, c_void_p]),

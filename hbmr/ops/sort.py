@@ -237,3 +237,128 @@ def keys_from_bytes(keys: list) -> tuple[torch.Tensor, torch.Tensor]:
     hi = np.array([int.from_bytes(k[:8].ljust(8, b"\0"), "big") for k in keys], dtype=np.uint64)
     lo = np.array([int.from_bytes(k[8:10].ljust(2, b"\0"), "big") for k in keys], dtype=np.uint64)
     return torch.from_numpy(hi.view(np.int64)), torch.from_numpy(lo.view(np.int64))
+
+
+# --------------------------------------------------------------------------- range-partitioned TeraSort
+def tera_keys_part(records: torch.Tensor, split_hi: torch.Tensor, split_lo: torch.Tensor,
+                   stream=None):
+    """(hi, lo, pid) of every record: key words and its range partition (the
+    number of splitters <= key; splitters sorted, at most 4096)."""
+    n, stride = records.shape
+    ns = split_hi.numel()
+    if _on_gpu(records):
+        if ns > 4096:
+            raise ValueError("at most 4096 splitters (4097 partitions)")
+        hi = torch.empty(n, dtype=torch.int64, device=records.device)
+        lo = torch.empty(n, dtype=torch.int64, device=records.device)
+        pid = torch.empty(n, dtype=torch.int64, device=records.device)
+        sh = split_hi.to(records.device)
+        sl = split_lo.to(records.device)
+        rc = _lib.load().hbmr_tera_keys_part(_ptr(records), n, stride, _ptr(sh) if ns else None,
+                                              _ptr(sl) if ns else None, ns, _ptr(hi), _ptr(lo),
+                                              _ptr(pid), _lib.stream_handle(stream))
+        _lib.check(rc, "hbmr_tera_keys_part")
+        return hi, lo, pid
+    hi, lo = tera_keys(records)
+    h = hi.numpy().view(np.uint64)
+    lw = lo.numpy().view(np.uint64)
+    sh = split_hi.numpy().view(np.uint64)
+    sl = split_lo.numpy().view(np.uint64)
+    # pid = #splitters <= key (lexicographic (hi, lo))
+    pid = np.searchsorted(sh, h, side="left").astype(np.int64)
+    for j in range(ns):      # ties on hi: decide by lo
+        tie = h == sh[j]
+        pid[tie & (lw >= sl[j])] = np.maximum(pid[tie & (lw >= sl[j])], j + 1)
+    return hi, lo, torch.from_numpy(pid)
+
+
+def _ptr_table(ts, device):
+    return torch.tensor([t.data_ptr() for t in ts], dtype=torch.int64, device=device)
+
+
+def tera_collect(his, los, rows, starts, lens, with_keys=True, stream=None):
+    """Concatenate pieces [starts[s], starts[s]+lens[s]) of per-split (hi, lo,
+    row) arrays → (hi, lo, split, row) (hi/lo None unless ``with_keys``)."""
+    S = len(rows)
+    n = int(sum(lens))
+    dev = rows[0].device
+    if not _on_gpu(rows[0]):
+        sel = [slice(int(a), int(a) + int(m)) for a, m in zip(starts, lens)]
+        split = torch.cat([torch.full((int(m),), s, dtype=torch.int32) for s, m in enumerate(lens)])
+        row = torch.cat([r[sl] for r, sl in zip(rows, sel)])
+        if not with_keys:
+            return None, None, split, row
+        return (torch.cat([h[sl] for h, sl in zip(his, sel)]),
+                torch.cat([lw[sl] for lw, sl in zip(los, sel)]), split, row)
+    prefix = np.zeros(S + 1, dtype=np.int64)
+    np.cumsum(np.asarray(lens, dtype=np.int64), out=prefix[1:])
+    meta = torch.from_numpy(np.concatenate([np.asarray(starts, dtype=np.int64), prefix])).to(dev)
+    split = torch.empty(n, dtype=torch.int32, device=dev)
+    row = torch.empty(n, dtype=torch.int32, device=dev)
+    ohi = torch.empty(n, dtype=torch.int64, device=dev) if with_keys else None
+    olo = torch.empty(n, dtype=torch.int64, device=dev) if with_keys else None
+    th = _ptr_table(his, dev) if with_keys else None
+    tl = _ptr_table(los, dev) if with_keys else None
+    tr = _ptr_table(rows, dev)
+    rc = _lib.load().hbmr_tera_collect(_ptr(th), _ptr(tl), _ptr(tr), _ptr(meta),
+                                        _ptr(meta) + 8 * S, S, n, _ptr(ohi), _ptr(olo),
+                                        _ptr(split), _ptr(row), _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_tera_collect")
+    return ohi, olo, split, row
+
+
+def gather_records_multi(bases, split: torch.Tensor, row: torch.Tensor, perm=None,
+                         out=None, stream=None) -> torch.Tensor:
+    """out[i] = bases[split[k]][row[k]], k = perm[i] (or i): 100-byte records
+    gathered from several split tensors in one pass."""
+    n = split.numel()
+    rb = bases[0].shape[1]
+    if not _on_gpu(split):
+        k = perm.long() if perm is not None else torch.arange(n)
+        s, r = split[k].long(), row[k].long()
+        res = torch.empty(n, rb, dtype=torch.uint8) if out is None else out
+        for j, b in enumerate(bases):
+            m = s == j
+            if m.any():
+                res[m] = b[r[m]]
+        return res
+    res = torch.empty(n, rb, dtype=torch.uint8, device=split.device) if out is None else out
+    tb = _ptr_table(bases, split.device)
+    rc = _lib.load().hbmr_gather_records_multi(_ptr(tb), _ptr(split), _ptr(row), _ptr(perm), n, rb,
+                                                _ptr(res), _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_gather_records_multi")
+    return res
+
+
+def gather_u64(src: torch.Tensor, perm: torch.Tensor, stream=None) -> torch.Tensor:
+    """dst[i] = src[perm[i]] for int64 storage (perm int32)."""
+    if not _on_gpu(src):
+        return src[perm.long()]
+    dst = torch.empty(perm.numel(), dtype=src.dtype, device=src.device)
+    rc = _lib.load().hbmr_gather_u64(_ptr(src), _ptr(perm), perm.numel(), _ptr(dst),
+                                      _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_gather_u64")
+    return dst
+
+
+def count_unsorted_dev(hi: torch.Tensor, lo: torch.Tensor, stream=None) -> torch.Tensor:
+    """count_unsorted as a 0-d int64 device tensor (no host sync)."""
+    n = hi.numel()
+    if n <= 1 or not _on_gpu(hi):
+        return torch.tensor(count_unsorted(hi, lo), dtype=torch.int64, device=hi.device)
+    bad = torch.zeros(1, dtype=torch.int64, device=hi.device)
+    rc = _lib.load().hbmr_check_sorted(_ptr(hi), _ptr(lo), n, _ptr(bad),
+                                        _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_check_sorted")
+    return bad[0]
+
+
+_SIGN = -0x8000000000000000
+
+
+def pair_greater(a, b) -> torch.Tensor:
+    """1 if key a > key b (a, b: (hi, lo) 1-element int64 tensors holding uint64),
+    as a 0-d int64 tensor on their device (no host sync)."""
+    ah, al = a[0] ^ _SIGN, a[1]
+    bh, bl = b[0] ^ _SIGN, b[1]
+    return ((ah > bh) | ((ah == bh) & (al > bl))).to(torch.int64).reshape(())

@@ -56,6 +56,16 @@ int hbmr_split_offsets(const uint64_t* hi, const uint64_t* lo, long n, const uin
                        const uint64_t* slo, int nparts, long* offsets, hipStream_t st);
 int hbmr_check_sorted(const uint64_t* hi, const uint64_t* lo, long n, unsigned long long* bad,
                       hipStream_t st);
+int hbmr_tera_keys_part(const void* records, long n, int stride, const uint64_t* shi,
+                        const uint64_t* slo, int nsplit, uint64_t* hi, uint64_t* lo,
+                        uint64_t* pid, hipStream_t st);
+int hbmr_tera_collect(const uint64_t* const* his, const uint64_t* const* los,
+                      const uint32_t* const* rows, const long* starts, const long* prefix, int S,
+                      long n, uint64_t* ohi, uint64_t* olo, uint32_t* osplit, uint32_t* orow,
+                      hipStream_t st);
+int hbmr_gather_records_multi(const void* const* bases, const uint32_t* split, const uint32_t* row,
+                              const uint32_t* perm, long n, int record_bytes, void* dst,
+                              hipStream_t st);
 #endif
 long hbmr_radix_sort_workspace_bytes(long n);
 

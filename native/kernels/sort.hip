@@ -330,6 +330,79 @@ __global__ __launch_bounds__(256) void check_sorted_kernel(const uint64_t* __res
   if ((threadIdx.x & 63) == 0 && m) atomicAdd(bad, (unsigned long long)__popcll(m));
 }
 
+// Key words + range partition of each record: pid = number of splitters <= key
+// (partition p holds keys in [split[p-1], split[p]), as split_offsets cuts a
+// sorted run).  Splitters are staged in LDS once per workgroup; each workgroup
+// then walks a grid-stride slice of the records.
+constexpr int kMaxSplitters = 4096;
+
+__global__ __launch_bounds__(256) void tera_keys_part_kernel(
+    const uint8_t* __restrict__ rec, long n, int stride, const uint64_t* __restrict__ shi,
+    const uint64_t* __restrict__ slo, int nsplit, uint64_t* __restrict__ hi,
+    uint64_t* __restrict__ lo, uint64_t* __restrict__ pid) {
+  __shared__ uint64_t s_hi[kMaxSplitters];
+  __shared__ uint16_t s_lo[kMaxSplitters];
+  for (int j = threadIdx.x; j < nsplit; j += 256) {
+    s_hi[j] = shi[j];
+    s_lo[j] = (uint16_t)slo[j];
+  }
+  __syncthreads();
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const uint8_t* r = rec + i * stride;
+    uint64_t h = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) h = (h << 8) | r[j];
+    const uint32_t l = ((uint32_t)r[8] << 8) | r[9];
+    int a = 0, b = nsplit;
+    while (a < b) {
+      const int m = (a + b) >> 1;
+      const bool le = s_hi[m] < h || (s_hi[m] == h && s_lo[m] <= l);
+      if (le) a = m + 1; else b = m;
+    }
+    hi[i] = h;
+    lo[i] = l;
+    pid[i] = (uint64_t)a;
+  }
+}
+
+// Concatenate S pieces: piece s is [starts[s], starts[s] + len_s) of its split's
+// (hi, lo, row) arrays, placed at [prefix[s], prefix[s+1]) of the output; the
+// output also records which split each element came from.  hi/lo (in and out)
+// may be null (records-only collection for the shuffle).
+__global__ __launch_bounds__(256) void tera_collect_kernel(
+    const uint64_t* const* __restrict__ his, const uint64_t* const* __restrict__ los,
+    const uint32_t* const* __restrict__ rows, const long* __restrict__ starts,
+    const long* __restrict__ prefix, int S, long n, uint64_t* __restrict__ ohi,
+    uint64_t* __restrict__ olo, uint32_t* __restrict__ osplit, uint32_t* __restrict__ orow) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    int a = 0, b = S;          // largest s with prefix[s] <= i
+    while (b - a > 1) {
+      const int m = (a + b) >> 1;
+      if (prefix[m] <= i) a = m; else b = m;
+    }
+    const long j = starts[a] + (i - prefix[a]);
+    if (ohi) ohi[i] = his[a][j];
+    if (olo) olo[i] = los[a][j];
+    osplit[i] = (uint32_t)a;
+    orow[i] = rows[a][j];
+  }
+}
+
+// dst record i = record row[k] of split split[k], k = perm ? perm[i] : i; records
+// of `words` 4-byte words, one word per lane (25 lanes cover a 100-byte record)
+__global__ __launch_bounds__(256) void gather_records_multi_kernel(
+    const uint32_t* const* __restrict__ bases, const uint32_t* __restrict__ split,
+    const uint32_t* __restrict__ row, const uint32_t* __restrict__ perm, long n, int words,
+    uint32_t* __restrict__ dst) {
+  const long total = n * words;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
+    const long r = e / words;
+    const int w = (int)(e - r * words);
+    const long k = perm ? (long)perm[r] : r;
+    dst[e] = bases[split[k]][(long)row[k] * words + w];
+  }
+}
+
 inline long ceil_div(long a, long b) { return (a + b - 1) / b; }
 
 }  // namespace
@@ -423,6 +496,43 @@ int hbmr_check_sorted(const uint64_t* hi, const uint64_t* lo, long n, unsigned l
   if (n <= 1) return 0;
   hipLaunchKernelGGL(check_sorted_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, hi,
                      lo, n, bad);
+  return (int)hipGetLastError();
+}
+
+int hbmr_tera_keys_part(const void* records, long n, int stride, const uint64_t* shi,
+                        const uint64_t* slo, int nsplit, uint64_t* hi, uint64_t* lo,
+                        uint64_t* pid, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (nsplit < 0 || nsplit > kMaxSplitters) return (int)hipErrorInvalidValue;
+  const long grid = std::min<long>(ceil_div(n, 256), 256L * 64);
+  hipLaunchKernelGGL(tera_keys_part_kernel, dim3((unsigned)grid), dim3(256), 0, st,
+                     reinterpret_cast<const uint8_t*>(records), n, stride, shi, slo, nsplit, hi,
+                     lo, pid);
+  return (int)hipGetLastError();
+}
+
+int hbmr_tera_collect(const uint64_t* const* his, const uint64_t* const* los,
+                      const uint32_t* const* rows, const long* starts, const long* prefix, int S,
+                      long n, uint64_t* ohi, uint64_t* olo, uint32_t* osplit, uint32_t* orow,
+                      hipStream_t st) {
+  if (n <= 0) return 0;
+  if (S <= 0) return (int)hipErrorInvalidValue;
+  const long grid = std::min<long>(ceil_div(n, 256), 256L * 256);
+  hipLaunchKernelGGL(tera_collect_kernel, dim3((unsigned)grid), dim3(256), 0, st, his, los, rows,
+                     starts, prefix, S, n, ohi, olo, osplit, orow);
+  return (int)hipGetLastError();
+}
+
+int hbmr_gather_records_multi(const void* const* bases, const uint32_t* split, const uint32_t* row,
+                              const uint32_t* perm, long n, int record_bytes, void* dst,
+                              hipStream_t st) {
+  if (n <= 0) return 0;
+  if (record_bytes % 4) return (int)hipErrorInvalidValue;
+  const int words = record_bytes / 4;
+  const long grid = std::min<long>(ceil_div(n * words, 256), 1L << 20);
+  hipLaunchKernelGGL(gather_records_multi_kernel, dim3((unsigned)grid), dim3(256), 0, st,
+                     reinterpret_cast<const uint32_t* const*>(bases), split, row, perm, n, words,
+                     reinterpret_cast<uint32_t*>(dst));
   return (int)hipGetLastError();
 }
 

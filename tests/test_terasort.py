@@ -54,6 +54,39 @@ def test_terasort_on_cluster_sorts_and_validates(tmp_path, trackers):
     assert np.array_equal(got, _ref_sorted(rows))
 
 
+@pytest.mark.parametrize("trackers", [1, 2, 3])
+def test_terasort_more_partitions_than_trackers(tmp_path, trackers):
+    """R part files for any R (TeraSort.java writes one per reduce): a rank
+    owning several partitions cuts its sorted range by the splitters; one rank
+    alone sorts its partitions one at a time."""
+    rows = 12000
+    out = tmp_path / "out"
+    with LocalCluster(JobConf(), num_trackers=trackers, cpu_slots=2) as cl:
+        rj = cl.submit_job(T.terasort_conf(rows=rows, split_rows=2500, output=str(out),
+                                           partitions=7))
+        rj.waitForCompletion(120)
+        assert rj.isSuccessful(), rj.getFailureInfo()
+        res = rj._impl.jip.result
+    assert all(r["unsorted"] == 0 and r["checksum_ok"] for r in res.values())
+    parts = sorted(f for f in os.listdir(out) if f.startswith("part-"))
+    assert parts == [f"part-{i:05d}" for i in range(7)]
+    got = np.concatenate([np.fromfile(out / p, dtype=np.uint8).reshape(-1, 100) for p in parts])
+    assert np.array_equal(got, _ref_sorted(rows))
+    assert T.teravalidate(str(out))["misordered"] == 0
+
+
+def test_partition_ops_cpu():
+    recs = torch.from_numpy(S.teragen_cpu(0, 5000))
+    sp = T.create_partitions(recs.numpy()[::50, :10].copy(), 6)
+    shi, slo = (torch.from_numpy(x.view(np.int64)) for x in T._key_words(sp))
+    hi, lo, pid = S.tera_keys_part(recs, shi, slo)
+    h = hi.numpy().view(np.uint64)
+    lw = lo.numpy().view(np.uint64)
+    keys = list(zip(h.tolist(), lw.tolist()))
+    spl = list(zip(shi.numpy().view(np.uint64).tolist(), slo.numpy().view(np.uint64).tolist()))
+    assert pid.tolist() == [sum(1 for s_ in spl if s_ <= k) for k in keys]
+
+
 def test_terasort_from_teragen_files(tmp_path):
     inp = tmp_path / "in"
     inp.mkdir()
@@ -117,3 +150,47 @@ def test_gpu_terasort_job(tmp_path):
     assert res["records"] == rows and res["unsorted"] == 0 and res["checksum_ok"]
     got = np.fromfile(tmp_path / "out" / "part-00000", dtype=np.uint8).reshape(-1, 100)
     assert np.array_equal(got[:1000], _ref_sorted(rows)[:1000])
+
+
+@pytest.mark.gpu
+def test_gpu_partition_collect_and_multi_gather_match_cpu():
+    n = 200000
+    recs_c = torch.from_numpy(S.teragen_cpu(777, n))
+    recs = recs_c.cuda()
+    sp = T.create_partitions(recs_c.numpy()[::101, :10].copy(), 37)
+    shi, slo = (torch.from_numpy(x.view(np.int64)) for x in T._key_words(sp))
+    g = S.tera_keys_part(recs, shi, slo)
+    c = S.tera_keys_part(recs_c, shi, slo)
+    for a, b in zip(g, c):
+        assert torch.equal(a.cpu(), b)
+    # collect pieces of three "splits" and gather their records
+    parts = [recs[:70000], recs[70000:150000], recs[150000:]]
+    his = [S.tera_keys(p)[0] for p in parts]
+    los = [S.tera_keys(p)[1] for p in parts]
+    rows = [torch.arange(p.shape[0], dtype=torch.int32, device="cuda").flip(0).contiguous()
+            for p in parts]
+    starts, lens = [5, 0, 1000], [100, 70000, 17]
+    h, lw, sp_, rw = S.tera_collect(his, los, rows, starts, lens)
+    hc, lc, spc, rwc = S.tera_collect([x.cpu() for x in his], [x.cpu() for x in los],
+                                      [x.cpu() for x in rows], starts, lens)
+    assert torch.equal(h.cpu(), hc) and torch.equal(lw.cpu(), lc)
+    assert torch.equal(sp_.cpu(), spc) and torch.equal(rw.cpu(), rwc)
+    perm = torch.randperm(h.numel(), dtype=torch.int32).cuda()
+    out = S.gather_records_multi(parts, sp_, rw, perm)
+    outc = S.gather_records_multi([p.cpu() for p in parts], spc, rwc, perm.cpu())
+    assert torch.equal(out.cpu(), outc)
+
+
+@pytest.mark.gpu
+def test_gpu_terasort_many_partitions_one_gpu(tmp_path):
+    rows = 3_000_000
+    with LocalCluster(JobConf(), num_trackers=1, gpus=[[0]], cpu_slots=0) as cl:
+        rj = cl.submit_job(T.terasort_conf(rows=rows, split_rows=700_000, partitions=6,
+                                           output=str(tmp_path / "out")))
+        rj.waitForCompletion(300)
+        assert rj.isSuccessful(), rj.getFailureInfo()
+        res = rj._impl.jip.result[0]
+    assert res["records"] == rows and res["unsorted"] == 0 and res["checksum_ok"]
+    assert res["partitions"] == 6
+    v = T.teravalidate(str(tmp_path / "out"))
+    assert v["files"] == 6 and v["records"] == rows and v["misordered"] == 0

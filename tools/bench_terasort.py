@@ -1,11 +1,15 @@
 """TeraSort benchmark (BASELINE config 5) on the local GPUs.
 
-One job = TeraGen straight into HBM (map input) + per-split radix sort +
-range partition + all-to-all-v shuffle + final sort + validation.  The first
-job materialises the splits in HBM (split cache); timed jobs re-sort them.
+One job = map: key extraction + range partition (counting sort by partition)
+of every HBM-resident split; reduce: per partition, collect the pieces of
+every map, radix-sort the keys and gather the 100-byte records once (one GPU),
+or gather + all-to-all-v over RCCL/xGMI + sort (several GPUs); validation
+(order within and across partitions, key checksum) on the device.  The first
+job generates the input into HBM with TeraGen (split cache); timed jobs
+re-sort it.  The GPU work runs in the per-rank GPU worker process, so the
+timing brackets are sync jobs (every worker synchronises its device).
 
-  python tools/bench_terasort.py --rows 100000000 --split-rows 10000000 --steps 3
-  torchrun --nproc-per-node N tools/bench_terasort.py ...   (multi-GPU)
+  python tools/bench_terasort.py --rows 1000000000 --split-rows 10000000 --steps 3   # 100 GB
 """
 import argparse
 import json
@@ -23,9 +27,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--output", default=None)
+    ap.add_argument("--partitions", type=int, default=0)
     a = ap.parse_args()
-    import torch
-
     from hbmr.gpu.syncjob import sync_conf
     from hbmr.mapred.jobconf import JobConf
     from hbmr.mapred.node import Node
@@ -44,7 +47,7 @@ def main():
 
     def job():
         rj = node.submit_job(T.terasort_conf(conf, rows=a.rows, split_rows=a.split_rows,
-                                             output=a.output))
+                                             output=a.output, partitions=a.partitions))
         rj.waitForCompletion()
         if not rj.isSuccessful():
             raise RuntimeError(rj.getFailureInfo())
@@ -54,12 +57,10 @@ def main():
         for _ in range(a.warmup):
             job()
         node.submit_job(sync_conf(conf)).waitForCompletion()
-        torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(a.steps):
             rj = job()
         node.submit_job(sync_conf(conf)).waitForCompletion()
-        torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / a.steps
         res = rj._impl.jip.result
         ok = all(r["unsorted"] == 0 and r["checksum_ok"] for r in res.values())
@@ -70,6 +71,10 @@ def main():
                           "seconds_per_sort": round(dt, 4), "rows": a.rows,
                           "split_rows": a.split_rows, "n_gpus": node.world,
                           "validated": ok and total == a.rows,
+                          "data_gb": round(a.rows * 100 / 1e9, 2),
+                          "partitions": max(r.get("partitions", 0) for r in res.values()),
+                          "peak_hbm_gb_per_gpu": round(max(r.get("peak_hbm_bytes", 0)
+                                                           for r in res.values()) / 1e9, 2),
                           "timeline": rj._impl.jip.timeline()}))
     finally:
         node.shutdown()
