@@ -155,6 +155,7 @@ class GpuRuntime:
                                    "runner (hadoop.pipes.gpu.executable)")
             now = time.time()
             ctxs, datas = [], []
+            prefetched = self._prefetch_hosts(dev, runs, sj, SplitSpec)
             with torch.cuda.stream(slot.stream):
                 for r in runs:
                     rep = TaskReporter()
@@ -162,9 +163,14 @@ class GpuRuntime:
                     try:
                         tracker._maybe_inject_fault(r)
                         sspec = SplitSpec.from_dict(r.spec.split)
+                        host = prefetched.get(sspec.key)
+                        if host is not None:
+                            loader = (lambda s=sspec, h=host:
+                                      sj.load_split_from_host(s, h, dev.torch_device))
+                        else:
+                            loader = (lambda s=sspec: sj.load_split(s, dev.torch_device))
                         data, hit = tracker.split_cache.get_or_load(
-                            sspec.key, dev.index,
-                            lambda s=sspec: sj.load_split(s, dev.torch_device), sj.split_nbytes)
+                            sspec.key, dev.index, loader, sj.split_nbytes)
                     except BaseException as e:  # noqa: BLE001
                         tracker._finish(r, P.FAILED, f"{type(e).__name__}: {e}\n"
                                                      f"{traceback.format_exc()[-2000:]}")
@@ -196,6 +202,35 @@ class GpuRuntime:
                 if r.status.state not in P.TERMINAL:
                     tracker._finish(r, P.FAILED,
                                     f"{type(e).__name__}: {e}\n{traceback.format_exc()[-2000:]}")
+
+    def _prefetch_hosts(self, dev, runs, sj, SplitSpec):  # noqa: N803
+        """Cold splits of a batch whose job can load them on the host
+        (``load_split_host``: file decode into pinned memory) are read by a
+        thread pool in parallel; the H2D copies then go on the slot's stream."""
+        if sj is None or not hasattr(sj, "load_split_host"):
+            return {}
+        cold = []
+        for r in runs:
+            sspec = SplitSpec.from_dict(r.spec.split)
+            if sspec.kind == "file" and \
+                    self.tracker.split_cache.get(sspec.key, dev.index) is None:
+                cold.append(sspec)
+        if len(cold) < 2:
+            return {}
+        import concurrent.futures as cf
+        if getattr(self, "_loader_pool", None) is None:
+            n = max(1, self.tracker.conf.get_int("hbmr.gpu.load.threads", 8))
+            self._loader_pool = cf.ThreadPoolExecutor(n, thread_name_prefix="split-loader")
+        futs = {s.key: self._loader_pool.submit(sj.load_split_host, s) for s in cold}
+        out = {}
+        for k, f in futs.items():
+            try:
+                h = f.result()
+            except Exception:  # noqa: BLE001 — the per-task load reports it
+                h = None
+            if h is not None:
+                out[k] = h
+        return out
 
     def _completer(self, slot: _Slot):
         torch.cuda.set_device(slot.device)

@@ -382,6 +382,9 @@ class TaskTracker:
         self.reduce_pool.shutdown(wait=False, cancel_futures=True)
         if self.child_manager is not None:
             self.child_manager.shutdown()
+        pipes_app = sys.modules.get("hbmr.pipes.application")
+        if pipes_app is not None:
+            pipes_app.POOL.close_all()      # reused Pipes children (hbmr.pipes.child.reuse)
 
     def _hb_loop(self):
         initial = True

@@ -207,6 +207,7 @@ def _save_centroids_async(cdir, key, prev, cen):
 
 
 _SAVED: dict = {}
+_PINNED_INFLIGHT: list = []     # (event, pinned host buffer) of in-flight split loads
 
 
 # --------------------------------------------------------------------------- the job
@@ -284,22 +285,63 @@ class KMeansSplitJob(SplitJob):
             p = spec.params
             x = synthetic_points(p["seed"], p["start"], p["n"], self.d, self.centers, device)
         else:
-            from ..mapred.formats import FileSplit, SequenceFileRecordReader
-            from ..mapred.jobconf import JobConf
-            p = spec.params
-            rr = SequenceFileRecordReader(JobConf(), FileSplit(p["path"], p["start"],
-                                                               p["length"]))
-            rows = []
-            while True:
-                raw = rr.next_raw()
-                if raw is None:
-                    break
-                rows.append(np.frombuffer(raw[1][4:], dtype=">f4"))
-            rr.close()
-            arr = np.stack(rows).astype(np.float32) if rows else np.zeros((0, self.d), np.float32)
-            x = torch.from_numpy(arr).to(device)
+            x = self._load_file_split(spec.params, device)
         # bf16 is the storage precision of the points on every slot type
         return x.to(torch.bfloat16)
+
+    def load_split_host(self, spec: SplitSpec):
+        """Host half of a file split's load (native decode into pinned memory),
+        run by the GPU runtime's loader threads in parallel; None for synthetic
+        splits (they are generated on the device)."""
+        if spec.kind != "file":
+            return None
+        from ..io import nativeio
+        p = spec.params
+        n = nativeio.count_points(p["path"], p["start"], p["length"])
+        host = torch.empty(n, self.d, dtype=torch.float32,
+                           pin_memory=torch.cuda.is_available())
+        got = nativeio.read_points_into(p["path"], p["start"], p["length"], host.data_ptr(),
+                                        self.d, n)
+        return host[:got]
+
+    def load_split_from_host(self, spec: SplitSpec, host, device):
+        """Device half: one async H2D on the current stream, bf16 + padding."""
+        from ..ops import kmeans as km
+        x = host.to(device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        _PINNED_INFLIGHT.append((ev, host))
+        while _PINNED_INFLIGHT and _PINNED_INFLIGHT[0][0].query():
+            _PINNED_INFLIGHT.pop(0)
+        xb = x.to(torch.bfloat16)
+        dp = km.padded_dim(self.d)
+        if dp == self.d:
+            return xb.contiguous()
+        out = torch.zeros(xb.shape[0], dp, dtype=torch.bfloat16, device=device)
+        out[:, :self.d] = xb
+        return out
+
+    def _load_file_split(self, p, device):
+        """A SequenceFile split → fp32 [n, d] on ``device``: the native reader
+        decodes the records straight into pinned host memory, then one
+        asynchronous H2D copy on the current (slot) stream."""
+        from ..io import nativeio
+        n = nativeio.count_points(p["path"], p["start"], p["length"])
+        dev = torch.device(device)
+        host = torch.empty(n, self.d, dtype=torch.float32, pin_memory=dev.type == "cuda")
+        got = nativeio.read_points_into(p["path"], p["start"], p["length"], host.data_ptr(),
+                                        self.d, n)
+        host = host[:got]
+        if dev.type != "cuda":
+            return host
+        x = host.to(dev, non_blocking=True)
+        # the pinned buffer must outlive the copy: keep it until the stream passes
+        ev = torch.cuda.Event()
+        ev.record()
+        _PINNED_INFLIGHT.append((ev, host))
+        while _PINNED_INFLIGHT and _PINNED_INFLIGHT[0][0].query():
+            _PINNED_INFLIGHT.pop(0)
+        return x
 
     def load_split_sample(self, spec: SplitSpec, device, fraction: float):
         if spec.kind == "synthetic":

@@ -47,6 +47,15 @@ def write_points(path, n, d, seed=1, centers=8, files=1, bf16_exact=True, chunk=
     for fi in range(files):
         a, b = fi * per, min(n, (fi + 1) * per)
         fn = os.path.join(path, f"points-{fi:05d}.seq")
+        if compression == "NONE" and codec is None:
+            # native writer (native/io/seqpoints.cc): same bytes, ~100x faster
+            from ..io import nativeio
+            x = K.synthetic_points(seed, a, b - a, d, centers, "cpu")
+            if bf16_exact:
+                x = x.to(torch.bfloat16).to(torch.float32)
+            nativeio.write_points(fn, x.numpy(), first_id=a)
+            out.append(fn)
+            continue
         with seqf.Writer(fn, LongWritable, FloatVectorWritable, compression=compression,
                          codec=codec) as w:
             for c0 in range(a, b, chunk):
@@ -87,7 +96,7 @@ def read_centroids(outdir, old: torch.Tensor) -> torch.Tensor:
 
 
 def iteration_conf(base, inp, out, cen_file, k, d, cpubin=None, gpubin=None, reduces=1,
-                   maps=None) -> JobConf:
+                   maps=None, reuse=True) -> JobConf:
     from ..pipes import submitter
     job = JobConf(base)
     job.set_job_name(f"kmeans-pipes {os.path.basename(out)}")
@@ -99,6 +108,9 @@ def iteration_conf(base, inp, out, cen_file, k, d, cpubin=None, gpubin=None, red
     job.set_int("hbmr.kmeans.k", k)
     job.set_int("hbmr.kmeans.dims", d)
     job.set("hbmr.kmeans.centroids.file", os.path.abspath(cen_file))
+    # keep the task binaries alive across tasks and iteration jobs: the GPU
+    # binary keeps its HIP context and the HBM-resident splits
+    job.set_boolean("hbmr.pipes.child.reuse", reuse)
     job.set_num_reduce_tasks(reduces)
     if maps:
         job.set_num_map_tasks(maps)

@@ -93,7 +93,7 @@ class OutputHandler:
 class Application:
     def __init__(self, job, collector, reporter, key_class, value_class, executable: str,
                  run_on_gpu: bool = False, gpu_device_id: int = -1, partitioner=None,
-                 work_dir: str | None = None):
+                 work_dir: str | None = None, reuse: bool = False):
         if not executable:
             raise ValueError("no Pipes executable configured (hadoop.pipes.executable / "
                              "hadoop.pipes.gpu.executable)")
@@ -135,9 +135,10 @@ class Application:
         client.settimeout(None)
         client.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
         self.client = client
+        self.reuse = reuse
         self.handler = OutputHandler(collector, reporter, key_class, value_class, partitioner)
         self.downlink = DownwardProtocol(client)
-        self.uplink = UplinkReader(client, self.handler)
+        self.uplink = UplinkReader(client, self.handler, reuse=reuse)
         self.uplink.start()
         challenge = secrets.token_hex(16)
         digest = create_digest(password, challenge)
@@ -159,6 +160,16 @@ class Application:
         except OSError:
             return ""
 
+    def alive(self):
+        return self.proc.poll() is None and self.uplink.is_alive()
+
+    def begin_task(self, job, collector, reporter, key_class, value_class, partitioner=None):
+        """Next task on a reused child: its own output handler, its task conf."""
+        self.handler = OutputHandler(collector, reporter, key_class, value_class, partitioner)
+        self.uplink.handler = self.handler
+        self.job = job
+        self.downlink.set_job_conf(job)
+
     def wait_for_finish(self):
         try:
             self.handler.wait_for_finish()
@@ -166,6 +177,8 @@ class Application:
             rc = self.proc.wait(timeout=30)
             raise RuntimeError(f"pipes child failed (exit {rc}): {e}; {self._stderr_tail()}") \
                 from e
+        if self.reuse:
+            return True          # the child waits for its next task
         rc = self.proc.wait()
         if rc != 0:
             raise RuntimeError(f"pipes child exited with {rc}: {self._stderr_tail()}")
@@ -194,6 +207,87 @@ class Application:
         except OSError:
             pass
 
+    def close_child(self, timeout=10.0):
+        """End a reused child: CLOSE while it waits for a task, then reap it."""
+        try:
+            self.downlink.end_of_input()
+            self.downlink.flush()
+        except OSError:
+            pass
+        try:
+            self.proc.wait(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            self.proc.kill()
+            self.proc.wait()
+        self.cleanup()
+
     def incr_records(self, reporter, n):
         if reporter is not None:
             reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, n)
+
+
+class ChildPool:
+    """Idle reusable Pipes children (``hbmr.pipes.child.reuse``), keyed by
+    (executable, device, map|reduce): the Pipes analogue of the JvmManager's
+    JVM reuse (JvmManager.java:119-413).  A GPU binary that stays up keeps its
+    HIP context, device buffers and HBM-resident splits for the next task.
+    Idle children are closed after ``hbmr.pipes.child.idle.s`` seconds."""
+
+    def __init__(self, idle_s: float = 30.0):
+        self.idle_s = idle_s
+        self._idle: dict = {}
+        self._lock = threading.Lock()
+        self._reaper = None
+
+    def acquire(self, key):
+        import time
+        with self._lock:
+            lst = self._idle.get(key) or []
+            while lst:
+                app, _t = lst.pop()
+                if app.alive():
+                    return app
+                app.cleanup()
+        return None
+
+    def release(self, key, app, idle_s=None):
+        import time
+        if not app.alive():
+            app.cleanup()
+            return
+        with self._lock:
+            self._idle.setdefault(key, []).append((app, time.time()))
+            if idle_s is not None:
+                self.idle_s = idle_s
+            if self._reaper is None:
+                self._reaper = threading.Thread(target=self._reap, daemon=True,
+                                                name="pipes-child-reaper")
+                self._reaper.start()
+
+    def _reap(self):
+        import time
+        while True:
+            time.sleep(min(5.0, max(0.5, self.idle_s / 4)))
+            now = time.time()
+            stale = []
+            with self._lock:
+                for key, lst in list(self._idle.items()):
+                    keep = [(a, t) for a, t in lst if now - t < self.idle_s and a.alive()]
+                    stale += [a for a, t in lst if (a, t) not in keep]
+                    self._idle[key] = keep
+            for a in stale:
+                a.close_child()
+
+    def close_all(self):
+        with self._lock:
+            apps = [a for lst in self._idle.values() for a, _ in lst]
+            self._idle.clear()
+        for a in apps:
+            a.close_child()
+
+    def size(self):
+        with self._lock:
+            return sum(len(v) for v in self._idle.values())
+
+
+POOL = ChildPool()

@@ -159,10 +159,13 @@ class DownwardProtocol:
 class UplinkReader(threading.Thread):
     """Reads child → parent messages and dispatches them to ``handler``."""
 
-    def __init__(self, sock, handler):
+    def __init__(self, sock, handler, reuse=False):
         super().__init__(daemon=True, name="pipes-uplink")
         self.inp = sock.makefile("rb", buffering=BUFFER_SIZE)
         self.handler = handler
+        # a reused child runs task after task on this connection: DONE ends a
+        # task, not the stream, and each task installs its own handler
+        self.reuse = reuse
 
     def _bytes(self):
         n = read_vint(self.inp)
@@ -173,6 +176,7 @@ class UplinkReader(threading.Thread):
         try:
             while True:
                 cmd = read_vint(self.inp)
+                h = self.handler
                 if cmd == OUTPUT:
                     k = self._bytes()
                     v = self._bytes()
@@ -188,7 +192,8 @@ class UplinkReader(threading.Thread):
                     h.progress(struct.unpack(">f", self.inp.read(4))[0])
                 elif cmd == DONE:
                     h.done()
-                    return
+                    if not self.reuse:
+                        return
                 elif cmd == REGISTER_COUNTER:
                     cid = read_vint(self.inp)
                     grp = self._bytes().decode()

@@ -21,13 +21,16 @@ from ..mapred import counters as C
 from ..mapred.api import InputFormat, MapRunnable, Partitioner, RecordReader, Reducer
 from ..mapred.formats import FileSplit
 from ..utils.reflection import load_class, new_instance
-from .application import Application
+from .application import POOL, Application
 
 JAVA_RR = "hadoop.pipes.java.recordreader"
 JAVA_MAPPER = "hadoop.pipes.java.mapper"
 JAVA_REDUCER = "hadoop.pipes.java.reducer"
 JAVA_RW = "hadoop.pipes.java.recordwriter"
 JAVA_PARTITIONER = "hadoop.pipes.partitioner"
+# keep Pipes children alive between tasks (hbmr/pipes/application.py ChildPool)
+REUSE = "hbmr.pipes.child.reuse"
+IDLE = "hbmr.pipes.child.idle.s"
 
 
 def _work_dir(job, suffix):
@@ -63,10 +66,19 @@ class PipesMapRunner(MapRunnable):
         part = getattr(output, "partitioner", None)
         if isinstance(part, PipesPartitioner):
             partitioner = part
-        app = Application(job, output, reporter, job.get_map_output_key_class(),
-                          job.get_map_output_value_class(), self.executable(),
-                          run_on_gpu=self.run_on_gpu, gpu_device_id=self.device(),
-                          partitioner=partitioner, work_dir=_work_dir(job, "map"))
+        reuse = job.get_boolean(REUSE, False)
+        key = (self.executable(), self.device(), "map")
+        app = POOL.acquire(key) if reuse else None
+        if app is not None:
+            app.begin_task(job, output, reporter, job.get_map_output_key_class(),
+                           job.get_map_output_value_class(), partitioner)
+        else:
+            app = Application(job, output, reporter, job.get_map_output_key_class(),
+                              job.get_map_output_value_class(), self.executable(),
+                              run_on_gpu=self.run_on_gpu, gpu_device_id=self.device(),
+                              partitioner=partitioner, work_dir=_work_dir(job, "map"),
+                              reuse=reuse)
+        ok = False
         try:
             is_java_input = job.get_boolean(JAVA_RR, False)
             if is_java_input:
@@ -91,11 +103,15 @@ class PipesMapRunner(MapRunnable):
                 app.downlink.run_map(_split_bytes(reporter), job.get_num_reduce_tasks(), False)
                 app.downlink.flush()
             app.wait_for_finish()
+            ok = True
         except BaseException:
             app.abort()
             raise
         finally:
-            app.cleanup()
+            if ok and reuse:
+                POOL.release(key, app, job.get_float(IDLE, 30.0))
+            else:
+                app.cleanup()
 
 
 class PipesGPUMapRunner(PipesMapRunner):
@@ -118,9 +134,16 @@ class PipesReducer(Reducer):
     def _start(self, output, reporter):
         job = self.job
         exe = job.get_cpu_executable() or job.get_gpu_executable()
-        self.app = Application(job, output, reporter, job.get_output_key_class(),
-                               job.get_output_value_class(), exe,
-                               work_dir=_work_dir(job, "reduce"))
+        self.reuse = job.get_boolean(REUSE, False)
+        self.key = (exe, -1, "reduce")
+        self.app = POOL.acquire(self.key) if self.reuse else None
+        if self.app is not None:
+            self.app.begin_task(job, output, reporter, job.get_output_key_class(),
+                                job.get_output_value_class())
+        else:
+            self.app = Application(job, output, reporter, job.get_output_key_class(),
+                                   job.get_output_value_class(), exe,
+                                   work_dir=_work_dir(job, "reduce"), reuse=self.reuse)
         # piped output: the child's records come back up and the framework's
         # OutputFormat writes them; otherwise the child's own RecordWriter does
         piped_output = job.get_boolean(JAVA_RW, False)
@@ -140,14 +163,19 @@ class PipesReducer(Reducer):
         if self.app is None:
             # no input: still let the child run setup/teardown
             self._start(_NullCollector(), None)
+        ok = False
         try:
             self.app.downlink.end_of_input()
             self.app.wait_for_finish()
+            ok = True
         except BaseException:
             self.app.abort()
             raise
         finally:
-            self.app.cleanup()
+            if ok and self.reuse:
+                POOL.release(self.key, self.app, self.job.get_float(IDLE, 30.0))
+            else:
+                self.app.cleanup()
 
 
 class _NullCollector:

@@ -222,6 +222,8 @@ class TaskContextImpl : public MapContext, public ReduceContext {
           break;
         }
         case SET_JOB_CONF: {
+          // a reused child may get the next job's conf: start from scratch
+          conf = JobConfImpl();
           const int n = deserializeInt(*down);
           for (int i = 0; i + 1 < n; i += 2) {
             string k, v;
@@ -371,7 +373,36 @@ class TaskContextImpl : public MapContext, public ReduceContext {
     return false;
   }
 
+  // Child reuse (hbmr.pipes.child.reuse, the Pipes analogue of
+  // mapred.job.reuse.jvm.num.tasks): after DONE the child waits for the next
+  // RUN_MAP / RUN_REDUCE (optionally after a new SET_JOB_CONF) on the same
+  // connection instead of exiting, so a GPU binary keeps its HIP context and
+  // device buffers across tasks; CLOSE ends it.
   void run() {
+    while (true) {
+      runOne();
+      if (!hasTask || !conf.hasKey("hbmr.pipes.child.reuse") ||
+          !conf.getBoolean("hbmr.pipes.child.reuse"))
+        return;
+      resetTask();
+    }
+  }
+
+  void resetTask() {
+    hasTask = false;
+    closed = false;
+    pendingKey = false;
+    reader.reset();
+    sink.reset();
+    direct.reset();
+    combiner.reset();
+    partitioner.reset();
+    writer.reset();
+    mapper.reset();
+    reducer.reset();
+  }
+
+  void runOne() {
     waitForTask();
     if (done && !hasTask) {
       up->done();

@@ -67,3 +67,67 @@ def test_pipes_kmeans_gpu_binary_on_gpu_slots(tmp_path):
     ref = _split_job_centroids(3)
     # bf16 MFMA distances may flip exact near-ties; centroids agree closely
     assert (cen - ref).abs().max() < 1e-2
+
+
+def test_native_point_writer_and_reader_match_python_sequencefile(tmp_path):
+    from hbmr.io import nativeio
+    from hbmr.io import sequencefile as seqf
+    x = K.synthetic_points(9, 0, 3000, 12, 4, "cpu").numpy()
+    nativeio.write_points(tmp_path / "p.seq", x, first_id=100)
+    rows = []
+    with seqf.Reader(str(tmp_path / "p.seq")) as r:      # the Python reader reads it
+        while True:
+            raw = r.next_raw()
+            if raw is None:
+                break
+            rows.append((int.from_bytes(raw[0], "big"), raw[1]))
+    assert [k for k, _ in rows] == list(range(100, 3100))
+    import numpy as np
+    got = np.stack([np.frombuffer(v[4:], dtype=">f4") for _, v in rows]).astype(np.float32)
+    assert np.array_equal(got, x)
+    size = os.path.getsize(tmp_path / "p.seq")
+    # splits by byte range: every record exactly once (SequenceFileRecordReader rule)
+    parts = [nativeio.read_points(tmp_path / "p.seq", a, b - a, 12)
+             for a, b in [(0, size // 3), (size // 3, 2 * size // 3), (2 * size // 3, size)]]
+    assert np.array_equal(np.concatenate(parts), x)
+
+
+def _file_job_centroids(inp, iters, gpus=None):
+    conf = JobConf()
+    with LocalCluster(conf, num_trackers=1, gpus=gpus, cpu_slots=0 if gpus else 2) as cl:
+        drv = K.KMeansDriver(cl.submit_job, lambda rj: rj._impl.jip.result[0], conf=conf, k=KC,
+                             d=D, inp=inp, split_points=4000)
+        for _ in range(iters):
+            assert drv.step()["points"] == N
+        return drv.centroids()
+
+
+def test_kmeans_split_job_on_sequencefile_input_matches_synthetic(tmp_path):
+    # the file path (native reader → pinned host → device) sees the same bf16
+    # points as the synthetic generator, so the exact partials give equal centroids
+    KP.write_points(str(tmp_path / "pts"), N, D, seed=3, centers=KC, files=3)
+    assert torch.equal(_file_job_centroids(str(tmp_path / "pts"), 3), _split_job_centroids(3))
+
+
+@pytest.mark.gpu
+def test_gpu_kmeans_split_job_on_sequencefile_input(tmp_path):
+    KP.write_points(str(tmp_path / "pts"), N, D, seed=3, centers=KC, files=3)
+    got = _file_job_centroids(str(tmp_path / "pts"), 3, gpus=[[0]])
+    ref = _file_job_centroids(str(tmp_path / "pts"), 3)
+    assert (got - ref).abs().max() < 1e-2      # bf16 MFMA distances on the GPU
+
+
+@pytest.mark.gpu
+def test_gpu_pipes_binary_is_reused_and_keeps_splits_in_hbm(tmp_path):
+    from hbmr.pipes.application import POOL
+    KP.write_points(str(tmp_path / "pts"), N, D, seed=3, centers=KC, files=3)
+    init = K.initial_centroids(f"synthetic:{N}:3", KC, D)
+    with LocalCluster(JobConf(), num_trackers=1, gpus=[[0]], cpu_slots=0,
+                      gpu_slots_per_device=1) as cl:
+        drv = KP.KMeansPipesDriver(str(tmp_path / "work"), str(tmp_path / "pts"), KC, D, init,
+                                   cluster=cl, reduces=1)
+        drv.run(3)
+        assert POOL.size() >= 1             # the children wait for the next job
+    hits = [h["counters"].get("KMEANS", "GPU_SPLIT_CACHE_HITS") for h in drv.history]
+    assert hits[0] == 0 and hits[1] == 3 and hits[2] == 3
+    POOL.close_all()
