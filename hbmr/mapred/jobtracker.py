@@ -317,7 +317,14 @@ class JobInProgress:
         scheduling): for a GPU the split must be re-materialised either way."""
         if not self.pending_maps:
             return None
-        multi = len(self.jt.trackers) > 1
+        ntr = len(self.jt.trackers)
+        multi = ntr > 1
+
+        def avoid(tip):
+            # a TIP avoids trackers it failed on, unless it failed on all of them
+            # (JobInProgress.findNewMapTask: hasFailedOnMachine vs numUniqueHosts)
+            return multi and tracker.name in tip.failed_trackers and \
+                len(tip.failed_trackers) < ntr
         idx = self._index(tracker, on_gpu, device)
         for level in (0, 1, 2, 3):
             if level == 3 and not allow_nonlocal:
@@ -325,12 +332,12 @@ class JobInProgress:
             stack = idx[level]
             while stack:
                 tip = stack.pop()
-                if tip in self.pending_maps and not (multi and tracker.name in tip.failed_trackers):
+                if tip in self.pending_maps and not avoid(tip):
                     self._take(tip)
                     self._count_locality(level)
                     return tip, level
         for tip in self.pending_maps:
-            if multi and tracker.name in tip.failed_trackers:
+            if avoid(tip):
                 continue
             self._take(tip)
             self._count_locality(4)

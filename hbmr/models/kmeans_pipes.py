@@ -143,10 +143,17 @@ class KMeansPipesDriver:
         out = os.path.join(self.workdir, f"iter-{i:03d}")
         job = iteration_conf(self.base, self.inp, out, cen_file, self.k, self.d, self.cpubin,
                              self.gpubin, self.reduces, self.maps)
+        from ..utils.trace import TRACE
+        if TRACE.on:
+            TRACE.instant("kmeans_pipes.submit")
         rj = submitter.run_job(job, cluster=self.cluster, verbose=False)
+        if TRACE.on:
+            TRACE.instant("kmeans_pipes.job_done")
         if not rj.isSuccessful():
             raise RuntimeError(f"K-Means Pipes iteration {i} failed: {rj.getFailureInfo()}")
         new = read_centroids(out, self.centroids)
+        if TRACE.on:
+            TRACE.instant("kmeans_pipes.centroids_read")
         shift = float((new - self.centroids).norm(dim=1).max())
         self.centroids = new
         self.history.append({"iteration": i, "shift": shift, "counters": rj.getCounters()})

@@ -66,9 +66,12 @@ class PipesMapRunner(MapRunnable):
         part = getattr(output, "partitioner", None)
         if isinstance(part, PipesPartitioner):
             partitioner = part
+        from ..utils.trace import TRACE
         reuse = job.get_boolean(REUSE, False)
         key = (self.executable(), self.device(), "map")
         app = POOL.acquire(key) if reuse else None
+        if TRACE.on:
+            TRACE.instant("pipes.map.child", reused=app is not None)
         if app is not None:
             app.begin_task(job, output, reporter, job.get_map_output_key_class(),
                            job.get_map_output_value_class(), partitioner)
@@ -104,6 +107,8 @@ class PipesMapRunner(MapRunnable):
                 app.downlink.flush()
             app.wait_for_finish()
             ok = True
+            if TRACE.on:
+                TRACE.instant("pipes.map.done", records=app.handler.records)
         except BaseException:
             app.abort()
             raise
