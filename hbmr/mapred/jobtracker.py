@@ -344,6 +344,19 @@ class JobInProgress:
             return tip, 4
         return None
 
+    def locality_possible(self) -> bool:
+        """Does any split name a live tracker (by tracker name, host or rack)?
+        If not, waiting for a local slot (delay scheduling) cannot help."""
+        live = self.jt.trackers
+        key = len(live)
+        if getattr(self, "_loc_possible", None) is not None and self._loc_possible[0] == key:
+            return self._loc_possible[1]
+        names = set(live) | {t.status.host for t in live.values()}
+        ok = any(loc in names for tip in self.maps for loc in tip.locations()) or \
+            any(tip.split_key() for tip in self.maps)   # HBM-resident splits
+        self._loc_possible = (key, ok)
+        return ok
+
     def _count_locality(self, level):
         # JobInProgress.Counter DATA_LOCAL_MAPS / RACK_LOCAL_MAPS (+ hbmr's
         # HBM-resident level)

@@ -203,7 +203,8 @@ class HybridTaskScheduler(TaskScheduler):
                         key = (str(jip.job_id), tr.name, dev)
                         first = self._skips.get(key)
                         allow_nonlocal = self.policy == "stock" or (
-                            first is not None and now - first >= self.locality_wait)
+                            first is not None and now - first >= self.locality_wait) or \
+                            not jip.locality_possible()
                         got = jip.obtain_map(tr, True, dev, allow_nonlocal=allow_nonlocal)
                         if got is None:
                             if first is None:
