@@ -297,7 +297,9 @@ class KMeansSplitJob(SplitJob):
             return None
         from ..io import nativeio
         p = spec.params
-        n = nativeio.count_points(p["path"], p["start"], p["length"])
+        # one pass: size for the most records the byte range can hold (a record
+        # is >= 4+4+8+4+4d bytes), decode straight into pinned memory
+        n = p["length"] // (20 + 4 * self.d) + 2
         host = torch.empty(n, self.d, dtype=torch.float32,
                            pin_memory=torch.cuda.is_available())
         got = nativeio.read_points_into(p["path"], p["start"], p["length"], host.data_ptr(),
@@ -326,7 +328,7 @@ class KMeansSplitJob(SplitJob):
         decodes the records straight into pinned host memory, then one
         asynchronous H2D copy on the current (slot) stream."""
         from ..io import nativeio
-        n = nativeio.count_points(p["path"], p["start"], p["length"])
+        n = p["length"] // (20 + 4 * self.d) + 2
         dev = torch.device(device)
         host = torch.empty(n, self.d, dtype=torch.float32, pin_memory=dev.type == "cuda")
         got = nativeio.read_points_into(p["path"], p["start"], p["length"], host.data_ptr(),
