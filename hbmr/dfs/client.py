@@ -22,6 +22,7 @@ import socket
 import threading
 import uuid
 
+from ..fs import STATS
 from .datanode import ChecksumError, resolve_datanode
 from .namenode import norm
 
@@ -87,6 +88,7 @@ class DFSOutputStream(io.RawIOBase):
         return True
 
     def write(self, b):
+        STATS.add("hdfs", written=len(b))
         self.buf += b
         while len(self.buf) >= self.block_size:
             self._flush_block(bytes(self.buf[:self.block_size]))
@@ -182,6 +184,7 @@ class DFSInputStream(io.RawIOBase):
                 data = self._read_at(b, off, want)
                 buf[:len(data)] = data
                 self.pos += len(data)
+                STATS.add("hdfs", read=len(data))
                 return len(data)
         return 0
 

@@ -150,7 +150,16 @@ class SplitSleepJob(SplitJob):
     def map_cpu(self, ctx, data):
         frac = data[1] if isinstance(data, tuple) else 1.0   # a sampled probe sleeps pro rata
         if self.map_ms > 0:
-            time.sleep(self.map_ms * frac / 1000.0)
+            # sleep in slices so a killed attempt (preemption) frees its slot
+            kill = getattr(ctx, "kill_event", None)
+            end = time.time() + self.map_ms * frac / 1000.0
+            while True:
+                left = end - time.time()
+                if left <= 0:
+                    break
+                if kill is not None and kill.is_set():
+                    raise RuntimeError("killed")
+                time.sleep(min(left, 0.01))
         return 1
 
     def map_gpu(self, ctx, data):

@@ -16,6 +16,43 @@ from dataclasses import dataclass
 DEFAULT_BLOCK_SIZE = 64 * 1024 * 1024  # dfs.block.size default (hdfs-default.xml:259-260)
 
 
+class Statistics:
+    """Per-thread bytes read/written by scheme (FileSystem.Statistics,
+    hadoop-1.0.3/src/core/org/apache/hadoop/fs/FileSystem.java): a task running
+    on a thread snapshots them around its run to fill the FileSystemCounters
+    (HDFS_BYTES_READ, FILE_BYTES_WRITTEN, ...)."""
+
+    def __init__(self):
+        import threading
+        self._tl = threading.local()
+
+    def _d(self):
+        d = getattr(self._tl, "d", None)
+        if d is None:
+            d = self._tl.d = {}
+        return d
+
+    def add(self, scheme: str, read: int = 0, written: int = 0):
+        d = self._d()
+        r, w = d.get(scheme, (0, 0))
+        d[scheme] = (r + read, w + written)
+
+    def snapshot(self) -> dict:
+        return dict(self._d())
+
+    @staticmethod
+    def delta(before: dict, after: dict) -> dict:
+        out = {}
+        for k, (r, w) in after.items():
+            r0, w0 = before.get(k, (0, 0))
+            if r - r0 or w - w0:
+                out[k] = (r - r0, w - w0)
+        return out
+
+
+STATS = Statistics()
+
+
 def strip_scheme(path) -> str:
     p = str(path)
     if p.startswith("file://"):

@@ -46,6 +46,7 @@ def run_split_cpu_map(host, run):
         rep = TaskReporter()
         run.task = SplitTaskShim(rep, run.kill)
         ctx = TaskContext(host, js, spec, rep, device="cpu")
+        ctx.kill_event = run.kill          # cooperative kill (preemption, speculation)
         sspec = SplitSpec.from_dict(spec.split)
         if spec.profile_fraction:
             # sampled profiling probe: time the CPU map on a slice; the output is

@@ -369,3 +369,133 @@ class Reader:
 def createWriter(path, key_class, value_class, compression=NONE, codec=None, metadata=None,  # noqa: N802
                  **kw):
     return Writer(path, key_class, value_class, compression, codec, metadata, **kw)
+
+
+class Sorter:
+    """SequenceFile.Sorter (hadoop-1.0.3/src/core/org/apache/hadoop/io/
+    SequenceFile.java:2269): sort the records of SequenceFiles by key into one
+    SequenceFile, or merge already-sorted ones.
+
+    ``sort`` reads the inputs in order, cuts them into runs of at most
+    ``io.sort.mb`` (``hbmr.io.sort.bytes``) raw bytes, sorts each run in memory
+    (stable, by the key type's raw comparator — ``key_class.raw_sort_key`` or a
+    given ``comparator`` over raw key bytes) and writes it as a temporary
+    SequenceFile; ``merge`` combines sorted files ``io.sort.factor`` at a time
+    (multi-pass) with a streaming k-way merge whose ties go to the earlier
+    input, so equal keys keep their input order.  Output compression defaults
+    to NONE (``compression``/``codec`` as for :class:`Writer`)."""
+
+    def __init__(self, key_class, value_class, conf=None, comparator=None,
+                 compression: str = NONE, codec=None, tmp_dir=None):
+        self.kcls, self.vcls = key_class, value_class
+        get = (lambda k, d: conf.get_int(k, d)) if conf is not None else (lambda k, d: d)
+        self.memory = get("hbmr.io.sort.bytes", get("io.sort.mb", 100) << 20)
+        self.factor = max(2, get("io.sort.factor", 10))
+        self.sort_key = comparator or key_class.raw_sort_key
+        self.compression, self.codec = compression, codec
+        self.tmp_dir = tmp_dir
+        self.runs_written = 0
+        self.merge_passes = 0
+
+    def _writer(self, path):
+        return Writer(path, self.kcls, self.vcls, self.compression, self.codec)
+
+    def _tmp(self, out_path, i):
+        d = self.tmp_dir or (str(out_path) + ".sort-tmp")
+        os.makedirs(d, exist_ok=True)
+        return os.path.join(d, f"run-{i:05d}.seq")
+
+    @staticmethod
+    def _records(path):
+        with Reader(path) as r:
+            while True:
+                raw = r.next_raw()
+                if raw is None:
+                    return
+                yield raw
+
+    def sort(self, in_paths, out_path, delete_input=False) -> int:
+        """Sort the records of ``in_paths`` into ``out_path``; returns the count."""
+        if isinstance(in_paths, (str, os.PathLike)):
+            in_paths = [in_paths]
+        runs, buf, size, total = [], [], 0, 0
+        sk = self.sort_key
+
+        def flush():
+            nonlocal buf, size
+            if not buf and runs:
+                return
+            buf.sort(key=lambda r: sk(r[0]))          # stable
+            path = self._tmp(out_path, len(runs))
+            with self._writer(path) as w:
+                for kb, vb in buf:
+                    w.append_raw(kb, vb)
+            runs.append(path)
+            self.runs_written += 1
+            buf, size = [], 0
+        for p in in_paths:
+            for kb, vb in self._records(str(p)):
+                buf.append((kb, vb))
+                size += len(kb) + len(vb) + 16
+                total += 1
+                if size >= self.memory:
+                    flush()
+        flush()
+        if len(runs) == 1:
+            os.replace(runs[0], str(out_path))
+        else:
+            self.merge(runs, out_path, delete_input=True)
+        tmp = self.tmp_dir or (str(out_path) + ".sort-tmp")
+        if os.path.isdir(tmp) and not os.listdir(tmp):
+            os.rmdir(tmp)
+        if delete_input:
+            for p in in_paths:
+                os.remove(str(p))
+        return total
+
+    def _merge_iter(self, paths):
+        import heapq
+        sk = self.sort_key
+
+        def deco(i, it):
+            for j, (kb, vb) in enumerate(it):
+                yield sk(kb), i, j, kb, vb
+        for _k, _i, _j, kb, vb in heapq.merge(*[deco(i, self._records(str(p)))
+                                                for i, p in enumerate(paths)]):
+            yield kb, vb
+
+    def merge(self, in_paths, out_path, delete_input=False) -> int:
+        """Merge sorted ``in_paths`` into ``out_path`` (multi-pass at
+        ``io.sort.factor``); returns the number of records."""
+        paths = [str(p) for p in in_paths]
+        owned: set = set()
+        gen = 0
+        while len(paths) > self.factor:
+            nxt = []
+            for i in range(0, len(paths), self.factor):
+                grp = paths[i:i + self.factor]
+                if len(grp) == 1:
+                    nxt.append(grp[0])
+                    continue
+                tmp = self._tmp(out_path, 100000 + gen)
+                gen += 1
+                with self._writer(tmp) as w:
+                    for kb, vb in self._merge_iter(grp):
+                        w.append_raw(kb, vb)
+                for g in grp:
+                    if g in owned or delete_input:
+                        os.remove(g)
+                owned.add(tmp)
+                nxt.append(tmp)
+            paths = nxt
+            self.merge_passes += 1
+        n = 0
+        with self._writer(str(out_path)) as w:
+            for kb, vb in self._merge_iter(paths):
+                w.append_raw(kb, vb)
+                n += 1
+        self.merge_passes += 1
+        for g in paths:
+            if g in owned or delete_input:
+                os.remove(g)
+        return n

@@ -84,7 +84,7 @@ class TrackerInfo:
 class Attempt:
     __slots__ = ("aid", "tip", "tracker", "run_on_gpu", "device", "state", "progress",
                  "start", "finish", "counters", "output", "diagnostic", "speculative",
-                 "device_time", "_released", "profile_only", "profile_fraction")
+                 "device_time", "_released", "profile_only", "profile_fraction", "slots")
 
     def __init__(self, aid, tip, tracker, run_on_gpu, device, speculative=False):
         self.aid = aid
@@ -102,6 +102,7 @@ class Attempt:
         self.speculative = speculative
         self.device_time = 0.0
         self._released = False
+        self.slots = 1              # CPU / reduce slots held (memory matching)
         self.profile_only = False   # a CPU profiling probe left running after its TIP won
         self.profile_fraction = 0.0  # >0: sampled probe, timed on this fraction of a split
 
@@ -655,8 +656,12 @@ class JobTracker:
         self.job_tokens.add_job(jid)
         self._persist_job(jid, conf)
         jip = JobInProgress(self, jid, conf)
+        too_big = self._memory_violation(conf)
         with self.lock:
             self.jobs[str(jid)] = jip
+            if too_big:
+                self._finish_job(jip, FAILED, too_big)
+                return RunningJob(jid, _JTJobHandle(jip), conf)
             self.history.log("JOB_SUBMITTED", job=str(jid), name=conf.get_job_name(),
                              user=conf.get_user())
             try:
@@ -672,6 +677,17 @@ class JobTracker:
         for cb in self.listeners:
             cb("submitted", jip)
         return RunningJob(jid, _JTJobHandle(jip), conf)
+
+    def _memory_violation(self, conf):
+        """JobTracker.checkMemoryRequirements: a job asking for more memory per
+        task than ``mapred.cluster.max.{map,reduce}.memory.mb`` is rejected."""
+        for kind in ("map", "reduce"):
+            mx = self.conf.get_int(f"mapred.cluster.max.{kind}.memory.mb", -1)
+            need = conf.get_int(f"mapred.job.{kind}.memory.mb", -1)
+            if mx > 0 and need > mx:
+                return (f"job's {kind} memory {need} MB exceeds the cluster maximum "
+                        f"mapred.cluster.max.{kind}.memory.mb = {mx} MB")
+        return None
 
     def get_job(self, job_id) -> RunningJob | None:
         """JobClient.getJob: a handle on a known (e.g. recovered) job."""
@@ -912,9 +928,9 @@ class JobTracker:
                 if a.run_on_gpu:
                     tr.running_gpu[a.device] = max(0, tr.running_gpu.get(a.device, 1) - 1)
                 else:
-                    tr.running_cpu = max(0, tr.running_cpu - 1)
+                    tr.running_cpu = max(0, tr.running_cpu - a.slots)
             else:
-                tr.running_reduce = max(0, tr.running_reduce - 1)
+                tr.running_reduce = max(0, tr.running_reduce - a.slots)
 
     def _attempt_succeeded(self, a: Attempt):
         tip = a.tip
@@ -1100,6 +1116,22 @@ class JobTracker:
         self._update_progress(jip)
         self._kick()
 
+    def preempt_attempt(self, a: Attempt, why="preempted"):
+        """Kill a running attempt to give its slot to another pool (fair-share
+        preemption): KILLED, not FAILED — its TIP goes back to pending without
+        counting a failure (FairScheduler.preemptTasks, JobInProgress
+        .killTask(..., shouldFail=false))."""
+        if a.state in P.TERMINAL:
+            return
+        t = self.trackers.get(a.tracker)
+        if t is not None:
+            t.kills.add(a.aid)
+        jip = a.tip.job
+        jip.counters.incr(C.JOB_GROUP, "NUM_PREEMPTED_TASKS")
+        self.history.log("TASK_PREEMPTED", attempt=a.aid, tracker=a.tracker, why=why)
+        self._attempt_failed(a, why, killed=True)
+        self._kick()
+
     def _outputs_lost(self, tr: TrackerInfo, aids):
         """Map outputs held by a tracker's GPU worker are gone (the worker died):
         re-execute those maps if their job still needs them (the per-attempt
@@ -1186,10 +1218,11 @@ class JobTracker:
 
     # -- launching (called by the scheduler under the lock) -------------------------------
     def launch(self, tr: TrackerInfo, tip: TaskInProgress, on_gpu=False, device=-1,
-               speculative=False, extra=None, profile_fraction=0.0):
+               speculative=False, extra=None, profile_fraction=0.0, slots=1):
         jip = tip.job
         aid = tip.new_attempt_id()
         a = Attempt(str(aid), tip, tr.name, on_gpu, device, speculative)
+        a.slots = max(1, slots) if not on_gpu else 1
         if profile_fraction:
             # a sampled CPU probe rides on a TIP without being one of its attempts:
             # the TIP stays pending for real execution
@@ -1207,7 +1240,7 @@ class JobTracker:
                 tr.running_gpu[device] = tr.running_gpu.get(device, 0) + 1
                 jip.running_gpu += 1
             else:
-                tr.running_cpu += 1
+                tr.running_cpu += a.slots
                 jip.running_cpu += 1
             self.cost_model.task_started(jip.signature, a.aid, on_gpu, a.start)
             if not profile_fraction:
@@ -1215,7 +1248,7 @@ class JobTracker:
         else:
             if not jip.t_first_reduce:
                 jip.t_first_reduce = a.start
-            tr.running_reduce += 1
+            tr.running_reduce += a.slots
             jip.counters.incr(C.JOB_GROUP, C.TOTAL_LAUNCHED_REDUCES)
         spec = P.TaskSpec(attempt_id=a.aid, job_id=str(jip.job_id), is_map=tip.is_map,
                           partition=tip.partition, run_on_gpu=on_gpu, gpu_device_id=device,

@@ -17,16 +17,36 @@ min shares first, then by weight, never above a pool's demand; inside a pool
 jobs split equally (fair) or in submit order (fifo).  The most starved job
 (running / share) is served first.
 
+Preemption (FairScheduler.preemptTasksIfNecessary, FairScheduler.java:837),
+with ``mapred.fairscheduler.preemption`` = true: a pool below its min share for
+``hbmr.fair.pool.<p>.minSharePreemptionTimeout`` seconds (default 60), or below
+half its fair share for ``mapred.fairscheduler.fairSharePreemptionTimeout``
+seconds (default 600), gets slots back by killing the most recently launched
+attempts of pools above their fair share (never taking a pool below it).
+Preempted attempts are KILLED, not FAILED: their TIPs go back to pending.
+
 CapacityScheduler (contrib/capacity-scheduler): queues
 ``mapred.queue.names`` with ``mapred.capacity-scheduler.queue.<q>.capacity``
-percent; a job's queue is ``mapred.job.queue.name``.  Unused capacity flows to
-queues with demand; inside a queue jobs run in priority/submit order.
+percent and an optional hard ``.maximum-capacity``; a job's queue is
+``mapred.job.queue.name``.  Unused capacity flows to queues with demand.
+Inside a queue jobs run in priority/submit order, and each user is capped at
+max(queue share × ``.minimum-user-limit-percent`` / 100, queue share / active
+users) (CapacitySchedulerQueue.java:724 user limits).  Memory matching
+(CapacityTaskScheduler.java:315-340): with ``mapred.cluster.map.memory.mb`` /
+``mapred.cluster.reduce.memory.mb`` set, a job asking for
+``mapred.job.map.memory.mb`` / ``mapred.job.reduce.memory.mb`` above the slot
+size occupies ceil(job / slot) slots per task, and a job larger than
+``mapred.cluster.max.map.memory.mb`` is rejected at submission.
 """
 from __future__ import annotations
 
+import logging
 import math
+import time
 
 from .hybrid import HybridTaskScheduler, _prio
+
+log = logging.getLogger("hbmr.scheduler.fair")
 
 KINDS = ("gpu", "cpu", "reduce")
 
@@ -107,6 +127,16 @@ class _ShareScheduler(HybridTaskScheduler):
 
 
 class FairScheduler(_ShareScheduler):
+    def __init__(self, jt, conf):
+        super().__init__(jt, conf)
+        self.preemption = conf.get_boolean("mapred.fairscheduler.preemption", False)
+        self.fair_timeout = conf.get_float("mapred.fairscheduler.fairSharePreemptionTimeout",
+                                           600.0)
+        self.preempted = 0
+        self._below_min: dict = {}    # (pool, kind) -> since
+        self._below_fair: dict = {}
+        self.pool_shares: dict = {}   # kind -> {pool: share}
+
     def pool_of(self, jip):
         c = jip.conf
         p = c.get("mapred.fairscheduler.pool")
@@ -129,6 +159,7 @@ class FairScheduler(_ShareScheduler):
         minkey = {"gpu": "minGpuMaps", "cpu": "minMaps", "reduce": "minReduces"}[kind]
         mins = [float(self._pool_conf(p, minkey, 0)) for p in names]
         pshare = water_fill(total, demands, weights, mins)
+        self.pool_shares[kind] = {p: (ps, mn, pools[p]) for p, ps, mn in zip(names, pshare, mins)}
         for p, ps in zip(names, pshare):
             js = sorted(pools[p], key=lambda j: (_prio(j.priority), j.submit_time))
             if self._pool_conf(p, "mode", "fair") == "fifo":
@@ -144,6 +175,15 @@ class FairScheduler(_ShareScheduler):
 
 
 class CapacityScheduler(_ShareScheduler):
+    def slots_per_task(self, jip, kind):
+        """Memory-based slot matching: slots a task of ``jip`` occupies."""
+        kk = "reduce" if kind == "reduce" else "map"
+        slot = self.conf.get_int(f"mapred.cluster.{kk}.memory.mb", -1)
+        need = jip.conf.get_int(f"mapred.job.{kk}.memory.mb", -1)
+        if slot <= 0 or need <= 0:
+            return 1
+        return max(1, math.ceil(need / slot))
+
     def queue_of(self, jip):
         return jip.conf.get("mapred.job.queue.name", "default")
 
@@ -154,15 +194,98 @@ class CapacityScheduler(_ShareScheduler):
         for j in self.jobs:
             queues.setdefault(self.queue_of(j), []).append(j)
         names = list(queues)
-        caps = [self.conf.get_float(f"mapred.capacity-scheduler.queue.{q}.capacity",
-                                    100.0 / max(1, len(names))) for q in names]
-        demands = [sum(self.demand[j][kind] for j in queues[q]) for q in names]
+        pre = "mapred.capacity-scheduler.queue"
+        caps = [self.conf.get_float(f"{pre}.{q}.capacity", 100.0 / max(1, len(names)))
+                for q in names]
+        maxcaps = [self.conf.get_float(f"{pre}.{q}.maximum-capacity", -1.0) for q in names]
+        # demand in slots (high-memory tasks take several), capped by max capacity
+        demands = []
+        for q, mx in zip(names, maxcaps):
+            d = sum(self.demand[j][kind] * self.slots_per_task(j, kind) for j in queues[q])
+            if mx > 0:
+                d = min(d, total * mx / 100.0)
+            demands.append(d)
         guaranteed = [total * c / 100.0 for c in caps]
         # guaranteed capacity first, then the unused remainder ∝ capacity
         qshare = water_fill(total, demands, [max(c, 1e-6) for c in caps], guaranteed)
         for q, qs in zip(names, qshare):
+            ul = self.conf.get_float(f"{pre}.{q}.minimum-user-limit-percent", 100.0)
+            users: dict = {}
+            for j in queues[q]:
+                users.setdefault(j.conf.get_user(), []).append(j)
+            active = [u for u, js in users.items() if any(self.demand[j][kind] for j in js)]
+            user_cap = max(qs * ul / 100.0, qs / max(1, len(active)))
+            used: dict = {}
             left = qs
             for j in sorted(queues[q], key=lambda j: (_prio(j.priority), j.submit_time)):
-                s = min(left, self.demand[j][kind])
-                self.shares[j][kind] = s
+                u = j.conf.get_user()
+                spt = self.slots_per_task(j, kind)
+                room = min(left, user_cap - used.get(u, 0.0))
+                s = max(0.0, min(room, self.demand[j][kind] * spt))
+                self.shares[j][kind] = s / spt      # tasks
+                used[u] = used.get(u, 0.0) + s
                 left -= s
+
+
+def _fair_begin_round(self, tr, total_cpu, total_gpu):
+    _ShareScheduler.begin_round(self, tr, total_cpu, total_gpu)
+    if self.preemption:
+        self.preempt_if_necessary(time.time())
+
+
+def _preempt_if_necessary(self, now):
+    """FairScheduler.preemptTasksIfNecessary: per slot kind, pools starved past
+    their timeout take slots back from pools above their fair share."""
+    for kind, pools in self.pool_shares.items():
+        running = {p: sum(self.running[j][kind] for j in jobs)
+                   for p, (_sh, _mn, jobs) in pools.items()}
+        want = 0
+        for p, (share, mn, _jobs) in pools.items():
+            tmin = float(self._pool_conf(p, "minSharePreemptionTimeout", 60.0))
+            key = (p, kind)
+            target = 0
+            if running[p] < min(mn, share) - 1e-9:
+                since = self._below_min.setdefault(key, now)
+                if now - since >= tmin:
+                    target = max(target, math.ceil(min(mn, share) - running[p]))
+            else:
+                self._below_min.pop(key, None)
+            if running[p] < share / 2 - 1e-9:
+                since = self._below_fair.setdefault(key, now)
+                if now - since >= self.fair_timeout:
+                    target = max(target, math.ceil(share - running[p]))
+            else:
+                self._below_fair.pop(key, None)
+            want += target
+        if want > 0:
+            self._preempt(kind, pools, running, want, now)
+
+
+def _preempt(self, kind, pools, running, want, now):
+    # victims: attempts of pools above their fair share, newest first, without
+    # taking any pool below its share
+    cands = []
+    for p, (share, _mn, jobs) in pools.items():
+        over = running[p] - math.ceil(share - 1e-9)
+        if over <= 0:
+            continue
+        mine = []
+        for j in jobs:
+            tips = j.reduces if kind == "reduce" else j.maps
+            for tip in tips:
+                for a in tip.running_attempts():
+                    if kind == "reduce" or (a.run_on_gpu == (kind == "gpu")):
+                        mine.append(a)
+        mine.sort(key=lambda a: -a.start)
+        cands += mine[:over]
+    cands.sort(key=lambda a: -a.start)
+    for a in cands[:want]:
+        self._below_min.clear()
+        self._below_fair.clear()
+        self.jt.preempt_attempt(a, f"preempted by the fair scheduler ({kind} slots)")
+        self.preempted += 1
+
+
+FairScheduler.begin_round = _fair_begin_round
+FairScheduler.preempt_if_necessary = _preempt_if_necessary
+FairScheduler._preempt = _preempt

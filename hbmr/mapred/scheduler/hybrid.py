@@ -142,13 +142,15 @@ class HybridTaskScheduler(TaskScheduler):
                     if jip.collective_reduce:
                         if tip.pinned_tracker != tr.name:
                             continue
-                    elif reduce_free <= 0 or n_red >= self.max_reduces_per_hb or \
+                    elif reduce_free < self.slots_per_task(jip, "reduce") or \
+                            n_red >= self.max_reduces_per_hb or \
                             n_red >= self.job_limit(jip, "reduce"):
                         break
                     extra = {"map_outputs": jt.reduce_inputs(jip, tr.name)}
-                    actions.append(jt.launch(tr, tip, extra=extra))
+                    spt = 1 if jip.collective_reduce else self.slots_per_task(jip, "reduce")
+                    actions.append(jt.launch(tr, tip, extra=extra, slots=spt))
                     n_red += 1
-                    reduce_free -= 1
+                    reduce_free -= spt
             if not jip.pending_maps:
                 # ---- speculative backups of stragglers onto idle GPUs
                 if jip.speculative and jip.gpu_capable and not jip.maps_complete():
@@ -170,7 +172,8 @@ class HybridTaskScheduler(TaskScheduler):
             if cpu_free > 0 and jip.pending_maps:
                 allowed = min(self._cpu_allowed(jip, total_cpu, total_gpu, now),
                               self.job_limit(jip, "cpu"))
-                while cpu_free > 0 and allowed > 0 and jip.pending_maps:
+                spt = self.slots_per_task(jip, "cpu")
+                while cpu_free >= spt and allowed > 0 and jip.pending_maps:
                     if budget <= 0:
                         tr.more = True
                         break
@@ -178,8 +181,8 @@ class HybridTaskScheduler(TaskScheduler):
                     if got is None:
                         break
                     tip, _ = got
-                    actions.append(jt.launch(tr, tip, on_gpu=False))
-                    cpu_free -= 1
+                    actions.append(jt.launch(tr, tip, on_gpu=False, slots=spt))
+                    cpu_free -= spt
                     allowed -= 1
                     reserve -= 1
                     budget -= 1
@@ -267,6 +270,10 @@ class HybridTaskScheduler(TaskScheduler):
 
     def job_order(self, tr):
         return sorted(self.jt.job_queue, key=lambda j: (_prio(j.priority), j.submit_time))
+
+    def slots_per_task(self, jip, kind) -> int:
+        """Slots one task of ``jip`` occupies (memory matching; 1 by default)."""
+        return 1
 
     def job_limit(self, jip, kind) -> int:
         """Most new tasks of ``kind`` (gpu/cpu/reduce) this job may take now."""

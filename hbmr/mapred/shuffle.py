@@ -153,9 +153,11 @@ class ShuffleMerger:
 
     @staticmethod
     def _write_body(path, body):
+        from ..fs import STATS
         with open(path, "wb") as f:
             f.write(body)
             f.write(struct.pack(">I", zlib.crc32(body) & 0xFFFFFFFF))
+        STATS.add("file", written=len(body) + 4)
 
     def _records(self, run):
         if run.data is not None:

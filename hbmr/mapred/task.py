@@ -373,6 +373,7 @@ class MapOutputBuffer(OutputCollector):
                 rec.put(p, *w.close())
         rec.write(path + ".index")
         self.spills.append((path, rec))
+        _fs_written(path)
         self.reporter.incrCounter(C.TASK_GROUP, C.SPILLED_RECORDS, spilled)
 
     # -- native path ------------------------------------------------------------------------
@@ -424,6 +425,7 @@ class MapOutputBuffer(OutputCollector):
                 rec.put(p, *sortbuf.write_segment(f, body, self.codec))
         rec.write(path + ".index")
         self.spills.append((path, rec))
+        _fs_written(path)
         self.reporter.incrCounter(C.TASK_GROUP, C.SPILLED_RECORDS, spilled)
 
     def _merge_parts_native(self, final):
@@ -450,6 +452,7 @@ class MapOutputBuffer(OutputCollector):
                 spilled += nrec
                 rec_out.put(p, *sortbuf.write_segment(f, body, self.codec))
         rec_out.write(final + ".index")
+        _fs_written(final)
         for path, _ in self.spills:
             for q in (path, path + ".index"):
                 if os.path.exists(q):
@@ -498,11 +501,31 @@ class MapOutputBuffer(OutputCollector):
                 spilled += n
                 rec_out.put(p, *w.close())
         rec_out.write(final + ".index")
+        _fs_written(final)
         for path, _ in self.spills:
             for q in (path, path + ".index"):
                 if os.path.exists(q):
                     os.remove(q)
         self.reporter.incrCounter(C.TASK_GROUP, C.SPILLED_RECORDS, spilled)
+
+
+def _fs_written(path):
+    """Local bytes a task wrote (FILE_BYTES_WRITTEN via FileSystem statistics)."""
+    from ..fs import STATS
+    try:
+        STATS.add("file", written=os.path.getsize(path))
+    except OSError:
+        pass
+
+
+def _fs_counters(rep, before):
+    """FileSystemCounters of a task from the thread's FileSystem statistics."""
+    from ..fs import STATS
+    for scheme, (r, w) in STATS.delta(before, STATS.snapshot()).items():
+        if r:
+            rep.incrCounter(C.FS_GROUP, f"{scheme.upper()}_BYTES_READ", r)
+        if w:
+            rep.incrCounter(C.FS_GROUP, f"{scheme.upper()}_BYTES_WRITTEN", w)
 
 
 def merge_segments(segments, factor: int = 10):
@@ -536,6 +559,14 @@ class MapTask(Task):
         self.output_file = None  # (path to file.out) when R > 0
 
     def run(self, local_dir: str):
+        from ..fs import STATS
+        fs0 = STATS.snapshot()
+        try:
+            return self._run(local_dir)
+        finally:
+            _fs_counters(self.reporter, fs0)
+
+    def _run(self, local_dir: str):
         self.start_time = time.time()
         job = self._task_conf()
         self.local_dir = local_dir
@@ -680,6 +711,14 @@ class ReduceTask(Task):
                 delay = 0.001
 
     def run(self, local_dir: str):
+        from ..fs import STATS
+        fs0 = STATS.snapshot()
+        try:
+            return self._run(local_dir)
+        finally:
+            _fs_counters(self.reporter, fs0)
+
+    def _run(self, local_dir: str):
         self.start_time = time.time()
         job = self._task_conf()
         self.local_dir = local_dir

@@ -42,7 +42,8 @@ def attempt_records(jip):
                    "gpu": bool(a.run_on_gpu), "device": a.device, "start": a.start,
                    "finish": a.finish, "device_time": a.device_time,
                    "speculative": bool(a.speculative), "successful": tip.successful is a,
-                   "diagnostic": (a.diagnostic or "")[:500]}
+                   "diagnostic": (a.diagnostic or "")[:500],
+                   "counters": a.counters if isinstance(a.counters, dict) else {}}
 
 
 def write_job_history(jip, directory) -> str:
@@ -144,6 +145,7 @@ def diagnose(job, attempts) -> list:
     if fails:
         out.append({"rule": "failures", "severity": "high",
                     "text": f"{len(fails)} failed attempts, e.g. {fails[0]['diagnostic'][:160]}"})
+    out += vaidya_rules(job, attempts)
     reds = [a for a in attempts if a["successful"] and a["type"] == "REDUCE"]
     if job and job.get("finish") and reds:
         tail = job["finish"] - end
@@ -151,4 +153,111 @@ def diagnose(job, attempts) -> list:
         if span > 0 and tail / span > 0.5:
             out.append({"rule": "reduce-tail", "severity": "medium",
                         "text": f"reduce phase is {100 * tail / span:.0f}% of the makespan"})
+    return out
+
+
+# ---------------------------------------------------------------------------- Vaidya
+_TASK = "org.apache.hadoop.mapred.Task$Counter"
+_JIP = "org.apache.hadoop.mapred.JobInProgress$Counter"
+_FS = "FileSystemCounters"
+
+
+def _ctr(counters, group, name):
+    return int(((counters or {}).get(group) or {}).get(name, 0) or 0)
+
+
+def _severity(impact, threshold):
+    return "high" if impact >= max(threshold, 0.5) else ("medium" if impact >= threshold
+                                                         else "info")
+
+
+def vaidya_rules(job, attempts, thresholds=None) -> list:
+    """The reference's post-execution diagnosis tests (contrib/vaidya/.../
+    postexdiagnosis/tests/*.java), same inputs and impact formulas:
+
+    * MapSideDiskSpill: (local bytes written by maps − map output bytes) /
+      map output bytes, normalised by 3.0 (a map-only job: all of it);
+    * BalancedReducePartitioning: 1 − (reducers holding 90 % of the reduce
+      input records) / reducers;
+    * MapsReExecutionImpact / ReducesReExecutionImpact: (launched − total) /
+      total tasks;
+    * ReadingHDFSFilesAsSideEffect: HDFS bytes read / map input bytes,
+      normalised by 2.0.
+
+    Each finding carries the rule name, its impact in [0, 1] and the
+    reference's prescription; impacts over the threshold (0.2 by default,
+    ``thresholds[rule]``) are medium/high."""
+    th = {"MapSideDiskSpill": 0.3, "BalancedReducePartitioning": 0.4,
+          "MapsReExecutionImpact": 0.4, "ReducesReExecutionImpact": 0.4,
+          "ReadingHDFSFilesAsSideEffect": 0.3}
+    th.update(thresholds or {})
+    if not job:
+        return []
+    jc = job.get("counters") or {}
+    out = []
+    maps = [a for a in attempts if a["type"] == "MAP"]
+    reds_ok = [a for a in attempts if a["type"] == "REDUCE" and a["successful"]]
+    total_maps = job.get("maps", 0)
+    total_reds = job.get("reduces", 0)
+
+    def add(rule, impact, text, prescription):
+        out.append({"rule": rule, "impact": round(float(impact), 4),
+                    "severity": _severity(impact, th[rule]), "text": text,
+                    "prescription": prescription})
+
+    # MapSideDiskSpill
+    written = sum(_ctr(a.get("counters"), _FS, "FILE_BYTES_WRITTEN") for a in maps
+                  if a["successful"])
+    mob = _ctr(jc, _TASK, "MAP_OUTPUT_BYTES")
+    if mob > 0:
+        imp = (written - mob) / mob if total_reds > 0 else written / mob
+        imp = 1.0 if imp > 3.0 else max(0.0, imp) / 3.0
+        add("MapSideDiskSpill", imp,
+            f"maps wrote {written} local bytes for {mob} map-output bytes",
+            "Use a combiner or compress map output; raise io.sort.mb / "
+            "io.sort.record.percent so maps spill once")
+    # BalancedReducePartitioning
+    if total_reds > 0 and reds_ok:
+        recs = sorted((_ctr(a.get("counters"), _TASK, "REDUCE_INPUT_RECORDS") for a in reds_ok),
+                      reverse=True)
+        tot = sum(recs)
+        if tot > 0:
+            want = 0.90 * tot
+            acc, busy = 0, 0
+            for r in recs:
+                acc += r
+                busy += 1
+                if acc >= want:
+                    break
+            imp = 1 - busy / total_reds
+            add("BalancedReducePartitioning", imp,
+                f"{busy} of {total_reds} reducers process 90% of the reduce input records",
+                "Use a better partitioner (or sample keys, TotalOrderPartitioner) so "
+                "reduce input is spread evenly")
+    # Maps / Reduces re-execution
+    launched_m = _ctr(jc, _JIP, "TOTAL_LAUNCHED_MAPS")
+    if total_maps > 0 and launched_m:
+        imp = max(0.0, (launched_m - total_maps) / total_maps)
+        add("MapsReExecutionImpact", min(1.0, imp),
+            f"{launched_m} map attempts launched for {total_maps} maps",
+            "Find why maps are re-executed: unstable nodes or application failures")
+    launched_r = _ctr(jc, _JIP, "TOTAL_LAUNCHED_REDUCES")
+    if total_reds > 0 and launched_r:
+        imp = max(0.0, (launched_r - total_reds) / total_reds)
+        add("ReducesReExecutionImpact", min(1.0, imp),
+            f"{launched_r} reduce attempts launched for {total_reds} reduces",
+            "Find why reduces are re-executed: unstable nodes or application failures")
+    # ReadingHDFSFilesAsSideEffect
+    hdfs_read = _ctr(jc, _FS, "HDFS_BYTES_READ")
+    mib = _ctr(jc, _TASK, "MAP_INPUT_BYTES")
+    if hdfs_read:
+        if mib == 0:
+            imp = 1.0
+        else:
+            imp = hdfs_read / mib
+            imp = 1.0 if imp >= 2.0 else imp / 2.0
+        add("ReadingHDFSFilesAsSideEffect", imp,
+            f"tasks read {hdfs_read} HDFS bytes for {mib} map-input bytes",
+            "Tasks read HDFS data beyond their input splits (side files): ship it with the "
+            "DistributedCache instead")
     return out

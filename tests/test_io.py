@@ -160,3 +160,55 @@ def test_jobconf_gpu_keys_and_typo_alias():
     assert job.get_gpu_map_runner_class() is MapRunner
     job.set_gpu_executable("/bin/gpu")
     assert job.getGPUExecutable() == "/bin/gpu" and job.is_gpu_capable()
+
+
+@pytest.mark.parametrize("comp", [seqf.NONE, seqf.BLOCK])
+def test_sequencefile_sorter_multi_run(tmp_path, comp):
+    """SequenceFile.Sorter (SequenceFile.java:2269): many inputs, a memory
+    budget that forces several runs and a factor that forces merge passes;
+    the output is sorted by the key comparator and stable for equal keys."""
+    rng = np.random.default_rng(3)
+    ins, recs = [], []
+    for f in range(4):
+        p = tmp_path / f"in{f}.seq"
+        with seqf.Writer(p, IntWritable, Text, compression=comp, block_size=1500) as w:
+            for i in range(700):
+                k = int(rng.integers(-50, 50))
+                w.append(IntWritable(k), Text(f"{f}-{i}"))
+                recs.append((k, f"{f}-{i}"))
+        ins.append(p)
+    conf = Configuration()
+    conf.set("hbmr.io.sort.bytes", "4000")
+    conf.set("io.sort.factor", "3")
+    s = seqf.Sorter(IntWritable, Text, conf)
+    out = tmp_path / "sorted.seq"
+    assert s.sort(ins, out) == len(recs)
+    assert s.runs_written > 3 and s.merge_passes >= 2
+    got = [(k.get(), str(v)) for k, v in seqf.Reader(out)]
+    assert got == sorted(recs, key=lambda r: r[0])          # Python sort is stable
+    assert not (tmp_path / "sorted.seq.sort-tmp").exists()
+    assert all(p.exists() for p in ins)
+
+
+def test_sequencefile_sorter_text_and_merge(tmp_path):
+    """Text keys order by raw bytes (Text.Comparator); merge of sorted files."""
+    words = ["pear", "apple", "Zeta", "apricot", "", "é", "b", "apple"]
+    parts = []
+    for j in range(3):
+        p = tmp_path / f"s{j}.seq"
+        ws = sorted((w + str(j) for w in words), key=lambda s: s.encode())
+        with seqf.Writer(p, Text, IntWritable) as w:
+            for i, x in enumerate(ws):
+                w.append(Text(x), IntWritable(j))
+        parts.append(p)
+    out = tmp_path / "m.seq"
+    s = seqf.Sorter(Text, IntWritable)
+    n = s.merge(parts, out)
+    assert n == 3 * len(words)
+    got = [str(k) for k, _ in seqf.Reader(out)]
+    assert got == sorted((w + str(j) for j in range(3) for w in words), key=lambda s: s.encode())
+    # sort with delete_input removes the inputs
+    out2 = tmp_path / "m2.seq"
+    assert seqf.Sorter(Text, IntWritable).sort(parts, out2, delete_input=True) == n
+    assert [str(k) for k, _ in seqf.Reader(out2)] == got
+    assert not any(p.exists() for p in parts)
