@@ -131,8 +131,10 @@ class RemoteGpuRuntime:
             except OSError:
                 pass
         if self.proc is not None:
+            # under a profiler the worker's exit handlers write its trace: wait for them
+            profiled = any(k.startswith("ROCPROF") for k in os.environ)
             try:
-                self.proc.wait(timeout=20)
+                self.proc.wait(timeout=180 if profiled else 20)
             except subprocess.TimeoutExpired:
                 self.proc.kill()
                 self.proc.wait()

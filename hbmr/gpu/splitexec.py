@@ -87,6 +87,8 @@ def run_split_reduce(host, run, device=None):
         rep = TaskReporter()
         run.task = SplitTaskShim(rep, run.kill)
         ctx = TaskContext(host, js, spec, rep)
+        comm = getattr(host, "comm", None)
+        before = dict(getattr(comm, "stats", None) or {})
         with js.lock:
             outs = [js.map_outputs[a] for _tid, a, _o in spec.map_outputs if a in js.map_outputs]
         missing = [a for _tid, a, _o in spec.map_outputs if a not in js.map_outputs]
@@ -104,6 +106,10 @@ def run_split_reduce(host, run, device=None):
             js.result = js.split_job.reduce(ctx, combined)
         with js.lock:
             js.map_outputs.clear()       # consumed
+        from ..parallel.collectives import COLLECTIVE_GROUP
+        for k, v in (getattr(comm, "stats", None) or {}).items():
+            if v != before.get(k, 0):
+                rep.incrCounter(COLLECTIVE_GROUP, k, v - before.get(k, 0))
         small = js.result if isinstance(js.result, dict) else None
         host._finish(run, P.SUCCEEDED, output={"tracker": host.name, "result": small})
     except BaseException as e:  # noqa: BLE001

@@ -302,10 +302,14 @@ def main(argv=None):
             sock.close()
         except OSError:
             pass
-    # skip interpreter teardown of the HIP runtime / process group (the parent
-    # only needs the exit status; the grid has drained in serve())
     sys.stdout.flush()
     sys.stderr.flush()
+    if os.environ.get("HBMR_WORKER_CLEAN_EXIT") or \
+            any(k.startswith("ROCPROF") for k in os.environ):
+        # a normal exit, so a profiler's exit handlers write this process's trace
+        sys.exit(rc)
+    # skip interpreter teardown of the HIP runtime / process group (the parent
+    # only needs the exit status; the grid has drained in serve())
     os._exit(rc)
 
 

@@ -27,6 +27,20 @@ from .tasktracker import TaskTracker
 log = logging.getLogger("hbmr.node")
 
 
+def group_plan(use_gpu: bool, worker_mode: bool, shared: bool, backend: str | None = None):
+    """(backend of the rank processes' group, backend of the device collectives).
+
+    Device collectives run on ``nccl`` (RCCL over xGMI) unless there is no GPU
+    or every rank shares one device (``HBMR_SHARED_DEVICE``, where RCCL refuses
+    two ranks on one GPU and gloo stages device tensors through host memory).
+    In worker mode the device work — and so the device group — lives in the
+    per-rank GPU workers; the rank processes then only need host collectives
+    (gloo) and never create a HIP context."""
+    dev = "gloo" if (shared or not use_gpu) else (backend or "nccl")
+    rank = "gloo" if (worker_mode or not use_gpu) else dev
+    return rank, dev
+
+
 class Node:
     def __init__(self, conf: JobConf | None = None, use_gpu: bool | None = None,
                  backend: str | None = None):
@@ -48,7 +62,8 @@ class Node:
                                                  self.use_gpu or simulate)
         if self.worker_mode:
             self.conf.set("hbmr.gpu.worker.process", "true")
-        dev_backend = "gloo" if (shared is not None or not self.use_gpu) else "nccl"
+        rank_be, dev_backend = group_plan(self.use_gpu, self.worker_mode, shared is not None,
+                                          backend)
         self.jt = None
         self.server = None
         self.dist = None
@@ -59,20 +74,12 @@ class Node:
         if self.world > 1:
             import torch.distributed as dist
             self.dist = dist
-            # the rank processes only need host collectives when the device work
-            # lives in the workers (which form their own group, see below)
-            be = "gloo" if (self.worker_mode or not self.use_gpu) else (backend or dev_backend)
-            kw = {}
-            if be == "nccl":
-                kw["device_id"] = torch.device("cuda", self.local_rank)
-            dist.init_process_group(be, timeout=datetime.timedelta(seconds=600), **kw)
-            cpu_group = dist.new_group(backend="gloo") if be != "gloo" else None
-            self.comm = TorchComm(group=None, cpu_group=cpu_group)
+            self.comm = self._init_dist(rank_be)
             self.store = dist.distributed_c10d._get_default_store()
             if self.worker_mode:
                 worker_comm = {"host": os.environ.get("MASTER_ADDR", "127.0.0.1"),
                                "port": int(os.environ["MASTER_PORT"]), "rank": self.rank,
-                               "world": self.world, "backend": backend or dev_backend}
+                               "world": self.world, "backend": dev_backend}
         if self.rank == 0:
             self.jt = JobTracker(self.conf)
             if self.world > 1:
@@ -93,6 +100,17 @@ class Node:
             if not self.jt.wait_for_trackers(self.world, timeout=300):
                 raise RuntimeError("not all TaskTrackers registered with the JobTracker")
             self.jt.start_expiry_thread()
+
+    def _init_dist(self, be: str):
+        """The default process group on backend ``be`` (plus a gloo group for
+        host tensors when ``be`` is nccl); returns the data-plane comm."""
+        dist = self.dist
+        kw = {}
+        if be == "nccl":
+            kw["device_id"] = torch.device("cuda", self.local_rank)
+        dist.init_process_group(be, timeout=datetime.timedelta(seconds=600), **kw)
+        cpu_group = dist.new_group(backend="gloo") if be != "gloo" else None
+        return TorchComm(group=None, cpu_group=cpu_group)
 
     @property
     def is_master(self):

@@ -53,6 +53,9 @@ RETURN_KEY = "hbmr.kmeans.return.centroids"   # reduce result carries the new ce
 # so a tracker whose GPU worker restarted can re-localise the input centroids of
 # the next iteration (the DistributedCache role; the fast path stays in memory)
 CDIR_KEY = "hbmr.kmeans.centroids.dir"
+# exact mode: bf16 MFMA assign certified against the fp32 data (top-3 + fp64
+# re-score of uncertain points) and fp32 fixed-point sums (ops.kmeans.ExactSplit)
+EXACT_KEY = "hbmr.kmeans.exact"
 
 # --------------------------------------------------------------------------- data
 _M32 = 0xFFFFFFFF
@@ -211,6 +214,20 @@ _PINNED_INFLIGHT: list = []     # (event, pinned host buffer) of in-flight split
 
 
 # --------------------------------------------------------------------------- the job
+_EXACT_STATS: dict = {}
+_EXACT_LOCK = threading.Lock()
+
+
+def _exact_stats(cin, device):
+    """Device counters (flagged, relabelled) of exact mode for one iteration."""
+    key = (cin, str(device))
+    with _EXACT_LOCK:
+        t = _EXACT_STATS.get(key)
+        if t is None:
+            t = _EXACT_STATS[key] = torch.zeros(3, dtype=torch.int64, device=device)
+        return t
+
+
 class KMeansSplitJob(SplitJob):
     collective_reduce = True
     needs_reduce = True
@@ -226,6 +243,7 @@ class KMeansSplitJob(SplitJob):
         self.centers = conf.get_int(NCENTERS_KEY, self.k)
         self.fx_shift = conf.get_int("hbmr.kmeans.fx.shift", 24)
         self.cdir = conf.get(CDIR_KEY)
+        self.exact = conf.get_boolean(EXACT_KEY, False)
         init = conf.get(INIT_KEY)
         if init and self.cin and STORE.host_centroids(self.cin) is None:
             STORE.put_host(self.cin, decode_centroids(init))
@@ -240,7 +258,8 @@ class KMeansSplitJob(SplitJob):
     def get_splits(self, conf, trackers):
         if self.input.startswith("synthetic:"):
             # iteration jobs re-split the same input: reuse the split list
-            mk = (self.input, self.split_points, self.d, self.centers, tuple(trackers))
+            mk = (self.input, self.split_points, self.d, self.centers, tuple(trackers),
+                  self.exact)
             got = KMeansSplitJob._split_memo.get(mk)
             if got is not None:
                 return got
@@ -259,7 +278,8 @@ class KMeansSplitJob(SplitJob):
         for i in range(nsplits):
             a = i * per
             m = min(per, n - a)
-            key = f"kmeans-syn:{seed}:{self.d}:{self.centers}:{a}:{m}"
+            key = f"kmeans-syn:{seed}:{self.d}:{self.centers}:{a}:{m}" + \
+                (":exact" if self.exact else "")
             loc = [trackers[i * len(trackers) // nsplits]] if trackers else []
             out.append(SplitSpec(i, key, "synthetic",
                                  {"seed": seed, "start": a, "n": m}, loc, m * self.d * 2))
@@ -274,20 +294,27 @@ class KMeansSplitJob(SplitJob):
         splits = fmt.getSplits(jc, max(1, conf.get_int("mapred.map.tasks", 1)))
         out = []
         for i, s in enumerate(splits):
-            key = f"kmeans-file:{s.path}:{s.start}:{s.length}"
+            key = f"kmeans-file:{s.path}:{s.start}:{s.length}" + (":exact" if self.exact else "")
             loc = [trackers[i % len(trackers)]] if trackers else []
             out.append(SplitSpec(i, key, "file", {"path": s.path, "start": s.start,
                                                   "length": s.length}, loc, s.length))
         return out
 
-    def _load_fp32(self, spec: SplitSpec, device):
+    def _load_raw(self, spec: SplitSpec, device):
         if spec.kind == "synthetic":
             p = spec.params
-            x = synthetic_points(p["seed"], p["start"], p["n"], self.d, self.centers, device)
-        else:
-            x = self._load_file_split(spec.params, device)
+            return synthetic_points(p["seed"], p["start"], p["n"], self.d, self.centers, device)
+        return self._load_file_split(spec.params, device)
+
+    def _load_fp32(self, spec: SplitSpec, device):
         # bf16 is the storage precision of the points on every slot type
-        return x.to(torch.bfloat16)
+        return self._load_raw(spec, device).to(torch.bfloat16)
+
+    def split_nbytes(self, data) -> int:
+        nb = getattr(data, "nbytes", None)
+        if callable(nb):
+            return int(nb())
+        return super().split_nbytes(data)
 
     def load_split_host(self, spec: SplitSpec):
         """Host half of a file split's load (native decode into pinned memory),
@@ -315,6 +342,8 @@ class KMeansSplitJob(SplitJob):
         _PINNED_INFLIGHT.append((ev, host))
         while _PINNED_INFLIGHT and _PINNED_INFLIGHT[0][0].query():
             _PINNED_INFLIGHT.pop(0)
+        if self.exact:
+            return km.ExactSplit(x, km.padded_dim(self.d))
         xb = x.to(torch.bfloat16)
         dp = km.padded_dim(self.d)
         if dp == self.d:
@@ -356,6 +385,13 @@ class KMeansSplitJob(SplitJob):
 
     def load_split(self, spec: SplitSpec, device):
         from ..ops import kmeans as km
+        if self.exact:
+            # exact mode keeps the fp32 data: CPU slots compute on it directly,
+            # GPU slots hold it beside the bf16 copy
+            x = self._load_raw(spec, device)
+            if str(device) == "cpu":
+                return x.contiguous()
+            return km.ExactSplit(x, km.padded_dim(self.d))
         xb = self._load_fp32(spec, device)
         if str(device) == "cpu":
             return xb.to(torch.float32)
@@ -393,6 +429,8 @@ class KMeansSplitJob(SplitJob):
         ctx = ctxs[0]
         img = STORE.image(self.cin, ctx.device)
         B = len(datas)
+        if self.exact:
+            return self._map_exact(ctxs, datas, img)
         ws, labels = self._scratch(ctx, [d.shape[0] for d in datas], self.k)
         sums = torch.empty(B, self.k, img.dp, dtype=torch.int64, device=ctx.device)
         counts = torch.empty(B, self.k, dtype=torch.int64, device=ctx.device)
@@ -402,14 +440,35 @@ class KMeansSplitJob(SplitJob):
             c.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, d.shape[0])
         return [(sums[i], counts[i]) for i in range(B)]
 
+    def _map_exact(self, ctxs, datas, img):
+        """Exact mode: per task top-3 assign, certification / fp64 re-score,
+        fp32 combiner.  The flagged / relabelled counts accumulate on the device
+        per (job, device) and are reported by the reduce (no host sync here)."""
+        from ..ops import kmeans as km
+        ctx = ctxs[0]
+        store = ctx.tracker.__dict__.setdefault("_scratch", {})
+        scratch = store.setdefault(("kmeans-exact", str(ctx.device), id(ctx.stream)), {})
+        stats = _exact_stats(self.cin, ctx.device)
+        outs = []
+        for c, d in zip(ctxs, datas):
+            sums = torch.zeros(self.k, img.dp, dtype=torch.int64, device=ctx.device)
+            counts = torch.zeros(self.k, dtype=torch.int64, device=ctx.device)
+            km.map_split_exact(d, img, sums, counts, scratch, stats, stream=ctx.stream)
+            c.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, d.shape[0])
+            outs.append((sums, counts))
+        return outs
+
     def map_cpu(self, ctx, points):
         from ..ops import kmeans as km
         cen = STORE.host_centroids(self.cin)
         if cen is None:
             raise KeyError(f"centroids {self.cin!r} not resident")
         sums, counts = km.new_partials(self.k, self.d, "cpu")
+        st = [0]
         km.map_split_cpu(points, cen, sums, counts, nthreads=ctx.cpu_threads,
-                         fx_shift=self.fx_shift)
+                         fx_shift=self.fx_shift, exact=self.exact, stats=st)
+        if self.exact:
+            ctx.reporter.incrCounter("KMEANS", "EXACT_FLAGGED_POINTS", st[0])
         ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, points.shape[0])
         return sums, counts
 
@@ -452,6 +511,13 @@ class KMeansSplitJob(SplitJob):
             ctx.comm.all_reduce(packed)        # exact: int64 over RCCL / gloo
         sums = packed[:k * dp].view(k, dp)
         counts = packed[k * dp:]
+        if self.exact and sums.device.type == "cuda":
+            st = _EXACT_STATS.pop((self.cin, str(sums.device)), None)
+            if st is not None:
+                flagged, relabelled, rescans = (int(v) for v in st.tolist())
+                ctx.reporter.incrCounter("KMEANS", "EXACT_FLAGGED_POINTS", flagged)
+                ctx.reporter.incrCounter("KMEANS", "EXACT_RELABELLED_POINTS", relabelled)
+                ctx.reporter.incrCounter("KMEANS", "EXACT_NEIGHBOUR_SCANS", rescans)
         if sums.device.type == "cuda":
             old = STORE.image(self.cin, sums.device)
             img = km.CentroidImage.__new__(km.CentroidImage)
@@ -570,7 +636,8 @@ class KMeansDriver:
 
     def step(self):
         i = self.iteration
-        init = initial_centroids(self.inp, self.k, self.d) if i == 0 else None
+        centers = self.base.get_int(NCENTERS_KEY, self.k) if self.base is not None else None
+        init = initial_centroids(self.inp, self.k, self.d, centers) if i == 0 else None
         if init is not None:
             STORE.put_host(self.key(0), init)
         job = make_iteration_conf(self.base, self.k, self.d, self.inp, self.split_points,

@@ -30,6 +30,14 @@ _SIGS = {
                                         c_void_p, c_void_p, c_void_p]),
     "hbmr_kmeans_accum_bf16": (c_int, [c_void_p, c_long, c_int, c_void_p, c_int, c_void_p,
                                        c_void_p, c_int, c_void_p, c_long, c_int, c_void_p]),
+    "hbmr_kmeans_accum_f32": (c_int, [c_void_p, c_long, c_int, c_void_p, c_int, c_void_p,
+                                      c_void_p, c_int, c_void_p, c_long, c_int, c_void_p]),
+    "hbmr_kmeans_assign_top3_bf16": (c_int, [c_void_p, c_long, c_int, c_void_p, c_void_p, c_int,
+                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "hbmr_kmeans_refine_f32": (c_int, [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p,
+                                       c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_void_p]),
     "hbmr_kmeans_accum_workspace_bytes": (c_long, [c_long, c_int]),
     "hbmr_kmeans_batch_workspace_bytes": (c_long, [c_long, c_int, c_int]),
     "hbmr_kmeans_map_batch": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
@@ -40,6 +48,9 @@ _SIGS = {
     "hbmr_kmeans_padded_k": (c_int, [c_int]),
     "hbmr_kmeans_map_cpu_f32": (c_int, [c_void_p, c_long, c_int, c_void_p, c_int, c_void_p,
                                         c_void_p, c_void_p, c_double_p, c_int, c_int]),
+    "hbmr_kmeans_map_cpu_f32_ex": (c_int, [c_void_p, c_long, c_int, c_void_p, c_int, c_void_p,
+                                           c_void_p, c_void_p, c_double_p, c_int, c_int, c_int,
+                                           c_void_p]),
     "hbmr_kmeans_padded_dim": (c_int, [c_int]),
     "hbmr_f32_to_bf16_pad": (c_int, [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p]),
     # sort / shuffle (native/kernels/sort.hip)

@@ -14,12 +14,18 @@ Data layout contract (built by :class:`hbmr.gpu.split_cache.SplitCache`):
 from __future__ import annotations
 
 import ctypes
+import threading
 
 import torch
 
 from . import _lib
 
 SUPPORTED_DP = (64, 128, 256)
+
+
+def _nullctx():
+    import contextlib
+    return contextlib.nullcontext()
 FX_SHIFT = 24  # fixed-point fraction bits of the partial sums
 
 
@@ -76,10 +82,44 @@ class CentroidImage:
                                     _ptr(self.chalf), _ptr(self.shift2),
                                     _lib.stream_handle(stream))
         _lib.check(rc, "hbmr_kmeans_update")
+        # |c_j| for exact mode's certification bound, on the same stream as the
+        # update (consumers are ordered after the reduce like cen/cbf/chalf)
+        with torch.cuda.stream(stream) if stream is not None else _nullctx():
+            cn = self.cen.double().norm(dim=1).float()
+            self._norms = (cn, cn.max().reshape(1))
+        self._nbr = None
+        if getattr(self, "_nbr_lock", None) is None:
+            self._nbr_lock = threading.Lock()
 
     def set_centroids(self, centroids: torch.Tensor, stream=None):
         self.cen.copy_(centroids.to(self.cen.device, torch.float32))
         self.refresh(stream=stream)
+
+    def norms(self):
+        """(|c_j| fp32 [k], max_j |c_j| fp32 [1]) of the fp32 master centroids
+        (exact mode's certification bound), computed in fp64 by refresh()."""
+        return self._norms
+
+    def neighbors(self, L: int = 256):
+        """Each centroid's L nearest centroids (itself first) and their
+        distances, fp64 rounded DOWN to fp32 — exact mode's Elkan scan.  Built
+        once per image on the first caller's stream; other streams wait on it."""
+        with self._nbr_lock:
+            if self._nbr is None:
+                L = max(1, min(L, self.k))
+                c = self.cen.double()
+                dist = torch.cdist(c, c, compute_mode="donot_use_mm_for_euclid_dist")
+                dist.fill_diagonal_(0.0)
+                dv, di = dist.sort(dim=1, stable=True)
+                dv, di = dv[:, :L].contiguous(), di[:, :L].to(torch.int32).contiguous()
+                f = dv.float()
+                f = torch.where(f.double() > dv, torch.nextafter(f, torch.full_like(f, -1.0)), f)
+                ev = torch.cuda.Event()
+                ev.record()
+                self._nbr = (di, f.contiguous(), L, ev)
+        di, f, L, ev = self._nbr
+        torch.cuda.current_stream().wait_event(ev)
+        return di, f, L
 
     def max_shift(self) -> float:
         return float(self.shift2.max().sqrt().item()) if self.k else 0.0
@@ -146,14 +186,123 @@ def accumulate(points: torch.Tensor, labels: torch.Tensor, k: int, sums: torch.T
         raise ValueError(f"sums must be int64 [{k}, {dp}]")
     if counts.shape != (k,) or counts.dtype != torch.int64:
         raise ValueError(f"counts must be int64 [{k}]")
+    if points.dtype not in (torch.bfloat16, torch.float32) or not points.is_contiguous() or \
+            dp not in SUPPORTED_DP or labels.numel() < n:
+        raise ValueError("points must be contiguous bf16/fp32 [n, dp] with n labels")
     lib = _lib.load()
     if workspace is None and mode != ACCUM_LDS:
         workspace = accum_workspace(n, k, points.device)
-    rc = lib.hbmr_kmeans_accum_bf16(_ptr(points), n, dp, _ptr(labels), k, _ptr(sums),
-                                    _ptr(counts), fx_shift, _ptr(workspace),
-                                    0 if workspace is None else workspace.numel(), mode,
-                                    _lib.stream_handle(stream))
-    _lib.check(rc, "hbmr_kmeans_accum_bf16")
+    fn, name = ((lib.hbmr_kmeans_accum_f32, "hbmr_kmeans_accum_f32")
+                if points.dtype == torch.float32 else
+                (lib.hbmr_kmeans_accum_bf16, "hbmr_kmeans_accum_bf16"))
+    rc = fn(_ptr(points), n, dp, _ptr(labels), k, _ptr(sums), _ptr(counts), fx_shift,
+            _ptr(workspace), 0 if workspace is None else workspace.numel(), mode,
+            _lib.stream_handle(stream))
+    _lib.check(rc, name)
+
+
+# --------------------------------------------------------------------------- exact mode
+class ExactSplit:
+    """A split held for exact mode (``hbmr.kmeans.exact``): the bf16 copy the
+    MFMA assign reads, the fp32 data (rows padded to dp) the certification
+    re-score and the combiner read, and per point |x| (fp32 data) and |x~|²
+    (bf16 copy), both computed in fp64."""
+    __slots__ = ("xb", "x32", "xnorm", "xbn2", "d")
+
+    def __init__(self, x32: torch.Tensor, dp: int):
+        n, d = x32.shape
+        self.d = d
+        x64 = x32.double()
+        self.xnorm = x64.norm(dim=1).float()
+        xb = x32.to(torch.bfloat16)
+        self.xbn2 = xb.double().pow(2).sum(1).float()
+        if dp == d:
+            self.xb, self.x32 = xb.contiguous(), x32.contiguous()
+        else:
+            self.xb = torch.zeros(n, dp, dtype=torch.bfloat16, device=x32.device)
+            self.xb[:, :d] = xb
+            self.x32 = torch.zeros(n, dp, dtype=torch.float32, device=x32.device)
+            self.x32[:, :d] = x32
+
+    @property
+    def shape(self):
+        return self.xb.shape
+
+    def nbytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in (self.xb, self.x32, self.xnorm,
+                                                          self.xbn2))
+
+
+def assign_top3(points: torch.Tensor, img: CentroidImage, labels, cand, scores, margin,
+                stream=None) -> None:
+    """bf16 MFMA assign keeping the three best clusters: labels [n] (best),
+    cand [2n] (second | third), scores [n] (best score), margin [2n]
+    (best - second | best - third)."""
+    n, dp = points.shape
+    if points.dtype != torch.bfloat16 or dp != img.dp or not points.is_contiguous():
+        raise ValueError("points must be contiguous bf16 [n, dp] matching the centroid image")
+    for t, dt, m in ((labels, torch.int32, 1), (cand, torch.int32, 2), (scores, torch.float32, 1),
+                     (margin, torch.float32, 2)):
+        if t.numel() != m * n or t.dtype != dt or not t.is_contiguous():
+            raise ValueError("top-3 outputs: labels/scores [n], cand/margin [2n]")
+    rc = _lib.load().hbmr_kmeans_assign_top3_bf16(
+        _ptr(points), n, dp, _ptr(img.cbf), _ptr(img.chalf), img.k_pad, _ptr(labels),
+        _ptr(cand), _ptr(scores), _ptr(margin), _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_kmeans_assign_top3_bf16")
+
+
+def refine_f32(split: ExactSplit, img: CentroidImage, labels, cand, scores, margin,
+               stats: torch.Tensor, stream=None) -> None:
+    """Certify the bf16 labels against the fp32 data; re-score the uncertain
+    points in fp64 (hbmr_kmeans_refine_f32).  stats (int64 [3]) += (flagged,
+    relabelled, points that needed the neighbour scan)."""
+    n = split.shape[0]
+    if stats.dtype != torch.int64 or stats.numel() < 3:
+        raise ValueError("stats must be int64 [3]")
+    if labels.numel() != n or cand.numel() != 2 * n or margin.numel() != 2 * n:
+        raise ValueError("labels [n], cand/margin [2n] from assign_top3 expected")
+    cn, cmax = img.norms()
+    with torch.cuda.stream(stream) if stream is not None else _nullctx():
+        ni, nd, L = img.neighbors()
+    rc = _lib.load().hbmr_kmeans_refine_f32(
+        _ptr(split.x32), n, img.d, split.x32.shape[1], _ptr(split.xnorm), _ptr(split.xbn2),
+        _ptr(img.cen), img.k, img.k_pad, _ptr(cn), _ptr(cmax), _ptr(ni), _ptr(nd), L,
+        _ptr(labels), _ptr(cand), _ptr(scores), _ptr(margin), _ptr(stats),
+        _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_kmeans_refine_f32")
+
+
+def assign_exact(split: ExactSplit, img: CentroidImage, stats: torch.Tensor,
+                 scratch: dict | None = None, stream=None) -> torch.Tensor:
+    """Exact labels of the split's fp32 points: top-3 bf16 assign +
+    certification / fp64 re-score.  Returns labels [n] (a scratch view)."""
+    n = split.shape[0]
+    dev = split.xb.device
+    scratch = {} if scratch is None else scratch
+    key = ("exact", n)
+    bufs = scratch.get(key)
+    if bufs is None:
+        bufs = scratch[key] = (torch.empty(n, dtype=torch.int32, device=dev),
+                               torch.empty(2 * n, dtype=torch.int32, device=dev),
+                               torch.empty(n, dtype=torch.float32, device=dev),
+                               torch.empty(2 * n, dtype=torch.float32, device=dev))
+    lab, cand, sc, mg = bufs
+    assign_top3(split.xb, img, lab, cand, sc, mg, stream=stream)
+    refine_f32(split, img, lab, cand, sc, mg, stats, stream=stream)
+    return lab
+
+
+def map_split_exact(split: ExactSplit, img: CentroidImage, sums, counts, scratch: dict,
+                    stats: torch.Tensor, stream=None) -> None:
+    """One exact-mode GPU map task: top-3 assign, certification + fp64 re-score,
+    then the int64 fixed-point combiner over the fp32 rows."""
+    n = split.shape[0]
+    lab = assign_exact(split, img, stats, scratch, stream=stream)
+    need = workspace_bytes(n, img.k)
+    if scratch.get("ws") is None or scratch["ws"].numel() < need:
+        scratch["ws"] = torch.empty(max(need, 1 << 20), dtype=torch.uint8, device=split.xb.device)
+    accumulate(split.x32, lab, img.k, sums, counts, fx_shift=img.fx_shift, stream=stream,
+               workspace=scratch["ws"])
 
 
 def map_batch_gpu(splits: list, img: CentroidImage, sums: torch.Tensor, counts: torch.Tensor,
@@ -193,11 +342,13 @@ def map_split_gpu(points, img: CentroidImage, sums, counts, labels=None, stream=
 
 def map_split_cpu(points: torch.Tensor, centroids: torch.Tensor, sums: torch.Tensor,
                   counts: torch.Tensor, nthreads: int = 1, labels: torch.Tensor | None = None,
-                  fx_shift: int = FX_SHIFT):
+                  fx_shift: int = FX_SHIFT, exact: bool = False, stats: list | None = None):
     """CPU K-Means map task (native C++, fp32 math, int64 fixed-point partials).
 
     ``sums`` is int64 ``[k, d]`` (or ``[k, dp]``: only the first d columns are
-    touched).  Returns the partial cost Σ min_j ||x - c_j||².
+    touched).  Returns the partial cost Σ min_j ||x - c_j||².  ``exact``: near
+    ties (fp32 margin within the fp32 error bound) are re-scored in fp64;
+    ``stats[0]`` += re-scored points.
     """
     x = points.detach().to(torch.float32).contiguous()
     c = centroids.detach().to(torch.float32).contiguous()
@@ -210,9 +361,13 @@ def map_split_cpu(points: torch.Tensor, centroids: torch.Tensor, sums: torch.Ten
         target = torch.zeros(k, d, dtype=torch.int64)
     cost = ctypes.c_double(0.0)
     lib = _lib.load()
-    rc = lib.hbmr_kmeans_map_cpu_f32(_ptr(x), n, d, _ptr(c), k, _ptr(labels), _ptr(target),
-                                     _ptr(counts), ctypes.byref(cost), fx_shift, int(nthreads))
-    _lib.check(rc, "hbmr_kmeans_map_cpu_f32")
+    res = ctypes.c_long(0)
+    rc = lib.hbmr_kmeans_map_cpu_f32_ex(_ptr(x), n, d, _ptr(c), k, _ptr(labels), _ptr(target),
+                                        _ptr(counts), ctypes.byref(cost), fx_shift, int(nthreads),
+                                        int(exact), ctypes.byref(res))
+    _lib.check(rc, "hbmr_kmeans_map_cpu_f32_ex")
+    if stats is not None:
+        stats[0] += res.value
     if target is not sums:
         sums[:, :d] += target
     return cost.value

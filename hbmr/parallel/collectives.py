@@ -17,14 +17,25 @@ collective code paths.  :class:`SoloComm` is the 1-tracker no-op.
 """
 from __future__ import annotations
 
+import collections
 import threading
 
 import torch
+
+COLLECTIVE_GROUP = "hbmr.CollectiveCounters"
 
 
 class Comm:
     rank = 0
     world_size = 1
+    stats: collections.Counter = None
+
+    def _note(self, op: str, t: torch.Tensor):
+        """Count a collective by op and tensor device (reported per reduce task
+        as ``hbmr.CollectiveCounters``: which path the data plane really took)."""
+        if self.stats is None:
+            self.stats = collections.Counter()
+        self.stats[f"{op.upper()}_{t.device.type.upper()}"] += 1
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         raise NotImplementedError
@@ -45,6 +56,7 @@ class Comm:
     def all_to_all_v(self, send: torch.Tensor, counts: list):
         """Variable all-to-all of one buffer: rows [sum(counts[:j]), +counts[j]) of
         ``send`` go to rank j.  Returns (recv, recv_counts), recv ordered by source."""
+        self._note("all_to_all_v", send)
         outs = list(torch.split(send, [int(c) for c in counts]))
         ins = self.all_to_all(outs)
         return (torch.cat(ins) if ins else send[:0]), [int(t.shape[0]) for t in ins]
@@ -104,6 +116,7 @@ class InProcessComm(Comm):
         return got
 
     def all_reduce(self, t):
+        self._note("all_reduce", t)
         # exchange snapshots: peers may still be reading while we write into t
         got = self._exchange(t.detach().clone())
         out = got[0].to(t.device).clone()
@@ -113,13 +126,16 @@ class InProcessComm(Comm):
         return t
 
     def all_gather(self, t):
+        self._note("all_gather", t)
         return [g.to(t.device) for g in self._exchange(t)]
 
     def all_to_all(self, outs):
+        self._note("all_to_all", outs[0])
         got = self._exchange(list(outs))
         return [got[j][self.rank] for j in range(self.world_size)]
 
     def broadcast(self, t, src=0):
+        self._note("broadcast", t)
         got = self._exchange(t.detach().clone())
         t.copy_(got[src].to(t.device))
         return t
@@ -129,7 +145,13 @@ class InProcessComm(Comm):
 
 
 class TorchComm(Comm):
-    """torch.distributed collectives (nccl/RCCL for device tensors, gloo for host)."""
+    """torch.distributed collectives (nccl/RCCL for device tensors, gloo for host).
+
+    Device tensors on a ``gloo`` group (the 1-GPU rehearsal of the multi-rank
+    path, ``HBMR_SHARED_DEVICE``: RCCL refuses two ranks on one GPU) are staged
+    through host memory — one D2H, the gloo collective, one H2D — so the same
+    device-tensor code runs unchanged; counted as ``<OP>_STAGED``.  Under RCCL
+    they go device to device."""
 
     def __init__(self, group=None, cpu_group=None):
         import torch.distributed as dist
@@ -138,24 +160,46 @@ class TorchComm(Comm):
         self.cpu_group = cpu_group
         self.rank = dist.get_rank()
         self.world_size = dist.get_world_size()
+        self.backend = str(dist.get_backend(group))
+        self.stage = self.backend == "gloo"
 
     def _grp(self, t):
         if t.device.type == "cpu" and self.cpu_group is not None:
             return self.cpu_group
         return self.group
 
+    def _staged(self, op, t):
+        """True when device tensor ``t`` must go through host memory."""
+        self._note(op, t)
+        if self.stage and t.device.type != "cpu":
+            self.stats[f"{op.upper()}_STAGED"] += 1
+            return True
+        return False
+
     def all_reduce(self, t):
+        if self._staged("all_reduce", t):
+            h = t.cpu()
+            self.dist.all_reduce(h, group=self.cpu_group or self.group)
+            t.copy_(h)
+            return t
         self.dist.all_reduce(t, group=self._grp(t))
         return t
 
     def all_gather(self, t):
+        if self._staged("all_gather", t):
+            h = t.contiguous().cpu()
+            out = [torch.empty_like(h) for _ in range(self.world_size)]
+            self.dist.all_gather(out, h, group=self.cpu_group or self.group)
+            return [o.to(t.device) for o in out]
         out = [torch.empty_like(t) for _ in range(self.world_size)]
         self.dist.all_gather(out, t.contiguous(), group=self._grp(t))
         return out
 
     def all_to_all(self, outs):
-        # sizes first (tensors may differ in length along dim 0)
         dev = outs[0].device
+        if self._staged("all_to_all", outs[0]):
+            return [x.to(dev) for x in self._all_to_all_host([o.cpu() for o in outs])]
+        # sizes first (tensors may differ in length along dim 0)
         sizes = torch.tensor([o.shape[0] for o in outs], dtype=torch.int64, device=dev)
         in_sizes = torch.empty_like(sizes)
         self.dist.all_to_all_single(in_sizes, sizes, group=self._grp(outs[0]))
@@ -164,28 +208,47 @@ class TorchComm(Comm):
         self.dist.all_to_all(ins, [o.contiguous() for o in outs], group=self._grp(outs[0]))
         return ins
 
+    def _all_to_all_host(self, outs):
+        send, counts = torch.cat(outs), [int(o.shape[0]) for o in outs]
+        recv, rcounts = self._a2av(send, counts, self.cpu_group or self.group)
+        return list(torch.split(recv, rcounts))
+
     def broadcast(self, t, src=0):
+        if self._staged("broadcast", t):
+            h = t.cpu()
+            self.dist.broadcast(h, src, group=self.cpu_group or self.group)
+            t.copy_(h)
+            return t
         self.dist.broadcast(t, src, group=self._grp(t))
         return t
 
-    def all_to_all_v(self, send, counts):
+    def _a2av(self, send, counts, group):
         # one all_to_all_single with split sizes: a single RCCL alltoallv (grouped
         # point-to-point over the xGMI mesh) instead of per-peer tensors
         dev = send.device
         sc = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=dev)
         rc = torch.empty_like(sc)
-        self.dist.all_to_all_single(rc, sc, group=self._grp(send))
+        self.dist.all_to_all_single(rc, sc, group=group)
         rcounts = [int(x) for x in rc.tolist()]
         recv = torch.empty((sum(rcounts),) + tuple(send.shape[1:]), dtype=send.dtype, device=dev)
         self.dist.all_to_all_single(recv, send.contiguous(), output_split_sizes=rcounts,
-                                    input_split_sizes=[int(c) for c in counts],
-                                    group=self._grp(send))
+                                    input_split_sizes=[int(c) for c in counts], group=group)
         return recv, rcounts
+
+    def all_to_all_v(self, send, counts):
+        if self._staged("all_to_all_v", send):
+            recv, rcounts = self._a2av(send.cpu(), counts, self.cpu_group or self.group)
+            return recv.to(send.device), rcounts
+        return self._a2av(send, counts, self._grp(send))
 
     def barrier(self):
         self.dist.barrier(group=self.cpu_group or self.group)
 
     def reduce_scatter(self, t):
+        if self.stage:
+            # gloo has no reduce_scatter_tensor: all-reduce and keep this rank's rows
+            return Comm.reduce_scatter(self, t)
+        self._note("reduce_scatter", t)
         n = t.shape[0]
         per = (n + self.world_size - 1) // self.world_size
         if per * self.world_size != n:

@@ -24,6 +24,20 @@ int hbmr_kmeans_assign_bf16(const void* X, long n, int dp, const void* C, const 
 int hbmr_kmeans_accum_bf16(const void* X, long n, int dp, const int32_t* labels, int k,
                            long long* sums, long long* counts, int fx_shift, void* ws,
                            long ws_bytes, int mode, hipStream_t st);
+// Exact mode (hbmr.kmeans.exact): fp32-data combiner, top-2 assign, fp64 re-score
+int hbmr_kmeans_accum_f32(const float* X, long n, int dp, const int32_t* labels, int k,
+                          long long* sums, long long* counts, int fx_shift, void* ws,
+                          long ws_bytes, int mode, hipStream_t st);
+// cand: [2n] runner-ups (second | third), margin: [2n] best-second | best-third
+int hbmr_kmeans_assign_top3_bf16(const void* X, long n, int dp, const void* C, const float* chalf,
+                                 int k_pad, int32_t* labels, int32_t* cand, float* scores,
+                                 float* margin, hipStream_t st);
+int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float* xnorm,
+                           const float* xbn2, const float* C32, int k, int k_pad,
+                           const float* cnorm, const float* cmax, const int32_t* nbr_idx,
+                           const float* nbr_dist, int L, int32_t* labels, const int32_t* cand,
+                           const float* scores, const float* margin, unsigned long long* stats,
+                           hipStream_t st);
 int hbmr_kmeans_update(const long long* sums, const long long* counts, int fx_shift, int k, int d,
                        int dp, int k_pad, float* cen, void* cbf, float* chalf, float* shift2,
                        hipStream_t st);
@@ -100,6 +114,9 @@ long hbmr_kmeans_batch_workspace_bytes(long total_n, int ntasks, int k);
 int hbmr_kmeans_map_cpu_f32(const float* X, long n, int d, const float* C, int k,
                             int32_t* labels, long long* sums, long long* counts, double* cost,
                             int fx_shift, int nthreads);
+int hbmr_kmeans_map_cpu_f32_ex(const float* X, long n, int d, const float* C, int k,
+                               int32_t* labels, long long* sums, long long* counts, double* cost,
+                               int fx_shift, int nthreads, int exact, long* rescored);
 
 #ifdef __cplusplus
 }

@@ -27,6 +27,7 @@
 #include "../include/hbmr/hbmr.h"
 #include <algorithm>
 #include <cstring>
+#include <type_traits>
 
 namespace {
 
@@ -86,7 +87,7 @@ __device__ __forceinline__ float vmax3(float a, float b, float c) {
 // mantissa bits of every score are overwritten with a (tile, register) code,
 // so the running maximum needs no index registers: per tile and 32-point block
 // it costs 16 v_and_or_b32 + 8 v_max3_f32 into two partial maxima.  lb ≤ 12,
-// i.e. ≤ 2^-12 relative perturbation — below the bf16 operand rounding (2^-9).
+// i.e. ≤ 2^-12 relative perturbation — below the bf16 operand rounding (2^-8).
 // v_max3_f32 goes through asm because __builtin_fmaxf canonicalises both
 // operands in IEEE mode (an extra v_max_f32 x,x,x per input, which made the
 // epilogue as long as the MFMA chain); the and_or stays compiler-visible so
@@ -137,14 +138,131 @@ struct PackedArgMax {
   }
 };
 
+__device__ __forceinline__ float vmed3(float a, float b, float c) {
+  float r;
+  asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// Packed running TOP-3 (exact mode, hbmr.kmeans.exact): same (tile, register)
+// codes as PackedArgMax, but each of two register-parity tracks keeps its best
+// three b >= s >= t.  Inserting u: t = med3(s, t, u), s = med3(b, s, u),
+// b = max(b, u) (the middle of a sorted pair and u is the new lower member) —
+// 3 VALU ops per score instead of 0.5, two independent chains per 32 points.
+struct PackedTop3 : PackedArgMax {
+  float s0, s1, t0, t1;
+  __device__ __forceinline__ void init(int ntiles) {
+    PackedArgMax::init(ntiles);
+    s0 = s1 = t0 = t1 = -3.0e38f;
+  }
+  __device__ __forceinline__ static void insert(float& b, float& s, float& t, float u) {
+    t = vmed3(s, t, u);
+    s = vmed3(b, s, u);
+    b = vmax3(b, u, u);
+  }
+  __device__ __forceinline__ void update(const f32x16& acc, int tt) {
+    const uint32_t base = top - ((uint32_t)tt << 4);
+    uint32_t code[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      code[r] = base | (15u - r);
+      asm("" : "+s"(code[r]));
+    }
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      const float u0 = __uint_as_float((__float_as_uint(acc[r + 0]) & vmask) | code[r + 0]);
+      const float u1 = __uint_as_float((__float_as_uint(acc[r + 1]) & vmask) | code[r + 1]);
+      insert(b0, s0, t0, u0);
+      insert(b1, s1, t1, u1);
+    }
+  }
+  __device__ __forceinline__ void top3(float& b, float& s, float& t) const {
+    b = b0; s = s0; t = t0;
+    insert(b, s, t, b1);
+    insert(b, s, t, s1);
+    insert(b, s, t, t1);
+  }
+};
+
+template <bool EXACT>
+using ArgMaxT = typename std::conditional<EXACT, PackedTop3, PackedArgMax>::type;
+
+// (score, cluster) insertion into a sorted triple; ties to the lower cluster
+__device__ __forceinline__ void insert3(float (&v)[3], int (&c)[3], float u, int cu) {
+  auto gt = [](float a, int ca, float b, int cb) { return a > b || (a == b && ca < cb); };
+  if (gt(u, cu, v[2], c[2])) {
+    v[2] = u; c[2] = cu;
+    if (gt(v[2], c[2], v[1], c[1])) {
+      float tv = v[1]; v[1] = v[2]; v[2] = tv;
+      int tc = c[1]; c[1] = c[2]; c[2] = tc;
+      if (gt(v[1], c[1], v[0], c[0])) {
+        tv = v[0]; v[0] = v[1]; v[1] = tv;
+        tc = c[0]; c[0] = c[1]; c[1] = tc;
+      }
+    }
+  }
+}
+
+// Finish one point: lane-local arg-max (exact mode: top 3), then across the
+// two lane halves (each half saw a different set of cluster rows).  Exact mode
+// writes the runner-ups cand[p], cand[n+p] and the score margins best-second,
+// best-third (masked scores) to margin[p], margin[n+p].
+template <bool EXACT, class AM>
+__device__ __forceinline__ void finish_point(const AM& am, int h, long p, long n,
+                                             int32_t* __restrict__ labels,
+                                             int32_t* __restrict__ cand,
+                                             float* __restrict__ scores,
+                                             float* __restrict__ margin,
+                                             uint32_t* __restrict__ hist) {
+  if constexpr (!EXACT) {
+    float bv = am.best();
+    int cluster = am.cluster(bv, h);
+    const float ov = __shfl_xor(bv, 32);
+    const int oc = __shfl_xor(cluster, 32);
+    if (ov > bv || (ov == bv && oc < cluster)) { bv = ov; cluster = oc; }
+    if (h == 0 && p < n) {
+      labels[p] = cluster;
+      if (scores) scores[p] = am.score(bv);
+      if (hist) atomicAdd(hist + cluster, 1u);  // fused histogram for the sorted combiner
+    }
+  } else {
+    float v[3];
+    int c[3];
+    am.top3(v[0], v[1], v[2]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) c[i] = am.cluster(v[i], h);
+    float ov[3];
+    int oc[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      ov[i] = __shfl_xor(v[i], 32);
+      oc[i] = __shfl_xor(c[i], 32);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) insert3(v, c, ov[i], oc[i]);
+    if (h == 0 && p < n) {
+      labels[p] = c[0];
+      cand[p] = c[1];
+      cand[n + p] = c[2];
+      const float bs = am.score(v[0]);
+      scores[p] = bs;
+      margin[p] = bs - am.score(v[1]);
+      margin[n + p] = bs - am.score(v[2]);
+      if (hist) atomicAdd(hist + c[0], 1u);
+    }
+  }
+}
+
 // One workgroup's tile of points [blk*PTS, (blk+1)*PTS) of one split.
-template <int D>
+template <int D, bool EXACT = false>
 __device__ __forceinline__ void assign_tile(const __bf16* __restrict__ X, long n,
                                             const __bf16* __restrict__ C,
                                             const float* __restrict__ chalf, int nchunks,
                                             int32_t* __restrict__ labels,
                                             float* __restrict__ scores,
-                                            uint32_t* __restrict__ hist, long blk, char* smem) {
+                                            uint32_t* __restrict__ hist, long blk, char* smem,
+                                            int32_t* __restrict__ cand = nullptr,
+                                            float* __restrict__ margin = nullptr) {
   using Cfg = AssignCfg<D>;
   constexpr int KS = Cfg::KS, PB = Cfg::PB;
 
@@ -172,7 +290,7 @@ __device__ __forceinline__ void assign_tile(const __bf16* __restrict__ X, long n
     }
   }
 
-  PackedArgMax am[PB];
+  ArgMaxT<EXACT> am[PB];
 #pragma unroll
   for (int pb = 0; pb < PB; ++pb) am[pb].init(nchunks * (kCK / 32));
 
@@ -226,21 +344,9 @@ __device__ __forceinline__ void assign_tile(const __bf16* __restrict__ X, long n
     __syncthreads();
   }
 
-  // Finish: lane-local packed arg-max, then across the lane halves.
 #pragma unroll
-  for (int pb = 0; pb < PB; ++pb) {
-    float bv = am[pb].best();
-    int cluster = am[pb].cluster(bv, h);
-    float ov = __shfl_xor(bv, 32);
-    int oc = __shfl_xor(cluster, 32);
-    if (ov > bv || (ov == bv && oc < cluster)) { bv = ov; cluster = oc; }
-    const long p = p0 + pb * 32 + col;
-    if (h == 0 && p < n) {
-      labels[p] = cluster;
-      if (scores) scores[p] = am[pb].score(bv);
-      if (hist) atomicAdd(hist + cluster, 1u);  // fused histogram for the sorted combiner
-    }
-  }
+  for (int pb = 0; pb < PB; ++pb)
+    finish_point<EXACT>(am[pb], h, p0 + pb * 32 + col, n, labels, cand, scores, margin, hist);
 }
 
 // ---------------------------------------------------------------------------
@@ -334,12 +440,14 @@ __device__ __forceinline__ void read_tile32(const char* buf, int col, int h, bf1
   }
 }
 
-template <int D, int PB>
+template <int D, int PB, bool EXACT = false>
 __device__ __forceinline__ void assign_tile_v2(const __bf16* __restrict__ X, long n,
                                                const __bf16* __restrict__ C,
                                                const float* __restrict__ chalf, int ntiles,
                                                int32_t* __restrict__ labels,
-                                               float* __restrict__ scores, long blk, char* smem) {
+                                               float* __restrict__ scores, long blk, char* smem,
+                                               int32_t* __restrict__ cand = nullptr,
+                                               float* __restrict__ margin = nullptr) {
   static_assert(D <= 128, "v2 keeps PB point blocks of D ≤ 128 in registers");
   using V = AssignV2<D>;
   constexpr int KS = V::KS;
@@ -363,7 +471,7 @@ __device__ __forceinline__ void assign_tile_v2(const __bf16* __restrict__ X, lon
 #pragma unroll
     for (int s = 0; s < KS; ++s) bfrag[pb][s] = __builtin_bit_cast(bf16x8, row[2 * s + h]);
   }
-  PackedArgMax am[PB];
+  ArgMaxT<EXACT> am[PB];
 #pragma unroll
   for (int pb = 0; pb < PB; ++pb) am[pb].init(ntiles);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -422,18 +530,8 @@ __device__ __forceinline__ void assign_tile_v2(const __bf16* __restrict__ X, lon
   }
 
 #pragma unroll
-  for (int pb = 0; pb < PB; ++pb) {
-    float bv = am[pb].best();
-    int cluster = am[pb].cluster(bv, h);
-    const float ov = __shfl_xor(bv, 32);
-    const int oc = __shfl_xor(cluster, 32);
-    if (ov > bv || (ov == bv && oc < cluster)) { bv = ov; cluster = oc; }
-    const long p = p0 + pb * 32 + col;
-    if (h == 0 && p < n) {
-      labels[p] = cluster;
-      if (scores) scores[p] = am[pb].score(bv);
-    }
-  }
+  for (int pb = 0; pb < PB; ++pb)
+    finish_point<EXACT>(am[pb], h, p0 + pb * 32 + col, n, labels, cand, scores, margin, nullptr);
 }
 
 template <int D>
@@ -454,6 +552,27 @@ __global__ __launch_bounds__(AssignV2<D>::THREADS, AssignV2<D>::MINB) void kmean
   extern __shared__ __attribute__((aligned(16))) char smem[];
   assign_tile_v2<D, PB>(X, n, C, chalf, ntiles, labels, scores,
                     hbmr_xcd_remap(blockIdx.x, gridDim.x), smem);
+}
+
+// Exact mode: the same kernels with the top-3 epilogue.
+template <int D>
+__global__ __launch_bounds__(kThreads, 2) void kmeans_assign_top3_kernel(
+    const __bf16* __restrict__ X, long n, const __bf16* __restrict__ C,
+    const float* __restrict__ chalf, int nchunks, int32_t* __restrict__ labels,
+    int32_t* __restrict__ cand, float* __restrict__ scores, float* __restrict__ margin) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  assign_tile<D, true>(X, n, C, chalf, nchunks, labels, scores, nullptr,
+                       hbmr_xcd_remap(blockIdx.x, gridDim.x), smem, cand, margin);
+}
+
+template <int D, int PB>
+__global__ __launch_bounds__(AssignV2<D>::THREADS, AssignV2<D>::MINB) void kmeans_assign_top3_v2_kernel(
+    const __bf16* __restrict__ X, long n, const __bf16* __restrict__ C,
+    const float* __restrict__ chalf, int ntiles, int32_t* __restrict__ labels,
+    int32_t* __restrict__ cand, float* __restrict__ scores, float* __restrict__ margin) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  assign_tile_v2<D, PB, true>(X, n, C, chalf, ntiles, labels, scores,
+                              hbmr_xcd_remap(blockIdx.x, gridDim.x), smem, cand, margin);
 }
 
 // 1 = the chunked kernel above, 2 = the pipelined v2 (D ≤ 128); HBMR_KMEANS_ASSIGN
@@ -549,11 +668,37 @@ template <int D> struct AccCfg {
   static constexpr int TPP = D / 8;         // lanes per point
 };
 
-template <int D>
-__device__ __forceinline__ void lds_add_row(u64* s_rows, int r, int sub, const uint4 v,
+// Eight consecutive features of one row, as loaded by one lane: bf16 rows
+// (the normal path, one 16-B load) or fp32 rows (exact mode, two 16-B loads).
+// `ld` is the padded row length in elements.
+template <typename T> struct Row8;
+template <> struct Row8<__bf16> {
+  uint4 v;
+  __device__ __forceinline__ void load(const __bf16* X, size_t row, int ld, int sub) {
+    v = reinterpret_cast<const uint4*>(X + row * ld)[sub];
+  }
+  __device__ __forceinline__ void unpack(float f[8]) const { hbmr_unpack8(v, f); }
+};
+template <> struct Row8<float> {
+  uint4 a, b;
+  __device__ __forceinline__ void load(const float* X, size_t row, int ld, int sub) {
+    const uint4* r = reinterpret_cast<const uint4*>(X + row * ld) + 2 * sub;
+    a = r[0];
+    b = r[1];
+  }
+  __device__ __forceinline__ void unpack(float f[8]) const {
+    f[0] = __uint_as_float(a.x); f[1] = __uint_as_float(a.y);
+    f[2] = __uint_as_float(a.z); f[3] = __uint_as_float(a.w);
+    f[4] = __uint_as_float(b.x); f[5] = __uint_as_float(b.y);
+    f[6] = __uint_as_float(b.z); f[7] = __uint_as_float(b.w);
+  }
+};
+
+template <int D, typename T>
+__device__ __forceinline__ void lds_add_row(u64* s_rows, int r, int sub, const Row8<T>& v,
                                             float scale) {
   float f[8];
-  hbmr_unpack8(v, f);
+  v.unpack(f);
   u64* dst = s_rows + r * AccCfg<D>::RS + sub * 9;
   long long q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   hbmr_fx_accum8(f, scale, q);
@@ -579,9 +724,9 @@ __device__ __forceinline__ void flush_rows(const u64* s_rows, const uint32_t* s_
 
 // Small k: every workgroup holds all k rows in LDS; grid-stride over points.
 // Each lane group keeps U rows (and labels) in flight before its LDS adds.
-template <int D, int U>
+template <typename T, int D, int U>
 __global__ __launch_bounds__(256) void kmeans_accum_lds_kernel(
-    const __bf16* __restrict__ X, long n, const int32_t* __restrict__ labels, int k,
+    const T* __restrict__ X, long n, const int32_t* __restrict__ labels, int k,
     long long* __restrict__ sums, long long* __restrict__ counts, float scale) {
   using A = AccCfg<D>;
   extern __shared__ __attribute__((aligned(16))) u64 s_acc[];  // k*RS sums, then k counts
@@ -597,11 +742,11 @@ __global__ __launch_bounds__(256) void kmeans_accum_lds_kernel(
   long p = (long)blockIdx.x * PPI + pi;
   for (; p + (U - 1) * stride < n; p += U * stride) {
     int lab[U];
-    uint4 v[U];
+    Row8<T> v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       lab[u] = labels[p + u * stride];
-      v[u] = reinterpret_cast<const uint4*>(X + (p + u * stride) * D)[sub];
+      v[u].load(X, p + u * stride, D, sub);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -611,7 +756,9 @@ __global__ __launch_bounds__(256) void kmeans_accum_lds_kernel(
   }
   for (; p < n; p += stride) {
     const int l0 = labels[p];
-    lds_add_row<D>(s_acc, l0, sub, reinterpret_cast<const uint4*>(X + p * D)[sub], scale);
+    Row8<T> v0;
+    v0.load(X, p, D, sub);
+    lds_add_row<D>(s_acc, l0, sub, v0, scale);
     if (sub == 0) atomicAdd(s_cnt + l0, 1u);
   }
   __syncthreads();
@@ -627,9 +774,9 @@ __global__ __launch_bounds__(256) void kmeans_accum_lds_kernel(
 constexpr int kAccWaves = 8;
 constexpr int kQueue = 256;  // queue entries per wave (one step's worth)
 
-template <int D, int U>
+template <typename T, int D, int U>
 __global__ __launch_bounds__(512) void kmeans_accum_chunked_kernel(
-    const __bf16* __restrict__ X, long n, const int32_t* __restrict__ labels, int k, int CC,
+    const T* __restrict__ X, long n, const int32_t* __restrict__ labels, int k, int CC,
     long pts_per_block, long long* __restrict__ sums, long long* __restrict__ counts,
     float scale) {
   using A = AccCfg<D>;
@@ -673,14 +820,13 @@ __global__ __launch_bounds__(512) void kmeans_accum_chunked_kernel(
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     for (int e = 0; e < cnt; e += U * GPW) {
-      uint4 v[U];
+      Row8<T> v[U];
       uint32_t ent[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int idx = e + u * GPW + grp;
         ent[u] = idx < cnt ? q[idx] : 0xffffffffu;
-        if (ent[u] != 0xffffffffu)
-          v[u] = reinterpret_cast<const uint4*>(X + (base + (ent[u] >> 16)) * D)[sub];
+        if (ent[u] != 0xffffffffu) v[u].load(X, base + (ent[u] >> 16), D, sub);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -808,8 +954,8 @@ __global__ __launch_bounds__(256) void kmeans_scatter_kernel(const int32_t* __re
 // at the segment end the groups are reduced with xor-shuffles so each cluster
 // costs one 128-value atomic flush per wave — spread over all groups — rather
 // than one per group.  Segment bounds are wave-uniform (scalar loads).
-template <int D, int U>
-__device__ __forceinline__ void segsum_range(const __bf16* __restrict__ X,
+template <typename T, int D, int U>
+__device__ __forceinline__ void segsum_range(const T* __restrict__ X,
                                              const uint32_t* __restrict__ pm,
                                              const uint32_t* __restrict__ of, int k, long s0,
                                              long e, u64* __restrict__ out, float scale) {
@@ -833,7 +979,7 @@ __device__ __forceinline__ void segsum_range(const __bf16* __restrict__ X,
       for (int j = 0; j < 8; ++j) acc[j] = 0;
       for (long base = p + grp; base < segE; base += (long)U * GPW) {
         uint32_t idx[U];
-        uint4 v[U];
+        Row8<T> v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const long q = base + (long)u * GPW;
@@ -842,14 +988,14 @@ __device__ __forceinline__ void segsum_range(const __bf16* __restrict__ X,
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const long q = base + (long)u * GPW;
-          if (q < segE) v[u] = reinterpret_cast<const uint4*>(X + (size_t)idx[u] * D)[sub];
+          if (q < segE) v[u].load(X, idx[u], D, sub);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const long q = base + (long)u * GPW;
           if (q < segE) {
             float f[8];
-            hbmr_unpack8(v[u], f);
+            v[u].unpack(f);
             hbmr_fx_accum8(f, scale, acc);
           }
         }
@@ -869,16 +1015,16 @@ __device__ __forceinline__ void segsum_range(const __bf16* __restrict__ X,
   }
 }
 
-template <int D, int U>
+template <typename T, int D, int U>
 __global__ __launch_bounds__(256) void kmeans_segsum_kernel(
-    const __bf16* __restrict__ X, long n, const uint32_t* __restrict__ perm,
+    const T* __restrict__ X, long n, const uint32_t* __restrict__ perm,
     const uint32_t* __restrict__ offsets, int k, long chunk, long long* __restrict__ sums,
     float scale) {
   const long wid = (long)blockIdx.x * (blockDim.x / HBMR_WAVE) + threadIdx.x / HBMR_WAVE;
   const long s = wid * chunk;
   if (s >= n) return;
-  segsum_range<D, U>(X, perm, offsets, k, s, min(n, s + chunk), reinterpret_cast<u64*>(sums),
-                     scale);
+  segsum_range<T, D, U>(X, perm, offsets, k, s, min(n, s + chunk), reinterpret_cast<u64*>(sums),
+                        scale);
 }
 
 // ---- grouped sorted combiner ------------------------------------------------------
@@ -996,7 +1142,7 @@ __global__ __launch_bounds__(256) void kmeans_segsum_grouped_kernel(
   const int sidx = __builtin_amdgcn_readfirstlane(find_split(tbl, wid));
   const long n = tbl.n[sidx];
   const long s0 = (wid - tbl.blk[sidx]) * chunk;
-  segsum_range<D, U>(tbl.X[sidx], perm + tbl.off[sidx], offsets + (size_t)sidx * (k + 1), k, s0,
+  segsum_range<__bf16, D, U>(tbl.X[sidx], perm + tbl.off[sidx], offsets + (size_t)sidx * (k + 1), k, s0,
                      min(n, s0 + chunk), reinterpret_cast<u64*>(sums) + (size_t)sidx * k * D,
                      scale);
 }
@@ -1104,19 +1250,19 @@ void launch_grouped_assign(long nb, const SplitTable& t, const void* C, const fl
                      k_pad / kCK, labels, hist);
 }
 
-template <int D>
+template <typename T, int D>
 int launch_accum(const void* Xv, long n, const int32_t* labels, int k, long long* sums,
                  long long* counts, float scale, int num_cu, hipStream_t st) {
   using A = AccCfg<D>;
   if (n <= 0) return 0;
-  const __bf16* X = reinterpret_cast<const __bf16*>(Xv);
+  const T* X = reinterpret_cast<const T*>(Xv);
   const size_t small_bytes = (size_t)k * A::RS * 8 + (size_t)k * 4;
   if (small_bytes <= 76 * 1024) {
     constexpr int U = 8;
     const long per_block = 256 / A::TPP * U;
     long grid = std::min<long>((n + per_block - 1) / per_block, (long)num_cu * 2);
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL((kmeans_accum_lds_kernel<D, U>), dim3((unsigned)grid), dim3(256),
+    hipLaunchKernelGGL((kmeans_accum_lds_kernel<T, D, U>), dim3((unsigned)grid), dim3(256),
                        small_bytes, st, X, n, labels, k, sums, counts, scale);
   } else {
     // one workgroup per CU: CC u64 rows + queues + counts within ~150 KiB
@@ -1131,7 +1277,7 @@ int launch_accum(const void* Xv, long n, const int32_t* labels, int k, long long
     ppb = ((ppb + 2047) / 2048) * 2048;
     nb = (n + ppb - 1) / ppb;
     const size_t lds = (size_t)CC * A::RS * 8 + qbytes + (size_t)CC * 4;
-    hipLaunchKernelGGL((kmeans_accum_chunked_kernel<D, U>), dim3((unsigned)nb, (unsigned)nchunk),
+    hipLaunchKernelGGL((kmeans_accum_chunked_kernel<T, D, U>), dim3((unsigned)nb, (unsigned)nchunk),
                        dim3(kAccWaves * HBMR_WAVE), lds, st, X, n, labels, k, CC, ppb, sums,
                        counts, scale);
   }
@@ -1165,17 +1311,223 @@ bool set_lds_limits() {
         (void)hipGetLastError();
     };
 #define HBMR_LDS_OPTIN(fn) optin((const void*)(fn))
-    HBMR_LDS_OPTIN((kmeans_accum_lds_kernel<64, 8>));
-    HBMR_LDS_OPTIN((kmeans_accum_lds_kernel<128, 8>));
-    HBMR_LDS_OPTIN((kmeans_accum_lds_kernel<256, 8>));
-    HBMR_LDS_OPTIN((kmeans_accum_chunked_kernel<64, 8>));
-    HBMR_LDS_OPTIN((kmeans_accum_chunked_kernel<128, 8>));
-    HBMR_LDS_OPTIN((kmeans_accum_chunked_kernel<256, 8>));
+    HBMR_LDS_OPTIN((kmeans_accum_lds_kernel<__bf16, 64, 8>));
+    HBMR_LDS_OPTIN((kmeans_accum_lds_kernel<__bf16, 128, 8>));
+    HBMR_LDS_OPTIN((kmeans_accum_lds_kernel<__bf16, 256, 8>));
+    HBMR_LDS_OPTIN((kmeans_accum_chunked_kernel<__bf16, 64, 8>));
+    HBMR_LDS_OPTIN((kmeans_accum_chunked_kernel<__bf16, 128, 8>));
+    HBMR_LDS_OPTIN((kmeans_accum_chunked_kernel<__bf16, 256, 8>));
+    HBMR_LDS_OPTIN((kmeans_accum_lds_kernel<float, 64, 8>));
+    HBMR_LDS_OPTIN((kmeans_accum_lds_kernel<float, 128, 8>));
+    HBMR_LDS_OPTIN((kmeans_accum_lds_kernel<float, 256, 8>));
+    HBMR_LDS_OPTIN((kmeans_accum_chunked_kernel<float, 64, 8>));
+    HBMR_LDS_OPTIN((kmeans_accum_chunked_kernel<float, 128, 8>));
+    HBMR_LDS_OPTIN((kmeans_accum_chunked_kernel<float, 256, 8>));
     HBMR_LDS_OPTIN(kmeans_scatter_grouped_kernel);
 #undef HBMR_LDS_OPTIN
     done = true;
   }
   return done;
+}
+
+// ---------------------------------------------------------------------------
+// Exact mode, step 2: certify each point's bf16 arg-max against its fp32 data
+// and re-score the uncertain points in fp64.
+//
+// The assign kernel ranks s~_j = x~.c~_j - |c~_j|^2/2 (x~, c~ = bf16 of the fp32
+// x, c; fp32 accumulation), i.e. the bf16 distances D~_j = |x~ - c~_j|^2.  With
+// u = 2^-8 (bf16 unit roundoff: 8 significant bits)
+// |(x~ - c~_j) - (x - c_j)| <= a_j = u(|x| + |c_j|), so
+// |D~_j - D_j| <= a_j (2 sqrt(D~_j) + a_j).  In score units (D/2), adding the
+// fp32 accumulation error e_acc and the arg-max packing truncation e_pack:
+//     E_j = a_j (2 sqrt(D~_j) + a_j) / 2 + e_acc_j + e_pack_j,   |s~_j - s_j| <= E_j.
+// Any cluster t ranked below a cluster r by the kernel (s~_t <= s~_r, so
+// D~_t >= D~_r) has  s_t <= s~_r + E_max(r)  (E with |c_t| <= cmax; the score
+// falls faster than E_t grows once sqrt(D~_r) >= 2 a_max).  Hence, with the
+// kernel's top three b, s, t:
+//   1. margin(b, s) > E_b + E_max(s)                 -> b is the exact winner;
+//   2. else D_b, D_s, D_t in fp64 from the fp32 rows; the winner w of the three
+//      (ties to the lower index) is exact if (|x|^2 - D_w)/2 > s~_t + E_max(t);
+//   3. else an Elkan scan: |x - c_j| >= |c_w - c_j| - |x - c_w|, so walking w's
+//      centroid neighbours in ascending |c_w - c_j| (nbr_idx / nbr_dist, L per
+//      centroid, distances rounded down) can stop at |c_w - c_j| > r_w + r_best;
+//      a point that outruns its L neighbours scans every centroid.
+// Steps 2-3 run on groups of 16 lanes (8 features per lane, fp64, the point
+// held in registers), four flagged points per wave at a time.
+// stats += (flagged, relabelled, points that needed step 3).
+constexpr int kRefineGroup = 16;
+constexpr int kRefineMaxDp = 256;
+constexpr int kRefinePer = kRefineMaxDp / kRefineGroup;  // features per lane
+
+// Error bound E of a kernel score sc (point norm xn, |x~|^2 = x2) against a
+// centroid of norm cn, and a lower bound of sqrt(D~) for the monotonicity test.
+__device__ __forceinline__ void exact_bound(double sc, double cn, double xn, double x2, double u,
+                                            double gam, double pack_rel, double& e,
+                                            double& dlo) {
+  const double a = u * (xn + cn);
+  const double eacc = gam * (1.0 + u) * (1.0 + u) * (xn * cn + 0.5 * cn * cn);
+  const double epack = fabs(sc) * pack_rel;
+  const double slack = 2.0 * (eacc + epack) + x2 * 0x1p-22;
+  const double dhi = fmax(0.0, x2 - 2.0 * sc) + slack;
+  dlo = sqrt(fmax(0.0, x2 - 2.0 * sc - slack));
+  e = a * (2.0 * sqrt(dhi) + a) * 0.5 + eacc + epack;
+}
+
+__device__ __forceinline__ double group_sum16(double v) {
+#pragma unroll
+  for (int off = 1; off < kRefineGroup; off <<= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// |x - c_j|^2 in fp64; xv holds this lane's features 8*sub + 128*m + (0..7)
+__device__ __forceinline__ double group_dist2(const double (&xv)[kRefinePer],
+                                              const float* __restrict__ c, int d, int sub) {
+  double acc = 0.0;
+#pragma unroll
+  for (int m = 0; m < kRefinePer / 8; ++m) {
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int i = 8 * sub + 8 * kRefineGroup * m + jj;
+      if (i < d) {
+        const double e = xv[8 * m + jj] - (double)c[i];
+        acc = fma(e, e, acc);
+      }
+    }
+  }
+  return group_sum16(acc);
+}
+
+__global__ __launch_bounds__(256) void kmeans_refine_kernel(
+    const float* __restrict__ X32, long n, int d, int ldx, const float* __restrict__ xnorm,
+    const float* __restrict__ xbn2, const float* __restrict__ C32, int k,
+    const float* __restrict__ cnorm, const float* __restrict__ cmax, double pack_rel,
+    const int32_t* __restrict__ nbr_idx, const float* __restrict__ nbr_dist, int L,
+    int32_t* __restrict__ labels, const int32_t* __restrict__ cand,
+    const float* __restrict__ score, const float* __restrict__ margin,
+    unsigned long long* __restrict__ stats) {
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const double u = 0x1.004p-8;  // bf16 keeps 8 significant bits: unit roundoff 2^-8
+  const double inflate = 1.0 + 0x1p-20;
+  const double gam = (double)(d + 2) * 0x1p-23 * 1.01;
+  const double cm = (double)cmax[0] * inflate;
+  bool flag = false;
+  int b = 0, s2 = 0, s3 = 0;
+  double xn = 0.0, x2 = 0.0, sb = 0.0, m3 = 0.0;
+  if (p < n) {
+    b = labels[p];
+    s2 = cand[p];
+    s3 = cand[n + p];
+    if (s2 < k) {  // a padded runner-up (-1e30) is never close: k == 1
+      xn = (double)xnorm[p] * inflate;
+      x2 = (double)xbn2[p];
+      sb = score[p];
+      const double m2 = margin[p];
+      m3 = margin[n + p];
+      double eb, es, dl_b, dl_s;
+      exact_bound(sb, (double)cnorm[b] * inflate, xn, x2, u, gam, pack_rel, eb, dl_b);
+      exact_bound(sb - m2, cm, xn, x2, u, gam, pack_rel, es, dl_s);
+      flag = !(m2 > eb + es && dl_s >= 2.0 * u * (xn + cm));
+    }
+  }
+  unsigned long long mask = __ballot(flag);
+  if (lane == 0 && mask) atomicAdd(stats, (unsigned long long)__popcll(mask));
+  const int grp = lane / kRefineGroup, sub = lane % kRefineGroup;
+  // four groups take the flagged points of this wave in turn
+  while (mask) {
+    unsigned long long m = mask;  // the grp-th set bit of mask (or none)
+    for (int i = 0; i < grp && m; ++i) m &= m - 1;
+    const bool have = m != 0;
+    const int src = have ? __ffsll((long long)m) - 1 : 0;
+    for (int i = 0; i < 4 && mask; ++i) mask &= mask - 1;
+    const long q = __shfl(p, src);
+    const int qb = __shfl(b, src), qs = __shfl(s2, src), qt = __shfl(s3, src);
+    const double qsb = __shfl(sb, src), qm3 = __shfl(m3, src);
+    const double qxn = __shfl(xn, src), qx2 = __shfl(x2, src);
+    if (!have) continue;
+    const float* xr = X32 + (size_t)q * ldx;
+    double xv[kRefinePer];
+    double xx = 0.0;
+#pragma unroll
+    for (int mm = 0; mm < kRefinePer / 8; ++mm)
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int i = 8 * sub + 8 * kRefineGroup * mm + jj;
+        xv[8 * mm + jj] = i < d ? (double)xr[i] : 0.0;
+        xx = fma(xv[8 * mm + jj], xv[8 * mm + jj], xx);
+      }
+    xx = group_sum16(xx);
+    const bool t_real = qt < k;
+    const double db = group_dist2(xv, C32 + (size_t)qb * d, d, sub);
+    const double ds = group_dist2(xv, C32 + (size_t)qs * d, d, sub);
+    const double dt = t_real ? group_dist2(xv, C32 + (size_t)qt * d, d, sub) : 0.0;
+    int w = qb;
+    double dw = db;
+    if (ds < dw || (ds == dw && qs < w)) { w = qs; dw = ds; }
+    if (t_real && (dt < dw || (dt == dw && qt < w))) { w = qt; dw = dt; }
+    bool certified = !t_real;
+    if (t_real) {
+      double et, dl_t;
+      exact_bound(qsb - qm3, cm, qxn, qx2, u, gam, pack_rel, et, dl_t);
+      certified = 0.5 * (xx - dw) > (qsb - qm3) + et && dl_t >= 2.0 * u * (qxn + cm);
+    }
+    if (!certified) {
+      if (sub == 0) atomicAdd(stats + 2, 1ull);
+      // step 3: Elkan scan around w0 = w (exact distance r0)
+      const int w0 = w;
+      const double r0 = sqrt(dw);
+      bool done = false;
+      const int32_t* ni = nbr_idx + (size_t)w0 * L;
+      const float* nd = nbr_dist + (size_t)w0 * L;
+      for (int jj = 0; jj < L; ++jj) {
+        const double rb = sqrt(dw);
+        if ((double)nd[jj] > (r0 + rb) * (1.0 + 0x1p-40)) {
+          done = true;
+          break;
+        }
+        const int j = ni[jj];
+        const double dj = group_dist2(xv, C32 + (size_t)j * d, d, sub);
+        if (dj < dw || (dj == dw && j < w)) { w = j; dw = dj; }
+      }
+      if (!done && L < k) {
+        for (int j = 0; j < k; ++j) {  // outran the neighbour list: every centroid
+          const double dj = group_dist2(xv, C32 + (size_t)j * d, d, sub);
+          if (dj < dw || (dj == dw && j < w)) { w = j; dw = dj; }
+        }
+      }
+    }
+    if (sub == 0 && w != qb) {
+      labels[q] = w;
+      atomicAdd(stats + 1, 1ull);
+    }
+  }
+}
+
+template <int D>
+int launch_assign_top3(const void* X, long n, const void* C, const float* chalf, int k_pad,
+                       int32_t* labels, int32_t* cand, float* scores, float* margin,
+                       hipStream_t st) {
+  if (n <= 0) return 0;
+  if (k_pad % kCK) return (int)hipErrorInvalidValue;
+  if constexpr (D <= 128) {
+    if (assign_version(D) == 2) {
+      const int pts = AssignV2<D>::WAVES * 2 * 32;
+      const long nblk = (n + pts - 1) / pts;
+      if (nblk > 0x7fffffffL) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL((kmeans_assign_top3_v2_kernel<D, 2>), dim3((unsigned)nblk),
+                         dim3(AssignV2<D>::THREADS), AssignV2<D>::LDS_BYTES, st,
+                         reinterpret_cast<const __bf16*>(X), n, reinterpret_cast<const __bf16*>(C),
+                         chalf, k_pad / 32, labels, cand, scores, margin);
+      return (int)hipGetLastError();
+    }
+  }
+  const long nblk = (n + AssignCfg<D>::PTS - 1) / AssignCfg<D>::PTS;
+  if (nblk > 0x7fffffffL) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kmeans_assign_top3_kernel<D>, dim3((unsigned)nblk), dim3(kThreads),
+                     AssignCfg<D>::LDS_BYTES, st, reinterpret_cast<const __bf16*>(X), n,
+                     reinterpret_cast<const __bf16*>(C), chalf, k_pad / kCK, labels, cand, scores,
+                     margin);
+  return (int)hipGetLastError();
 }
 
 }  // namespace
@@ -1200,9 +1552,12 @@ long hbmr_kmeans_accum_workspace_bytes(long n, int k) {
   return (long)(3 * ws_align(((size_t)k + 1) * 4) + ws_align((size_t)n * 4));
 }
 
-int hbmr_kmeans_accum_bf16(const void* X, long n, int dp, const int32_t* labels, int k,
-                           long long* sums, long long* counts, int fx_shift, void* ws,
-                           long ws_bytes, int mode, hipStream_t st) {
+}  // extern "C"
+
+template <typename T>
+static int accum_impl(const void* X, long n, int dp, const int32_t* labels, int k,
+                      long long* sums, long long* counts, int fx_shift, void* ws, long ws_bytes,
+                      int mode, hipStream_t st) {
   set_lds_limits();
   const int cus = cu_count();
   const float scale = ldexpf(1.0f, fx_shift);
@@ -1240,8 +1595,8 @@ int hbmr_kmeans_accum_bf16(const void* X, long n, int dp, const int32_t* labels,
     switch (dp) {
 #define HBMR_SEG(DD)                                                                        \
   case DD:                                                                                 \
-    hipLaunchKernelGGL((kmeans_segsum_kernel<DD, 8>), dim3((unsigned)sblocks), dim3(256), 0, \
-                       st, reinterpret_cast<const __bf16*>(X), n, perm, offsets, k, chunk,  \
+    hipLaunchKernelGGL((kmeans_segsum_kernel<T, DD, 8>), dim3((unsigned)sblocks), dim3(256), \
+                       0, st, reinterpret_cast<const T*>(X), n, perm, offsets, k, chunk,    \
                        sums, scale);                                                        \
     break;
       HBMR_SEG(64)
@@ -1253,11 +1608,27 @@ int hbmr_kmeans_accum_bf16(const void* X, long n, int dp, const int32_t* labels,
     return (int)hipGetLastError();
   }
   switch (dp) {
-    case 64: return launch_accum<64>(X, n, labels, k, sums, counts, scale, cus, st);
-    case 128: return launch_accum<128>(X, n, labels, k, sums, counts, scale, cus, st);
-    case 256: return launch_accum<256>(X, n, labels, k, sums, counts, scale, cus, st);
+    case 64: return launch_accum<T, 64>(X, n, labels, k, sums, counts, scale, cus, st);
+    case 128: return launch_accum<T, 128>(X, n, labels, k, sums, counts, scale, cus, st);
+    case 256: return launch_accum<T, 256>(X, n, labels, k, sums, counts, scale, cus, st);
     default: return (int)hipErrorInvalidValue;
   }
+}
+
+extern "C" {
+
+int hbmr_kmeans_accum_bf16(const void* X, long n, int dp, const int32_t* labels, int k,
+                           long long* sums, long long* counts, int fx_shift, void* ws,
+                           long ws_bytes, int mode, hipStream_t st) {
+  return accum_impl<__bf16>(X, n, dp, labels, k, sums, counts, fx_shift, ws, ws_bytes, mode, st);
+}
+
+// Exact mode: the combiner over the fp32 points (rows of dp floats), so the
+// partial sums are the int64 fixed point of the fp32 data, not of its bf16 copy.
+int hbmr_kmeans_accum_f32(const float* X, long n, int dp, const int32_t* labels, int k,
+                          long long* sums, long long* counts, int fx_shift, void* ws,
+                          long ws_bytes, int mode, hipStream_t st) {
+  return accum_impl<float>(X, n, dp, labels, k, sums, counts, fx_shift, ws, ws_bytes, mode, st);
 }
 
 int hbmr_kmeans_update(const long long* sums, const long long* counts, int fx_shift, int k, int d,
@@ -1433,4 +1804,37 @@ int hbmr_kmeans_map_batch(int ntasks, const void* const* X, const long* n, int d
   return 0;
 }
 
+int hbmr_kmeans_assign_top3_bf16(const void* X, long n, int dp, const void* C, const float* chalf,
+                                 int k_pad, int32_t* labels, int32_t* cand, float* scores,
+                                 float* margin, hipStream_t st) {
+  if (!labels || !cand || !scores || !margin) return (int)hipErrorInvalidValue;
+  switch (dp) {
+    case 64: return launch_assign_top3<64>(X, n, C, chalf, k_pad, labels, cand, scores, margin, st);
+    case 128: return launch_assign_top3<128>(X, n, C, chalf, k_pad, labels, cand, scores, margin, st);
+    case 256: return launch_assign_top3<256>(X, n, C, chalf, k_pad, labels, cand, scores, margin, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float* xnorm,
+                           const float* xbn2, const float* C32, int k, int k_pad,
+                           const float* cnorm, const float* cmax, const int32_t* nbr_idx,
+                           const float* nbr_dist, int L, int32_t* labels, const int32_t* cand,
+                           const float* scores, const float* margin, unsigned long long* stats,
+                           hipStream_t st) {
+  if (n <= 0) return 0;
+  if (d > ldx || d > kRefineMaxDp || k <= 0 || k_pad < k || L < 1 || L > k)
+    return (int)hipErrorInvalidValue;
+  // packing truncation of the arg-max codes: lb = 4 + ceil(log2(k_pad / 32)) bits
+  int tb = 0;
+  while ((1 << tb) < k_pad / 32) ++tb;
+  const double pack_rel = ldexp(1.0, 4 + tb - 23);
+  const long blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(kmeans_refine_kernel, dim3((unsigned)blocks), dim3(256), 0, st, X32, n, d,
+                     ldx, xnorm, xbn2, C32, k, cnorm, cmax, pack_rel, nbr_idx, nbr_dist, L,
+                     labels, cand, scores, margin, stats);
+  return (int)hipGetLastError();
+}
+
 }  // extern "C"
+

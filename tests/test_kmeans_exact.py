@@ -1,0 +1,151 @@
+"""Exact K-Means mode (hbmr.kmeans.exact): top-2 MFMA assign, certification of
+the bf16 arg-max against the fp32 data with fp64 re-scoring of uncertain
+points, and the fp32-input fixed-point combiner.  GPU numerics are checked
+against fp64 (the "exact" assignment of the fp32 data) and a plain fp32
+PyTorch reference; the CPU test runs an exact-mode job on CPU slots."""
+import pytest
+import torch
+
+from hbmr.mapred.cluster import LocalCluster
+from hbmr.mapred.jobconf import JobConf
+from hbmr.models import kmeans as K
+
+
+def truth_labels(x32, c32, chunk=1 << 18):
+    """argmin_j |x - c_j|^2 in fp64 (ties to the lower index)."""
+    c = c32.double()
+    cn = (c * c).sum(1)
+    out = []
+    for a in range(0, x32.shape[0], chunk):
+        x = x32[a:a + chunk].double()
+        out.append((cn[None, :] - 2.0 * x @ c.T).argmin(1))
+    return torch.cat(out).to(torch.int32)
+
+
+def lloyd64(x32, c0, iters):
+    """Lloyd's algorithm with fp64 assignments and the framework's storage
+    rules: fixed-point (2^-24) partial sums and fp32 centroids."""
+    c = c0.double().clone()
+    q = torch.round(x32.double() * (1 << 24)).long()
+    for _ in range(iters):
+        lab = truth_labels(x32, c).long()
+        s = torch.zeros(c.shape, dtype=torch.int64, device=c.device).index_add_(0, lab, q)
+        n = torch.bincount(lab, minlength=c.shape[0]).double()[:, None]
+        c = torch.where(n > 0, (s.double() / (1 << 24)) / n.clamp(min=1), c).float().double()
+    return c
+
+
+def test_exact_mode_job_on_cpu_slots_matches_fp64_lloyd():
+    """Exact mode keeps the fp32 data on CPU slots (no bf16 storage rounding)."""
+    n, k, d = 20000, 12, 16
+    inp = f"synthetic:{n}:9"
+    conf = JobConf()
+    conf.set_boolean(K.EXACT_KEY, True)
+    with LocalCluster(conf, num_trackers=2, cpu_slots=2) as cl:
+        drv = K.KMeansDriver(cl.submit_job, lambda rj: rj._impl.jip.result[0], conf=conf, k=k,
+                             d=d, inp=inp, split_points=5000)
+        for _ in range(3):
+            drv.step()
+        got = drv.centroids()
+    x = K.synthetic_points(9, 0, n, d, k, "cpu")
+    ref = lloyd64(x, K.initial_centroids(inp, k, d), 3)
+    err = (got.double() - ref).abs().max().item()
+    assert err < 1e-4, err
+
+
+# ------------------------------------------------------------------------------ GPU
+def _blobs(n, d, k, seed, dup=2):
+    """Points of the bench distribution with k/dup true centers, so about
+    every cluster shares its blob with another centroid: many near-ties."""
+    x = K.synthetic_points(seed, 0, n, d, max(1, k // dup), "cuda")
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    c = x[torch.randperm(n, device="cuda", generator=g)[:k]].clone()
+    return x, c
+
+
+@pytest.mark.gpu
+def test_top3_assign_matches_fp32_reference():
+    from hbmr.ops import kmeans as km
+    n, d, k = 40000, 128, 256
+    x, c = _blobs(n, d, k, 3)
+    img = km.CentroidImage(c, "cuda")
+    sp = km.ExactSplit(x, km.padded_dim(d))
+    lab = torch.empty(n, dtype=torch.int32, device="cuda")
+    cand = torch.empty(2 * n, dtype=torch.int32, device="cuda")
+    sc, mg = torch.empty(n, device="cuda"), torch.empty(2 * n, device="cuda")
+    km.assign_top3(sp.xb, img, lab, cand, sc, mg)
+    # reference: fp32 scores of the bf16 operands (what the MFMA computes)
+    xb = sp.xb[:, :d].float()
+    cb = img.cbf[:k, :d].float()
+    s = xb @ cb.T + img.chalf[:k][None, :]
+    top = s.topk(3, dim=1)
+    got = torch.stack([lab.long(), cand[:n].long(), cand[n:].long()], 1)
+    # scores of the kernel's picks must equal the reference top-3 scores up to
+    # the accumulation-order / packing tolerance (ties may swap indices)
+    picked = s.gather(1, got)
+    tol = 1e-3 * top.values[:, :1].abs().clamp(min=1)
+    assert ((picked - top.values).abs() <= tol).all(1).float().mean().item() > 0.9999
+    # (the packed arg-max truncates 4 + log2(k/32) mantissa bits: near-equal
+    # scores may swap, which the score check above already bounds)
+    assert (got == top.indices).all(1).float().mean().item() > 0.995
+    ref_m = top.values[:, :1] - top.values[:, 1:]
+    got_m = torch.stack([mg[:n], mg[n:]], 1)
+    assert ((got_m - ref_m).abs() <= tol + 1e-2).all(1).float().mean().item() > 0.999
+    assert torch.equal(lab, km.assign(sp.xb, img))       # same winner as the plain kernel
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d", [64, 128])
+def test_exact_assign_agrees_with_fp64(d):
+    from hbmr.ops import kmeans as km
+    n, k = 1_000_000, 256
+    x, c = _blobs(n, d, k, 11)
+    img = km.CentroidImage(c, "cuda")
+    sp = km.ExactSplit(x, km.padded_dim(d))
+    truth = truth_labels(x, c)
+    bf16 = km.assign(sp.xb, img)
+    stats = torch.zeros(3, dtype=torch.int64, device="cuda")
+    lab = km.assign_exact(sp, img, stats)
+    agree_exact = (lab == truth).float().mean().item()
+    agree_bf16 = (bf16 == truth).float().mean().item()
+    flagged, relabelled, rescans = stats.tolist()
+    print(f"d={d}: bf16 agreement {agree_bf16:.6f}, exact {agree_exact:.7f}, "
+          f"flagged {flagged / n:.4f}, relabelled {relabelled}, neighbour scans {rescans}")
+    assert int((lab != truth).sum()) <= 1          # fp64 ties aside: the exact assignment
+    assert 0 < flagged < n and relabelled == int((bf16 != lab).sum())
+
+
+@pytest.mark.gpu
+def test_accum_f32_is_fixed_point_of_fp32_data():
+    from hbmr.ops import kmeans as km
+    n, d, k = 300000, 128, 1024
+    x = torch.randn(n, d, device="cuda") * 30
+    lab = torch.randint(0, k, (n,), device="cuda", dtype=torch.int32)
+    sums = torch.zeros(k, d, dtype=torch.int64, device="cuda")
+    counts = torch.zeros(k, dtype=torch.int64, device="cuda")
+    km.accumulate(x.contiguous(), lab, k, sums, counts)
+    q = torch.round(x.double() * (1 << km.FX_SHIFT)).long()     # round-half-even
+    ref = torch.zeros(k, d, dtype=torch.int64, device="cuda").index_add_(0, lab.long(), q)
+    assert torch.equal(sums, ref)
+    assert torch.equal(counts, torch.bincount(lab.long(), minlength=k))
+
+
+@pytest.mark.gpu
+def test_exact_mode_job_matches_fp64_lloyd():
+    n, k, d, sp = 400000, 64, 128, 100000
+    inp = f"synthetic:{n}:5"
+    conf = JobConf()
+    conf.set_boolean(K.EXACT_KEY, True)
+    conf.set(K.NCENTERS_KEY, str(k // 2))     # duplicated blobs: near-ties
+    with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=0) as cl:
+        drv = K.KMeansDriver(cl.submit_job, lambda rj: rj._impl.jip.result[0], conf=conf, k=k,
+                             d=d, inp=inp, split_points=sp)
+        for _ in range(3):
+            r = drv.step()
+        got = drv.centroids()
+        flagged = r["counters"].get("KMEANS", "EXACT_FLAGGED_POINTS")
+    x = K.synthetic_points(5, 0, n, d, k // 2, "cuda")
+    ref = lloyd64(x, K.initial_centroids(inp, k, d, centers=k // 2).cuda(), 3)
+    # identical assignments: centroids differ only by the 2^-24 fixed-point rounding
+    assert (got.cuda().double() - ref).abs().max().item() < 1e-5
+    assert flagged > 0
