@@ -277,11 +277,21 @@ class TaskTracker:
         with open(confp, "w") as fh:
             js.conf.write_xml(fh)
         args = shlex.split(script) + files + [confp]
-        prog = js.conf.get("hadoop.pipes.executable")
+        # the program the attempt ran (GPU attempts: the GPU binary)
+        on_gpu = bool(getattr(run.spec, "run_on_gpu", False))
+        prog = (js.conf.get("hadoop.pipes.gpu.executable") if on_gpu else None) or \
+            js.conf.get("hadoop.pipes.executable") or js.conf.get("hadoop.pipes.gpu.executable")
         if prog:
             args.append(prog)
+        # where a Pipes child of this attempt ran (and would have dumped core)
+        import glob
+        env = dict(os.environ)
+        import tempfile
+        base = js.conf.get("hbmr.local.scratch") or tempfile.gettempdir()
+        dirs = [d for d in glob.glob(os.path.join(base, f"_pipes_{aid}_*")) if os.path.isdir(d)]
+        env["HBMR_DEBUG_DIRS"] = ":".join(dirs)
         try:
-            r = subprocess.run(args, cwd=logd, capture_output=True, text=True,
+            r = subprocess.run(args, cwd=logd, capture_output=True, text=True, env=env,
                                timeout=js.conf.get_int("hbmr.task.debug.script.timeout.s", 60))
             out = r.stdout + r.stderr
         except (OSError, subprocess.TimeoutExpired) as e:

@@ -34,7 +34,11 @@ IDLE = "hbmr.pipes.child.idle.s"
 
 
 def _work_dir(job, suffix):
-    base = job.get("mapred.work.output.dir") or job.get("hbmr.local.scratch") or "/tmp"
+    """The Pipes child's working directory (its cwd: core dumps land here; the
+    task debug script looks for them, TaskTracker._run_debug_script).  Not the
+    task's output work dir, whose contents are committed as job output."""
+    import tempfile
+    base = job.get("hbmr.local.scratch") or tempfile.gettempdir()
     d = os.path.join(base, f"_pipes_{job.get('mapred.task.id', 'task')}_{suffix}")
     os.makedirs(d, exist_ok=True)
     return d

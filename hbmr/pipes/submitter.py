@@ -22,12 +22,28 @@ from .runner import (JAVA_MAPPER, JAVA_PARTITIONER, JAVA_REDUCER, JAVA_RR, JAVA_
 log = logging.getLogger("hbmr.pipes")
 
 
+DEFAULT_DEBUG_SCRIPT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "debug",
+                                    "pipes-default-script")
+
+
+def _exe(path):
+    """``<path>#<name>`` (DistributedCache symlink form) -> (abs path, name)."""
+    p, _, link = str(path).partition("#")
+    return os.path.abspath(p), link or None
+
+
 def set_executable(conf, path):
-    conf.set_cpu_executable(os.path.abspath(path))
+    p, link = _exe(path)
+    conf.set_cpu_executable(p)
+    if link:
+        conf.set("hbmr.pipes.executable.link", link)
 
 
 def set_gpu_executable(conf, path):
-    conf.set_gpu_executable(os.path.abspath(path))
+    p, link = _exe(path)
+    conf.set_gpu_executable(p)
+    if link:
+        conf.set("hbmr.pipes.gpu.executable.link", link)
 
 
 def setup_pipes_job(conf: JobConf):
@@ -58,6 +74,12 @@ def setup_pipes_job(conf: JobConf):
     cpu, gpu = conf.get_cpu_executable(), conf.get_gpu_executable()
     if not cpu and not gpu:
         raise ValueError("No application program defined (-program/-cpubin/-gpubin).")
+    # executables given as <path>#<name>: default gdb-style debug scripts for
+    # failed map and reduce attempts (Submitter.java:341-347)
+    if conf.get("hbmr.pipes.executable.link") or conf.get("hbmr.pipes.gpu.executable.link"):
+        for key in ("mapred.map.task.debug.script", "mapred.reduce.task.debug.script"):
+            if conf.get(key) is None:
+                conf.set(key, DEFAULT_DEBUG_SCRIPT)
     for exe in (cpu, gpu):
         if exe and not os.access(exe, os.X_OK):
             raise FileNotFoundError(f"pipes executable {exe} is not executable")

@@ -145,3 +145,30 @@ def test_text_protocol_debug_mode():
     assert r.returncode == 0, r.stderr
     assert [ln for ln in r.stdout.splitlines() if ln.startswith("output")] == \
         ["output\ta\t3", "output\tb\t5"]
+
+
+def test_pipes_default_debug_script_reports_core(tmp_path):
+    """Executables given as <path>#<name> get the default gdb-style debug
+    script (Submitter.java:341-347): a failed attempt's diagnostics carry the
+    core file found in the Pipes child's working directory."""
+    crash = tmp_path / "crasher"
+    crash.write_text("#!/bin/sh\necho dying >&2\necho fake > core.4242\nexit 3\n")
+    crash.chmod(0o755)
+    conf, out, _ = _job(tmp_path, "wordcount-simple", reduces=1)
+    conf.unset("hadoop.pipes.executable")
+    submitter.set_executable(conf, f"{crash}#crasher")
+    conf.set("hbmr.local.scratch", str(tmp_path / "scratch"))
+    conf.set_int("mapred.map.max.attempts", 1)
+    conf.set_num_map_tasks(1)
+    submitter.setup_pipes_job(conf)
+    assert conf.get("hadoop.pipes.executable") == str(crash)
+    assert conf.get("mapred.map.task.debug.script") == submitter.DEFAULT_DEBUG_SCRIPT
+    with LocalCluster(JobConf(), num_trackers=1) as cl:
+        rj = submitter.submit_job(conf, cluster=cl)
+        rj.waitForCompletion(60)
+        assert not rj.isSuccessful()
+        jip = rj._impl.jip
+        diags = [a.diagnostic for t in jip.maps for a in t.attempts.values() if a.diagnostic]
+    text = "\n".join(diags)
+    assert "Debug script output" in text and "core file:" in text and "core.4242" in text
+    assert "dying" in text          # the child's stderr tail
