@@ -128,8 +128,8 @@ class Configuration:
 
     # -- raw access ----------------------------------------------------------
     def _substitute(self, value):
-        if value is None:
-            return None
+        if value is None or "${" not in value:
+            return value
         for _ in range(_MAX_SUBST):
             m = _VAR.search(value)
             if not m:

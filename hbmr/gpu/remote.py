@@ -32,6 +32,7 @@ import time
 
 from ..mapred import protocol as P
 from ..mapred.counters import Counters
+from ..utils.trace import TRACE
 from .worker import recv_msg, send_msg
 
 log = logging.getLogger("hbmr.gpu.remote")
@@ -89,6 +90,9 @@ class RemoteGpuRuntime:
         tr = self.tracker
         parent, child = socket.socketpair()
         env = dict(os.environ)
+        if "{rank}" in env.get("HBMR_TRACE", ""):
+            # the worker's own trace dump beside the tracker's
+            env["HBMR_TRACE"] = env["HBMR_TRACE"].replace("{rank}", "{rank}_worker")
         env["PYTHONPATH"] = _ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH")
                                      else "")
         self.proc = subprocess.Popen([sys.executable, "-m", "hbmr.gpu.worker",
@@ -224,12 +228,26 @@ class RemoteGpuRuntime:
         by_job: dict = {}
         for r in runs:
             by_job.setdefault(r.spec.job_id, []).append(r)
+        if TRACE.on:
+            TRACE.instant("remote.dispatch", kind=kind, n=len(runs))
         try:
             for jid, rs in by_job.items():
                 self._ensure_job(rs[0])
                 if kind == "maps":
-                    send_msg(self.sock, ("maps", jid, [r.spec.to_dict() for r in rs]),
-                             self._send_lock)
+                    s0 = rs[0].spec
+                    common = (s0.is_map, s0.run_on_gpu, s0.gpu_device_id, s0.num_maps,
+                              s0.num_reduces, s0.collective)
+                    if all((r.spec.is_map, r.spec.run_on_gpu, r.spec.gpu_device_id,
+                            r.spec.num_maps, r.spec.num_reduces, r.spec.collective) == common
+                           and not r.spec.map_outputs and not r.spec.profile_fraction
+                           for r in rs):
+                        # a bulk launch: shared fields once, (attempt, partition, split) each
+                        send_msg(self.sock, ("maps_c", jid, common,
+                                             [(r.spec.attempt_id, r.spec.partition, r.spec.split)
+                                              for r in rs]), self._send_lock)
+                    else:
+                        send_msg(self.sock, ("maps", jid, [r.spec.to_dict() for r in rs]),
+                                 self._send_lock)
                 else:
                     for r in rs:
                         send_msg(self.sock, (kind, r.spec.to_dict()), self._send_lock)

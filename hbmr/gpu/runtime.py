@@ -60,6 +60,7 @@ class GpuRuntime:
         self.devices = {d: _Device(d, max(1, slots_per_device)) for d in devices}
         self.slots_per_device = max(1, slots_per_device)
         self.max_batch = max(1, tracker.conf.get_int("hbmr.gpu.batch.max", 64))
+        self.first_chunk = max(1, tracker.conf.get_int("hbmr.gpu.first.chunk", 4))
         self._stop = threading.Event()
         reserve = tracker.conf.get_float("hbmr.gpu.hbm.reserve.gb", 16.0) * (1 << 30)
         for d, dev in self.devices.items():
@@ -98,17 +99,28 @@ class GpuRuntime:
                 s.done_q.put(None)
 
     def submit(self, run):
-        d = run.spec.gpu_device_id
-        if d not in self.devices:
-            # placement bug guard: never silently run on another device (B1)
-            self.tracker._finish(run, P.FAILED, f"device {d} not on tracker {self.tracker.name}")
-            return
-        self.devices[d].q.put(run)
+        self.submit_many([run])
+
+    def submit_many(self, runs):
+        """Queue attempts; a job's bulk launch arrives as one list, so the
+        launcher plans the whole batch at once (first_chunk)."""
+        by_dev: dict = {}
+        for run in runs:
+            d = run.spec.gpu_device_id
+            if d not in self.devices:
+                # placement bug guard: never silently run on another device (B1)
+                self.tracker._finish(run, P.FAILED,
+                                     f"device {d} not on tracker {self.tracker.name}")
+                continue
+            by_dev.setdefault(d, []).append(run)
+        for d, rs in by_dev.items():
+            self.devices[d].q.put(rs)
 
     # -- launcher -----------------------------------------------------------------------
     def _drain(self, dev: _Device, first):
-        """first + whatever else is queued right now (up to max_batch)."""
-        runs = [first]
+        """first + whatever else is queued right now (queue items are lists of
+        runs; at least everything of ``first``, then up to max_batch)."""
+        runs = list(first)
         while len(runs) < self.max_batch:
             try:
                 r = dev.q.get_nowait()
@@ -117,7 +129,7 @@ class GpuRuntime:
             if r is None:
                 dev.q.put(None)
                 break
-            runs.append(r)
+            runs.extend(r)
         return runs
 
     def _worker(self, dev: _Device):
@@ -138,11 +150,20 @@ class GpuRuntime:
             for runs in groups.values():
                 js = runs[0].job
                 sj = js.split_job
-                # split a job's batch over the slots so streams overlap
-                nslot = len(dev.slots) if hasattr(sj, "map_gpu_batch") else len(runs)
-                per = max(1, -(-len(runs) // max(1, nslot)))
-                for i in range(0, len(runs), per):
-                    self._launch_batch(dev, runs[i:i + per], js, sj, SplitSpec, TaskContext)
+                i = 0
+                if hasattr(sj, "map_gpu_batch") and len(runs) > 2 * self.first_chunk and \
+                        not any(s.inflight for s in dev.slots):
+                    # idle device: start it on a few tasks while the rest are
+                    # prepared (each task costs ~20 µs of host work to launch)
+                    self._launch_batch(dev, runs[:self.first_chunk], js, sj, SplitSpec,
+                                       TaskContext)
+                    i = self.first_chunk
+                # split the rest of the job's batch over the slots so streams overlap
+                rest = len(runs) - i
+                nslot = len(dev.slots) if hasattr(sj, "map_gpu_batch") else rest
+                per = min(self.max_batch, max(1, -(-rest // max(1, nslot))))
+                for j in range(i, len(runs), per):
+                    self._launch_batch(dev, runs[j:j + per], js, sj, SplitSpec, TaskContext)
 
     def _launch_batch(self, dev, runs, js, sj, SplitSpec, TaskContext):  # noqa: N803
         tracker = self.tracker
@@ -154,6 +175,8 @@ class GpuRuntime:
                 raise RuntimeError("GPU map of a non split-level job requires the Pipes GPU "
                                    "runner (hadoop.pipes.gpu.executable)")
             now = time.time()
+            if TRACE.on:
+                TRACE.instant("gpu.prep", n=len(runs))
             ctxs, datas = [], []
             prefetched = self._prefetch_hosts(dev, runs, sj, SplitSpec)
             with torch.cuda.stream(slot.stream):
@@ -186,6 +209,8 @@ class GpuRuntime:
                     return
                 ev0 = torch.cuda.Event(enable_timing=True)
                 ev1 = torch.cuda.Event(enable_timing=True)
+                if TRACE.on:
+                    TRACE.instant("gpu.native", n=len(live))
                 ev0.record(slot.stream)
                 if len(live) > 1 and hasattr(sj, "map_gpu_batch"):
                     outs = sj.map_gpu_batch(ctxs, datas)

@@ -113,14 +113,22 @@ class SimulatedGpuRuntime:
             self._done_cv.notify_all()
 
     def submit(self, run):
-        d = run.spec.gpu_device_id
-        if d not in self.devices:
-            self.tracker._finish(run, P.FAILED, f"device {d} not on tracker {self.tracker.name}")
-            return
-        self.devices[d].q.put(run)
+        self.submit_many([run])
+
+    def submit_many(self, runs):
+        by_dev: dict = {}
+        for run in runs:
+            d = run.spec.gpu_device_id
+            if d not in self.devices:
+                self.tracker._finish(run, P.FAILED,
+                                     f"device {d} not on tracker {self.tracker.name}")
+                continue
+            by_dev.setdefault(d, []).append(run)
+        for d, rs in by_dev.items():
+            self.devices[d].q.put(rs)
 
     def _drain(self, dev, first):
-        runs = [first]
+        runs = list(first)
         while len(runs) < self.max_batch:
             try:
                 r = dev.q.get_nowait()
@@ -129,7 +137,7 @@ class SimulatedGpuRuntime:
             if r is None:
                 dev.q.put(None)
                 break
-            runs.append(r)
+            runs.extend(r)
         return runs
 
     def _worker(self, dev: _SimDevice):

@@ -45,6 +45,8 @@ import sys
 import threading
 import time
 
+from ..utils.trace import TRACE
+
 _LEN = struct.Struct(">I")
 log = logging.getLogger("hbmr.gpu.worker")
 
@@ -246,14 +248,31 @@ def serve(sock):
             host.runs[spec.attempt_id] = r
         return r
 
+    def _runs_compact(jid, common, tasks):
+        is_map, on_gpu, dev_id, nm, nr, coll = common
+        js = _job(jid)
+        now = time.time()
+        out = []
+        for aid, part, split in tasks:
+            spec = P.TaskSpec(aid, jid, is_map, part, on_gpu, dev_id, split, nm, nr, [], coll)
+            st = P.TaskStatus(aid, is_map, P.RUNNING, 0.0, on_gpu, dev_id, now)
+            out.append(_Running(spec, st, js, _Flag()))
+        with host._lock:
+            for r in out:
+                host.runs[r.spec.attempt_id] = r
+        return out
+
     while True:
         msg = recv_msg(sock)
         if msg is None:
             break                       # the tracker is gone
         typ = msg[0]
-        if typ == "maps":
-            for d in msg[2]:
-                runtime.submit(_run(d))
+        if TRACE.on:
+            TRACE.instant("wk.recv", kind=typ)
+        if typ == "maps_c":
+            runtime.submit_many(_runs_compact(msg[1], msg[2], msg[3]))
+        elif typ == "maps":
+            runtime.submit_many([_run(d) for d in msg[2]])
         elif typ == "job":
             jid, conf_dict = msg[1], msg[2]
             if jid not in host.jobs:
@@ -262,6 +281,8 @@ def serve(sock):
                 for k, v in conf_dict.items():
                     conf.set(k, v)
                 host.jobs[jid] = JobState(jid, conf)
+                if TRACE.on:
+                    TRACE.instant("wk.job_ready")
         elif typ == "cpu":
             cpu_pool.submit(run_split_cpu_map, host, _run(msg[1], threading.Event()))
         elif typ == "reduce":

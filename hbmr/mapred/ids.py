@@ -8,19 +8,58 @@
 from __future__ import annotations
 
 import re
-from dataclasses import dataclass
 
 
-@dataclass(frozen=True, order=True)
-class JobID:
-    jt: str
-    id: int
+class _ID:
+    """Immutable id with value semantics (eq / order / hash by its fields) and
+    its Hadoop string form computed once; plain slots instead of a frozen
+    dataclass (ids are built per task and attempt on the scheduling path)."""
+    __slots__ = ()
 
-    def __post_init__(self):
-        object.__setattr__(self, "_s", f"job_{self.jt}_{self.id:04d}")
+    def _key(self):
+        raise NotImplementedError
+
+    def __eq__(self, o):
+        return type(o) is type(self) and self._key() == o._key()
+
+    def __lt__(self, o):
+        return self._key() < o._key()
+
+    def __le__(self, o):
+        return self._key() <= o._key()
+
+    def __gt__(self, o):
+        return self._key() > o._key()
+
+    def __ge__(self, o):
+        return self._key() >= o._key()
+
+    def __hash__(self):
+        return hash(self._s)
 
     def __str__(self):
         return self._s
+
+    def __setattr__(self, k, v):
+        raise AttributeError(f"{type(self).__name__} is immutable")
+
+    def __reduce__(self):
+        return (type(self), self._key())
+
+
+class JobID(_ID):
+    __slots__ = ("jt", "id", "_s")
+
+    def __init__(self, jt: str, id: int):  # noqa: A002
+        object.__setattr__(self, "jt", jt)
+        object.__setattr__(self, "id", id)
+        object.__setattr__(self, "_s", f"job_{jt}_{id:04d}")
+
+    def _key(self):
+        return (self.jt, self.id)
+
+    def __repr__(self):
+        return f"JobID(jt={self.jt!r}, id={self.id!r})"
 
     @classmethod
     def for_name(cls, s: str) -> "JobID":
@@ -32,18 +71,21 @@ class JobID:
     forName = for_name  # noqa: N815
 
 
-@dataclass(frozen=True, order=True)
-class TaskID:
-    job: JobID
-    is_map: bool
-    id: int
+class TaskID(_ID):
+    __slots__ = ("job", "is_map", "id", "_s")
 
-    def __post_init__(self):
-        object.__setattr__(self, "_s", f"task_{self.job.jt}_{self.job.id:04d}_"
-                                       f"{'m' if self.is_map else 'r'}_{self.id:06d}")
+    def __init__(self, job: JobID, is_map: bool, id: int):  # noqa: A002
+        object.__setattr__(self, "job", job)
+        object.__setattr__(self, "is_map", is_map)
+        object.__setattr__(self, "id", id)
+        object.__setattr__(self, "_s", f"task_{job.jt}_{job.id:04d}_"
+                                       f"{'m' if is_map else 'r'}_{id:06d}")
 
-    def __str__(self):
-        return self._s
+    def _key(self):
+        return (self.job, self.is_map, self.id)
+
+    def __repr__(self):
+        return f"TaskID(job={self.job!r}, is_map={self.is_map!r}, id={self.id!r})"
 
     @classmethod
     def for_name(cls, s: str) -> "TaskID":
@@ -56,16 +98,19 @@ class TaskID:
         return self.is_map
 
 
-@dataclass(frozen=True, order=True)
-class TaskAttemptID:
-    task: TaskID
-    id: int
+class TaskAttemptID(_ID):
+    __slots__ = ("task", "id", "_s")
 
-    def __post_init__(self):
-        object.__setattr__(self, "_s", "attempt" + str(self.task)[4:] + f"_{self.id}")
+    def __init__(self, task: TaskID, id: int):  # noqa: A002
+        object.__setattr__(self, "task", task)
+        object.__setattr__(self, "id", id)
+        object.__setattr__(self, "_s", "attempt" + task._s[4:] + f"_{id}")
 
-    def __str__(self):
-        return self._s
+    def _key(self):
+        return (self.task, self.id)
+
+    def __repr__(self):
+        return f"TaskAttemptID(task={self.task!r}, id={self.id!r})"
 
     @property
     def job(self):

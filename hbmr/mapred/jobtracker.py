@@ -656,6 +656,8 @@ class JobTracker:
         self.job_tokens.add_job(jid)
         self._persist_job(jid, conf)
         jip = JobInProgress(self, jid, conf)
+        if TRACE.on:
+            TRACE.instant("jt.jip_created")
         too_big = self._memory_violation(conf)
         with self.lock:
             self.jobs[str(jid)] = jip
@@ -666,6 +668,8 @@ class JobTracker:
                              user=conf.get_user())
             try:
                 jip.init_tasks()
+                if TRACE.on:
+                    TRACE.instant("jt.tasks_inited", maps=len(jip.maps))
             except Exception as e:  # noqa: BLE001
                 log.exception("job init failed")
                 self._finish_job(jip, FAILED, f"init failed: {type(e).__name__}: {e}")
@@ -829,6 +833,8 @@ class JobTracker:
                     tr.extra_actions = []
                 if tr.status.healthy and not tr.blacklisted:
                     resp["actions"] += self.scheduler.assign_tasks(tr)
+                    if TRACE.on:
+                        TRACE.instant("jt.assigned", n=len(resp["actions"]))
         tr.wake = False
         resp["more"] = tr.more
         return resp

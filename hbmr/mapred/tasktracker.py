@@ -559,6 +559,8 @@ class TaskTracker:
                 self.gpu_pipes_pool.submit(self._run_cpu_map, r)
             return
         submit_many = getattr(self.gpu_runtime, "submit_many", None)
+        if TRACE.on:
+            TRACE.instant("tt.launch_batch", n=len(runs))
         if submit_many is not None:
             submit_many(runs)
         else:
