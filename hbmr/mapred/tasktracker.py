@@ -546,26 +546,34 @@ class TaskTracker:
         dev = act["device"]
         nm, nr, coll = act["num_maps"], act["num_reduces"], act["collective"]
         now = time.time()
-        runs = []
-        for aid, part, split in act["tasks"]:
-            spec = P.TaskSpec(aid, jid, True, part, True, dev, split, nm, nr, (), coll)
-            st = P.TaskStatus(aid, True, P.RUNNING, 0.0, True, dev, now)
-            runs.append(_Running(spec, st, js, _Flag()))
-        with self._lock:
-            for r in runs:
-                self.running[r.spec.attempt_id] = r
-        if js.split_job is None or self.gpu_runtime is None:
-            for r in runs:      # not a split job: the per-attempt GPU Pipes path
-                self.gpu_pipes_pool.submit(self._run_cpu_map, r)
-            return
-        submit_many = getattr(self.gpu_runtime, "submit_many", None)
-        if TRACE.on:
-            TRACE.instant("tt.launch_batch", n=len(runs))
-        if submit_many is not None:
-            submit_many(runs)
-        else:
-            for r in runs:
-                self.gpu_runtime.submit(r)
+        tasks = act["tasks"]
+        split_job = js.split_job is not None and self.gpu_runtime is not None
+        submit_many = getattr(self.gpu_runtime, "submit_many", None) if split_job else None
+        # an idle device starts on the first few tasks while the rest are built
+        # (per-task bookkeeping is a few µs here and again in the GPU worker)
+        first = self.conf.get_int("hbmr.gpu.first.chunk", 4) if submit_many else len(tasks)
+        for lo, hi in ((0, min(first, len(tasks))), (min(first, len(tasks)), len(tasks))):
+            if lo >= hi:
+                continue
+            runs = []
+            for aid, part, split in tasks[lo:hi]:
+                spec = P.TaskSpec(aid, jid, True, part, True, dev, split, nm, nr, (), coll)
+                st = P.TaskStatus(aid, True, P.RUNNING, 0.0, True, dev, now)
+                runs.append(_Running(spec, st, js, _Flag()))
+            with self._lock:
+                for r in runs:
+                    self.running[r.spec.attempt_id] = r
+            if not split_job:
+                for r in runs:      # not a split job: the per-attempt GPU Pipes path
+                    self.gpu_pipes_pool.submit(self._run_cpu_map, r)
+                continue
+            if TRACE.on:
+                TRACE.instant("tt.launch_batch", n=len(runs))
+            if submit_many is not None:
+                submit_many(runs)
+            else:
+                for r in runs:
+                    self.gpu_runtime.submit(r)
 
     def _maybe_inject_fault(self, run):
         if self.fault_p > 0 and self._rng.random() < self.fault_p:

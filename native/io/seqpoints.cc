@@ -10,8 +10,14 @@
 //                            so the split goes to HBM in one hipMemcpyAsync)
 //
 // The file→HBM loader of SURVEY.md §2.6 (NativeIO row): no per-record Python.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
 #include <cstdint>
 #include <cstring>
+#include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -79,11 +85,107 @@ long hbmr_seq_count_points(const char* path, long start, long length) {
   }
 }
 
+}  // extern "C"
+
+namespace {
+
+// Uncompressed files: parse the records in place from a populated read-only
+// mapping of the split's bytes (no per-record stdio reads or string copies) and
+// byte-swap each vector straight into `out` (the loop vectorises to vpshufb).
+// Same boundary rule as SeqSplitReader: after syncing to the first marker at
+// or after `start`, records are taken until one that starts at or past the
+// split end is preceded by a sync marker.
+long read_points_mapped(hbmr::io::SeqReader& r, long start, long length, int d, float* out,
+                        long cap) {
+  const int64_t flen = r.file_length();
+  const int64_t end = start + length;
+  if (start > r.position()) r.sync_to(start);
+  const int64_t pos0 = r.position();
+  if (pos0 >= end || pos0 >= flen) return 0;
+  const long page = sysconf(_SC_PAGESIZE);
+  const int64_t map_off = pos0 / page * page;
+  const int fd = open(r.path().c_str(), O_RDONLY);
+  if (fd < 0) throw std::runtime_error("cannot open " + r.path());
+  struct Map {
+    int fd;
+    void* p = MAP_FAILED;
+    size_t n = 0;
+    ~Map() {
+      if (p != MAP_FAILED) munmap(p, n);
+      close(fd);
+    }
+  } m{fd};
+  // the split's bytes (+1 MiB for the records up to the next sync marker past
+  // its end) populated in one go; the rest of the file only if the parse runs on
+  int64_t mapped = std::min<int64_t>(flen - map_off, end - map_off + (1 << 20));
+  m.n = (size_t)mapped;
+  m.p = mmap(nullptr, m.n, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, map_off);
+  if (m.p == MAP_FAILED) throw std::runtime_error("mmap failed for " + r.path());
+  const uint8_t* b = static_cast<const uint8_t*>(m.p) - map_off;  // b[file offset]
+  auto need = [&](int64_t upto) {  // bytes [.., upto) must be mapped
+    if (upto <= map_off + mapped) return;
+    munmap(m.p, m.n);
+    mapped = flen - map_off;
+    m.n = (size_t)mapped;
+    m.p = mmap(nullptr, m.n, PROT_READ, MAP_PRIVATE, fd, map_off);
+    if (m.p == MAP_FAILED) throw std::runtime_error("mmap failed for " + r.path());
+    b = static_cast<const uint8_t*>(m.p) - map_off;
+  };
+  const uint8_t* sync = r.sync_bytes();
+  const size_t rec_val = 4 + 4 * (size_t)d;
+  int64_t pos = pos0;
+  long n = 0;
+  while (n < cap && pos + 4 <= flen) {
+    const int64_t rec_pos = pos;
+    bool sync_seen = false;
+    need(pos + 4);
+    int32_t len = (int32_t)be32(b + pos);
+    if (len == -1) {
+      if (pos + 4 + 16 > flen) throw std::runtime_error(r.path() + ": sync check failure");
+      need(pos + 24);
+      if (memcmp(b + pos + 4, sync, 16) != 0)
+        throw std::runtime_error(r.path() + ": sync check failure");
+      sync_seen = true;
+      pos += 20;
+      if (pos + 4 > flen) break;
+      len = (int32_t)be32(b + pos);
+    }
+    if (rec_pos >= end && sync_seen) break;
+    if (pos + 8 > flen) throw std::runtime_error("truncated record");
+    const int32_t klen = (int32_t)be32(b + pos + 4);
+    if (klen < 0 || klen > len || pos + 8 + len > flen) throw std::runtime_error("corrupt record");
+    need(pos + 8 + len);
+    const uint8_t* v = b + pos + 8 + klen;
+    if ((size_t)(len - klen) < rec_val || (int)be32(v) != d)
+      throw std::runtime_error("point of wrong dimension");
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(v + 4);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(out + (size_t)n * d);
+    for (int j = 0; j < d; ++j) {
+      uint32_t u;
+      memcpy(&u, src + j, 4);
+      dst[j] = __builtin_bswap32(u);
+    }
+    pos += 8 + len;
+    ++n;
+  }
+  return n;
+}
+
+}  // namespace
+
+extern "C" {
+
 // Decode up to `cap` records of the split into out[cap, d] (fp32); returns the
 // count, or -1 on error (wrong dimension, I/O).
 long hbmr_seq_read_points(const char* path, long start, long length, int d, float* out,
                           long cap) {
   try {
+    {
+      hbmr::io::SeqReader r(path);
+      if (r.compression() == hbmr::io::Compression::NONE &&
+          getenv("HBMR_SEQ_NO_MMAP") == nullptr)
+        return read_points_mapped(r, start, length, d, out, cap);
+    }
     hbmr::io::SeqSplitReader rr(path, start, length);
     std::string k, v;
     long n = 0;

@@ -43,6 +43,8 @@ class SeqReader {
   Compression compression() const { return comp_; }
   int64_t header_end() const { return header_end_; }
   int64_t file_length() const { return file_len_; }
+  const uint8_t* sync_bytes() const { return sync_; }
+  const std::string& path() const { return path_; }
 
   int64_t position() const;
   void seek(int64_t pos);

@@ -131,3 +131,25 @@ def test_gpu_pipes_binary_is_reused_and_keeps_splits_in_hbm(tmp_path):
     hits = [h["counters"].get("KMEANS", "GPU_SPLIT_CACHE_HITS") for h in drv.history]
     assert hits[0] == 0 and hits[1] == 3 and hits[2] == 3
     POOL.close_all()
+
+
+def test_native_mapped_reader_matches_stream_reader_on_random_splits(tmp_path, monkeypatch):
+    """The mmap fast path of hbmr_seq_read_points keeps the split boundary rule
+    of the stdio SequenceFile reader: any cut of the file yields every record
+    exactly once, identically on both paths."""
+    import numpy as np
+
+    from hbmr.io import nativeio
+    x = K.synthetic_points(4, 0, 5000, 16, 4, "cpu").numpy()
+    p = tmp_path / "p.seq"
+    nativeio.write_points(p, x)
+    size = os.path.getsize(p)
+    rng = np.random.default_rng(0)
+    for trial in range(12):
+        cuts = sorted({0, size, *rng.integers(1, size, size=int(rng.integers(1, 9))).tolist()})
+        mapped = [nativeio.read_points(p, a, b - a, 16) for a, b in zip(cuts, cuts[1:])]
+        monkeypatch.setenv("HBMR_SEQ_NO_MMAP", "1")
+        stream = [nativeio.read_points(p, a, b - a, 16) for a, b in zip(cuts, cuts[1:])]
+        monkeypatch.delenv("HBMR_SEQ_NO_MMAP")
+        assert [m.shape[0] for m in mapped] == [s.shape[0] for s in stream], cuts
+        assert np.array_equal(np.concatenate(mapped), x), trial
