@@ -54,6 +54,40 @@ class _Device:
         self.last_error = ""
 
 
+class _NoPrefetch:
+    @staticmethod
+    def take(key):
+        return None
+
+
+class _Prefetch:
+    """Host buffers of cold splits decoded ahead of their tasks (in task order,
+    at most ``window`` decoded or in flight)."""
+
+    def __init__(self, pool, sj, cold, window):
+        self.pool, self.sj = pool, sj
+        self.todo = list(cold)
+        self.futs: dict = {}
+        self.window = max(1, window)
+        self._fill()
+
+    def _fill(self):
+        while self.todo and len(self.futs) < self.window:
+            s = self.todo.pop(0)
+            self.futs[s.key] = self.pool.submit(self.sj.load_split_host, s)
+
+    def take(self, key):
+        f = self.futs.pop(key, None)
+        if f is None:
+            return None
+        try:
+            h = f.result()
+        except Exception:  # noqa: BLE001 — the per-task load reports it
+            h = None
+        self._fill()
+        return h
+
+
 class GpuRuntime:
     def __init__(self, tracker, devices, slots_per_device):
         self.tracker = tracker
@@ -186,7 +220,7 @@ class GpuRuntime:
                     try:
                         tracker._maybe_inject_fault(r)
                         sspec = SplitSpec.from_dict(r.spec.split)
-                        host = prefetched.get(sspec.key)
+                        host = prefetched.take(sspec.key)
                         if host is not None:
                             loader = (lambda s=sspec, h=host:
                                       sj.load_split_from_host(s, h, dev.torch_device))
@@ -231,9 +265,11 @@ class GpuRuntime:
     def _prefetch_hosts(self, dev, runs, sj, SplitSpec):  # noqa: N803
         """Cold splits of a batch whose job can load them on the host
         (``load_split_host``: file decode into pinned memory) are read by a
-        thread pool in parallel; the H2D copies then go on the slot's stream."""
+        thread pool ahead of their tasks, a bounded window at a time; each task
+        takes its buffer when it is its turn, so the H2D copies on the slot's
+        stream overlap the decoding of the splits behind it."""
         if sj is None or not hasattr(sj, "load_split_host"):
-            return {}
+            return _NoPrefetch
         cold = []
         for r in runs:
             sspec = SplitSpec.from_dict(r.spec.split)
@@ -241,21 +277,12 @@ class GpuRuntime:
                     self.tracker.split_cache.get(sspec.key, dev.index) is None:
                 cold.append(sspec)
         if len(cold) < 2:
-            return {}
+            return _NoPrefetch
         import concurrent.futures as cf
+        n = max(1, self.tracker.conf.get_int("hbmr.gpu.load.threads", 8))
         if getattr(self, "_loader_pool", None) is None:
-            n = max(1, self.tracker.conf.get_int("hbmr.gpu.load.threads", 8))
             self._loader_pool = cf.ThreadPoolExecutor(n, thread_name_prefix="split-loader")
-        futs = {s.key: self._loader_pool.submit(sj.load_split_host, s) for s in cold}
-        out = {}
-        for k, f in futs.items():
-            try:
-                h = f.result()
-            except Exception:  # noqa: BLE001 — the per-task load reports it
-                h = None
-            if h is not None:
-                out[k] = h
-        return out
+        return _Prefetch(self._loader_pool, sj, cold, window=2 * n)
 
     def _completer(self, slot: _Slot):
         torch.cuda.set_device(slot.device)
