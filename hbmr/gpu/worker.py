@@ -167,7 +167,7 @@ class WorkerHost:
         if out or added or removed:
             send_msg(self.sock, ("batch", out, added, removed), self.send_lock)
 
-    def wakeup(self, _name=None):
+    def wakeup(self, _name=None, _seq=None):
         self.notify_jobtracker()
 
 

@@ -62,6 +62,7 @@ class TrackerInfo:
         self.blacklisted = False
         self.jobs_seen: set[str] = set()
         self.wake = False
+        self.wake_seq = 0    # highest TaskTracker notification count seen by wakeup()
         # long-poll doorbell: set by wakeup() (no JobTracker lock needed, so a
         # tracker's completion thread never queues behind a heartbeat) and by
         # _kick() when new work may exist for every tracker
@@ -768,12 +769,17 @@ class JobTracker:
             cb("finished", jip)
 
     # -- heartbeat ----------------------------------------------------------------------
-    def wakeup(self, tracker_name: str):
+    def wakeup(self, tracker_name: str, seq: int | None = None):
         """A tracker has news (a task finished): end its long-poll heartbeat now.
-        Lock-free: dict lookup + attribute store + Event.set."""
+        Lock-free: dict lookup + attribute store + Event.set.  ``seq`` is the
+        tracker's notification count: it survives the heartbeat entry's reset,
+        so news that arrives while the heartbeat is in flight is never lost."""
         tr = self.trackers.get(tracker_name)
         if tr is not None:
-            tr.wake = True
+            if seq is None:
+                tr.wake = True
+            elif seq > tr.wake_seq:
+                tr.wake_seq = seq
             tr.bell.set()
 
     def _kick(self):
@@ -793,6 +799,8 @@ class JobTracker:
         so idle trackers learn about new tasks immediately instead of on their
         next periodic heartbeat (the reference's 3 s floor, B13)."""
         name = status["tracker_name"] if isinstance(status, dict) else status.tracker_name
+        seen = (status.get("notify_seq", 0) if isinstance(status, dict)
+                else getattr(status, "notify_seq", 0))
         tr0 = self.trackers.get(name)
         if tr0 is not None:
             # clear before this call's assignment: a ring from here on re-polls
@@ -813,7 +821,7 @@ class JobTracker:
         if tr is None:
             return resp
         while not resp["actions"]:
-            if tr.wake or self._stop.is_set():
+            if tr.wake or tr.wake_seq > seen or self._stop.is_set():
                 break
             left = deadline - time.time()
             if left <= 0:
@@ -821,8 +829,8 @@ class JobTracker:
             tr.bell.wait(left)
             tr.bell.clear()
             if TRACE.on:
-                TRACE.instant("jt.longpoll.wake", wake=tr.wake)
-            if tr.wake or self.trackers.get(name) is not tr:
+                TRACE.instant("jt.longpoll.wake", wake=tr.wake or tr.wake_seq > seen)
+            if tr.wake or tr.wake_seq > seen or self.trackers.get(name) is not tr:
                 break
             if getattr(self, "_shutdown_trackers", False):
                 resp["actions"].append(P.shutdown_action())

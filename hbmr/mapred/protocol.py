@@ -17,7 +17,7 @@ from __future__ import annotations
 
 from dataclasses import dataclass, field
 
-PROTOCOL_VERSION = 3
+PROTOCOL_VERSION = 4
 
 # task states (TaskStatus.State)
 UNASSIGNED = "UNASSIGNED"
@@ -95,6 +95,10 @@ class TaskTrackerStatus:
     # the tracker's GPU worker process died and its collective peers must be
     # restarted with it (world > 1): the JobTracker answers restart_gpu_worker
     gpu_worker_lost: bool = False
+    # the tracker's count of wakeup() notifications when this status was built:
+    # a wakeup with a higher count carries news this heartbeat does not have,
+    # so the JobTracker must not swallow it in the long-poll
+    notify_seq: int = 0
 
     @property
     def max_gpu_map_slots(self):

@@ -233,8 +233,8 @@ class JobTrackerProxy:
         return self.rpc.call("heartbeat", status, initial=initial,
                              accept_new_tasks=accept_new_tasks, block=block)
 
-    def wakeup(self, tracker_name):
-        return self.rpc.call("wakeup", tracker_name)
+    def wakeup(self, tracker_name, seq=None):
+        return self.rpc.call("wakeup", tracker_name, seq)
 
     def map_completion_events(self, job_id, start=0):
         return self.rpc.call("map_completion_events", job_id, start)

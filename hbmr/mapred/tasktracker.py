@@ -167,6 +167,7 @@ class TaskTracker:
         self._lock = threading.Lock()
         self._changed: set[str] = set()
         self._bulk: list[dict] = []          # batched GPU completions not yet reported
+        self._notify_seq = 0                 # wakeup() notifications sent (notify_seq)
         self._lost: list[str] = []           # succeeded attempts whose output was lost
         self._worker_lost = False            # GPU worker died: the gang must restart
         self._news = threading.Event()
@@ -224,7 +225,9 @@ class TaskTracker:
             bulk, self._bulk = self._bulk, []
             lost, self._lost = self._lost, []
             wlost, self._worker_lost = self._worker_lost, False
+            seq = self._notify_seq
         return P.TaskTrackerStatus(tracker_name=self.name, host=self.host, bulk_reports=bulk,
+                                   notify_seq=seq,
                                    lost_outputs=lost, gpu_worker_lost=wlost,
                                    max_cpu_map_slots=self.cpu_slots,
                                    max_reduce_slots=self.reduce_slots, gpus=gpus,
@@ -363,10 +366,16 @@ class TaskTracker:
         self.notify_jobtracker()
 
     def notify_jobtracker(self):
-        """Cut our long-polling heartbeat short so finished tasks are reported now."""
+        """Cut our long-polling heartbeat short so finished tasks are reported now.
+        The notification count lets the JobTracker tell a wakeup that carries
+        news the pending heartbeat lacks from a stale one (TaskTrackerStatus.
+        notify_seq)."""
+        with self._lock:
+            self._notify_seq += 1
+            seq = self._notify_seq
         self._news.set()
         try:
-            self.jt.wakeup(self.name)
+            self.jt.wakeup(self.name, seq)
         except Exception:  # noqa: BLE001
             pass
 
