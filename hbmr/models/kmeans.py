@@ -214,6 +214,39 @@ _PINNED_INFLIGHT: list = []     # (event, pinned host buffer) of in-flight split
 
 
 # --------------------------------------------------------------------------- the job
+def _sum_slabs(outs):
+    """Sum of per-task (sums, counts) partials.  A batch's tasks are views
+    [i] of one [B, k, dp] slab (map_gpu_batch): a batch whose every view is
+    present is reduced straight from its slab, without first stacking copies
+    of the views; anything else is stacked."""
+    groups: dict = {}
+    loose = []
+    for s, c in outs:
+        bs, bc = s._base, c._base
+        if bs is not None and bc is not None and bs.dim() == 3 and bc.dim() == 2 and \
+                tuple(s.shape) == tuple(bs.shape[1:]) and tuple(c.shape) == tuple(bc.shape[1:]):
+            g = groups.setdefault(id(bs), [bs, bc, 0, []])
+            g[2] += 1
+            g[3].append((s, c))
+        else:
+            loose.append((s, c))
+    parts_s, parts_c = [], []
+    for bs, bc, n, members in groups.values():
+        if n == bs.shape[0] and len({m[0].data_ptr() for m in members}) == n:
+            parts_s.append(bs.sum(0))
+            parts_c.append(bc.sum(0))
+        else:
+            loose.extend(members)
+    if loose:
+        parts_s.append(torch.stack([s for s, _ in loose]).sum(0))
+        parts_c.append(torch.stack([c for _, c in loose]).sum(0))
+    sums, counts = parts_s[0], parts_c[0]
+    for s, c in zip(parts_s[1:], parts_c[1:]):
+        sums = sums + s
+        counts = counts + c
+    return sums, counts
+
+
 _EXACT_STATS: dict = {}
 _EXACT_LOCK = threading.Lock()
 
@@ -490,9 +523,7 @@ class KMeansSplitJob(SplitJob):
         same = [(s, c) for s, c in outputs if s.device == dev and s.shape[1] == dp]
         other = [(s, c) for s, c in outputs if not (s.device == dev and s.shape[1] == dp)]
         if same:
-            # one reduction kernel over all task slabs instead of one add per task
-            sums = torch.stack([s for s, _ in same]).sum(0)
-            counts = torch.stack([c for _, c in same]).sum(0)
+            sums, counts = _sum_slabs(same)
         else:
             sums = torch.zeros(self.k, dp, dtype=torch.int64, device=dev)
             counts = torch.zeros(self.k, dtype=torch.int64, device=dev)
@@ -528,7 +559,9 @@ class KMeansSplitJob(SplitJob):
             img.shift2 = torch.zeros_like(old.shift2)
             img.refresh(sums, counts)
             STORE.put_image(self.cout, sums.device, img)
-            shift = img.max_shift()
+            # the shift and the point count in one device->host copy (one sync)
+            shift, npts = torch.stack([img.shift2.max().double().sqrt(),
+                                       counts.sum().double()]).tolist()
             new_cen = None
         else:
             old = STORE.host_centroids(self.cin)
@@ -537,9 +570,10 @@ class KMeansSplitJob(SplitJob):
             new_cen = torch.where(cnt > 0, s / cnt.clamp(min=1), old.to(torch.float64)).to(
                 torch.float32)
             shift = float((new_cen - old).norm(dim=1).max()) if self.k else 0.0
+            npts = int(counts.sum().item())
             STORE.put_host(self.cout, new_cen)
         self._write_output(ctx, counts, new_cen)
-        res = {"shift": shift, "points": int(counts.sum().item()), "centroids_key": self.cout}
+        res = {"shift": shift, "points": int(npts), "centroids_key": self.cout}
         if ctx.rank == 0 and self.cdir:
             cen = new_cen if new_cen is not None else STORE.image(self.cout, sums.device).cen
             _save_centroids_async(self.cdir, self.cout, self.cin, cen[:, :self.d])

@@ -82,11 +82,7 @@ class CentroidImage:
                                     _ptr(self.chalf), _ptr(self.shift2),
                                     _lib.stream_handle(stream))
         _lib.check(rc, "hbmr_kmeans_update")
-        # |c_j| for exact mode's certification bound, on the same stream as the
-        # update (consumers are ordered after the reduce like cen/cbf/chalf)
-        with torch.cuda.stream(stream) if stream is not None else _nullctx():
-            cn = self.cen.double().norm(dim=1).float()
-            self._norms = (cn, cn.max().reshape(1))
+        self._norms = None     # exact mode's |c_j| and neighbour table: built on demand
         self._nbr = None
         if getattr(self, "_nbr_lock", None) is None:
             self._nbr_lock = threading.Lock()
@@ -97,8 +93,17 @@ class CentroidImage:
 
     def norms(self):
         """(|c_j| fp32 [k], max_j |c_j| fp32 [1]) of the fp32 master centroids
-        (exact mode's certification bound), computed in fp64 by refresh()."""
-        return self._norms
+        (exact mode's certification bound), computed in fp64 once per image on
+        the first caller's stream; other streams wait on it."""
+        with self._nbr_lock:
+            if self._norms is None:
+                cn = self.cen.double().norm(dim=1).float()
+                ev = torch.cuda.Event()
+                ev.record()
+                self._norms = (cn, cn.max().reshape(1), ev)
+        cn, cm, ev = self._norms
+        torch.cuda.current_stream().wait_event(ev)
+        return cn, cm
 
     def neighbors(self, L: int = 256):
         """Each centroid's L nearest centroids (itself first) and their
@@ -261,8 +266,8 @@ def refine_f32(split: ExactSplit, img: CentroidImage, labels, cand, scores, marg
         raise ValueError("stats must be int64 [3]")
     if labels.numel() != n or cand.numel() != 2 * n or margin.numel() != 2 * n:
         raise ValueError("labels [n], cand/margin [2n] from assign_top3 expected")
-    cn, cmax = img.norms()
     with torch.cuda.stream(stream) if stream is not None else _nullctx():
+        cn, cmax = img.norms()
         ni, nd, L = img.neighbors()
     rc = _lib.load().hbmr_kmeans_refine_f32(
         _ptr(split.x32), n, img.d, split.x32.shape[1], _ptr(split.xnorm), _ptr(split.xbn2),
