@@ -87,6 +87,10 @@ def main():
     conf.set_int("hbmr.gpu.queue.depth", a.queue_depth)
     conf.set_int("hbmr.heartbeat.interval.ms", 200)
     conf.set_int("mapred.task.timeout", 0)
+    # splits are placed on their designated tracker and stay HBM-resident there;
+    # only a tracker that is seconds late (not one still warming up) loses its
+    # splits to another GPU's queue, which would skew every later iteration
+    conf.set_int("hbmr.locality.wait.ms", 5000)
     # device_count() does not initialise HIP in this process: with the default
     # per-rank GPU worker process (hbmr.gpu.worker.process) the device work and
     # its synchronisation happen in the workers (the barrier job synchronises

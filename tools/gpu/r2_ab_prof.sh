@@ -3,6 +3,6 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-(cd abtest/base && HBMR_WORKER_CLEAN_EXIT=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d ../../gpurun_out/prof_base -o run -- python3 bench.py --steps 10 --warmup 3 > ../../gpurun_out/prof_base.log 2>&1) ; echo base rc=$?
-HBMR_WORKER_CLEAN_EXIT=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_head -o run -- python3 bench.py --steps 10 --warmup 3 > gpurun_out/prof_head.log 2>&1; echo head rc=$?
+(cd abtest/base && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d ../../gpurun_out/prof_base -o run -- python3 bench.py --in-process --steps 10 --warmup 3 > ../../gpurun_out/prof_base.log 2>&1) ; echo base rc=$?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_head -o run -- python3 bench.py --in-process --steps 10 --warmup 3 > gpurun_out/prof_head.log 2>&1; echo head rc=$?
 ls gpurun_out/prof_base gpurun_out/prof_head
