@@ -98,6 +98,10 @@ class TeraSortSplitJob(SplitJob):
         self.nparts_conf = conf.get_int(PARTS_KEY, 0)
         self.sample = conf.get_long(SAMPLE_KEY, 100000)
         self.out = conf.get("mapred.output.dir")
+        # one-rank reduce: consecutive partitions sorted together, up to this many
+        # record bytes per sort (bigger sorts run the radix passes at full
+        # occupancy; the working set is 1.4x the group)
+        self.group_bytes = conf.get_long("hbmr.terasort.reduce.group.bytes", 8 << 30)
 
     # -- splits + sampling (JobTracker side) -----------------------------------------
     def _ranges(self):
@@ -272,9 +276,11 @@ class TeraSortSplitJob(SplitJob):
         return recs, hs, ls
 
     def _reduce_local(self, ctx, outs, offs, nparts, dev):
-        """One rank owns every partition: no record shuffle.  Partitions are
-        sorted one at a time (working set = one partition), so peak HBM is the
-        input splits + 20 B/record of map output + one partition."""
+        """One rank owns every partition: no record shuffle.  Consecutive
+        partitions are sorted in groups of about ``group_bytes`` (a partition is
+        a key range, so a group sorts to its partitions in order and is cut by
+        their counts), so peak HBM is the input splits + 20 B/record of map
+        output + one group."""
         if not outs:
             return 0, 0, 0, (-1, -1), (-1, -1)
         his = [o["hi"] for o in outs]
@@ -287,9 +293,19 @@ class TeraSortSplitJob(SplitJob):
         prev_last = None
         first = last = None
         n = 0
-        for p in range(nparts):
-            starts = offs[:, p]
-            lens = offs[:, p + 1] - offs[:, p]
+        sizes = (offs[:, 1:] - offs[:, :-1]).sum(axis=0)     # records per partition
+        groups, pa = [], 0
+        while pa < nparts:
+            pb, acc = pa, 0
+            while pb < nparts and (pb == pa or (acc + int(sizes[pb])) * S.RECORD <=
+                                   self.group_bytes):
+                acc += int(sizes[pb])
+                pb += 1
+            groups.append((pa, pb))
+            pa = pb
+        for pa, pb in groups:
+            starts = offs[:, pa]
+            lens = offs[:, pb] - offs[:, pa]
             m = int(lens.sum())
             if m == 0:
                 continue
@@ -304,7 +320,10 @@ class TeraSortSplitJob(SplitJob):
             csum = csum + hs.sum() + ls.sum()
             n += m
             if self.out:
-                self._write_part(p, recs)
+                at = 0
+                for p in range(pa, pb):
+                    self._write_part(p, recs[at:at + int(sizes[p])])
+                    at += int(sizes[p])
             del recs, hs, ls
         fl = torch.cat([first[0], first[1], last[0], last[1]]).to("cpu").tolist()
         return n, int(bad.item()), int(csum.item()), (fl[0], fl[1]), (fl[2], fl[3])

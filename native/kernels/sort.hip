@@ -390,16 +390,22 @@ __global__ __launch_bounds__(256) void tera_collect_kernel(
 
 // dst record i = record row[k] of split split[k], k = perm ? perm[i] : i; records
 // of `words` 4-byte words, one word per lane (25 lanes cover a 100-byte record)
+// A workgroup copies 256 / words whole records per step: lane t moves word
+// t % words of record t / words (one 32-bit division per thread, not one
+// 64-bit division per word), so each record's index loads are shared by its
+// lanes and its words are read and written as one contiguous run.
 __global__ __launch_bounds__(256) void gather_records_multi_kernel(
     const uint32_t* const* __restrict__ bases, const uint32_t* __restrict__ split,
     const uint32_t* __restrict__ row, const uint32_t* __restrict__ perm, long n, int words,
     uint32_t* __restrict__ dst) {
-  const long total = n * words;
-  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long)gridDim.x * 256) {
-    const long r = e / words;
-    const int w = (int)(e - r * words);
+  const int rpb = 256 / words;
+  const int t = threadIdx.x;
+  if (t >= rpb * words) return;
+  const int lr = t / words;
+  const int w = t - lr * words;
+  for (long r = (long)blockIdx.x * rpb + lr; r < n; r += (long)gridDim.x * rpb) {
     const long k = perm ? (long)perm[r] : r;
-    dst[e] = bases[split[k]][(long)row[k] * words + w];
+    dst[r * words + w] = bases[split[k]][(long)row[k] * words + w];
   }
 }
 
@@ -527,9 +533,9 @@ int hbmr_gather_records_multi(const void* const* bases, const uint32_t* split, c
                               const uint32_t* perm, long n, int record_bytes, void* dst,
                               hipStream_t st) {
   if (n <= 0) return 0;
-  if (record_bytes % 4) return (int)hipErrorInvalidValue;
+  if (record_bytes % 4 || record_bytes > 4 * 256) return (int)hipErrorInvalidValue;
   const int words = record_bytes / 4;
-  const long grid = std::min<long>(ceil_div(n * words, 256), 1L << 20);
+  const long grid = std::min<long>(ceil_div(n, 256 / words), 1L << 20);
   hipLaunchKernelGGL(gather_records_multi_kernel, dim3((unsigned)grid), dim3(256), 0, st,
                      reinterpret_cast<const uint32_t* const*>(bases), split, row, perm, n, words,
                      reinterpret_cast<uint32_t*>(dst));

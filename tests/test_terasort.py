@@ -54,6 +54,27 @@ def test_terasort_on_cluster_sorts_and_validates(tmp_path, trackers):
     assert np.array_equal(got, _ref_sorted(rows))
 
 
+@pytest.mark.parametrize("group_bytes", [1, 300_000, 8 << 30])
+def test_terasort_partition_groups_one_rank(tmp_path, group_bytes):
+    """The one-rank reduce sorts consecutive partitions together (one per sort,
+    a few, or all); output files and order are the same."""
+    rows = 12000
+    out = tmp_path / "out"
+    conf = T.terasort_conf(rows=rows, split_rows=2500, output=str(out), partitions=7)
+    conf.set("hbmr.terasort.reduce.group.bytes", str(group_bytes))
+    with LocalCluster(JobConf(), num_trackers=1, cpu_slots=2) as cl:
+        rj = cl.submit_job(conf)
+        rj.waitForCompletion(120)
+        assert rj.isSuccessful(), rj.getFailureInfo()
+        res = rj._impl.jip.result[0]
+    assert res["unsorted"] == 0 and res["checksum_ok"] and res["records"] == rows
+    parts = sorted(f for f in os.listdir(out) if f.startswith("part-"))
+    assert parts == [f"part-{i:05d}" for i in range(7)]
+    got = np.concatenate([np.fromfile(out / p, dtype=np.uint8).reshape(-1, 100) for p in parts])
+    assert np.array_equal(got, _ref_sorted(rows))
+    assert T.teravalidate(str(out))["misordered"] == 0
+
+
 @pytest.mark.parametrize("trackers", [1, 2, 3])
 def test_terasort_more_partitions_than_trackers(tmp_path, trackers):
     """R part files for any R (TeraSort.java writes one per reduce): a rank
