@@ -648,10 +648,17 @@ def initial_centroids(inp, k, d, centers=None):
 
 class KMeansDriver:
     """Chains K-Means iteration jobs (what the paper's K-Means driver does with
-    separate Hadoop jobs)."""
+    separate Hadoop jobs).
+
+    Checkpoint / resume: every iteration's centroids land in ``checkpoint_dir``
+    (the reduce writes them asynchronously, the last few are kept) next to a
+    ``driver.json`` manifest; :meth:`resume` restarts a run from the newest
+    complete centroid file, so a driver that died continues where it stopped."""
+
+    MANIFEST = "driver.json"
 
     def __init__(self, submit, result_of, conf=None, k=64, d=128, inp="synthetic:100000:1",
-                 split_points=500_000, run_id=None, return_centroids=None):
+                 split_points=500_000, run_id=None, return_centroids=None, checkpoint_dir=None):
         self.submit = submit          # conf -> RunningJob
         self.result_of = result_of    # RunningJob -> reduce result dict
         self.base = conf
@@ -663,7 +670,48 @@ class KMeansDriver:
         # the bench-sized one (k*d = 128K floats) only when asked
         self.return_centroids = (k * d <= 65536) if return_centroids is None else return_centroids
         base_dir = (conf.get("mapred.local.dir") if conf is not None else None) or "/tmp/hbmr-local"
-        self.centroid_dir = os.path.join(base_dir, "kmeans-centroids", self.run_id)
+        self.centroid_dir = checkpoint_dir or os.path.join(base_dir, "kmeans-centroids",
+                                                           self.run_id)
+        self._manifest_written = False
+
+    def _write_manifest(self):
+        import json
+        os.makedirs(self.centroid_dir, exist_ok=True)
+        path = os.path.join(self.centroid_dir, self.MANIFEST)
+        with open(path + ".tmp", "w") as f:
+            json.dump({"run_id": self.run_id, "k": self.k, "d": self.d, "input": self.inp,
+                       "split_points": self.split_points}, f)
+        os.replace(path + ".tmp", path)
+        self._manifest_written = True
+
+    @classmethod
+    def resume(cls, submit, result_of, checkpoint_dir, conf=None, **kw):
+        """A driver continuing the run saved in ``checkpoint_dir``: its iteration
+        is that of the newest centroid file that loads (a file cut short by a
+        crash is skipped for the one before it)."""
+        import json
+        import re
+        with open(os.path.join(checkpoint_dir, cls.MANIFEST)) as f:
+            m = json.load(f)
+        drv = cls(submit, result_of, conf=conf, k=m["k"], d=m["d"], inp=m["input"],
+                  split_points=m["split_points"], run_id=m["run_id"],
+                  checkpoint_dir=checkpoint_dir, **kw)
+        pat = re.compile(re.escape(_centroid_file("", drv.key(0))[:-len("_0.npy")]) +
+                         r"_(\d+)\.npy$")
+        found = sorted((int(mm.group(1)), fn) for fn in os.listdir(checkpoint_dir)
+                       for mm in [pat.match(fn)] if mm)
+        for i, fn in reversed(found):
+            try:
+                c = torch.from_numpy(np.load(os.path.join(checkpoint_dir, fn)))
+            except (OSError, ValueError):
+                continue
+            if tuple(c.shape) != (drv.k, drv.d):
+                continue
+            drv.iteration = i
+            STORE.put_host(drv.key(i), c.to(torch.float32))
+            break
+        drv._manifest_written = True
+        return drv
 
     def key(self, i):
         return f"{self.run_id}:{i}"
@@ -678,6 +726,8 @@ class KMeansDriver:
                                   self.key(i), self.key(i + 1), init=init,
                                   return_centroids=self.return_centroids)
         job.set(CDIR_KEY, self.centroid_dir)
+        if not self._manifest_written:
+            self._write_manifest()
         t0 = time.time()
         rj = self.submit(job)
         rj.waitForCompletion()

@@ -149,3 +149,37 @@ def test_exact_mode_job_matches_fp64_lloyd():
     # identical assignments: centroids differ only by the 2^-24 fixed-point rounding
     assert (got.cuda().double() - ref).abs().max().item() < 1e-5
     assert flagged > 0
+
+
+def test_kmeans_driver_resumes_from_checkpoint(tmp_path):
+    """A driver that stops after 2 iterations and a new one resumed from its
+    checkpoint directory produce the same centroids as 3 uninterrupted
+    iterations (fixed-point partials make the iteration exact)."""
+    import os
+    import time as _t
+    n, k, d = 12000, 6, 8
+    inp = f"synthetic:{n}:21"
+    ck = str(tmp_path / "ck")
+    conf = JobConf()
+    with LocalCluster(conf, num_trackers=1, cpu_slots=2) as cl:
+        res = lambda rj: rj._impl.jip.result[0]   # noqa: E731
+        ref = K.KMeansDriver(cl.submit_job, res, conf=conf, k=k, d=d, inp=inp, split_points=3000)
+        for _ in range(3):
+            ref.step()
+        want = ref.centroids().clone()
+        a = K.KMeansDriver(cl.submit_job, res, conf=conf, k=k, d=d, inp=inp, split_points=3000,
+                           checkpoint_dir=ck)
+        a.step()
+        a.step()
+        f2 = os.path.join(ck, K._centroid_file("", a.key(2)))
+        for _ in range(200):             # the reduce writes centroid files asynchronously
+            if os.path.exists(f2):
+                break
+            _t.sleep(0.01)
+        K.STORE.host.clear()
+        K.STORE.images.clear()
+        b = K.KMeansDriver.resume(cl.submit_job, res, ck, conf=conf)
+        assert b.iteration == 2 and b.run_id == a.run_id
+        b.step()
+        got = b.centroids()
+    assert torch.equal(got, want)
