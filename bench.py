@@ -60,6 +60,10 @@ def main():
                     help="CPU rehearsal: simulated GPU slots with this device time per split")
     ap.add_argument("--in-process", action="store_true",
                     help="run the GPU slots inside the tracker process (no worker process)")
+    ap.add_argument("--prefetch", action="store_true",
+                    help="submit each iteration job while its predecessor runs, held by the "
+                         "JobTracker until that one succeeds (hbmr.job.depends.on); default: "
+                         "submit after it finished")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args()
     logging.basicConfig(level=logging.INFO if a.verbose else logging.WARNING,
@@ -122,15 +126,18 @@ def main():
 
     try:
         t_setup = time.time()
-        for _ in range(a.warmup):
-            drv.step()
+        pre = a.prefetch
+        for w in range(a.warmup):
+            drv.step(prefetch=pre and w < a.warmup - 1)
         t_warm = time.time() - t_setup
         barrier()
         if in_process:
             torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(a.steps):
-            drv.step()
+        # every timed job is submitted inside the timed window (the first by this
+        # loop, each next one while its predecessor runs); none crosses a barrier
+        for s in range(a.steps):
+            drv.step(prefetch=pre and s < a.steps - 1)
         barrier()
         if in_process:
             torch.cuda.synchronize()
@@ -175,7 +182,8 @@ def main():
                        "parallelism": f"dp{world}", "k": a.k, "split_points": a.split_points,
                        "map_tasks_per_job": splits, "policy": a.policy,
                        "cpu_slots_per_tracker": a.cpu_slots, "gpu_slots_per_gpu": a.gpu_slots,
-                       "gpu_worker_process": not in_process},
+                       "gpu_worker_process": not in_process,
+                       "iteration_jobs_prefetched": a.prefetch},
             "job_makespan_ms": round(ms, 3),
             "phases_ms": phases_ms,
             "points_per_sec": round(a.points * a.steps / dt, 1),

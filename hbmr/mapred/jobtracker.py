@@ -38,6 +38,9 @@ from ..net.topology import DEFAULT_RACK, Topology
 from ..utils.metrics import METRICS
 from ..utils.trace import TRACE
 
+# a job submitted with this key holds until that job succeeds (JobControl)
+DEPENDS_KEY = "hbmr.job.depends.on"
+
 log = logging.getLogger("hbmr.jobtracker")
 
 
@@ -182,6 +185,7 @@ class JobInProgress:
         self.priority = conf.get("mapred.job.priority", "NORMAL")
         self.submit_time = time.time()
         self.launch_time = 0.0
+        self.release_time = 0.0     # a dependent job: when its dependency succeeded
         self.t_first_map = 0.0       # first map attempt launched
         self.t_maps_done = 0.0       # last map completed
         self.t_first_reduce = 0.0    # first reduce attempt launched
@@ -386,9 +390,9 @@ class JobInProgress:
 
     def timeline(self) -> dict:
         """Phase breakdown in seconds (submit → first map launch → last map done
-        → first reduce launch → finish)."""
+        → first reduce launch → finish); a dependent job counts from its release."""
         st = self.status
-        t0 = self.submit_time
+        t0 = self.release_time or self.submit_time
         rel = lambda t: round(t - t0, 6) if t else None  # noqa: E731
         return {"first_map": rel(self.t_first_map), "maps_done": rel(self.t_maps_done),
                 "first_reduce": rel(self.t_first_reduce), "finish": rel(st.finish_time)}
@@ -452,6 +456,7 @@ class JobTracker:
         from ..security import JobTokenSecretManager
         self.job_tokens = JobTokenSecretManager()
         self.job_queue: list[JobInProgress] = []
+        self.waiting: dict[str, list] = {}   # job id -> dependent jobs held for it
         self.trackers: dict[str, TrackerInfo] = {}
         self.attempt_index: dict[str, Attempt] = {}
         self.cost_model = CostModel(conf.get_float("hbmr.costmodel.ewma.alpha", 0.3))
@@ -675,6 +680,17 @@ class JobTracker:
                 log.exception("job init failed")
                 self._finish_job(jip, FAILED, f"init failed: {type(e).__name__}: {e}")
                 return RunningJob(jid, _JTJobHandle(jip), conf)
+            dep = conf.get(DEPENDS_KEY)
+            dj = self.jobs.get(dep) if dep else None
+            if dj is not None and not dj.completed():
+                # a dependent job (JobControl's ControlledJob): initialised now,
+                # scheduled the moment the job it depends on succeeds
+                jip.status.state = PREP
+                self.waiting.setdefault(dep, []).append(jip)
+                return RunningJob(jid, _JTJobHandle(jip), conf)
+            if dj is not None and dj.status.state != SUCCEEDED:
+                self._finish_job(jip, FAILED, f"job {dep} it depends on {dj.status.state}")
+                return RunningJob(jid, _JTJobHandle(jip), conf)
             self.job_queue.append(jip)
             if not jip.maps and not jip.reduces:
                 self._finish_job(jip, SUCCEEDED)
@@ -765,6 +781,17 @@ class JobTracker:
                 log.exception("writing job history failed")
         self._forget_job(jip.job_id)
         jip.done.set()
+        for w in self.waiting.pop(str(jip.job_id), []):
+            if w.completed():
+                continue             # killed while it waited
+            if state == SUCCEEDED:
+                w.status.state = RUNNING
+                w.launch_time = w.release_time = time.time()
+                self.job_queue.append(w)
+            else:
+                self._finish_job(w, FAILED, f"job {jip.job_id} it depends on {state}")
+        if state == SUCCEEDED:
+            self._kick()
         for cb in self.listeners:
             cb("finished", jip)
 

@@ -673,6 +673,7 @@ class KMeansDriver:
         self.centroid_dir = checkpoint_dir or os.path.join(base_dir, "kmeans-centroids",
                                                            self.run_id)
         self._manifest_written = False
+        self.prefetch_delay = 0.005     # s after a job's submission before the next one's
 
     def _write_manifest(self):
         import json
@@ -716,8 +717,7 @@ class KMeansDriver:
     def key(self, i):
         return f"{self.run_id}:{i}"
 
-    def step(self):
-        i = self.iteration
+    def _job_conf(self, i, depends_on=None):
         centers = self.base.get_int(NCENTERS_KEY, self.k) if self.base is not None else None
         init = initial_centroids(self.inp, self.k, self.d, centers) if i == 0 else None
         if init is not None:
@@ -726,10 +726,25 @@ class KMeansDriver:
                                   self.key(i), self.key(i + 1), init=init,
                                   return_centroids=self.return_centroids)
         job.set(CDIR_KEY, self.centroid_dir)
+        if depends_on is not None:
+            from ..mapred.jobtracker import DEPENDS_KEY
+            job.set(DEPENDS_KEY, str(depends_on))
+        return job
+
+    def step(self, prefetch=False):
+        """One iteration job.  ``prefetch``: also submit the next iteration now,
+        held by the JobTracker until this one succeeds (its set-up overlaps this
+        job; the next step() uses it).  A run that stops early kills it."""
+        i = self.iteration
         if not self._manifest_written:
             self._write_manifest()
         t0 = time.time()
-        rj = self.submit(job)
+        rj, self._next = getattr(self, "_next", None), None
+        if rj is None:
+            rj = self.submit(self._job_conf(i))
+        if prefetch and not rj.waitForCompletion(self.prefetch_delay):
+            # submitted once this job's own launch is under way, not in its path
+            self._next = self.submit(self._job_conf(i + 1, depends_on=rj.getID()))
         rj.waitForCompletion()
         if not rj.isSuccessful():
             raise RuntimeError(f"K-Means iteration {i} failed: {rj.getFailureInfo()}")
@@ -754,6 +769,12 @@ class KMeansDriver:
             if r.get("shift", 1.0) <= tol:
                 break
         return self.centroids()
+
+    def cancel_prefetch(self):
+        """Kill a pre-submitted next iteration (the run stopped before it)."""
+        nxt, self._next = getattr(self, "_next", None), None
+        if nxt is not None:
+            nxt.killJob()
 
     def centroids(self):
         c = STORE.host_centroids(self.key(self.iteration))

@@ -154,3 +154,28 @@ def test_vaidya_rules_on_real_job_history(tmp_path):
     assert rules["MapsReExecutionImpact"]["impact"] == pytest.approx(
         min(1.0, (launched - 8) / 8))
     assert all(0.0 <= f["impact"] <= 1.0 for f in rules.values() if "impact" in f)
+
+
+def test_dependent_job_runs_after_success_and_fails_with_its_dependency():
+    """hbmr.job.depends.on (JobControl's depending jobs): held until the job it
+    names succeeds; failed if that job is killed."""
+    from hbmr.examples.sleepjob import split_sleep_conf
+    from hbmr.mapred.cluster import LocalCluster
+    from hbmr.mapred.jobconf import JobConf
+    from hbmr.mapred.jobtracker import DEPENDS_KEY
+    with LocalCluster(JobConf(), num_trackers=1, cpu_slots=2) as cl:
+        a = cl.submit_job(split_sleep_conf(4, map_ms=50.0))
+        bc = split_sleep_conf(2, map_ms=1.0)
+        bc.set(DEPENDS_KEY, str(a.getID()))
+        b = cl.submit_job(bc)
+        assert b.status().state == "PREP"
+        assert b.waitForCompletion(30) and a.waitForCompletion(30)
+        assert b.isSuccessful()
+        assert b._impl.jip.release_time >= a._impl.jip.status.finish_time
+        c = cl.submit_job(split_sleep_conf(4, map_ms=2000.0))
+        dc = split_sleep_conf(2, map_ms=1.0)
+        dc.set(DEPENDS_KEY, str(c.getID()))
+        d = cl.submit_job(dc)
+        c.killJob()
+        assert d.waitForCompletion(30)
+        assert d.status().state == "FAILED" and "depends on" in d.getFailureInfo()

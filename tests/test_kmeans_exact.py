@@ -183,3 +183,35 @@ def test_kmeans_driver_resumes_from_checkpoint(tmp_path):
         b.step()
         got = b.centroids()
     assert torch.equal(got, want)
+
+
+def test_prefetched_iterations_match_and_wait_for_their_dependency():
+    """step(prefetch=True) submits iteration i+1 held on iteration i
+    (hbmr.job.depends.on): same centroids as plain steps; a held job starts
+    only after its dependency finished; a cancelled one is killed."""
+    n, k, d = 12000, 6, 8
+    inp = f"synthetic:{n}:23"
+    conf = JobConf()
+    res = lambda rj: rj._impl.jip.result[0]   # noqa: E731
+    with LocalCluster(conf, num_trackers=1, cpu_slots=2) as cl:
+        a = K.KMeansDriver(cl.submit_job, res, conf=conf, k=k, d=d, inp=inp, split_points=3000)
+        for _ in range(4):
+            a.step()
+        want = a.centroids().clone()
+        b = K.KMeansDriver(cl.submit_job, res, conf=conf, k=k, d=d, inp=inp, split_points=3000)
+        b.prefetch_delay = 0.0
+        for s in range(4):
+            b.step(prefetch=s < 3)
+        got = b.centroids()
+        jobs = [cl.jt.jobs[h["job"]] for h in b.history]
+        for prev, nxt in zip(jobs, jobs[1:]):
+            assert nxt.release_time >= prev.status.finish_time > 0
+            assert nxt.t_first_map >= nxt.release_time
+        c = K.KMeansDriver(cl.submit_job, res, conf=conf, k=k, d=d, inp=inp, split_points=3000)
+        c.prefetch_delay = 0.0
+        c.step(prefetch=True)
+        held = c._next
+        c.cancel_prefetch()
+        assert held.waitForCompletion(10)
+        assert held.status().state == "KILLED"   # (released and running by then)
+    assert torch.equal(got, want)
