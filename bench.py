@@ -101,7 +101,8 @@ def main():
     # every worker's device), and this process never holds a HIP context
     has_gpu = torch.cuda.device_count() > 0 and a.simulate_ms is None
     in_process = a.in_process and has_gpu
-    conf.set_boolean("hbmr.gpu.worker.process", not in_process)
+    # (a simulated run may also keep its simulated slots in the tracker process)
+    conf.set_boolean("hbmr.gpu.worker.process", not (in_process or a.in_process))
     if a.simulate_ms is not None:
         if world > 1:
             conf.set_int("hbmr.worker.torch.threads", 1)
@@ -143,6 +144,14 @@ def main():
             torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         hist = drv.history[a.warmup:]
+        if a.verbose:
+            J = "org.apache.hadoop.mapred.JobInProgress$Counter"
+            for i, h in enumerate(drv.history):
+                c = h["counters"]
+                print(f"job {i}: maps/tracker {sorted((h.get('maps_per_tracker') or {}).values())}"
+                      f" hbm-local {c.get(J, 'HBM_LOCAL_MAPS')} data-local "
+                      f"{c.get(J, 'DATA_LOCAL_MAPS')} cpu {c.get(J, 'CPU_MAP_TASKS')}",
+                      file=sys.stderr, flush=True)
         n_maps = sum(h["counters"].get("org.apache.hadoop.mapred.JobInProgress$Counter",
                                        "TOTAL_LAUNCHED_MAPS") for h in hist)
         gpu_maps = sum(h["counters"].get("org.apache.hadoop.mapred.JobInProgress$Counter",
@@ -182,7 +191,7 @@ def main():
                        "parallelism": f"dp{world}", "k": a.k, "split_points": a.split_points,
                        "map_tasks_per_job": splits, "policy": a.policy,
                        "cpu_slots_per_tracker": a.cpu_slots, "gpu_slots_per_gpu": a.gpu_slots,
-                       "gpu_worker_process": not in_process,
+                       "gpu_worker_process": not (in_process or a.in_process),
                        "iteration_jobs_prefetched": a.prefetch},
             "job_makespan_ms": round(ms, 3),
             "phases_ms": phases_ms,

@@ -910,10 +910,12 @@ class JobTracker:
             if accept_new_tasks and st.healthy and not tr.blacklisted:
                 actions += self.scheduler.assign_tasks(tr)
             # kill attempts of jobs that are done / tasks already completed
-            # (detached CPU profiling probes excepted)
+            # (CPU profiling probes excepted: a sampled probe rides on a TIP that
+            # the GPUs finish long before it, and killing it would leave the cost
+            # model a censored bound instead of the CPU time)
             for aid in list(tr.running):
                 a = self.attempt_index.get(aid)
-                if a is not None and not a.profile_only and (
+                if a is not None and not a.profile_only and not a.profile_fraction and (
                         a.tip.job.completed() or
                         (a.tip.successful is not None and a.tip.successful is not a)):
                     tr.kills.add(aid)
@@ -1283,7 +1285,8 @@ class JobTracker:
             else:
                 tr.running_cpu += a.slots
                 jip.running_cpu += 1
-            self.cost_model.task_started(jip.signature, a.aid, on_gpu, a.start)
+            self.cost_model.task_started(jip.signature, a.aid, on_gpu, a.start,
+                                         fraction=profile_fraction or 1.0)
             if not profile_fraction:
                 jip.counters.incr(C.JOB_GROUP, C.TOTAL_LAUNCHED_MAPS)
         else:

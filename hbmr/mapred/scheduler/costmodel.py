@@ -12,7 +12,10 @@ Here:
   the same signature so iterative jobs (K-Means iterations) start profiled;
 * running attempts give a censored lower bound: a CPU probe that has run for
   t seconds proves t_cpu ≥ t, so the GPU/CPU ratio is bounded before the probe
-  finishes;
+  finishes (a sampled probe's elapsed time is scaled to a whole split);
+* GPU attempts wait in a device queue behind each other: their age is queue
+  time, not execution time, so it never raises a GPU estimate that completed
+  tasks already give (it did, and the inflated t_gpu handed maps to CPUs);
 * the min-makespan split of P pending maps over C CPU and G GPU slots,
   ``min_x max(ceil(x/C)·t_c, ceil((P-x)/G)·t_g)``, is solved exactly in O(P/C).
 """
@@ -33,6 +36,8 @@ class TimeStats:
     running: dict = field(default_factory=dict)   # attempt -> start time
     lower_bound: float = 0.0   # censored: killed/failed attempts ran at least this long
     probe: str | None = None   # the first attempt on this slot type (profiling probe)
+    queued: bool = False       # attempts wait in a queue (GPU): age is not run time
+    scale: dict = field(default_factory=dict)     # attempt -> 1/fraction (sampled probes)
 
     def add(self, dt: float, alpha: float):
         self.n += 1
@@ -47,14 +52,19 @@ class TimeStats:
 
     def estimate(self, now: float):
         """(estimate seconds or None, is_lower_bound)."""
+        sc = self.scale
         if self.n:
             est = self.ewma
+            if self.queued:
+                return est, False
             # a running attempt older than the estimate raises it (stragglers)
-            oldest = max((now - s for s in self.running.values()), default=0.0)
+            oldest = max(((now - s) * sc.get(a, 1.0) for a, s in self.running.items()),
+                         default=0.0)
             if oldest > 2 * est:
                 return oldest, True
             return est, False
-        lb = max([now - s for s in self.running.values()] + [self.lower_bound])
+        lb = max([(now - s) * sc.get(a, 1.0) for a, s in self.running.items()] +
+                 [self.lower_bound])
         if lb > 0:
             return lb, True
         return None, False
@@ -69,17 +79,20 @@ class CostModel:
     def _get(self, sig):
         d = self._stats.get(sig)
         if d is None:
-            d = self._stats[sig] = {"cpu": TimeStats(), "gpu": TimeStats()}
+            d = self._stats[sig] = {"cpu": TimeStats(), "gpu": TimeStats(queued=True)}
         return d
 
     def is_probe(self, sig, attempt, on_gpu) -> bool:
         with self._lock:
             return self._get(sig)["gpu" if on_gpu else "cpu"].probe == attempt
 
-    def task_started(self, sig, attempt, on_gpu, t):
+    def task_started(self, sig, attempt, on_gpu, t, fraction=1.0):
+        """``fraction`` < 1: a sampled probe timed on that fraction of a split."""
         with self._lock:
             st = self._get(sig)["gpu" if on_gpu else "cpu"]
             st.running[attempt] = t
+            if fraction < 1.0:
+                st.scale[attempt] = 1.0 / fraction
             if st.probe is None and st.n == 0:
                 st.probe = attempt
 
@@ -117,12 +130,13 @@ class CostModel:
         with self._lock:
             st = self._get(sig)["gpu" if on_gpu else "cpu"]
             st.running.pop(attempt, None)
+            k = st.scale.pop(attempt, 1.0)
             if succeeded and finish >= start:
                 st.add(finish - start, self.alpha)
             elif not succeeded and finish > start:
                 # a killed attempt (e.g. a CPU probe overtaken by its GPU backup)
                 # still proves the task takes at least this long on that slot type
-                st.lower_bound = max(st.lower_bound, finish - start)
+                st.lower_bound = max(st.lower_bound, (finish - start) * k)
 
     def stats(self, sig, on_gpu) -> TimeStats:
         with self._lock:
