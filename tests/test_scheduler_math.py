@@ -127,3 +127,23 @@ def test_optional_rule_idles_cpus_only_when_gpus_can_drain_the_queue():
     assert cpu_small == 0
     t_big, cpu_big, gpu_big = run_policy("optional", 40, 20.0, 200.0, 4)
     assert cpu_big > 0 and cpu_big + gpu_big == 40
+
+
+def test_costmodel_queued_gpu_age_and_sampled_probe_bound():
+    """Queued GPU attempts do not raise a measured GPU estimate (their age is
+    queue time); a killed sampled probe bounds the whole-split CPU time."""
+    from hbmr.mapred.scheduler.costmodel import CostModel
+    cm = CostModel()
+    cm.tasks_finished("s", ["g0"], True, 0.001)
+    cm.tasks_started("s", [f"g{i}" for i in range(1, 64)], True, 100.0)
+    t, lb = cm.stats("s", True).estimate(100.5)
+    assert (t, lb) == (0.001, False)
+    cm.task_started("s", "probe", False, 100.0, fraction=1 / 32)
+    t, lb = cm.stats("s", False).estimate(100.01)
+    assert lb and abs(t - 0.32) < 1e-6
+    cm.task_finished("s", "probe", False, 100.0, 100.02, succeeded=False)
+    assert abs(cm.stats("s", False).lower_bound - 0.64) < 1e-6
+    # a CPU slot still raises its estimate for a straggler
+    cm.task_finished("s", "c0", False, 0.0, 0.1)
+    cm.task_started("s", "c1", False, 200.0)
+    assert cm.stats("s", False).estimate(201.0) == (1.0, True)
