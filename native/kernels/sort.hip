@@ -19,6 +19,7 @@
 #include "../include/hbmr/hbmr.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -189,6 +190,139 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
     kout[dst] = key;
     vout[dst] = s_v[j];
   }
+}
+
+// (3') stable scatter with wave-private ranking.  Each wave owns a contiguous
+// 1024-key quarter of the tile (loads stay 512 B per wave instruction), ranks
+// its keys among equal digits with 8 ballots and a wave-private LDS counter per
+// digit — no workgroup barrier inside the per-key loop (radix_scatter_kernel
+// takes three per key) — then one digit-major scan over the 4 waves' counts
+// places every key.  Order (wave, item, lane) is index order, so stable.
+__global__ __launch_bounds__(kSortThreads) void radix_scatter_v2_kernel(
+    const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin, uint64_t* __restrict__ kout,
+    uint32_t* __restrict__ vout, long n, int shift, long ntiles, const uint32_t* __restrict__ hist,
+    const uint32_t* __restrict__ totals) {
+  __shared__ uint64_t s_k[kSortTile];
+  __shared__ uint32_t s_v[kSortTile];
+  __shared__ uint32_t s_wh[kSortWaves][kRadix];  // per-wave digit counts, then wave offsets
+  __shared__ uint32_t s_toff[kRadix];
+  __shared__ uint32_t s_gbase[kRadix];
+  __shared__ uint32_t s_w[4];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const long tile = blockIdx.x;
+  const long base = tile * kSortTile;
+  const int tile_n = (int)min((long)kSortTile, n - base);
+  constexpr int kWaveSpan = kSortTile / kSortWaves;  // 1024 keys per wave
+
+#pragma unroll
+  for (int i = 0; i < kSortWaves; ++i) s_wh[i][t] = 0u;
+  uint64_t k[kSortItems];
+  uint32_t v[kSortItems];
+  const long wbase = base + (long)w * kWaveSpan;
+#pragma unroll
+  for (int i = 0; i < kSortItems; ++i) {
+    const long e = wbase + i * HBMR_WAVE + lane;
+    if (e < n) {
+      k[i] = kin[e];
+      v[i] = vin ? vin[e] : (uint32_t)e;
+    }
+  }
+  __syncthreads();
+  const uint64_t lt = __lanemask_lt();
+  uint32_t rank[kSortItems];
+#pragma unroll
+  for (int i = 0; i < kSortItems; ++i) {
+    const bool valid = w * kWaveSpan + i * HBMR_WAVE + lane < tile_n;
+    const uint32_t d = valid ? digit_of(k[i], shift) : 0u;
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const uint64_t bal = __ballot((d >> b) & 1u);
+      m &= ((d >> b) & 1u) ? bal : ~bal;
+    }
+    const uint32_t pre = __popcll(m & lt);
+    uint32_t old = 0u;
+    if (valid) old = s_wh[w][d];
+    __builtin_amdgcn_wave_barrier();
+    rank[i] = old + pre;
+    if (valid && pre == 0) s_wh[w][d] = old + (uint32_t)__popcll(m);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  // thread t = digit t: tile offset of the digit, each wave's offset within it,
+  // and the digit's global start for this tile
+  {
+    uint32_t c[kSortWaves], cnt = 0;
+#pragma unroll
+    for (int i = 0; i < kSortWaves; ++i) {
+      c[i] = s_wh[i][t];
+      cnt += c[i];
+    }
+    const uint32_t gb = block_excl_scan256(totals[t], s_w);
+    s_gbase[t] = gb + hist[(long)t * ntiles + tile];
+    const uint32_t toff = block_excl_scan256(cnt, s_w);
+    s_toff[t] = toff;
+    uint32_t run = toff;
+#pragma unroll
+    for (int i = 0; i < kSortWaves; ++i) {
+      s_wh[i][t] = run;
+      run += c[i];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kSortItems; ++i) {
+    if (w * kWaveSpan + i * HBMR_WAVE + lane < tile_n) {
+      const uint32_t local = s_wh[w][digit_of(k[i], shift)] + rank[i];
+      s_k[local] = k[i];
+      s_v[local] = v[i];
+    }
+  }
+  __syncthreads();
+  for (int j = t; j < tile_n; j += kSortThreads) {
+    const uint64_t key = s_k[j];
+    const uint32_t d = digit_of(key, shift);
+    const long dst = (long)s_gbase[d] + (j - (long)s_toff[d]);
+    kout[dst] = key;
+    vout[dst] = s_v[j];
+  }
+}
+
+// (1') digit histogram per tile with one LDS add per (wave, digit) group:
+// 8 ballots find the lanes sharing a digit and its leader adds their count
+// (radix_hist_kernel issues one contended LDS atomic per key)
+__global__ __launch_bounds__(kSortThreads) void radix_hist_v2_kernel(const uint64_t* __restrict__ keys,
+                                                                     long n, int shift, long ntiles,
+                                                                     uint32_t* __restrict__ hist) {
+  __shared__ uint32_t s[kSortWaves][kRadix];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+#pragma unroll
+  for (int i = 0; i < kSortWaves; ++i) s[i][t] = 0u;
+  __syncthreads();
+  constexpr int kWaveSpan = kSortTile / kSortWaves;
+  const long wbase = (long)blockIdx.x * kSortTile + (long)w * kWaveSpan;
+  const uint64_t lt = __lanemask_lt();
+  uint64_t k[kSortItems];
+#pragma unroll
+  for (int i = 0; i < kSortItems; ++i) {
+    const long e = wbase + i * HBMR_WAVE + lane;
+    k[i] = e < n ? keys[e] : 0ull;
+  }
+#pragma unroll
+  for (int i = 0; i < kSortItems; ++i) {
+    const bool valid = wbase + i * HBMR_WAVE + lane < n;
+    const uint32_t d = digit_of(k[i], shift);
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const uint64_t bal = __ballot((d >> b) & 1u);
+      m &= ((d >> b) & 1u) ? bal : ~bal;
+    }
+    if (valid && __popcll(m & lt) == 0) s[w][d] += (uint32_t)__popcll(m);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  hist[(long)t * ntiles + blockIdx.x] = s[0][t] + s[1][t] + s[2][t] + s[3][t];
 }
 
 // ------------------------------------------------------------------------ TeraSort
@@ -438,13 +572,26 @@ int hbmr_radix_sort_pairs_u64(uint64_t* keys, uint32_t* vals, uint64_t* tkeys, u
   uint32_t* va = vals;
   uint64_t* kb = tkeys;
   uint32_t* vb = tvals;
+  // HBMR_RADIX_V1=1: the round-1 kernels (per-key atomics, 3 barriers per key), for A/B
+  static const bool v1 = [] {
+    const char* e = getenv("HBMR_RADIX_V1");
+    return e && *e == '1';
+  }();
   int passes = 0;
   for (int shift = begin_bit; shift < end_bit; shift += 8, ++passes) {
-    hipLaunchKernelGGL(radix_hist_kernel, dim3((unsigned)ntiles), dim3(kSortThreads), 0, st, ka, n,
-                       shift, ntiles, hist);
+    if (v1)
+      hipLaunchKernelGGL(radix_hist_kernel, dim3((unsigned)ntiles), dim3(kSortThreads), 0, st, ka,
+                         n, shift, ntiles, hist);
+    else
+      hipLaunchKernelGGL(radix_hist_v2_kernel, dim3((unsigned)ntiles), dim3(kSortThreads), 0, st,
+                         ka, n, shift, ntiles, hist);
     hipLaunchKernelGGL(radix_scan_kernel, dim3(kRadix), dim3(1024), 0, st, hist, ntiles, totals);
-    hipLaunchKernelGGL(radix_scatter_kernel, dim3((unsigned)ntiles), dim3(kSortThreads), 0, st,
-                       ka, va, kb, vb, n, shift, ntiles, hist, totals);
+    if (v1)
+      hipLaunchKernelGGL(radix_scatter_kernel, dim3((unsigned)ntiles), dim3(kSortThreads), 0, st,
+                         ka, va, kb, vb, n, shift, ntiles, hist, totals);
+    else
+      hipLaunchKernelGGL(radix_scatter_v2_kernel, dim3((unsigned)ntiles), dim3(kSortThreads), 0, st,
+                         ka, va, kb, vb, n, shift, ntiles, hist, totals);
     std::swap(ka, kb);
     std::swap(va, vb);
   }
