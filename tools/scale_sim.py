@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--in-process", action="store_true",
+                    help="simulated slots inside each tracker process (no GPU worker processes)")
     a = ap.parse_args()
     rows = []
     for n in [int(x) for x in a.ranks.split(",")]:
@@ -35,7 +37,8 @@ def main():
         for _ in range(a.reps):
             r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n),
                                 "--simulate-ms", str(a.ms), "--steps", str(a.steps),
-                                "--warmup", str(a.warmup)], capture_output=True, text=True,
+                                "--warmup", str(a.warmup)] + (["--in-process"] if a.in_process
+                                                              else []), capture_output=True, text=True,
                                timeout=900)
             line = [x for x in r.stdout.splitlines() if x.startswith("{")]
             if r.returncode != 0 or not line:
@@ -48,12 +51,14 @@ def main():
                "simulated_device_ms_per_job": device_ms,
                "overhead_ms_per_job": statistics.median(ms) - device_ms,
                "phases_ms_median_run": med.get("phases_ms"),
-               "map_tasks_per_s": med["value"]}
+               "map_tasks_per_s": med["value"],
+               "maps_per_tracker_last_job": med.get("maps_per_tracker_last_job")}
         rows.append(row)
         print(json.dumps(row), flush=True)
     out = {"what": "bench.py --simulate-ms rehearsal of the 1/2/4/8-rank headline job on CPU "
                    "(gloo, simulated GPU slots, no split data)",
            "host": {"cpus": os.cpu_count()}, "simulate_ms_per_split": a.ms,
+           "gpu_worker_process": not a.in_process,
            "note": "all ranks, their GPU worker processes and the JobTracker share this host's "
                    "CPUs; on a GPU node they do not, so overhead here is an upper bound",
            "rows": rows, "when": time.strftime("%Y-%m-%d %H:%M:%S")}
