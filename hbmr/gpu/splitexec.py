@@ -103,7 +103,11 @@ def run_split_reduce(host, run, device=None):
         else:
             ctx.device = None
             combined = js.split_job.combine(ctx, outs)
+            if TRACE.on:
+                TRACE.instant("tt.reduce.combined", attempt=spec.attempt_id)
             js.result = js.split_job.reduce(ctx, combined)
+        if TRACE.on:
+            TRACE.instant("tt.reduce.done", attempt=spec.attempt_id)
         with js.lock:
             js.map_outputs.clear()       # consumed
         from ..parallel.collectives import COLLECTIVE_GROUP

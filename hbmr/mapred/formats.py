@@ -160,6 +160,12 @@ class FileInputFormat(InputFormat):
 
 
 class LineRecordReader(RecordReader):
+    """Lines of a split (LineRecordReader.java: a split owns every line that
+    starts at or before its end; the first partial line belongs to the previous
+    split).  Reads 1 MiB chunks and splits them into lines in C (bytes.split)
+    instead of one readline() per record; keys and values are fresh objects."""
+    CHUNK = 1 << 20
+
     def __init__(self, job, split: FileSplit):
         self.start = split.start
         self.end = split.start + split.length
@@ -177,20 +183,41 @@ class LineRecordReader(RecordReader):
             # skip the first (partial) line; the previous split owns it
             skipped = self.f.readline()
             self.pos += len(skipped)
+        self._lines = []        # lines of the current chunk (newline stripped)
+        self._i = 0
+        self._nl = 1            # 1: the chunk's lines each ended with "\n"
+        self._tail = b""        # partial last line of the chunk read so far
+
+    def _fill(self):
+        while True:
+            data = self.f.read(self.CHUNK)
+            if not data:
+                if self._tail:
+                    self._lines, self._tail, self._i, self._nl = [self._tail], b"", 0, 0
+                    return True
+                return False
+            parts = (self._tail + data if self._tail else data).split(b"\n")
+            self._tail = parts.pop()
+            if parts:
+                self._lines, self._i, self._nl = parts, 0, 1
+                return True
 
     def next(self):
-        if self.pos > self.end:
+        pos = self.pos
+        if pos > self.end:
             return None
-        line = self.f.readline()
-        if not line:
+        if self._i >= len(self._lines) and not self._fill():
             return None
-        key = LongWritable(self.pos)
-        self.pos += len(line)
-        if line.endswith(b"\n"):
+        line = self._lines[self._i]
+        self._i += 1
+        self.pos = pos + len(line) + self._nl
+        if line.endswith(b"\r"):
             line = line[:-1]
-            if line.endswith(b"\r"):
-                line = line[:-1]
-        return key, Text(line)
+        key = LongWritable.__new__(LongWritable)
+        key.value = pos
+        val = Text.__new__(Text)
+        val.bytes = line
+        return key, val
 
     def getPos(self):  # noqa: N802
         return self.pos

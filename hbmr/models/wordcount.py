@@ -2,19 +2,63 @@
 
 Same job as hadoop-1.0.3/src/examples/org/apache/hadoop/examples/WordCount.java:
 map emits (word, 1) per whitespace token, combiner + reducer sum.
+
+By default the mapper combines in memory (``hbmr.wordcount.inmapper.combine``):
+it counts the split's tokens in a C-level Counter and emits each distinct word
+once, with its count, when the split ends (or when ``hbmr.wordcount.inmapper.
+max.words`` distinct words are held).  The reduce output is the same; the map
+side does what WordCount's combiner (IntSumReducer) would, without a Python
+collect() per token, which bound the per-token job at 4.4 MB/s.  ``false``
+restores the reference's per-token emit.
 """
 from __future__ import annotations
 
+from collections import Counter
+
 from ..io.writable import IntWritable, Text
 from ..mapred import FileInputFormat, FileOutputFormat, JobClient, JobConf, Mapper, Reducer
+
+INMAPPER_KEY = "hbmr.wordcount.inmapper.combine"
 
 
 class WordCountMapper(Mapper):
     one = IntWritable(1)
 
+    def configure(self, job):
+        self.inmapper = job.get_boolean(INMAPPER_KEY, True)
+        self.max_words = job.get_int("hbmr.wordcount.inmapper.max.words", 1 << 20)
+        self.counts = Counter()
+        self.lines = []         # lines held back: counted 4096 at a time in one C call
+        self.out = None
+
     def map(self, key, value, output, reporter):
-        for w in value.bytes.split():
-            output.collect(Text(w), self.one)
+        if not getattr(self, "inmapper", False):
+            for w in value.bytes.split():
+                output.collect(Text(w), self.one)
+            return
+        self.out = output
+        lines = self.lines
+        lines.append(value.bytes)
+        if len(lines) >= 4096:
+            self._count()
+            if len(self.counts) >= self.max_words:
+                self._flush()
+
+    def _count(self):
+        if self.lines:
+            self.counts.update(b"\n".join(self.lines).split())
+            self.lines.clear()
+
+    def _flush(self):
+        self._count()
+        out = self.out
+        for w, c in self.counts.items():
+            out.collect(Text(w), IntWritable(c))
+        self.counts.clear()
+
+    def close(self):
+        if self.out is not None and (self.counts or self.lines):
+            self._flush()
 
 
 class IntSumReducer(Reducer):
