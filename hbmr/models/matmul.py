@@ -27,6 +27,9 @@ M_KEY, K_KEY, N_KEY = "hbmr.matmul.m", "hbmr.matmul.k", "hbmr.matmul.n"
 ROWS_KEY = "hbmr.matmul.split.rows"
 SEED_KEY = "hbmr.matmul.seed"
 OUTC_KEY = "hbmr.matmul.output.dtype"   # float32 | bfloat16
+# GPU GEMM of a map task: "hbmr" = native/kernels/gemm.hip (MFMA, hand-written);
+# "hipblaslt" = torch.matmul (the vendor library, for comparison: a plain GEMM)
+GEMM_KEY = "hbmr.matmul.gemm"
 
 _M32 = 0xFFFFFFFF
 
@@ -91,6 +94,9 @@ class MatmulSplitJob(SplitJob):
         self.out_dtype = torch.bfloat16 if conf.get(OUTC_KEY, "float32") == "bfloat16" \
             else torch.float32
         self.out = conf.get("mapred.output.dir")
+        self.gemm = conf.get(GEMM_KEY, "hbmr")
+        if self.gemm not in ("hbmr", "hipblaslt"):
+            raise ValueError(f"{GEMM_KEY} must be hbmr or hipblaslt, not {self.gemm!r}")
 
     def get_splits(self, conf, trackers):
         out = []
@@ -114,11 +120,18 @@ class MatmulSplitJob(SplitJob):
     def _map(self, ctx, data):
         a = data["a"]
         bt = SIDE.bt(self.seed, self.k, self.n, a.device)
-        c = G.matmul_tn(a, bt, out_dtype=self.out_dtype if a.device.type == "cuda"
-                        else torch.float32)
+        if a.device.type == "cuda" and self.gemm == "hipblaslt":
+            c = torch.matmul(a, bt.t())
+            if self.out_dtype != torch.bfloat16:
+                c = c.float()
+            cs = c.sum(dtype=torch.float64)
+        else:
+            # the checksum comes out of the GEMM epilogue (no second pass over C)
+            c, cs = G.matmul_tn(a, bt, out_dtype=self.out_dtype if a.device.type == "cuda"
+                                else torch.float32, with_sum=True)
         ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, a.shape[0])
         ctx.reporter.incrCounter("hbmr.Matmul", "FLOPS", 2 * a.shape[0] * self.k * self.n)
-        return {"row0": data["row0"], "c": c, "checksum": c.double().sum()}
+        return {"row0": data["row0"], "c": c, "checksum": cs}
 
     def map_gpu(self, ctx, data):
         return self._map(ctx, data)

@@ -85,6 +85,8 @@ _SIGS = {
     # GEMM (native/kernels/gemm.hip)
     "hbmr_gemm_bf16_tn": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_long, c_long,
                                   ctypes.c_float, c_int, c_void_p]),
+    "hbmr_gemm_bf16_tn_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_long, c_long,
+                                     ctypes.c_float, c_int, c_void_p, c_void_p]),
 }
 
 

@@ -24,14 +24,16 @@ def _pad(x: torch.Tensor, rows: int, cols: int) -> torch.Tensor:
 
 
 def matmul_tn(a: torch.Tensor, bt: torch.Tensor, alpha: float = 1.0,
-              out_dtype=torch.float32, stream=None) -> torch.Tensor:
+              out_dtype=torch.float32, stream=None, with_sum=False):
+    """C = alpha · A · Btᵀ.  ``with_sum``: returns (C, fp64 sum of C's elements
+    as stored), the sum taken in the GEMM epilogue (per-tile partials)."""
     if a.dim() != 2 or bt.dim() != 2 or a.shape[1] != bt.shape[1]:
         raise ValueError("A[M,K], Bt[N,K] required")
     M, K = a.shape
     N = bt.shape[0]
     if a.device.type != "cuda":
-        c = (a.float() @ bt.float().t()) * alpha
-        return c.to(out_dtype)
+        c = ((a.float() @ bt.float().t()) * alpha).to(out_dtype)
+        return (c, c.sum(dtype=torch.float64)) if with_sum else c
     if a.dtype != torch.bfloat16 or bt.dtype != torch.bfloat16:
         raise ValueError("bf16 operands required on the GPU")
     Mp, Np, Kp = -(-M // TM) * TM, -(-N // TN) * TN, -(-K // TK) * TK
@@ -39,11 +41,15 @@ def matmul_tn(a: torch.Tensor, bt: torch.Tensor, alpha: float = 1.0,
     if out_dtype not in (torch.float32, torch.bfloat16):
         raise ValueError("C must be fp32 or bf16")
     c = torch.empty(Mp, Np, dtype=out_dtype, device=a.device)
-    rc = _lib.load().hbmr_gemm_bf16_tn(ap.data_ptr(), bp.data_ptr(), c.data_ptr(), Mp, Np, Kp,
-                                        float(alpha), int(out_dtype == torch.bfloat16),
-                                        _lib.stream_handle(stream))
-    _lib.check(rc, "hbmr_gemm_bf16_tn")
-    return c if (Mp == M and Np == N) else c[:M, :N]
+    part = torch.empty((Mp // TM) * (Np // TN), dtype=torch.float64, device=a.device) \
+        if with_sum else None
+    rc = _lib.load().hbmr_gemm_bf16_tn_ex(ap.data_ptr(), bp.data_ptr(), c.data_ptr(), Mp, Np, Kp,
+                                           float(alpha), int(out_dtype == torch.bfloat16),
+                                           part.data_ptr() if part is not None else None,
+                                           _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_gemm_bf16_tn_ex")
+    c = c if (Mp == M and Np == N) else c[:M, :N]
+    return (c, part.sum()) if with_sum else c
 
 
 def matmul(a: torch.Tensor, b: torch.Tensor, **kw) -> torch.Tensor:

@@ -89,6 +89,9 @@ long hbmr_radix_sort_workspace_bytes(long n);
 // M, N multiples of 256, K of 64.
 int hbmr_gemm_bf16_tn(const void* A, const void* Bt, void* C, long M, long N, long K, float alpha,
                       int out_bf16, hipStream_t st);
+// ... plus partials[(M/256)·(N/256)] = fp64 sum of each 256×256 tile of C (null: none)
+int hbmr_gemm_bf16_tn_ex(const void* A, const void* Bt, void* C, long M, long N, long K,
+                         float alpha, int out_bf16, double* partials, hipStream_t st);
 #endif
 // ---- text / WordCount (native/kernels/text.hip) ---------------------------------
 #ifndef HBMR_NO_HIP_DECLS

@@ -49,7 +49,7 @@ __device__ __forceinline__ void stage_tile(char* lds, const __bf16* __restrict__
 template <bool OUT_BF16>
 __global__ __launch_bounds__(kGemmThreads, 1) void gemm_bf16_tn_kernel(
     const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void* __restrict__ Cv, long M,
-    long N, long K, float alpha) {
+    long N, long K, float alpha, double* __restrict__ partials) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -105,7 +105,10 @@ __global__ __launch_bounds__(kGemmThreads, 1) void gemm_bf16_tn_kernel(
     }
   }
 
-  // C/D map of 16x16x32: col = lane & 15, row = 4 (lane >> 4) + reg
+  // C/D map of 16x16x32: col = lane & 15, row = 4 (lane >> 4) + reg.
+  // partials != null: the tile's sum of the stored C values (fp64), one per
+  // workgroup — the map task's checksum without a second pass over C.
+  double csum = 0.0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
 #pragma unroll
@@ -115,11 +118,28 @@ __global__ __launch_bounds__(kGemmThreads, 1) void gemm_bf16_tn_kernel(
       for (int r = 0; r < 4; ++r) {
         const long row = m0 + wm * 128 + i * 16 + fq * 4 + r;
         const float v = acc[i][j][r] * alpha;
-        if (OUT_BF16)
-          reinterpret_cast<uint16_t*>(Cv)[row * N + col] = hbmr_f32_to_bf16(v);
-        else
+        if (OUT_BF16) {
+          const uint16_t h = hbmr_f32_to_bf16(v);
+          reinterpret_cast<uint16_t*>(Cv)[row * N + col] = h;
+          csum += (double)__uint_as_float((uint32_t)h << 16);
+        } else {
           reinterpret_cast<float*>(Cv)[row * N + col] = v;
+          csum += (double)v;
+        }
       }
+    }
+  }
+  if (partials) {
+    __shared__ double s_red[kGemmThreads / 64];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) csum += __shfl_xor(csum, o);
+    if (lane == 0) s_red[wave] = csum;
+    __syncthreads();
+    if (tid == 0) {
+      double s = 0.0;
+#pragma unroll
+      for (int w = 0; w < kGemmThreads / 64; ++w) s += s_red[w];
+      partials[blockIdx.x] = s;
     }
   }
 }
@@ -130,9 +150,10 @@ bool g_gemm_lds_set = false;
 
 extern "C" {
 
-// C = alpha · A · Btᵀ; out_bf16 selects a bf16 C (else fp32).
-int hbmr_gemm_bf16_tn(const void* A, const void* Bt, void* C, long M, long N, long K, float alpha,
-                      int out_bf16, hipStream_t st) {
+// C = alpha · A · Btᵀ; out_bf16 selects a bf16 C (else fp32).  partials (may be
+// null): (M/256)·(N/256) doubles, each workgroup's sum of its stored C tile.
+int hbmr_gemm_bf16_tn_ex(const void* A, const void* Bt, void* C, long M, long N, long K,
+                         float alpha, int out_bf16, double* partials, hipStream_t st) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   if (M % kBM || N % kBN || K % kBK) return (int)hipErrorInvalidValue;
   if (!g_gemm_lds_set) {
@@ -147,12 +168,17 @@ int hbmr_gemm_bf16_tn(const void* A, const void* Bt, void* C, long M, long N, lo
   if (out_bf16)
     hipLaunchKernelGGL(gemm_bf16_tn_kernel<true>, dim3((unsigned)tiles), dim3(kGemmThreads),
                        kGemmLds, st, reinterpret_cast<const __bf16*>(A),
-                       reinterpret_cast<const __bf16*>(Bt), C, M, N, K, alpha);
+                       reinterpret_cast<const __bf16*>(Bt), C, M, N, K, alpha, partials);
   else
     hipLaunchKernelGGL(gemm_bf16_tn_kernel<false>, dim3((unsigned)tiles), dim3(kGemmThreads),
                        kGemmLds, st, reinterpret_cast<const __bf16*>(A),
-                       reinterpret_cast<const __bf16*>(Bt), C, M, N, K, alpha);
+                       reinterpret_cast<const __bf16*>(Bt), C, M, N, K, alpha, partials);
   return (int)hipGetLastError();
+}
+
+int hbmr_gemm_bf16_tn(const void* A, const void* Bt, void* C, long M, long N, long K, float alpha,
+                      int out_bf16, hipStream_t st) {
+  return hbmr_gemm_bf16_tn_ex(A, Bt, C, M, N, K, alpha, out_bf16, nullptr, st);
 }
 
 }  // extern "C"

@@ -46,6 +46,11 @@ def test_gemm_kernel_matches_fp32_reference(m, k, n):
     assert torch.allclose(c, ref, atol=2e-3 * k ** 0.5, rtol=1e-3), (c - ref).abs().max()
     cb = G.matmul_tn(a.cuda(), bt.cuda(), out_dtype=torch.bfloat16).cpu().float()
     assert torch.allclose(cb, ref, atol=0.05 * k ** 0.5, rtol=2e-2)
+    # the epilogue checksum is the fp64 sum of C as stored (padding adds zeros)
+    for dt in (torch.float32, torch.bfloat16):
+        c2, cs = G.matmul_tn(a.cuda(), bt.cuda(), out_dtype=dt, with_sum=True)
+        want = c2.double().sum().item()
+        assert abs(cs.item() - want) <= 1e-9 * max(1.0, c2.double().abs().sum().item())
 
 
 @pytest.mark.gpu

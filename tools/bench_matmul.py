@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--split-rows", type=int, default=8192)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--gemm", default="hbmr", choices=["hbmr", "hipblaslt"],
+                    help="map-task GEMM (hbmr.matmul.gemm)")
     a = ap.parse_args()
     import torch
 
@@ -58,6 +60,7 @@ def main():
     conf = JobConf()
     conf.set_int("hbmr.gpu.queue.depth", 16)
     conf.set_int("mapred.task.timeout", 0)
+    conf.set("hbmr.matmul.gemm", a.gemm)
     with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=0) as cl:
         job = MM.matmul_conf(conf, m=a.m, k=a.k, n=a.n, split_rows=a.split_rows,
                              out_dtype="bfloat16")
@@ -73,7 +76,7 @@ def main():
         cl.submit_job(sync_conf(conf)).waitForCompletion()
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / a.steps
-    res.update(job_m=a.m, job_k=a.k, job_n=a.n, split_rows=a.split_rows,
+    res.update(gemm=a.gemm, job_m=a.m, job_k=a.k, job_n=a.n, split_rows=a.split_rows,
                job_seconds=round(dt, 4), job_tflops=round(2.0 * a.m * a.k * a.n / dt / 1e12, 1),
                map_tasks_per_s=round(-(-a.m // a.split_rows) / dt, 1))
     print(json.dumps(res))
