@@ -53,10 +53,14 @@ def run_split_cpu_map(host, run):
             # dropped (the GPUs run the real task)
             sample = js.split_job.load_split_sample(sspec, "cpu", spec.profile_fraction)
             run.status.start_time = time.time()
+            t0 = time.perf_counter()
             js.split_job.map_cpu(ctx, sample)
+            compute = time.perf_counter() - t0
             rep.counters = C.Counters()
+            # the probe's own compute time rides in device_time: the JobTracker
+            # scales it by 1/fraction, and launch/report latency must not be
             host._finish(run, P.SUCCEEDED, output={"tracker": host.name, "where": "cpu",
-                                                   "profile": True})
+                                                   "profile": True}, device_time=compute)
             return
         data, _hit = host.split_cache.get_or_load(
             sspec.key, "cpu", lambda: js.split_job.load_split(sspec, "cpu"),

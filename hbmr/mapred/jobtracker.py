@@ -983,7 +983,10 @@ class JobTracker:
         if a.profile_fraction:
             # sampled profiling probe: its only product is the CPU time estimate
             # (measured on the sample, scaled to a whole split)
-            dt = max(0.0, a.finish - a.start) / a.profile_fraction
+            # (its own compute time when the tracker reports it: the launch and
+            # report latency around it would be multiplied by 1/fraction too)
+            meas = a.device_time if a.device_time > 0 else a.finish - a.start
+            dt = max(0.0, meas) / a.profile_fraction
             self.cost_model.task_finished(jip.signature, a.aid, False, a.start, a.start + dt)
             self.history.log("PROFILE_FINISHED", attempt=a.aid, tracker=a.tracker,
                              fraction=a.profile_fraction, est_seconds=dt)
