@@ -15,6 +15,7 @@ SURVEY.md B2) — here both spellings address one key.
 """
 from __future__ import annotations
 
+import functools
 import getpass
 import os
 import re
@@ -41,6 +42,13 @@ def _conf_dir() -> Path | None:
             return Path(v)
     return None
 
+
+
+@functools.lru_cache(maxsize=1)
+def _login_user():
+    """getpass.getuser() once per process (``${user.name}`` in every
+    hadoop.tmp.dir lookup called it on each job's hot path)."""
+    return getpass.getuser()
 
 class Configuration:
     _default_resources = ["core-default.xml", "core-site.xml"]
@@ -139,7 +147,7 @@ class Configuration:
             if rep is None:
                 rep = self.get_raw(var)
             if rep is None and var in ("USER", "user.name"):
-                rep = getpass.getuser()
+                rep = _login_user()
             if rep is None:
                 return value
             value = value[:m.start()] + rep + value[m.end():]

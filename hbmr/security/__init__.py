@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import base64
 import contextlib
+import functools
 import getpass
 import grp
 import hashlib
@@ -101,6 +102,7 @@ class UserGroupInformation:
         return f"UGI({self.user})"
 
 
+@functools.lru_cache(maxsize=1)
 def _login_name():
     try:
         return getpass.getuser()
