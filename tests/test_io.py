@@ -150,6 +150,28 @@ def test_configuration_layering(tmp_path, monkeypatch):
     assert "<name>c</name>" in buf.getvalue()
 
 
+def test_configuration_default_snapshot_tracks_site_files(tmp_path, monkeypatch):
+    """New Configurations copy a cached layering of the default resources;
+    editing (or adding) a site file in the conf dir invalidates it."""
+    import os
+    monkeypatch.setenv("HBMR_CONF_DIR", str(tmp_path))
+    assert Configuration().get("snap.k") is None
+    site = tmp_path / "core-site.xml"
+    site.write_text("<configuration><property><name>snap.k</name><value>1</value>"
+                    "</property></configuration>")
+    assert Configuration().get("snap.k") == "1"
+    a = Configuration()
+    a.set("snap.k", "local")            # a copy, not the shared snapshot
+    assert Configuration().get("snap.k") == "1"
+    site.write_text("<configuration><property><name>snap.k</name><value>2</value>"
+                    "</property></configuration>")
+    st = os.stat(site)
+    os.utime(site, ns=(st.st_atime_ns, st.st_mtime_ns + 1_000_000))
+    assert Configuration().get("snap.k") == "2"
+    monkeypatch.delenv("HBMR_CONF_DIR")
+    assert Configuration().get("snap.k") is None
+
+
 def test_jobconf_gpu_keys_and_typo_alias():
     job = JobConf()
     assert job.get_int("mapred.tasktracker.map.gpu.tasks.maximum") == 0
