@@ -65,6 +65,8 @@ def main():
                          "JobTracker until that one succeeds (hbmr.job.depends.on); default: "
                          "submit after it finished")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("-D", dest="defines", action="append", default=[], metavar="KEY=VALUE",
+                    help="extra configuration (e.g. -D hbmr.gpu.first.chunk=8)")
     a = ap.parse_args()
     logging.basicConfig(level=logging.INFO if a.verbose else logging.WARNING,
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
@@ -109,6 +111,9 @@ def main():
         conf.set("hbmr.gpu.simulate", "true")
         conf.set("hbmr.gpu.simulate.nodata", "true")
         conf.set("hbmr.gpu.simulate.task.ms", str(a.simulate_ms))
+    for kv in a.defines:
+        k, _, v = kv.partition("=")
+        conf.set(k.strip(), v.strip())
     node = Node(conf, use_gpu=has_gpu)
     if not node.is_master:
         node.serve_until_shutdown()

@@ -54,6 +54,12 @@ class _Device:
         self.last_error = ""
 
 
+class _Batch(list):
+    """A queued list of runs whose submitter waits (``picked``) until the
+    launcher has put it on the device."""
+    picked = None
+
+
 class _NoPrefetch:
     @staticmethod
     def take(key):
@@ -95,6 +101,11 @@ class GpuRuntime:
         self.slots_per_device = max(1, slots_per_device)
         self.max_batch = max(1, tracker.conf.get_int("hbmr.gpu.batch.max", 64))
         self.first_chunk = max(1, tracker.conf.get_int("hbmr.gpu.first.chunk", 4))
+        # > 0: the submitter of an idle device's first chunk waits (up to this
+        # long) until it is launched.  In-process traces show the device
+        # starting ~1 ms earlier, but same-box A/Bs of the bench measured no
+        # end-to-end gain (worker process: 33.7 vs 35.5 ms median), so off
+        self.handoff_s = tracker.conf.get_float("hbmr.gpu.first.chunk.handoff.ms", 0.0) / 1e3
         self._stop = threading.Event()
         reserve = tracker.conf.get_float("hbmr.gpu.hbm.reserve.gb", 16.0) * (1 << 30)
         for d, dev in self.devices.items():
@@ -148,12 +159,25 @@ class GpuRuntime:
                 continue
             by_dev.setdefault(d, []).append(run)
         for d, rs in by_dev.items():
-            self.devices[d].q.put(rs)
+            dev = self.devices[d]
+            if len(rs) <= self.first_chunk and self.handoff_s > 0 and dev.q.empty() and \
+                    not any(s.inflight for s in dev.slots):
+                # an idle device's first chunk of a bulk launch: the caller goes
+                # on to build the rest of the batch and, holding the interpreter,
+                # kept the launcher from starting the device for ~0.7 ms (traced
+                # on the box); wait until the chunk is on its streams
+                b = _Batch(rs)
+                b.picked = threading.Event()
+                dev.q.put(b)
+                b.picked.wait(self.handoff_s)
+            else:
+                dev.q.put(rs)
 
     # -- launcher -----------------------------------------------------------------------
-    def _drain(self, dev: _Device, first):
+    def _drain(self, dev: _Device, first, picked):
         """first + whatever else is queued right now (queue items are lists of
-        runs; at least everything of ``first``, then up to max_batch)."""
+        runs; at least everything of ``first``, then up to max_batch); the
+        submitters waiting on them are collected in ``picked``."""
         runs = list(first)
         while len(runs) < self.max_batch:
             try:
@@ -164,6 +188,8 @@ class GpuRuntime:
                 dev.q.put(None)
                 break
             runs.extend(r)
+            if getattr(r, "picked", None) is not None:
+                picked.append(r.picked)
         return runs
 
     def _worker(self, dev: _Device):
@@ -176,7 +202,8 @@ class GpuRuntime:
             if run is None:
                 break
             groups: dict = {}
-            for r in self._drain(dev, run):
+            picked = [run.picked] if getattr(run, "picked", None) is not None else []
+            for r in self._drain(dev, run, picked):
                 if r.kill.is_set():
                     tracker._finish(r, P.KILLED, "killed before start")
                     continue
@@ -196,8 +223,12 @@ class GpuRuntime:
                 rest = len(runs) - i
                 nslot = len(dev.slots) if hasattr(sj, "map_gpu_batch") else rest
                 per = min(self.max_batch, max(1, -(-rest // max(1, nslot))))
+                if rest <= self.first_chunk and hasattr(sj, "map_gpu_batch"):
+                    per = max(1, rest)       # a first chunk: one launch, no split
                 for j in range(i, len(runs), per):
                     self._launch_batch(dev, runs[j:j + per], js, sj, SplitSpec, TaskContext)
+            for ev in picked:
+                ev.set()
 
     def _launch_batch(self, dev, runs, js, sj, SplitSpec, TaskContext):  # noqa: N803
         tracker = self.tracker

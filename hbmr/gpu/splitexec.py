@@ -103,6 +103,8 @@ def run_split_reduce(host, run, device=None):
             ctx.device = device
             with torch.cuda.device(device):
                 combined = js.split_job.combine(ctx, outs)
+                if TRACE.on:
+                    TRACE.instant("tt.reduce.combined", attempt=spec.attempt_id)
                 js.result = js.split_job.reduce(ctx, combined)
         else:
             ctx.device = None

@@ -206,9 +206,16 @@ def _save_centroids_async(cdir, key, prev, cen):
                 os.remove(old.pop(0))
             except OSError:
                 pass
-    threading.Thread(target=_write, daemon=True, name="kmeans-centroid-save").start()
+    global _SAVER
+    if _SAVER is None:
+        import concurrent.futures as cf
+        # one long-lived writer: files land in iteration order, and starting a
+        # thread per reduce cost ~0.1 ms on the job's critical path
+        _SAVER = cf.ThreadPoolExecutor(1, thread_name_prefix="kmeans-centroid-save")
+    _SAVER.submit(_write)
 
 
+_SAVER = None
 _SAVED: dict = {}
 _PINNED_INFLIGHT: list = []     # (event, pinned host buffer) of in-flight split loads
 
@@ -558,10 +565,14 @@ class KMeansSplitJob(SplitJob):
             img.chalf = old.chalf.clone()
             img.shift2 = torch.zeros_like(old.shift2)
             img.refresh(sums, counts)
+            if TRACE.on:
+                TRACE.instant("kmeans.refresh_launched")
             STORE.put_image(self.cout, sums.device, img)
             # the shift and the point count in one device->host copy (one sync)
             shift, npts = torch.stack([img.shift2.max().double().sqrt(),
                                        counts.sum().double()]).tolist()
+            if TRACE.on:
+                TRACE.instant("kmeans.shift_synced")
             new_cen = None
         else:
             old = STORE.host_centroids(self.cin)
@@ -573,6 +584,8 @@ class KMeansSplitJob(SplitJob):
             npts = int(counts.sum().item())
             STORE.put_host(self.cout, new_cen)
         self._write_output(ctx, counts, new_cen)
+        if TRACE.on:
+            TRACE.instant("kmeans.output_written")
         res = {"shift": shift, "points": int(npts), "centroids_key": self.cout}
         if ctx.rank == 0 and self.cdir:
             cen = new_cen if new_cen is not None else STORE.image(self.cout, sums.device).cen
@@ -582,6 +595,8 @@ class KMeansSplitJob(SplitJob):
             # in another process than the reduce, e.g. with GPU worker processes)
             cen = new_cen if new_cen is not None else STORE.image(self.cout, sums.device).cen
             res["centroids"] = encode_centroids(cen[:, :self.d])
+        if TRACE.on:
+            TRACE.instant("kmeans.reduce_return")
         return res
 
     def _write_output(self, ctx, counts, new_cen):

@@ -102,3 +102,18 @@ def test_split_cache_hits_after_first_iteration():
         assert r2["counters"].get(g, "GPU_SPLIT_CACHE_HITS") == 4
         assert r2["counters"].get(g, "GPU_SPLIT_CACHE_MISSES") == 0
         assert torch.cuda.is_available()
+
+
+@pytest.mark.gpu
+def test_gpu_first_chunk_handoff_gives_same_result():
+    """hbmr.gpu.first.chunk.handoff.ms > 0 (the submitter of an idle device's
+    first chunk waits until it is launched) changes only launch timing: the
+    iteration's centroids equal those of the default launch path."""
+    n, k, d, sp = 120000, 16, 128, 5000      # 24 maps: a first chunk of 4 + the rest
+    inp = f"synthetic:{n}:9"
+    base, r0 = _one_step(JobConf(), True, inp, k, d, sp, iters=2)
+    conf = JobConf()
+    conf.set("hbmr.gpu.first.chunk.handoff.ms", "2.0")
+    got, r1 = _one_step(conf, True, inp, k, d, sp, iters=2)
+    assert r1["counters"].get(JOB, "GPU_MAP_TASKS") == n // sp
+    assert torch.equal(base, got)
