@@ -60,10 +60,12 @@ def main():
                     help="CPU rehearsal: simulated GPU slots with this device time per split")
     ap.add_argument("--in-process", action="store_true",
                     help="run the GPU slots inside the tracker process (no worker process)")
-    ap.add_argument("--prefetch", action="store_true",
+    ap.add_argument("--prefetch", action=argparse.BooleanOptionalAction, default=True,
                     help="submit each iteration job while its predecessor runs, held by the "
-                         "JobTracker until that one succeeds (hbmr.job.depends.on); default: "
-                         "submit after it finished")
+                         "JobTracker until that one succeeds (hbmr.job.depends.on), as a "
+                         "JobControl driver would; --no-prefetch submits after it finished "
+                         "(same-box A/B, 1x MI355X: 32.4 vs 33.5 ms median, "
+                         "profiles/r02_prefetch_ab.json)")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("-D", dest="defines", action="append", default=[], metavar="KEY=VALUE",
                     help="extra configuration (e.g. -D hbmr.gpu.first.chunk=8)")
