@@ -52,6 +52,13 @@ class _Device:
         self.total_mem = props.total_memory
         self.device_errors = 0      # consecutive failed batches with a device-level error
         self.last_error = ""
+        # device-time accounting: batch intervals are placed on one timeline
+        # (offsets from ``ref``) and a batch is charged only the busy time it
+        # adds beyond the frontier, so overlapping slot streams are not
+        # double-counted in the tasks' device time (the cost model's t_gpu)
+        self.ref = None
+        self.busy_frontier = 0.0
+        self.busy_lock = threading.Lock()
 
 
 class _Batch(list):
@@ -194,6 +201,10 @@ class GpuRuntime:
 
     def _worker(self, dev: _Device):
         torch.cuda.set_device(dev.index)
+        ref = torch.cuda.Event(enable_timing=True)
+        ref.record()
+        ref.synchronize()
+        dev.ref = ref
         tracker = self.tracker
         from ..gpu.splitjob import SplitSpec
         from ..mapred.tasktracker import TaskContext
@@ -328,8 +339,11 @@ class GpuRuntime:
                 ev1.synchronize()
                 if TRACE.on:
                     TRACE.instant("gpu.complete", n=len(runs), slot=slot.index)
-                # a batch completes together; its device time is shared evenly
-                dt = ev0.elapsed_time(ev1) / 1000.0 / max(1, len(runs))
+                # a batch completes together; the busy time it adds to the
+                # device (beyond what overlapping batches on the other slots
+                # already account for) is shared evenly by its tasks
+                dt = self._busy_ms(self.devices[slot.device.index], ev0, ev1) / 1000.0 / \
+                    max(1, len(runs))
                 for r, out in zip(runs, outs):   # a batch may mix jobs
                     with r.job.lock:
                         r.job.map_outputs[r.spec.attempt_id] = out
@@ -347,6 +361,18 @@ class GpuRuntime:
                                     f"{type(e).__name__}: {e}\n{traceback.format_exc()[-2000:]}")
             finally:
                 slot.inflight -= len(runs)
+
+    @staticmethod
+    def _busy_ms(dev, ev0, ev1):
+        elapsed = ev0.elapsed_time(ev1)
+        if dev.ref is None:
+            return elapsed
+        start = dev.ref.elapsed_time(ev0)
+        end = start + elapsed
+        with dev.busy_lock:
+            busy = max(0.0, end - max(start, dev.busy_frontier))
+            dev.busy_frontier = max(dev.busy_frontier, end)
+        return busy
 
     # -- device health (NodeHealthChecker probes) --------------------------------------
     def _note_error(self, d, exc):

@@ -117,3 +117,25 @@ def test_gpu_first_chunk_handoff_gives_same_result():
     got, r1 = _one_step(conf, True, inp, k, d, sp, iters=2)
     assert r1["counters"].get(JOB, "GPU_MAP_TASKS") == n // sp
     assert torch.equal(base, got)
+
+
+@pytest.mark.gpu
+def test_gpu_device_time_does_not_double_count_overlapping_slots():
+    """Two GPU slots (streams) run a job's batches concurrently; the tasks'
+    device time (GPU_KERNEL_US, the cost model's t_gpu) sums to the device's
+    busy time, which cannot exceed the job's wall time."""
+    import time
+    n, k, d, sp = 1_600_000, 256, 128, 50_000      # 32 maps over 2 slots
+    inp = f"synthetic:{n}:4"
+    conf = JobConf()
+    with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=0,
+                      gpu_slots_per_device=2) as cl:
+        drv = K.KMeansDriver(cl.submit_job, lambda rj: rj._impl.jip.result[0], conf=conf, k=k,
+                             d=d, inp=inp, split_points=sp)
+        drv.step()                                  # splits materialised in HBM
+        t0 = time.perf_counter()
+        r = drv.step()
+        wall_us = (time.perf_counter() - t0) * 1e6
+    assert r["counters"].get(JOB, "GPU_MAP_TASKS") == n // sp
+    busy_us = r["counters"].get("hbmr.GpuCounters", "GPU_KERNEL_US")
+    assert 0 < busy_us <= wall_us * 1.02, (busy_us, wall_us)
