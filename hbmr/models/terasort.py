@@ -337,6 +337,24 @@ class TeraSortSplitJob(SplitJob):
         # a rank that ran no map learns R (and the splitters) from its peers
         nparts = max(int(g[0]) for g in comm.all_gather(
             torch.tensor([nparts or 0], dtype=torch.int64)))
+        # ... and the splitters, which a rank owning several partitions needs to
+        # cut its output (every rank takes part: the collective sequence must
+        # not depend on whether a rank ran maps)
+        spl = None
+        if nparts > 1:
+            k = nparts - 1
+            mine = torch.zeros(1 + 2 * k, dtype=torch.int64)
+            if outs:
+                shi, slo = _parse_keys(self._splitters_of(outs))
+                assert shi.numel() == k, (shi.numel(), k)
+                mine[0] = 1
+                mine[1:1 + k] = shi
+                mine[1 + k:] = slo
+            for g in comm.all_gather(mine):
+                g = g.cpu()
+                if int(g[0]):
+                    spl = (g[1:1 + k], g[1 + k:])
+                    break
         counts = [0] * W
         splits, rowsl = [], []
         if outs:
@@ -370,7 +388,9 @@ class TeraSortSplitJob(SplitJob):
         if self.out:
             a, b = self.owner_range(me, W, nparts)
             if b - a > 1:
-                shi, slo = _parse_keys(self._splitters_of(outs))
+                if spl is None:
+                    raise RuntimeError("no rank holds the splitters of this job")
+                shi, slo = spl
                 cut = S.split_offsets(hs, ls, shi[a:b - 1].to(dev), slo[a:b - 1].to(dev)) \
                     .to("cpu").tolist()
                 cut = [0] + cut[1:-1] + [n]

@@ -96,6 +96,23 @@ def test_terasort_more_partitions_than_trackers(tmp_path, trackers):
     assert T.teravalidate(str(out))["misordered"] == 0
 
 
+def test_terasort_rank_without_maps_writes_its_partitions(tmp_path):
+    """2 splits on 3 trackers: at least one rank runs no map, yet owns two of
+    the 7 partitions; it learns R and the splitters from its peers (the
+    collective sequence is the same on every rank) and writes its part files."""
+    rows = 5000
+    out = tmp_path / "out"
+    with LocalCluster(JobConf(), num_trackers=3, cpu_slots=2) as cl:
+        rj = cl.submit_job(T.terasort_conf(rows=rows, split_rows=2500, output=str(out),
+                                           partitions=7))
+        rj.waitForCompletion(120)
+        assert rj.isSuccessful(), rj.getFailureInfo()
+    parts = sorted(f for f in os.listdir(out) if f.startswith("part-"))
+    assert parts == [f"part-{i:05d}" for i in range(7)]
+    got = np.concatenate([np.fromfile(out / p, dtype=np.uint8).reshape(-1, 100) for p in parts])
+    assert np.array_equal(got, _ref_sorted(rows))
+
+
 def test_partition_ops_cpu():
     recs = torch.from_numpy(S.teragen_cpu(0, 5000))
     sp = T.create_partitions(recs.numpy()[::50, :10].copy(), 6)
