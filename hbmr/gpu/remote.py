@@ -260,6 +260,20 @@ class RemoteGpuRuntime:
         except OSError:
             pass
 
+    def drop_job(self, jid):
+        """The job is finished or killed (KillJobAction): the worker frees its
+        state (map outputs held on the device), and its attempts no longer count
+        as held outputs should the worker die later."""
+        with self._lock:
+            self.held.pop(jid, None)
+            sent = jid in self.jobs_sent
+            self.jobs_sent.discard(jid)
+        if sent:
+            try:
+                send_msg(self.sock, ("drop", jid), self._send_lock)
+            except OSError:
+                pass
+
     # -- receiving ---------------------------------------------------------------------
     def _read_loop(self, sock, proc):
         tr = self.tracker

@@ -372,7 +372,10 @@ class GpuRuntime:
         with dev.busy_lock:
             busy = max(0.0, end - max(start, dev.busy_frontier))
             dev.busy_frontier = max(dev.busy_frontier, end)
-        return busy
+        # completers of the slot streams may process batches out of device
+        # order, and a batch that overlaps an already-charged one would be
+        # charged ~0; it shares the device with at most len(slots) streams
+        return max(busy, elapsed / max(1, len(dev.slots)))
 
     # -- device health (NodeHealthChecker probes) --------------------------------------
     def _note_error(self, d, exc):

@@ -88,6 +88,11 @@ def run_split_reduce(host, run, device=None):
         crash = getattr(host, "_maybe_inject_crash", None)
         if crash is not None:
             crash(run)          # GPU worker crash injection (tests of crash isolation)
+        fail_on = js.conf.get("hbmr.faultinject.reduce.fail.attempt")
+        if fail_on and fail_on in spec.attempt_id:
+            # an ordinary task failure (not a crash): the attempt FAILS and the
+            # JobTracker re-runs the collective gang on the same worker
+            raise RuntimeError(f"injected reduce failure ({spec.attempt_id})")
         rep = TaskReporter()
         run.task = SplitTaskShim(rep, run.kill)
         ctx = TaskContext(host, js, spec, rep)

@@ -236,27 +236,38 @@ def serve(sock):
     status = [g.__dict__ for g in runtime.device_status()]
     send_msg(sock, ("ready", status, os.getpid()), host.send_lock)
 
-    def _job(jid):
-        return host.jobs[jid]
+    def _unknown_job(runs):
+        # the tracker sent attempts of a job this worker does not hold (it was
+        # dropped): fail them instead of taking the serve loop down with a KeyError
+        for r in runs:
+            host._finish(r, P.FAILED, f"job {r.spec.job_id} unknown to the GPU worker",
+                         wake=False)
+        host.notify_jobtracker()
+        return []
 
     def _run(d, kill=None):
         spec = P.TaskSpec.from_dict(d)
         st = P.TaskStatus(spec.attempt_id, spec.is_map, P.RUNNING, 0.0, spec.run_on_gpu,
                           spec.gpu_device_id, time.time())
-        r = _Running(spec, st, _job(spec.job_id), kill or _Flag())
+        r = _Running(spec, st, host.jobs.get(spec.job_id), kill or _Flag())
+        if r.job is None:
+            _unknown_job([r])
+            return None
         with host._lock:
             host.runs[spec.attempt_id] = r
         return r
 
     def _runs_compact(jid, common, tasks):
         is_map, on_gpu, dev_id, nm, nr, coll = common
-        js = _job(jid)
+        js = host.jobs.get(jid)
         now = time.time()
         out = []
         for aid, part, split in tasks:
             spec = P.TaskSpec(aid, jid, is_map, part, on_gpu, dev_id, split, nm, nr, [], coll)
             st = P.TaskStatus(aid, is_map, P.RUNNING, 0.0, on_gpu, dev_id, now)
             out.append(_Running(spec, st, js, _Flag()))
+        if js is None:
+            return _unknown_job(out)
         with host._lock:
             for r in out:
                 host.runs[r.spec.attempt_id] = r
@@ -272,7 +283,7 @@ def serve(sock):
         if typ == "maps_c":
             runtime.submit_many(_runs_compact(msg[1], msg[2], msg[3]))
         elif typ == "maps":
-            runtime.submit_many([_run(d) for d in msg[2]])
+            runtime.submit_many([r for r in (_run(d) for d in msg[2]) if r is not None])
         elif typ == "job":
             jid, conf_dict = msg[1], msg[2]
             if jid not in host.jobs:
@@ -284,12 +295,19 @@ def serve(sock):
                 if TRACE.on:
                     TRACE.instant("wk.job_ready")
         elif typ == "cpu":
-            cpu_pool.submit(run_split_cpu_map, host, _run(msg[1], threading.Event()))
+            r = _run(msg[1], threading.Event())
+            if r is not None:
+                cpu_pool.submit(run_split_cpu_map, host, r)
         elif typ == "reduce":
             def _reduce(r):
                 run_split_reduce(host, r, dev)
-                host.jobs.pop(r.spec.job_id, None)   # the job is done on this worker
-            red_pool.submit(_reduce, _run(msg[1], threading.Event()))
+                if r.status.state == P.SUCCEEDED:
+                    # the job is done on this worker; after a FAILED reduce the
+                    # JobTracker re-runs maps / the reduce of the same job here
+                    host.jobs.pop(r.spec.job_id, None)
+            r = _run(msg[1], threading.Event())
+            if r is not None:
+                red_pool.submit(_reduce, r)
         elif typ == "kill":
             with host._lock:
                 r = host.runs.get(msg[1])

@@ -682,6 +682,11 @@ class JobTracker:
                 return RunningJob(jid, _JTJobHandle(jip), conf)
             dep = conf.get(DEPENDS_KEY)
             dj = self.jobs.get(dep) if dep else None
+            if dep and dj is None:
+                # a typo, or a job this JobTracker never saw (retired, or finished
+                # before a restart): nothing to wait for, but say so
+                log.warning("job %s depends on unknown job %s: scheduling it now", jid, dep)
+                self.history.log("JOB_DEPENDENCY_UNKNOWN", job=str(jid), depends_on=dep)
             if dj is not None and not dj.completed():
                 # a dependent job (JobControl's ControlledJob): initialised now,
                 # scheduled the moment the job it depends on succeeds
@@ -780,6 +785,14 @@ class JobTracker:
             except Exception:  # noqa: BLE001
                 log.exception("writing job history failed")
         self._forget_job(jip.job_id)
+        # KillJobAction to every tracker that holds state of the job (the
+        # reference purges finished jobs from trackers the same way): its GPU
+        # worker frees the job's device map outputs
+        jid_s = str(jip.job_id)
+        for t in self.trackers.values():
+            if jid_s in t.jobs_seen:
+                t.jobs_seen.discard(jid_s)
+                t.extra_actions.append(P.kill_job_action(jid_s))
         jip.done.set()
         for w in self.waiting.pop(str(jip.job_id), []):
             if w.completed():

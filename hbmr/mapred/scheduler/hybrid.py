@@ -71,15 +71,27 @@ class HybridTaskScheduler(TaskScheduler):
 
     # -- cluster capacity ----------------------------------------------------------------
     def _totals(self):
-        cpu = gpu = 0
+        cpu = gpu = ndev = 0
         for t in self.jt.trackers.values():
             if t.blacklisted:
                 continue
             cpu += t.status.max_cpu_map_slots
             gpu += sum(g["max_slots"] for g in t.status.gpus)
+            ndev += len(t.status.gpus)
+        self._devices = ndev
         return cpu, gpu
 
+    def _gpu_servers(self, jip, total_gpu):
+        """G of the makespan model.  A split job's GPU task time is the device's
+        busy time per task (its slot streams overlap on one device: the time is
+        de-overlapped by the runtime), so G counts devices; a per-attempt GPU
+        Pipes task is timed on its slot, so G counts slots."""
+        if jip.split_job is not None:
+            return max(1, getattr(self, "_devices", 0)) if total_gpu else 0
+        return total_gpu
+
     def _cpu_allowed(self, jip, total_cpu, total_gpu, now):
+        total_gpu = self._gpu_servers(jip, total_gpu)
         if not jip.cpu_capable:
             return 0
         running_cpu = jip.running_maps(on_gpu=False)

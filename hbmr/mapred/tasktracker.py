@@ -163,6 +163,7 @@ class TaskTracker:
             conf.get("mapred.local.dir", "/tmp/hbmr-local"), self.name)
         os.makedirs(self.local_dir, exist_ok=True)
         self.jobs: dict[str, JobState] = {}
+        self._results: dict = {}             # results of purged (finished) jobs, newest last
         self.running: dict[str, _Running] = {}
         self._lock = threading.Lock()
         self._changed: set[str] = set()
@@ -479,9 +480,18 @@ class TaskTracker:
             if r is not None:
                 r.status.commit_granted = True  # picked up by the waiting task
         elif typ == "kill_job":
-            self.jobs.pop(act["job_id"], None)
+            # KillJobAction: the job is finished or killed; purge its state here
+            # and in the GPU worker (held device map outputs, worker JobState)
+            jid = act["job_id"]
+            js = self.jobs.pop(jid, None)
+            if js is not None and js.result is not None:
+                self._results[jid] = js.result
+                while len(self._results) > 64:
+                    self._results.pop(next(iter(self._results)))
+            if getattr(self.gpu_runtime, "remote", False):
+                self.gpu_runtime.drop_job(jid)
             if self.child_manager is not None:
-                self.child_manager.job_done(act["job_id"])
+                self.child_manager.job_done(jid)
         elif typ == "reinit":
             # the JobTracker does not know us (it restarted, or expired us):
             # drop every attempt and job, re-advertise the HBM-resident splits
@@ -687,7 +697,9 @@ class TaskTracker:
 
     def job_result(self, job_id):
         js = self.jobs.get(str(job_id))
-        return None if js is None else js.result
+        if js is None:
+            return self._results.get(str(job_id))
+        return js.result
 
 
 def _lower_priority(nice):

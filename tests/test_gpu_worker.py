@@ -73,6 +73,39 @@ def test_worker_crash_in_collective_reduce_reruns_the_gang(tmp_path):
     assert torch.equal(got, ref)
 
 
+def test_worker_reduce_that_raises_is_retried_by_the_same_worker(tmp_path):
+    """A collective reduce that FAILS (raises, no crash) in worker mode: the
+    worker keeps the job, the gang re-runs there (maps again, then the reduce)
+    and the worker never dies."""
+    ref, _ = _kmeans(_conf(), tmp=tmp_path / "ref")
+    conf = _conf()
+    conf.set("hbmr.faultinject.reduce.fail.attempt", "_0002_r_000000_0")
+    got, info = _kmeans(conf, tmp=tmp_path / "fail")
+    assert info["deaths"] == 0
+    assert "COLLECTIVE_RESTART" in info["events"]
+    assert torch.equal(got, ref)
+
+
+def test_finished_jobs_are_purged_from_trackers_and_workers(tmp_path):
+    """KillJobAction after a job finishes: the tracker and its GPU worker drop
+    the job (its device map outputs), so held state does not grow per job."""
+    import time
+    conf = _conf()
+    conf.set("mapred.local.dir", str(tmp_path))
+    with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=0) as cl:
+        drv = K.KMeansDriver(cl.submit_job, lambda rj: rj._impl.jip.result[0], conf=conf, k=4,
+                             d=8, inp="synthetic:4000:5", split_points=1000)
+        for _ in range(3):
+            drv.step()
+        tt = cl.trackers[0]
+        deadline = time.time() + 10
+        while time.time() < deadline and (tt.jobs or tt.gpu_runtime.held or
+                                           tt.gpu_runtime.jobs_sent):
+            time.sleep(0.05)
+        assert not tt.jobs and not tt.gpu_runtime.held and not tt.gpu_runtime.jobs_sent
+        assert tt.job_result(drv.history[-1]["job"]) is not None
+
+
 def _free_port():
     import socket
     s = socket.socket()

@@ -154,3 +154,23 @@ def test_costmodel_queued_gpu_age_and_sampled_probe_bound():
     cm.task_finished("s", "c0", False, 0.0, 0.1)
     cm.task_started("s", "c1", False, 200.0)
     assert cm.stats("s", False).estimate(201.0) == (1.0, True)
+
+
+def test_split_jobs_plan_gpu_capacity_in_devices_not_slots():
+    """A split job's GPU task time is the device's de-overlapped busy time per
+    task, so the makespan model's G is the number of devices; two slot streams
+    on one device must not double the GPU capacity (which starved CPU slots)."""
+    from types import SimpleNamespace as NS
+
+    from hbmr.mapred.scheduler.hybrid import HybridTaskScheduler
+    tr = NS(blacklisted=False, status=NS(max_cpu_map_slots=4,
+                                         gpus=[{"device": 0, "max_slots": 2}]))
+    jt = NS(trackers={"t0": tr})
+    s = HybridTaskScheduler(jt, JobConf())
+    cpu, gpu = s._totals()
+    assert (cpu, gpu) == (4, 2)
+    assert s._gpu_servers(NS(split_job=object()), gpu) == 1      # one device
+    assert s._gpu_servers(NS(split_job=None), gpu) == 2          # per-slot Pipes tasks
+    # 40 maps, CPU 10x slower: one device gives CPUs 10 maps, two "servers" only 4
+    assert min_makespan_cpu_tasks(40, 4, 1, 0.2, 0.02) == 10
+    assert min_makespan_cpu_tasks(40, 4, 2, 0.2, 0.02) < 10
