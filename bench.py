@@ -60,12 +60,13 @@ def main():
                     help="CPU rehearsal: simulated GPU slots with this device time per split")
     ap.add_argument("--in-process", action="store_true",
                     help="run the GPU slots inside the tracker process (no worker process)")
-    ap.add_argument("--prefetch", action=argparse.BooleanOptionalAction, default=True,
-                    help="submit each iteration job while its predecessor runs, held by the "
-                         "JobTracker until that one succeeds (hbmr.job.depends.on), as a "
-                         "JobControl driver would; --no-prefetch submits after it finished "
-                         "(same-box A/B, 1x MI355X: 32.4 vs 33.5 ms median, "
-                         "profiles/r02_prefetch_ab.json)")
+    ap.add_argument("--prefetch", type=int, default=2, metavar="N",
+                    help="keep N iteration jobs submitted ahead, each held by the JobTracker "
+                         "until its predecessor succeeds (hbmr.job.depends.on), as a "
+                         "JobControl driver would; 0 submits each after the previous finished")
+    ap.add_argument("--prestage", action=argparse.BooleanOptionalAction, default=True,
+                    help="let the JobTracker stage held iteration jobs: their GPU maps wait "
+                         "on the device behind the predecessor's reduce (hbmr.job.prestage)")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("-D", dest="defines", action="append", default=[], metavar="KEY=VALUE",
                     help="extra configuration (e.g. -D hbmr.gpu.first.chunk=8)")
@@ -99,6 +100,8 @@ def main():
     # only a tracker that is seconds late (not one still warming up) loses its
     # splits to another GPU's queue, which would skew every later iteration
     conf.set_int("hbmr.locality.wait.ms", 5000)
+    conf.set_boolean("hbmr.job.prestage", a.prestage)
+    conf.set_int("hbmr.job.prestage.depth", max(1, a.prefetch))
     # device_count() does not initialise HIP in this process: with the default
     # per-rank GPU worker process (hbmr.gpu.worker.process) the device work and
     # its synchronisation happen in the workers (the barrier job synchronises
@@ -134,9 +137,10 @@ def main():
 
     try:
         t_setup = time.time()
-        pre = a.prefetch
+        pre = max(0, a.prefetch)
         for w in range(a.warmup):
-            drv.step(prefetch=pre and w < a.warmup - 1)
+            # (no job submitted ahead crosses into the timed window)
+            drv.step(prefetch=min(pre, a.warmup - 1 - w))
         t_warm = time.time() - t_setup
         barrier()
         if in_process:
@@ -145,7 +149,7 @@ def main():
         # every timed job is submitted inside the timed window (the first by this
         # loop, each next one while its predecessor runs); none crosses a barrier
         for s in range(a.steps):
-            drv.step(prefetch=pre and s < a.steps - 1)
+            drv.step(prefetch=min(pre, a.steps - 1 - s))
         barrier()
         if in_process:
             torch.cuda.synchronize()
@@ -199,7 +203,8 @@ def main():
                        "map_tasks_per_job": splits, "policy": a.policy,
                        "cpu_slots_per_tracker": a.cpu_slots, "gpu_slots_per_gpu": a.gpu_slots,
                        "gpu_worker_process": not (in_process or a.in_process),
-                       "iteration_jobs_prefetched": a.prefetch},
+                       "iteration_jobs_ahead": a.prefetch, "prestage": a.prestage,
+                       "combiner": conf.get("hbmr.kmeans.combiner") or "delta"},
             "job_makespan_ms": round(ms, 3),
             "phases_ms": phases_ms,
             "points_per_sec": round(a.points * a.steps / dt, 1),

@@ -236,9 +236,10 @@ class RemoteGpuRuntime:
                 if kind == "maps":
                     s0 = rs[0].spec
                     common = (s0.is_map, s0.run_on_gpu, s0.gpu_device_id, s0.num_maps,
-                              s0.num_reduces, s0.collective)
+                              s0.num_reduces, s0.collective, s0.gate)
                     if all((r.spec.is_map, r.spec.run_on_gpu, r.spec.gpu_device_id,
-                            r.spec.num_maps, r.spec.num_reduces, r.spec.collective) == common
+                            r.spec.num_maps, r.spec.num_reduces, r.spec.collective,
+                            r.spec.gate) == common
                            and not r.spec.map_outputs and not r.spec.profile_fraction
                            for r in rs):
                         # a bulk launch: shared fields once, (attempt, partition, split) each

@@ -117,9 +117,22 @@ class GpuRuntime:
         reserve = tracker.conf.get_float("hbmr.gpu.hbm.reserve.gb", 16.0) * (1 << 30)
         for d, dev in self.devices.items():
             tracker.split_cache.capacity[d] = max(0, int(dev.total_mem - reserve))
+        from .gates import Gates
+        self.gates = Gates()
 
     def torch_device(self, d):
         return self.devices[d].torch_device
+
+    # -- staged maps (hbmr/gpu/gates.py) ---------------------------------------------------
+    def open_gate(self, job_id, event=None):
+        """Job ``job_id``'s reduce result is enqueued on the device (``event``):
+        its staged dependents' held maps go to the slots, behind the event."""
+        held = self.gates.open(job_id, event)
+        if held:
+            self.submit_many(held)
+
+    def drop_held(self, job_id):
+        return self.gates.drop(job_id)
 
     def device_status(self):
         out = []
@@ -155,7 +168,9 @@ class GpuRuntime:
 
     def submit_many(self, runs):
         """Queue attempts; a job's bulk launch arrives as one list, so the
-        launcher plans the whole batch at once (first_chunk)."""
+        launcher plans the whole batch at once (first_chunk).  Staged attempts
+        of an unopened gate are held (open_gate)."""
+        runs = self.gates.admit(runs)
         by_dev: dict = {}
         for run in runs:
             d = run.spec.gpu_device_id
@@ -283,6 +298,11 @@ class GpuRuntime:
                     live.append(r)
                 if not live:
                     return
+                # staged attempts: the job they depend on enqueued its reduce
+                # result; the kernels wait for it on the device, not the host
+                waits = {id(r.wait): r.wait for r in live if r.wait is not None}
+                for w in waits.values():
+                    slot.stream.wait_event(w)
                 ev0 = torch.cuda.Event(enable_timing=True)
                 ev1 = torch.cuda.Event(enable_timing=True)
                 if TRACE.on:
@@ -296,6 +316,13 @@ class GpuRuntime:
             slot.inflight += len(live)
             if TRACE.on:
                 TRACE.instant("gpu.launch", n=len(live), slot=slot.index)
+            # an early collective reduce may consume the outputs now, ordered
+            # behind ev1 on its own stream
+            by_job: dict = {}
+            for r, out in zip(live, outs):
+                by_job.setdefault(id(r.job), (r.job, []))[1].append((r.spec.attempt_id, out, ev1))
+            for js, items in by_job.values():
+                js.note_launched(items)
             slot.done_q.put((live, ev0, ev1, outs))
         except BaseException as e:  # noqa: BLE001
             self._note_error(dev.index, e)

@@ -77,9 +77,21 @@ class SimulatedGpuRuntime:
         reserve = conf.get_float("hbmr.gpu.hbm.reserve.gb", 16.0) * (1 << 30)
         for d, dev in self.devices.items():
             tracker.split_cache.capacity[d] = max(0, int(dev.total_mem - reserve))
+        from .gates import Gates
+        self.gates = Gates()
 
     def torch_device(self, d):
         return torch.device("cpu")
+
+    def open_gate(self, job_id, event=None):
+        """Staged maps held for ``job_id`` go to the device queue; a simulated
+        device runs them after its earlier work (busy_until), as a stream would."""
+        held = self.gates.open(job_id, event)
+        if held:
+            self.submit_many(held)
+
+    def drop_held(self, job_id):
+        return self.gates.drop(job_id)
 
     def device_status(self):
         return [P.GpuDeviceStatus(device=d, max_slots=len(dev.slots),
@@ -116,6 +128,7 @@ class SimulatedGpuRuntime:
         self.submit_many([run])
 
     def submit_many(self, runs):
+        runs = self.gates.admit(runs)
         by_dev: dict = {}
         for run in runs:
             d = run.spec.gpu_device_id
@@ -192,6 +205,13 @@ class SimulatedGpuRuntime:
             start = max(time.time(), dev.busy_until)
             slot.busy_until = dev.busy_until = start + self.task_s * len(live)
             slot.inflight += len(live)
+            # outputs for an early collective reduce, "ready" at the simulated end
+            by_job: dict = {}
+            for r, out in zip(live, outs):
+                by_job.setdefault(id(r.job), (r.job, []))[1].append(
+                    (r.spec.attempt_id, out, slot.busy_until))
+            for js, items in by_job.values():
+                js.note_launched(items)
             if TRACE.on:
                 TRACE.instant("gpu.launch", n=len(live))
             with self._done_cv:

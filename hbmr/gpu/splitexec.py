@@ -75,15 +75,64 @@ def run_split_cpu_map(host, run):
         host._finish(run, state, f"{type(e).__name__}: {e}\n{traceback.format_exc()[-2000:]}")
 
 
+def _gather_outputs(js, spec, run):
+    """The map outputs this collective reduce combines, and their readiness
+    markers.  A reduce launched early (``spec.expect``) waits until every
+    expected attempt's kernels are ENQUEUED (JobState.note_launched): each
+    output comes with its batch's end event (device) or simulated ready time,
+    so the reduce orders itself behind the maps on the device instead of
+    waiting on the host for them to finish."""
+    want = [a for _tid, a, _o in spec.map_outputs]
+    if not spec.expect:
+        with js.lock:
+            outs = [js.map_outputs[a] for a in want if a in js.map_outputs]
+            missing = [a for a in want if a not in js.map_outputs]
+        if missing:
+            raise RuntimeError(f"map outputs lost: {missing[:4]}")
+        return outs, []
+    with js.cond:
+        while True:
+            if run.kill.is_set():
+                raise RuntimeError("killed while waiting for its expected map outputs")
+            bad = [a for a in want if a in js.failed]
+            if bad:
+                raise RuntimeError(f"expected map attempts failed: {bad[:4]}")
+            if all(a in js.map_outputs or a in js.launched for a in want):
+                break
+            js.cond.wait(0.5)
+        outs, marks = [], []
+        for a in want:
+            if a in js.map_outputs:
+                outs.append(js.map_outputs[a])
+            else:
+                o, m = js.launched[a]
+                outs.append(o)
+                if m is not None:
+                    marks.append(m)
+    return outs, marks
+
+
+def _reduce_stream(host, device):
+    import torch
+    st = host.__dict__.get("_reduce_stream")
+    if st is None:
+        st = host.__dict__.setdefault("_reduce_stream", torch.cuda.Stream(device=device))
+    return st
+
+
 def run_split_reduce(host, run, device=None):
     """The collective reduce of a split job on this tracker: combine the
     committed map outputs held here, then ``reduce`` (collectives over
-    ``host.comm``).  ``device``: the tracker's GPU (combine + reduce on it)."""
+    ``host.comm``).  ``device``: the tracker's GPU (combine + reduce on it, on
+    a reduce stream of its own).  As soon as the reduce has *enqueued* its
+    result (the split job calls ``ctx.release_dependents()``, else when
+    ``reduce`` returns) the maps of jobs staged behind this one are released
+    on this tracker's GPU runtime, behind a device event (hbmr/gpu/gates.py)."""
     from ..mapred.tasktracker import TaskContext
     spec, js = run.spec, run.job
     run.status.start_time = time.time()
     if TRACE.on:
-        TRACE.instant("tt.reduce.start", attempt=spec.attempt_id)
+        TRACE.instant("tt.reduce.start", attempt=spec.attempt_id, expect=spec.expect)
     try:
         crash = getattr(host, "_maybe_inject_crash", None)
         if crash is not None:
@@ -98,29 +147,58 @@ def run_split_reduce(host, run, device=None):
         ctx = TaskContext(host, js, spec, rep)
         comm = getattr(host, "comm", None)
         before = dict(getattr(comm, "stats", None) or {})
-        with js.lock:
-            outs = [js.map_outputs[a] for _tid, a, _o in spec.map_outputs if a in js.map_outputs]
-        missing = [a for _tid, a, _o in spec.map_outputs if a not in js.map_outputs]
-        if missing:
-            raise RuntimeError(f"map outputs lost on {host.name}: {missing[:4]}")
-        if device is not None and device.type == "cuda":
+        try:
+            outs, marks = _gather_outputs(js, spec, run)
+        except RuntimeError as e:
+            raise RuntimeError(f"{e} on {host.name}") from None
+        cuda = device is not None and device.type == "cuda"
+        rt = getattr(host, "gpu_runtime", None)
+        released = [False]
+
+        def release_dependents():
+            if released[0]:
+                return
+            released[0] = True
+            if rt is None or not hasattr(rt, "open_gate"):
+                return
+            ev = None
+            if cuda:
+                import torch
+                ev = torch.cuda.Event()
+                ev.record()
+            rt.open_gate(spec.job_id, ev)
+            if TRACE.on:
+                TRACE.instant("tt.reduce.gate_open", job=spec.job_id)
+        ctx.release_dependents = release_dependents
+        if cuda:
             import torch
             ctx.device = device
-            with torch.cuda.device(device):
+            with torch.cuda.device(device), torch.cuda.stream(_reduce_stream(host, device)):
+                cur = torch.cuda.current_stream()
+                for ev in {id(m): m for m in marks}.values():
+                    cur.wait_event(ev)
                 combined = js.split_job.combine(ctx, outs)
                 if TRACE.on:
                     TRACE.instant("tt.reduce.combined", attempt=spec.attempt_id)
                 js.result = js.split_job.reduce(ctx, combined)
+                release_dependents()
         else:
+            if marks:
+                # simulated device: the outputs are "ready" at these times
+                delay = max(marks) - time.time()
+                if delay > 0:
+                    time.sleep(delay)
             ctx.device = None
             combined = js.split_job.combine(ctx, outs)
             if TRACE.on:
                 TRACE.instant("tt.reduce.combined", attempt=spec.attempt_id)
             js.result = js.split_job.reduce(ctx, combined)
+            release_dependents()
         if TRACE.on:
             TRACE.instant("tt.reduce.done", attempt=spec.attempt_id)
         with js.lock:
             js.map_outputs.clear()       # consumed
+            js.launched.clear()
         from ..parallel.collectives import COLLECTIVE_GROUP
         for k, v in (getattr(comm, "stats", None) or {}).items():
             if v != before.get(k, 0):

@@ -131,6 +131,8 @@ class WorkerHost:
 
     def _finish(self, run, state, diag="", output=None, device_time=0.0, wake=True):
         from ..mapred import protocol as P
+        if state != P.SUCCEEDED and run.spec.is_map and run.job is not None:
+            run.job.note_failed(run.spec.attempt_id)
         st = run.status
         st.state = state
         st.finish_time = time.time()
@@ -228,11 +230,11 @@ def serve(sock):
         from ..ops import _lib
         _lib.load()      # fail loudly now, not in the first task
     runtime = Rt(host, devices, init["slots"])
+    host.gpu_runtime = runtime      # the reduce opens gates of staged maps on it
     runtime.start()
     dev = None if simulate else runtime.torch_device(devices[0])
     cpu_pool = cf.ThreadPoolExecutor(max(1, init.get("cpu_slots", 1)),
                                      thread_name_prefix="worker-cpu")
-    red_pool = cf.ThreadPoolExecutor(2, thread_name_prefix="worker-red")
     status = [g.__dict__ for g in runtime.device_status()]
     send_msg(sock, ("ready", status, os.getpid()), host.send_lock)
 
@@ -258,12 +260,13 @@ def serve(sock):
         return r
 
     def _runs_compact(jid, common, tasks):
-        is_map, on_gpu, dev_id, nm, nr, coll = common
+        is_map, on_gpu, dev_id, nm, nr, coll, gate = common
         js = host.jobs.get(jid)
         now = time.time()
         out = []
         for aid, part, split in tasks:
-            spec = P.TaskSpec(aid, jid, is_map, part, on_gpu, dev_id, split, nm, nr, [], coll)
+            spec = P.TaskSpec(aid, jid, is_map, part, on_gpu, dev_id, split, nm, nr, [], coll,
+                              gate=gate)
             st = P.TaskStatus(aid, is_map, P.RUNNING, 0.0, on_gpu, dev_id, now)
             out.append(_Running(spec, st, js, _Flag()))
         if js is None:
@@ -307,7 +310,10 @@ def serve(sock):
                     host.jobs.pop(r.spec.job_id, None)
             r = _run(msg[1], threading.Event())
             if r is not None:
-                red_pool.submit(_reduce, r)
+                # own thread: an early ("expect") reduce waits for maps held
+                # behind an earlier job's reduce, which a bounded pool could starve
+                threading.Thread(target=_reduce, args=(r,), daemon=True,
+                                 name=f"worker-red-{r.spec.attempt_id[-12:]}").start()
         elif typ == "kill":
             with host._lock:
                 r = host.runs.get(msg[1])
@@ -317,6 +323,8 @@ def serve(sock):
                     r.task.kill_event.set()
         elif typ == "drop":
             host.jobs.pop(msg[1], None)
+            for r in runtime.drop_held(msg[1]) if hasattr(runtime, "drop_held") else ():
+                host._finish(r, P.KILLED, "job purged", wake=False)
         elif typ == "probe":
             reason = runtime.probe(msg[1]) if hasattr(runtime, "probe") else None
             send_msg(sock, ("probe", msg[1], reason), host.send_lock)

@@ -88,7 +88,8 @@ class TrackerInfo:
 class Attempt:
     __slots__ = ("aid", "tip", "tracker", "run_on_gpu", "device", "state", "progress",
                  "start", "finish", "counters", "output", "diagnostic", "speculative",
-                 "device_time", "_released", "profile_only", "profile_fraction", "slots")
+                 "device_time", "_released", "profile_only", "profile_fraction", "slots",
+                 "gated")
 
     def __init__(self, aid, tip, tracker, run_on_gpu, device, speculative=False):
         self.aid = aid
@@ -109,6 +110,7 @@ class Attempt:
         self.slots = 1              # CPU / reduce slots held (memory matching)
         self.profile_only = False   # a CPU profiling probe left running after its TIP won
         self.profile_fraction = 0.0  # >0: sampled probe, timed on this fraction of a split
+        self.gated = False          # launched staged, behind another job's reduce
 
 
 class TaskInProgress:
@@ -213,6 +215,14 @@ class JobInProgress:
         self.reduce_in_child = use_child_process(conf)
         self.slowstart = conf.get_float("mapred.reduce.slowstart.completed.maps", 0.05)
         self.slowstart_maps = 0
+        # pre-staging (hbmr/gpu/gates.py): the job this one's GPU maps are
+        # gated on while it waits for it, its staged launches per (tracker,
+        # device), a finish deferred until that job succeeded, and whether its
+        # collective reduce was launched before its maps finished ("expect")
+        self.staged_on: str | None = None
+        self.staged_launched: dict = {}
+        self.pending_finish = False
+        self.expect_mode = False
 
     @staticmethod
     def _signature(conf):
@@ -457,6 +467,11 @@ class JobTracker:
         self.job_tokens = JobTokenSecretManager()
         self.job_queue: list[JobInProgress] = []
         self.waiting: dict[str, list] = {}   # job id -> dependent jobs held for it
+        # dependent jobs whose GPU maps may already be launched, gated on the
+        # job they wait for (hbmr/gpu/gates.py); chains up to prestage.depth
+        self.staged: list[JobInProgress] = []
+        self.prestage = conf.get_boolean("hbmr.job.prestage", True)
+        self.prestage_depth = max(1, conf.get_int("hbmr.job.prestage.depth", 2))
         self.trackers: dict[str, TrackerInfo] = {}
         self.attempt_index: dict[str, Attempt] = {}
         self.cost_model = CostModel(conf.get_float("hbmr.costmodel.ewma.alpha", 0.3))
@@ -689,9 +704,11 @@ class JobTracker:
                 self.history.log("JOB_DEPENDENCY_UNKNOWN", job=str(jid), depends_on=dep)
             if dj is not None and not dj.completed():
                 # a dependent job (JobControl's ControlledJob): initialised now,
-                # scheduled the moment the job it depends on succeeds
+                # scheduled the moment the job it depends on succeeds — and,
+                # when both are collective split jobs, staged at once
                 jip.status.state = PREP
                 self.waiting.setdefault(dep, []).append(jip)
+                self._maybe_stage(jip, dj)
                 return RunningJob(jid, _JTJobHandle(jip), conf)
             if dj is not None and dj.status.state != SUCCEEDED:
                 self._finish_job(jip, FAILED, f"job {dep} it depends on {dj.status.state}")
@@ -703,6 +720,33 @@ class JobTracker:
         for cb in self.listeners:
             cb("submitted", jip)
         return RunningJob(jid, _JTJobHandle(jip), conf)
+
+    def _stage_depth(self, jip) -> int:
+        d = 0
+        while jip is not None and jip.staged_on is not None:
+            d += 1
+            jip = self.jobs.get(jip.staged_on)
+        return d
+
+    def _maybe_stage(self, w: JobInProgress, j: JobInProgress):
+        """Stage dependent job ``w`` on ``j`` (running, or staged itself): its
+        GPU map attempts may be launched now, each gated on j's collective
+        reduce on its tracker (the device runs w's maps right after j's reduce
+        result, with no JobTracker round trip in between); w still completes
+        only after j succeeded.  Both must be collective split jobs."""
+        if not self.prestage or w.staged_on is not None or w.completed() or j.completed():
+            return
+        if w.split_job is None or not w.collective_reduce or not w.gpu_capable or \
+                j.split_job is None or not j.collective_reduce:
+            return
+        if j.status.state != RUNNING and j.staged_on is None:
+            return          # j itself still waits, unstaged
+        if self._stage_depth(j) + 1 > self.prestage_depth:
+            return
+        w.staged_on = str(j.job_id)
+        self.staged.append(w)
+        self.history.log("JOB_STAGED", job=str(w.job_id), gate=str(j.job_id))
+        self._kick()
 
     def _memory_violation(self, conf):
         """JobTracker.checkMemoryRequirements: a job asking for more memory per
@@ -754,6 +798,9 @@ class JobTracker:
             tip.killed = state != SUCCEEDED
         if jip in self.job_queue:
             self.job_queue.remove(jip)
+        if jip in self.staged:
+            self.staged.remove(jip)
+        jip.staged_on = None
         jip.fold_counters()
         jip.counters.incr(C.JOB_GROUP, C.CPU_MAP_TASKS, jip.finished_cpu_maps)
         jip.counters.incr(C.JOB_GROUP, C.GPU_MAP_TASKS, jip.finished_gpu_maps)
@@ -798,9 +845,19 @@ class JobTracker:
             if w.completed():
                 continue             # killed while it waited
             if state == SUCCEEDED:
+                if w in self.staged:
+                    self.staged.remove(w)
+                w.staged_on = None
                 w.status.state = RUNNING
                 w.launch_time = w.release_time = time.time()
+                if w.pending_finish:
+                    # every task of the staged job finished before this one did
+                    self._finish_job(w, SUCCEEDED)
+                    continue
                 self.job_queue.append(w)
+                # jobs waiting for w may now be staged on it
+                for x in self.waiting.get(str(w.job_id), []):
+                    self._maybe_stage(x, w)
             else:
                 self._finish_job(w, FAILED, f"job {jip.job_id} it depends on {state}")
         if state == SUCCEEDED:
@@ -972,6 +1029,9 @@ class JobTracker:
     def _release(self, a: Attempt):
         if a.tip.is_map and not a._released:
             jip = a.tip.job
+            if a.gated:
+                key = (a.tracker, a.device)
+                jip.staged_launched[key] = max(0, jip.staged_launched.get(key, 1) - 1)
             if a.run_on_gpu:
                 jip.running_gpu = max(0, jip.running_gpu - 1)
             else:
@@ -1097,6 +1157,9 @@ class JobTracker:
                 jp = tip.job
                 if not a._released:
                     a._released = True
+                    if a.gated:
+                        key = (a.tracker, a.device)
+                        jp.staged_launched[key] = max(0, jp.staged_launched.get(key, 1) - 1)
                     jp.running_gpu = max(0, jp.running_gpu - 1)
                     tr.running.discard(a.aid)
                     tr.running_gpu[a.device] = max(0, tr.running_gpu.get(a.device, 1) - 1)
@@ -1148,6 +1211,8 @@ class JobTracker:
         forget finished ones and re-execute the maps (their outputs were consumed
         by finished members or died with a worker)."""
         self.history.log("COLLECTIVE_RESTART", job=str(jip.job_id), diag=diag[:500])
+        jip.expect_mode = False
+        jip.pending_finish = False
         for r in jip.reduces:
             for a in r.running_attempts():
                 a.state = P.KILLED
@@ -1215,6 +1280,8 @@ class JobTracker:
                 jip.finished_cpu_maps -= 1
             jip.add_pending(tip, front=True)
             self.history.log("MAP_OUTPUT_LOST", attempt=aid, tracker=tr.name)
+            if jip.expect_mode:
+                self._restart_collective(jip, "map output lost")
         self._kick()
 
     def _attempt_failed(self, a: Attempt, diag, killed=False):
@@ -1257,6 +1324,9 @@ class JobTracker:
         if not tip.running_attempts():
             if tip.is_map:
                 jip.add_pending(tip, front=True)  # failed tasks first (findNewMapTask)
+                if jip.expect_mode:
+                    # the gang was launched expecting this attempt's output
+                    self._restart_collective(jip, diag)
             elif jip.collective_reduce:
                 # a collective gang cannot restart one member: the whole gang re-runs
                 self._restart_collective(jip, diag)
@@ -1273,6 +1343,11 @@ class JobTracker:
         if jip.maps_done < len(jip.maps) or jip.reduces_done < len(jip.reduces):
             return
         if all(t.is_complete() for t in jip.maps) and all(t.is_complete() for t in jip.reduces):
+            if jip.staged_on is not None:
+                # a staged job ran ahead of the job it depends on: it succeeds
+                # when that one does (or fails with it)
+                jip.pending_finish = True
+                return
             self._finish_job(jip, SUCCEEDED)
 
     # -- launching (called by the scheduler under the lock) -------------------------------
@@ -1327,7 +1402,7 @@ class JobTracker:
                     type="map" if tip.is_map else "reduce", where="gpu" if on_gpu else "cpu")
         return P.launch_action(spec)
 
-    def launch_gpu_batch(self, tr: TrackerInfo, tips, device):
+    def launch_gpu_batch(self, tr: TrackerInfo, tips, device, gate=None):
         """One bulk LaunchTaskAction for GPU map attempts of one job on one device
         (the per-task launch() costs ~50 µs of JobTracker time; this ~3 µs).
         The tracker queues them on the device's slots as one batch."""
@@ -1342,6 +1417,7 @@ class JobTracker:
             tip.next_attempt += 1
             a = Attempt(aid, tip, tr.name, True, device)
             a.start = now
+            a.gated = gate is not None
             tip.attempts[aid] = a
             index[aid] = a
             running.add(aid)
@@ -1361,17 +1437,29 @@ class JobTracker:
         act = {"type": "launch_batch", "job_id": str(jip.job_id), "run_on_gpu": True,
                "device": device, "num_maps": len(jip.maps), "num_reduces": len(jip.reduces),
                "collective": jip.collective_reduce, "tasks": tasks}
+        if gate is not None:
+            act["gate"] = gate
+            key = (tr.name, device)
+            jip.staged_launched[key] = jip.staged_launched.get(key, 0) + n
         if str(jip.job_id) not in tr.jobs_seen:
             act["conf"] = jip.conf_dict
             tr.jobs_seen.add(str(jip.job_id))
         return act
 
-    def reduce_inputs(self, jip: JobInProgress, tracker_name=None):
+    def reduce_inputs(self, jip: JobInProgress, tracker_name=None, expect=False):
         """Map outputs a reduce needs: classic = every map's output location;
-        collective = the committed map attempts that ran on ``tracker_name``."""
+        collective = the committed map attempts that ran on ``tracker_name``
+        (``expect``: plus the single running attempt of every unfinished map)."""
         if jip.collective_reduce:
-            return [[str(t.tid), t.successful.aid, t.successful.output] for t in jip.maps
-                    if t.successful is not None and t.successful.tracker == tracker_name]
+            out = []
+            for t in jip.maps:
+                a = t.successful
+                if a is None and expect:
+                    ra = t.running_attempts()
+                    a = ra[0] if len(ra) == 1 else None
+                if a is not None and a.tracker == tracker_name:
+                    out.append([str(t.tid), a.aid, a.output or {}])
+            return out
         return [[str(t.tid), t.successful.aid, t.successful.output] for t in jip.maps
                 if t.successful is not None]
 

@@ -17,7 +17,7 @@ from __future__ import annotations
 
 from dataclasses import dataclass, field
 
-PROTOCOL_VERSION = 4
+PROTOCOL_VERSION = 5
 
 # task states (TaskStatus.State)
 UNASSIGNED = "UNASSIGNED"
@@ -129,6 +129,12 @@ class TaskSpec:
     collective: bool = False
     conf: dict | None = None                      # job conf (sent once per tracker per job)
     profile_fraction: float = 0.0                 # >0: sampled CPU profiling probe
+    # map attempt of a staged job: held on the tracker until job ``gate``'s
+    # collective reduce there has enqueued its result (JobTracker pre-staging)
+    gate: str | None = None
+    # collective reduce launched before its maps finished: ``map_outputs`` lists
+    # the expected attempts, some still running; it waits for them to launch
+    expect: bool = False
 
     def to_dict(self):
         return dict(self.__dict__)   # shallow: fields are plain values / dicts
@@ -145,7 +151,7 @@ def launch_action(spec: TaskSpec):
 
 # {"type": "launch_batch", "job_id", "run_on_gpu", "device", "num_maps",
 #  "num_reduces", "collective", "tasks": [[attempt_id, partition, split], ...],
-#  "conf"?} — built by JobTracker.launch_gpu_batch
+#  "conf"?, "gate"?} — built by JobTracker.launch_gpu_batch
 
 
 def kill_task_action(attempt_id: str):

@@ -147,25 +147,11 @@ class HybridTaskScheduler(TaskScheduler):
                 continue
             # ---- reduces
             if jip.reduces and self._reduces_may_start(jip):
-                n_red = 0
-                for tip in jip.reduces:
-                    if tip.is_complete() or tip.is_running():
-                        continue
-                    if jip.collective_reduce:
-                        if tip.pinned_tracker != tr.name:
-                            continue
-                    elif reduce_free < self.slots_per_task(jip, "reduce") or \
-                            n_red >= self.max_reduces_per_hb or \
-                            n_red >= self.job_limit(jip, "reduce"):
-                        break
-                    extra = {"map_outputs": jt.reduce_inputs(jip, tr.name)}
-                    spt = 1 if jip.collective_reduce else self.slots_per_task(jip, "reduce")
-                    actions.append(jt.launch(tr, tip, extra=extra, slots=spt))
-                    n_red += 1
-                    reduce_free -= spt
+                reduce_free = self._assign_reduces(tr, jip, reduce_free, actions)
             if not jip.pending_maps:
                 # ---- speculative backups of stragglers onto idle GPUs
-                if jip.speculative and jip.gpu_capable and not jip.maps_complete():
+                if jip.speculative and jip.gpu_capable and not jip.maps_complete() and \
+                        not jip.expect_mode:
                     self._speculate(tr, jip, gpu_free, now, actions)
                 continue
             # ---- CPU maps (first, as the fork's loop order, JobQueueTaskScheduler.java
@@ -238,9 +224,59 @@ class HybridTaskScheduler(TaskScheduler):
                         self.decisions += 1
                     if batch:
                         actions.append(jt.launch_gpu_batch(tr, batch, dev))
-            if jip.speculative and jip.gpu_capable and not jip.pending_maps:
+            if jip.speculative and jip.gpu_capable and not jip.pending_maps and \
+                    not jip.expect_mode:
                 self._speculate(tr, jip, gpu_free, now, actions)
+        # ---- staged jobs (JobTracker._maybe_stage): GPU maps gated on the job
+        # they wait for, and their collective reduce once every map is launched
+        for jip in list(jt.staged):
+            if jip.completed() or jip.staged_on is None:
+                continue
+            if jip.reduces and self._reduces_may_start(jip):
+                reduce_free = self._assign_reduces(tr, jip, reduce_free, actions)
+            if jip.pending_maps and jip.gpu_capable:
+                self._stage_maps(tr, jip, depth, actions)
         return actions
+
+    def _assign_reduces(self, tr, jip, reduce_free, actions):
+        jt = self.jt
+        n_red = 0
+        expect = jip.expect_mode and not jip.maps_complete()
+        for tip in jip.reduces:
+            if tip.is_complete() or tip.is_running():
+                continue
+            if jip.collective_reduce:
+                if tip.pinned_tracker != tr.name:
+                    continue
+            elif reduce_free < self.slots_per_task(jip, "reduce") or \
+                    n_red >= self.max_reduces_per_hb or \
+                    n_red >= self.job_limit(jip, "reduce"):
+                break
+            extra = {"map_outputs": jt.reduce_inputs(jip, tr.name, expect=expect)}
+            if expect:
+                extra["expect"] = True
+            spt = 1 if jip.collective_reduce else self.slots_per_task(jip, "reduce")
+            actions.append(jt.launch(tr, tip, extra=extra, slots=spt))
+            n_red += 1
+            reduce_free -= spt
+        return reduce_free
+
+    def _stage_maps(self, tr, jip, depth, actions):
+        """Launch a staged job's pending maps that are local to this tracker's
+        GPUs (HBM-resident / node-local splits), gated on the job it waits for;
+        up to one queue depth per device."""
+        for g in tr.status.gpus:
+            dev = g["device"]
+            cap = g["max_slots"] * depth - jip.staged_launched.get((tr.name, dev), 0)
+            batch = []
+            while cap > 0 and jip.pending_maps:
+                got = jip.obtain_map(tr, True, dev, allow_nonlocal=False)
+                if got is None:
+                    break
+                batch.append(got[0])
+                cap -= 1
+            if batch:
+                actions.append(self.jt.launch_gpu_batch(tr, batch, dev, gate=jip.staged_on))
 
     def _reduces_may_start(self, jip) -> bool:
         """Reduce slow-start (JobInProgress.java:879-881): classic reduces launch
@@ -250,9 +286,28 @@ class HybridTaskScheduler(TaskScheduler):
         at launch)."""
         if jip.maps_complete():
             return True
+        if jip.collective_reduce and jip.split_job is not None and self.jt.prestage and \
+                self._expect_ready(jip):
+            # every map is launched, once, on a GPU: the gang can start now and
+            # take each output as its kernels are enqueued ("expect" mode)
+            jip.expect_mode = True
+            return True
         if jip.collective_reduce or jip.split_job is not None or jip.reduce_in_child:
             return False
         return jip.maps_done >= jip.slowstart_maps
+
+    @staticmethod
+    def _expect_ready(jip) -> bool:
+        if jip.expect_mode:
+            return True
+        if jip.pending_maps or jip.running_cpu:
+            return False
+        for t in jip.maps:
+            if t.successful is None:
+                ra = t.running_attempts()
+                if len(ra) != 1 or not ra[0].run_on_gpu:
+                    return False
+        return True
 
     def _speculate(self, tr, jip, gpu_free, now, actions):
         """Back up stragglers on fully idle GPUs (JobInProgress.java:2312's

@@ -58,6 +58,24 @@ class JobState:
         self.lock = threading.Lock()
         self.result = None
         self.scratch: dict = {}
+        # device map outputs as soon as their kernels are ENQUEUED (attempt ->
+        # (output, end event / simulated ready time)) and map attempts that
+        # failed here: what an early ("expect") collective reduce waits on
+        self.launched: dict[str, tuple] = {}
+        self.failed: set[str] = set()
+        self.cond = threading.Condition(self.lock)
+
+    def note_launched(self, items):
+        """items: (attempt id, output, end marker) of maps just enqueued."""
+        with self.cond:
+            for aid, out, ev in items:
+                self.launched[aid] = (out, ev)
+            self.cond.notify_all()
+
+    def note_failed(self, aid):
+        with self.cond:
+            self.failed.add(aid)
+            self.cond.notify_all()
 
 
 class TaskContext:
@@ -105,7 +123,7 @@ class _Flag:
 
 
 class _Running:
-    __slots__ = ("spec", "status", "task", "kill", "job")
+    __slots__ = ("spec", "status", "task", "kill", "job", "wait")
 
     def __init__(self, spec, status, job, kill=None):
         self.spec = spec
@@ -113,6 +131,7 @@ class _Running:
         self.task = None
         self.kill = threading.Event() if kill is None else kill
         self.job = job
+        self.wait = None        # device event of an opened gate (staged attempts)
 
 
 class TaskTracker:
@@ -305,6 +324,9 @@ class TaskTracker:
         return out
 
     def _finish(self, run: _Running, state, diag="", output=None, device_time=0.0, wake=True):
+        if state != P.SUCCEEDED and run.spec is not None and run.spec.is_map and \
+                run.job is not None:
+            run.job.note_failed(run.spec.attempt_id)
         if state == P.FAILED:
             dbg = self._run_debug_script(run, diag)
             if dbg:
@@ -551,6 +573,12 @@ class TaskTracker:
                 self.gpu_runtime.submit_reduce(run)
         elif spec.is_map:
             self.cpu_pool.submit(self._run_cpu_map, run)
+        elif spec.collective and js.split_job is not None:
+            # a collective reduce gets a thread of its own: it may wait for maps
+            # held behind an earlier job's reduce (pre-staging), which a bounded
+            # pool could starve; one per job and tracker (pinned gang member)
+            threading.Thread(target=self._run_reduce, args=(run,), daemon=True,
+                             name=f"{self.name}-coll-{spec.attempt_id[-12:]}").start()
         else:
             self.reduce_pool.submit(self._run_reduce, run)
 
@@ -575,8 +603,10 @@ class TaskTracker:
             if lo >= hi:
                 continue
             runs = []
+            gate = act.get("gate")
             for aid, part, split in tasks[lo:hi]:
-                spec = P.TaskSpec(aid, jid, True, part, True, dev, split, nm, nr, (), coll)
+                spec = P.TaskSpec(aid, jid, True, part, True, dev, split, nm, nr, (), coll,
+                                  gate=gate)
                 st = P.TaskStatus(aid, True, P.RUNNING, 0.0, True, dev, now)
                 runs.append(_Running(spec, st, js, _Flag()))
             with self._lock:

@@ -56,6 +56,10 @@ CDIR_KEY = "hbmr.kmeans.centroids.dir"
 # exact mode: bf16 MFMA assign certified against the fp32 data (top-3 + fp64
 # re-score of uncertain points) and fp32 fixed-point sums (ops.kmeans.ExactSplit)
 EXACT_KEY = "hbmr.kmeans.exact"
+# GPU combiner: "delta" (default) sums only the points whose label changed
+# against the split's reference partition (ops.kmeans.Baseline) — bit-identical
+# to "sorted", the counting-sort combiner over every point
+COMBINER_KEY = "hbmr.kmeans.combiner"
 
 # --------------------------------------------------------------------------- data
 _M32 = 0xFFFFFFFF
@@ -180,42 +184,28 @@ def _centroid_file(cdir, key):
     return os.path.join(cdir, key.replace("/", "_").replace(":", "_") + ".npy")
 
 
-def _save_centroids_async(cdir, key, prev, cen):
-    """Write centroid version ``key`` (and drop the one before ``prev``) off the
-    critical path: the device->host copy is queued on the current stream and the
-    file is written by a helper thread once it lands."""
-    host = torch.empty(cen.shape, dtype=torch.float32, pin_memory=cen.is_cuda)
-    host.copy_(cen, non_blocking=cen.is_cuda)
-    ev = None
-    if cen.is_cuda:
-        ev = torch.cuda.Event()
-        ev.record()
-
-    def _write():
-        if ev is not None:
-            ev.synchronize()
-        os.makedirs(cdir, exist_ok=True)
-        path = _centroid_file(cdir, key)
-        tmp = path + ".tmp.npy"
-        np.save(tmp, host.numpy())
-        os.replace(tmp, path)
-        old = _SAVED.setdefault(cdir, [])
-        old.append(path)
-        while len(old) > 3:
-            try:
-                os.remove(old.pop(0))
-            except OSError:
-                pass
-    global _SAVER
-    if _SAVER is None:
-        import concurrent.futures as cf
-        # one long-lived writer: files land in iteration order, and starting a
-        # thread per reduce cost ~0.1 ms on the job's critical path
-        _SAVER = cf.ThreadPoolExecutor(1, thread_name_prefix="kmeans-centroid-save")
-    _SAVER.submit(_write)
+def _save_centroids(cdir, key, cen):
+    """Commit centroid version ``key`` to the centroid directory before the
+    reduce reports success (the DistributedCache side file of the next
+    iteration): a tracker whose GPU worker restarts re-localises it from here,
+    so it must exist once the job counts as done — an asynchronous writer could
+    die with its worker first.  Runs after the reduce's host sync, when the
+    next iteration's maps are already on the device."""
+    host = cen.detach().to("cpu", torch.float32).numpy()
+    os.makedirs(cdir, exist_ok=True)
+    path = _centroid_file(cdir, key)
+    tmp = path + ".tmp.npy"
+    np.save(tmp, host)
+    os.replace(tmp, path)
+    old = _SAVED.setdefault(cdir, [])
+    old.append(path)
+    while len(old) > 3:
+        try:
+            os.remove(old.pop(0))
+        except OSError:
+            pass
 
 
-_SAVER = None
 _SAVED: dict = {}
 _PINNED_INFLIGHT: list = []     # (event, pinned host buffer) of in-flight split loads
 
@@ -257,6 +247,56 @@ def _sum_slabs(outs):
 _EXACT_STATS: dict = {}
 _EXACT_LOCK = threading.Lock()
 
+# Reference partitions of the delta combiner, per (split, device, k, dp,
+# fx_shift, exact) in this (worker) process; least recently used first.  A
+# baseline is a pure function of the split's points and a labelling, so it is
+# valid for any job over the same split whatever its centroids.
+_BASELINES: "dict" = {}
+_BASE_LOCK = threading.Lock()
+_BASE_MAX = 4096
+
+
+def _baseline_plan(ctxs, datas, k, dp, fx, exact, enabled):
+    """Split a batch into tasks with a usable baseline (delta path), tasks that
+    get one from this batch (direct combiner, then installed) and the rest
+    (direct combiner only: a second attempt of a split in the same batch)."""
+    have, new, plain = [], [], []
+    bases, keys = [], []
+    seen = set()
+    for i, (c, d) in enumerate(zip(ctxs, datas)):
+        sk = (c.spec.split or {}).get("key") if isinstance(c.spec.split, dict) else None
+        key = None if (sk is None or not enabled) else (sk, str(c.device), k, dp, fx, exact)
+        keys.append(key)
+        if key is None or key in seen:
+            plain.append(i)
+            bases.append(None)
+            continue
+        seen.add(key)
+        x = d.xb if exact else d
+        with _BASE_LOCK:
+            b = _BASELINES.get(key)
+        if b is not None and b.data_ptr == x.data_ptr() and b.n == x.shape[0]:
+            have.append(i)
+            bases.append(b)
+        else:
+            new.append(i)
+            bases.append(None)
+    return have, new, plain, bases, keys
+
+
+def _install_baselines(entries, stream):
+    """entries: (key, Baseline) updated or created by a batch just enqueued on
+    ``stream``; their event marks its end."""
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    with _BASE_LOCK:
+        for key, b in entries:
+            b.event, b.stream = ev, stream
+            _BASELINES.pop(key, None)
+            _BASELINES[key] = b
+        while len(_BASELINES) > _BASE_MAX:
+            _BASELINES.pop(next(iter(_BASELINES)))
+
 
 def _exact_stats(cin, device):
     """Device counters (flagged, relabelled) of exact mode for one iteration."""
@@ -284,6 +324,9 @@ class KMeansSplitJob(SplitJob):
         self.fx_shift = conf.get_int("hbmr.kmeans.fx.shift", 24)
         self.cdir = conf.get(CDIR_KEY)
         self.exact = conf.get_boolean(EXACT_KEY, False)
+        self.combiner = (conf.get(COMBINER_KEY) or "delta").lower()
+        if self.combiner not in ("delta", "sorted"):
+            raise ValueError(f"{COMBINER_KEY} must be delta or sorted, not {self.combiner!r}")
         init = conf.get(INIT_KEY)
         if init and self.cin and STORE.host_centroids(self.cin) is None:
             STORE.put_host(self.cin, decode_centroids(init))
@@ -452,6 +495,7 @@ class KMeansSplitJob(SplitJob):
         store = ctx.tracker.__dict__.setdefault("_scratch", {})
         ws, labels = store.get(key, (None, None))
         need_lab, need_ws = km.batch_scratch_sizes(ns, k)
+        need_ws = max(need_ws, km.delta_workspace_bytes(int(sum(ns)), len(ns), k))
         if ws is None or ws.numel() < need_ws:
             ws = torch.empty(max(need_ws, 1 << 20), dtype=torch.uint8, device=ctx.device)
         if labels is None or labels.numel() < need_lab:
@@ -463,40 +507,122 @@ class KMeansSplitJob(SplitJob):
         return self.map_gpu_batch([ctx], [points])[0]
 
     def map_gpu_batch(self, ctxs, datas):
+        st = ctxs[0].stream
+        if st is None:
+            return self._map_gpu_batch(ctxs, datas)
+        with torch.cuda.stream(st):
+            return self._map_gpu_batch(ctxs, datas)
+
+    def _map_gpu_batch(self, ctxs, datas):
         """All queued map tasks of this job on one stream, launched by one
-        native call (hbmr_kmeans_map_batch); each task keeps its own slab."""
+        native call per combiner path; each task keeps its own slab.  Splits
+        with a reference partition take the delta combiner
+        (hbmr_kmeans_map_batch_delta); the others the direct one
+        (hbmr_kmeans_map_batch), whose labels become their reference partition."""
         from ..ops import kmeans as km
         ctx = ctxs[0]
         img = STORE.image(self.cin, ctx.device)
+        # the image may live on the reduce's stream (pipelined iterations)
+        for t in (img.cbf, img.chalf):
+            t.record_stream(torch.cuda.current_stream())
         B = len(datas)
         if self.exact:
             return self._map_exact(ctxs, datas, img)
+        have, new, plain, bases, keys = _baseline_plan(
+            ctxs, datas, self.k, img.dp, img.fx_shift, False, self.combiner == "delta")
         ws, labels = self._scratch(ctx, [d.shape[0] for d in datas], self.k)
         sums = torch.empty(B, self.k, img.dp, dtype=torch.int64, device=ctx.device)
         counts = torch.empty(B, self.k, dtype=torch.int64, device=ctx.device)
-        km.map_batch_gpu(datas, img, sums, counts, labels, ws, stream=ctx.stream,
-                         zero_outputs=True)
+        order = have + new + plain
+        pos = {i: j for j, i in enumerate(order)}
+        H = len(have)
+        installed = []
+        if have:
+            hb = [bases[i] for i in have]
+            km.map_batch_delta([datas[i] for i in have], img, sums[:H], counts[:H], labels, ws,
+                               hb, stream=ctx.stream)
+            for i, b in zip(have, hb):
+                b.S0, b.N0 = sums[pos[i]], counts[pos[i]]
+                installed.append((keys[i], b))
+        rest = new + plain
+        if rest:
+            km.map_batch_gpu([datas[i] for i in rest], img, sums[H:], counts[H:], labels, ws,
+                             stream=ctx.stream, zero_outputs=True)
+            off = 0
+            for i in rest:
+                n = datas[i].shape[0]
+                if keys[i] is not None and i in new:
+                    # this batch's labels become the split's reference partition
+                    g = labels[off:off + n].clone()
+                    b = km.Baseline(g, sums[pos[i]], counts[pos[i]], datas[i].data_ptr(), n)
+                    installed.append((keys[i], b))
+                off += n
+        if installed:
+            _install_baselines(installed, ctx.stream)
         for c, d in zip(ctxs, datas):
             c.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, d.shape[0])
-        return [(sums[i], counts[i]) for i in range(B)]
+        return [(sums[pos[i]], counts[pos[i]]) for i in range(B)]
 
     def _map_exact(self, ctxs, datas, img):
-        """Exact mode: per task top-3 assign, certification / fp64 re-score,
-        fp32 combiner.  The flagged / relabelled counts accumulate on the device
-        per (job, device) and are reported by the reduce (no host sync here)."""
+        """Exact mode: per task top-3 assign and certification / fp64 re-score,
+        then ONE fp32-row combiner call for the batch (delta against the
+        splits' reference partitions where they exist).  The flagged /
+        relabelled counts accumulate on the device per (job, device) and are
+        reported by the reduce (no host sync here)."""
         from ..ops import kmeans as km
         ctx = ctxs[0]
         store = ctx.tracker.__dict__.setdefault("_scratch", {})
         scratch = store.setdefault(("kmeans-exact", str(ctx.device), id(ctx.stream)), {})
         stats = _exact_stats(self.cin, ctx.device)
-        outs = []
+        have, new, plain, bases, keys = _baseline_plan(
+            ctxs, datas, self.k, img.dp, img.fx_shift, True, self.combiner == "delta")
+        B = len(datas)
+        sums = torch.empty(B, self.k, img.dp, dtype=torch.int64, device=ctx.device)
+        counts = torch.empty(B, self.k, dtype=torch.int64, device=ctx.device)
+        order = have + new + plain
+        pos = {i: j for j, i in enumerate(order)}
+        H = len(have)
+        installed = []
+        if have:
+            ns = [datas[i].shape[0] for i in have]
+            total = sum(ns)
+            lab = scratch.get("labcat")
+            if lab is None or lab.numel() < total:
+                lab = scratch["labcat"] = torch.empty(total, dtype=torch.int32, device=ctx.device)
+            need = km.delta_workspace_bytes(total, H, self.k)
+            if scratch.get("dws") is None or scratch["dws"].numel() < need:
+                scratch["dws"] = torch.empty(need, dtype=torch.uint8, device=ctx.device)
+            off = 0
+            for i, n in zip(have, ns):
+                lab[off:off + n].copy_(km.assign_exact(datas[i], img, stats, scratch,
+                                                       stream=ctx.stream))
+                off += n
+            hb = [bases[i] for i in have]
+            km.delta_combine([datas[i].x32 for i in have], lab, self.k, sums[:H], counts[:H],
+                             scratch["dws"], hb, fx_shift=img.fx_shift, stream=ctx.stream)
+            for i, b in zip(have, hb):
+                b.S0, b.N0 = sums[pos[i]], counts[pos[i]]
+                installed.append((keys[i], b))
+        for i in new + plain:
+            d = datas[i]
+            s, c = sums[pos[i]], counts[pos[i]]
+            s.zero_()
+            c.zero_()
+            lab = km.assign_exact(d, img, stats, scratch, stream=ctx.stream)
+            need = km.workspace_bytes(d.shape[0], img.k)
+            if scratch.get("ws") is None or scratch["ws"].numel() < need:
+                scratch["ws"] = torch.empty(max(need, 1 << 20), dtype=torch.uint8,
+                                            device=ctx.device)
+            km.accumulate(d.x32, lab, img.k, s, c, fx_shift=img.fx_shift, stream=ctx.stream,
+                          workspace=scratch["ws"])
+            if keys[i] is not None and i in new:
+                b = km.Baseline(lab.clone(), s, c, d.xb.data_ptr(), d.shape[0])
+                installed.append((keys[i], b))
+        if installed:
+            _install_baselines(installed, ctx.stream)
         for c, d in zip(ctxs, datas):
-            sums = torch.zeros(self.k, img.dp, dtype=torch.int64, device=ctx.device)
-            counts = torch.zeros(self.k, dtype=torch.int64, device=ctx.device)
-            km.map_split_exact(d, img, sums, counts, scratch, stats, stream=ctx.stream)
             c.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, d.shape[0])
-            outs.append((sums, counts))
-        return outs
+        return [(sums[pos[i]], counts[pos[i]]) for i in range(B)]
 
     def map_cpu(self, ctx, points):
         from ..ops import kmeans as km
@@ -527,6 +653,14 @@ class KMeansSplitJob(SplitJob):
         dev = ctx.device if ctx.device is not None else torch.device("cpu")
         dp = km.padded_dim(self.d) if dev.type == "cuda" else self.d
         outputs = [o for o in outputs if o is not None]   # simulated no-data maps
+        if dev.type == "cuda":
+            # the slabs were allocated on the slot streams; this (reduce) stream
+            # reads them, possibly before those streams are done with the memory
+            cur = torch.cuda.current_stream()
+            for s, c in outputs:
+                if s.is_cuda:
+                    s.record_stream(cur)
+                    c.record_stream(cur)
         same = [(s, c) for s, c in outputs if s.device == dev and s.shape[1] == dp]
         other = [(s, c) for s, c in outputs if not (s.device == dev and s.shape[1] == dp)]
         if same:
@@ -568,6 +702,11 @@ class KMeansSplitJob(SplitJob):
             if TRACE.on:
                 TRACE.instant("kmeans.refresh_launched")
             STORE.put_image(self.cout, sums.device, img)
+            # the next iteration's staged maps may go on the device now, behind
+            # the update kernel (hbmr/gpu/gates.py); the host sync comes after
+            rel = getattr(ctx, "release_dependents", None)
+            if rel is not None:
+                rel()
             # the shift and the point count in one device->host copy (one sync)
             shift, npts = torch.stack([img.shift2.max().double().sqrt(),
                                        counts.sum().double()]).tolist()
@@ -583,13 +722,16 @@ class KMeansSplitJob(SplitJob):
             shift = float((new_cen - old).norm(dim=1).max()) if self.k else 0.0
             npts = int(counts.sum().item())
             STORE.put_host(self.cout, new_cen)
+            rel = getattr(ctx, "release_dependents", None)
+            if rel is not None:
+                rel()
         self._write_output(ctx, counts, new_cen)
         if TRACE.on:
             TRACE.instant("kmeans.output_written")
         res = {"shift": shift, "points": int(npts), "centroids_key": self.cout}
         if ctx.rank == 0 and self.cdir:
             cen = new_cen if new_cen is not None else STORE.image(self.cout, sums.device).cen
-            _save_centroids_async(self.cdir, self.cout, self.cin, cen[:, :self.d])
+            _save_centroids(self.cdir, self.cout, cen[:, :self.d])
         if ctx.rank == 0 and self.conf.get_boolean(RETURN_KEY, False):
             # the new centroids travel back with the result (the client may live
             # in another process than the reduce, e.g. with GPU worker processes)
@@ -689,6 +831,7 @@ class KMeansDriver:
                                                            self.run_id)
         self._manifest_written = False
         self.prefetch_delay = 0.005     # s after a job's submission before the next one's
+        self._ahead: list = []          # iteration jobs submitted ahead, oldest first
 
     def _write_manifest(self):
         import json
@@ -747,19 +890,28 @@ class KMeansDriver:
         return job
 
     def step(self, prefetch=False):
-        """One iteration job.  ``prefetch``: also submit the next iteration now,
-        held by the JobTracker until this one succeeds (its set-up overlaps this
-        job; the next step() uses it).  A run that stops early kills it."""
+        """One iteration job.  ``prefetch`` (True = 1, or a count): keep that
+        many next iterations submitted ahead, each depending on the one before
+        (hbmr.job.depends.on).  The JobTracker holds each until its predecessor
+        succeeds — and stages its GPU maps behind the predecessor's reduce
+        (JobTracker._maybe_stage), so consecutive iterations meet on the device
+        without a round trip.  A run that stops early kills them
+        (cancel_prefetch)."""
         i = self.iteration
         if not self._manifest_written:
             self._write_manifest()
         t0 = time.time()
-        rj, self._next = getattr(self, "_next", None), None
-        if rj is None:
-            rj = self.submit(self._job_conf(i))
-        if prefetch and not rj.waitForCompletion(self.prefetch_delay):
+        rj = self._ahead.pop(0) if self._ahead else self.submit(self._job_conf(i))
+        depth = int(prefetch)
+        if depth > 0 and len(self._ahead) < depth and \
+                not rj.waitForCompletion(self.prefetch_delay):
             # submitted once this job's own launch is under way, not in its path
-            self._next = self.submit(self._job_conf(i + 1, depends_on=rj.getID()))
+            last = self._ahead[-1] if self._ahead else rj
+            while len(self._ahead) < depth:
+                nxt = self.submit(self._job_conf(i + 1 + len(self._ahead),
+                                                 depends_on=last.getID()))
+                self._ahead.append(nxt)
+                last = nxt
         rj.waitForCompletion()
         if not rj.isSuccessful():
             raise RuntimeError(f"K-Means iteration {i} failed: {rj.getFailureInfo()}")
@@ -786,9 +938,9 @@ class KMeansDriver:
         return self.centroids()
 
     def cancel_prefetch(self):
-        """Kill a pre-submitted next iteration (the run stopped before it)."""
-        nxt, self._next = getattr(self, "_next", None), None
-        if nxt is not None:
+        """Kill the iterations submitted ahead (the run stopped before them)."""
+        ahead, self._ahead = self._ahead, []
+        for nxt in reversed(ahead):
             nxt.killJob()
 
     def centroids(self):

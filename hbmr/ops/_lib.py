@@ -43,6 +43,14 @@ _SIGS = {
     "hbmr_kmeans_map_batch": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
                                       c_int, c_void_p, c_void_p, c_long, c_void_p, c_void_p,
                                       c_int, c_int, c_void_p]),
+    "hbmr_kmeans_delta_workspace_bytes": (c_long, [c_long, c_int, c_int]),
+    "hbmr_kmeans_delta_combine": (c_int, [c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                                          c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_int,
+                                          c_void_p, c_void_p, c_void_p, c_void_p]),
+    "hbmr_kmeans_map_batch_delta": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                                            c_int, c_int, c_void_p, c_void_p, c_long, c_void_p,
+                                            c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                                            c_void_p]),
     "hbmr_kmeans_update": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "hbmr_kmeans_padded_k": (c_int, [c_int]),

@@ -338,6 +338,108 @@ def map_batch_gpu(splits: list, img: CentroidImage, sums: torch.Tensor, counts: 
     _lib.check(rc, "hbmr_kmeans_map_batch")
 
 
+# --------------------------------------------------------------------------- delta combiner
+class Baseline:
+    """Reference partition of one split for the delta combiner: labels ``g``
+    (int32 [n]) and its exact partials ``S0`` (int64 [k, dp]), ``N0`` (int64
+    [k]).  Invariant: S0[c] = Σ_{g(p)=c} fx(x_p), N0[c] = #{p: g(p)=c} — it
+    holds for ANY g, so the map output computed against it is bit-identical to
+    the direct combiner's; it only pays off when few points changed label.
+    ``event`` marks the end of the batch that last updated it (its stream is
+    ``stream``): a batch on another stream waits for it first."""
+    __slots__ = ("g", "S0", "N0", "event", "stream", "data_ptr", "n")
+
+    def __init__(self, g, S0, N0, data_ptr, n):
+        self.g, self.S0, self.N0 = g, S0, N0
+        self.event = None
+        self.stream = None
+        self.data_ptr, self.n = data_ptr, n
+
+
+def delta_workspace_bytes(total: int, ntasks: int, k: int) -> int:
+    return int(_lib.load().hbmr_kmeans_delta_workspace_bytes(total, ntasks, k))
+
+
+def _delta_args(xs, bases, stream):
+    B = len(xs)
+    st = torch.cuda.current_stream() if stream is None else stream
+    for b in bases:
+        # the reference partition may have been written (g) / allocated (S0, N0)
+        # on another stream: order this batch after it, and keep the memory from
+        # being reused under this stream's pending reads
+        if b.event is not None and b.stream is not None and b.stream != st:
+            st.wait_event(b.event)
+        for t in (b.g, b.S0, b.N0):
+            t.record_stream(st)
+    ptrs = (ctypes.c_void_p * B)(*[x.data_ptr() for x in xs])
+    ns = (ctypes.c_long * B)(*[x.shape[0] for x in xs])
+    gs = (ctypes.c_void_p * B)(*[b.g.data_ptr() for b in bases])
+    s0 = (ctypes.c_void_p * B)(*[b.S0.data_ptr() for b in bases])
+    n0 = (ctypes.c_void_p * B)(*[b.N0.data_ptr() for b in bases])
+    return ptrs, ns, gs, s0, n0
+
+
+def map_batch_delta(splits: list, img: CentroidImage, sums: torch.Tensor, counts: torch.Tensor,
+                    labels: torch.Tensor, workspace: torch.Tensor, bases: list,
+                    stream=None) -> None:
+    """A batch of map tasks against reference partitions (hbmr_kmeans_map_batch_delta):
+    grouped MFMA assign, then the delta combiner.  sums/counts [B, k, dp] /
+    [B, k] are overwritten; every ``bases[t]`` advances to this batch's labels."""
+    B = len(splits)
+    if B == 0:
+        return
+    if B > 64 or len(bases) != B:
+        raise ValueError("at most 64 splits per delta batch, one baseline each")
+    for s, b in zip(splits, bases):
+        if s.dtype != torch.bfloat16 or s.shape[1] != img.dp or not s.is_contiguous():
+            raise ValueError("splits must be contiguous bf16 [n, dp]")
+        if b.g.numel() != s.shape[0] or tuple(b.S0.shape) != (img.k, img.dp) or \
+                b.N0.numel() != img.k:
+            raise ValueError("baseline does not match its split")
+    if sums.shape != (B, img.k, img.dp) or counts.shape != (B, img.k) or \
+            not sums.is_contiguous() or not counts.is_contiguous():
+        raise ValueError("batch output shape mismatch")
+    total = sum(s.shape[0] for s in splits)
+    if labels.numel() < total:
+        raise ValueError("labels scratch too small")
+    need = delta_workspace_bytes(total, B, img.k)
+    if workspace.numel() < need:
+        raise ValueError("workspace too small")
+    ptrs, ns, gs, s0, n0 = _delta_args(splits, bases, stream)
+    rc = _lib.load().hbmr_kmeans_map_batch_delta(
+        B, ptrs, ns, img.dp, _ptr(img.cbf), _ptr(img.chalf), img.k_pad, img.k, _ptr(labels),
+        _ptr(workspace), workspace.numel(), _ptr(sums), _ptr(counts), img.fx_shift, gs, s0, n0,
+        _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_kmeans_map_batch_delta")
+
+
+def delta_combine(xs: list, labels: torch.Tensor, k: int, sums: torch.Tensor,
+                  counts: torch.Tensor, workspace: torch.Tensor, bases: list,
+                  fx_shift: int = FX_SHIFT, stream=None) -> None:
+    """The delta combiner alone over precomputed labels (concatenated in task
+    order): rows are bf16 or fp32 (exact mode) ``[n_t, dp]``."""
+    B = len(xs)
+    if B == 0:
+        return
+    dp = xs[0].shape[1]
+    f32 = xs[0].dtype == torch.float32
+    for x, b in zip(xs, bases):
+        if x.dtype != xs[0].dtype or x.shape[1] != dp or not x.is_contiguous() or \
+                b.g.numel() != x.shape[0]:
+            raise ValueError("delta_combine: rows/baselines mismatch")
+    if B > 64 or dp not in SUPPORTED_DP or sums.shape != (B, k, dp) or counts.shape != (B, k):
+        raise ValueError("delta_combine: shape mismatch")
+    total = sum(x.shape[0] for x in xs)
+    need = delta_workspace_bytes(total, B, k)
+    if workspace.numel() < need or labels.numel() < total:
+        raise ValueError("delta_combine: scratch too small")
+    ptrs, ns, gs, s0, n0 = _delta_args(xs, bases, stream)
+    rc = _lib.load().hbmr_kmeans_delta_combine(
+        B, ptrs, ns, dp, int(f32), k, _ptr(labels), _ptr(workspace), workspace.numel(),
+        _ptr(sums), _ptr(counts), fx_shift, gs, s0, n0, _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_kmeans_delta_combine")
+
+
 def map_split_gpu(points, img: CentroidImage, sums, counts, labels=None, stream=None):
     """One GPU K-Means map task over an HBM-resident split: assign + combine."""
     labels = assign(points, img, labels=labels, stream=stream)

@@ -954,11 +954,19 @@ __global__ __launch_bounds__(256) void kmeans_scatter_kernel(const int32_t* __re
 // at the segment end the groups are reduced with xor-shuffles so each cluster
 // costs one 128-value atomic flush per wave — spread over all groups — rather
 // than one per group.  Segment bounds are wave-uniform (scalar loads).
-template <typename T, int D, int U>
+// Row indirection of a segsum entry: the plain combiner's perm holds row
+// indices; the delta combiner's holds (mover << 1 | sign) — see kmeans_delta_*.
+struct IdentityRows {
+  __device__ __forceinline__ uint32_t row(uint32_t i) const { return i; }
+  __device__ __forceinline__ bool neg(uint32_t) const { return false; }
+};
+
+template <typename T, int D, int U, class Rows = IdentityRows>
 __device__ __forceinline__ void segsum_range(const T* __restrict__ X,
                                              const uint32_t* __restrict__ pm,
                                              const uint32_t* __restrict__ of, int k, long s0,
-                                             long e, u64* __restrict__ out, float scale) {
+                                             long e, u64* __restrict__ out, float scale,
+                                             Rows rows = Rows()) {
   constexpr int TPP = D / 8;            // lanes per row
   constexpr int GPW = HBMR_WAVE / TPP;  // row groups per wave
   const int lane = threadIdx.x & 63;
@@ -988,7 +996,7 @@ __device__ __forceinline__ void segsum_range(const T* __restrict__ X,
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const long q = base + (long)u * GPW;
-          if (q < segE) v[u].load(X, idx[u], D, sub);
+          if (q < segE) v[u].load(X, rows.row(idx[u]), D, sub);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -996,6 +1004,11 @@ __device__ __forceinline__ void segsum_range(const T* __restrict__ X,
           if (q < segE) {
             float f[8];
             v[u].unpack(f);
+            if (rows.neg(idx[u])) {
+              // round-half-even fixed point is odd-symmetric: fx(-x) = -fx(x)
+#pragma unroll
+              for (int j = 0; j < 8; ++j) f[j] = -f[j];
+            }
             hbmr_fx_accum8(f, scale, acc);
           }
         }
@@ -1145,6 +1158,188 @@ __global__ __launch_bounds__(256) void kmeans_segsum_grouped_kernel(
   segsum_range<__bf16, D, U>(tbl.X[sidx], perm + tbl.off[sidx], offsets + (size_t)sidx * (k + 1), k, s0,
                      min(n, s0 + chunk), reinterpret_cast<u64*>(sums) + (size_t)sidx * k * D,
                      scale);
+}
+
+// ---- delta combiner --------------------------------------------------------------
+// The combiner output of a split is a function of its points and their labels
+// only.  Given a reference partition g of the split (labels of an earlier
+// pass) with its exact int64 sums S0[c] = Σ_{g(p)=c} fx(x_p) and counts N0,
+// the sums for the new labels l are
+//     S[c] = S0[c] + Σ_{l(p)=c, g(p)≠c} fx(x_p) - Σ_{g(p)=c, l(p)≠c} fx(x_p)
+// (integer arithmetic: bit-identical to the direct combiner for ANY g).  Only
+// the points whose label changed ("movers") are gathered, so once K-Means
+// settles the combiner no longer re-reads the split: it is a pass over the
+// labels plus a few thousand rows.  Afterwards (S0, N0, g) := (S, N, l), which
+// the diff kernel does for g in place.
+//
+//   kmeans_slab_copy      : sums[t] = S0[t], counts[t] = N0[t]
+//   kmeans_delta_diff     : movers (p, new << 16 | old), hist[c] = #entries,
+//                           counts[t] += in - out, g[p] = l
+//   kmeans_delta_scatter  : entries e = (mover << 1 | sign) sorted by cluster
+//                           (+new for sign 0, -old for sign 1)
+//   kmeans_delta_segsum   : segmented signed row sums of the entries into sums[t]
+struct SlabTable {
+  const long long* s[kMaxGroup];
+  const long long* c[kMaxGroup];
+};
+struct GTable {
+  int32_t* g[kMaxGroup];
+};
+
+__global__ __launch_bounds__(256) void kmeans_slab_copy_kernel(const SlabTable src, long slab,
+                                                               int k, long long* __restrict__ sums,
+                                                               long long* __restrict__ counts) {
+  const int t = blockIdx.y;
+  const long long* s = src.s[t];
+  long long* d = sums + (size_t)t * slab;
+  // slab = k * dp int64 (dp ≥ 64): whole 16-byte pieces
+  const long npc = slab / 2;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < npc; i += (long)gridDim.x * 256)
+    reinterpret_cast<int4*>(d)[i] = reinterpret_cast<const int4*>(s)[i];
+  if (blockIdx.x == 0) {
+    const long long* c = src.c[t];
+    for (int i = threadIdx.x; i < k; i += 256) counts[(size_t)t * k + i] = c[i];
+  }
+}
+
+constexpr long kDiffPts = 8192;  // points per diff workgroup
+
+__global__ __launch_bounds__(256) void kmeans_delta_diff_kernel(
+    const SplitTable tbl, const GTable gt, const int32_t* __restrict__ labels,
+    uint2* __restrict__ movers, uint32_t* __restrict__ mcount, uint32_t* __restrict__ hist,
+    long long* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_bins[];  // in[k] | out[k]
+  const int k = tbl.k;
+  const int s = __builtin_amdgcn_readfirstlane(find_split(tbl, blockIdx.x));
+  const long local = blockIdx.x - tbl.blk[s];
+  const long n = tbl.n[s];
+  for (int i = threadIdx.x; i < 2 * k; i += 256) s_bins[i] = 0u;
+  __syncthreads();
+  const int32_t* lab = labels + tbl.off[s];
+  int32_t* g = gt.g[s];
+  uint2* mv = movers + tbl.off[s];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  const long p1 = min(n, (local + 1) * kDiffPts);
+  for (long base = local * kDiffPts + wave * 64; base < p1; base += 256) {
+    const long p = base + lane;
+    int l = 0, o = 0;
+    bool ch = false;
+    if (p < p1) {
+      l = lab[p];
+      o = g[p];
+      ch = l != o;
+    }
+    const unsigned long long m = __ballot(ch);
+    if (m == 0) continue;
+    uint32_t first = 0;
+    if (lane == 0) first = atomicAdd(mcount + s, (uint32_t)__popcll(m));
+    first = __shfl(first, 0);
+    if (ch) {
+      const uint32_t i = first + (uint32_t)__popcll(m & lt);
+      mv[i] = make_uint2((uint32_t)p, ((uint32_t)l << 16) | (uint32_t)o);
+      g[p] = l;
+      atomicAdd(s_bins + l, 1u);
+      atomicAdd(s_bins + k + o, 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t* hs = hist + (size_t)s * k;
+  u64* cs = reinterpret_cast<u64*>(counts) + (size_t)s * k;
+  for (int c = threadIdx.x; c < k; c += 256) {
+    const uint32_t in = s_bins[c], out = s_bins[k + c];
+    if (in | out) {
+      atomicAdd(hs + c, in + out);
+      if (in != out) atomicAdd(cs + c, (u64)((long long)in - (long long)out));
+    }
+  }
+}
+
+// tbl.blk: prefix of scatter workgroups per split sized for the worst case
+// (every point moved: 2n entries); surplus workgroups leave after the scan.
+__global__ __launch_bounds__(256) void kmeans_delta_scatter_kernel(
+    const SplitTable tbl, const uint2* __restrict__ movers, const uint32_t* __restrict__ mcount,
+    const uint32_t* __restrict__ hist, uint32_t* __restrict__ cursor,
+    uint32_t* __restrict__ offsets, uint32_t* __restrict__ perm) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_h[];  // off[k] | cnt[k] | base[k]
+  const int k = tbl.k;
+  __shared__ uint32_t s_total;
+  const int s = __builtin_amdgcn_readfirstlane(find_split(tbl, blockIdx.x));
+  const long local = blockIdx.x - tbl.blk[s];
+  const long ne = 2L * (long)__builtin_amdgcn_readfirstlane(mcount[s]);
+  if (local > 0 && local * kScatterPts >= ne) return;   // uniform: nothing for this block
+  uint32_t* s_off = s_h;
+  uint32_t* s_cnt = s_h + k;
+  uint32_t* s_base = s_h + 2 * k;
+  const int t = threadIdx.x;
+  for (int i = t; i < k; i += 256) s_cnt[i] = 0u;
+  block_exclusive_scan(hist + (size_t)s * k, k, s_off, &s_total);
+  if (local == 0) {
+    uint32_t* os = offsets + (size_t)s * (k + 1);
+    for (int i = t; i < k; i += 256) os[i] = s_off[i];
+    if (t == 0) os[k] = s_total;
+  }
+  constexpr int PER = kScatterPts / 256;
+  const uint2* mv = movers + tbl.off[s];
+  const long e0 = local * kScatterPts + (long)t * PER;
+  int cl[PER];
+  uint32_t rank[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const long e = e0 + j;
+    cl[j] = -1;
+    if (e < ne) {
+      const uint32_t y = mv[e >> 1].y;
+      cl[j] = (e & 1) ? (int)(y & 0xffffu) : (int)(y >> 16);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) rank[j] = cl[j] >= 0 ? atomicAdd(s_cnt + cl[j], 1u) : 0u;
+  __syncthreads();
+  uint32_t* cur_s = cursor + (size_t)s * k;
+  for (int i = t; i < k; i += 256) {
+    const uint32_t c = s_cnt[i];
+    s_base[i] = c ? s_off[i] + atomicAdd(cur_s + i, c) : 0u;
+  }
+  __syncthreads();
+  uint32_t* perm_s = perm + 2 * tbl.off[s];
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    if (cl[j] >= 0) perm_s[s_base[cl[j]] + rank[j]] = (uint32_t)(e0 + j);
+}
+
+struct MoverRows {
+  const uint2* mv;
+  __device__ __forceinline__ uint32_t row(uint32_t e) const { return mv[e >> 1].x; }
+  __device__ __forceinline__ bool neg(uint32_t e) const { return (e & 1u) != 0u; }
+};
+
+// Persistent grid: wave items (split, chunk of `chunk` entries) in split order,
+// counted from the device-side mover counts.
+template <typename T, int D, int U>
+__global__ __launch_bounds__(256) void kmeans_delta_segsum_kernel(
+    const SplitTable tbl, const uint2* __restrict__ movers, const uint32_t* __restrict__ mcount,
+    const uint32_t* __restrict__ perm, const uint32_t* __restrict__ offsets, long chunk,
+    long long* __restrict__ sums, float scale) {
+  const int k = tbl.k;
+  const long nw = (long)gridDim.x * (blockDim.x / HBMR_WAVE);
+  long wid = (long)blockIdx.x * (blockDim.x / HBMR_WAVE) + threadIdx.x / HBMR_WAVE;
+  int s = 0;
+  long sbase = 0;
+  long items = (2L * (long)__builtin_amdgcn_readfirstlane(mcount[0]) + chunk - 1) / chunk;
+  for (; ; wid += nw) {
+    while (wid >= sbase + items) {
+      sbase += items;
+      if (++s >= tbl.nsplit) return;
+      items = (2L * (long)__builtin_amdgcn_readfirstlane(mcount[s]) + chunk - 1) / chunk;
+    }
+    const long ne = 2L * (long)__builtin_amdgcn_readfirstlane(mcount[s]);
+    const long e0 = (wid - sbase) * chunk;
+    segsum_range<T, D, U, MoverRows>(
+        reinterpret_cast<const T*>(tbl.X[s]), perm + 2 * tbl.off[s],
+        offsets + (size_t)s * (k + 1), k, e0, min(ne, e0 + chunk),
+        reinterpret_cast<u64*>(sums) + (size_t)s * k * D, scale, MoverRows{movers + tbl.off[s]});
+  }
 }
 
 // Reduce side + next-iteration prep.  One workgroup per cluster.
@@ -1324,6 +1519,8 @@ bool set_lds_limits() {
     HBMR_LDS_OPTIN((kmeans_accum_chunked_kernel<float, 128, 8>));
     HBMR_LDS_OPTIN((kmeans_accum_chunked_kernel<float, 256, 8>));
     HBMR_LDS_OPTIN(kmeans_scatter_grouped_kernel);
+    HBMR_LDS_OPTIN(kmeans_delta_scatter_kernel);
+    HBMR_LDS_OPTIN(kmeans_delta_diff_kernel);
 #undef HBMR_LDS_OPTIN
     done = true;
   }
@@ -1802,6 +1999,168 @@ int hbmr_kmeans_map_batch(int ntasks, const void* const* X, const long* n, int d
     if (rc) return rc;
   }
   return 0;
+}
+
+// ---- delta combiner (see kmeans_delta_* above) ------------------------------------
+// workspace: hist[B*k] | cursor[B*k] | offsets[B*(k+1)] | mcount[B] | movers[total]
+// (uint2) | perm[2*total] (u32), regions 256-B aligned.
+long hbmr_kmeans_delta_workspace_bytes(long total_n, int ntasks, int k) {
+  return (long)(2 * ws_align((size_t)ntasks * k * 4) + ws_align((size_t)ntasks * (k + 1) * 4) +
+                ws_align((size_t)ntasks * 4) + 2 * ws_align((size_t)total_n * 8));
+}
+
+}  // extern "C"
+
+template <typename T>
+static int delta_combine_impl(int ntasks, const void* const* X, const long* n, int dp, int k,
+                              const int32_t* labels, void* ws, long long* sums,
+                              long long* counts, int fx_shift, int32_t* const* g,
+                              const long long* const* S0, const long long* const* N0,
+                              hipStream_t st) {
+  SplitTable t;
+  memset(&t, 0, sizeof(t));
+  t.nsplit = ntasks;
+  t.k = k;
+  long total = 0;
+  for (int i = 0; i < ntasks; ++i) {
+    t.X[i] = reinterpret_cast<const __bf16*>(X[i]);
+    t.n[i] = n[i];
+    t.off[i] = total;
+    total += n[i];
+  }
+  char* w = reinterpret_cast<char*>(ws);
+  const size_t hb = ws_align((size_t)ntasks * k * 4);
+  const size_t ob = ws_align((size_t)ntasks * (k + 1) * 4);
+  const size_t mb = ws_align((size_t)ntasks * 4);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(w);
+  uint32_t* cursor = reinterpret_cast<uint32_t*>(w + hb);
+  uint32_t* offsets = reinterpret_cast<uint32_t*>(w + 2 * hb);
+  uint32_t* mcount = reinterpret_cast<uint32_t*>(w + 2 * hb + ob);
+  uint2* movers = reinterpret_cast<uint2*>(w + 2 * hb + ob + mb);
+  uint32_t* perm = reinterpret_cast<uint32_t*>(w + 2 * hb + ob + mb + ws_align((size_t)total * 8));
+  HBMR_RETURN_IF_ERROR(hipMemsetAsync(hist, 0, 2 * hb, st));   // hist + cursor
+  HBMR_RETURN_IF_ERROR(hipMemsetAsync(mcount, 0, mb, st));
+  // 0. outputs start from the reference partition's sums and counts
+  SlabTable src;
+  memset(&src, 0, sizeof(src));
+  for (int i = 0; i < ntasks; ++i) {
+    src.s[i] = S0[i];
+    src.c[i] = N0[i];
+  }
+  const long slab = (long)k * dp;
+  const unsigned gx = (unsigned)std::max<long>(1, std::min<long>((slab / 2 + 255) / 256, 64));
+  hipLaunchKernelGGL(kmeans_slab_copy_kernel, dim3(gx, (unsigned)ntasks), dim3(256), 0, st, src,
+                     slab, k, sums, counts);
+  HBMR_RETURN_IF_ERROR(hipGetLastError());
+  // 1. movers, entry histogram, count deltas, g := labels
+  long nb = 0;
+  for (int i = 0; i < ntasks; ++i) {
+    t.blk[i] = nb;
+    nb += (n[i] + kDiffPts - 1) / kDiffPts;
+  }
+  t.blk[ntasks] = nb;
+  GTable gt;
+  memset(&gt, 0, sizeof(gt));
+  for (int i = 0; i < ntasks; ++i) gt.g[i] = g[i];
+  if (nb > 0) {
+    hipLaunchKernelGGL(kmeans_delta_diff_kernel, dim3((unsigned)nb), dim3(256), (size_t)2 * k * 4,
+                       st, t, gt, labels, movers, mcount, hist, counts);
+    HBMR_RETURN_IF_ERROR(hipGetLastError());
+  }
+  // 2. entries sorted by cluster (grid for the worst case, 2n entries per split)
+  nb = 0;
+  for (int i = 0; i < ntasks; ++i) {
+    t.blk[i] = nb;
+    nb += std::max<long>(1, (2 * n[i] + kScatterPts - 1) / kScatterPts);
+  }
+  t.blk[ntasks] = nb;
+  hipLaunchKernelGGL(kmeans_delta_scatter_kernel, dim3((unsigned)nb), dim3(256),
+                     (size_t)3 * k * 4, st, t, movers, mcount, hist, cursor, offsets, perm);
+  HBMR_RETURN_IF_ERROR(hipGetLastError());
+  // 3. signed segmented row sums (persistent waves over the device-side counts)
+  const float scale = ldexpf(1.0f, fx_shift);
+  const unsigned blocks = (unsigned)cu_count() * 4;
+  switch (dp) {
+#define HBMR_DS(DD)                                                                          \
+  case DD:                                                                                   \
+    hipLaunchKernelGGL((kmeans_delta_segsum_kernel<T, DD, 8>), dim3(blocks), dim3(256), 0,   \
+                       st, t, movers, mcount, perm, offsets, 256L, sums, scale);             \
+    break;
+    HBMR_DS(64)
+    HBMR_DS(128)
+    HBMR_DS(256)
+#undef HBMR_DS
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" {
+
+int hbmr_kmeans_delta_combine(int ntasks, const void* const* X, const long* n, int dp, int x_f32,
+                              int k, const int32_t* labels, void* ws, long ws_bytes,
+                              long long* sums, long long* counts, int fx_shift,
+                              int32_t* const* g, const long long* const* S0,
+                              const long long* const* N0, hipStream_t st) {
+  if (ntasks <= 0) return 0;
+  if (ntasks > kMaxGroup || k <= 0 || k > 8192 || (dp != 64 && dp != 128 && dp != 256))
+    return (int)hipErrorInvalidValue;
+  long total = 0;
+  for (int i = 0; i < ntasks; ++i) {
+    if (n[i] < 0 || n[i] >= (1L << 31)) return (int)hipErrorInvalidValue;
+    total += n[i];
+  }
+  if (ws == nullptr || ws_bytes < hbmr_kmeans_delta_workspace_bytes(total, ntasks, k))
+    return (int)hipErrorInvalidValue;
+  set_lds_limits();
+  return x_f32 ? delta_combine_impl<float>(ntasks, X, n, dp, k, labels, ws, sums, counts,
+                                           fx_shift, g, S0, N0, st)
+               : delta_combine_impl<__bf16>(ntasks, X, n, dp, k, labels, ws, sums, counts,
+                                            fx_shift, g, S0, N0, st);
+}
+
+// A batch of map tasks against reference partitions: grouped MFMA assign of
+// every split into `labels`, then the delta combiner.
+int hbmr_kmeans_map_batch_delta(int ntasks, const void* const* X, const long* n, int dp,
+                                const void* C, const float* chalf, int k_pad, int k,
+                                int32_t* labels, void* ws, long ws_bytes, long long* sums,
+                                long long* counts, int fx_shift, int32_t* const* g,
+                                const long long* const* S0, const long long* const* N0,
+                                hipStream_t st) {
+  if (ntasks <= 0) return 0;
+  if (ntasks > kMaxGroup || k_pad % kCK) return (int)hipErrorInvalidValue;
+  SplitTable t;
+  memset(&t, 0, sizeof(t));
+  t.nsplit = ntasks;
+  t.k = k;
+  int pts = 0;
+  switch (dp) {
+    case 64: pts = assign_pts<64>(false); break;
+    case 128: pts = assign_pts<128>(false); break;
+    case 256: pts = assign_pts<256>(false); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  long total = 0, nb = 0;
+  for (int i = 0; i < ntasks; ++i) {
+    t.X[i] = reinterpret_cast<const __bf16*>(X[i]);
+    t.n[i] = n[i];
+    t.off[i] = total;
+    total += n[i];
+    t.blk[i] = nb;
+    nb += (n[i] + pts - 1) / pts;
+  }
+  t.blk[ntasks] = nb;
+  if (nb > 0x7fffffffL) return (int)hipErrorInvalidValue;
+  if (nb > 0) {
+    switch (dp) {
+      case 64: launch_grouped_assign<64>(nb, t, C, chalf, k_pad, labels, nullptr, st); break;
+      case 128: launch_grouped_assign<128>(nb, t, C, chalf, k_pad, labels, nullptr, st); break;
+      case 256: launch_grouped_assign<256>(nb, t, C, chalf, k_pad, labels, nullptr, st); break;
+    }
+    HBMR_RETURN_IF_ERROR(hipGetLastError());
+  }
+  return hbmr_kmeans_delta_combine(ntasks, X, n, dp, 0, k, labels, ws, ws_bytes, sums, counts,
+                                   fx_shift, g, S0, N0, st);
 }
 
 int hbmr_kmeans_assign_top3_bf16(const void* X, long n, int dp, const void* C, const float* chalf,

@@ -210,7 +210,7 @@ def test_prefetched_iterations_match_and_wait_for_their_dependency():
         c = K.KMeansDriver(cl.submit_job, res, conf=conf, k=k, d=d, inp=inp, split_points=3000)
         c.prefetch_delay = 0.0
         c.step(prefetch=True)
-        held = c._next
+        held = c._ahead[0]
         c.cancel_prefetch()
         assert held.waitForCompletion(10)
         assert held.status().state == "KILLED"   # (released and running by then)

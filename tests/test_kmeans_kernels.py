@@ -137,3 +137,90 @@ def test_map_batch_matches_per_split(k, dp, sizes):
         ref_c = torch.bincount(lab.long(), minlength=k)
         assert torch.equal(counts[t], ref_c), t
         assert torch.equal(sums[t], ref_s), t
+
+
+# ---------------------------------------------------------------- delta combiner
+def _fx_ref(x, lab, k):
+    fx = torch.round(x.double() * (1 << km.FX_SHIFT)).long()
+    s = torch.zeros(k, x.shape[1], dtype=torch.int64, device=x.device).index_add_(0, lab.long(), fx)
+    return s, torch.bincount(lab.long(), minlength=k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("k,dp,sizes,churn", [(1024, 128, [5000, 1, 70000, 4096], 0.05),
+                                              (64, 128, [3000, 9000], 1.0),
+                                              (300, 64, [777, 20000, 5], 0.3),
+                                              (8192, 256, [30000], 0.01),
+                                              (1024, 128, [4000, 4000], 0.0)])
+def test_delta_combiner_is_bit_identical_to_direct(dtype, k, dp, sizes, churn):
+    """sums/counts from a reference partition + movers equal the direct
+    combiner's for the new labels, bit for bit; the baseline advances."""
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(11)
+    xs = [(torch.randn(n, dp, generator=g) * 3).to(dev, dtype) for n in sizes]
+    B = len(xs)
+    bases, new_labs = [], []
+    for x in xs:
+        n = x.shape[0]
+        l0 = torch.randint(0, k, (n,), generator=g).to(dev, torch.int32)
+        s0, c0 = _fx_ref(x, l0, k)
+        bases.append(km.Baseline(l0.clone(), s0, c0, x.data_ptr(), n))
+        move = torch.rand(n, generator=g) < churn
+        l1 = torch.where(move, torch.randint(0, k, (n,), generator=g), l0.cpu().long())
+        new_labs.append(l1.to(dev, torch.int32))
+    labcat = torch.cat(new_labs)
+    sums = torch.full((B, k, dp), 7, dtype=torch.int64, device=dev)
+    counts = torch.full((B, k), 7, dtype=torch.int64, device=dev)
+    ws = torch.empty(km.delta_workspace_bytes(labcat.numel(), B, k), dtype=torch.uint8,
+                     device=dev)
+    km.delta_combine(xs, labcat, k, sums, counts, ws, bases)
+    torch.cuda.synchronize()
+    for t, (x, l1) in enumerate(zip(xs, new_labs)):
+        rs, rc = _fx_ref(x, l1, k)
+        assert torch.equal(counts[t], rc), t
+        assert torch.equal(sums[t], rs), t
+        assert torch.equal(bases[t].g, l1), t       # g advanced in place
+
+
+@pytest.mark.gpu
+def test_map_batch_delta_tracks_lloyd_iterations_exactly():
+    """Several Lloyd iterations: the delta map batch (assign + movers) gives the
+    same partials as the direct map batch at every step."""
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(5)
+    k, dp = 256, 128
+    centers = torch.randn(64, dp, generator=g) * 6
+    sizes = [20000, 777, 50000]
+    xs = []
+    for n in sizes:
+        lab = torch.randint(0, 64, (n,), generator=g)
+        xs.append((centers[lab] + torch.randn(n, dp, generator=g)).to(dev, torch.bfloat16))
+    img = km.CentroidImage(xs[0][:k].float(), dev)
+    B, tot = len(xs), sum(sizes)
+    nlab, nws = km.batch_scratch_sizes(sizes, k)
+    labels = torch.empty(nlab, dtype=torch.int32, device=dev)
+    ws = torch.empty(max(nws, km.delta_workspace_bytes(tot, B, k)), dtype=torch.uint8, device=dev)
+    bases = None
+    for it in range(5):
+        ref_s = torch.empty(B, k, dp, dtype=torch.int64, device=dev)
+        ref_c = torch.empty(B, k, dtype=torch.int64, device=dev)
+        km.map_batch_gpu(xs, img, ref_s, ref_c, labels, ws)
+        if bases is None:
+            bases = []
+            off = 0
+            for t, x in enumerate(xs):
+                n = x.shape[0]
+                bases.append(km.Baseline(labels[off:off + n].clone(), ref_s[t].clone(),
+                                         ref_c[t].clone(), x.data_ptr(), n))
+                off += n
+        else:
+            s = torch.empty_like(ref_s)
+            c = torch.empty_like(ref_c)
+            km.map_batch_delta(xs, img, s, c, labels, ws, bases)
+            torch.cuda.synchronize()
+            assert torch.equal(s, ref_s), it
+            assert torch.equal(c, ref_c), it
+            for t, b in enumerate(bases):
+                b.S0, b.N0 = s[t], c[t]
+        img.refresh(ref_s.sum(0), ref_c.sum(0))

@@ -1,0 +1,99 @@
+"""Pre-staged iteration jobs (hbmr/gpu/gates.py, JobTracker._maybe_stage): a
+job that depends on a running collective split job has its GPU maps launched
+early, held on each tracker until the predecessor's reduce there released its
+result, and its own collective reduce launched before its maps finished
+("expect" mode).  The reference can only start the next K-Means iteration
+after a JobControl poll (JobControl.java) and a >= 3 s heartbeat
+(MRConstants.java:28).  Simulated GPU slots keep these tests on the CPU."""
+import pytest
+import torch
+
+from hbmr.mapred.cluster import LocalCluster
+from hbmr.mapred.jobconf import JobConf
+from hbmr.models import kmeans as K
+
+JIP = "org.apache.hadoop.mapred.JobInProgress$Counter"
+
+
+def _conf(worker, prestage=True, task_ms=3.0, **kw):
+    conf = JobConf()
+    conf.set_boolean("hbmr.gpu.simulate", True)
+    conf.set_boolean("hbmr.gpu.worker.process", worker)
+    conf.set_float("hbmr.gpu.simulate.task.ms", task_ms)
+    conf.set_int("mapred.tasktracker.map.gpu.tasks.maximum", 2)
+    conf.set_int("hbmr.gpu.queue.depth", 16)
+    conf.set_int("mapred.task.timeout", 0)
+    conf.set_boolean("hbmr.job.prestage", prestage)
+    for k, v in kw.items():
+        conf.set(k, str(v))
+    return conf
+
+
+def _run(conf, tmp, steps=5, depth=2, trackers=1):
+    conf.set("mapred.local.dir", str(tmp))
+    gpus = [[i] for i in range(trackers)]
+    with LocalCluster(conf, num_trackers=trackers, gpus=gpus, cpu_slots=0) as cl:
+        drv = K.KMeansDriver(cl.submit_job, lambda rj: rj._impl.jip.result[0], conf=conf, k=5,
+                             d=8, inp="synthetic:8000:3", split_points=1000)
+        drv.prefetch_delay = 0.0
+        for s in range(steps):
+            assert drv.step(prefetch=min(depth, steps - 1 - s))["points"] == 8000
+        jobs = [cl.jt.jobs[h["job"]] for h in drv.history]
+        events = [e for e in cl.jt.history.events]
+        return drv.centroids(), jobs, events, drv
+
+
+@pytest.mark.parametrize("worker", [False, True])
+def test_staged_iterations_run_ahead_and_give_the_same_centroids(worker, tmp_path):
+    want, _, ev0, _ = _run(_conf(worker, prestage=False), tmp_path / "plain")
+    assert not any(e["event"] == "JOB_STAGED" for e in ev0)
+    got, jobs, events, _ = _run(_conf(worker), tmp_path / "staged")
+    assert torch.equal(got, want)
+    assert sum(e["event"] == "JOB_STAGED" for e in events) >= 3
+    for prev, nxt in zip(jobs, jobs[1:]):
+        # a staged job never completes before the job it depends on
+        assert nxt.status.finish_time >= prev.status.finish_time > 0
+    # maps of later iterations were launched before their predecessor finished
+    ahead = [nxt.t_first_map < prev.status.finish_time for prev, nxt in zip(jobs, jobs[1:])]
+    assert sum(ahead) >= 2, ahead
+    # and collective reduces started before the last map of their job finished
+    assert any(j.t_first_reduce and j.t_maps_done and j.t_first_reduce < j.t_maps_done
+               for j in jobs)
+
+
+def test_staged_iterations_over_two_trackers(tmp_path):
+    want, _, _, _ = _run(_conf(False, prestage=False), tmp_path / "plain", trackers=2)
+    got, jobs, events, _ = _run(_conf(False), tmp_path / "staged", trackers=2)
+    assert torch.equal(got, want)
+    assert any(e["event"] == "JOB_STAGED" for e in events)
+
+
+def test_staged_job_survives_a_worker_crash_in_its_predecessor(tmp_path):
+    """Iteration 3's map crashes the GPU worker while iteration 4 is staged on
+    it: the held staged attempts die with the worker, everything re-runs and
+    the answer is the same."""
+    want, _, _, _ = _run(_conf(True, prestage=False), tmp_path / "plain")
+    got, jobs, events, _ = _run(
+        _conf(True, **{"hbmr.faultinject.worker.exit.attempt": "_0003_m_000002_0"}),
+        tmp_path / "crash")
+    assert torch.equal(got, want)
+
+
+def test_killing_a_staged_job_fails_its_dependents(tmp_path):
+    conf = _conf(False, task_ms=20.0)
+    conf.set("mapred.local.dir", str(tmp_path))
+    with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=0) as cl:
+        drv = K.KMeansDriver(cl.submit_job, lambda rj: rj._impl.jip.result[0], conf=conf, k=5,
+                             d=8, inp="synthetic:8000:3", split_points=1000)
+        drv.prefetch_delay = 0.0
+        drv.step(prefetch=2)
+        a, b = drv._ahead
+        drv.cancel_prefetch()
+        assert a.waitForCompletion(20) and b.waitForCompletion(20)
+        assert a.status().state == "KILLED"
+        assert b.status().state in ("KILLED", "FAILED")
+        assert not cl.jt.staged
+        # the cluster still runs iterations afterwards
+        drv2 = K.KMeansDriver(cl.submit_job, lambda rj: rj._impl.jip.result[0], conf=conf, k=5,
+                              d=8, inp="synthetic:8000:3", split_points=1000)
+        assert drv2.step()["points"] == 8000

@@ -41,8 +41,42 @@ def summary(rows, top):
     return "\n".join(lines)
 
 
+def iterations(rows, end_pat="kmeans_update_kernel",
+               map_pat=r"kmeans_(assign|segsum|scatter|hist|delta|slab)"):
+    """Per K-Means iteration (delimited by the reduce's update kernel): span
+    between update ends, GPU busy (union of kernel intervals), idle between the
+    previous update end and the first assign, last map kernel end -> update end."""
+    ends = [i for i, r in enumerate(rows) if end_pat in r[0]]
+    rx = re.compile(map_pat)
+    out = ["| iteration span ms | GPU busy ms | idle before first assign ms | "
+           "last map kernel -> update end ms |", "|---|---|---|---|"]
+    for a, b in zip(ends, ends[1:]):
+        prev_end = rows[a][2]
+        seg = rows[a + 1:b + 1]
+        iv = sorted((max(s, prev_end), e) for _n, s, e, *_ in seg if e > prev_end)
+        busy, cur_s, cur_e = 0, None, None
+        for s, e in iv:
+            if cur_e is None or s > cur_e:
+                if cur_e is not None:
+                    busy += cur_e - cur_s
+                cur_s, cur_e = s, e
+            else:
+                cur_e = max(cur_e, e)
+        if cur_e is not None:
+            busy += cur_e - cur_s
+        first = min((s for n, s, e, *_ in seg if "assign" in n), default=None)
+        last_map = max((e for n, s, e, *_ in seg if rx.search(n)), default=None)
+        upd = rows[b][2]
+        out.append(f"| {(upd - prev_end) / 1e6:.2f} | {busy / 1e6:.2f} | "
+                   f"{((first - prev_end) / 1e6) if first else float('nan'):.2f} | "
+                   f"{((upd - last_map) / 1e6) if last_map else float('nan'):.2f} |")
+    return "\n".join(out)
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--iterations", action="store_true",
+                    help="per-iteration K-Means table (spans, busy, idle gaps)")
     ap.add_argument("db")
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--timeline")
@@ -59,6 +93,9 @@ def main():
         span = (rows[-1][2] - rows[0][1]) / 1e3 if rows else 0.0
         print(f"window: {len(rows)} dispatches over {span:.1f} µs (first to last end)\n")
     print(summary(rows, a.top))
+    if a.iterations:
+        print()
+        print(iterations(rows))
     if a.timeline:
         t0 = None
         rx = re.compile(a.timeline)
