@@ -86,7 +86,8 @@ class Tracer:
     def to_jsonl(self, path):
         with open(path, "w") as f:
             for ts, th, ph, name, dur, args in self.events:
-                rec = {"ts_us": wall_ns(ts) / 1e3, "thread": th, "ph": ph, "name": name}
+                rec = {"ts_us": wall_ns(ts) / 1e3, "mono_ns": ts, "thread": th, "ph": ph,
+                       "name": name}
                 if ph == "X":
                     rec["dur_us"] = dur / 1e3
                 if args:

@@ -1228,7 +1228,9 @@ __global__ __launch_bounds__(256) void kmeans_delta_diff_kernel(
     if (p < p1) {
       l = lab[p];
       o = g[p];
-      ch = l != o;
+      // (a label outside [0, k) would index past the bins and the slabs:
+      // such a point is never a mover — the bit-exactness tests catch it)
+      ch = l != o && (unsigned)l < (unsigned)k && (unsigned)o < (unsigned)k;
     }
     const unsigned long long m = __ballot(ch);
     if (m == 0) continue;
@@ -1991,12 +1993,16 @@ int hbmr_kmeans_map_batch(int ntasks, const void* const* X, const long* n, int d
     return map_batch_grouped(ntasks, X, n, dp, C, chalf, k_pad, k, labels, ws, sums, counts,
                              fx_shift, st, cu_count());
   }
+  // every task's labels at its offset in `labels` (as the grouped path lays
+  // them out): callers keep them, e.g. as the delta combiner's reference partition
+  long off = 0;
   for (int t = 0; t < ntasks; ++t) {
-    int rc = hbmr_kmeans_assign_bf16(X[t], n[t], dp, C, chalf, k_pad, labels, nullptr, st);
+    int rc = hbmr_kmeans_assign_bf16(X[t], n[t], dp, C, chalf, k_pad, labels + off, nullptr, st);
     if (rc) return rc;
-    rc = hbmr_kmeans_accum_bf16(X[t], n[t], dp, labels, k, sums + (size_t)t * k * dp,
+    rc = hbmr_kmeans_accum_bf16(X[t], n[t], dp, labels + off, k, sums + (size_t)t * k * dp,
                                 counts + (size_t)t * k, fx_shift, ws, ws_bytes, 0, st);
     if (rc) return rc;
+    off += n[t];
   }
   return 0;
 }

@@ -175,3 +175,31 @@ def test_gpu_worker_process_runs_the_hip_kernels_and_survives_a_crash(tmp_path):
     assert deaths2 == 1
     assert sum(h["counters"].get(JIP, "NUM_FAILED_MAPS") for h in hist2) >= 1
     assert torch.equal(got2, ref)
+
+
+@pytest.mark.gpu
+def test_gpu_prestaged_iterations_with_delta_combiner_match_plain_runs(tmp_path):
+    """On the MI355X: iterations staged two ahead (maps gated on the device
+    behind the previous reduce) with the delta combiner give exactly the
+    centroids of plain, one-at-a-time iterations with the sorted combiner."""
+    def run(tmp, prestage, combiner, ahead):
+        conf = JobConf()
+        conf.set_boolean("hbmr.gpu.worker.process", True)
+        conf.set_int("mapred.tasktracker.map.gpu.tasks.maximum", 2)
+        conf.set_int("hbmr.gpu.queue.depth", 16)
+        conf.set_int("mapred.task.timeout", 0)
+        conf.set_boolean("hbmr.job.prestage", prestage)
+        conf.set("hbmr.kmeans.combiner", combiner)
+        conf.set("mapred.local.dir", str(tmp))
+        with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=0) as cl:
+            drv = K.KMeansDriver(cl.submit_job, lambda rj: rj._impl.jip.result[0], conf=conf,
+                                 k=256, d=128, inp="synthetic:600000:3", split_points=50000)
+            drv.prefetch_delay = 0.0
+            for s in range(6):
+                assert drv.step(prefetch=min(ahead, 5 - s))["points"] == 600000
+            staged = sum(e["event"] == "JOB_STAGED" for e in cl.jt.history.events)
+            return drv.centroids(), staged
+    ref, s0 = run(tmp_path / "plain", False, "sorted", 0)
+    got, s1 = run(tmp_path / "staged", True, "delta", 2)
+    assert s0 == 0 and s1 >= 3
+    assert torch.equal(got, ref)

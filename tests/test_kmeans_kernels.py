@@ -130,8 +130,12 @@ def test_map_batch_matches_per_split(k, dp, sizes):
     ws = torch.empty(nws, dtype=torch.uint8, device=dev)
     km.map_batch_gpu(splits, img, sums, counts, labels, ws)
     torch.cuda.synchronize()
+    off = 0
     for t, x in enumerate(splits):
         lab = km.assign(x, img)
+        # every task's labels at its offset (the delta combiner keeps them)
+        assert torch.equal(labels[off:off + x.shape[0]], lab), t
+        off += x.shape[0]
         fx = torch.round(x.double() * (1 << km.FX_SHIFT)).long()
         ref_s = torch.zeros(k, dp, dtype=torch.int64, device=dev).index_add_(0, lab.long(), fx)
         ref_c = torch.bincount(lab.long(), minlength=k)
