@@ -376,6 +376,8 @@ TOOLS = {  # src/tools + contrib commands of bin/hadoop
     "logalyzer": "hbmr.tools.logalyzer:main",
     "distch": "hbmr.tools.distch:main",
     "failmon": "hbmr.utils.failmon:main",
+    "isolationrunner": "hbmr.mapred.isolation:main",
+    "org.apache.hadoop.mapred.IsolationRunner": "hbmr.mapred.isolation:main",
 }
 
 

@@ -10,6 +10,7 @@ PROGRAMS = {
                            "An Aggregate based map/reduce program that counts the words in the input files."),
     "aggregatewordhist": ("hbmr.examples.aggregatewordcount:main_histogram",
                           "An Aggregate based map/reduce program that computes the histogram of the words in the input files."),
+    "dbcount": ("hbmr.examples.dbcount:main", "An example job that count the pageview counts from a database."),
     "grep": ("hbmr.examples.grep:main", "A map/reduce program that counts the matches of a regex in the input."),
     "join": ("hbmr.examples.join:main", "A job that effects a join over sorted, equally partitioned datasets"),
     "multifilewc": ("hbmr.examples.multifilewc:main", "A job that counts words from several files."),

@@ -108,6 +108,10 @@ class GpuRuntime:
         self.slots_per_device = max(1, slots_per_device)
         self.max_batch = max(1, tracker.conf.get_int("hbmr.gpu.batch.max", 64))
         self.first_chunk = max(1, tracker.conf.get_int("hbmr.gpu.first.chunk", 4))
+        # tasks per launch after the first chunk: smaller batches reach the
+        # device sooner (each costs ~10-20 µs of host work per task to prepare),
+        # larger ones amortise the per-launch kernels
+        self.batch_target = max(1, tracker.conf.get_int("hbmr.gpu.batch.target", 16))
         # > 0: the submitter of an idle device's first chunk waits (up to this
         # long) until it is launched.  In-process traces show the device
         # starting ~1 ms earlier, but same-box A/Bs of the bench measured no
@@ -248,7 +252,7 @@ class GpuRuntime:
                 # split the rest of the job's batch over the slots so streams overlap
                 rest = len(runs) - i
                 nslot = len(dev.slots) if hasattr(sj, "map_gpu_batch") else rest
-                per = min(self.max_batch, max(1, -(-rest // max(1, nslot))))
+                per = min(self.max_batch, self.batch_target, max(1, -(-rest // max(1, nslot))))
                 if rest <= self.first_chunk and hasattr(sj, "map_gpu_batch"):
                     per = max(1, rest)       # a first chunk: one launch, no split
                 for j in range(i, len(runs), per):

@@ -203,6 +203,11 @@ class SimulatedGpuRuntime:
             # the slots are streams of ONE device: work on any slot queues behind
             # the device's earlier work (task.ms is the device's time per task)
             start = max(time.time(), dev.busy_until)
+            # staged runs of an opened gate: not before the reduce's (simulated)
+            # device result is ready
+            waits = [r.wait for r in live if isinstance(getattr(r, "wait", None), float)]
+            if waits:
+                start = max(start, max(waits))
             slot.busy_until = dev.busy_until = start + self.task_s * len(live)
             slot.inflight += len(live)
             # outputs for an early collective reduce, "ready" at the simulated end

@@ -145,6 +145,14 @@ def run_split_reduce(host, run, device=None):
         rep = TaskReporter()
         run.task = SplitTaskShim(rep, run.kill)
         ctx = TaskContext(host, js, spec, rep)
+        hconf = getattr(host, "conf", None)
+        if hconf is not None and hconf.get_boolean("hbmr.gpu.simulate.nodata", False) and \
+                (hconf.get("hbmr.gpu.simulate.collective") or "device") == "device":
+            # control-plane rehearsal without data: the device collective (RCCL
+            # all-reduce over xGMI) is modelled as device time like the maps are,
+            # instead of moving zeros through gloo on the host
+            ctx.simulated_collective_s = hconf.get_float(
+                "hbmr.gpu.simulate.collective.ms", 0.1) / 1e3
         comm = getattr(host, "comm", None)
         before = dict(getattr(comm, "stats", None) or {})
         try:
@@ -161,7 +169,7 @@ def run_split_reduce(host, run, device=None):
             released[0] = True
             if rt is None or not hasattr(rt, "open_gate"):
                 return
-            ev = None
+            ev = getattr(ctx, "sim_ready", None)   # simulated device: a ready time
             if cuda:
                 import torch
                 ev = torch.cuda.Event()

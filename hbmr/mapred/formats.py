@@ -379,6 +379,156 @@ class SequenceFileAsTextInputFormat(SequenceFileInputFormat):
         return _AsText()
 
 
+class SequenceFileAsBinaryInputFormat(SequenceFileInputFormat):
+    """Keys and values as raw BytesWritable, not deserialised
+    (SequenceFileAsBinaryInputFormat.java): the record bytes exactly as stored
+    (after RECORD/BLOCK decompression), for jobs that move records unread."""
+
+    def getRecordReader(self, split, job, reporter):  # noqa: N802
+        from ..io.writable import BytesWritable
+        rr = SequenceFileRecordReader(job, split)
+
+        class _AsBinary(RecordReader):
+            def next(self_inner):
+                raw = rr.next_raw()
+                return None if raw is None else (BytesWritable(raw[0]), BytesWritable(raw[1]))
+
+            def getKeyClassName(self_inner):  # noqa: N802,N805
+                return rr.reader.key_class_name
+
+            def getValueClassName(self_inner):  # noqa: N802,N805
+                return rr.reader.value_class_name
+
+            def getProgress(self_inner):  # noqa: N802
+                return rr.getProgress()
+
+            def getPos(self_inner):  # noqa: N802
+                return rr.getPos()
+
+            def close(self_inner):
+                rr.close()
+
+        return _AsBinary()
+
+
+FILTER_CLASS = "sequencefile.filter.class"
+FILTER_FREQUENCY = "sequencefile.filter.frequency"
+FILTER_REGEX = "sequencefile.filter.regex"
+
+
+class SequenceFileInputFilter(SequenceFileInputFormat):
+    """Only the records whose KEY passes ``sequencefile.filter.class``
+    (SequenceFileInputFilter.java): RegexFilter (``sequencefile.filter.regex``
+    must match the whole key), PercentFilter (the 1st of every
+    ``sequencefile.filter.frequency`` records, default 10) or MD5Filter (keys
+    whose MD5's first 8 bytes, as a signed long, are a multiple of the
+    frequency — a stable sample of keys)."""
+
+    class Filter:
+        def configure(self, conf):
+            pass
+
+        def accept(self, key) -> bool:
+            raise NotImplementedError
+
+    class RegexFilter(Filter):
+        @staticmethod
+        def setPattern(conf, regex):  # noqa: N802
+            import re
+            try:
+                re.compile(regex)
+            except re.error as e:
+                raise ValueError(f"Invalid pattern: {regex}") from e
+            conf.set(FILTER_REGEX, regex)
+
+        def configure(self, conf):
+            import re
+            regex = conf.get(FILTER_REGEX)
+            if regex is None:
+                raise RuntimeError(f"{FILTER_REGEX} not set")
+            self.p = re.compile(regex)
+
+        def accept(self, key):
+            return self.p.fullmatch(str(key)) is not None
+
+    class PercentFilter(Filter):
+        @staticmethod
+        def setFrequency(conf, f):  # noqa: N802
+            if f <= 0:
+                raise ValueError(f"Negative {FILTER_FREQUENCY}: {f}")
+            conf.set_int(FILTER_FREQUENCY, f)
+
+        def configure(self, conf):
+            self.frequency = conf.get_int(FILTER_FREQUENCY, 10)
+            if self.frequency <= 0:
+                raise RuntimeError(f"Negative {FILTER_FREQUENCY}: {self.frequency}")
+            self.count = 0
+
+        def accept(self, key):
+            ok = self.count == 0
+            self.count += 1
+            if self.count == self.frequency:
+                self.count = 0
+            return ok
+
+    class MD5Filter(Filter):
+        setFrequency = staticmethod(lambda conf, f: SequenceFileInputFilter.PercentFilter  # noqa: E731,N815
+                                    .setFrequency(conf, f))
+
+        def configure(self, conf):
+            self.frequency = conf.get_int(FILTER_FREQUENCY, 10)
+            if self.frequency <= 0:
+                raise RuntimeError(f"Negative {FILTER_FREQUENCY}: {self.frequency}")
+
+        @staticmethod
+        def md5_hashcode(b: bytes) -> int:
+            import hashlib
+            h = int.from_bytes(hashlib.md5(b).digest()[:8], "big")
+            return h - (1 << 64) if h & (1 << 63) else h
+
+        def accept(self, key):
+            from ..io.writable import BytesWritable
+            if isinstance(key, Text):
+                b = key.bytes
+            elif isinstance(key, BytesWritable):
+                b = key.get()
+            else:
+                b = str(key).encode("utf-8")
+            h = self.md5_hashcode(bytes(b))
+            # Java's h / f * f == h: integer division truncates toward zero
+            q = abs(h) // self.frequency * (1 if h >= 0 else -1)
+            return q * self.frequency == h
+
+    @staticmethod
+    def setFilterClass(conf, cls):  # noqa: N802
+        from ..utils.reflection import class_name
+        conf.set(FILTER_CLASS, class_name(cls))
+
+    def getRecordReader(self, split, job, reporter):  # noqa: N802
+        from ..utils.reflection import new_instance
+        rr = SequenceFileRecordReader(job, split)
+        flt = new_instance(job.get_class(FILTER_CLASS, SequenceFileInputFilter.PercentFilter),
+                           job)
+
+        class _Filtered(RecordReader):
+            def next(self_inner):
+                while True:
+                    kv = rr.next()
+                    if kv is None or flt.accept(kv[0]):
+                        return kv
+
+            def getProgress(self_inner):  # noqa: N802
+                return rr.getProgress()
+
+            def getPos(self_inner):  # noqa: N802
+                return rr.getPos()
+
+            def close(self_inner):
+                rr.close()
+
+        return _Filtered()
+
+
 # --------------------------------------------------------------------------- outputs
 def get_task_output_path(job, name: str) -> str:
     """Where a task attempt writes: the committer's work dir if set."""
@@ -481,6 +631,64 @@ class SequenceFileOutputFormat(FileOutputFormat):
     def get_readers(path):
         files = sorted(p for p in F.listdir(path) if p.startswith("part-"))
         return [seqf.Reader(os.path.join(path, p)) for p in files]
+
+
+SEQBINARY_KEY_CLASS = "mapred.seqbinary.output.key.class"
+SEQBINARY_VALUE_CLASS = "mapred.seqbinary.output.value.class"
+
+
+class _RawSeqWriter(RecordWriter):
+    def __init__(self, w):
+        self.w = w
+
+    def write(self, key, value):
+        # BytesWritable payloads go into the file as the record's key/value bytes
+        self.w.append_raw(bytes(key.get()), bytes(value.get()))
+
+    def close(self, reporter=None):
+        self.w.close()
+
+
+class SequenceFileAsBinaryOutputFormat(SequenceFileOutputFormat):
+    """Writes BytesWritable keys/values as the raw record bytes of a
+    SequenceFile whose header names the real classes
+    (``mapred.seqbinary.output.{key,value}.class``, default the job's output
+    classes) — SequenceFileAsBinaryOutputFormat.java; the output of
+    SequenceFileAsBinaryInputFormat round-trips unchanged."""
+
+    @staticmethod
+    def setSequenceFileOutputKeyClass(conf, cls):  # noqa: N802
+        conf.set_class(SEQBINARY_KEY_CLASS, cls)
+
+    @staticmethod
+    def setSequenceFileOutputValueClass(conf, cls):  # noqa: N802
+        conf.set_class(SEQBINARY_VALUE_CLASS, cls)
+
+    @staticmethod
+    def getSequenceFileOutputKeyClass(conf):  # noqa: N802
+        return conf.get(SEQBINARY_KEY_CLASS) or conf.get_output_key_class()
+
+    @staticmethod
+    def getSequenceFileOutputValueClass(conf):  # noqa: N802
+        return conf.get(SEQBINARY_VALUE_CLASS) or conf.get_output_value_class()
+
+    def getRecordWriter(self, fs, job, name, progress=None):  # noqa: N802
+        path = get_task_output_path(job, name)
+        comp, codec = seqf.NONE, None
+        if self.get_compress_output(job):
+            comp = job.get("mapred.output.compression.type", "RECORD").upper()
+            codec = job.get("mapred.output.compression.codec",
+                            "org.apache.hadoop.io.compress.DefaultCodec")
+        w = seqf.Writer(path, self.getSequenceFileOutputKeyClass(job),
+                        self.getSequenceFileOutputValueClass(job), comp, codec)
+        return _RawSeqWriter(w)
+
+    def checkOutputSpecs(self, fs, job):  # noqa: N802
+        super().checkOutputSpecs(fs, job)
+        if self.get_compress_output(job) and \
+                job.get("mapred.output.compression.type", "RECORD").upper() == seqf.RECORD:
+            raise ValueError("SequenceFileAsBinaryOutputFormat doesn't support Record "
+                             "Compression")
 
 
 class MapFileOutputFormat(FileOutputFormat):

@@ -160,7 +160,8 @@ class JobConf(Configuration):
         """Returns a sort-key function over serialised map-output keys."""
         c = self._cls("mapred.output.key.comparator.class", None)
         if c is not None:
-            return c().sort_key if isinstance(c, type) else c
+            from ..utils.reflection import new_instance
+            return new_instance(c, self).sort_key if isinstance(c, type) else c
         return self.get_map_output_key_class().raw_sort_key
 
     def set_output_key_comparator_class(self, c):
@@ -169,7 +170,8 @@ class JobConf(Configuration):
     def get_output_value_grouping_comparator(self):
         c = self._cls("mapred.output.value.groupfn.class", None)
         if c is not None:
-            return c().sort_key if isinstance(c, type) else c
+            from ..utils.reflection import new_instance
+            return new_instance(c, self).sort_key if isinstance(c, type) else c
         return self.get_output_key_comparator()
 
     def set_output_value_grouping_comparator(self, c):

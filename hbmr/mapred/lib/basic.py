@@ -71,28 +71,7 @@ class RegexMapper(Mapper):
             output.collect(Text(m.group(self.group)), one)
 
 
-class KeyFieldBasedPartitioner(Partitioner):
-    """Partition on a subset of key fields (``num.key.fields.for.partition`` or
-    ``mapred.text.key.partitioner.options`` -kN,M) split by
-    ``map.output.key.field.separator``."""
-
-    def configure(self, job):
-        self.sep = job.get("map.output.key.field.separator", "\t")
-        opts = job.get("mapred.text.key.partitioner.options")
-        self.lo, self.hi = 1, job.get_int("num.key.fields.for.partition", 0) or None
-        if opts:
-            m = re.match(r"-k(\d+)(?:,(\d+))?", opts)
-            if m:
-                self.lo = int(m.group(1))
-                self.hi = int(m.group(2)) if m.group(2) else None
-
-    def getPartition(self, key, value, num_partitions):  # noqa: N802
-        if not hasattr(self, "sep"):
-            self.sep, self.lo, self.hi = "\t", 1, None
-        fields = str(key).split(self.sep)
-        sel = fields[self.lo - 1:self.hi] if self.hi else fields[self.lo - 1:]
-        h = hash_bytes(self.sep.join(sel).encode("utf-8"))
-        return (h & 0x7FFFFFFF) % num_partitions
+from .keyfield import KeyFieldBasedComparator, KeyFieldBasedPartitioner  # noqa: E402,F401
 
 
 class TotalOrderPartitioner(Partitioner):

@@ -268,6 +268,12 @@ class DataDrivenDBInputFormat(DBInputFormat):
         return out
 
     def getRecordReader(self, split, job, reporter):  # noqa: N802
+        if job.get(INPUT_QUERY):
+            # a free-form query carries the split's range at ``$CONDITIONS``
+            # (DataDrivenDBRecordReader.getSelectQuery)
+            q = job.get(INPUT_QUERY).replace("$CONDITIONS",
+                                             f"( {split.where.format(ph=_ph(job))} )")
+            return DBRecordReader(split, job, q, split.params)
         fields = ", ".join(job.get_strings(INPUT_FIELDS) or ["*"])
         conds = [split.where.format(ph=_ph(job))]
         if job.get(INPUT_CONDITIONS):

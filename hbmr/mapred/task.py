@@ -602,10 +602,13 @@ class MapTask(Task):
             reader.close()
         if R == 0:
             collector.flush()
-            if committer.needs_task_commit(job, self.attempt_id):
-                committer.commit_task(job, self.attempt_id)
         else:
             self.output_file = collector.flush()
+        # side files (MultipleOutputs, lazily created outputs) of a map with
+        # reduces are committed the same way as a map-only task's part file
+        # (Task.done: commit whenever needsTaskCommit)
+        if committer.needs_task_commit(job, self.attempt_id):
+            committer.commit_task(job, self.attempt_id)
         rep.set_progress(1.0)
         self.finish_time = time.time()
         return self.output_file

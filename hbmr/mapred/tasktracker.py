@@ -20,10 +20,12 @@ MI355X-first differences:
 from __future__ import annotations
 
 import concurrent.futures as cf
+import json
 import logging
 import os
 import queue
 import random
+import re
 import socket
 import sys
 import threading
@@ -643,6 +645,7 @@ class TaskTracker:
                 return
             if use_child_process(js.conf):
                 path = self._run_in_child(run, is_map=True)
+                self._keep_task_files(spec, js, failed=False)
                 self._finish(run, P.SUCCEEDED, output={"tracker": self.name, "path": path})
                 return
             split = _split_from_dict(spec.split)
@@ -654,10 +657,37 @@ class TaskTracker:
             run.task = task
             path = run_profiled(js.conf, spec.attempt_id, True, spec.partition, task.run,
                                 os.path.join(self.local_dir, spec.job_id, spec.attempt_id))
+            self._keep_task_files(spec, js, failed=False)
             self._finish(run, P.SUCCEEDED, output={"tracker": self.name, "path": path})
         except BaseException as e:  # noqa: BLE001
             state = P.KILLED if run.kill.is_set() else P.FAILED
+            if state == P.FAILED:
+                self._keep_task_files(spec, js, failed=True)
             self._finish(run, state, f"{type(e).__name__}: {e}\n{traceback.format_exc()[-2000:]}")
+
+    def _keep_task_files(self, spec, js, failed):
+        """Keep a map attempt's task conf and split for IsolationRunner
+        (TaskTracker.java keepFailedTaskFiles / keepTaskFiles pattern):
+        ``<local>/<job>/<attempt>/job.xml`` and ``split.dta``."""
+        conf = js.conf
+        pat = conf.get("keep.task.files.pattern")
+        keep = (failed and conf.get_boolean("keep.failed.task.files", False)) or \
+            (pat is not None and re.fullmatch(pat, spec.attempt_id) is not None)
+        if not keep or spec.split is None:
+            return
+        try:
+            d = os.path.join(self.local_dir, spec.job_id, spec.attempt_id)
+            os.makedirs(d, exist_ok=True)
+            tc = JobConf(conf)
+            tc.set("mapred.task.id", spec.attempt_id)
+            tc.set_int("mapred.task.partition", spec.partition)
+            tc.set_boolean("mapred.task.is.map", True)
+            tc.set("mapred.local.dir", self.local_dir)
+            tc.write_xml(os.path.join(d, "job.xml"))
+            with open(os.path.join(d, "split.dta"), "w") as f:
+                json.dump(spec.split, f)
+        except OSError as e:
+            log.warning("could not keep task files of %s: %s", spec.attempt_id, e)
 
     # -- reduces ---------------------------------------------------------------------------
     def _run_reduce(self, run: _Running):

@@ -263,24 +263,26 @@ def _baseline_plan(ctxs, datas, k, dp, fx, exact, enabled):
     have, new, plain = [], [], []
     bases, keys = [], []
     seen = set()
-    for i, (c, d) in enumerate(zip(ctxs, datas)):
-        sk = (c.spec.split or {}).get("key") if isinstance(c.spec.split, dict) else None
-        key = None if (sk is None or not enabled) else (sk, str(c.device), k, dp, fx, exact)
-        keys.append(key)
-        if key is None or key in seen:
-            plain.append(i)
-            bases.append(None)
-            continue
-        seen.add(key)
-        x = d.xb if exact else d
-        with _BASE_LOCK:
+    dev = str(ctxs[0].device)
+    with _BASE_LOCK:
+        for i, (c, d) in enumerate(zip(ctxs, datas)):
+            sp = c.spec.split
+            sk = sp.get("key") if enabled and isinstance(sp, dict) else None
+            key = None if sk is None else (sk, dev, k, dp, fx, exact)
+            keys.append(key)
+            if key is None or key in seen:
+                plain.append(i)
+                bases.append(None)
+                continue
+            seen.add(key)
             b = _BASELINES.get(key)
-        if b is not None and b.data_ptr == x.data_ptr() and b.n == x.shape[0]:
-            have.append(i)
-            bases.append(b)
-        else:
-            new.append(i)
-            bases.append(None)
+            x = d.xb if exact else d
+            if b is not None and b.data_ptr == x.data_ptr() and b.n == x.shape[0]:
+                have.append(i)
+                bases.append(b)
+            else:
+                new.append(i)
+                bases.append(None)
     return have, new, plain, bases, keys
 
 
@@ -534,34 +536,41 @@ class KMeansSplitJob(SplitJob):
         sums = torch.empty(B, self.k, img.dp, dtype=torch.int64, device=ctx.device)
         counts = torch.empty(B, self.k, dtype=torch.int64, device=ctx.device)
         order = have + new + plain
-        pos = {i: j for j, i in enumerate(order)}
         H = len(have)
+        S, N = sums.unbind(0), counts.unbind(0)     # slab views in task order `order`
+        out = [None] * B
+        for j, i in enumerate(order):
+            out[i] = (S[j], N[j])
         installed = []
         if have:
             hb = [bases[i] for i in have]
             km.map_batch_delta([datas[i] for i in have], img, sums[:H], counts[:H], labels, ws,
                                hb, stream=ctx.stream)
             for i, b in zip(have, hb):
-                b.S0, b.N0 = sums[pos[i]], counts[pos[i]]
+                b.S0, b.N0 = out[i]
                 installed.append((keys[i], b))
         rest = new + plain
         if rest:
             km.map_batch_gpu([datas[i] for i in rest], img, sums[H:], counts[H:], labels, ws,
                              stream=ctx.stream, zero_outputs=True)
-            off = 0
-            for i in rest:
-                n = datas[i].shape[0]
-                if keys[i] is not None and i in new:
-                    # this batch's labels become the split's reference partition
-                    g = labels[off:off + n].clone()
-                    b = km.Baseline(g, sums[pos[i]], counts[pos[i]], datas[i].data_ptr(), n)
-                    installed.append((keys[i], b))
-                off += n
+            if new:
+                # this batch's labels become the new splits' reference partitions
+                # (one allocation for all of them)
+                total = sum(datas[i].shape[0] for i in rest)
+                gall = labels[:total].clone()
+                off = 0
+                newset = set(new)
+                for i in rest:
+                    n = datas[i].shape[0]
+                    if keys[i] is not None and i in newset:
+                        installed.append((keys[i], km.Baseline(gall[off:off + n], *out[i],
+                                                                datas[i].data_ptr(), n)))
+                    off += n
         if installed:
             _install_baselines(installed, ctx.stream)
         for c, d in zip(ctxs, datas):
             c.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, d.shape[0])
-        return [(sums[pos[i]], counts[pos[i]]) for i in range(B)]
+        return out
 
     def _map_exact(self, ctxs, datas, img):
         """Exact mode: per task top-3 assign and certification / fp64 re-score,
@@ -679,8 +688,14 @@ class KMeansSplitJob(SplitJob):
         sums, counts = combined
         k, dp = sums.shape
         packed = torch.cat([sums.reshape(-1), counts])
+        sim = getattr(ctx, "simulated_collective_s", None)
         with TRACE.span("kmeans.allreduce", nbytes=packed.numel() * 8):
-            ctx.comm.all_reduce(packed)        # exact: int64 over RCCL / gloo
+            if sim is None:
+                ctx.comm.all_reduce(packed)        # exact: int64 over RCCL / gloo
+            else:
+                # rehearsal without data (hbmr.gpu.simulate.nodata): the device
+                # all-reduce is modelled as device time ending at this instant
+                ctx.sim_ready = time.time() + sim
         sums = packed[:k * dp].view(k, dp)
         counts = packed[k * dp:]
         if self.exact and sums.device.type == "cuda":
@@ -715,12 +730,17 @@ class KMeansSplitJob(SplitJob):
             new_cen = None
         else:
             old = STORE.host_centroids(self.cin)
-            cnt = counts.to(torch.float64)[:, None]
-            s = sums[:, :self.d].to(torch.float64) / float(1 << self.fx_shift)
-            new_cen = torch.where(cnt > 0, s / cnt.clamp(min=1), old.to(torch.float64)).to(
-                torch.float32)
-            shift = float((new_cen - old).norm(dim=1).max()) if self.k else 0.0
-            npts = int(counts.sum().item())
+            if sim is not None:
+                # no-data rehearsal: every partial is zero, the centroids stay
+                # (the device's update kernel is part of the modelled time)
+                new_cen, shift, npts = old, 0.0, 0
+            else:
+                cnt = counts.to(torch.float64)[:, None]
+                s = sums[:, :self.d].to(torch.float64) / float(1 << self.fx_shift)
+                new_cen = torch.where(cnt > 0, s / cnt.clamp(min=1),
+                                      old.to(torch.float64)).to(torch.float32)
+                shift = float((new_cen - old).norm(dim=1).max()) if self.k else 0.0
+                npts = int(counts.sum().item())
             STORE.put_host(self.cout, new_cen)
             rel = getattr(ctx, "release_dependents", None)
             if rel is not None:

@@ -363,14 +363,21 @@ def delta_workspace_bytes(total: int, ntasks: int, k: int) -> int:
 def _delta_args(xs, bases, stream):
     B = len(xs)
     st = torch.cuda.current_stream() if stream is None else stream
+    events, blocks = {}, {}
     for b in bases:
         # the reference partition may have been written (g) / allocated (S0, N0)
         # on another stream: order this batch after it, and keep the memory from
-        # being reused under this stream's pending reads
+        # being reused under this stream's pending reads (once per event and
+        # per allocation: the baselines of a batch share a few slabs)
         if b.event is not None and b.stream is not None and b.stream != st:
-            st.wait_event(b.event)
+            events[id(b.event)] = b.event
         for t in (b.g, b.S0, b.N0):
-            t.record_stream(st)
+            base = t._base if t._base is not None else t
+            blocks[id(base)] = base
+    for ev in events.values():
+        st.wait_event(ev)
+    for t in blocks.values():
+        t.record_stream(st)
     ptrs = (ctypes.c_void_p * B)(*[x.data_ptr() for x in xs])
     ns = (ctypes.c_long * B)(*[x.shape[0] for x in xs])
     gs = (ctypes.c_void_p * B)(*[b.g.data_ptr() for b in bases])

@@ -127,3 +127,64 @@ def test_output_rolls_back_on_error(tmp_path):
     con = sqlite3.connect(path)
     assert con.execute("SELECT COUNT(*) FROM totals").fetchone()[0] == 0
     con.close()
+
+
+from hbmr.mapreduce import Mapper as _NewMapper, Reducer as _NewReducer  # noqa: E402
+
+
+class NewM(_NewMapper):
+    def map(self, key, value, context):
+        context.write(Text(value.dept), Text(f"{value.salary}"))
+
+
+class NewR(_NewReducer):
+    def reduce(self, key, values, context):
+        xs = [float(str(v)) for v in values]
+        context.write(DeptTotal(str(key), sum(xs), len(xs)), None)
+
+
+@pytest.mark.parametrize("form", ["table", "query"])
+def test_new_api_db_job(tmp_path, form):
+    """mapreduce.lib.db: DataDrivenDBInputFormat (table form, and a free-form
+    query with $CONDITIONS + bounding query) into DBOutputFormat."""
+    from hbmr.mapreduce import Job
+    from hbmr.mapreduce.lib import db as ndb
+    path = str(tmp_path / "n.db")
+    _db(path)
+    conf = JobConf()
+    conf.set("mapred.job.tracker", "local")
+    job = Job(conf, "db")
+    c = job.getConfiguration()
+    ndb.DBConfiguration.configureDB(c, "sqlite3", path)
+    if form == "table":
+        ndb.DataDrivenDBInputFormat.setInput(job, Employee, "emp", None, "id",
+                                             "id", "name", "dept", "salary")
+    else:
+        ndb.DataDrivenDBInputFormat.setInput(
+            job, Employee, "SELECT id, name, dept, salary FROM emp WHERE $CONDITIONS",
+            "SELECT MIN(id), MAX(id) FROM emp")
+        c.set(db.INPUT_ORDER_BY, "id")
+    ndb.DBOutputFormat.setOutput(job, "totals", "dept", "total", "n")
+    c.set_num_map_tasks(3)
+    job.setMapperClass(NewM)
+    job.setReducerClass(NewR)
+    job.setMapOutputKeyClass(Text)
+    job.setMapOutputValueClass(Text)
+    job.setNumReduceTasks(2)
+    assert job.waitForCompletion(False)
+    con = sqlite3.connect(path)
+    got = {d: (t, n) for d, t, n in con.execute("SELECT dept, total, n FROM totals")}
+    con.close()
+    assert got == _expected()
+
+
+def test_new_api_splitters():
+    from hbmr.mapreduce.lib import db as ndb
+    conf = JobConf()
+    conf.set_num_map_tasks(4)
+    sp = ndb.IntegerSplitter().split(conf, 0, 100, "id")
+    assert len(sp) == 4 and sp[0].params[0] == 0 and sp[-1].params[1] == 100
+    assert "<=" in sp[-1].where and "<=" not in sp[0].where.split("AND")[1]
+    ts = ndb.TextSplitter().split(conf, "aaa", "azz", "name")
+    assert ts[0].params[0] == "aaa" and ts[-1].params[1] == "azz"
+    assert all(a.params[1] == b.params[0] for a, b in zip(ts, ts[1:]))

@@ -111,8 +111,9 @@ def test_reduce_side_join(tmp_path, cluster):
     (tmp_path / "a" / "x").write_text("k1\ta1\nk2\ta2\nk3\ta3\n")
     (tmp_path / "b" / "y").write_text("k1\tb1\nk1\tb1x\nk3\tb3\nk4\tb4\n")
     from hbmr.mapred import JobClient
-    JobClient.runJob(join.make_job([str(tmp_path / "a"), str(tmp_path / "b")],
-                                   str(tmp_path / "out")), cluster=cluster, verbose=False)
+    JobClient.runJob(join.make_reduce_side_job([str(tmp_path / "a"), str(tmp_path / "b")],
+                                               str(tmp_path / "out")), cluster=cluster,
+                     verbose=False)
     got = sorted(tuple(r) for r in _read_kv(tmp_path / "out"))
     assert got == [("k1", "a1", "b1"), ("k1", "a1", "b1x"), ("k3", "a3", "b3")]
 
@@ -160,3 +161,16 @@ def test_teragen_terasort_teravalidate_cli(tmp_path, cluster):
     v = T.teravalidate(str(tmp_path / "sorted"))
     assert v["misordered"] == 0 and v["records"] == 5000 and v["files"] == 2
     assert T.teravalidate(str(tmp_path / "gen"))["misordered"] > 0
+
+
+def test_dbcount_pageview(tmp_path):
+    """DBCountPageView over sqlite3: page views per URL add up to the log."""
+    import sqlite3
+    from hbmr.examples import dbcount
+    url = str(tmp_path / "URLAccess.db")
+    assert dbcount.main(["sqlite3", url]) == 0
+    con = sqlite3.connect(url)
+    want = dict(con.execute("SELECT url, COUNT(*) FROM Access GROUP BY url"))
+    got = dict(con.execute("SELECT url, pageview FROM Pageview"))
+    con.close()
+    assert got == want and sum(got.values()) >= 50
