@@ -695,6 +695,12 @@ class JobTracker:
                 log.exception("job init failed")
                 self._finish_job(jip, FAILED, f"init failed: {type(e).__name__}: {e}")
                 return RunningJob(jid, _JTJobHandle(jip), conf)
+            check = getattr(self.scheduler, "check_submission", None)
+            refused = check(jip) if check is not None else None
+            if refused:
+                # the scheduler's job-submission limits (capacity scheduler)
+                self._finish_job(jip, FAILED, refused)
+                return RunningJob(jid, _JTJobHandle(jip), conf)
             dep = conf.get(DEPENDS_KEY)
             dj = self.jobs.get(dep) if dep else None
             if dep and dj is None:

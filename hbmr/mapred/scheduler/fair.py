@@ -17,6 +17,16 @@ min shares first, then by weight, never above a pool's demand; inside a pool
 jobs split equally (fair) or in submit order (fifo).  The most starved job
 (running / share) is served first.
 
+Pools can instead (or as well) be described by the reference's allocation
+file (``mapred.fairscheduler.allocation.file``, see
+:mod:`~hbmr.mapred.scheduler.pools`), reloaded while the JobTracker runs.
+Job limits (FairScheduler.updateRunnability): jobs are made runnable in
+priority/submit order while their pool has fewer than ``maxRunningJobs``
+(``poolMaxJobsDefault``) and their user fewer than the user's
+``maxRunningJobs`` (``userMaxJobsDefault``) runnable jobs; the others get no
+slots until one finishes.  ``maxMaps`` / ``maxGpuMaps`` / ``maxReduces`` cap a
+pool's demand (so its share) per slot kind.
+
 Preemption (FairScheduler.preemptTasksIfNecessary, FairScheduler.java:837),
 with ``mapred.fairscheduler.preemption`` = true: a pool below its min share for
 ``hbmr.fair.pool.<p>.minSharePreemptionTimeout`` seconds (default 60), or below
@@ -29,6 +39,15 @@ CapacityScheduler (contrib/capacity-scheduler): queues
 ``mapred.queue.names`` with ``mapred.capacity-scheduler.queue.<q>.capacity``
 percent and an optional hard ``.maximum-capacity``; a job's queue is
 ``mapred.job.queue.name``.  Unused capacity flows to queues with demand.
+Job limits (CapacitySchedulerQueue.java:378-400, 1227-1345, CapacitySchedulerConf
+keys ``mapred.capacity-scheduler.maximum-system-jobs`` (5000),
+``…queue.<q>.init-accept-jobs-factor`` (10),
+``…queue.<q>.maximum-initialized-active-tasks`` (200000) and
+``…-per-user`` (100000)): a queue initialises at most ceil(system jobs ×
+capacity%) jobs and a user ceil(that × minimum-user-limit%), within the
+active-task limits; uninitialised jobs wait (no slots).  Submission is
+refused when the queue already holds init × factor jobs (user: likewise) or
+a job has more tasks than the per-user active-task limit.
 Inside a queue jobs run in priority/submit order, and each user is capped at
 max(queue share × ``.minimum-user-limit-percent`` / 100, queue share / active
 users) (CapacitySchedulerQueue.java:724 user limits).  Memory matching
@@ -45,6 +64,7 @@ import math
 import time
 
 from .hybrid import HybridTaskScheduler, _prio
+from .pools import INF, PoolManager
 
 log = logging.getLogger("hbmr.scheduler.fair")
 
@@ -85,9 +105,14 @@ def water_fill(total, demands, weights, mins=None):
 class _ShareScheduler(HybridTaskScheduler):
     """Common machinery: per-kind demand/running, shares, starvation order."""
 
+    def admitted(self, jobs):
+        """Jobs allowed to take slots this round (job limits); default all."""
+        return set(jobs)
+
     def begin_round(self, tr, total_cpu, total_gpu):
         jt = self.jt
         self.jobs = [j for j in jt.job_queue if not j.completed()]
+        ok = self.admitted(self.jobs)
         totals = {"gpu": total_gpu * self.queue_depth, "cpu": total_cpu,
                   "reduce": sum(t.status.max_reduce_slots for t in jt.trackers.values()
                                 if not t.blacklisted)}
@@ -99,6 +124,9 @@ class _ShareScheduler(HybridTaskScheduler):
             red_pend = sum(1 for t in j.reduces if not t.is_complete() and not t.is_running()) \
                 if j.maps_complete() else 0
             self.running[j] = {"gpu": j.running_gpu, "cpu": j.running_cpu, "reduce": red_run}
+            if j not in ok:
+                self.demand[j] = {"gpu": 0, "cpu": 0, "reduce": 0}
+                continue
             self.demand[j] = {"gpu": (pend + j.running_gpu) if j.gpu_capable else 0,
                               "cpu": (pend + j.running_cpu) if j.cpu_capable else 0,
                               "reduce": red_pend + red_run}
@@ -130,8 +158,9 @@ class FairScheduler(_ShareScheduler):
     def __init__(self, jt, conf):
         super().__init__(jt, conf)
         self.preemption = conf.get_boolean("mapred.fairscheduler.preemption", False)
-        self.fair_timeout = conf.get_float("mapred.fairscheduler.fairSharePreemptionTimeout",
-                                           600.0)
+        self.pools = PoolManager(conf)
+        self._fair_timeout = conf.get_float("mapred.fairscheduler.fairSharePreemptionTimeout",
+                                            600.0)
         self.preempted = 0
         self._below_min: dict = {}    # (pool, kind) -> since
         self._below_fair: dict = {}
@@ -145,16 +174,42 @@ class FairScheduler(_ShareScheduler):
         prop = self.conf.get("mapred.fairscheduler.poolnameproperty", "user.name")
         return c.get(prop) or c.get_user()
 
+    @property
+    def fair_timeout(self):
+        return self.pools.fair_share_timeout(self._fair_timeout)
+
     def _pool_conf(self, pool, key, default):
-        v = self.conf.get(f"hbmr.fair.pool.{pool}.{key}")
-        return type(default)(v) if v is not None else default
+        return self.pools.pool_value(pool, key, default)
+
+    def admitted(self, jobs):
+        """FairScheduler.updateRunnability: runnable in priority/submit order
+        within the pool's and the user's running-job limits."""
+        self.pools.reload_if_necessary()
+        per_pool: dict = {}
+        per_user: dict = {}
+        ok = set()
+        for j in sorted(jobs, key=lambda j: (_prio(j.priority), j.submit_time)):
+            p, u = self.pool_of(j), j.conf.get_user()
+            if per_pool.get(p, 0) < self.pools.pool_max_jobs(p) and \
+                    per_user.get(u, 0) < self.pools.user_max_jobs(u):
+                per_pool[p] = per_pool.get(p, 0) + 1
+                per_user[u] = per_user.get(u, 0) + 1
+                ok.add(j)
+        self.runnable = ok
+        return ok
 
     def compute_shares(self, kind, total):
         pools: dict = {}
         for j in self.jobs:
             pools.setdefault(self.pool_of(j), []).append(j)
         names = sorted(pools)
-        demands = [sum(self.demand[j][kind] for j in pools[p]) for p in names]
+        maxkey = {"gpu": "maxGpuMaps", "cpu": "maxMaps", "reduce": "maxReduces"}[kind]
+        demands = []
+        for p in names:
+            cap = self._pool_conf(p, maxkey, INF)
+            if kind == "gpu" and cap == INF:
+                cap = self._pool_conf(p, "maxMaps", INF)
+            demands.append(min(sum(self.demand[j][kind] for j in pools[p]), cap))
         weights = [self._pool_conf(p, "weight", 1.0) for p in names]
         minkey = {"gpu": "minGpuMaps", "cpu": "minMaps", "reduce": "minReduces"}[kind]
         mins = [float(self._pool_conf(p, minkey, 0)) for p in names]
@@ -175,6 +230,85 @@ class FairScheduler(_ShareScheduler):
 
 
 class CapacityScheduler(_ShareScheduler):
+    PRE = "mapred.capacity-scheduler.queue"
+
+    def __init__(self, jt, conf):
+        super().__init__(jt, conf)
+        self.initialized: set = set()       # job ids admitted (initialised) so far
+
+    def _limits(self, q):
+        """(maxJobsToInit, maxJobsPerUserToInit, maxActiveTasks,
+        maxActiveTasksPerUser, initToAcceptFactor) of queue ``q``."""
+        c = self.conf
+        names = [x.strip() for x in c.get("mapred.queue.names", "default").split(",") if x.strip()]
+        cap = c.get_float(f"{self.PRE}.{q}.capacity", 100.0 / max(1, len(names)))
+        ul = c.get_float(f"{self.PRE}.{q}.minimum-user-limit-percent", 100.0)
+        sys_jobs = c.get_int("mapred.capacity-scheduler.maximum-system-jobs", 5000)
+        if sys_jobs <= 0:
+            raise ValueError(f"Invalid maximum system jobs: {sys_jobs}")
+        factor = c.get_int(f"{self.PRE}.{q}.init-accept-jobs-factor",
+                           c.get_int("mapred.capacity-scheduler.default-init-accept-jobs-factor",
+                                     10))
+        if factor <= 0:
+            raise ValueError(f"Invalid maximum jobs per user configuration {factor}")
+        tasks = c.get_int(f"{self.PRE}.{q}.maximum-initialized-active-tasks", c.get_int(
+            "mapred.capacity-scheduler.default-maximum-active-tasks-per-queue", 200000))
+        tasks_u = c.get_int(f"{self.PRE}.{q}.maximum-initialized-active-tasks-per-user", c.get_int(
+            "mapred.capacity-scheduler.default-maximum-active-tasks-per-user", 100000))
+        jobs = math.ceil(sys_jobs * cap / 100.0)
+        jobs_u = math.ceil(sys_jobs * cap / 100.0 * ul / 100.0)
+        return jobs, jobs_u, tasks, tasks_u, factor
+
+    @staticmethod
+    def _tasks(j):
+        return len(j.maps) + len(j.reduces)
+
+    def check_submission(self, jip):
+        """CapacitySchedulerQueue.checkJobSubmissionLimits: a refusal reason or None."""
+        q, u = self.queue_of(jip), jip.conf.get_user()
+        jobs, jobs_u, _tasks, tasks_u, factor = self._limits(q)
+        if self._tasks(jip) > tasks_u:
+            return (f"Job '{jip.job_id}' from user '{u}' rejected since it has "
+                    f"{self._tasks(jip)} tasks which exceeds the limit of {tasks_u} tasks "
+                    f"per-user which can be initialized for queue '{q}'")
+        live = [j for j in self.jt.job_queue + [w for ws in self.jt.waiting.values() for w in ws]
+                if not j.completed() and j is not jip and self.queue_of(j) == q]
+        if len(live) >= jobs * factor:
+            return (f"Job '{jip.job_id}' from user '{u}' rejected since queue '{q}' already "
+                    f"has {len(live)} jobs - Exceeds limit of {jobs * factor} jobs to accept")
+        mine = sum(1 for j in live if j.conf.get_user() == u)
+        if mine >= jobs_u * factor:
+            return (f"Job '{jip.job_id}' rejected since user '{u}' already has {mine} jobs - "
+                    f"Exceeds limit of {jobs_u * factor} jobs to accept in queue '{q}'")
+        return None
+
+    def admitted(self, jobs):
+        """JobInitializationPoller + initializeJobForQueue/ForUser: jobs are
+        initialised in priority/submit order within the queue and user job
+        and active-task limits; an initialised job stays so until it ends."""
+        live = {j.job_id for j in jobs}
+        self.initialized &= live
+        ok = set()
+        stats: dict = {}
+        order = sorted(jobs, key=lambda j: (j.job_id not in self.initialized, _prio(j.priority),
+                                            j.submit_time))
+        for j in order:
+            q, u = self.queue_of(j), j.conf.get_user()
+            jobs_q, jobs_u, tasks_q, tasks_u, _f = self._limits(q)
+            st = stats.setdefault(q, {"jobs": 0, "tasks": 0, "ujobs": {}, "utasks": {}})
+            n = self._tasks(j)
+            if j.job_id not in self.initialized:
+                if st["jobs"] >= jobs_q or st["tasks"] + n > tasks_q or \
+                        st["ujobs"].get(u, 0) >= jobs_u or st["utasks"].get(u, 0) + n > tasks_u:
+                    continue
+                self.initialized.add(j.job_id)
+            st["jobs"] += 1
+            st["tasks"] += n
+            st["ujobs"][u] = st["ujobs"].get(u, 0) + 1
+            st["utasks"][u] = st["utasks"].get(u, 0) + n
+            ok.add(j)
+        return ok
+
     def slots_per_task(self, jip, kind):
         """Memory-based slot matching: slots a task of ``jip`` occupies."""
         kk = "reduce" if kind == "reduce" else "map"
