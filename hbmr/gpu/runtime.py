@@ -121,6 +121,8 @@ class GpuRuntime:
         reserve = tracker.conf.get_float("hbmr.gpu.hbm.reserve.gb", 16.0) * (1 << 30)
         for d, dev in self.devices.items():
             tracker.split_cache.capacity[d] = max(0, int(dev.total_mem - reserve))
+        from .split_cache import configure as _configure_split_cache
+        _configure_split_cache(tracker)
         from .gates import Gates
         self.gates = Gates()
 

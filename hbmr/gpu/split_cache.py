@@ -5,7 +5,11 @@ Each tracker keeps the splits its GPU tasks materialised, keyed by
 iteration) find their data already in HBM — "locality" for the scheduler means
 *resident in this GPU's HBM* (SURVEY.md §7 "HBM-resident split sizing").
 Capacity is bounded by ``hbmr.gpu.hbm.reserve.gb`` below the device's free
-memory; eviction is LRU.  The tracker reports additions/evictions in its next
+memory (or set outright by ``hbmr.gpu.split.cache.bytes``); eviction is LRU,
+or with ``hbmr.gpu.split.cache.policy=scan`` a full cache keeps its resident
+splits and streams the rest through (iterative jobs over more data than HBM:
+LRU would miss on every split of every iteration, scan hits on the resident
+fraction).  The tracker reports additions/evictions in its next
 heartbeat so the JobTracker's locality view stays current.
 """
 from __future__ import annotations
@@ -15,7 +19,10 @@ import threading
 
 
 class SplitCache:
-    def __init__(self, capacity_bytes_per_device: dict | None = None):
+    def __init__(self, capacity_bytes_per_device: dict | None = None, policy: str = "lru"):
+        if policy not in ("lru", "scan"):
+            raise ValueError(f"split cache policy must be lru or scan, not {policy!r}")
+        self.policy = policy
         self._lock = threading.Lock()
         self._entries: "collections.OrderedDict[tuple, tuple]" = collections.OrderedDict()
         self._bytes = collections.Counter()
@@ -24,6 +31,7 @@ class SplitCache:
         self.removed: list = []
         self.hits = 0
         self.misses = 0
+        self.bypassed = 0       # splits streamed through without being cached (scan policy)
 
     def get(self, key, device):
         with self._lock:
@@ -42,6 +50,14 @@ class SplitCache:
             if k in self._entries:
                 return
             cap = self.capacity.get(device)
+            if cap is not None and self.policy == "scan" and \
+                    self._bytes[device] + nbytes > cap:
+                # scan-resistant: a data set larger than HBM is read in the same
+                # split order every iteration, where LRU would evict each split
+                # just before its next use (no hits at all); instead the
+                # resident set stays and the overflow streams through
+                self.bypassed += 1
+                return
             if cap is not None:
                 while self._bytes[device] + nbytes > cap:
                     victim = next((kk for kk in self._entries if kk[1] == device), None)
@@ -89,3 +105,17 @@ class SplitCache:
                     _, b = self._entries.pop(k)
                     self._bytes[k[1]] -= b
                     self.removed.append(list(k))
+
+
+def configure(tracker):
+    """Apply the tracker's split-cache keys (capacity override, policy)."""
+    conf = tracker.conf
+    cache = tracker.split_cache
+    cap = conf.get_long("hbmr.gpu.split.cache.bytes", 0)
+    if cap > 0:
+        for d in list(cache.capacity) or [0]:
+            cache.capacity[d] = cap
+    policy = conf.get("hbmr.gpu.split.cache.policy", "lru")
+    if policy not in ("lru", "scan"):
+        raise ValueError(f"hbmr.gpu.split.cache.policy must be lru or scan, not {policy!r}")
+    cache.policy = policy

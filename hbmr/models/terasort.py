@@ -12,16 +12,19 @@ MI355X design:
 
 * map (per split, on its GPU slot): records are generated straight into HBM
   (``teragen:<rows>`` input; the LCG jumps ahead in O(log n), bit-identical to
-  TeraGen) or read from TeraGen files; keys are radix-sorted (10 passes of the
-  native LSD sort), the 100-byte records gathered once, and the splitters
-  cut the sorted split into R runs (offsets only — no per-record partition
-  calls);
+  TeraGen) or read from TeraGen files; one kernel computes every record's
+  key words and range partition (splitters in LDS) and counts the partition
+  sizes, a second scatters (key words, record number) into partition order
+  (20 B per record; the 100-byte records stay where they are);
 * shuffle: one all-to-all-v per tracker over RCCL/xGMI (each GPU owns a
   contiguous range of partitions) — the HTTP shuffle + merge of the
   reference (ReduceTask.java:1231-2514) disappears;
-* reduce (collective, one per tracker): radix-sort the received runs, verify
+* reduce (collective, one per tracker): per group of consecutive partitions,
+  collect the pieces every map produced, radix-sort the keys (8 passes over
+  the high 8 key bytes, runs of equal high words ordered by the last 2 bytes),
+  gather the 100-byte records once (4 records in flight per lane), verify
   order locally and against the neighbouring ranks' boundary keys
-  (TeraValidate), write ``part-NNNNN`` files if an output directory is set.
+  (TeraValidate), and write ``part-NNNNN`` files if an output directory is set.
 
 CPU slots run the same steps with numpy (hbmr.ops.sort CPU twins).
 """
@@ -102,6 +105,10 @@ class TeraSortSplitJob(SplitJob):
         # record bytes per sort (bigger sorts run the radix passes at full
         # occupancy; the working set is 1.4x the group)
         self.group_bytes = conf.get_long("hbmr.terasort.reduce.group.bytes", 8 << 30)
+        # several ranks: each sender sorts every destination's run before the
+        # all-to-all and receivers merge the W sorted runs (K8 merge path,
+        # log2 W passes) instead of re-sorting what they received
+        self.sorted_runs = conf.get_boolean("hbmr.terasort.shuffle.sorted.runs", False)
 
     # -- splits + sampling (JobTracker side) -----------------------------------------
     def _ranges(self):
@@ -191,21 +198,11 @@ class TeraSortSplitJob(SplitJob):
         nparts = data["nparts"]
         shi, slo = _parse_keys(data["splitters"]) if nparts > 1 else (
             torch.zeros(0, dtype=torch.int64), torch.zeros(0, dtype=torch.int64))
-        hi, lo, pid = S.tera_keys_part(recs, shi, slo, stream=stream)
         n = recs.shape[0]
-        row = torch.arange(n, dtype=torch.int32, device=recs.device)
-        if nparts > 1:
-            bits = max(1, int(math.ceil(math.log2(nparts))))
-            S.radix_sort_pairs(pid, row, 0, min(64, 8 * ((bits + 7) // 8)), stream=stream)
-            hp, lp = S.gather_u64(hi, row, stream=stream), S.gather_u64(lo, row, stream=stream)
-        else:
-            hp, lp = hi, lo
-        counts = torch.bincount(pid, minlength=nparts) if n else \
-            torch.zeros(nparts, dtype=torch.int64, device=recs.device)
-        offs = torch.zeros(nparts + 1, dtype=torch.int64, device=recs.device)
-        torch.cumsum(counts, 0, out=offs[1:])
+        # key words + partition + partition sizes, scan, one tile-ranked scatter
+        hp, lp, row, offs = S.tera_partition(recs, shi, slo, stream=stream)
         # order-independent checksum of the input keys, kept on the device
-        csum = hi.sum() + lo.sum()
+        csum = hp.sum() + lp.sum()
         ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, n)
         ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_OUTPUT_RECORDS, n)
         return {"records": recs, "hi": hp, "lo": lp, "row": row, "offsets": offs,
@@ -240,14 +237,26 @@ class TeraSortSplitJob(SplitJob):
         dev = ctx.device if ctx.device is not None else torch.device("cpu")
         nparts = combined["nparts"]
         csum_in = combined["checksum"]
-        csum_in = int(csum_in.item()) if torch.is_tensor(csum_in) else int(csum_in)
-        if comm.world_size == 1:
-            stats = self._reduce_local(ctx, outs, combined["offsets"], nparts or 1, dev)
-        else:
-            stats = self._reduce_shuffle(ctx, outs, combined["offsets"], nparts, dev)
-        n, bad, csum_here, first, last = stats
-        meta = torch.tensor([n, _s64(csum_in), _s64(csum_here), bad, first[0], first[1], last[0],
-                             last[1]], dtype=torch.int64)
+        if self.out:
+            self._open_output(ctx)
+        try:
+            if comm.world_size == 1:
+                stats = self._reduce_local(ctx, outs, combined["offsets"], nparts or 1, dev)
+            else:
+                stats = self._reduce_shuffle(ctx, outs, combined["offsets"], nparts, dev)
+        finally:
+            self._close_output(ctx)
+        # one device->host copy of this rank's statistics (no per-value syncs)
+        n, st = stats
+        if not torch.is_tensor(csum_in):
+            csum_in = torch.tensor(_s64(int(csum_in)), dtype=torch.int64)
+        if st is None:
+            st = torch.tensor([0, 0, -1, -1, -1, -1], dtype=torch.int64)
+        meta = torch.cat([torch.tensor([n], dtype=torch.int64),
+                          csum_in.reshape(1).to("cpu", torch.int64), st.to("cpu")])
+        meta = torch.stack([meta[0], meta[1], meta[3], meta[2], meta[4], meta[5], meta[6],
+                            meta[7]])
+        bad = int(meta[3])
         gathered = comm.all_gather(meta)
         total = sum(int(g[0]) for g in gathered)
         c_in = sum(int(g[1]) for g in gathered)
@@ -282,7 +291,7 @@ class TeraSortSplitJob(SplitJob):
         their counts), so peak HBM is the input splits + 20 B/record of map
         output + one group."""
         if not outs:
-            return 0, 0, 0, (-1, -1), (-1, -1)
+            return 0, None
         his = [o["hi"] for o in outs]
         los = [o["lo"] for o in outs]
         rows = [o["row"] for o in outs]
@@ -322,11 +331,13 @@ class TeraSortSplitJob(SplitJob):
             if self.out:
                 at = 0
                 for p in range(pa, pb):
-                    self._write_part(p, recs[at:at + int(sizes[p])])
+                    self._write_part(ctx, p, recs[at:at + int(sizes[p])])
                     at += int(sizes[p])
             del recs, hs, ls
-        fl = torch.cat([first[0], first[1], last[0], last[1]]).to("cpu").tolist()
-        return n, int(bad.item()), int(csum.item()), (fl[0], fl[1]), (fl[2], fl[3])
+        if first is None:
+            return 0, None
+        return n, torch.cat([bad.reshape(1), csum.reshape(1), first[0], first[1], last[0],
+                             last[1]])
 
     def _reduce_shuffle(self, ctx, outs, offs, nparts, dev):
         """world > 1: every rank gathers the records of each destination's
@@ -356,35 +367,48 @@ class TeraSortSplitJob(SplitJob):
                     spl = (g[1:1 + k], g[1 + k:])
                     break
         counts = [0] * W
-        splits, rowsl = [], []
+        splits, rowsl, perms = [], [], []
         if outs:
+            his = [o["hi"] for o in outs]
+            los = [o["lo"] for o in outs]
             rows = [o["row"] for o in outs]
             bases = [o["records"] for o in outs]
+            at = 0
             for d in range(W):
                 a, b = self.owner_range(d, W, nparts)
                 starts = offs[:, a]
                 lens = offs[:, b] - offs[:, a]
                 counts[d] = int(lens.sum())
                 if counts[d]:
-                    _h, _l, sp, rw = S.tera_collect(None, None, rows, starts, lens, with_keys=False)
+                    h, lw, sp, rw = S.tera_collect(his, los, rows, starts, lens,
+                                                   with_keys=self.sorted_runs)
+                    if self.sorted_runs:
+                        perm, _hs, _ls = S.sort_keys(h, lw)
+                        perms.append(perm + at)
+                        del h, lw, _hs, _ls
                     splits.append(sp)
                     rowsl.append(rw)
+                    at += counts[d]
             if splits:
-                send = S.gather_records_multi(bases, torch.cat(splits), torch.cat(rowsl))
+                send = S.gather_records_multi(bases, torch.cat(splits), torch.cat(rowsl),
+                                              torch.cat(perms) if perms else None)
             else:
                 send = torch.empty(0, S.RECORD, dtype=torch.uint8, device=dev)
-            del splits, rowsl
+            del splits, rowsl, perms
         else:
             send = torch.empty(0, S.RECORD, dtype=torch.uint8, device=dev)
-        recv, _ = comm.all_to_all_v(send, counts)
+        recv, rcounts = comm.all_to_all_v(send, counts)
         del send
         if recv.shape[0] == 0:
-            return 0, 0, 0, (-1, -1), (-1, -1)
-        srt, hs, ls = S.sort_records(recv)
+            return 0, None
+        if self.sorted_runs:
+            srt, hs, ls = self._merge_received(recv, rcounts)
+        else:
+            srt, hs, ls = S.sort_records(recv)
         del recv
-        bad = S.count_unsorted(hs, ls)
-        csum_here = int(hs.sum().item()) + int(ls.sum().item())
         n = int(srt.shape[0])
+        st = torch.cat([S.count_unsorted_dev(hs, ls).reshape(1),
+                        (hs.sum() + ls.sum()).reshape(1), hs[:1], ls[:1], hs[-1:], ls[-1:]])
         if self.out:
             a, b = self.owner_range(me, W, nparts)
             if b - a > 1:
@@ -397,18 +421,127 @@ class TeraSortSplitJob(SplitJob):
             else:
                 cut = [0, n]
             for i, p in enumerate(range(a, b)):
-                self._write_part(p, srt[cut[i]:cut[i + 1]])
-        fl = torch.stack([hs[0], ls[0], hs[-1], ls[-1]]).to("cpu").tolist()
-        return n, bad, csum_here, (fl[0], fl[1]), (fl[2], fl[3])
+                self._write_part(ctx, p, srt[cut[i]:cut[i + 1]])
+        return n, st
+
+    @staticmethod
+    def _merge_received(recv, rcounts):
+        """recv holds one sorted run per source rank: merge them (K8)."""
+        hi, lo = S.tera_keys(recv)
+        runs, at = [], 0
+        for c in rcounts:
+            if c:
+                idx = torch.arange(at, at + c, dtype=torch.int32, device=recv.device)
+                runs.append((hi[at:at + c], lo[at:at + c], idx))
+            at += c
+        hs, ls, perm = S.merge_runs(runs)
+        return S.gather_records(recv, perm), hs, ls
 
     def _splitters_of(self, outs):
         if not outs:
             raise RuntimeError("writing several partitions needs the splitters of a local map")
         return outs[0]["splitters"]
 
-    def _write_part(self, p, recs):
-        os.makedirs(self.out, exist_ok=True)
-        recs.to("cpu").numpy().tofile(os.path.join(self.out, f"part-{p:05d}"))
+    # -- output (TeraOutputFormat + FileOutputCommitter) ---------------------------------
+    def _open_output(self, ctx):
+        """Part files go to the attempt's work directory and are committed
+        (renamed into the output directory) when the reduce ends
+        (FileOutputCommitter); ``terasort.final.sync`` (TeraSort sets it)
+        fsyncs every part before it is closed (TeraOutputFormat.java:63-75)."""
+        from ..mapred.committer import FileOutputCommitter
+        com = FileOutputCommitter()
+        attempt = getattr(ctx, "attempt_id", None) or "attempt_local_r_000000_0"
+        com.setup_task(self.conf, attempt)
+        dev = getattr(ctx, "device", None)
+        ctx.tera_out = (com, attempt, com.work_path(self.conf, attempt),
+                        _PartWriter(dev, self.conf.get_boolean("terasort.final.sync", True)))
+
+    def _write_part(self, ctx, p, recs):
+        _com, _att, workdir, pw = ctx.tera_out
+        pw.write(os.path.join(workdir, f"part-{p:05d}"), recs)
+
+    def _close_output(self, ctx):
+        out = getattr(ctx, "tera_out", None)
+        if out is None:
+            return
+        ctx.tera_out = None
+        com, attempt, _wd, pw = out
+        pw.close()
+        if com.needs_task_commit(self.conf, attempt):
+            com.commit_task(self.conf, attempt)
+
+    def job_succeeded(self, jip):
+        if self.out:
+            from ..mapred.committer import FileOutputCommitter
+            FileOutputCommitter().commit_job(jip.conf)
+
+
+class _PartWriter:
+    """Streams device record runs to files: chunks are copied into two pinned
+    host buffers on a copy stream while a writer thread writes the previous
+    chunk, so D2H (≈50 GB/s) and file writes overlap; CPU tensors are written
+    directly."""
+
+    CHUNK = 256 << 20
+
+    def __init__(self, device, final_sync):
+        import concurrent.futures as cf
+        self.sync = final_sync
+        self.pool = cf.ThreadPoolExecutor(1, thread_name_prefix="tera-out")
+        self.cuda = device is not None and getattr(device, "type", "") == "cuda"
+        self.bufs = self.events = None
+        self.pending = [None, None]
+        self.k = 0
+        if self.cuda:
+            self.bufs = [torch.empty(self.CHUNK, dtype=torch.uint8, pin_memory=True)
+                         for _ in range(2)]
+            self.stream = torch.cuda.Stream(device)
+        self.files = []
+
+    def _wait(self, i):
+        if self.pending[i] is not None:
+            self.pending[i].result()
+            self.pending[i] = None
+
+    def write(self, path, recs):
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        f = open(path, "wb")
+        self.files.append(f)
+        flat = recs.reshape(-1)
+        if not self.cuda or not flat.is_cuda:
+            self.pool.submit(lambda a=flat.numpy().copy(): a.tofile(f)).result()
+            return
+        self.stream.wait_stream(torch.cuda.current_stream(flat.device))
+        flat.record_stream(self.stream)
+        for off in range(0, flat.numel(), self.CHUNK):
+            c = min(self.CHUNK, flat.numel() - off)
+            i = self.k % 2
+            self.k += 1
+            self._wait(i)
+            buf = self.bufs[i]
+            with torch.cuda.stream(self.stream):
+                buf[:c].copy_(flat[off:off + c], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.stream)
+
+            def put(ev=ev, view=buf[:c], f=f):
+                ev.synchronize()
+                f.write(memoryview(view.numpy()))
+            self.pending[i] = self.pool.submit(put)
+
+    def close(self):
+        for i in range(2):
+            self._wait(i)
+
+        def fin():
+            for f in self.files:
+                f.flush()
+                if self.sync:
+                    os.fsync(f.fileno())
+                f.close()
+        self.pool.submit(fin).result()
+        self.pool.shutdown()
+        self.files = []
 
 
 def terasort_conf(base=None, rows=1_000_000, split_rows=None, output=None, inp=None,

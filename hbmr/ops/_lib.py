@@ -78,6 +78,12 @@ _SIGS = {
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "hbmr_gather_records_multi": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int,
                                           c_void_p, c_void_p]),
+    "hbmr_tera_partition_workspace_bytes": (c_long, [c_long, c_int]),
+    "hbmr_merge_path": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p,
+                                c_long, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "hbmr_tera_tie_fix": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p]),
+    "hbmr_tera_partition": (c_int, [c_void_p, c_long, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p]),
     # text / WordCount (native/kernels/text.hip)
     "hbmr_wc_tiles": (c_long, [c_long]),
     "hbmr_wc_tokenize_count": (c_int, [c_void_p, c_long, c_void_p, c_void_p]),

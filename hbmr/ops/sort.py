@@ -18,6 +18,9 @@ from . import _lib
 
 RECORD = 100
 KEY = 10
+# HBMR_TERA_SORT80=1: always the full 10-pass 80-bit key sort (A/B of the
+# hi-only sort + tie fix-up)
+_SORT80 = __import__("os").environ.get("HBMR_TERA_SORT80") == "1"
 
 
 def _ptr(t):
@@ -179,6 +182,23 @@ def sort_keys(hi: torch.Tensor, lo: torch.Tensor, stream=None):
         return (torch.from_numpy(order), torch.from_numpy(h[order].view(np.int64).copy()),
                 torch.from_numpy(lw[order].view(np.int64).copy()))
     lib = _lib.load()
+    if not _SORT80:
+        # 8 passes over hi only, lo gathered, then runs of equal hi (rare: hi
+        # holds 8 of the 10 key bytes) ordered by lo in place; a run longer
+        # than the fix-up handles falls back to the full 80-bit sort below
+        perm = torch.arange(n, dtype=torch.int32, device=hi.device)
+        hi_k = hi.clone()
+        radix_sort_pairs(hi_k, perm, 0, 64, stream=stream)
+        lo_s = torch.empty_like(lo)
+        rc = lib.hbmr_gather_u64(_ptr(lo), _ptr(perm), n, _ptr(lo_s), _lib.stream_handle(stream))
+        _lib.check(rc, "hbmr_gather_u64")
+        flag = torch.zeros(1, dtype=torch.int32, device=hi.device)
+        rc = lib.hbmr_tera_tie_fix(_ptr(hi_k), _ptr(lo_s), _ptr(perm), n, _ptr(flag),
+                                   _lib.stream_handle(stream))
+        _lib.check(rc, "hbmr_tera_tie_fix")
+        if not int(flag.item()):
+            return perm, hi_k, lo_s
+        del perm, hi_k, lo_s
     # LSD: 2 passes over the low 16 bits, then 8 over the high 64 (stable)
     lo_k = lo.clone()
     perm = torch.arange(n, dtype=torch.int32, device=hi.device)
@@ -285,6 +305,79 @@ def tera_keys_part(records: torch.Tensor, split_hi: torch.Tensor, split_lo: torc
         tie = h == sh[j]
         pid[tie & (lw >= sl[j])] = np.maximum(pid[tie & (lw >= sl[j])], j + 1)
     return hi, lo, torch.from_numpy(pid)
+
+
+def tera_partition(records: torch.Tensor, split_hi: torch.Tensor, split_lo: torch.Tensor,
+                   stream=None):
+    """Range-partition a split: (hi, lo, row, offsets) — key words and record
+    numbers in partition order (order inside a partition unspecified) and
+    offsets[R+1] of the R = #splitters + 1 partitions (int64, on the records'
+    device).  On the GPU: one key/partition/count kernel, an on-device scan and
+    one tile-ranked scatter (no sort, no gathers)."""
+    n, stride = records.shape
+    ns = split_hi.numel()
+    nparts = ns + 1
+    if not _on_gpu(records):
+        hi, lo, pid = tera_keys_part(records, split_hi, split_lo)
+        order = torch.from_numpy(np.argsort(pid.numpy(), kind="stable"))
+        counts = torch.bincount(pid, minlength=nparts)
+        offs = torch.zeros(nparts + 1, dtype=torch.int64)
+        torch.cumsum(counts, 0, out=offs[1:])
+        return hi[order], lo[order], order.to(torch.int32), offs
+    if ns > 4096:
+        raise ValueError("at most 4096 splitters (4097 partitions)")
+    dev = records.device
+    lib = _lib.load()
+    hi = torch.empty(n, dtype=torch.int64, device=dev)
+    lo = torch.empty(n, dtype=torch.int64, device=dev)
+    row = torch.empty(n, dtype=torch.int32, device=dev)
+    offs = torch.empty(nparts + 1, dtype=torch.int64, device=dev)
+    wsb = int(lib.hbmr_tera_partition_workspace_bytes(n, nparts))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    sh = split_hi.to(dev)
+    sl = split_lo.to(dev)
+    rc = lib.hbmr_tera_partition(_ptr(records), n, stride, _ptr(sh) if ns else None,
+                                 _ptr(sl) if ns else None, ns, _ptr(hi), _ptr(lo), _ptr(row),
+                                 _ptr(offs), _ptr(ws), wsb, _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_tera_partition")
+    return hi, lo, row, offs
+
+
+def merge_runs(runs, stream=None):
+    """K8: merge sorted runs [(hi, lo, val)] (keys uint64 in int64 storage, val
+    int32; each run sorted by (hi, lo)) into one sorted (hi, lo, val) — a
+    pairwise merge-path tree, log2(#runs) passes; stable (earlier runs first
+    on equal keys)."""
+    runs = [r for r in runs if r[0].numel()]
+    if not runs:
+        return (torch.empty(0, dtype=torch.int64), torch.empty(0, dtype=torch.int64),
+                torch.empty(0, dtype=torch.int32))
+    if not _on_gpu(runs[0][0]):
+        h = torch.cat([r[0] for r in runs]).numpy().view(np.uint64)
+        lw = torch.cat([r[1] for r in runs]).numpy().view(np.uint64)
+        v = torch.cat([r[2] for r in runs])
+        order = np.lexsort((np.arange(h.size), lw, h))     # stable: run order on ties
+        o = torch.from_numpy(order)
+        return (torch.from_numpy(h[order].view(np.int64).copy()),
+                torch.from_numpy(lw[order].view(np.int64).copy()), v[o])
+    lib = _lib.load()
+    while len(runs) > 1:
+        nxt = []
+        for i in range(0, len(runs) - 1, 2):
+            (ah, al, av), (bh, bl, bv) = runs[i], runs[i + 1]
+            n = ah.numel() + bh.numel()
+            oh = torch.empty(n, dtype=torch.int64, device=ah.device)
+            ol = torch.empty(n, dtype=torch.int64, device=ah.device)
+            ov = torch.empty(n, dtype=torch.int32, device=ah.device)
+            rc = lib.hbmr_merge_path(_ptr(ah), _ptr(al), _ptr(av), ah.numel(), _ptr(bh), _ptr(bl),
+                                     _ptr(bv), bh.numel(), _ptr(oh), _ptr(ol), _ptr(ov),
+                                     _lib.stream_handle(stream))
+            _lib.check(rc, "hbmr_merge_path")
+            nxt.append((oh, ol, ov))
+        if len(runs) % 2:
+            nxt.append(runs[-1])
+        runs = nxt
+    return runs[0]
 
 
 def _ptr_table(ts, device):

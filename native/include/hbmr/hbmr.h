@@ -80,8 +80,17 @@ int hbmr_tera_collect(const uint64_t* const* his, const uint64_t* const* los,
 int hbmr_gather_records_multi(const void* const* bases, const uint32_t* split, const uint32_t* row,
                               const uint32_t* perm, long n, int record_bytes, void* dst,
                               hipStream_t st);
+int hbmr_merge_path(const uint64_t* ahi, const uint64_t* alo, const uint32_t* av, long na,
+                    const uint64_t* bhi, const uint64_t* blo, const uint32_t* bv, long nb,
+                    uint64_t* ohi, uint64_t* olo, uint32_t* ov, hipStream_t st);
+int hbmr_tera_tie_fix(const uint64_t* hi, uint64_t* lo, uint32_t* perm, long n,
+                      unsigned int* flag, hipStream_t st);
+int hbmr_tera_partition(const void* records, long n, int stride, const uint64_t* shi,
+                        const uint64_t* slo, int nsplit, uint64_t* ohi, uint64_t* olo,
+                        uint32_t* orow, long* offsets, void* ws, long ws_bytes, hipStream_t st);
 #endif
 long hbmr_radix_sort_workspace_bytes(long n);
+long hbmr_tera_partition_workspace_bytes(long n, int nparts);
 
 // ---- GEMM (native/kernels/gemm.hip) -------------------------------------------
 #ifndef HBMR_NO_HIP_DECLS

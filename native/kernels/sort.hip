@@ -543,6 +543,246 @@ __global__ __launch_bounds__(256) void gather_records_multi_kernel(
   }
 }
 
+// ---- TeraSort map v3: partition without a sort ------------------------------
+// (A) key words + partition id of every record, and the partition sizes: a
+// per-workgroup LDS histogram flushed with one global add per touched bin.
+__global__ __launch_bounds__(256) void tera_part_count_kernel(
+    const uint8_t* __restrict__ rec, long n, int stride, const uint64_t* __restrict__ shi,
+    const uint64_t* __restrict__ slo, int nsplit, uint64_t* __restrict__ hi,
+    uint64_t* __restrict__ lo, uint16_t* __restrict__ pid, unsigned int* __restrict__ counts) {
+  __shared__ uint64_t s_hi[kMaxSplitters];
+  __shared__ uint16_t s_lo[kMaxSplitters];
+  __shared__ unsigned int s_cnt[kMaxSplitters + 1];
+  const int nparts = nsplit + 1;
+  for (int j = threadIdx.x; j < nsplit; j += 256) {
+    s_hi[j] = shi[j];
+    s_lo[j] = (uint16_t)slo[j];
+  }
+  for (int j = threadIdx.x; j < nparts; j += 256) s_cnt[j] = 0u;
+  __syncthreads();
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const uint8_t* r = rec + i * stride;
+    uint64_t h = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) h = (h << 8) | r[j];
+    const uint32_t l = ((uint32_t)r[8] << 8) | r[9];
+    int a = 0, b = nsplit;
+    while (a < b) {
+      const int m = (a + b) >> 1;
+      const bool le = s_hi[m] < h || (s_hi[m] == h && s_lo[m] <= l);
+      if (le) a = m + 1; else b = m;
+    }
+    hi[i] = h;
+    lo[i] = l;
+    pid[i] = (uint16_t)a;
+    atomicAdd(&s_cnt[a], 1u);
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < nparts; j += 256)
+    if (s_cnt[j]) atomicAdd(&counts[j], s_cnt[j]);
+}
+
+// exclusive scan of the partition sizes (one workgroup; nparts <= 4097)
+__global__ __launch_bounds__(1024) void tera_part_offsets_kernel(
+    const unsigned int* __restrict__ counts, int nparts, unsigned int* __restrict__ cursor,
+    long* __restrict__ offsets) {
+  __shared__ long s_w[16];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  constexpr int kPer = 5;   // 1024 * 5 >= 4097
+  long v[kPer], sum = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int idx = t * kPer + j;
+    v[j] = idx < nparts ? (long)counts[idx] : 0;
+    sum += v[j];
+  }
+  long x = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const long u = __shfl_up(x, o);
+    if (lane >= o) x += u;
+  }
+  if (lane == 63) s_w[w] = x;
+  __syncthreads();
+  long run = x - sum;
+  for (int i = 0; i < w; ++i) run += s_w[i];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int idx = t * kPer + j;
+    if (idx < nparts) {
+      offsets[idx] = run;
+      cursor[idx] = (unsigned int)run;
+    }
+    run += v[j];
+    if (idx == nparts - 1) offsets[nparts] = run;
+  }
+}
+
+// (B) scatter (hi, lo, row) into partition order.  Each workgroup takes a tile
+// of kSortTile records, ranks them per partition in LDS, reserves one range per
+// touched partition from the global cursors, and writes.  Order inside a
+// partition follows the reservation order (the reduce sorts by key anyway).
+__global__ __launch_bounds__(kSortThreads) void tera_part_scatter_kernel(
+    const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo,
+    const uint16_t* __restrict__ pid, long n, int nparts, unsigned int* __restrict__ cursor,
+    uint64_t* __restrict__ ohi, uint64_t* __restrict__ olo, uint32_t* __restrict__ orow) {
+  __shared__ unsigned int s_cnt[kMaxSplitters + 1];
+  const int t = threadIdx.x;
+  const long base = (long)blockIdx.x * kSortTile;
+  for (int j = t; j < nparts; j += kSortThreads) s_cnt[j] = 0u;
+  __syncthreads();
+  unsigned int loc[kSortItems];
+  uint16_t p[kSortItems];
+#pragma unroll
+  for (int i = 0; i < kSortItems; ++i) {
+    const long e = base + (long)i * kSortThreads + t;
+    if (e < n) {
+      p[i] = pid[e];
+      loc[i] = atomicAdd(&s_cnt[p[i]], 1u);
+    }
+  }
+  __syncthreads();
+  for (int j = t; j < nparts; j += kSortThreads) {
+    const unsigned int c = s_cnt[j];
+    s_cnt[j] = c ? atomicAdd(&cursor[j], c) : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kSortItems; ++i) {
+    const long e = base + (long)i * kSortThreads + t;
+    if (e < n) {
+      const long d = (long)s_cnt[p[i]] + loc[i];
+      ohi[d] = hi[e];
+      olo[d] = lo[e];
+      orow[d] = (uint32_t)e;
+    }
+  }
+}
+
+// dst record i = record row[k] of split split[k], k = perm ? perm[i] : i, with
+// U records per lane in flight: the index loads of all U records are issued,
+// then their words, then the stores, so each lane keeps U independent random
+// reads outstanding (the v1 loop waited on one record at a time).  Lane t
+// moves word t % words of record t / words; iteration j of a block covers
+// records r0 + j * stride, so the stores of every j stay coalesced.
+template <int U>
+__global__ __launch_bounds__(256) void gather_records_multi_v3_kernel(
+    const uint32_t* const* __restrict__ bases, const uint32_t* __restrict__ split,
+    const uint32_t* __restrict__ row, const uint32_t* __restrict__ perm, long n, int words,
+    uint32_t* __restrict__ dst) {
+  const int rpb = 256 / words;
+  const int t = threadIdx.x;
+  if (t >= rpb * words) return;
+  const int lr = t / words;
+  const int w = t - lr * words;
+  const long stride = (long)gridDim.x * rpb;
+  for (long r0 = (long)blockIdx.x * rpb + lr; r0 < n; r0 += stride * U) {
+    const uint32_t* src[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const long r = r0 + j * stride;
+      src[j] = nullptr;
+      if (r < n) {
+        const long k = perm ? (long)perm[r] : r;
+        src[j] = bases[split[k]] + (long)row[k] * words;
+      }
+    }
+    uint32_t v[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) v[j] = src[j] ? src[j][w] : 0u;
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const long r = r0 + j * stride;
+      if (r < n) dst[r * words + w] = v[j];
+    }
+  }
+}
+
+// After a sort by hi only: order each run of equal hi by lo (insertion sort,
+// carrying perm).  Runs are rare for TeraSort keys (8 of 10 key bytes in hi);
+// a run longer than kTieRun is left alone and flagged, and the caller falls
+// back to the full 80-bit sort.
+constexpr int kTieRun = 64;
+
+__global__ __launch_bounds__(256) void tera_tie_fix_kernel(const uint64_t* __restrict__ hi,
+                                                           uint64_t* __restrict__ lo,
+                                                           uint32_t* __restrict__ perm, long n,
+                                                           unsigned int* __restrict__ flag) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n - 1) return;
+  const uint64_t h = hi[i];
+  if (hi[i + 1] != h || (i > 0 && hi[i - 1] == h)) return;   // not the start of a run
+  long e = i + 1;
+  while (e < n && hi[e] == h && e - i < kTieRun) ++e;
+  if (e < n && hi[e] == h) {
+    atomicOr(flag, 1u);
+    return;
+  }
+  for (long a = i + 1; a < e; ++a) {
+    const uint64_t kl = lo[a];
+    const uint32_t kp = perm[a];
+    long b = a - 1;
+    while (b >= i && lo[b] > kl) {
+      lo[b + 1] = lo[b];
+      perm[b + 1] = perm[b];
+      --b;
+    }
+    lo[b + 1] = kl;
+    perm[b + 1] = kp;
+  }
+}
+
+// ---- K8: merge of sorted runs (merge path) -----------------------------------
+// Merge two sorted runs A[0,na) and B[0,nb) of (hi, lo) keys with u32 payloads
+// (stable: A before B on equal keys).  Thread t owns output [t*kMergeItems,
+// (t+1)*kMergeItems): it finds where that diagonal crosses the merge path by
+// binary search, then merges its items sequentially.  Runs are bound by HBM
+// bandwidth (each element read once, written once; the search touches
+// log2(n) elements per thread).
+constexpr int kMergeItems = 16;
+
+__device__ __forceinline__ bool key_lt(uint64_t ah, uint64_t al, uint64_t bh, uint64_t bl) {
+  return ah < bh || (ah == bh && al < bl);
+}
+
+__global__ __launch_bounds__(256) void merge_path_kernel(
+    const uint64_t* __restrict__ ahi, const uint64_t* __restrict__ alo,
+    const uint32_t* __restrict__ av, long na, const uint64_t* __restrict__ bhi,
+    const uint64_t* __restrict__ blo, const uint32_t* __restrict__ bv, long nb,
+    uint64_t* __restrict__ ohi, uint64_t* __restrict__ olo, uint32_t* __restrict__ ov) {
+  const long n = na + nb;
+  const long d = ((long)blockIdx.x * 256 + threadIdx.x) * kMergeItems;
+  if (d >= n) return;
+  // largest i in [max(0, d-nb), min(d, na)] with A[i-1] <= B[d-i] (A wins ties)
+  long lo_i = d > nb ? d - nb : 0, hi_i = d < na ? d : na;
+  while (lo_i < hi_i) {
+    const long i = (lo_i + hi_i + 1) >> 1;
+    const long j = d - i;
+    // i is feasible iff A[i-1] <= B[j] (j < nb) — i.e. not B[j] < A[i-1]
+    if (j >= nb || !key_lt(bhi[j], blo[j], ahi[i - 1], alo[i - 1])) lo_i = i;
+    else hi_i = i - 1;
+  }
+  long i = lo_i, j = d - lo_i;
+  const long end = d + kMergeItems < n ? d + kMergeItems : n;
+  for (long o = d; o < end; ++o) {
+    bool take_a;
+    if (i >= na) take_a = false;
+    else if (j >= nb) take_a = true;
+    else take_a = !key_lt(bhi[j], blo[j], ahi[i], alo[i]);
+    if (take_a) {
+      ohi[o] = ahi[i];
+      olo[o] = alo[i];
+      ov[o] = av[i];
+      ++i;
+    } else {
+      ohi[o] = bhi[j];
+      olo[o] = blo[j];
+      ov[o] = bv[j];
+      ++j;
+    }
+  }
+}
+
 inline long ceil_div(long a, long b) { return (a + b - 1) / b; }
 
 }  // namespace
@@ -676,16 +916,83 @@ int hbmr_tera_collect(const uint64_t* const* his, const uint64_t* const* los,
   return (int)hipGetLastError();
 }
 
+// TeraSort map v3: (hi, lo, row) of n records in partition order and the
+// partition boundaries offsets[0..nparts] (int64, device).  ws: device scratch
+// of hbmr_tera_partition_workspace_bytes(n, nparts) bytes.
+long hbmr_tera_partition_workspace_bytes(long n, int nparts) {
+  return n * 8 * 2 + n * 2 + 2L * (nparts + 1) * 4 + 64;
+}
+
+int hbmr_tera_partition(const void* records, long n, int stride, const uint64_t* shi,
+                        const uint64_t* slo, int nsplit, uint64_t* ohi, uint64_t* olo,
+                        uint32_t* orow, long* offsets, void* ws, long ws_bytes, hipStream_t st) {
+  const int nparts = nsplit + 1;
+  if (nsplit < 0 || nsplit > kMaxSplitters) return (int)hipErrorInvalidValue;
+  if (n < 0 || n >= (1L << 32)) return (int)hipErrorInvalidValue;
+  if (ws_bytes < hbmr_tera_partition_workspace_bytes(n, nparts)) return (int)hipErrorInvalidValue;
+  uint8_t* p = reinterpret_cast<uint8_t*>(ws);
+  uint64_t* hi = reinterpret_cast<uint64_t*>(p);
+  uint64_t* lo = hi + n;
+  uint16_t* pid = reinterpret_cast<uint16_t*>(lo + n);
+  unsigned int* counts = reinterpret_cast<unsigned int*>(
+      (reinterpret_cast<uintptr_t>(pid + n) + 15) & ~uintptr_t(15));
+  unsigned int* cursor = counts + (nparts + 1);
+  HBMR_RETURN_IF_ERROR(hipMemsetAsync(counts, 0, (size_t)(nparts + 1) * 4, st));
+  if (n > 0) {
+    const long grid = std::min<long>(ceil_div(n, 256), 256L * 64);
+    hipLaunchKernelGGL(tera_part_count_kernel, dim3((unsigned)grid), dim3(256), 0, st,
+                       reinterpret_cast<const uint8_t*>(records), n, stride, shi, slo, nsplit, hi,
+                       lo, pid, counts);
+  }
+  hipLaunchKernelGGL(tera_part_offsets_kernel, dim3(1), dim3(1024), 0, st, counts, nparts, cursor,
+                     offsets);
+  if (n > 0)
+    hipLaunchKernelGGL(tera_part_scatter_kernel, dim3((unsigned)ceil_div(n, kSortTile)),
+                       dim3(kSortThreads), 0, st, hi, lo, pid, n, nparts, cursor, ohi, olo, orow);
+  return (int)hipGetLastError();
+}
+
+int hbmr_tera_tie_fix(const uint64_t* hi, uint64_t* lo, uint32_t* perm, long n,
+                      unsigned int* flag, hipStream_t st) {
+  if (n <= 1) return 0;
+  hipLaunchKernelGGL(tera_tie_fix_kernel, dim3((unsigned)ceil_div(n - 1, 256)), dim3(256), 0, st,
+                     hi, lo, perm, n, flag);
+  return (int)hipGetLastError();
+}
+
+int hbmr_merge_path(const uint64_t* ahi, const uint64_t* alo, const uint32_t* av, long na,
+                    const uint64_t* bhi, const uint64_t* blo, const uint32_t* bv, long nb,
+                    uint64_t* ohi, uint64_t* olo, uint32_t* ov, hipStream_t st) {
+  const long n = na + nb;
+  if (n <= 0) return 0;
+  if (na < 0 || nb < 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(merge_path_kernel, dim3((unsigned)ceil_div(ceil_div(n, kMergeItems), 256)),
+                     dim3(256), 0, st, ahi, alo, av, na, bhi, blo, bv, nb, ohi, olo, ov);
+  return (int)hipGetLastError();
+}
+
 int hbmr_gather_records_multi(const void* const* bases, const uint32_t* split, const uint32_t* row,
                               const uint32_t* perm, long n, int record_bytes, void* dst,
                               hipStream_t st) {
   if (n <= 0) return 0;
   if (record_bytes % 4 || record_bytes > 4 * 256) return (int)hipErrorInvalidValue;
   const int words = record_bytes / 4;
-  const long grid = std::min<long>(ceil_div(n, 256 / words), 1L << 20);
-  hipLaunchKernelGGL(gather_records_multi_kernel, dim3((unsigned)grid), dim3(256), 0, st,
-                     reinterpret_cast<const uint32_t* const*>(bases), split, row, perm, n, words,
-                     reinterpret_cast<uint32_t*>(dst));
+  static const bool v1 = [] {
+    const char* e = getenv("HBMR_GATHER_V1");
+    return e && *e == '1';
+  }();
+  if (v1) {
+    const long grid = std::min<long>(ceil_div(n, 256 / words), 1L << 20);
+    hipLaunchKernelGGL(gather_records_multi_kernel, dim3((unsigned)grid), dim3(256), 0, st,
+                       reinterpret_cast<const uint32_t* const*>(bases), split, row, perm, n, words,
+                       reinterpret_cast<uint32_t*>(dst));
+  } else {
+    constexpr int U = 4;
+    const long grid = std::min<long>(ceil_div(n, (256 / words) * U), 1L << 18);
+    hipLaunchKernelGGL(gather_records_multi_v3_kernel<U>, dim3((unsigned)grid), dim3(256), 0, st,
+                       reinterpret_cast<const uint32_t* const*>(bases), split, row, perm, n, words,
+                       reinterpret_cast<uint32_t*>(dst));
+  }
   return (int)hipGetLastError();
 }
 

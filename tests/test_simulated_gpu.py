@@ -107,3 +107,34 @@ def test_tracer_records_task_flow_and_exports_chrome(tmp_path):
     TRACE.to_jsonl(str(tmp_path / "trace.jsonl"))
     assert (tmp_path / "trace.jsonl").read_text().count("\n") == len(TRACE.events)
     TRACE.clear()
+
+
+def test_split_cache_scan_policy_keeps_a_resident_fraction():
+    """Cyclic access to more splits than fit: LRU never hits, scan keeps the
+    first ones resident and streams the rest (out-of-core iterations)."""
+    from hbmr.gpu.split_cache import SplitCache
+    for policy, want_hits in (("lru", 0), ("scan", 3 * 4)):
+        c = SplitCache({0: 400}, policy=policy)
+        for _ in range(4):
+            for i in range(10):
+                c.get_or_load(f"s{i}", 0, lambda: object(), lambda _d: 100)
+        assert c.hits == want_hits, policy
+        assert c.bytes_on(0) <= 400
+
+
+def test_kmeans_beyond_hbm_streams_splits_with_scan_cache():
+    """A data set larger than the (simulated) HBM split cache: every iteration
+    is exact and the resident fraction hits."""
+    cap = 3 * 2000 * 16 * 4 + 1024       # three of the six fp32 splits
+    conf = _sim_conf(**{"hbmr.gpu.split.cache.bytes": cap,
+                        "hbmr.gpu.split.cache.policy": "scan"})
+    with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=0) as cl:
+        drv = _kmeans(cl, conf, iters=4)
+        cache = cl.trackers[0].split_cache
+        c_small = drv.centroids()
+        assert 0 < cache.bytes_on(0) <= cap
+        assert cache.hits >= 3 * 3 and cache.bypassed >= 3 * 3
+    plain = JobConf()
+    with LocalCluster(plain, num_trackers=1, cpu_slots=2) as cl:
+        c_cpu = _kmeans(cl, plain, iters=4).centroids()
+    assert torch.equal(c_small, c_cpu)

@@ -37,12 +37,16 @@ def test_create_partitions_rule():
     assert sp[:, 0].tolist() == [5, 10, 15]
 
 
-@pytest.mark.parametrize("trackers", [1, 2, 3])
-def test_terasort_on_cluster_sorts_and_validates(tmp_path, trackers):
+@pytest.mark.parametrize("trackers,merge", [(1, False), (2, False), (3, False), (3, True)])
+def test_terasort_on_cluster_sorts_and_validates(tmp_path, trackers, merge):
+    """merge: senders sort each destination's run and receivers merge the
+    runs (K8 merge path) instead of re-sorting — the same output bytes."""
     rows = 20000
     out = tmp_path / "out"
     with LocalCluster(JobConf(), num_trackers=trackers, cpu_slots=2) as cl:
-        rj = cl.submit_job(T.terasort_conf(rows=rows, split_rows=3000, output=str(out)))
+        conf = T.terasort_conf(rows=rows, split_rows=3000, output=str(out))
+        conf.set_boolean("hbmr.terasort.shuffle.sorted.runs", merge)
+        rj = cl.submit_job(conf)
         rj.waitForCompletion(120)
         assert rj.isSuccessful(), rj.getFailureInfo()
         res = rj._impl.jip.result
@@ -232,3 +236,97 @@ def test_gpu_terasort_many_partitions_one_gpu(tmp_path):
     assert res["partitions"] == 6
     v = T.teravalidate(str(tmp_path / "out"))
     assert v["files"] == 6 and v["records"] == rows and v["misordered"] == 0
+
+
+@pytest.mark.gpu
+def test_gpu_tera_partition_matches_cpu():
+    """Map v3 (key/partition/count kernel + scan + tile-ranked scatter): the
+    same partition boundaries as the CPU twin and, inside every partition,
+    the same (hi, lo, row) multiset (order there is unspecified)."""
+    n = 250_003
+    recs_c = torch.from_numpy(S.teragen_cpu(4242, n))
+    sp = T.create_partitions(recs_c.numpy()[::89, :10].copy(), 29)
+    shi, slo = (torch.from_numpy(x.view(np.int64)) for x in T._key_words(sp))
+    hg, lg, rg, og = S.tera_partition(recs_c.cuda(), shi, slo)
+    hc, lc, rc, oc = S.tera_partition(recs_c, shi, slo)
+    assert torch.equal(og.cpu(), oc)
+    hg, lg, rg = hg.cpu(), lg.cpu(), rg.cpu()
+    for p in range(29):
+        a, b = int(oc[p]), int(oc[p + 1])
+        g = sorted(zip(hg[a:b].tolist(), lg[a:b].tolist(), rg[a:b].tolist()))
+        c = sorted(zip(hc[a:b].tolist(), lc[a:b].tolist(), rc[a:b].tolist()))
+        assert g == c, p
+    # one partition (no splitters) keeps every record
+    h1, _l1, r1, o1 = S.tera_partition(recs_c[:1000].cuda(), shi[:0], slo[:0])
+    assert o1.cpu().tolist() == [0, 1000] and sorted(r1.cpu().tolist()) == list(range(1000))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("run", [3, 200])
+def test_gpu_sort_keys_orders_ties_on_the_low_word(run):
+    """The hi-only sort + tie fix-up: equal high words ordered by the low 16
+    bits; a run longer than the fix-up handles takes the full 80-bit sort."""
+    n = 100_000
+    g = torch.Generator().manual_seed(run)
+    hi = torch.randint(0, 1 << 40, (n,), generator=g, dtype=torch.int64)
+    hi[: n // 2] = hi[: n // 2] // run * run          # many runs of equal hi
+    hi[::997] = hi[0]                                  # one long run
+    lo = torch.randint(0, 1 << 16, (n,), generator=g, dtype=torch.int64)
+    perm, hs, ls = S.sort_keys(hi.cuda(), lo.cuda())
+    pc, hc, lc = S.sort_keys(hi, lo)
+    assert torch.equal(hs.cpu(), hc) and torch.equal(ls.cpu(), lc)
+    p = perm.cpu().long()
+    assert torch.equal(hi[p], hc) and torch.equal(lo[p], lc)
+    assert S.count_unsorted(hs, ls) == 0
+
+
+@pytest.mark.gpu
+def test_gpu_terasort_commits_output(tmp_path):
+    """TeraSort's output goes through the attempt work dir and the committer:
+    parts in the output dir, _SUCCESS, no _temporary left."""
+    rows = 1_000_000
+    out = tmp_path / "out"
+    with LocalCluster(JobConf(), num_trackers=1, gpus=[[0]], cpu_slots=0) as cl:
+        rj = cl.submit_job(T.terasort_conf(rows=rows, split_rows=300_000, partitions=3,
+                                           output=str(out)))
+        rj.waitForCompletion(300)
+        assert rj.isSuccessful(), rj.getFailureInfo()
+    assert (out / "_SUCCESS").exists() and not (out / "_temporary").exists()
+    v = T.teravalidate(str(out))
+    assert v["files"] == 3 and v["records"] == rows and v["misordered"] == 0
+
+
+def test_merge_runs_cpu_is_stable_and_sorted():
+    g = torch.Generator().manual_seed(3)
+    runs = []
+    for r in range(5):
+        h = torch.randint(0, 50, (200 + r,), generator=g, dtype=torch.int64)
+        lo = torch.randint(0, 4, (200 + r,), generator=g, dtype=torch.int64)
+        o = np.lexsort((lo.numpy(), h.numpy()))
+        runs.append((h[o], lo[o], torch.arange(r * 1000, r * 1000 + 200 + r, dtype=torch.int32)))
+    hs, ls, vs = S.merge_runs(runs)
+    assert S.count_unsorted(hs, ls) == 0 and hs.numel() == sum(r[0].numel() for r in runs)
+    # stable: equal keys keep run order (payloads ascend by run)
+    key = hs * 8 + ls
+    for k in torch.unique(key)[:20]:
+        v = vs[key == k]
+        assert torch.all(v[1:] // 1000 >= v[:-1] // 1000)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sizes", [(1000, 1), (0, 5000), (33333, 77777, 5, 123456, 9)])
+def test_gpu_merge_runs_matches_cpu(sizes):
+    g = torch.Generator().manual_seed(sum(sizes))
+    runs = []
+    base = 0
+    for n in sizes:
+        h = torch.randint(0, 1 << 20, (n,), generator=g, dtype=torch.int64)
+        h[::3] = 7                                          # many equal keys across runs
+        lo = torch.randint(0, 1 << 16, (n,), generator=g, dtype=torch.int64)
+        lo[::3] = 1
+        o = np.lexsort((lo.numpy(), h.numpy())) if n else np.zeros(0, dtype=np.int64)
+        runs.append((h[o], lo[o], torch.arange(base, base + n, dtype=torch.int32)))
+        base += n
+    hc, lc, vc = S.merge_runs(runs)
+    hg, lg, vg = S.merge_runs([(a.cuda(), b.cuda(), c.cuda()) for a, b, c in runs])
+    assert torch.equal(hg.cpu(), hc) and torch.equal(lg.cpu(), lc) and torch.equal(vg.cpu(), vc)
