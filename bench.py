@@ -67,6 +67,9 @@ def main():
     ap.add_argument("--prestage", action=argparse.BooleanOptionalAction, default=True,
                     help="let the JobTracker stage held iteration jobs: their GPU maps wait "
                          "on the device behind the predecessor's reduce (hbmr.job.prestage)")
+    ap.add_argument("--exact", action="store_true",
+                    help="fp32-faithful assignment (hbmr.kmeans.exact: bf16 MFMA top-3, "
+                         "certified, fp64 re-score of uncertain points); dtype bf16-certified-fp32")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("-D", dest="defines", action="append", default=[], metavar="KEY=VALUE",
                     help="extra configuration (e.g. -D hbmr.gpu.first.chunk=8)")
@@ -116,6 +119,8 @@ def main():
         conf.set("hbmr.gpu.simulate", "true")
         conf.set("hbmr.gpu.simulate.nodata", "true")
         conf.set("hbmr.gpu.simulate.task.ms", str(a.simulate_ms))
+    if a.exact:
+        conf.set_boolean("hbmr.kmeans.exact", True)
     for kv in a.defines:
         k, _, v = kv.partition("=")
         conf.set(k.strip(), v.strip())
@@ -192,7 +197,8 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16-certified-fp32" if conf.get_boolean("hbmr.kmeans.exact", False)
+                     else "bf16",
             "data": "synthetic" if a.simulate_ms is None else
                     f"simulated GPU slots ({a.simulate_ms} ms/split), CPU only",
             "config": {"model": "K-Means 100M pts x 128-d, k=1024 (hybrid CPU+GPU scheduling)"

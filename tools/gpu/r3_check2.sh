@@ -10,6 +10,8 @@ timeout -k 10 500 python -u -m pytest -x -v --timeout 120 --timeout-method threa
 tail -3 gpurun_out/${P}_gpu_tests.txt; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 240 python bench.py --steps 20 --warmup 3 > gpurun_out/${P}_bench.json 2> gpurun_out/${P}_bench.err || exit 1
 tail -1 gpurun_out/${P}_bench.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('bench', d['ms_per_step'], d['phases_ms'])"
+timeout -k 10 300 python bench.py --steps 10 --warmup 3 --exact > gpurun_out/${P}_bench_exact.json 2> gpurun_out/${P}_bench_exact.err || { tail -5 gpurun_out/${P}_bench_exact.err; exit 1; }
+tail -1 gpurun_out/${P}_bench_exact.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('exact', d['dtype'], d['ms_per_step'], d['phases_ms'])"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${P}_tera20 -o run -- python3 tools/bench_terasort.py --rows 200000000 --steps 2 > gpurun_out/${P}_tera20.json 2> gpurun_out/${P}_tera20.err || { tail -5 gpurun_out/${P}_tera20.err; exit 1; }
 tail -1 gpurun_out/${P}_tera20.json
 timeout -k 10 400 python tools/bench_terasort.py --rows 1000000000 --split-rows 10000000 --steps 3 > gpurun_out/${P}_tera100.json 2> gpurun_out/${P}_tera100.err || { tail -5 gpurun_out/${P}_tera100.err; exit 1; }
