@@ -70,6 +70,9 @@ def main():
     ap.add_argument("--exact", action="store_true",
                     help="fp32-faithful assignment (hbmr.kmeans.exact: bf16 MFMA top-3, "
                          "certified, fp64 re-score of uncertain points); dtype bf16-certified-fp32")
+    ap.add_argument("--input", default=None, metavar="DIR",
+                    help="SequenceFile input (tools/write_kmeans_input.py writes the synthetic "
+                         "set as files) instead of points generated in HBM")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("-D", dest="defines", action="append", default=[], metavar="KEY=VALUE",
                     help="extra configuration (e.g. -D hbmr.gpu.first.chunk=8)")
@@ -130,7 +133,10 @@ def main():
         node.shutdown()
         return 0
 
-    inp = f"synthetic:{a.points}:7"
+    inp = a.input or f"synthetic:{a.points}:7"
+    if a.input:
+        # one split per input file (the writer's files hold --split-points each)
+        conf.set_int("mapred.map.tasks", -(-a.points // a.split_points))
     drv = K.KMeansDriver(node.submit_job, node.job_result, conf=conf, k=a.k, d=a.dims, inp=inp,
                          split_points=a.split_points)
 
@@ -199,7 +205,8 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16-certified-fp32" if conf.get_boolean("hbmr.kmeans.exact", False)
                      else "bf16",
-            "data": "synthetic" if a.simulate_ms is None else
+            "data": (f"sequencefile input {a.input} (the synthetic set written to disk)"
+                     if a.input else "synthetic") if a.simulate_ms is None else
                     f"simulated GPU slots ({a.simulate_ms} ms/split), CPU only",
             "config": {"model": "K-Means 100M pts x 128-d, k=1024 (hybrid CPU+GPU scheduling)"
                        if (a.points, a.dims, a.k) == (100_000_000, 128, 1024) else
