@@ -10,6 +10,10 @@ max.words`` distinct words are held).  The reduce output is the same; the map
 side does what WordCount's combiner (IntSumReducer) would, without a Python
 collect() per token, which bound the per-token job at 4.4 MB/s.  ``false``
 restores the reference's per-token emit.
+
+``hbmr.wordcount.native`` (default true) runs the map through
+:class:`NativeWordCountRunner`: the same counts from a C++ tokenizer + hash
+table over 4 MiB blocks of the split (native/cpu/wordcount.cc).
 """
 from __future__ import annotations
 
@@ -17,6 +21,7 @@ from collections import Counter
 
 from ..io.writable import IntWritable, Text
 from ..mapred import FileInputFormat, FileOutputFormat, JobClient, JobConf, Mapper, Reducer
+from ..mapred.maprunner import MapRunner
 
 INMAPPER_KEY = "hbmr.wordcount.inmapper.combine"
 
@@ -61,6 +66,119 @@ class WordCountMapper(Mapper):
             self._flush()
 
 
+class NativeWordCountRunner(MapRunner):
+    """Map runner counting a text split's words in C++ (native/cpu/wordcount.cc):
+    the split's bytes are read in 4 MiB blocks of whole lines (the lines
+    LineRecordReader would return: those starting at or before the split end),
+    tokenised on ASCII whitespace and counted in one open-addressing table, and
+    each distinct word is emitted once with its count — the in-mapper combine
+    of WordCountMapper without a Python call per line or token.  Other inputs
+    (compressed files, other record readers) take the per-record path."""
+
+    BLOCK = 4 << 20
+
+    def run(self, reader, output, reporter):
+        from ..mapred import counters as C
+        from ..mapred.formats import LineRecordReader
+        lr = getattr(reader, "r", reader)
+        lib = _wc_lib()
+        if lib is None or not isinstance(lr, LineRecordReader) or lr.codec is not None or \
+                type(self.mapper) is not WordCountMapper or \
+                not self.job.get_boolean(INMAPPER_KEY, True):
+            return super().run(reader, output, reporter)
+        h = lib.hbmr_wc_cpu_new()
+        lines = 0
+        try:
+            max_words = self.job.get_int("hbmr.wordcount.inmapper.max.words", 1 << 20)
+            for block in _owned_blocks(lr, self.BLOCK):
+                lines += block.count(b"\n") + (0 if block.endswith(b"\n") else 1)
+                if lib.hbmr_wc_cpu_add(h, block, len(block)) >= max_words:
+                    _emit(lib, h, output)
+                if reporter is not None:
+                    reporter.progress()
+            _emit(lib, h, output)
+        finally:
+            lib.hbmr_wc_cpu_free(h)
+        reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, lines)
+
+
+def _owned_blocks(lr, size):
+    """Blocks of whole lines of ``lr``'s split, from its current position (the
+    first partial line already skipped) through the line that starts at or
+    before the split end; each block ends with a newline except possibly the
+    file's last."""
+    f, pos, end = lr.f, lr.pos, lr.end
+    tail = b""
+    while pos <= end:
+        data = f.read(size)
+        if not data:
+            if tail:
+                yield tail
+            return
+        buf = tail + data if tail else data
+        base = pos - len(tail)          # file offset of buf[0]
+        cut = buf.rfind(b"\n")
+        if cut < 0:
+            tail = buf
+            pos = base + len(buf)
+            continue
+        # lines starting at <= end are ours: stop after the first newline at
+        # offset >= end (the line holding `end`, or the one starting there)
+        if base + cut >= end:
+            stop = buf.find(b"\n", max(0, end - base))
+            yield buf[:stop + 1]
+            return
+        yield buf[:cut + 1]
+        tail = buf[cut + 1:]
+        pos = base + len(buf)
+    if tail:
+        yield tail
+
+
+def _emit(lib, h, output):
+    import ctypes
+    import numpy as np
+    w = lib.hbmr_wc_cpu_words(h)
+    if w == 0:
+        return
+    nbytes = lib.hbmr_wc_cpu_bytes(h)
+    words = ctypes.create_string_buffer(max(1, nbytes))
+    offs = np.empty(w + 1, dtype=np.int64)
+    cnts = np.empty(w, dtype=np.int64)
+    lib.hbmr_wc_cpu_export(h, words, offs.ctypes.data, cnts.ctypes.data)
+    raw = words.raw[:nbytes]
+    o = offs.tolist()
+    for i, c in enumerate(cnts.tolist()):
+        output.collect(Text(raw[o[i]:o[i + 1]]), IntWritable(c))
+
+
+_WC_LIB = None
+
+
+def _wc_lib():
+    global _WC_LIB
+    if _WC_LIB is None:
+        import ctypes
+        import os
+        path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib",
+                            "libhbmr_cpu.so")
+        try:
+            L = ctypes.CDLL(path)
+            P, I64 = ctypes.c_void_p, ctypes.c_int64
+            L.hbmr_wc_cpu_new.restype = P
+            L.hbmr_wc_cpu_free.argtypes = [P]
+            L.hbmr_wc_cpu_add.argtypes = [P, ctypes.c_char_p, I64]
+            L.hbmr_wc_cpu_add.restype = I64
+            for f in ("hbmr_wc_cpu_words", "hbmr_wc_cpu_bytes", "hbmr_wc_cpu_tokens"):
+                getattr(L, f).argtypes = [P]
+                getattr(L, f).restype = I64
+            L.hbmr_wc_cpu_export.argtypes = [P, P, P, P]
+            _WC_LIB = L
+        except (OSError, AttributeError):
+            _WC_LIB = False
+    return _WC_LIB or None
+
+
 class IntSumReducer(Reducer):
     def reduce(self, key, values, output, reporter):
         output.collect(key, IntWritable(sum(v.value for v in values)))
@@ -72,6 +190,8 @@ def make_job(inputs, output, reduces=1, conf=None) -> JobConf:
     job.set_output_key_class(Text)
     job.set_output_value_class(IntWritable)
     job.set_mapper_class(WordCountMapper)
+    if job.get_boolean("hbmr.wordcount.native", True):
+        job.set_map_runner_class(NativeWordCountRunner)
     job.set_combiner_class(IntSumReducer)
     job.set_reducer_class(IntSumReducer)
     job.set_num_reduce_tasks(reduces)

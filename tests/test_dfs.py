@@ -148,7 +148,11 @@ def test_wordcount_over_hdfs_with_data_local_maps(tmp_path):
             for ln in lines:
                 cnt.update(ln.split())
         with LocalCluster(JobConf(), num_trackers=2, cpu_slots=2, hosts=hosts) as cl:
-            job = wordcount.make_job(f"{dfs.uri}/in", f"{dfs.uri}/out", reduces=2)
+            # the per-record mapper: maps long enough that each tracker is
+            # offered its own blocks before the other could take them
+            wc = JobConf()
+            wc.set_boolean("hbmr.wordcount.native", False)
+            job = wordcount.make_job(f"{dfs.uri}/in", f"{dfs.uri}/out", reduces=2, conf=wc)
             rj = JobClient.runJob(job, cluster=cl, verbose=False)
             cs = rj.getCounters()
         got = {}

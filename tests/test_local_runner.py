@@ -172,3 +172,44 @@ def test_type_mismatch_fails(tmp_path):
     assert not rj.isSuccessful()
     assert "Type mismatch" in rj.getFailureInfo()
     _ = IntWritable
+
+
+@pytest.mark.parametrize("split_mb", [0.0005, 0.003, 64])
+def test_native_wordcount_runner_matches_python_mapper(tmp_path, split_mb):
+    """NativeWordCountRunner (C++ tokenizer + table over whole-line blocks of
+    the split) gives the per-record mapper's counts for any split boundaries
+    (lines crossing splits, CRLF, tabs/form feeds, a last line without a newline)."""
+    import collections
+    from hbmr.models import wordcount as W
+    d = tmp_path / "in"
+    d.mkdir()
+    rng = __import__("random").Random(5)
+    words = [f"w{i}" for i in range(300)] + ["é", "naïve", "x" * 40]
+    lines = []
+    for i in range(3000):
+        sep = rng.choice([" ", "  ", "\t", " \x0c "])
+        lines.append(sep.join(rng.choice(words) for _ in range(rng.randrange(0, 9))))
+    text = "\r\n".join(lines[:1500]) + "\n" + "\n".join(lines[1500:])    # no final newline
+    (d / "a.txt").write_text(text)
+    want = collections.Counter(text.encode().split())
+    res = {}
+    for native in (True, False):
+        conf = JobConf()
+        conf.set("mapred.job.tracker", "local")
+        conf.set_boolean("hbmr.wordcount.native", native)
+        conf.set_long("mapred.min.split.size", 1)
+        conf.set_long("mapred.max.split.size", int(split_mb * (1 << 20)))
+        out = tmp_path / f"out{native}"
+        job = W.make_job(str(d), str(out), reduces=2, conf=conf)
+        job.set_num_map_tasks(max(1, int(len(text) / max(1, split_mb * (1 << 20)))))
+        rj = JobClient.runJob(job, verbose=False)
+        got = {}
+        for fn in os.listdir(out):
+            if fn.startswith("part-"):
+                for line in open(out / fn, "rb"):
+                    k, v = line.rstrip(b"\n").rsplit(b"\t", 1)
+                    got[k] = int(v)
+        res[native] = got
+        recs = rj.getCounters().get("org.apache.hadoop.mapred.Task$Counter", "MAP_INPUT_RECORDS")
+        assert recs == 3000 - 0, (native, recs)
+    assert res[True] == res[False] == dict(want)
