@@ -18,6 +18,8 @@
 // Shapes must be multiples of the tile (M, N % 256 == 0, K % 64 == 0); the
 // host wrapper (hbmr/ops/gemm.py) pads other shapes.
 #include "common.h"
+
+#include <cstdlib>
 #include "../include/hbmr/hbmr.h"
 
 namespace {
@@ -144,6 +146,130 @@ __global__ __launch_bounds__(kGemmThreads, 1) void gemm_bf16_tn_kernel(
   }
 }
 
+// ---- v2: 4 waves of 128×128 (v_mfma_f32_32x32x16_bf16) ----------------------
+// Same 256×256 tile, K-step, LDS image (XOR-swizzled 128-B rows) and DMA
+// staging as v1, but 4 waves as 2 (M) × 2 (N), each owning a 128×128 block =
+// 4×4 tiles of 32×32: per K-step a wave reads its 128 A rows and 128 B rows
+// once (128 KiB of LDS reads per workgroup instead of v1's 192 KiB for the
+// same 8.4 MFLOP), and issues 64 MFMAs of 32x32x16 (256 accumulators per lane,
+// AGPR-resident).  32x32x16 fragments: lane l holds row (l & 31) at k-offset
+// 8 (l >> 5) of a 16-wide step; C register r of lane l is row
+// (r & 3) + 8 (r >> 2) + 4 (l >> 5), column l & 31.
+constexpr int kGemmThreads2 = 256;
+
+__device__ __forceinline__ void stage_tile2(char* lds, const __bf16* __restrict__ G, long ld,
+                                            long row0, long k0, int tid) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int p = i * kGemmThreads2 + tid;  // 16-B piece index in the tile image
+    const int r = p >> 3, c = p & 7;
+    const int src_c = c ^ (r & 7);
+    const __bf16* g = G + (row0 + r) * ld + k0 + src_c * 8;
+    char* dst = lds + (size_t)(i * kGemmThreads2 + (tid & ~63)) * 16;
+    __builtin_amdgcn_global_load_lds((const void*)g, (void*)dst, 16, 0, 0);
+  }
+}
+
+template <bool OUT_BF16>
+__global__ __launch_bounds__(kGemmThreads2, 1) void gemm_bf16_tn_v2_kernel(
+    const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void* __restrict__ Cv, long M,
+    long N, long K, float alpha, double* __restrict__ partials) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;   // 2 × 2 waves
+  const long tiles_n = N / kBN;
+  const uint32_t t = hbmr_xcd_remap(blockIdx.x, gridDim.x);
+  const long bm = t / tiles_n, bn = t % tiles_n;
+  const long m0 = bm * kBM, n0 = bn * kBN;
+  const int nk = (int)(K / kBK);
+
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  stage_tile2(smem, A, K, m0, 0, tid);
+  stage_tile2(smem + kTileBytes, Bt, K, n0, 0, tid);
+
+  const int fr = lane & 31;   // fragment row (A) / column (B) within a 32-tile
+  const int h = lane >> 5;    // k-offset 8h within a 16-wide step
+
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * kStageBytes;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < nk) {
+      char* nxt = smem + ((kt + 1) & 1) * kStageBytes;
+      stage_tile2(nxt, A, K, m0, (long)(kt + 1) * kBK, tid);
+      stage_tile2(nxt + kTileBytes, Bt, K, n0, (long)(kt + 1) * kBK, tid);
+    }
+    const char* la = cur;
+    const char* lb = cur + kTileBytes;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int c = 2 * s + h;  // logical 16-B chunk of the 128-B row
+      bf16x8_t a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = wm * 128 + i * 32 + fr;
+        a[i] = *reinterpret_cast<const bf16x8_t*>(la + r * 128 + ((c ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = wn * 128 + j * 32 + fr;
+        b[j] = *reinterpret_cast<const bf16x8_t*>(lb + r * 128 + ((c ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // per (i, j) one lane base pointer; the 16 rows of a register block are
+  // uniform multiples of N (scalar offsets)
+  double csum = 0.0;
+  const long lane_off = (m0 + wm * 128 + 4 * h) * N + n0 + wn * 128 + fr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const long base = lane_off + (long)(i * 32) * N + j * 32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long off = base + (long)((r & 3) + 8 * (r >> 2)) * N;
+        const float v = acc[i][j][r] * alpha;
+        if (OUT_BF16) {
+          const uint16_t hv = hbmr_f32_to_bf16(v);
+          reinterpret_cast<uint16_t*>(Cv)[off] = hv;
+          csum += (double)__uint_as_float((uint32_t)hv << 16);
+        } else {
+          reinterpret_cast<float*>(Cv)[off] = v;
+          csum += (double)v;
+        }
+      }
+    }
+  }
+  if (partials) {
+    __shared__ double s_red2[kGemmThreads2 / 64];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) csum += __shfl_xor(csum, o);
+    if (lane == 0) s_red2[wave] = csum;
+    __syncthreads();
+    if (tid == 0) {
+      double sum = 0.0;
+#pragma unroll
+      for (int w = 0; w < kGemmThreads2 / 64; ++w) sum += s_red2[w];
+      partials[blockIdx.x] = sum;
+    }
+  }
+}
+
 bool g_gemm_lds_set = false;
 
 }  // namespace
@@ -161,10 +287,30 @@ int hbmr_gemm_bf16_tn_ex(const void* A, const void* Bt, void* C, long M, long N,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLds));
     HBMR_RETURN_IF_ERROR(hipFuncSetAttribute((const void*)gemm_bf16_tn_kernel<true>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLds));
+    HBMR_RETURN_IF_ERROR(hipFuncSetAttribute((const void*)gemm_bf16_tn_v2_kernel<false>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLds));
+    HBMR_RETURN_IF_ERROR(hipFuncSetAttribute((const void*)gemm_bf16_tn_v2_kernel<true>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLds));
     g_gemm_lds_set = true;
   }
   const long tiles = (M / kBM) * (N / kBN);
   if (tiles > 0x7fffffffL) return (int)hipErrorInvalidValue;
+  // HBMR_GEMM=2: the 4-wave 128x128 / 32x32x16 variant (A/B against v1)
+  static const int ver = [] {
+    const char* e = getenv("HBMR_GEMM");
+    return e && *e == '2' ? 2 : 1;
+  }();
+  if (ver == 2) {
+    if (out_bf16)
+      hipLaunchKernelGGL(gemm_bf16_tn_v2_kernel<true>, dim3((unsigned)tiles), dim3(kGemmThreads2),
+                         kGemmLds, st, reinterpret_cast<const __bf16*>(A),
+                         reinterpret_cast<const __bf16*>(Bt), C, M, N, K, alpha, partials);
+    else
+      hipLaunchKernelGGL(gemm_bf16_tn_v2_kernel<false>, dim3((unsigned)tiles),
+                         dim3(kGemmThreads2), kGemmLds, st, reinterpret_cast<const __bf16*>(A),
+                         reinterpret_cast<const __bf16*>(Bt), C, M, N, K, alpha, partials);
+    return (int)hipGetLastError();
+  }
   if (out_bf16)
     hipLaunchKernelGGL(gemm_bf16_tn_kernel<true>, dim3((unsigned)tiles), dim3(kGemmThreads),
                        kGemmLds, st, reinterpret_cast<const __bf16*>(A),

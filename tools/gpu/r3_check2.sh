@@ -26,4 +26,9 @@ tail -1 gpurun_out/${P}_tera10_out.json
 rm -rf /tmp/tera-out
 timeout -k 10 200 python tools/trace_config2.py --gpu > gpurun_out/${P}_config2_trace.txt 2>&1 || { tail -5 gpurun_out/${P}_config2_trace.txt; exit 1; }
 grep -E "iteration" gpurun_out/${P}_config2_trace.txt
+HBMR_GEMM=2 timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_matmul.py > gpurun_out/${P}_gemm2_tests.txt 2>&1 && tail -1 gpurun_out/${P}_gemm2_tests.txt && \
+timeout -k 10 200 python tools/bench_matmul.py > gpurun_out/${P}_matmul_v1.json 2>&1 && tail -2 gpurun_out/${P}_matmul_v1.json && \
+HBMR_GEMM=2 timeout -k 10 200 python tools/bench_matmul.py > gpurun_out/${P}_matmul_v2.json 2>&1 && tail -2 gpurun_out/${P}_matmul_v2.json || exit 1
+HBMR_SHARED_DEVICE=0 timeout -k 10 300 python bench.py --gpus 2 --steps 10 --warmup 3 > gpurun_out/${P}_bench_2rank_shared.json 2> gpurun_out/${P}_bench_2rank_shared.err || { tail -5 gpurun_out/${P}_bench_2rank_shared.err; exit 1; }
+tail -1 gpurun_out/${P}_bench_2rank_shared.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('2rank-shared', d['ms_per_step'], d['phases_ms'])"
 P=${P}_sim bash tools/gpu/r3_rehearsal.sh
