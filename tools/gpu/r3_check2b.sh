@@ -1,22 +1,10 @@
-# round 3: GPU tests + default bench + TeraSort v3 (20 GB rocprof, 100 GB, output-committed)
-# + config-2 Pipes trace + many-core CPU rehearsal
+# round 3 (part B): TeraSort v3 (20 GB rocprof, 100 GB, output-committed), config-2 Pipes
+# trace, GEMM v2 A/B, 2-rank shared-device bench, many-core CPU rehearsal
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 P=${P:-r3i}
-timeout -k 10 500 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests \
-  > gpurun_out/${P}_gpu_tests.txt 2>&1; rc=$?
-tail -3 gpurun_out/${P}_gpu_tests.txt; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 240 python bench.py --steps 20 --warmup 3 > gpurun_out/${P}_bench.json 2> gpurun_out/${P}_bench.err || exit 1
-tail -1 gpurun_out/${P}_bench.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('bench', d['ms_per_step'], d['phases_ms'])"
-timeout -k 10 300 python bench.py --steps 10 --warmup 3 --exact > gpurun_out/${P}_bench_exact.json 2> gpurun_out/${P}_bench_exact.err || { tail -5 gpurun_out/${P}_bench_exact.err; exit 1; }
-tail -1 gpurun_out/${P}_bench_exact.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('exact', d['dtype'], d['ms_per_step'], d['phases_ms'])"
-timeout -k 10 300 python tools/write_kmeans_input.py --dir /tmp/km100m > gpurun_out/${P}_write_input.txt 2>&1 || { tail -5 gpurun_out/${P}_write_input.txt; exit 1; }
-tail -1 gpurun_out/${P}_write_input.txt
-timeout -k 10 300 python bench.py --steps 10 --warmup 3 --input /tmp/km100m > gpurun_out/${P}_bench_file.json 2> gpurun_out/${P}_bench_file.err || { tail -5 gpurun_out/${P}_bench_file.err; exit 1; }
-tail -1 gpurun_out/${P}_bench_file.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('file', d['ms_per_step'], d['warmup_seconds'], d['phases_ms'])"
-rm -rf /tmp/km100m
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${P}_tera20 -o run -- python3 tools/bench_terasort.py --rows 200000000 --steps 2 > gpurun_out/${P}_tera20.json 2> gpurun_out/${P}_tera20.err || { tail -5 gpurun_out/${P}_tera20.err; exit 1; }
 tail -1 gpurun_out/${P}_tera20.json
 timeout -k 10 400 python tools/bench_terasort.py --rows 1000000000 --split-rows 10000000 --steps 3 > gpurun_out/${P}_tera100.json 2> gpurun_out/${P}_tera100.err || { tail -5 gpurun_out/${P}_tera100.err; exit 1; }
