@@ -89,7 +89,7 @@ def _gather_outputs(js, spec, run):
             missing = [a for a in want if a not in js.map_outputs]
         if missing:
             raise RuntimeError(f"map outputs lost: {missing[:4]}")
-        return outs, []
+        return outs, [None] * len(outs)
     with js.cond:
         while True:
             if run.kill.is_set():
@@ -104,11 +104,11 @@ def _gather_outputs(js, spec, run):
         for a in want:
             if a in js.map_outputs:
                 outs.append(js.map_outputs[a])
+                marks.append(None)
             else:
                 o, m = js.launched[a]
                 outs.append(o)
-                if m is not None:
-                    marks.append(m)
+                marks.append(m)
     return outs, marks
 
 
@@ -183,17 +183,24 @@ def run_split_reduce(host, run, device=None):
             ctx.device = device
             with torch.cuda.device(device), torch.cuda.stream(_reduce_stream(host, device)):
                 cur = torch.cuda.current_stream()
-                for ev in {id(m): m for m in marks}.values():
-                    cur.wait_event(ev)
+                if getattr(js.split_job, "orders_own_outputs", False):
+                    # the split job waits on each output's event itself (e.g.
+                    # TeraSort's shuffle waves: early outputs move while later
+                    # maps still run)
+                    ctx.output_marks = marks
+                else:
+                    for ev in {id(m): m for m in marks if m is not None}.values():
+                        cur.wait_event(ev)
                 combined = js.split_job.combine(ctx, outs)
                 if TRACE.on:
                     TRACE.instant("tt.reduce.combined", attempt=spec.attempt_id)
                 js.result = js.split_job.reduce(ctx, combined)
                 release_dependents()
         else:
-            if marks:
+            real = [m for m in marks if m is not None]
+            if real:
                 # simulated device: the outputs are "ready" at these times
-                delay = max(marks) - time.time()
+                delay = max(real) - time.time()
                 if delay > 0:
                     time.sleep(delay)
             ctx.device = None

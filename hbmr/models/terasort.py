@@ -39,6 +39,7 @@ import torch
 from ..gpu.splitjob import SplitJob, SplitSpec
 from ..mapred import counters as C
 from ..ops import sort as S
+from ..utils.trace import TRACE
 
 INPUT_KEY = "hbmr.terasort.input"            # "teragen:<rows>" or a directory of TeraGen files
 SPLIT_ROWS_KEY = "hbmr.terasort.split.rows"
@@ -109,6 +110,11 @@ class TeraSortSplitJob(SplitJob):
         # all-to-all and receivers merge the W sorted runs (K8 merge path,
         # log2 W passes) instead of re-sorting what they received
         self.sorted_runs = conf.get_boolean("hbmr.terasort.shuffle.sorted.runs", False)
+        # several ranks: the shuffle runs in this many waves of this rank's map
+        # outputs (in launch order), each wave's all-to-all-v issued as soon as
+        # its maps are done — with an early reduce (expect mode,
+        # hbmr.job.prestage) it overlaps the later maps (map ∥ shuffle)
+        self.waves = max(1, conf.get_int("hbmr.terasort.shuffle.waves", 1))
 
     # -- splits + sampling (JobTracker side) -----------------------------------------
     def _ranges(self):
@@ -222,7 +228,22 @@ class TeraSortSplitJob(SplitJob):
     def owner_range(rank, world, nparts):
         return rank * nparts // world, (rank + 1) * nparts // world
 
+    @property
+    def orders_own_outputs(self):
+        """Wave mode waits on each map output's event itself."""
+        return self.waves > 1
+
     def combine(self, ctx, outputs):
+        if self.waves > 1 and ctx.comm.world_size > 1:
+            marks = getattr(ctx, "output_marks", None) or [None] * len(outputs)
+            keep = [(o, m) for o, m in zip(outputs, marks) if o is not None]
+            return {"outs": [o for o, _ in keep], "marks": [m for _, m in keep], "waves": True,
+                    "nparts": keep[0][0]["nparts"] if keep else None, "offsets": None,
+                    "checksum": 0}
+        if ctx.device is not None and getattr(ctx, "output_marks", None):
+            cur = torch.cuda.current_stream()
+            for m in {id(m): m for m in ctx.output_marks if m is not None}.values():
+                cur.wait_event(m)
         outs = [o for o in outputs if o is not None]
         if not outs:
             return {"outs": [], "offsets": None, "nparts": None, "checksum": 0}
@@ -240,7 +261,10 @@ class TeraSortSplitJob(SplitJob):
         if self.out:
             self._open_output(ctx)
         try:
-            if comm.world_size == 1:
+            if combined.get("waves"):
+                stats, csum_in = self._reduce_shuffle_waves(ctx, outs, combined["marks"], nparts,
+                                                            dev)
+            elif comm.world_size == 1:
                 stats = self._reduce_local(ctx, outs, combined["offsets"], nparts or 1, dev)
             else:
                 stats = self._reduce_shuffle(ctx, outs, combined["offsets"], nparts, dev)
@@ -338,6 +362,125 @@ class TeraSortSplitJob(SplitJob):
             return 0, None
         return n, torch.cat([bad.reshape(1), csum.reshape(1), first[0], first[1], last[0],
                              last[1]])
+
+    def _agree_parts(self, comm, outs, nparts):
+        """R and the splitters, agreed by every rank (a rank may have run no map;
+        every rank takes part, so the collective sequence is the same)."""
+        nparts = max(int(g[0]) for g in comm.all_gather(
+            torch.tensor([nparts or 0], dtype=torch.int64)))
+        spl = None
+        if nparts > 1:
+            k = nparts - 1
+            mine = torch.zeros(1 + 2 * k, dtype=torch.int64)
+            if outs:
+                shi, slo = _parse_keys(self._splitters_of(outs))
+                assert shi.numel() == k, (shi.numel(), k)
+                mine[0] = 1
+                mine[1:1 + k] = shi
+                mine[1 + k:] = slo
+            for g in comm.all_gather(mine):
+                g = g.cpu()
+                if int(g[0]):
+                    spl = (g[1:1 + k], g[1 + k:])
+                    break
+        return nparts, spl
+
+    def _send_buffer(self, outs, offs, nparts, W, dev):
+        """This rank's records for every destination rank, in destination
+        order (one gather), and the per-destination counts."""
+        counts = [0] * W
+        splits, rowsl, perms = [], [], []
+        if not outs:
+            return torch.empty(0, S.RECORD, dtype=torch.uint8, device=dev), counts
+        his = [o["hi"] for o in outs]
+        los = [o["lo"] for o in outs]
+        rows = [o["row"] for o in outs]
+        bases = [o["records"] for o in outs]
+        at = 0
+        for d in range(W):
+            a, b = self.owner_range(d, W, nparts)
+            starts = offs[:, a]
+            lens = offs[:, b] - offs[:, a]
+            counts[d] = int(lens.sum())
+            if counts[d]:
+                h, lw, sp, rw = S.tera_collect(his, los, rows, starts, lens,
+                                               with_keys=self.sorted_runs)
+                if self.sorted_runs:
+                    perm, _hs, _ls = S.sort_keys(h, lw)
+                    perms.append(perm + at)
+                splits.append(sp)
+                rowsl.append(rw)
+                at += counts[d]
+        if not splits:
+            return torch.empty(0, S.RECORD, dtype=torch.uint8, device=dev), counts
+        return S.gather_records_multi(bases, torch.cat(splits), torch.cat(rowsl),
+                                      torch.cat(perms) if perms else None), counts
+
+    def _reduce_shuffle_waves(self, ctx, outs, marks, nparts, dev):
+        """The shuffle in ``waves`` all-to-all-v rounds over this rank's map
+        outputs in launch order: round g waits (on the device) only for its own
+        maps' events, reads their partition offsets, gathers and sends their
+        records, while later maps may still be running.  Every rank runs the
+        same number of rounds (empty ones send nothing)."""
+        comm = ctx.comm
+        W, me = comm.world_size, comm.rank
+        nparts, spl = self._agree_parts(comm, outs, nparts)
+        cuda = dev.type == "cuda"
+        cur = torch.cuda.current_stream() if cuda else None
+        n_local = len(outs)
+        bounds = [n_local * g // self.waves for g in range(self.waves + 1)]
+        csum = torch.zeros((), dtype=torch.int64, device=dev)
+        recvs, rcs = [], []
+        for g in range(self.waves):
+            grp = outs[bounds[g]:bounds[g + 1]]
+            if cuda:
+                for m in {id(m): m for m in marks[bounds[g]:bounds[g + 1]]
+                          if m is not None}.values():
+                    cur.wait_event(m)
+            offs = torch.stack([o["offsets"] for o in grp]).to("cpu").numpy() if grp else None
+            if grp:
+                csum = csum + torch.stack([o["checksum"].reshape(()) for o in grp]).sum()
+            send, counts = self._send_buffer(grp, offs, nparts, W, dev)
+            if TRACE.on:
+                TRACE.instant("tera.wave.send", wave=g, records=int(sum(counts)))
+            recv, rc = comm.all_to_all_v(send, counts)
+            del send
+            recvs.append(recv)
+            rcs.append(rc)
+        if self.sorted_runs:
+            # runs arrive per (wave, source): merge them all
+            recv = torch.cat(recvs)
+            runs_counts = [c for rc in rcs for c in rc]
+        else:
+            recv = torch.cat(recvs)
+        del recvs
+        if recv.shape[0] == 0:
+            return (0, None), csum
+        if self.sorted_runs:
+            srt, hs, ls = self._merge_received(recv, runs_counts)
+        else:
+            srt, hs, ls = S.sort_records(recv)
+        del recv
+        n = int(srt.shape[0])
+        st = torch.cat([S.count_unsorted_dev(hs, ls).reshape(1),
+                        (hs.sum() + ls.sum()).reshape(1), hs[:1], ls[:1], hs[-1:], ls[-1:]])
+        if self.out:
+            self._write_owned(ctx, srt, hs, ls, spl, nparts, W, me, n, dev)
+        return (n, st), csum
+
+    def _write_owned(self, ctx, srt, hs, ls, spl, nparts, W, me, n, dev):
+        a, b = self.owner_range(me, W, nparts)
+        if b - a > 1:
+            if spl is None:
+                raise RuntimeError("no rank holds the splitters of this job")
+            shi, slo = spl
+            cut = S.split_offsets(hs, ls, shi[a:b - 1].to(dev), slo[a:b - 1].to(dev)) \
+                .to("cpu").tolist()
+            cut = [0] + cut[1:-1] + [n]
+        else:
+            cut = [0, n]
+        for i, p in enumerate(range(a, b)):
+            self._write_part(ctx, p, srt[cut[i]:cut[i + 1]])
 
     def _reduce_shuffle(self, ctx, outs, offs, nparts, dev):
         """world > 1: every rank gathers the records of each destination's

@@ -58,13 +58,18 @@ def test_two_ranks_one_gpu_device_collectives_match_in_process(tmp_path):
     assert mp["kmeans_counters"].get("ALL_REDUCE_STAGED", 0) >= 2
     assert mp["terasort_counters"].get("ALL_TO_ALL_V_CUDA", 0) >= 2
     assert mp["wordcount_counters"].get("ALL_TO_ALL_V_CUDA", 0) >= 4
+    # waves: 3 all-to-all-v rounds (plus R/splitter agreement), same bytes
+    assert mp["terasort_waves_counters"].get("ALL_TO_ALL_V_CUDA", 0) >= 6
+    assert mp["terasort_waves"] == mp["terasort"]
 
     import mp_device
     conf = JobConf()
+    conf.set_boolean("hbmr.job.prestage", True)
     with LocalCluster(conf, num_trackers=2, gpus=[[0], [0]], cpu_slots=0) as cl:
         ip = mp_device.run_jobs(cl.submit_job, lambda rj: rj._impl.jip.result[0], conf,
                                 str(tmp_path / "ip"))
     assert ip["centroids"] == mp["centroids"]              # exact fixed-point partials
     assert ip["terasort"] == mp["terasort"] and len(mp["terasort"]) == 2
+    assert ip["terasort_waves"] == mp["terasort"]
     assert ip["wordcount"] == mp["wordcount"] and len(mp["wordcount"]) == 2
     assert ip["terasort_counters"].get("ALL_TO_ALL_V_CUDA", 0) >= 2   # InProcessComm, device

@@ -37,15 +37,18 @@ def test_create_partitions_rule():
     assert sp[:, 0].tolist() == [5, 10, 15]
 
 
-@pytest.mark.parametrize("trackers,merge", [(1, False), (2, False), (3, False), (3, True)])
-def test_terasort_on_cluster_sorts_and_validates(tmp_path, trackers, merge):
+@pytest.mark.parametrize("trackers,merge,waves", [(1, False, 1), (2, False, 1), (3, False, 1),
+                                                  (3, True, 1), (3, False, 3), (2, True, 4)])
+def test_terasort_on_cluster_sorts_and_validates(tmp_path, trackers, merge, waves):
     """merge: senders sort each destination's run and receivers merge the
-    runs (K8 merge path) instead of re-sorting — the same output bytes."""
+    runs (K8 merge path) instead of re-sorting; waves: the shuffle runs in
+    rounds over each rank's map outputs — the same output bytes."""
     rows = 20000
     out = tmp_path / "out"
     with LocalCluster(JobConf(), num_trackers=trackers, cpu_slots=2) as cl:
         conf = T.terasort_conf(rows=rows, split_rows=3000, output=str(out))
         conf.set_boolean("hbmr.terasort.shuffle.sorted.runs", merge)
+        conf.set_int("hbmr.terasort.shuffle.waves", waves)
         rj = cl.submit_job(conf)
         rj.waitForCompletion(120)
         assert rj.isSuccessful(), rj.getFailureInfo()
