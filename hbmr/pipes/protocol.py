@@ -89,12 +89,15 @@ class DownwardProtocol:
 
     def set_job_conf(self, conf):
         items = list(conf) if not isinstance(conf, dict) else list(conf.items())
+        # one buffer for the whole message (a few hundred strings per task)
+        parts = [encode_vint(SET_JOB_CONF), encode_vint(2 * len(items))]
+        for k, v in items:
+            kb = str(k).encode()
+            vb = ("" if v is None else str(v)).encode()
+            parts += (encode_vint(len(kb)), kb, encode_vint(len(vb)), vb)
+        msg = b"".join(parts)
         with self._lock:
-            self._int(SET_JOB_CONF)
-            self._int(2 * len(items))
-            for k, v in items:
-                self._bytes(str(k).encode())
-                self._bytes(("" if v is None else str(v)).encode())
+            self.out.write(msg)
 
     def set_input_types(self, key_type, value_type):
         with self._lock:
