@@ -167,7 +167,14 @@ class SimulatedGpuRuntime:
             dev.rr += 1
             live, outs = [], []
             now = time.time()
+            # the real launcher starts an idle device on its first chunk while
+            # it prepares the rest (GpuRuntime._worker): the device time of
+            # this batch starts once that many tasks are prepared
+            first = max(1, self.tracker.conf.get_int("hbmr.gpu.first.chunk", 4))
+            t_first = None
             for r in self._drain(dev, run):
+                if t_first is None and len(live) >= first:
+                    t_first = time.time()
                 if r.kill.is_set():
                     tracker._finish(r, P.KILLED, "killed before start")
                     continue
@@ -204,7 +211,7 @@ class SimulatedGpuRuntime:
                 continue
             # the slots are streams of ONE device: work on any slot queues behind
             # the device's earlier work (task.ms is the device's time per task)
-            start = max(time.time(), dev.busy_until)
+            start = max(t_first or time.time(), dev.busy_until)
             # staged runs of an opened gate: not before the reduce's (simulated)
             # device result is ready
             waits = [r.wait for r in live if isinstance(getattr(r, "wait", None), float)]

@@ -198,7 +198,12 @@ def run_split_reduce(host, run, device=None):
                 release_dependents()
         else:
             real = [m for m in marks if m is not None]
-            if real:
+            if real and getattr(ctx, "simulated_collective_s", None) is not None:
+                # no-data rehearsal: the reduce's device work queues behind the
+                # maps (as the real reduce stream waits on their events) — the
+                # split job orders its simulated result after this time
+                ctx.sim_base = max(real)
+            elif real:
                 # simulated device: the outputs are "ready" at these times
                 delay = max(real) - time.time()
                 if delay > 0:

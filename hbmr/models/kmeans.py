@@ -695,7 +695,7 @@ class KMeansSplitJob(SplitJob):
             else:
                 # rehearsal without data (hbmr.gpu.simulate.nodata): the device
                 # all-reduce is modelled as device time ending at this instant
-                ctx.sim_ready = time.time() + sim
+                ctx.sim_ready = max(time.time(), getattr(ctx, "sim_base", 0.0)) + sim
         sums = packed[:k * dp].view(k, dp)
         counts = packed[k * dp:]
         if self.exact and sums.device.type == "cuda":
@@ -745,6 +745,12 @@ class KMeansSplitJob(SplitJob):
             rel = getattr(ctx, "release_dependents", None)
             if rel is not None:
                 rel()
+            if sim is not None:
+                # the real reduce's host sync on the shift: done when the
+                # (simulated) device result is
+                delay = ctx.sim_ready - time.time()
+                if delay > 0:
+                    time.sleep(delay)
         self._write_output(ctx, counts, new_cen)
         if TRACE.on:
             TRACE.instant("kmeans.output_written")
