@@ -151,3 +151,47 @@ def test_new_api_field_selection(tmp_path):
         want.append("\t" + "-".join([kf[4], kf[3], kf[2], kf[1], kf[0]] + kf))
     assert got == sorted(want)
     _ = KeyValueTextInputFormat
+
+
+class Boom(Mapper):
+    def map(self, key, value, context):
+        raise RuntimeError("boom")
+
+
+def test_new_api_job_control_runs_a_dag(tmp_path):
+    """mapreduce.lib.jobcontrol: b depends on a (reads a's output); c depends
+    on a job that fails and becomes DEPENDENT_FAILED."""
+    import threading
+    from hbmr.mapreduce.lib.jobcontrol import ControlledJob, JobControl, State
+    from hbmr.mapreduce.lib.input import KeyValueTextInputFormat
+
+    inp = tmp_path / "in"
+    inp.mkdir()
+    (inp / "a.txt").write_text("3\n1\n2\n")
+
+    def mk(name, mapper, src, dst):
+        j = _job(tmp_path, name)
+        j.setMapperClass(mapper)
+        j.setNumReduceTasks(0)
+        j.setOutputKeyClass(Text)
+        j.setOutputValueClass(IntWritable)
+        FileInputFormat.addInputPath(j, src)
+        FileOutputFormat.setOutputPath(j, dst)
+        return j
+    a = ControlledJob(mk("a", EvenOnly, inp, tmp_path / "oa"))
+    b = ControlledJob(mk("b", Mapper, tmp_path / "oa", tmp_path / "ob"), [a])
+    bad = ControlledJob(mk("bad", Boom, inp, tmp_path / "obad"))
+    bad.getJob().getConfiguration().set_int("mapred.map.max.attempts", 1)
+    c = ControlledJob(mk("c", Mapper, inp, tmp_path / "oc"), [bad])
+    jc = JobControl("g")
+    jc.addJobCollection([a, b, bad, c])
+    assert [j.getJobID() for j in (a, b, bad, c)] == ["g1", "g2", "g3", "g4"]
+    t = threading.Thread(target=jc.run)
+    t.start()
+    t.join(60)
+    assert jc.allFinished()
+    assert a.getJobState() == b.getJobState() == State.SUCCESS
+    assert bad.getJobState() == State.FAILED and c.getJobState() == State.DEPENDENT_FAILED
+    assert set(jc.getSuccessfulJobList()) == {a, b} and set(jc.getFailedJobList()) == {bad, c}
+    assert sorted(_lines(tmp_path / "ob", "part-")) == ["0\t2\t2"]
+    _ = KeyValueTextInputFormat
