@@ -38,12 +38,54 @@ def wall_ns(perf_ns: int) -> int:
     return _WALL0 + (perf_ns - _PERF0)
 
 
+class _Roctx:
+    """roctx markers (``HBMR_ROCTX=1``): every traced instant becomes a
+    roctxMark and every span a roctxRangePush/Pop, so a ``rocprofv3
+    --marker-trace`` timeline shows the control plane's events beside the
+    kernels (libroctx64 from the ROCm install; silently off if absent)."""
+
+    def __init__(self):
+        self.lib = None
+        if os.environ.get("HBMR_ROCTX") != "1":
+            return
+        import ctypes
+        for name in ("libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
+            try:
+                lib = ctypes.CDLL(name)
+                lib.roctxMarkA.argtypes = [ctypes.c_char_p]
+                lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                lib.roctxRangePushA.restype = ctypes.c_int
+                lib.roctxRangePop.restype = ctypes.c_int
+                self.lib = lib
+                return
+            except (OSError, AttributeError):
+                continue
+
+    def mark(self, name, args):
+        self.lib.roctxMarkA(_label(name, args))
+
+    def push(self, name, args):
+        self.lib.roctxRangePushA(_label(name, args))
+
+    def pop(self):
+        self.lib.roctxRangePop()
+
+
+def _label(name, args):
+    if not args:
+        return name.encode()
+    return (name + " " + " ".join(f"{k}={v}" for k, v in args.items()))[:200].encode()
+
+
 class Tracer:
     def __init__(self):
         self.on = False
         self.events: list = []
         self.max_events = 2_000_000
         self._dump_path = None
+        self.roctx = _Roctx()
+        if self.roctx.lib is not None:
+            self.on = True
 
     def enable(self, dump_path: str | None = None):
         self.on = True
@@ -61,6 +103,8 @@ class Tracer:
     def instant(self, name, **args):
         if self.on and len(self.events) < self.max_events:
             self.events.append((_now(), threading.current_thread().name, "i", name, 0, args))
+            if self.roctx.lib is not None:
+                self.roctx.mark(name, args)
 
     def complete(self, name, t0_ns, t1_ns, track=None, **args):
         if self.on and len(self.events) < self.max_events:
@@ -73,9 +117,14 @@ class Tracer:
             yield
             return
         t0 = _now()
+        rx = self.roctx.lib is not None
+        if rx:
+            self.roctx.push(name, args)
         try:
             yield
         finally:
+            if rx:
+                self.roctx.pop()
             self.complete(name, t0, _now(), **args)
 
     # -- queries --------------------------------------------------------------------------

@@ -4,6 +4,8 @@ import json
 import os
 import urllib.request
 
+import pytest
+
 from hbmr import cli
 from hbmr.examples.sleepjob import split_sleep_conf
 from hbmr.mapred.cluster import LocalCluster
@@ -68,3 +70,27 @@ def test_cli_fs_and_version(tmp_path, capsys):
     assert "hello" in out and "Found 1 items" in out
     assert cli.main(["fs", "-rmr", str(tmp_path / "d")]) == 0
     assert not (tmp_path / "d").exists()
+
+
+def test_roctx_markers_when_requested():
+    """HBMR_ROCTX=1 turns tracer events into roctx marks / ranges (libroctx64)
+    for rocprofv3 --marker-trace timelines; without it the tracer stays off."""
+    import subprocess
+    import sys
+    code = ("from hbmr.utils.trace import TRACE\n"
+            "TRACE.instant('job.submit', job='j1')\n"
+            "with TRACE.span('reduce', n=3):\n    pass\n"
+            "print(TRACE.on, TRACE.roctx.lib is not None, len(TRACE.events))\n")
+    env = dict(os.environ, HBMR_ROCTX="1", PYTHONPATH=os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr
+    on, lib, n = out.stdout.split()
+    assert on == "True" and n == "2"
+    if lib != "True":
+        pytest.skip("libroctx64 not installed")
+    env.pop("HBMR_ROCTX")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                         timeout=120)
+    assert out.stdout.split()[:2] == ["False", "False"]
