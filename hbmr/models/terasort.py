@@ -115,6 +115,9 @@ class TeraSortSplitJob(SplitJob):
         # its maps are done — with an early reduce (expect mode,
         # hbmr.job.prestage) it overlaps the later maps (map ∥ shuffle)
         self.waves = max(1, conf.get_int("hbmr.terasort.shuffle.waves", 1))
+        # one-rank reduce: sort (high key word, packed record id) and gather by
+        # the id (false: the v3 path, sort keys then gather through a permutation)
+        self.gid = conf.get_boolean("hbmr.terasort.reduce.gid", True)
 
     # -- splits + sampling (JobTracker side) -----------------------------------------
     def _ranges(self):
@@ -301,7 +304,13 @@ class TeraSortSplitJob(SplitJob):
 
     def _sorted_partition(self, his, los, rows, starts, lens, bases, dev, stream=None):
         """Collect one partition's pieces from every map output, sort its keys,
-        gather its records: (records, sorted hi, sorted lo)."""
+        gather its records: (records, sorted hi, sorted lo).  The packed-id
+        path (v4, hbmr.terasort.reduce.gid) when the map outputs allow it."""
+        if self.gid and len(bases) <= S.GID_MAX_SPLITS and \
+                max(b.shape[0] for b in bases) < S.GID_MAX_ROWS:
+            got = S.sort_gathered(his, rows, starts, lens, bases, stream=stream)
+            if got is not None:
+                return got
         h, lw, split, row = S.tera_collect(his, los, rows, starts, lens, stream=stream)
         perm, hs, ls = S.sort_keys(h, lw, stream=stream)
         del h, lw

@@ -415,6 +415,83 @@ def tera_collect(his, los, rows, starts, lens, with_keys=True, stream=None):
     return ohi, olo, split, row
 
 
+GID_MAX_SPLITS = 256
+GID_MAX_ROWS = 1 << 24
+
+
+def tera_collect_gid(his, rows, starts, lens, stream=None):
+    """Pieces [starts[s], +lens[s]) of per-split (hi, row) arrays → (hi, gid)
+    with gid = s << 24 | row (int32 storage): the record ids the v4 reduce
+    sorts and gathers by (at most 256 splits of < 2^24 records)."""
+    S = len(rows)
+    if S > GID_MAX_SPLITS:
+        raise ValueError(f"at most {GID_MAX_SPLITS} map outputs per packed-id collect")
+    n = int(sum(lens))
+    dev = rows[0].device
+    if not _on_gpu(rows[0]):
+        sel = [slice(int(a), int(a) + int(m)) for a, m in zip(starts, lens)]
+        gid = torch.cat([(r[sl].to(torch.int64) | (s << 24)).to(torch.int32)
+                         for s, (r, sl) in enumerate(zip(rows, sel))])
+        return torch.cat([h[sl] for h, sl in zip(his, sel)]), gid
+    prefix = np.zeros(S + 1, dtype=np.int64)
+    np.cumsum(np.asarray(lens, dtype=np.int64), out=prefix[1:])
+    meta = torch.from_numpy(np.concatenate([np.asarray(starts, dtype=np.int64), prefix])).to(dev)
+    ohi = torch.empty(n, dtype=torch.int64, device=dev)
+    gid = torch.empty(n, dtype=torch.int32, device=dev)
+    th, tr = _ptr_table(his, dev), _ptr_table(rows, dev)
+    rc = _lib.load().hbmr_tera_collect_gid(_ptr(th), _ptr(tr), _ptr(meta), _ptr(meta) + 8 * S, S,
+                                            n, _ptr(ohi), _ptr(gid), _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_tera_collect_gid")
+    return ohi, gid
+
+
+def gather_records_gid(bases, gid: torch.Tensor, stream=None) -> torch.Tensor:
+    """out[i] = bases[gid[i] >> 24][gid[i] & 0xFFFFFF] (100-byte records)."""
+    n = gid.numel()
+    rb = bases[0].shape[1]
+    if not _on_gpu(gid):
+        g = gid.to(torch.int64) & 0xFFFFFFFF
+        s, r = g >> 24, g & 0xFFFFFF
+        res = torch.empty(n, rb, dtype=torch.uint8)
+        for j, b in enumerate(bases):
+            m = s == j
+            if m.any():
+                res[m] = b[r[m]]
+        return res
+    res = torch.empty(n, rb, dtype=torch.uint8, device=gid.device)
+    tb = _ptr_table(bases, gid.device)
+    rc = _lib.load().hbmr_gather_records_gid(_ptr(tb), _ptr(gid), n, rb, _ptr(res),
+                                              _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_gather_records_gid")
+    return res
+
+
+def sort_gathered(his, rows, starts, lens, bases, stream=None):
+    """TeraSort reduce v4 for one group: (hi, gid) collect, 8 radix passes over
+    hi carrying the gid, ONE record gather by gid, the low key words read back
+    from the sorted records, and runs of equal hi ordered by them in place.
+    Returns (records, hi, lo), or None when a run of equal high words is too
+    long for the in-place fix-up (the caller takes the full-key path)."""
+    h, gid = tera_collect_gid(his, rows, starts, lens, stream=stream)
+    radix_sort_pairs(h, gid, 0, 64, stream=stream)
+    recs = gather_records_gid(bases, gid, stream=stream)
+    del gid
+    _h2, lo = tera_keys(recs, stream=stream)
+    del _h2
+    if not _on_gpu(recs):
+        order = np.lexsort((lo.numpy().view(np.uint64), h.numpy().view(np.uint64)))
+        o = torch.from_numpy(order)
+        return recs[o], h[o], lo[o]
+    flag = torch.zeros(1, dtype=torch.int32, device=recs.device)
+    rc = _lib.load().hbmr_tera_tie_fix_records(_ptr(h), _ptr(lo), _ptr(recs), recs.shape[0],
+                                                recs.shape[1], _ptr(flag),
+                                                _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_tera_tie_fix_records")
+    if int(flag.item()):
+        return None
+    return recs, h, lo
+
+
 def gather_records_multi(bases, split: torch.Tensor, row: torch.Tensor, perm=None,
                          out=None, stream=None) -> torch.Tensor:
     """out[i] = bases[split[k]][row[k]], k = perm[i] (or i): 100-byte records

@@ -783,6 +783,89 @@ __global__ __launch_bounds__(256) void merge_path_kernel(
   }
 }
 
+// ---- TeraSort reduce v4: packed record ids ------------------------------------
+// A group's records are named by a 32-bit gid = split << 24 | row (splits < 256,
+// rows < 2^24): the key sort carries the gid itself, so the record gather makes
+// ONE dependent index load per record (v3: perm, then split and row).
+__global__ __launch_bounds__(256) void tera_collect_gid_kernel(
+    const uint64_t* const* __restrict__ his, const uint32_t* const* __restrict__ rows,
+    const long* __restrict__ starts, const long* __restrict__ prefix, int S, long n,
+    uint64_t* __restrict__ ohi, uint32_t* __restrict__ ogid) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    int a = 0, b = S;          // largest s with prefix[s] <= i
+    while (b - a > 1) {
+      const int m = (a + b) >> 1;
+      if (prefix[m] <= i) a = m; else b = m;
+    }
+    const long j = starts[a] + (i - prefix[a]);
+    ohi[i] = his[a][j];
+    ogid[i] = ((uint32_t)a << 24) | rows[a][j];
+  }
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void gather_records_gid_kernel(
+    const uint32_t* const* __restrict__ bases, const uint32_t* __restrict__ gid, long n,
+    int words, uint32_t* __restrict__ dst) {
+  const int rpb = 256 / words;
+  const int t = threadIdx.x;
+  if (t >= rpb * words) return;
+  const int lr = t / words;
+  const int w = t - lr * words;
+  const long stride = (long)gridDim.x * rpb;
+  for (long r0 = (long)blockIdx.x * rpb + lr; r0 < n; r0 += stride * U) {
+    const uint32_t* src[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const long r = r0 + j * stride;
+      src[j] = nullptr;
+      if (r < n) {
+        const uint32_t g = gid[r];
+        src[j] = bases[g >> 24] + (long)(g & 0xFFFFFFu) * words;
+      }
+    }
+    uint32_t v[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) v[j] = src[j] ? src[j][w] : 0u;
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const long r = r0 + j * stride;
+      if (r < n) dst[r * words + w] = v[j];
+    }
+  }
+}
+
+// After the hi-only sort and the record gather: order each run of equal hi by
+// lo, moving the (already gathered) records themselves; runs longer than
+// kTieRun are flagged for the full-key path.
+__global__ __launch_bounds__(256) void tera_tie_fix_records_kernel(
+    const uint64_t* __restrict__ hi, uint64_t* __restrict__ lo, uint32_t* __restrict__ rec,
+    long n, int words, unsigned int* __restrict__ flag) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n - 1) return;
+  const uint64_t h = hi[i];
+  if (hi[i + 1] != h || (i > 0 && hi[i - 1] == h)) return;
+  long e = i + 1;
+  while (e < n && hi[e] == h && e - i < kTieRun) ++e;
+  if (e < n && hi[e] == h) {
+    atomicOr(flag, 1u);
+    return;
+  }
+  // insertion sort by adjacent swaps (no per-lane record buffer)
+  for (long a = i + 1; a < e; ++a) {
+    for (long b = a - 1; b >= i && lo[b] > lo[b + 1]; --b) {
+      const uint64_t t = lo[b];
+      lo[b] = lo[b + 1];
+      lo[b + 1] = t;
+      for (int w = 0; w < words; ++w) {
+        const uint32_t x = rec[b * words + w];
+        rec[b * words + w] = rec[(b + 1) * words + w];
+        rec[(b + 1) * words + w] = x;
+      }
+    }
+  }
+}
+
 inline long ceil_div(long a, long b) { return (a + b - 1) / b; }
 
 }  // namespace
@@ -968,6 +1051,39 @@ int hbmr_merge_path(const uint64_t* ahi, const uint64_t* alo, const uint32_t* av
   if (na < 0 || nb < 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(merge_path_kernel, dim3((unsigned)ceil_div(ceil_div(n, kMergeItems), 256)),
                      dim3(256), 0, st, ahi, alo, av, na, bhi, blo, bv, nb, ohi, olo, ov);
+  return (int)hipGetLastError();
+}
+
+int hbmr_tera_collect_gid(const uint64_t* const* his, const uint32_t* const* rows,
+                          const long* starts, const long* prefix, int S, long n, uint64_t* ohi,
+                          uint32_t* ogid, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (S <= 0 || S > 256) return (int)hipErrorInvalidValue;
+  const long grid = std::min<long>(ceil_div(n, 256), 256L * 256);
+  hipLaunchKernelGGL(tera_collect_gid_kernel, dim3((unsigned)grid), dim3(256), 0, st, his, rows,
+                     starts, prefix, S, n, ohi, ogid);
+  return (int)hipGetLastError();
+}
+
+int hbmr_gather_records_gid(const void* const* bases, const uint32_t* gid, long n,
+                            int record_bytes, void* dst, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (record_bytes % 4 || record_bytes > 4 * 64) return (int)hipErrorInvalidValue;
+  const int words = record_bytes / 4;
+  constexpr int U = 4;
+  const long grid = std::min<long>(ceil_div(n, (256 / words) * U), 1L << 18);
+  hipLaunchKernelGGL(gather_records_gid_kernel<U>, dim3((unsigned)grid), dim3(256), 0, st,
+                     reinterpret_cast<const uint32_t* const*>(bases), gid, n, words,
+                     reinterpret_cast<uint32_t*>(dst));
+  return (int)hipGetLastError();
+}
+
+int hbmr_tera_tie_fix_records(const uint64_t* hi, uint64_t* lo, void* rec, long n,
+                              int record_bytes, unsigned int* flag, hipStream_t st) {
+  if (n <= 1) return 0;
+  if (record_bytes % 4 || record_bytes > 4 * 64) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(tera_tie_fix_records_kernel, dim3((unsigned)ceil_div(n - 1, 256)), dim3(256),
+                     0, st, hi, lo, reinterpret_cast<uint32_t*>(rec), n, record_bytes / 4, flag);
   return (int)hipGetLastError();
 }
 

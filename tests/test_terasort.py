@@ -333,3 +333,36 @@ def test_gpu_merge_runs_matches_cpu(sizes):
     hc, lc, vc = S.merge_runs(runs)
     hg, lg, vg = S.merge_runs([(a.cuda(), b.cuda(), c.cuda()) for a, b, c in runs])
     assert torch.equal(hg.cpu(), hc) and torch.equal(lg.cpu(), lc) and torch.equal(vg.cpu(), vc)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ties", [0, 5, 100])
+def test_gpu_sort_gathered_packed_ids(ties):
+    """Reduce v4 (hi + packed-id sort, one gather, lo from the gathered records,
+    in-place tie fix-up): the records of three map outputs come out in key
+    order; ties = equal 8-byte prefixes per run (100: longer than the fix-up
+    handles -> None, the caller's full-key path)."""
+    parts_c = [torch.from_numpy(S.teragen_cpu(1000 * i, 20_000 + i)) for i in range(3)]
+    if ties:
+        for p in parts_c:
+            p[:ties * 40, :8] = p[0, :8]          # runs of equal high words
+    parts = [p.cuda() for p in parts_c]
+    outs = [S.tera_partition(p, torch.zeros(0, dtype=torch.int64),
+                             torch.zeros(0, dtype=torch.int64)) for p in parts]
+    his = [o[0] for o in outs]
+    rows = [o[2] for o in outs]
+    lens = [p.shape[0] for p in parts]
+    got = S.sort_gathered(his, rows, [0, 0, 0], lens, parts)
+    if ties == 100:
+        assert got is None
+        return
+    recs, hs, ls = got
+    allr = torch.cat(parts_c).numpy()
+    keys = allr[:, :10]
+    order = np.lexsort([keys[:, j] for j in range(9, -1, -1)])
+    want = allr[order]
+    r = recs.cpu().numpy()
+    assert np.array_equal(r[:, :10], want[:, :10])
+    assert S.count_unsorted(hs, ls) == 0
+    # the same multiset of records (equal keys may come in either order)
+    assert sorted(map(bytes, r)) == sorted(map(bytes, want))
