@@ -343,9 +343,12 @@ def test_gpu_sort_gathered_packed_ids(ties):
     order; ties = equal 8-byte prefixes per run (100: longer than the fix-up
     handles -> None, the caller's full-key path)."""
     parts_c = [torch.from_numpy(S.teragen_cpu(1000 * i, 20_000 + i)) for i in range(3)]
-    if ties:
-        for p in parts_c:
-            p[:ties * 40, :8] = p[0, :8]          # runs of equal high words
+    for p in parts_c:
+        if ties == 100:
+            p[:100, :8] = p[0, :8]                 # one run longer than the fix-up
+        else:
+            for k in range(ties):                  # runs of 8 equal high words
+                p[k * 8:(k + 1) * 8, :8] = p[k * 8, :8]
     parts = [p.cuda() for p in parts_c]
     outs = [S.tera_partition(p, torch.zeros(0, dtype=torch.int64),
                              torch.zeros(0, dtype=torch.int64)) for p in parts]
