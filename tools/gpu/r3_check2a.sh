@@ -3,7 +3,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-P=${P:-r3i}
+P=${P:-r3j}
 timeout -k 10 500 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests \
   > gpurun_out/${P}_gpu_tests.txt 2>&1; rc=$?
 tail -3 gpurun_out/${P}_gpu_tests.txt; [ $rc -eq 0 ] || exit $rc
@@ -16,3 +16,5 @@ tail -1 gpurun_out/${P}_write_input.txt
 timeout -k 10 300 python bench.py --steps 10 --warmup 3 --input /tmp/km100m > gpurun_out/${P}_bench_file.json 2> gpurun_out/${P}_bench_file.err || { tail -5 gpurun_out/${P}_bench_file.err; exit 1; }
 tail -1 gpurun_out/${P}_bench_file.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('file', d['ms_per_step'], d['warmup_seconds'], d['phases_ms'])"
 rm -rf /tmp/km100m
+timeout -k 10 400 python tools/bench_terasort.py --rows 1000000000 --split-rows 10000000 --steps 3 > gpurun_out/${P}_tera100_v4.json 2> gpurun_out/${P}_tera100_v4.err || { tail -5 gpurun_out/${P}_tera100_v4.err; exit 1; }
+tail -1 gpurun_out/${P}_tera100_v4.json
