@@ -84,6 +84,9 @@ def main():
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(a.gpus)
 
+    from hbmr.utils.sampler import maybe_start
+    sampler = maybe_start()     # HBMR_SAMPLE_PROF=prefix: control-plane stack sampling
+
     import torch
     if a.simulate_ms is not None and world > 1:
         # N rank processes share this host's cores: no intra-op thread pools
@@ -235,6 +238,8 @@ def main():
         }
         print(json.dumps(out), flush=True)
     finally:
+        if sampler is not None:
+            sampler.dump()
         node.shutdown()
     return 0
 

@@ -73,6 +73,7 @@ class TrackerInfo:
         self.more = False    # the last assignment stopped at the per-heartbeat cap
         self.rack = DEFAULT_RACK
         self.kills: set[str] = set()   # attempts to kill on the next heartbeat
+        self.kill_epoch = -1           # JobTracker.kill_epoch this tracker was last scanned at
         self.extra_actions: list = []  # e.g. restart_gpu_worker, sent on the next heartbeat
 
     def gpu_devices(self):
@@ -470,6 +471,7 @@ class JobTracker:
         # dependent jobs whose GPU maps may already be launched, gated on the
         # job they wait for (hbmr/gpu/gates.py); chains up to prestage.depth
         self.staged: list[JobInProgress] = []
+        self.kill_epoch = 0    # bumped when attempts may have become killable
         self.prestage = conf.get_boolean("hbmr.job.prestage", True)
         self.prestage_depth = max(1, conf.get_int("hbmr.job.prestage.depth", 2))
         self.trackers: dict[str, TrackerInfo] = {}
@@ -794,6 +796,7 @@ class JobTracker:
     def _finish_job(self, jip: JobInProgress, state, info=""):
         if jip.completed():
             return
+        self.kill_epoch += 1          # its attempts still running anywhere get killed
         st = jip.status
         st.state = state
         st.failure_info = info
@@ -989,12 +992,17 @@ class JobTracker:
             # (CPU profiling probes excepted: a sampled probe rides on a TIP that
             # the GPUs finish long before it, and killing it would leave the cost
             # model a censored bound instead of the CPU time)
-            for aid in list(tr.running):
-                a = self.attempt_index.get(aid)
-                if a is not None and not a.profile_only and not a.profile_fraction and (
-                        a.tip.job.completed() or
-                        (a.tip.successful is not None and a.tip.successful is not a)):
-                    tr.kills.add(aid)
+            # (a scan per heartbeat over every running attempt was a top cost of
+            # the JobTracker at 4-8 ranks; only a job ending or a TIP won by one
+            # of several attempts can create work here — kill_epoch counts those)
+            if tr.kill_epoch != self.kill_epoch:
+                tr.kill_epoch = self.kill_epoch
+                for aid in list(tr.running):
+                    a = self.attempt_index.get(aid)
+                    if a is not None and not a.profile_only and not a.profile_fraction and (
+                            a.tip.job.completed() or
+                            (a.tip.successful is not None and a.tip.successful is not a)):
+                        tr.kills.add(aid)
             if tr.kills:
                 actions += [P.kill_task_action(aid) for aid in sorted(tr.kills)]
                 tr.kills.clear()
@@ -1080,6 +1088,8 @@ class JobTracker:
         if tip.successful is not None or tip.killed:
             return  # a speculative twin already won
         tip.successful = a
+        if len(tip.attempts) > 1:
+            self.kill_epoch += 1      # its twins (speculative / probe) may need killing
         if tip.is_map:
             jip.maps_done += 1
         else:
@@ -1170,6 +1180,8 @@ class JobTracker:
                     tr.running.discard(a.aid)
                     tr.running_gpu[a.device] = max(0, tr.running_gpu.get(a.device, 1) - 1)
                 tip.successful = a
+                if len(tip.attempts) > 1:
+                    self.kill_epoch += 1
                 jp.maps_done += 1
                 jp.finished_gpu_maps += 1
                 jp.completion_events.append({"map": str(tip.tid), "attempt": a.aid,

@@ -1,0 +1,108 @@
+"""A sampling profiler for the control plane: a daemon thread snapshots every
+thread's Python stack (``sys._current_frames``) every ``interval`` seconds and
+counts (thread-name prefix, function) samples — self time and inclusive time
+— so the JobTracker's and TaskTracker's threads can be profiled inside a live
+multi-rank run, where cProfile (one thread, heavy overhead) cannot.
+
+``HBMR_SAMPLE_PROF=/path/prefix`` in a bench or node process starts it; the
+report is written to ``<prefix>_<pid>.txt`` at exit."""
+from __future__ import annotations
+
+import atexit
+import collections
+import os
+import sys
+import threading
+import time
+
+
+class Sampler:
+    def __init__(self, interval=0.0005):
+        self.interval = interval
+        self.self_counts = collections.Counter()
+        self.incl_counts = collections.Counter()
+        self.thread_counts = collections.Counter()
+        self.samples = 0
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True, name="hbmr-sampler")
+
+    def start(self):
+        self._t.start()
+        return self
+
+    def stop(self):
+        self._stop.set()
+
+    def _run(self):
+        me = threading.get_ident()
+        while not self._stop.is_set():
+            names = {t.ident: t.name for t in threading.enumerate()}
+            for tid, frame in sys._current_frames().items():
+                if tid == me:
+                    continue
+                tname = names.get(tid, "?")
+                group = tname.split("-")[0] if "-" in tname else tname
+                if _idle(frame):
+                    continue
+                self.thread_counts[group] += 1
+                f = frame
+                key = _key(f)
+                self.self_counts[(group, key)] += 1
+                seen = set()
+                while f is not None:
+                    k = _key(f)
+                    if k not in seen:
+                        self.incl_counts[(group, k)] += 1
+                        seen.add(k)
+                    f = f.f_back
+            self.samples += 1
+            time.sleep(self.interval)
+
+    def report(self, top=40):
+        lines = [f"samples {self.samples} (interval {self.interval * 1e3:.2f} ms); busy "
+                 f"samples per thread group:"]
+        for g, n in self.thread_counts.most_common():
+            lines.append(f"  {n:7d}  {g}")
+        lines.append("\nself time (busy samples):")
+        for (g, k), n in self.self_counts.most_common(top):
+            lines.append(f"  {n:7d}  {g:<24} {k}")
+        lines.append("\ninclusive time (busy samples):")
+        for (g, k), n in self.incl_counts.most_common(top):
+            lines.append(f"  {n:7d}  {g:<24} {k}")
+        return "\n".join(lines)
+
+
+_IDLE = {"wait", "_wait_for_tstate_lock", "select", "accept", "recv_into", "recv", "get",
+         "sleep", "poll", "_recv_bytes", "readinto", "acquire", "_worker", "serve_forever",
+         "wait_for", "result", "join", "_recv_exact", "barrier", "serve_until_shutdown",
+         "recv_msg", "_wait"}
+
+
+def _idle(frame):
+    """A thread blocked in a wait/recv/select (its innermost Python frame)."""
+    return frame.f_code.co_name in _IDLE
+
+
+def _key(f):
+    c = f.f_code
+    fn = c.co_filename
+    i = fn.find("hbmr/")
+    fn = fn[i:] if i >= 0 else os.path.basename(fn)
+    return f"{fn}:{c.co_firstlineno} {c.co_name}"
+
+
+def maybe_start():
+    prefix = os.environ.get("HBMR_SAMPLE_PROF")
+    if not prefix:
+        return None
+    s = Sampler(float(os.environ.get("HBMR_SAMPLE_PROF_INTERVAL", "0.0005"))).start()
+
+    def dump():
+        if s._stop.is_set():
+            return
+        s.stop()
+        with open(f"{prefix}_{os.getpid()}.txt", "w") as f:
+            f.write(s.report())
+    s.dump = dump
+    atexit.register(dump)
+    return s
