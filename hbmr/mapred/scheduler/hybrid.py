@@ -302,6 +302,10 @@ class HybridTaskScheduler(TaskScheduler):
             return True
         if jip.pending_maps or jip.running_cpu:
             return False
+        # cheap necessary condition first (this runs on every heartbeat until
+        # it holds): one running GPU attempt per unfinished map
+        if jip.running_gpu != len(jip.maps) - jip.maps_done:
+            return False
         for t in jip.maps:
             if t.successful is None:
                 ra = t.running_attempts()

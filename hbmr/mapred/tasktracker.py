@@ -470,8 +470,14 @@ class TaskTracker:
                 self._stop.wait(min(1.0, self.interval * 5))
 
     def _check_timeouts(self):
-        """markUnresponsiveTasks: fail attempts without progress for mapred.task.timeout."""
+        """markUnresponsiveTasks: fail attempts without progress for mapred.task.timeout.
+        At most every 0.1 s: the heartbeat loop turns over once per completion
+        notification, and a scan of every running attempt each time showed up
+        in control-plane profiles (timeouts are whole seconds or more)."""
         now = time.time()
+        if now - getattr(self, "_last_timeout_scan", 0.0) < 0.1:
+            return
+        self._last_timeout_scan = now
         with self._lock:
             runs = list(self.running.values())
         for r in runs:
