@@ -116,8 +116,9 @@ class TeraSortSplitJob(SplitJob):
         # hbmr.job.prestage) it overlaps the later maps (map ∥ shuffle)
         self.waves = max(1, conf.get_int("hbmr.terasort.shuffle.waves", 1))
         # one-rank reduce: sort (high key word, packed record id) and gather by
-        # the id (false: the v3 path, sort keys then gather through a permutation)
-        self.gid = conf.get_boolean("hbmr.terasort.reduce.gid", True)
+        # the id (v4; default: the v3 path, sort keys then gather through a
+        # permutation — v4 stays opt-in until it has been measured on the GPU)
+        self.gid = conf.get_boolean("hbmr.terasort.reduce.gid", False)
 
     # -- splits + sampling (JobTracker side) -----------------------------------------
     def _ranges(self):

@@ -64,7 +64,6 @@ def test_two_ranks_one_gpu_device_collectives_match_in_process(tmp_path):
 
     import mp_device
     conf = JobConf()
-    conf.set_boolean("hbmr.job.prestage", True)
     with LocalCluster(conf, num_trackers=2, gpus=[[0], [0]], cpu_slots=0) as cl:
         ip = mp_device.run_jobs(cl.submit_job, lambda rj: rj._impl.jip.result[0], conf,
                                 str(tmp_path / "ip"))

@@ -49,8 +49,8 @@ def run_jobs(submit, result_of, conf, work):
     res["terasort"] = digest_dir(os.path.join(work, "ts"))
     res["terasort_counters"] = collective_counters(rj)
     # the same sort with the shuffle in 3 waves (each wave's all-to-all-v
-    # issued once its maps are done, the reduce started early) and sorted runs
-    # merged on arrival (K8)
+    # issued once its maps are done; with hbmr.job.prestage the reduce starts
+    # early and the waves overlap the maps) and sorted runs merged on arrival (K8)
     wc = T.terasort_conf(conf, rows=400_000, split_rows=50_000,
                          output=os.path.join(work, "tsw"))
     wc.set_int("hbmr.terasort.shuffle.waves", 3)
@@ -72,7 +72,6 @@ def run_jobs(submit, result_of, conf, work):
 def main():
     work = os.environ["HBMR_MP_DIR"]
     conf = JobConf()
-    conf.set_boolean("hbmr.job.prestage", True)     # early (expect-mode) collective reduces
     conf.set_int("mapred.tasktracker.map.cpu.tasks.maximum",
                  int(os.environ.get("HBMR_MP_CPU_SLOTS", "0")))   # >0: CPU dry run
     node = Node(conf)
