@@ -61,14 +61,17 @@ def test_terasort_on_cluster_sorts_and_validates(tmp_path, trackers, merge, wave
     assert np.array_equal(got, _ref_sorted(rows))
 
 
-@pytest.mark.parametrize("group_bytes", [1, 300_000, 8 << 30])
-def test_terasort_partition_groups_one_rank(tmp_path, group_bytes):
+@pytest.mark.parametrize("group_bytes,gid", [(1, False), (300_000, False), (8 << 30, False),
+                                            (300_000, True), (8 << 30, True)])
+def test_terasort_partition_groups_one_rank(tmp_path, group_bytes, gid):
     """The one-rank reduce sorts consecutive partitions together (one per sort,
-    a few, or all); output files and order are the same."""
+    a few, or all), through the permutation (v3) or packed record ids (v4);
+    output files and order are the same."""
     rows = 12000
     out = tmp_path / "out"
     conf = T.terasort_conf(rows=rows, split_rows=2500, output=str(out), partitions=7)
     conf.set("hbmr.terasort.reduce.group.bytes", str(group_bytes))
+    conf.set_boolean("hbmr.terasort.reduce.gid", gid)
     with LocalCluster(JobConf(), num_trackers=1, cpu_slots=2) as cl:
         rj = cl.submit_job(conf)
         rj.waitForCompletion(120)
