@@ -353,8 +353,14 @@ class HybridTaskScheduler(TaskScheduler):
     def _straggler(self, jip, now):
         """A running map whose only attempt is on a CPU (or has run > slowdown ×
         the GPU estimate) and has no backup yet."""
+        # a scan finds the earliest time any running attempt can become a
+        # straggler; until then (at most 0.25 s, so attempts launched since are
+        # looked at soon) idle-GPU heartbeats skip the O(maps) scan
+        if now < getattr(jip, "_no_straggler_until", 0.0):
+            return None
         cm = self.jt.cost_model
         t_gpu, _ = cm.stats(jip.signature, True).estimate(now)
+        next_check = now + 0.25
         for tip in jip.maps:
             if tip.is_complete():
                 continue
@@ -366,11 +372,15 @@ class HybridTaskScheduler(TaskScheduler):
             if self.policy == "stock":
                 if elapsed > self.stock_lag:
                     return tip
+                next_check = min(next_check, a.start + self.stock_lag)
                 continue
-            if not a.run_on_gpu and t_gpu is not None and elapsed > t_gpu * 2:
+            if t_gpu is None:
+                continue
+            limit = t_gpu * 2 if not a.run_on_gpu else self.speculate_after * t_gpu + 1.0
+            if elapsed > limit:
                 return tip
-            if a.run_on_gpu and t_gpu is not None and elapsed > self.speculate_after * t_gpu + 1.0:
-                return tip
+            next_check = min(next_check, a.start + limit)
+        jip._no_straggler_until = next_check
         return None
 
 
