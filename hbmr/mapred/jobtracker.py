@@ -176,6 +176,7 @@ class TaskInProgress:
 class JobInProgress:
     def __init__(self, jt, job_id: JobID, conf):
         self.jt = jt
+        self.fold_lock = threading.Lock()
         self.job_id = job_id
         self.conf = conf
         self.status = JobStatus(job_id, PREP)
@@ -440,7 +441,10 @@ class _JTJobHandle:
         return self.jip.status
 
     def counters(self):
-        with self.jip.jt.lock:
+        # folding needs no JobTracker lock (pending_counters is swapped
+        # atomically and Counters locks itself): a client reading counters must
+        # not stall every tracker's heartbeat
+        with self.jip.fold_lock:
             return self.jip.fold_counters()
 
     def wait(self, timeout=None):
