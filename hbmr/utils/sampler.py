@@ -21,6 +21,7 @@ class Sampler:
         self.interval = interval
         self.self_counts = collections.Counter()
         self.incl_counts = collections.Counter()
+        self.line_counts = collections.Counter()
         self.thread_counts = collections.Counter()
         self.samples = 0
         self._stop = threading.Event()
@@ -48,6 +49,7 @@ class Sampler:
                 f = frame
                 key = _key(f)
                 self.self_counts[(group, key)] += 1
+                self.line_counts[(group, f"{key} @{f.f_lineno}")] += 1
                 seen = set()
                 while f is not None:
                     k = _key(f)
@@ -65,6 +67,10 @@ class Sampler:
             lines.append(f"  {n:7d}  {g}")
         lines.append("\nself time (busy samples):")
         for (g, k), n in self.self_counts.most_common(top):
+            lines.append(f"  {n:7d}  {g:<24} {k}")
+        lines.append("\nself time by line (a line that blocks in C, e.g. a lock "
+                     "acquire or the GIL, shows here):")
+        for (g, k), n in self.line_counts.most_common(top // 2):
             lines.append(f"  {n:7d}  {g:<24} {k}")
         lines.append("\ninclusive time (busy samples):")
         for (g, k), n in self.incl_counts.most_common(top):

@@ -11,6 +11,7 @@ timing brackets are sync jobs (every worker synchronises its device).
 
   python tools/bench_terasort.py --rows 1000000000 --split-rows 10000000 --steps 3   # 100 GB
   ... --output /tmp/tera-out   # also time jobs that commit their output (reported alongside)
+  ... -D hbmr.terasort.reduce.gid=true   # job properties (here: the packed-id reduce)
 """
 import argparse
 import json
@@ -29,6 +30,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--output", default=None)
     ap.add_argument("--partitions", type=int, default=0)
+    ap.add_argument("-D", dest="defines", action="append", default=[],
+                    help="key=value job property, e.g. -D hbmr.terasort.reduce.gid=true")
     a = ap.parse_args()
     from hbmr.gpu.syncjob import sync_conf
     from hbmr.mapred.jobconf import JobConf
@@ -40,6 +43,9 @@ def main():
     conf.set_int("mapred.tasktracker.map.gpu.tasks.maximum", 1)
     conf.set_int("hbmr.gpu.queue.depth", 64)
     conf.set_int("mapred.task.timeout", 0)
+    for kv in a.defines:
+        k, _, v = kv.partition("=")
+        conf.set(k, v)
     node = Node(conf)
     if not node.is_master:
         node.serve_until_shutdown()
@@ -99,6 +105,7 @@ def main():
                           "partitions": max(r.get("partitions", 0) for r in res.values()),
                           "peak_hbm_gb_per_gpu": round(max(r.get("peak_hbm_bytes", 0)
                                                            for r in res.values()) / 1e9, 2),
+                          "defines": a.defines,
                           "timeline": rj._impl.jip.timeline(), **out_extra}))
     finally:
         node.shutdown()

@@ -20,3 +20,5 @@ tail -1 gpurun_out/${P}_bench_file.json | python -c "import json,sys; d=json.loa
 rm -rf /tmp/km100m
 timeout -k 10 300 python tools/bench_terasort.py --rows 1000000000 --split-rows 10000000 --steps 3 > gpurun_out/${P}_tera100_v3.json 2> gpurun_out/${P}_tera100_v3.err || { tail -5 gpurun_out/${P}_tera100_v3.err; exit 1; }
 tail -1 gpurun_out/${P}_tera100_v3.json
+timeout -k 10 300 python tools/bench_terasort.py --rows 1000000000 --split-rows 10000000 --steps 3 -D hbmr.terasort.reduce.gid=true > gpurun_out/${P}_tera100_v4.json 2> gpurun_out/${P}_tera100_v4.err || { tail -5 gpurun_out/${P}_tera100_v4.err; exit 1; }
+tail -1 gpurun_out/${P}_tera100_v4.json
