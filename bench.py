@@ -155,6 +155,13 @@ def main():
         for w in range(a.warmup):
             # (no job submitted ahead crosses into the timed window)
             drv.step(prefetch=min(pre, a.warmup - 1 - w))
+            # progress on stderr: a cold first iteration (file input) can take a while
+            J = "org.apache.hadoop.mapred.JobInProgress$Counter"
+            c = drv.history[-1]["counters"] if drv.history else None
+            print(f"bench: warmup {w + 1}/{a.warmup} done at {time.time() - t_setup:.2f} s" +
+                  (f" (last job: cpu maps {c.get(J, 'CPU_MAP_TASKS')}, gpu maps "
+                   f"{c.get(J, 'GPU_MAP_TASKS')})" if c is not None else ""),
+                  file=sys.stderr, flush=True)
         t_warm = time.time() - t_setup
         barrier()
         if in_process:
