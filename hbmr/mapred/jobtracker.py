@@ -223,6 +223,10 @@ class JobInProgress:
         # collective reduce was launched before its maps finished ("expect")
         self.staged_on: str | None = None
         self.staged_launched: dict = {}
+        # map TIPs by the trackers their attempts were launched on: a collective
+        # reduce collects its tracker's outputs from here, not from every map
+        self.launched_on: dict = {}
+        self.loc_counts = [0, 0, 0]     # HBM-local, data-local, rack-local maps
         self.pending_finish = False
         self.expect_mode = False
 
@@ -295,7 +299,16 @@ class JobInProgress:
         return self.maps_done == len(self.maps)
 
     def fold_counters(self) -> Counters:
-        """Merge the counters of newly succeeded attempts into the job's."""
+        """Merge the counters of newly succeeded attempts (and the locality
+        levels counted by obtain_map) into the job's."""
+        lc = self.loc_counts
+        if any(lc):
+            hbm, data, rack = lc
+            self.loc_counts = [0, 0, 0]
+            for name, v in (("HBM_LOCAL_MAPS", hbm), ("DATA_LOCAL_MAPS", data),
+                            ("RACK_LOCAL_MAPS", rack)):
+                if v:
+                    self.counters.incr(C.JOB_GROUP, name, v)
         pend, self.pending_counters = self.pending_counters, []
         for d in pend:
             if d:
@@ -309,10 +322,9 @@ class JobInProgress:
         key = (tracker.name, device if on_gpu else None)
         idx = self._loc_index.get(key)
         if idx is None or idx[4] != len(tracker.cached):
-            lv0, lv1, lv2, lv3 = [], [], [], []
+            lv0, lv1, lv2, rest = [], [], [], []
             cached_keys = {k for k, _ in tracker.cached}
             host = tracker.status.host
-            topo = self.jt.topology
             for tip in self.pending_maps:
                 sk = tip.split_key()
                 locs = tip.locations()
@@ -322,11 +334,20 @@ class JobInProgress:
                     lv1.append(tip)
                 elif tracker.name in locs or host in locs:
                     lv2.append(tip)
-                elif locs and tracker.rack in topo.resolve(locs):
-                    lv3.append(tip)
-            idx = [lv0[::-1], lv1[::-1], lv2[::-1], lv3[::-1], len(tracker.cached)]
+                elif locs:
+                    rest.append(tip)
+            # the rack-local level is resolved on first use (delay scheduling
+            # rarely gets there, and the topology lookups were most of a build)
+            idx = [lv0[::-1], lv1[::-1], lv2[::-1], None, len(tracker.cached), rest]
             self._loc_index[key] = idx
         return idx
+
+    def _rack_level(self, tracker, idx):
+        if idx[3] is None:
+            topo = self.jt.topology
+            idx[3] = [t for t in idx[5] if tracker.rack in topo.resolve(t.locations())][::-1]
+            idx[5] = None
+        return idx[3]
 
     def obtain_map(self, tracker: TrackerInfo, on_gpu: bool, device: int, allow_nonlocal=True):
         """findNewMapTask with locality levels: 0 split cached in this device's
@@ -347,7 +368,7 @@ class JobInProgress:
         for level in (0, 1, 2, 3):
             if level == 3 and not allow_nonlocal:
                 return None
-            stack = idx[level]
+            stack = idx[level] if level < 3 else self._rack_level(tracker, idx)
             while stack:
                 tip = stack.pop()
                 if tip in self.pending_maps and not avoid(tip):
@@ -377,13 +398,14 @@ class JobInProgress:
 
     def _count_locality(self, level):
         # JobInProgress.Counter DATA_LOCAL_MAPS / RACK_LOCAL_MAPS (+ hbmr's
-        # HBM-resident level)
+        # HBM-resident level): plain ints, folded into the counters on read
+        lc = self.loc_counts
         if level == 0:
-            self.counters.incr(C.JOB_GROUP, "HBM_LOCAL_MAPS")
+            lc[0] += 1
         if level <= 2:
-            self.counters.incr(C.JOB_GROUP, "DATA_LOCAL_MAPS")
+            lc[1] += 1
         elif level == 3:
-            self.counters.incr(C.JOB_GROUP, "RACK_LOCAL_MAPS")
+            lc[2] += 1
 
     def _take(self, tip):
         del self.pending_maps[tip]
@@ -1390,6 +1412,7 @@ class JobTracker:
         self.attempt_index[a.aid] = a
         tr.running.add(a.aid)
         if tip.is_map:
+            jip.launched_on.setdefault(tr.name, []).append(tip)
             if not jip.t_first_map:
                 jip.t_first_map = a.start
             if on_gpu:
@@ -1434,6 +1457,7 @@ class JobTracker:
         aids = []
         index = self.attempt_index
         running = tr.running
+        jip.launched_on.setdefault(tr.name, []).extend(tips)
         for tip in tips:
             aid = tip._aid_prefix + str(tip.next_attempt)
             tip.next_attempt += 1
@@ -1474,7 +1498,10 @@ class JobTracker:
         (``expect``: plus the single running attempt of every unfinished map)."""
         if jip.collective_reduce:
             out = []
-            for t in jip.maps:
+            # only maps launched on this tracker can have outputs here (a TIP
+            # re-run elsewhere is listed under that tracker too); map order
+            tips = jip.launched_on.get(tracker_name, ())
+            for t in sorted(set(tips), key=lambda t: t.partition):
                 a = t.successful
                 if a is None and expect:
                     ra = t.running_attempts()

@@ -27,12 +27,17 @@ import socket
 import socketserver
 import struct
 import threading
+import time
 
 import msgpack
 
 log = logging.getLogger("hbmr.rpc")
 
 _LEN = struct.Struct(">I")
+
+# per-method (calls, seconds in the handler incl. the reply) of this process's
+# RPC servers; on with HBMR_SAMPLE_PROF (reported by hbmr.utils.sampler)
+RPC_STATS: dict | None = {} if __import__("os").environ.get("HBMR_SAMPLE_PROF") else None
 
 
 def _send(sock, obj):
@@ -115,10 +120,15 @@ class RpcServer:
                     try:
                         if m not in outer.methods:
                             raise AttributeError(f"no RPC method {m!r}")
+                        t0 = time.perf_counter() if RPC_STATS is not None else 0.0
                         with ctx:
                             res = getattr(outer.target, m)(*req.get("a", ()),
                                                            **req.get("k", {}))
                         _send(s, {"r": res})
+                        if RPC_STATS is not None:
+                            st = RPC_STATS.setdefault(m, [0, 0.0])
+                            st[0] += 1
+                            st[1] += time.perf_counter() - t0
                     except Exception as e:  # noqa: BLE001
                         log.debug("rpc %s failed", m, exc_info=True)
                         try:

@@ -243,11 +243,12 @@ class HybridTaskScheduler(TaskScheduler):
         n_red = 0
         expect = jip.expect_mode and not jip.maps_complete()
         for tip in jip.reduces:
+            if jip.collective_reduce and tip.pinned_tracker != tr.name:
+                continue
             if tip.is_complete() or tip.is_running():
                 continue
             if jip.collective_reduce:
-                if tip.pinned_tracker != tr.name:
-                    continue
+                pass
             elif reduce_free < self.slots_per_task(jip, "reduce") or \
                     n_red >= self.max_reduces_per_hb or \
                     n_red >= self.job_limit(jip, "reduce"):

@@ -72,6 +72,11 @@ class Sampler:
                      "acquire or the GIL, shows here):")
         for (g, k), n in self.line_counts.most_common(top // 2):
             lines.append(f"  {n:7d}  {g:<24} {k}")
+        rpc = sys.modules.get("hbmr.mapred.rpc")
+        if rpc is not None and rpc.RPC_STATS:
+            lines.append("\nRPC server methods (calls, total s, mean us):")
+            for m, (n, t) in sorted(rpc.RPC_STATS.items(), key=lambda kv: -kv[1][1]):
+                lines.append(f"  {m:<28} {n:8d} {t:9.3f} {t / max(1, n) * 1e6:9.1f}")
         lines.append("\ninclusive time (busy samples):")
         for (g, k), n in self.incl_counts.most_common(top):
             lines.append(f"  {n:7d}  {g:<24} {k}")
