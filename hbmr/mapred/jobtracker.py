@@ -201,7 +201,7 @@ class JobInProgress:
         self._loc_index: dict = {}
         self.finished_cpu_maps = 0
         self.finished_gpu_maps = 0
-        self.completion_events: list[dict] = []
+        self.completion_events: list = []     # (map TaskID, attempt id, output)
         self.map_index: dict[str, TaskInProgress] = {}
         self.pending_maps: dict = {}   # TIP -> None: not yet started, insertion (FIFO) order
         self.by_split_key: dict = {}
@@ -1130,9 +1130,7 @@ class JobTracker:
                 jip.finished_gpu_maps += 1
             else:
                 jip.finished_cpu_maps += 1
-            jip.completion_events.append({"map": str(tip.tid), "attempt": a.aid,
-                                          "tracker": a.tracker, "output": a.output,
-                                          "gpu": a.run_on_gpu, "device": a.device})
+            jip.completion_events.append((tip.tid, a.aid, a.output))
         # kill other running attempts of this TIP
         for other in tip.running_attempts():
             if other is not a:
@@ -1176,9 +1174,13 @@ class JobTracker:
         index = self.attempt_index
         done = []
         odd = []
+        terminal = P.TERMINAL
+        succeeded = P.SUCCEEDED
+        running = tr.running
+        running_gpu = tr.running_gpu
         for aid in aids:
             a = index.get(aid)
-            if a is None or a.state in P.TERMINAL:
+            if a is None or a.state in terminal:
                 continue
             tip = a.tip
             if a.profile_fraction or tip.successful is not None or tip.killed or \
@@ -1189,35 +1191,30 @@ class JobTracker:
             a.finish = fin
             a.output = out
             a.device_time = dt
-            a.state = P.SUCCEEDED
+            a.state = succeeded
+            jp = tip.job
+            if not a._released:
+                a._released = True
+                if a.gated:
+                    key = (a.tracker, a.device)
+                    jp.staged_launched[key] = max(0, jp.staged_launched.get(key, 1) - 1)
+                jp.running_gpu = max(0, jp.running_gpu - 1)
+                running.discard(aid)
+                running_gpu[a.device] = max(0, running_gpu.get(a.device, 1) - 1)
+            tip.successful = a
+            jp.maps_done += 1
+            jp.finished_gpu_maps += 1
+            # (map id, attempt, output): map_completion_events renders them
+            jp.completion_events.append((tip.tid, aid, out))
             done.append(a)
         if done:
             jip = done[0].tip.job
-            n = 0
-            for a in done:
-                tip = a.tip
-                jp = tip.job
-                if not a._released:
-                    a._released = True
-                    if a.gated:
-                        key = (a.tracker, a.device)
-                        jp.staged_launched[key] = max(0, jp.staged_launched.get(key, 1) - 1)
-                    jp.running_gpu = max(0, jp.running_gpu - 1)
-                    tr.running.discard(a.aid)
-                    tr.running_gpu[a.device] = max(0, tr.running_gpu.get(a.device, 1) - 1)
-                tip.successful = a
-                if len(tip.attempts) > 1:
-                    self.kill_epoch += 1
-                jp.maps_done += 1
-                jp.finished_gpu_maps += 1
-                jp.completion_events.append({"map": str(tip.tid), "attempt": a.aid,
-                                             "tracker": a.tracker, "output": out, "gpu": True,
-                                             "device": a.device})
-                n += 1
-            self.cost_model.tasks_finished(jip.signature, [a.aid for a in done], True, dt)
+            n = len(done)
+            done_ids = [a.aid for a in done]
+            self.cost_model.tasks_finished(jip.signature, done_ids, True, dt)
             if rep.get("counters"):
                 jip.pending_counters.append(rep["counters"])
-            self.history.log("TASKS_FINISHED", attempts=[a.aid for a in done], tracker=tr.name,
+            self.history.log("TASKS_FINISHED", attempts=done_ids, tracker=tr.name,
                              gpu=True, device=done[0].device, finish=fin, device_time=dt)
             METRICS.inc("hbmr_tasks_succeeded_total", n, help="successful task attempts",
                         type="map", where="gpu")
@@ -1521,7 +1518,7 @@ class JobTracker:
             if jip is None:
                 return {"events": [], "num_maps": 0, "state": "UNKNOWN"}
             evs = jip.completion_events[start:]
-            return {"events": [[e["map"], e["attempt"], e["output"]] for e in evs],
+            return {"events": [[str(t), aid, out] for t, aid, out in evs],
                     "num_maps": len(jip.maps), "state": jip.status.state}
 
     # -- RPC-facing job submission protocol (JobSubmissionProtocol) -------------------------
