@@ -84,7 +84,8 @@ def main():
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(a.gpus)
 
-    from hbmr.utils.sampler import maybe_start
+    from hbmr.utils.sampler import maybe_arm_stackdump, maybe_start
+    maybe_arm_stackdump()       # HBMR_STACKDUMP_S=s: thread stacks to stderr every s
     sampler = maybe_start()     # HBMR_SAMPLE_PROF=prefix: control-plane stack sampling
 
     import torch
@@ -166,6 +167,9 @@ def main():
         barrier()
         if in_process:
             torch.cuda.synchronize()
+        cpu0 = time.process_time()
+        if sampler is not None:
+            sampler.mark()
         t0 = time.perf_counter()
         # every timed job is submitted inside the timed window (the first by this
         # loop, each next one while its predecessor runs); none crosses a barrier
@@ -175,6 +179,7 @@ def main():
         if in_process:
             torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        cpu_rank0 = time.process_time() - cpu0
         hist = drv.history[a.warmup:]
         if a.verbose:
             J = "org.apache.hadoop.mapred.JobInProgress$Counter"
@@ -233,6 +238,9 @@ def main():
             "points_per_sec": round(a.points * a.steps / dt, 1),
             "maps_launched": n_maps, "gpu_maps": gpu_maps, "cpu_maps": cpu_maps,
             "warmup_seconds": round(t_warm, 2),
+            # CPU time of this (rank-0) process per timed job: the JobTracker,
+            # its RPC handlers, the local TaskTracker and the driver
+            "rank0_cpu_ms_per_step": round(cpu_rank0 / a.steps * 1e3, 3),
             "final_shift": hist[-1].get("shift") if hist else None,
             "maps_per_tracker_last_job": hist[-1].get("maps_per_tracker") if hist else None,
             # per job signature: completed-task mean seconds on each slot type and the

@@ -341,6 +341,8 @@ def serve(sock):
 
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
+    from ..utils.sampler import maybe_arm_stackdump
+    maybe_arm_stackdump()
     sock = socket.socket(fileno=int(argv[0]))
     try:
         rc = serve(sock)

@@ -60,6 +60,10 @@ class Sampler:
             self.samples += 1
             time.sleep(self.interval)
 
+    def mark(self):
+        """Per-thread CPU is reported relative to now (e.g. a timed window)."""
+        self.cpu_mark = _thread_cpu()
+
     def report(self, top=40):
         lines = [f"samples {self.samples} (interval {self.interval * 1e3:.2f} ms); busy "
                  f"samples per thread group:"]
@@ -77,6 +81,23 @@ class Sampler:
             lines.append("\nRPC server methods (calls, total s, mean us):")
             for m, (n, t) in sorted(rpc.RPC_STATS.items(), key=lambda kv: -kv[1][1]):
                 lines.append(f"  {m:<28} {n:8d} {t:9.3f} {t / max(1, n) * 1e6:9.1f}")
+        now = _thread_cpu()
+        base = getattr(self, "cpu_mark", None)
+        lines.append("\nCPU seconds per thread (/proc, by thread name)" +
+                     (" since mark()" if base is not None else "") + ":")
+        if base is not None:
+            now = collections.Counter({g: t - base.get(g, 0.0) for g, t in now.items()})
+        for g, t in sorted(now.items(), key=lambda kv: -kv[1])[:20]:
+            lines.append(f"  {t:9.3f}  {g}")
+        if rpc is not None and getattr(rpc, "_PROFS", None):
+            import io, pstats
+            buf = io.StringIO()
+            ps = list(rpc._PROFS.values())
+            st = pstats.Stats(ps[0], stream=buf)
+            for p in ps[1:]:
+                st.add(p)
+            st.sort_stats("tottime").print_stats(45)
+            lines.append(buf.getvalue())
         lines.append("\ninclusive time (busy samples):")
         for (g, k), n in self.incl_counts.most_common(top):
             lines.append(f"  {n:7d}  {g:<24} {k}")
@@ -87,6 +108,27 @@ _IDLE = {"wait", "_wait_for_tstate_lock", "select", "accept", "recv_into", "recv
          "sleep", "poll", "_recv_bytes", "readinto", "acquire", "_worker", "serve_forever",
          "wait_for", "result", "join", "_recv_exact", "barrier", "serve_until_shutdown",
          "recv_msg", "_wait"}
+
+
+def _thread_cpu():
+    """utime+stime of this process's threads from /proc, by thread name
+    (threads that ended are not counted)."""
+    names = {t.native_id: t.name for t in threading.enumerate()}
+    tick = os.sysconf("SC_CLK_TCK")
+    out = collections.Counter()
+    try:
+        tids = os.listdir("/proc/self/task")
+    except OSError:
+        return out
+    for tid in tids:
+        try:
+            with open(f"/proc/self/task/{tid}/stat") as f:
+                parts = f.read().rsplit(")", 1)[1].split()
+        except OSError:
+            continue
+        name = names.get(int(tid), "native")
+        out[name] += (int(parts[11]) + int(parts[12])) / tick
+    return out
 
 
 def _idle(frame):
@@ -100,6 +142,16 @@ def _key(f):
     i = fn.find("hbmr/")
     fn = fn[i:] if i >= 0 else os.path.basename(fn)
     return f"{fn}:{c.co_firstlineno} {c.co_name}"
+
+
+def maybe_arm_stackdump():
+    """``HBMR_STACKDUMP_S=<s>``: every s seconds write every thread's Python
+    stack to stderr (faulthandler) — where a slow or stuck run is waiting."""
+    s = os.environ.get("HBMR_STACKDUMP_S")
+    if not s:
+        return
+    import faulthandler
+    faulthandler.dump_traceback_later(float(s), repeat=True, file=sys.stderr)
 
 
 def maybe_start():
