@@ -132,6 +132,9 @@ def main():
         k, _, v = kv.partition("=")
         conf.set(k.strip(), v.strip())
     node = Node(conf, use_gpu=has_gpu)
+    if node.is_master:
+        from hbmr.utils.sampler import maybe_watch_jobtracker
+        maybe_watch_jobtracker(node.jt)
     if not node.is_master:
         node.serve_until_shutdown()
         node.shutdown()

@@ -199,6 +199,24 @@ def _make_comm(init):
     return TorchComm(group=None, cpu_group=cpu_group)
 
 
+def _watch(host, runtime, every):
+    """HBMR_STACKDUMP_S: the worker's view every that many seconds (stderr):
+    attempts it holds, staged runs behind gates, device queues, busy slots."""
+    def loop():
+        while True:
+            time.sleep(every)
+            try:
+                devs = getattr(runtime, "devices", {})
+                q = {d: (dv.q.qsize(), sum(s.inflight for s in dv.slots))
+                     for d, dv in devs.items()}
+                print(f"worker-watch: runs={len(host.runs)} jobs={len(host.jobs)} "
+                      f"gated={runtime.gates.held_count()} queue/inflight={q}",
+                      file=sys.stderr, flush=True)
+            except Exception as e:  # noqa: BLE001
+                print(f"worker-watch: {e!r}", file=sys.stderr, flush=True)
+    threading.Thread(target=loop, daemon=True, name="hbmr-workerwatch").start()
+
+
 # --------------------------------------------------------------------------- main loop
 def serve(sock):
     msg = recv_msg(sock)
@@ -232,6 +250,8 @@ def serve(sock):
     runtime = Rt(host, devices, init["slots"])
     host.gpu_runtime = runtime      # the reduce opens gates of staged maps on it
     runtime.start()
+    if os.environ.get("HBMR_STACKDUMP_S"):
+        _watch(host, runtime, float(os.environ["HBMR_STACKDUMP_S"]))
     dev = None if simulate else runtime.torch_device(devices[0])
     cpu_pool = cf.ThreadPoolExecutor(max(1, init.get("cpu_slots", 1)),
                                      thread_name_prefix="worker-cpu")

@@ -35,9 +35,9 @@ _SIGS = {
     "hbmr_kmeans_assign_top3_bf16": (c_int, [c_void_p, c_long, c_int, c_void_p, c_void_p, c_int,
                                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "hbmr_kmeans_refine_f32": (c_int, [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p,
-                                       c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
-                                       c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                                       c_void_p, c_void_p]),
+                                       c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "hbmr_kmeans_accum_workspace_bytes": (c_long, [c_long, c_int]),
     "hbmr_kmeans_batch_workspace_bytes": (c_long, [c_long, c_int, c_int]),
     "hbmr_kmeans_map_batch": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,

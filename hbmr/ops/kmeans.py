@@ -92,18 +92,21 @@ class CentroidImage:
         self.refresh(stream=stream)
 
     def norms(self):
-        """(|c_j| fp32 [k], max_j |c_j| fp32 [1]) of the fp32 master centroids
-        (exact mode's certification bound), computed in fp64 once per image on
-        the first caller's stream; other streams wait on it."""
+        """(|c_j| [k], max_j |c_j| [1], |c_j - c~_j| [k], max_j |c_j - c~_j| [1])
+        fp32 of the fp32 master centroids and their bf16 image (exact mode's
+        certification bound; the errors rounded up), computed in fp64 once per
+        image on the first caller's stream; other streams wait on it."""
         with self._nbr_lock:
             if self._norms is None:
-                cn = self.cen.double().norm(dim=1).float()
+                c64 = self.cen.double()
+                cn = c64.norm(dim=1).float()
+                ce = _f32_up((c64 - self.cbf[:self.k, :self.d].double()).norm(dim=1))
                 ev = torch.cuda.Event()
                 ev.record()
-                self._norms = (cn, cn.max().reshape(1), ev)
-        cn, cm, ev = self._norms
+                self._norms = (cn, cn.max().reshape(1), ce, ce.max().reshape(1), ev)
+        cn, cm, ce, cem, ev = self._norms
         torch.cuda.current_stream().wait_event(ev)
-        return cn, cm
+        return cn, cm, ce, cem
 
     def neighbors(self, L: int = 256):
         """Each centroid's L nearest centroids (itself first) and their
@@ -207,12 +210,19 @@ def accumulate(points: torch.Tensor, labels: torch.Tensor, k: int, sums: torch.T
 
 
 # --------------------------------------------------------------------------- exact mode
+def _f32_up(v: torch.Tensor) -> torch.Tensor:
+    """fp64 → fp32 rounded towards +inf (an upper bound stays an upper bound)."""
+    f = v.float()
+    return torch.where(f.double() < v, torch.nextafter(f, torch.full_like(f, float("inf"))), f)
+
+
 class ExactSplit:
     """A split held for exact mode (``hbmr.kmeans.exact``): the bf16 copy the
     MFMA assign reads, the fp32 data (rows padded to dp) the certification
-    re-score and the combiner read, and per point |x| (fp32 data) and |x~|²
-    (bf16 copy), both computed in fp64."""
-    __slots__ = ("xb", "x32", "xnorm", "xbn2", "d")
+    re-score and the combiner read, and per point |x| (fp32 data), |x~|²
+    (bf16 copy) and the rounding error |x - x~| (an upper bound), computed in
+    fp64 once when the split is made resident."""
+    __slots__ = ("xb", "x32", "xnorm", "xbn2", "xerr", "d")
 
     def __init__(self, x32: torch.Tensor, dp: int):
         n, d = x32.shape
@@ -220,7 +230,10 @@ class ExactSplit:
         x64 = x32.double()
         self.xnorm = x64.norm(dim=1).float()
         xb = x32.to(torch.bfloat16)
-        self.xbn2 = xb.double().pow(2).sum(1).float()
+        xb64 = xb.double()
+        self.xbn2 = xb64.pow(2).sum(1).float()
+        self.xerr = _f32_up((x64 - xb64).norm(dim=1))
+        del x64, xb64
         if dp == d:
             self.xb, self.x32 = xb.contiguous(), x32.contiguous()
         else:
@@ -235,7 +248,7 @@ class ExactSplit:
 
     def nbytes(self) -> int:
         return sum(t.numel() * t.element_size() for t in (self.xb, self.x32, self.xnorm,
-                                                          self.xbn2))
+                                                          self.xbn2, self.xerr))
 
 
 def assign_top3(points: torch.Tensor, img: CentroidImage, labels, cand, scores, margin,
@@ -267,11 +280,12 @@ def refine_f32(split: ExactSplit, img: CentroidImage, labels, cand, scores, marg
     if labels.numel() != n or cand.numel() != 2 * n or margin.numel() != 2 * n:
         raise ValueError("labels [n], cand/margin [2n] from assign_top3 expected")
     with torch.cuda.stream(stream) if stream is not None else _nullctx():
-        cn, cmax = img.norms()
+        cn, cmax, ce, cemax = img.norms()
         ni, nd, L = img.neighbors()
     rc = _lib.load().hbmr_kmeans_refine_f32(
         _ptr(split.x32), n, img.d, split.x32.shape[1], _ptr(split.xnorm), _ptr(split.xbn2),
-        _ptr(img.cen), img.k, img.k_pad, _ptr(cn), _ptr(cmax), _ptr(ni), _ptr(nd), L,
+        _ptr(split.xerr), _ptr(img.cen), img.k, img.k_pad, _ptr(cn), _ptr(cmax), _ptr(ce),
+        _ptr(cemax), _ptr(ni), _ptr(nd), L,
         _ptr(labels), _ptr(cand), _ptr(scores), _ptr(margin), _ptr(stats),
         _lib.stream_handle(stream))
     _lib.check(rc, "hbmr_kmeans_refine_f32")

@@ -154,6 +154,40 @@ def maybe_arm_stackdump():
     faulthandler.dump_traceback_later(float(s), repeat=True, file=sys.stderr)
 
 
+def maybe_watch_jobtracker(jt):
+    """With ``HBMR_STACKDUMP_S``: also print the JobTracker's view of its
+    unfinished jobs and of each tracker every that many seconds (stderr)."""
+    s = os.environ.get("HBMR_STACKDUMP_S")
+    if not s or jt is None:
+        return
+
+    def loop():
+        while True:
+            time.sleep(float(s))
+            try:
+                lines = ["jt-watch:"]
+                with jt.lock:
+                    for jid, j in list(jt.jobs.items()):
+                        if j.completed():
+                            continue
+                        ra = sum(1 for t in j.maps for a in t.running_attempts())
+                        lines.append(
+                            f"  {jid} state={j.status.state} maps={len(j.maps)} "
+                            f"pending={len(j.pending_maps)} running_attempts={ra} "
+                            f"running_gpu={j.running_gpu} running_cpu={j.running_cpu} "
+                            f"done={j.maps_done} reduces_done="
+                            f"{sum(1 for r in j.reduces if r.successful)}/{len(j.reduces)} "
+                            f"staged_on={j.staged_on} expect={j.expect_mode}")
+                    for name, tr in jt.trackers.items():
+                        lines.append(f"  tracker {name}: running={len(tr.running)} "
+                                     f"gpu={dict(tr.running_gpu)} cpu={tr.running_cpu} "
+                                     f"cached={len(tr.cached)} more={tr.more}")
+                print("\n".join(lines), file=sys.stderr, flush=True)
+            except Exception as e:  # noqa: BLE001
+                print(f"jt-watch: {e!r}", file=sys.stderr, flush=True)
+    threading.Thread(target=loop, daemon=True, name="hbmr-jtwatch").start()
+
+
 def maybe_start():
     prefix = os.environ.get("HBMR_SAMPLE_PROF")
     if not prefix:

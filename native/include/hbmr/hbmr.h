@@ -33,8 +33,9 @@ int hbmr_kmeans_assign_top3_bf16(const void* X, long n, int dp, const void* C, c
                                  int k_pad, int32_t* labels, int32_t* cand, float* scores,
                                  float* margin, hipStream_t st);
 int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float* xnorm,
-                           const float* xbn2, const float* C32, int k, int k_pad,
-                           const float* cnorm, const float* cmax, const int32_t* nbr_idx,
+                           const float* xbn2, const float* xerr, const float* C32, int k,
+                           int k_pad, const float* cnorm, const float* cmax, const float* cerr,
+                           const float* cerrmax, const int32_t* nbr_idx,
                            const float* nbr_dist, int L, int32_t* labels, const int32_t* cand,
                            const float* scores, const float* margin, unsigned long long* stats,
                            hipStream_t st);

@@ -1535,14 +1535,17 @@ bool set_lds_limits() {
 //
 // The assign kernel ranks s~_j = x~.c~_j - |c~_j|^2/2 (x~, c~ = bf16 of the fp32
 // x, c; fp32 accumulation), i.e. the bf16 distances D~_j = |x~ - c~_j|^2.  With
-// u = 2^-8 (bf16 unit roundoff: 8 significant bits)
-// |(x~ - c~_j) - (x - c_j)| <= a_j = u(|x| + |c_j|), so
+// the rounding errors themselves, e_x = |x - x~| and e_j = |c_j - c~_j| (fp64,
+// rounded up; the worst case u = 2^-8 of bf16's 8 significant bits would give
+// u|x|, u|c_j| — about 3.5x looser for round-to-nearest data, and the flagged
+// fraction scales with it)
+// |(x~ - c~_j) - (x - c_j)| <= a_j = e_x + e_j, so
 // |D~_j - D_j| <= a_j (2 sqrt(D~_j) + a_j).  In score units (D/2), adding the
 // fp32 accumulation error e_acc and the arg-max packing truncation e_pack:
 //     E_j = a_j (2 sqrt(D~_j) + a_j) / 2 + e_acc_j + e_pack_j,   |s~_j - s_j| <= E_j.
 // Any cluster t ranked below a cluster r by the kernel (s~_t <= s~_r, so
-// D~_t >= D~_r) has  s_t <= s~_r + E_max(r)  (E with |c_t| <= cmax; the score
-// falls faster than E_t grows once sqrt(D~_r) >= 2 a_max).  Hence, with the
+// D~_t >= D~_r) has  s_t <= s~_r + E_max(r)  (E with |c_t| <= cmax and
+// e_t <= e_max; the score falls faster than E_t grows once sqrt(D~_r) >= 2 a_max).  Hence, with the
 // kernel's top three b, s, t:
 //   1. margin(b, s) > E_b + E_max(s)                 -> b is the exact winner;
 //   2. else D_b, D_s, D_t in fp64 from the fp32 rows; the winner w of the three
@@ -1559,11 +1562,11 @@ constexpr int kRefineMaxDp = 256;
 constexpr int kRefinePer = kRefineMaxDp / kRefineGroup;  // features per lane
 
 // Error bound E of a kernel score sc (point norm xn, |x~|^2 = x2) against a
-// centroid of norm cn, and a lower bound of sqrt(D~) for the monotonicity test.
-__device__ __forceinline__ void exact_bound(double sc, double cn, double xn, double x2, double u,
-                                            double gam, double pack_rel, double& e,
+// centroid of norm cn whose distance vector carries rounding error <= a, and a
+// lower bound of sqrt(D~) for the monotonicity test.
+__device__ __forceinline__ void exact_bound(double sc, double cn, double xn, double x2, double a,
+                                            double u, double gam, double pack_rel, double& e,
                                             double& dlo) {
-  const double a = u * (xn + cn);
   const double eacc = gam * (1.0 + u) * (1.0 + u) * (xn * cn + 0.5 * cn * cn);
   const double epack = fabs(sc) * pack_rel;
   const double slack = 2.0 * (eacc + epack) + x2 * 0x1p-22;
@@ -1598,8 +1601,10 @@ __device__ __forceinline__ double group_dist2(const double (&xv)[kRefinePer],
 
 __global__ __launch_bounds__(256) void kmeans_refine_kernel(
     const float* __restrict__ X32, long n, int d, int ldx, const float* __restrict__ xnorm,
-    const float* __restrict__ xbn2, const float* __restrict__ C32, int k,
-    const float* __restrict__ cnorm, const float* __restrict__ cmax, double pack_rel,
+    const float* __restrict__ xbn2, const float* __restrict__ xerr,
+    const float* __restrict__ C32, int k, const float* __restrict__ cnorm,
+    const float* __restrict__ cmax, const float* __restrict__ cerr,
+    const float* __restrict__ cerrmax, double pack_rel,
     const int32_t* __restrict__ nbr_idx, const float* __restrict__ nbr_dist, int L,
     int32_t* __restrict__ labels, const int32_t* __restrict__ cand,
     const float* __restrict__ score, const float* __restrict__ margin,
@@ -1610,9 +1615,10 @@ __global__ __launch_bounds__(256) void kmeans_refine_kernel(
   const double inflate = 1.0 + 0x1p-20;
   const double gam = (double)(d + 2) * 0x1p-23 * 1.01;
   const double cm = (double)cmax[0] * inflate;
+  const double cem = (double)cerrmax[0] * inflate;
   bool flag = false;
   int b = 0, s2 = 0, s3 = 0;
-  double xn = 0.0, x2 = 0.0, sb = 0.0, m3 = 0.0;
+  double xn = 0.0, x2 = 0.0, sb = 0.0, m3 = 0.0, amax = 0.0;
   if (p < n) {
     b = labels[p];
     s2 = cand[p];
@@ -1623,10 +1629,13 @@ __global__ __launch_bounds__(256) void kmeans_refine_kernel(
       sb = score[p];
       const double m2 = margin[p];
       m3 = margin[n + p];
+      const double xe = (double)xerr[p];
+      amax = (xe + cem) * inflate;
       double eb, es, dl_b, dl_s;
-      exact_bound(sb, (double)cnorm[b] * inflate, xn, x2, u, gam, pack_rel, eb, dl_b);
-      exact_bound(sb - m2, cm, xn, x2, u, gam, pack_rel, es, dl_s);
-      flag = !(m2 > eb + es && dl_s >= 2.0 * u * (xn + cm));
+      exact_bound(sb, (double)cnorm[b] * inflate, xn, x2, (xe + (double)cerr[b]) * inflate, u,
+                  gam, pack_rel, eb, dl_b);
+      exact_bound(sb - m2, cm, xn, x2, amax, u, gam, pack_rel, es, dl_s);
+      flag = !(m2 > eb + es && dl_s >= 2.0 * amax);
     }
   }
   unsigned long long mask = __ballot(flag);
@@ -1642,7 +1651,7 @@ __global__ __launch_bounds__(256) void kmeans_refine_kernel(
     const long q = __shfl(p, src);
     const int qb = __shfl(b, src), qs = __shfl(s2, src), qt = __shfl(s3, src);
     const double qsb = __shfl(sb, src), qm3 = __shfl(m3, src);
-    const double qxn = __shfl(xn, src), qx2 = __shfl(x2, src);
+    const double qxn = __shfl(xn, src), qx2 = __shfl(x2, src), qamax = __shfl(amax, src);
     if (!have) continue;
     const float* xr = X32 + (size_t)q * ldx;
     double xv[kRefinePer];
@@ -1667,8 +1676,8 @@ __global__ __launch_bounds__(256) void kmeans_refine_kernel(
     bool certified = !t_real;
     if (t_real) {
       double et, dl_t;
-      exact_bound(qsb - qm3, cm, qxn, qx2, u, gam, pack_rel, et, dl_t);
-      certified = 0.5 * (xx - dw) > (qsb - qm3) + et && dl_t >= 2.0 * u * (qxn + cm);
+      exact_bound(qsb - qm3, cm, qxn, qx2, qamax, u, gam, pack_rel, et, dl_t);
+      certified = 0.5 * (xx - dw) > (qsb - qm3) + et && dl_t >= 2.0 * qamax;
     }
     if (!certified) {
       if (sub == 0) atomicAdd(stats + 2, 1ull);
@@ -2182,8 +2191,9 @@ int hbmr_kmeans_assign_top3_bf16(const void* X, long n, int dp, const void* C, c
 }
 
 int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float* xnorm,
-                           const float* xbn2, const float* C32, int k, int k_pad,
-                           const float* cnorm, const float* cmax, const int32_t* nbr_idx,
+                           const float* xbn2, const float* xerr, const float* C32, int k,
+                           int k_pad, const float* cnorm, const float* cmax, const float* cerr,
+                           const float* cerrmax, const int32_t* nbr_idx,
                            const float* nbr_dist, int L, int32_t* labels, const int32_t* cand,
                            const float* scores, const float* margin, unsigned long long* stats,
                            hipStream_t st) {
@@ -2196,7 +2206,8 @@ int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float
   const double pack_rel = ldexp(1.0, 4 + tb - 23);
   const long blocks = (n + 255) / 256;
   hipLaunchKernelGGL(kmeans_refine_kernel, dim3((unsigned)blocks), dim3(256), 0, st, X32, n, d,
-                     ldx, xnorm, xbn2, C32, k, cnorm, cmax, pack_rel, nbr_idx, nbr_dist, L,
+                     ldx, xnorm, xbn2, xerr, C32, k, cnorm, cmax, cerr, cerrmax, pack_rel,
+                     nbr_idx, nbr_dist, L,
                      labels, cand, scores, margin, stats);
   return (int)hipGetLastError();
 }

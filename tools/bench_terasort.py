@@ -11,7 +11,7 @@ timing brackets are sync jobs (every worker synchronises its device).
 
   python tools/bench_terasort.py --rows 1000000000 --split-rows 10000000 --steps 3   # 100 GB
   ... --output /tmp/tera-out   # also time jobs that commit their output (reported alongside)
-  ... -D hbmr.terasort.reduce.gid=true   # job properties (here: the packed-id reduce)
+  ... -D hbmr.terasort.reduce.gid=false  # job properties (here: the v3 permutation reduce)
 """
 import argparse
 import json
@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--output", default=None)
     ap.add_argument("--partitions", type=int, default=0)
     ap.add_argument("-D", dest="defines", action="append", default=[],
-                    help="key=value job property, e.g. -D hbmr.terasort.reduce.gid=true")
+                    help="key=value job property, e.g. -D hbmr.terasort.reduce.gid=false")
     a = ap.parse_args()
     from hbmr.gpu.syncjob import sync_conf
     from hbmr.mapred.jobconf import JobConf
