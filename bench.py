@@ -84,7 +84,9 @@ def main():
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(a.gpus)
 
-    from hbmr.utils.sampler import maybe_arm_stackdump, maybe_start
+    from hbmr.utils.sampler import dump_profiles, maybe_arm_stackdump, maybe_profile_threads, \
+        maybe_start
+    cprof = maybe_profile_threads()   # HBMR_CPROFILE=path: cProfile of every thread
     maybe_arm_stackdump()       # HBMR_STACKDUMP_S=s: thread stacks to stderr every s
     sampler = maybe_start()     # HBMR_SAMPLE_PROF=prefix: control-plane stack sampling
 
@@ -258,6 +260,8 @@ def main():
     finally:
         if sampler is not None:
             sampler.dump()
+        if cprof:
+            dump_profiles(cprof)
         node.shutdown()
     return 0
 

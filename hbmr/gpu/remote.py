@@ -306,6 +306,8 @@ class RemoteGpuRuntime:
             with tr.split_cache._lock:
                 tr.split_cache.added.extend(added)
                 tr.split_cache.removed.extend(removed)
+        urgent = False
+        bulk_jobs = set()
         for it in items:
             if it[0] == "bulk":
                 _, aids, dt, output, counters = it
@@ -314,7 +316,9 @@ class RemoteGpuRuntime:
                     if runs:
                         self.held.setdefault(runs[0].spec.job_id, set()).update(aids)
                 tr.finish_bulk(runs, dt, output, counters)
+                bulk_jobs.update(r.spec.job_id for r in runs)
             else:
+                urgent = True
                 d = it[1]
                 with self._lock:
                     run = self.inflight.pop(d["attempt_id"], None)
@@ -333,7 +337,10 @@ class RemoteGpuRuntime:
                 run.status.start_time = d.get("start_time") or run.status.start_time
                 tr._finish(run, d["state"], d.get("diagnostic", ""), output=d.get("output"),
                            device_time=d.get("device_time", 0.0), wake=False)
-        tr.notify_jobtracker()
+        if urgent or added or removed or not bulk_jobs:
+            tr.notify_jobtracker()
+        else:
+            tr.maps_done_news(bulk_jobs)
 
     def _on_death(self, proc):
         tr = self.tracker

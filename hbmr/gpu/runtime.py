@@ -386,7 +386,11 @@ class GpuRuntime:
                 agg.incr("hbmr.GpuCounters", "GPU_KERNEL_US", int(dt * 1e6) * len(runs))
                 tracker.finish_bulk(runs, dt, {"tracker": tracker.name, "where": where},
                                     agg.to_dict())
-                tracker.notify_jobtracker()
+                news = getattr(tracker, "maps_done_news", None)
+                if news is not None:
+                    news({r.spec.job_id for r in runs})
+                else:
+                    tracker.notify_jobtracker()
             except BaseException as e:  # noqa: BLE001
                 self._note_error(slot.device.index, e)
                 for r in runs:

@@ -262,7 +262,11 @@ class SimulatedGpuRuntime:
                                                             "where": "simgpu"},
                                     device_time=self.task_s, wake=False)
             slot.inflight -= len(runs)
-            tracker.notify_jobtracker()
+            news = getattr(tracker, "maps_done_news", None)
+            if finish_bulk is not None and news is not None:
+                news({r.spec.job_id for r in runs})
+            else:
+                tracker.notify_jobtracker()
 
 
 class _Shim:

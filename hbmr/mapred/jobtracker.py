@@ -708,19 +708,26 @@ class JobTracker:
         if TRACE.on:
             TRACE.instant("jt.jip_created")
         too_big = self._memory_violation(conf)
-        with self.lock:
-            self.jobs[str(jid)] = jip
-            if too_big:
-                self._finish_job(jip, FAILED, too_big)
-                return RunningJob(jid, _JTJobHandle(jip), conf)
+        init_error = None
+        if not too_big:
             self.history.log("JOB_SUBMITTED", job=str(jid), name=conf.get_job_name(),
                              user=conf.get_user())
+            # splits, TIPs and job setup outside the JobTracker lock (the job
+            # is not visible yet): heartbeats are not held up by a submission
             try:
                 jip.init_tasks()
                 if TRACE.on:
                     TRACE.instant("jt.tasks_inited", maps=len(jip.maps))
             except Exception as e:  # noqa: BLE001
                 log.exception("job init failed")
+                init_error = e
+        with self.lock:
+            self.jobs[str(jid)] = jip
+            if too_big:
+                self._finish_job(jip, FAILED, too_big)
+                return RunningJob(jid, _JTJobHandle(jip), conf)
+            if init_error is not None:
+                e = init_error
                 self._finish_job(jip, FAILED, f"init failed: {type(e).__name__}: {e}")
                 return RunningJob(jid, _JTJobHandle(jip), conf)
             check = getattr(self.scheduler, "check_submission", None)
@@ -914,6 +921,25 @@ class JobTracker:
                 tr.wake_seq = seq
             tr.bell.set()
 
+    def report(self, status: dict):
+        """A tracker's news (finished attempts, lost outputs, cache changes)
+        while its heartbeat long-polls: processed like a heartbeat without
+        assignment, then the long-poll is rung so it assigns into any freed
+        slots and returns what that yields (and any actions the report left,
+        e.g. commit approvals or kills).  One call instead of wakeup → the
+        long-poll returning empty → a heartbeat with the news → a new
+        long-poll; per-tracker heartbeat work is what bounds multi-rank jobs."""
+        name = status["tracker_name"] if isinstance(status, dict) else status.tracker_name
+        tr = self.trackers.get(name)
+        if tr is None:
+            return {"reinit": True}
+        resp = self._heartbeat(status, False, False)
+        if resp["actions"]:
+            with self.lock:
+                tr.extra_actions += resp["actions"]
+        tr.bell.set()
+        return {}
+
     def _kick(self):
         """New work may be assignable: ring every long-polling tracker."""
         for tr in list(self.trackers.values()):
@@ -971,6 +997,9 @@ class JobTracker:
                 if tr.extra_actions:
                     resp["actions"] += tr.extra_actions
                     tr.extra_actions = []
+                if tr.kills:
+                    resp["actions"] += [P.kill_task_action(aid) for aid in sorted(tr.kills)]
+                    tr.kills.clear()
                 if tr.status.healthy and not tr.blacklisted:
                     resp["actions"] += self.scheduler.assign_tasks(tr)
                     if TRACE.on:
@@ -1003,10 +1032,12 @@ class JobTracker:
                 tr.cached.add(tuple(k))
             for k in st.cached_splits_removed:
                 tr.cached.discard(tuple(k))
-            for rep in st.task_reports:
-                self._update_task_status(tr, P.TaskStatus.from_dict(rep), actions)
+            # batched map completions first: they precede any reduce report
+            # that rides with them (TaskTracker.maps_done_news)
             for bulk in st.bulk_reports:
                 self._bulk_succeeded(tr, bulk)
+            for rep in st.task_reports:
+                self._update_task_status(tr, P.TaskStatus.from_dict(rep), actions)
             if st.lost_outputs:
                 self._outputs_lost(tr, st.lost_outputs)
             if self._to_recover:

@@ -228,7 +228,7 @@ class RpcClient:
             self._tl.sock = None
 
 
-JT_METHODS = ("heartbeat", "wakeup", "map_completion_events", "rpc_submit_job", "rpc_job_status", "rpc_kill_job",
+JT_METHODS = ("heartbeat", "wakeup", "report", "map_completion_events", "rpc_submit_job", "rpc_job_status", "rpc_kill_job",
               "rpc_job_result", "rpc_cluster_status", "rpc_list_jobs", "rpc_task_reports")
 
 
@@ -245,6 +245,9 @@ class JobTrackerProxy:
 
     def wakeup(self, tracker_name, seq=None):
         return self.rpc.call("wakeup", tracker_name, seq)
+
+    def report(self, status):
+        return self.rpc.call("report", status)
 
     def map_completion_events(self, job_id, start=0):
         return self.rpc.call("map_completion_events", job_id, start)

@@ -146,6 +146,9 @@ class TaskTracker:
         # other; with CPython's default 5 ms GIL switch interval a woken
         # thread can wait that long for the interpreter while another one
         # runs bookkeeping, idling the GPU.  0.2 ms keeps hand-offs prompt.
+        self.defer_map_reports = conf.get_boolean("hbmr.tracker.defer.map.reports", True)
+        # news reaches a long-polling JobTracker as one report call
+        self.report_news = conf.get_boolean("hbmr.tracker.report.news", True)
         si = conf.get_float("hbmr.python.switchinterval.ms", 0.2)
         if si > 0:
             sys.setswitchinterval(si / 1000.0)
@@ -189,6 +192,13 @@ class TaskTracker:
         self._lock = threading.Lock()
         self._changed: set[str] = set()
         self._bulk: list[dict] = []          # batched GPU completions not yet reported
+        # jobs with an early ("expect") collective reduce running here: their
+        # map outputs go to that reduce on the device, so finished map batches
+        # ride on the reduce's completion heartbeat instead of one of their own
+        # (maps_done_news)
+        self._expect_jobs: set = set()
+        self._polling = False       # the heartbeat thread is in a long-poll
+        self._requeued: list = []   # drained statuses whose report failed
         self._notify_seq = 0                 # wakeup() notifications sent (notify_seq)
         self._lost: list[str] = []           # succeeded attempts whose output was lost
         self._worker_lost = False            # GPU worker died: the gang must restart
@@ -244,15 +254,27 @@ class TaskTracker:
             ids = list(self._changed)
             self._changed.clear()
             reports = []
+            bulk, lost, wlost = [], [], False
+            for old in self._requeued:
+                reports += old.task_reports
+                bulk += old.bulk_reports
+                lost += old.lost_outputs
+                wlost = wlost or old.gpu_worker_lost
+                added = list(old.cached_splits_added) + list(added)
+                removed = list(old.cached_splits_removed) + list(removed)
+            self._requeued = []
             for aid in ids:
                 r = self.running.get(aid)
                 if r is not None:
                     reports.append(r.status.to_dict())
                     if r.status.state in P.TERMINAL:
                         self.running.pop(aid, None)
-            bulk, self._bulk = self._bulk, []
-            lost, self._lost = self._lost, []
-            wlost, self._worker_lost = self._worker_lost, False
+            bulk += self._bulk
+            self._bulk = []
+            lost += self._lost
+            self._lost = []
+            wlost = wlost or self._worker_lost
+            self._worker_lost = False
             seq = self._notify_seq
         return P.TaskTrackerStatus(tracker_name=self.name, host=self.host, bulk_reports=bulk,
                                    notify_seq=seq,
@@ -335,6 +357,9 @@ class TaskTracker:
         if state != P.SUCCEEDED and run.spec is not None and run.spec.is_map and \
                 run.job is not None:
             run.job.note_failed(run.spec.attempt_id)
+        if run.spec is not None and not run.spec.is_map and self._expect_jobs:
+            with self._lock:
+                self._expect_jobs.discard(run.spec.job_id)
         if state == P.FAILED:
             dbg = self._run_debug_script(run, diag)
             if dbg:
@@ -390,6 +415,18 @@ class TaskTracker:
                           where=(output or {}).get("where"))
         self._news.set()
 
+    def maps_done_news(self, job_ids):
+        """Finished GPU map batches of ``job_ids`` are queued for the next
+        heartbeat: wake the JobTracker now unless each of those jobs has an
+        early collective reduce running here — its completion (a few device
+        kernels later) reports them together, one heartbeat instead of two
+        (the JobTracker's per-heartbeat work bounds multi-rank scaling).
+        ``hbmr.tracker.defer.map.reports`` = false always reports at once."""
+        if self._expect_jobs and all(j in self._expect_jobs for j in job_ids):
+            self._news.set()
+            return
+        self.notify_jobtracker()
+
     def outputs_lost(self, aids, worker_lost=False):
         with self._lock:
             self._lost.extend(aids)
@@ -397,18 +434,40 @@ class TaskTracker:
         self.notify_jobtracker()
 
     def notify_jobtracker(self):
-        """Cut our long-polling heartbeat short so finished tasks are reported now.
-        The notification count lets the JobTracker tell a wakeup that carries
-        news the pending heartbeat lacks from a stale one (TaskTrackerStatus.
-        notify_seq)."""
+        """Finished tasks are reported now.  While the heartbeat long-polls,
+        the news goes to the JobTracker directly (JobTracker.report: processed
+        there, and the long-poll is rung to assign into the freed slots);
+        otherwise the heartbeat thread is between calls and takes it along on
+        its next one.  The fallback cuts the long-poll short (wakeup); the
+        notification count lets the JobTracker tell a wakeup that carries news
+        the pending heartbeat lacks from a stale one (TaskTrackerStatus.notify_seq)."""
         with self._lock:
             self._notify_seq += 1
             seq = self._notify_seq
+            polling = self._polling
         self._news.set()
+        if not polling:
+            return
+        if self.report_news and getattr(self.jt, "report", None) is not None:
+            st = self.status()
+            try:
+                r = self.jt.report(st.to_dict())
+                if not (isinstance(r, dict) and r.get("reinit")):
+                    return
+            except Exception:  # noqa: BLE001
+                pass
+            self._requeue(st)      # not delivered: the heartbeat thread sends it
         try:
             self.jt.wakeup(self.name, seq)
         except Exception:  # noqa: BLE001
             pass
+
+    def _requeue(self, st):
+        """A drained status whose report did not reach the JobTracker: its
+        contents go out with the next heartbeat."""
+        with self._lock:
+            self._requeued.append(st)
+            self._news.set()
 
     # -- lifecycle -----------------------------------------------------------------------
     def start(self):
@@ -442,12 +501,23 @@ class TaskTracker:
         while not self._stop.is_set():
             try:
                 self._news.clear()
+                # (set before the status is built: news from here on is
+                # either in it or reported to the JobTracker by the notifier)
+                with self._lock:
+                    self._polling = not (initial or more)
                 st = self.status()
                 block = 0.0 if (st.task_reports or initial or more) else self.interval
+                if block == 0.0:
+                    with self._lock:
+                        self._polling = False
                 if TRACE.on:
                     TRACE.instant("tt.heartbeat.send", reports=len(st.task_reports), block=block)
-                resp = self.jt.heartbeat(st.to_dict(), initial=initial,
-                                         accept_new_tasks=True, block=block)
+                try:
+                    resp = self.jt.heartbeat(st.to_dict(), initial=initial,
+                                             accept_new_tasks=True, block=block)
+                finally:
+                    with self._lock:
+                        self._polling = False
                 if TRACE.on:
                     TRACE.instant("tt.heartbeat.recv", actions=len(resp.get("actions", [])))
                 self.heartbeats += 1
@@ -570,6 +640,8 @@ class TaskTracker:
         run = _Running(spec, st, js)
         with self._lock:
             self.running[spec.attempt_id] = run
+            if not spec.is_map and spec.expect and self.defer_map_reports:
+                self._expect_jobs.add(spec.job_id)
         remote = getattr(self.gpu_runtime, "remote", False) and js.split_job is not None
         if spec.is_map and spec.run_on_gpu:
             if js.split_job is None:

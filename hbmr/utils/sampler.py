@@ -188,6 +188,60 @@ def maybe_watch_jobtracker(jt):
     threading.Thread(target=loop, daemon=True, name="hbmr-jtwatch").start()
 
 
+_PROFILES: list = []
+
+
+def maybe_profile_threads():
+    """``HBMR_CPROFILE=path``: every thread started from now on (and the
+    caller's) runs under its own cProfile; ``dump_profiles`` merges them."""
+    path = os.environ.get("HBMR_CPROFILE")
+    if not path:
+        return None
+    import cProfile
+    orig = threading.Thread.run
+
+    def run(self):
+        pr = cProfile.Profile()
+        _PROFILES.append(pr)
+        pr.enable()
+        try:
+            orig(self)
+        finally:
+            pr.disable()
+    threading.Thread.run = run
+    main = cProfile.Profile()
+    _PROFILES.append(main)
+    main.enable()
+    return path
+
+
+def dump_profiles(path):
+    import io
+    import pstats
+    for pr in _PROFILES:
+        try:
+            pr.disable()
+        except Exception:  # noqa: BLE001
+            pass
+    st = None
+    for pr in _PROFILES:
+        try:
+            if st is None:
+                st = pstats.Stats(pr, stream=io.StringIO())
+            else:
+                st.add(pr)
+        except TypeError:      # a profile that never ran
+            pass
+    if st is None:
+        return
+    buf = io.StringIO()
+    st.stream = buf
+    st.sort_stats("tottime").print_stats(60)
+    st.sort_stats("cumulative").print_stats(60)
+    with open(f"{path}_{os.getpid()}.txt", "w") as f:
+        f.write(buf.getvalue())
+
+
 def maybe_start():
     prefix = os.environ.get("HBMR_SAMPLE_PROF")
     if not prefix:
