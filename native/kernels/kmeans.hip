@@ -1655,16 +1655,13 @@ __global__ __launch_bounds__(256) void kmeans_refine_kernel(
     if (!have) continue;
     const float* xr = X32 + (size_t)q * ldx;
     double xv[kRefinePer];
-    double xx = 0.0;
 #pragma unroll
     for (int mm = 0; mm < kRefinePer / 8; ++mm)
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
         const int i = 8 * sub + 8 * kRefineGroup * mm + jj;
         xv[8 * mm + jj] = i < d ? (double)xr[i] : 0.0;
-        xx = fma(xv[8 * mm + jj], xv[8 * mm + jj], xx);
       }
-    xx = group_sum16(xx);
     const bool t_real = qt < k;
     const double db = group_dist2(xv, C32 + (size_t)qb * d, d, sub);
     const double ds = group_dist2(xv, C32 + (size_t)qs * d, d, sub);
@@ -1677,7 +1674,12 @@ __global__ __launch_bounds__(256) void kmeans_refine_kernel(
     if (t_real) {
       double et, dl_t;
       exact_bound(qsb - qm3, cm, qxn, qx2, qamax, u, gam, pack_rel, et, dl_t);
-      certified = 0.5 * (xx - dw) > (qsb - qm3) + et && dl_t >= 2.0 * qamax;
+      // scores are on the bf16 point's baseline: s_t = (|x~|^2 - D_t)/2 with
+      // exact D; |x~|^2 (qx2) was stored in fp32, hence the 2^-23 margin.
+      // (|x|^2 of the fp32 row would differ by ~|x| e_x, a shift the bound
+      // does not carry)
+      certified = 0.5 * (qx2 - dw) - qx2 * 0x1p-23 > (qsb - qm3) + et &&
+                  dl_t >= 2.0 * qamax;
     }
     if (!certified) {
       if (sub == 0) atomicAdd(stats + 2, 1ull);
