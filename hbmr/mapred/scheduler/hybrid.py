@@ -137,8 +137,18 @@ class HybridTaskScheduler(TaskScheduler):
         reduce_free = tr.status.max_reduce_slots - tr.running_reduce
         # stock Hadoop knows no queue behind a slot: one task per GPU slot
         depth = 1 if self.policy == "stock" else self.queue_depth
-        gpu_free = {g["device"]: g["max_slots"] * depth - tr.running_gpu.get(
-            g["device"], 0) for g in tr.status.gpus}
+        # maps of staged jobs wait behind their gate (in the GPU worker, not on
+        # the device queue) and have a budget of their own (_stage_maps): they
+        # must not take the queue from the job they wait for — whose maps
+        # beyond one queue's worth would otherwise never launch, and whose
+        # reduce the gate waits on
+        held = {}
+        for j in jt.staged:
+            for (tname, dev), n in j.staged_launched.items():
+                if tname == tr.name and n:
+                    held[dev] = held.get(dev, 0) + n
+        gpu_free = {g["device"]: g["max_slots"] * depth - tr.running_gpu.get(g["device"], 0) +
+                    held.get(g["device"], 0) for g in tr.status.gpus}
         budget = self.max_maps_per_hb
         tr.more = False
         self.begin_round(tr, total_cpu, total_gpu)

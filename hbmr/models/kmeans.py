@@ -376,7 +376,14 @@ class KMeansSplitJob(SplitJob):
         jc = JobConf(conf)
         FileInputFormat.setInputPaths(jc, self.input)
         fmt = SequenceFileInputFormat()
-        splits = fmt.getSplits(jc, max(1, conf.get_int("mapred.map.tasks", 1)))
+        nmaps = max(1, conf.get_int("mapred.map.tasks", 1))
+        if conf.get("mapred.min.split.size") is None and "://" not in self.input:
+            # a local file's block size means nothing here: splits are sized to
+            # stay HBM-resident, about input / mapred.map.tasks each (as the
+            # synthetic splits are), not one per 32-64 MiB block
+            total = sum(f.length for f in fmt.list_status(jc))
+            jc.set_long("mapred.min.split.size", max(1, -(-total // nmaps)))
+        splits = fmt.getSplits(jc, nmaps)
         out = []
         for i, s in enumerate(splits):
             key = f"kmeans-file:{s.path}:{s.start}:{s.length}" + (":exact" if self.exact else "")

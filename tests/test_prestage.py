@@ -97,3 +97,17 @@ def test_killing_a_staged_job_fails_its_dependents(tmp_path):
         drv2 = K.KMeansDriver(cl.submit_job, lambda rj: rj._impl.jip.result[0], conf=conf, k=5,
                               d=8, inp="synthetic:8000:3", split_points=1000)
         assert drv2.step()["points"] == 8000
+
+
+@pytest.mark.timeout(90)
+@pytest.mark.parametrize("worker", [False, True])
+def test_staged_maps_do_not_take_the_queue_their_gate_waits_on(worker, tmp_path):
+    """A job with more maps than one GPU queue holds (8 maps, 2 slots x depth 1):
+    the next iteration's staged maps have their own budget, so they cannot
+    fill the queue while the job they wait for still has maps to launch (that
+    deadlocked: its reduce, which opens their gate, needed those maps)."""
+    want, _, _, _ = _run(_conf(worker, prestage=False), tmp_path / "plain", steps=4)
+    conf = _conf(worker, **{"hbmr.gpu.queue.depth": 1})
+    got, jobs, events, _ = _run(conf, tmp_path / "staged", steps=4)
+    assert torch.equal(got, want)
+    assert sum(e["event"] == "JOB_STAGED" for e in events) >= 2
