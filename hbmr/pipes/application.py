@@ -239,10 +239,18 @@ class ChildPool:
         self._lock = threading.Lock()
         self._reaper = None
 
-    def acquire(self, key):
-        import time
+    def acquire(self, key, split=None):
+        """An idle child for ``key``: one that already mapped ``split`` (its
+        serialized bytes) if any — a GPU binary keeps the split resident —
+        else the most recently idle."""
         with self._lock:
             lst = self._idle.get(key) or []
+            if split:
+                for i in range(len(lst) - 1, -1, -1):
+                    app = lst[i][0]
+                    if split in getattr(app, "splits_seen", ()) and app.alive():
+                        del lst[i]
+                        return app
             while lst:
                 app, _t = lst.pop()
                 if app.alive():
@@ -250,11 +258,17 @@ class ChildPool:
                 app.cleanup()
         return None
 
-    def release(self, key, app, idle_s=None):
+    def release(self, key, app, idle_s=None, split=None):
         import time
         if not app.alive():
             app.cleanup()
             return
+        if split:
+            seen = getattr(app, "splits_seen", None)
+            if seen is None:
+                seen = app.splits_seen = set()
+            if len(seen) < 4096:
+                seen.add(split)
         with self._lock:
             self._idle.setdefault(key, []).append((app, time.time()))
             if idle_s is not None:

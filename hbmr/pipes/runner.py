@@ -73,7 +73,10 @@ class PipesMapRunner(MapRunnable):
         from ..utils.trace import TRACE
         reuse = job.get_boolean(REUSE, False)
         key = (self.executable(), self.device(), "map")
-        app = POOL.acquire(key) if reuse else None
+        split = _split_bytes(reporter)
+        # an idle child that already mapped this split (a GPU binary keeps it
+        # resident in HBM) is preferred over the most recently idle one
+        app = POOL.acquire(key, split) if reuse else None
         if TRACE.on:
             TRACE.instant("pipes.map.child", reused=app is not None)
         if app is not None:
@@ -96,7 +99,7 @@ class PipesMapRunner(MapRunnable):
                 if first is not None:
                     kc, vc = type(first[0]), type(first[1])
                     down.set_input_types(kc.java_name(), vc.java_name())
-                down.run_map(_split_bytes(reporter), job.get_num_reduce_tasks(), True)
+                down.run_map(split, job.get_num_reduce_tasks(), True)
                 kv = first
                 while kv is not None:
                     down.map_item(kv[0], kv[1])
@@ -107,7 +110,7 @@ class PipesMapRunner(MapRunnable):
                 down.end_of_input()
                 reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, n)
             else:
-                app.downlink.run_map(_split_bytes(reporter), job.get_num_reduce_tasks(), False)
+                app.downlink.run_map(split, job.get_num_reduce_tasks(), False)
                 app.downlink.flush()
             app.wait_for_finish()
             ok = True
@@ -118,7 +121,7 @@ class PipesMapRunner(MapRunnable):
             raise
         finally:
             if ok and reuse:
-                POOL.release(key, app, job.get_float(IDLE, 30.0))
+                POOL.release(key, app, job.get_float(IDLE, 30.0), split=split)
             else:
                 app.cleanup()
 

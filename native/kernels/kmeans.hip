@@ -1599,6 +1599,66 @@ __device__ __forceinline__ double group_dist2(const double (&xv)[kRefinePer],
   return group_sum16(acc);
 }
 
+// Four distances at once (the Elkan scan's candidates): the loads and FMA
+// chains of four centroid rows interleave, and so do the four reductions —
+// a scan step otherwise waits out one row's L2 latency and one shuffle chain.
+__device__ __forceinline__ void group_dist2x4(const double (&xv)[kRefinePer],
+                                              const float* __restrict__ c0,
+                                              const float* __restrict__ c1,
+                                              const float* __restrict__ c2,
+                                              const float* __restrict__ c3, int d, int sub,
+                                              double (&out)[4]) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+#pragma unroll
+  for (int m = 0; m < kRefinePer / 8; ++m) {
+    const int b = 8 * sub + 8 * kRefineGroup * m;
+    if (b + 8 <= d) {
+      float v0[8], v1[8], v2[8], v3[8];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        v0[jj] = c0[b + jj];
+        v1[jj] = c1[b + jj];
+        v2[jj] = c2[b + jj];
+        v3[jj] = c3[b + jj];
+      }
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const double x = xv[8 * m + jj];
+        const double e0 = x - (double)v0[jj], e1 = x - (double)v1[jj];
+        const double e2 = x - (double)v2[jj], e3 = x - (double)v3[jj];
+        a0 = fma(e0, e0, a0);
+        a1 = fma(e1, e1, a1);
+        a2 = fma(e2, e2, a2);
+        a3 = fma(e3, e3, a3);
+      }
+    } else {
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        if (b + jj < d) {
+          const double x = xv[8 * m + jj];
+          const double e0 = x - (double)c0[b + jj], e1 = x - (double)c1[b + jj];
+          const double e2 = x - (double)c2[b + jj], e3 = x - (double)c3[b + jj];
+          a0 = fma(e0, e0, a0);
+          a1 = fma(e1, e1, a1);
+          a2 = fma(e2, e2, a2);
+          a3 = fma(e3, e3, a3);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 1; off < kRefineGroup; off <<= 1) {
+    a0 += __shfl_xor(a0, off);
+    a1 += __shfl_xor(a1, off);
+    a2 += __shfl_xor(a2, off);
+    a3 += __shfl_xor(a3, off);
+  }
+  out[0] = a0;
+  out[1] = a1;
+  out[2] = a2;
+  out[3] = a3;
+}
+
 __global__ __launch_bounds__(256) void kmeans_refine_kernel(
     const float* __restrict__ X32, long n, int d, int ldx, const float* __restrict__ xnorm,
     const float* __restrict__ xbn2, const float* __restrict__ xerr,
@@ -1689,20 +1749,41 @@ __global__ __launch_bounds__(256) void kmeans_refine_kernel(
       bool done = false;
       const int32_t* ni = nbr_idx + (size_t)w0 * L;
       const float* nd = nbr_dist + (size_t)w0 * L;
-      for (int jj = 0; jj < L; ++jj) {
-        const double rb = sqrt(dw);
-        if ((double)nd[jj] > (r0 + rb) * (1.0 + 0x1p-40)) {
+      // four neighbours per step: the exit bound r0 + r_best is taken at the
+      // step's start (r_best only shrinks, so it admits a superset of the
+      // candidates the one-at-a-time walk would visit; the minimum over a
+      // superset is the same exact winner)
+      const float* cw0 = C32 + (size_t)w0 * d;
+      for (int jj = 0; jj < L; jj += 4) {
+        const double lim = (r0 + sqrt(dw)) * (1.0 + 0x1p-40);
+        if ((double)nd[jj] > lim) {
           done = true;
           break;
         }
-        const int j = ni[jj];
-        const double dj = group_dist2(xv, C32 + (size_t)j * d, d, sub);
-        if (dj < dw || (dj == dw && j < w)) { w = j; dw = dj; }
+        int jv[4];
+        const float* cp[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const bool ok = jj + u < L && (double)nd[jj + u] <= lim;
+          jv[u] = ok ? ni[jj + u] : -1;
+          cp[u] = ok ? C32 + (size_t)jv[u] * d : cw0;
+        }
+        double dj[4];
+        group_dist2x4(xv, cp[0], cp[1], cp[2], cp[3], d, sub, dj);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (jv[u] >= 0 && (dj[u] < dw || (dj[u] == dw && jv[u] < w))) { w = jv[u]; dw = dj[u]; }
       }
       if (!done && L < k) {
-        for (int j = 0; j < k; ++j) {  // outran the neighbour list: every centroid
-          const double dj = group_dist2(xv, C32 + (size_t)j * d, d, sub);
-          if (dj < dw || (dj == dw && j < w)) { w = j; dw = dj; }
+        for (int j = 0; j < k; j += 4) {  // outran the neighbour list: every centroid
+          const float* cp[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) cp[u] = C32 + (size_t)(j + u < k ? j + u : j) * d;
+          double dj[4];
+          group_dist2x4(xv, cp[0], cp[1], cp[2], cp[3], d, sub, dj);
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (j + u < k && (dj[u] < dw || (dj[u] == dw && j + u < w))) { w = j + u; dw = dj[u]; }
         }
       }
     }

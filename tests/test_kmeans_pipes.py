@@ -122,7 +122,12 @@ def test_gpu_pipes_binary_is_reused_and_keeps_splits_in_hbm(tmp_path):
     from hbmr.pipes.application import POOL
     KP.write_points(str(tmp_path / "pts"), N, D, seed=3, centers=KC, files=3)
     init = K.initial_centroids(f"synthetic:{N}:3", KC, D)
-    with LocalCluster(JobConf(), num_trackers=1, gpus=[[0]], cpu_slots=0,
+    # one child per slot: with hbmr.gpu.pipes.concurrency > 1 a split finds the
+    # child that holds it only when that child is idle (ChildPool prefers it),
+    # so every-split hit counts are exact only here
+    conf = JobConf()
+    conf.set_int("hbmr.gpu.pipes.concurrency", 1)
+    with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=0,
                       gpu_slots_per_device=1) as cl:
         drv = KP.KMeansPipesDriver(str(tmp_path / "work"), str(tmp_path / "pts"), KC, D, init,
                                    cluster=cl, reduces=1)
