@@ -377,7 +377,7 @@ class KMeansSplitJob(SplitJob):
         FileInputFormat.setInputPaths(jc, self.input)
         fmt = SequenceFileInputFormat()
         nmaps = max(1, conf.get_int("mapred.map.tasks", 1))
-        if conf.get("mapred.min.split.size") is None and "://" not in self.input:
+        if conf.get_long("mapred.min.split.size", 0) <= 1 and "://" not in self.input:
             # a local file's block size means nothing here: splits are sized to
             # stay HBM-resident, about input / mapred.map.tasks each (as the
             # synthetic splits are), not one per 32-64 MiB block

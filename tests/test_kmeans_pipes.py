@@ -109,6 +109,22 @@ def test_kmeans_split_job_on_sequencefile_input_matches_synthetic(tmp_path):
     assert torch.equal(_file_job_centroids(str(tmp_path / "pts"), 3), _split_job_centroids(3))
 
 
+def test_kmeans_file_splits_follow_map_count_not_local_blocks(tmp_path):
+    """Local SequenceFile input is split about input / mapred.map.tasks (splits
+    sized to stay HBM-resident), not once per local-FS block."""
+    from hbmr.utils.reflection import new_instance
+    KP.write_points(str(tmp_path / "pts"), N, D, seed=3, centers=KC, files=2)
+    conf = K.make_iteration_conf(JobConf(), KC, D, str(tmp_path / "pts"), 1000, "c0", "c1")
+    conf.set_long("fs.local.block.size", 4096)            # many blocks per file
+    conf.set_int("mapred.map.tasks", 2)
+    sj = new_instance(conf.get("hbmr.splitjob.class"), conf)
+    assert len(sj.get_splits(conf, ["t0"])) == 2
+    conf.set_long("mapred.min.split.size", 1 << 40)      # an explicit choice wins
+    assert len(sj.get_splits(conf, ["t0"])) == 2
+    conf.set_long("mapred.min.split.size", 4096)
+    assert len(sj.get_splits(conf, ["t0"])) > 2
+
+
 @pytest.mark.gpu
 def test_gpu_kmeans_split_job_on_sequencefile_input(tmp_path):
     KP.write_points(str(tmp_path / "pts"), N, D, seed=3, centers=KC, files=3)
