@@ -256,6 +256,8 @@ def serve(sock):
     cpu_pool = cf.ThreadPoolExecutor(max(1, init.get("cpu_slots", 1)),
                                      thread_name_prefix="worker-cpu")
     status = [g.__dict__ for g in runtime.device_status()]
+    from ..utils.gctune import tune
+    tune()      # torch and the runtime into the permanent GC generation
     send_msg(sock, ("ready", status, os.getpid()), host.send_lock)
 
     def _unknown_job(runs):

@@ -100,6 +100,10 @@ class Node:
             if not self.jt.wait_for_trackers(self.world, timeout=300):
                 raise RuntimeError("not all TaskTrackers registered with the JobTracker")
             self.jt.start_expiry_thread()
+        # start-up state into the permanent GC generation, rarer collections
+        # (hbmr/utils/gctune.py: full collections were ~60 ms GIL pauses)
+        from ..utils.gctune import tune
+        tune()
 
     def _init_dist(self, be: str):
         """The default process group on backend ``be`` (plus a gloo group for
