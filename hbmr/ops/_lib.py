@@ -37,7 +37,8 @@ _SIGS = {
     "hbmr_kmeans_refine_f32": (c_int, [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
-                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                       c_void_p]),
     "hbmr_kmeans_accum_workspace_bytes": (c_long, [c_long, c_int]),
     "hbmr_kmeans_batch_workspace_bytes": (c_long, [c_long, c_int, c_int]),
     "hbmr_kmeans_map_batch": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,

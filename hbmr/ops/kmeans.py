@@ -14,6 +14,7 @@ Data layout contract (built by :class:`hbmr.gpu.split_cache.SplitCache`):
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 
 import torch
@@ -27,6 +28,9 @@ def _nullctx():
     import contextlib
     return contextlib.nullcontext()
 FX_SHIFT = 24  # fixed-point fraction bits of the partial sums
+# exact mode's Elkan scan: neighbours listed per centroid (past them the scan
+# checks every centroid); HBMR_KMEANS_NBR_L overrides
+NBR_L = 256
 
 
 def padded_dim(d: int) -> int:
@@ -108,12 +112,14 @@ class CentroidImage:
         torch.cuda.current_stream().wait_event(ev)
         return cn, cm, ce, cem
 
-    def neighbors(self, L: int = 256):
+    def neighbors(self, L: int | None = None):
         """Each centroid's L nearest centroids (itself first) and their
         distances, fp64 rounded DOWN to fp32 — exact mode's Elkan scan.  Built
         once per image on the first caller's stream; other streams wait on it."""
         with self._nbr_lock:
             if self._nbr is None:
+                if L is None:
+                    L = int(os.environ.get("HBMR_KMEANS_NBR_L", NBR_L))
                 L = max(1, min(L, self.k))
                 c = self.cen.double()
                 dist = torch.cdist(c, c, compute_mode="donot_use_mm_for_euclid_dist")
@@ -273,7 +279,8 @@ def refine_f32(split: ExactSplit, img: CentroidImage, labels, cand, scores, marg
                stats: torch.Tensor, stream=None) -> None:
     """Certify the bf16 labels against the fp32 data; re-score the uncertain
     points in fp64 (hbmr_kmeans_refine_f32).  stats (int64 [3]) += (flagged,
-    relabelled, points that needed the neighbour scan)."""
+    relabelled, points that needed the neighbour scan); a [5] stats also
+    counts the scan's neighbour distances and its full scans."""
     n = split.shape[0]
     if stats.dtype != torch.int64 or stats.numel() < 3:
         raise ValueError("stats must be int64 [3]")
@@ -286,7 +293,7 @@ def refine_f32(split: ExactSplit, img: CentroidImage, labels, cand, scores, marg
         _ptr(split.x32), n, img.d, split.x32.shape[1], _ptr(split.xnorm), _ptr(split.xbn2),
         _ptr(split.xerr), _ptr(img.cen), img.k, img.k_pad, _ptr(cn), _ptr(cmax), _ptr(ce),
         _ptr(cemax), _ptr(ni), _ptr(nd), L,
-        _ptr(labels), _ptr(cand), _ptr(scores), _ptr(margin), _ptr(stats),
+        _ptr(labels), _ptr(cand), _ptr(scores), _ptr(margin), _ptr(stats), stats.numel(),
         _lib.stream_handle(stream))
     _lib.check(rc, "hbmr_kmeans_refine_f32")
 

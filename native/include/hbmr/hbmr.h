@@ -38,7 +38,7 @@ int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float
                            const float* cerrmax, const int32_t* nbr_idx,
                            const float* nbr_dist, int L, int32_t* labels, const int32_t* cand,
                            const float* scores, const float* margin, unsigned long long* stats,
-                           hipStream_t st);
+                           int nstats, hipStream_t st);
 int hbmr_kmeans_update(const long long* sums, const long long* counts, int fx_shift, int k, int d,
                        int dp, int k_pad, float* cen, void* cbf, float* chalf, float* shift2,
                        hipStream_t st);

@@ -1668,7 +1668,7 @@ __global__ __launch_bounds__(256) void kmeans_refine_kernel(
     const int32_t* __restrict__ nbr_idx, const float* __restrict__ nbr_dist, int L,
     int32_t* __restrict__ labels, const int32_t* __restrict__ cand,
     const float* __restrict__ score, const float* __restrict__ margin,
-    unsigned long long* __restrict__ stats) {
+    unsigned long long* __restrict__ stats, int nstats) {
   const long p = (long)blockIdx.x * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const double u = 0x1.004p-8;  // bf16 keeps 8 significant bits: unit roundoff 2^-8
@@ -1754,6 +1754,7 @@ __global__ __launch_bounds__(256) void kmeans_refine_kernel(
       // candidates the one-at-a-time walk would visit; the minimum over a
       // superset is the same exact winner)
       const float* cw0 = C32 + (size_t)w0 * d;
+      int evals = 0;
       for (int jj = 0; jj < L; jj += 4) {
         const double lim = (r0 + sqrt(dw)) * (1.0 + 0x1p-40);
         if ((double)nd[jj] > lim) {
@@ -1770,9 +1771,14 @@ __global__ __launch_bounds__(256) void kmeans_refine_kernel(
         }
         double dj[4];
         group_dist2x4(xv, cp[0], cp[1], cp[2], cp[3], d, sub, dj);
+        evals += 4;
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           if (jv[u] >= 0 && (dj[u] < dw || (dj[u] == dw && jv[u] < w))) { w = jv[u]; dw = dj[u]; }
+      }
+      if (nstats >= 5 && sub == 0) {
+        atomicAdd(stats + 3, (unsigned long long)evals);
+        if (!done && L < k) atomicAdd(stats + 4, 1ull);
       }
       if (!done && L < k) {
         for (int j = 0; j < k; j += 4) {  // outran the neighbour list: every centroid
@@ -2279,7 +2285,7 @@ int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float
                            const float* cerrmax, const int32_t* nbr_idx,
                            const float* nbr_dist, int L, int32_t* labels, const int32_t* cand,
                            const float* scores, const float* margin, unsigned long long* stats,
-                           hipStream_t st) {
+                           int nstats, hipStream_t st) {
   if (n <= 0) return 0;
   if (d > ldx || d > kRefineMaxDp || k <= 0 || k_pad < k || L < 1 || L > k)
     return (int)hipErrorInvalidValue;
@@ -2291,7 +2297,7 @@ int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float
   hipLaunchKernelGGL(kmeans_refine_kernel, dim3((unsigned)blocks), dim3(256), 0, st, X32, n, d,
                      ldx, xnorm, xbn2, xerr, C32, k, cnorm, cmax, cerr, cerrmax, pack_rel,
                      nbr_idx, nbr_dist, L,
-                     labels, cand, scores, margin, stats);
+                     labels, cand, scores, margin, stats, nstats);
   return (int)hipGetLastError();
 }
 

@@ -42,8 +42,11 @@ def main():
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--iters", type=int, default=3, help="Lloyd iterations before timing")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--nbr", type=int, default=0, help="neighbour list length (0: default)")
     a = ap.parse_args()
     dev = torch.device("cuda")
+    if a.nbr:
+        os.environ["HBMR_KMEANS_NBR_L"] = str(a.nbr)
     n, k, d = a.points, a.k, a.d
     dp = km.padded_dim(d)
     x32 = K.synthetic_points(7, 0, n, d, k, dev)
@@ -59,7 +62,7 @@ def main():
     splits = [km.ExactSplit(x32[s:s + a.split], dp) for s in range(0, n, a.split)]
     bsplits = [xb[s:s + a.split] for s in range(0, n, a.split)]
     torch.cuda.synchronize()
-    stats = torch.zeros(3, dtype=torch.int64, device=dev)
+    stats = torch.zeros(5, dtype=torch.int64, device=dev)
     bufs = {}
 
     def plain():
@@ -94,16 +97,19 @@ def main():
         for s in bsplits:
             km.accumulate(s, lab[:s.shape[0]], k, sums, cnt)
 
-    r = {"points": n, "k": k, "d": d, "split": a.split, "lloyd_iters": a.iters}
+    r = {"points": n, "k": k, "d": d, "split": a.split, "lloyd_iters": a.iters,
+         "nbr_l": img.neighbors()[2]}
     r["assign_bf16_ms"] = timeit(plain, a.reps)
     r["assign_top3_ms"] = timeit(top3, a.reps)
     stats.zero_()
     r["top3_plus_refine_ms"] = timeit(top3_refine, a.reps)
     runs = a.reps + 1
-    f, rl, sc = (int(v) // runs for v in stats.tolist())
+    f, rl, sc, ev, full = (int(v) // runs for v in stats.tolist())
     r.update(refine_ms=round(r["top3_plus_refine_ms"] - r["assign_top3_ms"], 3),
              flagged_frac=round(f / n, 5), relabelled_frac=round(rl / n, 6),
-             neighbour_scan_frac=round(sc / n, 6))
+             neighbour_scan_frac=round(sc / n, 6),
+             neighbours_per_scan=round(ev / max(1, sc), 1),
+             full_scan_frac=round(full / max(1, sc), 4))
     r["accum_f32_ms"] = timeit(acc32, a.reps)
     r["accum_bf16_ms"] = timeit(acc16, a.reps)
     print(json.dumps(r), flush=True)
