@@ -1671,6 +1671,11 @@ __global__ __launch_bounds__(256) void kmeans_refine_kernel(
     unsigned long long* __restrict__ stats, int nstats) {
   const long p = (long)blockIdx.x * 256 + threadIdx.x;
   const int lane = threadIdx.x & 63;
+  // the counters gather in LDS, one global atomic per counter and block: one
+  // per event on a single address serialised ~10^6 atomics per 12.5M points
+  __shared__ unsigned long long cnt[5];
+  if (threadIdx.x < 5) cnt[threadIdx.x] = 0;
+  __syncthreads();
   const double u = 0x1.004p-8;  // bf16 keeps 8 significant bits: unit roundoff 2^-8
   const double inflate = 1.0 + 0x1p-20;
   const double gam = (double)(d + 2) * 0x1p-23 * 1.01;
@@ -1699,7 +1704,7 @@ __global__ __launch_bounds__(256) void kmeans_refine_kernel(
     }
   }
   unsigned long long mask = __ballot(flag);
-  if (lane == 0 && mask) atomicAdd(stats, (unsigned long long)__popcll(mask));
+  if (lane == 0 && mask) atomicAdd(&cnt[0], (unsigned long long)__popcll(mask));
   const int grp = lane / kRefineGroup, sub = lane % kRefineGroup;
   // four groups take the flagged points of this wave in turn
   while (mask) {
@@ -1742,7 +1747,7 @@ __global__ __launch_bounds__(256) void kmeans_refine_kernel(
                   dl_t >= 2.0 * qamax;
     }
     if (!certified) {
-      if (sub == 0) atomicAdd(stats + 2, 1ull);
+      if (sub == 0) atomicAdd(&cnt[2], 1ull);
       // step 3: Elkan scan around w0 = w (exact distance r0)
       const int w0 = w;
       const double r0 = sqrt(dw);
@@ -1776,9 +1781,9 @@ __global__ __launch_bounds__(256) void kmeans_refine_kernel(
         for (int u = 0; u < 4; ++u)
           if (jv[u] >= 0 && (dj[u] < dw || (dj[u] == dw && jv[u] < w))) { w = jv[u]; dw = dj[u]; }
       }
-      if (nstats >= 5 && sub == 0) {
-        atomicAdd(stats + 3, (unsigned long long)evals);
-        if (!done && L < k) atomicAdd(stats + 4, 1ull);
+      if (sub == 0) {
+        atomicAdd(&cnt[3], (unsigned long long)evals);
+        if (!done && L < k) atomicAdd(&cnt[4], 1ull);
       }
       if (!done && L < k) {
         for (int j = 0; j < k; j += 4) {  // outran the neighbour list: every centroid
@@ -1795,9 +1800,12 @@ __global__ __launch_bounds__(256) void kmeans_refine_kernel(
     }
     if (sub == 0 && w != qb) {
       labels[q] = w;
-      atomicAdd(stats + 1, 1ull);
+      atomicAdd(&cnt[1], 1ull);
     }
   }
+  __syncthreads();
+  if (threadIdx.x < (nstats < 5 ? 3 : 5) && cnt[threadIdx.x])
+    atomicAdd(stats + threadIdx.x, cnt[threadIdx.x]);
 }
 
 template <int D>
