@@ -75,6 +75,9 @@ class TrackerInfo:
         self.kills: set[str] = set()   # attempts to kill on the next heartbeat
         self.kill_epoch = -1           # JobTracker.kill_epoch this tracker was last scanned at
         self.extra_actions: list = []  # e.g. restart_gpu_worker, sent on the next heartbeat
+        # not worth ending a long-poll for (KillJobAction purges of finished
+        # jobs): they ride on the next response the tracker gets anyway
+        self.lazy_actions: list = []
 
     def gpu_devices(self):
         return [g["device"] for g in self.status.gpus]
@@ -881,7 +884,7 @@ class JobTracker:
         for t in self.trackers.values():
             if jid_s in t.jobs_seen:
                 t.jobs_seen.discard(jid_s)
-                t.extra_actions.append(P.kill_job_action(jid_s))
+                t.lazy_actions.append(P.kill_job_action(jid_s))
         jip.done.set()
         for w in self.waiting.pop(str(jip.job_id), []):
             if w.completed():
@@ -973,7 +976,7 @@ class JobTracker:
             resp["actions"].append(P.shutdown_action())
             return resp
         if resp["actions"] or block <= 0 or not accept_new_tasks:
-            return resp
+            return self._with_lazy(tr0 or self.trackers.get(name), resp)
         deadline = time.time() + block
         tr = self.trackers.get(name)
         if tr is None:
@@ -1006,6 +1009,13 @@ class JobTracker:
                         TRACE.instant("jt.assigned", n=len(resp["actions"]))
         tr.wake = False
         resp["more"] = tr.more
+        return self._with_lazy(tr, resp)
+
+    def _with_lazy(self, tr, resp):
+        if tr is not None and tr.lazy_actions:
+            with self.lock:
+                resp["actions"] += tr.lazy_actions
+                tr.lazy_actions = []
         return resp
 
     def _heartbeat(self, status, initial, accept_new_tasks):
@@ -1191,8 +1201,15 @@ class JobTracker:
             jip.t_maps_done = time.time()
         self._check_job_done(jip)
         if tip.is_map and jip.reduces and (jip.maps_complete() or
-                                           jip.maps_done == jip.slowstart_maps):
+                                           jip.maps_done == jip.slowstart_maps) and \
+                self._reduces_waiting(jip):
             self._kick()  # reduces became schedulable: wake long-polling trackers
+
+    @staticmethod
+    def _reduces_waiting(jip) -> bool:
+        """Any reduce neither done nor running (an early collective reduce
+        gang already runs: ringing every tracker would find nothing to do)."""
+        return any(t.successful is None and not t.is_running() for t in jip.reduces)
 
     def _bulk_succeeded(self, tr: TrackerInfo, rep: dict):
         """A batch of GPU map attempts that completed together (one HIP event
@@ -1255,7 +1272,7 @@ class JobTracker:
                 if jp.maps_complete():
                     jp.t_maps_done = time.time()
                 self._check_job_done(jp)
-                if jp.reduces and jp.maps_complete():
+                if jp.reduces and jp.maps_complete() and self._reduces_waiting(jp):
                     self._kick()
         for a in odd:
             self._update_task_status(tr, P.TaskStatus(

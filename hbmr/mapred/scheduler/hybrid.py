@@ -242,10 +242,12 @@ class HybridTaskScheduler(TaskScheduler):
         for jip in list(jt.staged):
             if jip.completed() or jip.staged_on is None:
                 continue
-            if jip.reduces and self._reduces_may_start(jip):
-                reduce_free = self._assign_reduces(tr, jip, reduce_free, actions)
+            # maps first: once this tracker's maps are staged the reduce may
+            # go out in the same response instead of a heartbeat of its own
             if jip.pending_maps and jip.gpu_capable:
                 self._stage_maps(tr, jip, depth, actions)
+            if jip.reduces and self._reduces_may_start(jip):
+                reduce_free = self._assign_reduces(tr, jip, reduce_free, actions)
         return actions
 
     def _assign_reduces(self, tr, jip, reduce_free, actions):

@@ -98,6 +98,12 @@ class Sampler:
                 st.add(p)
             st.sort_stats("tottime").print_stats(45)
             lines.append(buf.getvalue())
+        jt = sys.modules.get("hbmr.mapred.jobtracker")
+        pl = getattr(getattr(jt, "_ProfLock", None), "STATS", None)
+        if pl:
+            lines.append("\nJT lock holds (calls, total ms):")
+            for k2, (n2, t2) in sorted(pl.items(), key=lambda kv: -kv[1][1])[:25]:
+                lines.append(f"  {k2:<40} {n2:7d} {t2 * 1e3:9.1f}")
         lines.append("\ninclusive time (busy samples):")
         for (g, k), n in self.incl_counts.most_common(top):
             lines.append(f"  {n:7d}  {g:<24} {k}")
