@@ -332,6 +332,8 @@ class HybridTaskScheduler(TaskScheduler):
         for dev in sorted(gpu_free):
             if gpu_free[dev] < tr.gpu_capacity(dev) * self.queue_depth:
                 continue  # only fully idle devices back up stragglers
+            if self.job_limit(jip, "gpu") <= 0:
+                break     # a backup is a running task too (maxRunningTasksPerJob)
             tip = self._straggler(jip, now)
             if tip is None:
                 break
