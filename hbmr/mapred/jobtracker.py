@@ -205,6 +205,9 @@ class JobInProgress:
         self.finished_cpu_maps = 0
         self.finished_gpu_maps = 0
         self.completion_events: list = []     # (map TaskID, attempt id, output)
+        # notified when completion events are added or the job ends: reduces
+        # long-poll map_completion_events on it instead of sleeping
+        self.events_cond = threading.Condition(threading.Lock())
         self.map_index: dict[str, TaskInProgress] = {}
         self.pending_maps: dict = {}   # TIP -> None: not yet started, insertion (FIFO) order
         self.by_split_key: dict = {}
@@ -886,6 +889,8 @@ class JobTracker:
                 t.jobs_seen.discard(jid_s)
                 t.lazy_actions.append(P.kill_job_action(jid_s))
         jip.done.set()
+        with jip.events_cond:
+            jip.events_cond.notify_all()      # reduces long-polling for events
         for w in self.waiting.pop(str(jip.job_id), []):
             if w.completed():
                 continue             # killed while it waited
@@ -1172,6 +1177,8 @@ class JobTracker:
             else:
                 jip.finished_cpu_maps += 1
             jip.completion_events.append((tip.tid, a.aid, a.output))
+            with jip.events_cond:
+                jip.events_cond.notify_all()
         # kill other running attempts of this TIP
         for other in tip.running_attempts():
             if other is not a:
@@ -1257,6 +1264,9 @@ class JobTracker:
             done.append(a)
         if done:
             jip = done[0].tip.job
+            for jp in {a.tip.job for a in done}:
+                with jp.events_cond:
+                    jp.events_cond.notify_all()
             n = len(done)
             done_ids = [a.aid for a in done]
             self.cost_model.tasks_finished(jip.signature, done_ids, True, dt)
@@ -1557,17 +1567,26 @@ class JobTracker:
         return [[str(t.tid), t.successful.aid, t.successful.output] for t in jip.maps
                 if t.successful is not None]
 
-    def map_completion_events(self, job_id, start=0):
+    def map_completion_events(self, job_id, start=0, wait=0.0):
         """TaskUmbilicalProtocol.getMapCompletionEvents (TaskUmbilicalProtocol.java:
         167): successful map outputs from index ``start`` on, for reduces that
-        started before every map finished (slow-start)."""
+        started before every map finished (slow-start).  ``wait`` > 0: with
+        nothing new, block up to that long for the next event (the reference's
+        GetMapEventsThread polls on a sleep; a copy that waits on a backed-off
+        poll starts late)."""
+        jip = self.jobs.get(str(job_id))
+        if jip is not None and wait > 0 and len(jip.completion_events) <= start:
+            with jip.events_cond:
+                jip.events_cond.wait_for(
+                    lambda: len(jip.completion_events) > start or jip.completed(), timeout=wait)
         with self.lock:
             jip = self.jobs.get(str(job_id))
             if jip is None:
                 return {"events": [], "num_maps": 0, "state": "UNKNOWN"}
             evs = jip.completion_events[start:]
             return {"events": [[str(t), aid, out] for t, aid, out in evs],
-                    "num_maps": len(jip.maps), "state": jip.status.state}
+                    "num_maps": len(jip.maps), "state": jip.status.state,
+                    "waited": wait > 0}
 
     # -- RPC-facing job submission protocol (JobSubmissionProtocol) -------------------------
     def rpc_submit_job(self, conf_dict):

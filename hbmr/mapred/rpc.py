@@ -249,8 +249,8 @@ class JobTrackerProxy:
     def report(self, status):
         return self.rpc.call("report", status)
 
-    def map_completion_events(self, job_id, start=0):
-        return self.rpc.call("map_completion_events", job_id, start)
+    def map_completion_events(self, job_id, start=0, wait=0.0):
+        return self.rpc.call("map_completion_events", job_id, start, wait)
 
 
 class _RemoteJob:

@@ -708,8 +708,10 @@ class ReduceTask(Task):
                 new = True
                 yield MapOutputLocation(aid, (out or {}).get("path"))
             if not new:
-                time.sleep(delay)
-                delay = min(0.05, delay * 2)
+                if not r.get("waited"):
+                    # a source that does not long-poll: back off between polls
+                    time.sleep(delay)
+                    delay = min(0.05, delay * 2)
             else:
                 delay = 0.001
 

@@ -800,7 +800,7 @@ class TaskTracker:
             if len(spec.map_outputs) < spec.num_maps:
                 # slow-start: the rest of the map outputs arrive as completion events
                 jt, jid = self.jt, spec.job_id
-                task.event_source = lambda start: jt.map_completion_events(jid, start)
+                task.event_source = lambda start: jt.map_completion_events(jid, start, 0.05)
             run_profiled(js.conf, spec.attempt_id, False, spec.partition, task.run,
                          os.path.join(self.local_dir, spec.job_id, spec.attempt_id))
             self._finish(run, P.SUCCEEDED, output={"tracker": self.name})
