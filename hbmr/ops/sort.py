@@ -11,6 +11,8 @@ the native library must load (no silent fallback).
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -22,6 +24,10 @@ KEY = 10
 # hi-only sort + tie fix-up)
 _SORT80 = __import__("os").environ.get("HBMR_TERA_SORT80") == "1"
 
+
+# TeraSort reduce v4: the radix sort covers hi >> TIE_SHIFT (the low bits of hi
+# and lo are ordered by the in-place tie fix); HBMR_TERA_TIE_SHIFT overrides
+TIE_SHIFT = int(os.environ.get("HBMR_TERA_TIE_SHIFT", "16"))
 
 def _ptr(t):
     return None if t is None else t.data_ptr()
@@ -467,13 +473,16 @@ def gather_records_gid(bases, gid: torch.Tensor, stream=None) -> torch.Tensor:
 
 
 def sort_gathered(his, rows, starts, lens, bases, stream=None):
-    """TeraSort reduce v4 for one group: (hi, gid) collect, 8 radix passes over
-    hi carrying the gid, ONE record gather by gid, the low key words read back
-    from the sorted records, and runs of equal hi ordered by them in place.
-    Returns (records, hi, lo), or None when a run of equal high words is too
-    long for the in-place fix-up (the caller takes the full-key path)."""
+    """TeraSort reduce v4 for one group: (hi, gid) collect, radix passes over
+    the top 64 - TIE_SHIFT bits of hi carrying the gid, ONE record gather by
+    gid, the low key words read back from the sorted records, and runs of an
+    equal sorted prefix ordered by the full key in place.  Returns (records,
+    hi, lo), or None when such a run is too long for the in-place fix-up (the
+    caller takes the full-key path)."""
     h, gid = tera_collect_gid(his, rows, starts, lens, stream=stream)
-    radix_sort_pairs(h, gid, 0, 64, stream=stream)
+    # the top 48 bits of hi (6 passes); the tie fix orders equal prefixes by
+    # the full key read back from the records
+    radix_sort_pairs(h, gid, TIE_SHIFT, 64, stream=stream)
     recs = gather_records_gid(bases, gid, stream=stream)
     del gid
     _h2, lo = tera_keys(recs, stream=stream)
@@ -484,7 +493,7 @@ def sort_gathered(his, rows, starts, lens, bases, stream=None):
         return recs[o], h[o], lo[o]
     flag = torch.zeros(1, dtype=torch.int32, device=recs.device)
     rc = _lib.load().hbmr_tera_tie_fix_records(_ptr(h), _ptr(lo), _ptr(recs), recs.shape[0],
-                                                recs.shape[1], _ptr(flag),
+                                                recs.shape[1], TIE_SHIFT, _ptr(flag),
                                                 _lib.stream_handle(stream))
     _lib.check(rc, "hbmr_tera_tie_fix_records")
     if int(flag.item()):

@@ -61,6 +61,8 @@ def from_wire(raw: bytes, cls):
     return cls.deserialize(raw)
 
 
+_SMALL_VINTS = [bytes((n,)) for n in range(128)]
+
 class DownwardProtocol:
     def __init__(self, sock):
         self.sock = sock
@@ -91,10 +93,13 @@ class DownwardProtocol:
         items = list(conf) if not isinstance(conf, dict) else list(conf.items())
         # one buffer for the whole message (a few hundred strings per task)
         parts = [encode_vint(SET_JOB_CONF), encode_vint(2 * len(items))]
+        small = _SMALL_VINTS            # lengths 0..127 are one byte (Hadoop VInt)
         for k, v in items:
             kb = str(k).encode()
             vb = ("" if v is None else str(v)).encode()
-            parts += (encode_vint(len(kb)), kb, encode_vint(len(vb)), vb)
+            nk, nv = len(kb), len(vb)
+            parts += (small[nk] if nk < 128 else encode_vint(nk), kb,
+                      small[nv] if nv < 128 else encode_vint(nv), vb)
         msg = b"".join(parts)
         with self._lock:
             self.out.write(msg)

@@ -86,8 +86,8 @@ int hbmr_tera_collect_gid(const uint64_t* const* his, const uint32_t* const* row
                           uint32_t* ogid, hipStream_t st);
 int hbmr_gather_records_gid(const void* const* bases, const uint32_t* gid, long n,
                             int record_bytes, void* dst, hipStream_t st);
-int hbmr_tera_tie_fix_records(const uint64_t* hi, uint64_t* lo, void* rec, long n,
-                              int record_bytes, unsigned int* flag, hipStream_t st);
+int hbmr_tera_tie_fix_records(uint64_t* hi, uint64_t* lo, void* rec, long n,
+                              int record_bytes, int shift, unsigned int* flag, hipStream_t st);
 int hbmr_merge_path(const uint64_t* ahi, const uint64_t* alo, const uint32_t* av, long na,
                     const uint64_t* bhi, const uint64_t* blo, const uint32_t* bv, long nb,
                     uint64_t* ohi, uint64_t* olo, uint32_t* ov, hipStream_t st);

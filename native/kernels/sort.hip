@@ -835,25 +835,32 @@ __global__ __launch_bounds__(256) void gather_records_gid_kernel(
   }
 }
 
-// After the hi-only sort and the record gather: order each run of equal hi by
-// lo, moving the (already gathered) records themselves; runs longer than
-// kTieRun are flagged for the full-key path.
+// After the sort on the high key word's top 64 - shift bits and the record
+// gather: order each run of an equal sorted prefix (hi >> shift) by the full
+// key (hi, lo), moving hi, lo and the (already gathered) records themselves;
+// runs longer than kTieRun are flagged for the full-key path.  shift = 16
+// saves two of eight radix passes: among the ~10^8 keys of a group, equal
+// 48-bit prefixes come in a few dozen pairs.
 __global__ __launch_bounds__(256) void tera_tie_fix_records_kernel(
-    const uint64_t* __restrict__ hi, uint64_t* __restrict__ lo, uint32_t* __restrict__ rec,
-    long n, int words, unsigned int* __restrict__ flag) {
+    uint64_t* __restrict__ hi, uint64_t* __restrict__ lo, uint32_t* __restrict__ rec,
+    long n, int words, int shift, unsigned int* __restrict__ flag) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n - 1) return;
-  const uint64_t h = hi[i];
-  if (hi[i + 1] != h || (i > 0 && hi[i - 1] == h)) return;
+  const uint64_t h = hi[i] >> shift;
+  if ((hi[i + 1] >> shift) != h || (i > 0 && (hi[i - 1] >> shift) == h)) return;
   long e = i + 1;
-  while (e < n && hi[e] == h && e - i < kTieRun) ++e;
-  if (e < n && hi[e] == h) {
+  while (e < n && (hi[e] >> shift) == h && e - i < kTieRun) ++e;
+  if (e < n && (hi[e] >> shift) == h) {
     atomicOr(flag, 1u);
     return;
   }
   // insertion sort by adjacent swaps (no per-lane record buffer)
   for (long a = i + 1; a < e; ++a) {
-    for (long b = a - 1; b >= i && lo[b] > lo[b + 1]; --b) {
+    for (long b = a - 1;
+         b >= i && (hi[b] > hi[b + 1] || (hi[b] == hi[b + 1] && lo[b] > lo[b + 1])); --b) {
+      const uint64_t th = hi[b];
+      hi[b] = hi[b + 1];
+      hi[b + 1] = th;
       const uint64_t t = lo[b];
       lo[b] = lo[b + 1];
       lo[b + 1] = t;
@@ -1078,12 +1085,14 @@ int hbmr_gather_records_gid(const void* const* bases, const uint32_t* gid, long 
   return (int)hipGetLastError();
 }
 
-int hbmr_tera_tie_fix_records(const uint64_t* hi, uint64_t* lo, void* rec, long n,
-                              int record_bytes, unsigned int* flag, hipStream_t st) {
+int hbmr_tera_tie_fix_records(uint64_t* hi, uint64_t* lo, void* rec, long n,
+                              int record_bytes, int shift, unsigned int* flag, hipStream_t st) {
   if (n <= 1) return 0;
-  if (record_bytes % 4 || record_bytes > 4 * 64) return (int)hipErrorInvalidValue;
+  if (record_bytes % 4 || record_bytes > 4 * 64 || shift < 0 || shift > 63)
+    return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(tera_tie_fix_records_kernel, dim3((unsigned)ceil_div(n - 1, 256)), dim3(256),
-                     0, st, hi, lo, reinterpret_cast<uint32_t*>(rec), n, record_bytes / 4, flag);
+                     0, st, hi, lo, reinterpret_cast<uint32_t*>(rec), n, record_bytes / 4, shift,
+                     flag);
   return (int)hipGetLastError();
 }
 

@@ -339,7 +339,7 @@ def test_gpu_merge_runs_matches_cpu(sizes):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ties", [0, 5, 100])
+@pytest.mark.parametrize("ties", [0, 5, 100, "prefix"])
 def test_gpu_sort_gathered_packed_ids(ties):
     """Reduce v4 (hi + packed-id sort, one gather, lo from the gathered records,
     in-place tie fix-up): the records of three map outputs come out in key
@@ -347,7 +347,12 @@ def test_gpu_sort_gathered_packed_ids(ties):
     handles -> None, the caller's full-key path)."""
     parts_c = [torch.from_numpy(S.teragen_cpu(1000 * i, 20_000 + i)) for i in range(3)]
     for p in parts_c:
-        if ties == 100:
+        if ties == "prefix":
+            # runs of 8 keys sharing the sorted 48-bit prefix (bytes 0-5) but
+            # not bytes 6-9: the tie fix must order them by the full key
+            for k in range(20):
+                p[k * 8:(k + 1) * 8, :6] = p[k * 8, :6]
+        elif ties == 100:
             p[:100, :8] = p[0, :8]                 # one run longer than the fix-up
         else:
             for k in range(ties):                  # runs of 8 equal high words
