@@ -82,7 +82,8 @@ _SIGS = {
     "hbmr_tera_partition_workspace_bytes": (c_long, [c_long, c_int]),
     "hbmr_tera_collect_gid": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_long,
                                       c_void_p, c_void_p, c_void_p]),
-    "hbmr_gather_records_gid": (c_int, [c_void_p, c_void_p, c_long, c_int, c_void_p, c_void_p]),
+    "hbmr_gather_records_gid": (c_int, [c_void_p, c_void_p, c_long, c_int, c_void_p, c_void_p,
+                                        c_void_p, c_void_p]),
     "hbmr_tera_tie_fix_records": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_int, c_int,
                                           c_void_p, c_void_p]),
     "hbmr_merge_path": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p,

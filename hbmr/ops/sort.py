@@ -451,8 +451,10 @@ def tera_collect_gid(his, rows, starts, lens, stream=None):
     return ohi, gid
 
 
-def gather_records_gid(bases, gid: torch.Tensor, stream=None) -> torch.Tensor:
-    """out[i] = bases[gid[i] >> 24][gid[i] & 0xFFFFFF] (100-byte records)."""
+def gather_records_gid(bases, gid: torch.Tensor, stream=None, keys=None) -> torch.Tensor:
+    """out[i] = bases[gid[i] >> 24][gid[i] & 0xFFFFFF] (100-byte records).
+    ``keys`` = (hi, lo) int64 [n] tensors also receive the gathered records'
+    keys (as tera_keys would read them back), on the GPU in the same pass."""
     n = gid.numel()
     rb = bases[0].shape[1]
     if not _on_gpu(gid):
@@ -463,11 +465,16 @@ def gather_records_gid(bases, gid: torch.Tensor, stream=None) -> torch.Tensor:
             m = s == j
             if m.any():
                 res[m] = b[r[m]]
+        if keys is not None:
+            h, lo = tera_keys(res)
+            keys[0].copy_(h)
+            keys[1].copy_(lo)
         return res
     res = torch.empty(n, rb, dtype=torch.uint8, device=gid.device)
     tb = _ptr_table(bases, gid.device)
-    rc = _lib.load().hbmr_gather_records_gid(_ptr(tb), _ptr(gid), n, rb, _ptr(res),
-                                              _lib.stream_handle(stream))
+    kh, kl = keys if keys is not None else (None, None)
+    rc = _lib.load().hbmr_gather_records_gid(_ptr(tb), _ptr(gid), n, rb, _ptr(res), _ptr(kh),
+                                              _ptr(kl), _lib.stream_handle(stream))
     _lib.check(rc, "hbmr_gather_records_gid")
     return res
 
@@ -483,10 +490,11 @@ def sort_gathered(his, rows, starts, lens, bases, stream=None):
     # the top 48 bits of hi (6 passes); the tie fix orders equal prefixes by
     # the full key read back from the records
     radix_sort_pairs(h, gid, TIE_SHIFT, 64, stream=stream)
-    recs = gather_records_gid(bases, gid, stream=stream)
+    # the sorted keys come with the gather (lo is new; h is rewritten with the
+    # same values): no second pass over the records
+    lo = torch.empty_like(h)
+    recs = gather_records_gid(bases, gid, stream=stream, keys=(h, lo))
     del gid
-    _h2, lo = tera_keys(recs, stream=stream)
-    del _h2
     if not _on_gpu(recs):
         order = np.lexsort((lo.numpy().view(np.uint64), h.numpy().view(np.uint64)))
         o = torch.from_numpy(order)

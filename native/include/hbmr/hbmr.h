@@ -85,7 +85,8 @@ int hbmr_tera_collect_gid(const uint64_t* const* his, const uint32_t* const* row
                           const long* starts, const long* prefix, int S, long n, uint64_t* ohi,
                           uint32_t* ogid, hipStream_t st);
 int hbmr_gather_records_gid(const void* const* bases, const uint32_t* gid, long n,
-                            int record_bytes, void* dst, hipStream_t st);
+                            int record_bytes, void* dst, uint64_t* hi, uint64_t* lo,
+                            hipStream_t st);
 int hbmr_tera_tie_fix_records(uint64_t* hi, uint64_t* lo, void* rec, long n,
                               int record_bytes, int shift, unsigned int* flag, hipStream_t st);
 int hbmr_merge_path(const uint64_t* ahi, const uint64_t* alo, const uint32_t* av, long na,

@@ -803,10 +803,14 @@ __global__ __launch_bounds__(256) void tera_collect_gid_kernel(
   }
 }
 
+// (with key outputs: the lanes holding words 0-2 of a record also store its
+// key — hi as two byte-swapped halves, lo from word 2 — so the sorted keys
+// need no second pass over the gathered records)
 template <int U>
 __global__ __launch_bounds__(256) void gather_records_gid_kernel(
     const uint32_t* const* __restrict__ bases, const uint32_t* __restrict__ gid, long n,
-    int words, uint32_t* __restrict__ dst) {
+    int words, uint32_t* __restrict__ dst, uint32_t* __restrict__ khi,
+    uint64_t* __restrict__ klo) {
   const int rpb = 256 / words;
   const int t = threadIdx.x;
   if (t >= rpb * words) return;
@@ -831,6 +835,18 @@ __global__ __launch_bounds__(256) void gather_records_gid_kernel(
     for (int j = 0; j < U; ++j) {
       const long r = r0 + j * stride;
       if (r < n) dst[r * words + w] = v[j];
+    }
+    if (khi != nullptr && w < 3) {
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const long r = r0 + j * stride;
+        if (r >= n) continue;
+        if (w < 2) {
+          khi[2 * r + 1 - w] = __builtin_bswap32(v[j]);  // hi = bytes 0-7, big-endian
+        } else {
+          klo[r] = ((uint64_t)(v[j] & 0xFFu) << 8) | ((v[j] >> 8) & 0xFFu);  // bytes 8-9
+        }
+      }
     }
   }
 }
@@ -1073,15 +1089,18 @@ int hbmr_tera_collect_gid(const uint64_t* const* his, const uint32_t* const* row
 }
 
 int hbmr_gather_records_gid(const void* const* bases, const uint32_t* gid, long n,
-                            int record_bytes, void* dst, hipStream_t st) {
+                            int record_bytes, void* dst, uint64_t* hi, uint64_t* lo,
+                            hipStream_t st) {
   if (n <= 0) return 0;
   if (record_bytes % 4 || record_bytes > 4 * 64) return (int)hipErrorInvalidValue;
+  if ((hi == nullptr) != (lo == nullptr) || (hi != nullptr && record_bytes < 12))
+    return (int)hipErrorInvalidValue;
   const int words = record_bytes / 4;
   constexpr int U = 4;
   const long grid = std::min<long>(ceil_div(n, (256 / words) * U), 1L << 18);
   hipLaunchKernelGGL(gather_records_gid_kernel<U>, dim3((unsigned)grid), dim3(256), 0, st,
                      reinterpret_cast<const uint32_t* const*>(bases), gid, n, words,
-                     reinterpret_cast<uint32_t*>(dst));
+                     reinterpret_cast<uint32_t*>(dst), reinterpret_cast<uint32_t*>(hi), lo);
   return (int)hipGetLastError();
 }
 
