@@ -1808,6 +1808,216 @@ __global__ __launch_bounds__(256) void kmeans_refine_kernel(
     atomicAdd(stats + threadIdx.x, cnt[threadIdx.x]);
 }
 
+// Refine v2: the same certification and the same fp64 sums, bit for bit, laid
+// out for latency.  v1 (above) reads rows with 211 scalar dword loads and
+// reduces with ds_bpermute shuffles at 163 VGPRs (3 waves per SIMD), so a
+// flagged point waits out one L2 round trip per row.  v2 takes NM = ceil(d/128)
+// chunks at compile time, loads every row as 16-byte vectors (d % 8 == 0,
+// 16-byte aligned rows), issues the point row and all candidate rows before
+// the first FMA, and reduces over the 16-lane group with DPP row operations
+// (quad_perm, row_half_mirror, row_mirror — one DPP row is 16 lanes), which
+// add in the same pairwise order as v1's xor butterfly.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double row_sum16(double v) {
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]: xor 1
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]: xor 2
+  v += dpp_f64<0x141>(v);  // row_half_mirror: the other quad of the half-row
+  v += dpp_f64<0x140>(v);  // row_mirror: the other half of the row
+  return v;
+}
+
+template <int NM>
+__device__ __forceinline__ void load_row8(const float* __restrict__ r, int d, int sub,
+                                          float (&v)[8 * NM]) {
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    const int b = 8 * sub + 8 * kRefineGroup * m;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), c = a;
+    if (b < d) {
+      a = *reinterpret_cast<const float4*>(r + b);
+      c = *reinterpret_cast<const float4*>(r + b + 4);
+    }
+    v[8 * m + 0] = a.x; v[8 * m + 1] = a.y; v[8 * m + 2] = a.z; v[8 * m + 3] = a.w;
+    v[8 * m + 4] = c.x; v[8 * m + 5] = c.y; v[8 * m + 6] = c.z; v[8 * m + 7] = c.w;
+  }
+}
+
+// R rows' |x - c|^2 (features past d are zero on both sides: fma(0, 0, acc) = acc)
+template <int NM, int R>
+__device__ __forceinline__ void rows_dist2(const double (&xv)[8 * NM],
+                                           const float* const (&rows)[R], int d, int sub,
+                                           double (&out)[R]) {
+  float cv[R][8 * NM];
+#pragma unroll
+  for (int r = 0; r < R; ++r) load_row8<NM>(rows[r], d, sub, cv[r]);
+  double acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = 0.0;
+#pragma unroll
+  for (int i = 0; i < 8 * NM; ++i)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const double e = xv[i] - (double)cv[r][i];
+      acc[r] = fma(e, e, acc[r]);
+    }
+#pragma unroll
+  for (int r = 0; r < R; ++r) out[r] = row_sum16(acc[r]);
+}
+
+template <int NM>
+__global__ __launch_bounds__(256) void kmeans_refine_v2_kernel(
+    const float* __restrict__ X32, long n, int d, int ldx, const float* __restrict__ xnorm,
+    const float* __restrict__ xbn2, const float* __restrict__ xerr,
+    const float* __restrict__ C32, int k, const float* __restrict__ cnorm,
+    const float* __restrict__ cmax, const float* __restrict__ cerr,
+    const float* __restrict__ cerrmax, double pack_rel,
+    const int32_t* __restrict__ nbr_idx, const float* __restrict__ nbr_dist, int L,
+    int32_t* __restrict__ labels, const int32_t* __restrict__ cand,
+    const float* __restrict__ score, const float* __restrict__ margin,
+    unsigned long long* __restrict__ stats, int nstats) {
+  const long p = (long)blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  __shared__ unsigned long long cnt[5];
+  if (threadIdx.x < 5) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const double u = 0x1.004p-8;
+  const double inflate = 1.0 + 0x1p-20;
+  const double gam = (double)(d + 2) * 0x1p-23 * 1.01;
+  const double cm = (double)cmax[0] * inflate;
+  const double cem = (double)cerrmax[0] * inflate;
+  bool flag = false;
+  int b = 0, s2 = 0, s3 = 0;
+  double xn = 0.0, x2 = 0.0, sb = 0.0, m3 = 0.0, amax = 0.0;
+  if (p < n) {
+    b = labels[p];
+    s2 = cand[p];
+    s3 = cand[n + p];
+    if (s2 < k) {
+      xn = (double)xnorm[p] * inflate;
+      x2 = (double)xbn2[p];
+      sb = score[p];
+      const double m2 = margin[p];
+      m3 = margin[n + p];
+      const double xe = (double)xerr[p];
+      amax = (xe + cem) * inflate;
+      double eb, es, dl_b, dl_s;
+      exact_bound(sb, (double)cnorm[b] * inflate, xn, x2, (xe + (double)cerr[b]) * inflate, u,
+                  gam, pack_rel, eb, dl_b);
+      exact_bound(sb - m2, cm, xn, x2, amax, u, gam, pack_rel, es, dl_s);
+      flag = !(m2 > eb + es && dl_s >= 2.0 * amax);
+    }
+  }
+  unsigned long long mask = __ballot(flag);
+  if (lane == 0 && mask) atomicAdd(&cnt[0], (unsigned long long)__popcll(mask));
+  const int grp = lane / kRefineGroup, sub = lane % kRefineGroup;
+  while (mask) {
+    unsigned long long m = mask;
+    for (int i = 0; i < grp && m; ++i) m &= m - 1;
+    const bool have = m != 0;
+    const int src = have ? __ffsll((long long)m) - 1 : 0;
+    for (int i = 0; i < 4 && mask; ++i) mask &= mask - 1;
+    const long q = __shfl(p, src);
+    const int qb = __shfl(b, src), qs = __shfl(s2, src), qt = __shfl(s3, src);
+    const double qsb = __shfl(sb, src), qm3 = __shfl(m3, src);
+    const double qxn = __shfl(xn, src), qx2 = __shfl(x2, src), qamax = __shfl(amax, src);
+    if (!have) continue;
+    const bool t_real = qt < k;
+    double xv[8 * NM];
+    {
+      float xf[8 * NM];
+      load_row8<NM>(X32 + (size_t)q * ldx, d, sub, xf);
+#pragma unroll
+      for (int i = 0; i < 8 * NM; ++i) xv[i] = (double)xf[i];
+    }
+    double d3[3];
+    {
+      const float* const rows[3] = {C32 + (size_t)qb * d, C32 + (size_t)qs * d,
+                                    C32 + (size_t)(t_real ? qt : qb) * d};
+      rows_dist2<NM, 3>(xv, rows, d, sub, d3);
+    }
+    int w = qb;
+    double dw = d3[0];
+    if (d3[1] < dw || (d3[1] == dw && qs < w)) { w = qs; dw = d3[1]; }
+    if (t_real && (d3[2] < dw || (d3[2] == dw && qt < w))) { w = qt; dw = d3[2]; }
+    bool certified = !t_real;
+    if (t_real) {
+      double et, dl_t;
+      exact_bound(qsb - qm3, cm, qxn, qx2, qamax, u, gam, pack_rel, et, dl_t);
+      certified = 0.5 * (qx2 - dw) - qx2 * 0x1p-23 > (qsb - qm3) + et &&
+                  dl_t >= 2.0 * qamax;
+    }
+    if (!certified) {
+      if (sub == 0) atomicAdd(&cnt[2], 1ull);
+      const int w0 = w;
+      const double r0 = sqrt(dw);
+      bool done = false;
+      const int32_t* ni = nbr_idx + (size_t)w0 * L;
+      const float* nd = nbr_dist + (size_t)w0 * L;
+      const float* cw0 = C32 + (size_t)w0 * d;
+      int evals = 0;
+      for (int jj = 0; jj < L; jj += 4) {
+        const double lim = (r0 + sqrt(dw)) * (1.0 + 0x1p-40);
+        if ((double)nd[jj] > lim) {
+          done = true;
+          break;
+        }
+        int jv[4];
+        const float* cp[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const bool ok = jj + v < L && (double)nd[jj + v] <= lim;
+          jv[v] = ok ? ni[jj + v] : -1;
+          cp[v] = ok ? C32 + (size_t)jv[v] * d : cw0;
+        }
+        double dj[4];
+        rows_dist2<NM, 4>(xv, cp, d, sub, dj);
+        evals += 4;
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          if (jv[v] >= 0 && (dj[v] < dw || (dj[v] == dw && jv[v] < w))) { w = jv[v]; dw = dj[v]; }
+      }
+      if (sub == 0) {
+        atomicAdd(&cnt[3], (unsigned long long)evals);
+        if (!done && L < k) atomicAdd(&cnt[4], 1ull);
+      }
+      if (!done && L < k) {
+        for (int j = 0; j < k; j += 4) {
+          const float* cp[4];
+#pragma unroll
+          for (int v = 0; v < 4; ++v) cp[v] = C32 + (size_t)(j + v < k ? j + v : j) * d;
+          double dj[4];
+          rows_dist2<NM, 4>(xv, cp, d, sub, dj);
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            if (j + v < k && (dj[v] < dw || (dj[v] == dw && j + v < w))) { w = j + v; dw = dj[v]; }
+        }
+      }
+    }
+    if (sub == 0 && w != qb) {
+      labels[q] = w;
+      atomicAdd(&cnt[1], 1ull);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < (nstats < 5 ? 3 : 5) && cnt[threadIdx.x])
+    atomicAdd(stats + threadIdx.x, cnt[threadIdx.x]);
+}
+
+int refine_version() {
+  static int v = 0;
+  if (!v) {
+    const char* e = getenv("HBMR_REFINE");
+    v = (e && atoi(e) == 1) ? 1 : 2;
+  }
+  return v;
+}
+
 template <int D>
 int launch_assign_top3(const void* X, long n, const void* C, const float* chalf, int k_pad,
                        int32_t* labels, int32_t* cand, float* scores, float* margin,
@@ -2302,6 +2512,16 @@ int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float
   while ((1 << tb) < k_pad / 32) ++tb;
   const double pack_rel = ldexp(1.0, 4 + tb - 23);
   const long blocks = (n + 255) / 256;
+  // v2 wants whole 8-feature lane slices and 16-byte aligned rows
+  const bool v2_ok = d % 8 == 0 && ldx % 4 == 0 && ((uintptr_t)X32 & 15) == 0 &&
+                     ((uintptr_t)C32 & 15) == 0;
+  if (v2_ok && refine_version() == 2) {
+    auto kern = d <= 128 ? kmeans_refine_v2_kernel<1> : kmeans_refine_v2_kernel<2>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, st, X32, n, d, ldx, xnorm,
+                       xbn2, xerr, C32, k, cnorm, cmax, cerr, cerrmax, pack_rel, nbr_idx,
+                       nbr_dist, L, labels, cand, scores, margin, stats, nstats);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(kmeans_refine_kernel, dim3((unsigned)blocks), dim3(256), 0, st, X32, n, d,
                      ldx, xnorm, xbn2, xerr, C32, k, cnorm, cmax, cerr, cerrmax, pack_rel,
                      nbr_idx, nbr_dist, L,
