@@ -304,13 +304,15 @@ class TeraSortSplitJob(SplitJob):
                 "checksum_ok": (c_in - c_out) % (1 << 64) == 0, "partitions": nparts or 1,
                 "peak_hbm_bytes": int(peak)}
 
-    def _sorted_partition(self, his, los, rows, starts, lens, bases, dev, stream=None):
+    def _sorted_partition(self, his, los, rows, starts, lens, bases, dev, stream=None,
+                          hi_range=None):
         """Collect one partition's pieces from every map output, sort its keys,
         gather its records: (records, sorted hi, sorted lo).  The packed-id
         path (v4, hbmr.terasort.reduce.gid) when the map outputs allow it."""
         if self.gid and len(bases) <= S.GID_MAX_SPLITS and \
                 max(b.shape[0] for b in bases) < S.GID_MAX_ROWS:
-            got = S.sort_gathered(his, rows, starts, lens, bases, stream=stream)
+            got = S.sort_gathered(his, rows, starts, lens, bases, stream=stream,
+                                  hi_range=hi_range)
             if got is not None:
                 return got
         h, lw, split, row = S.tera_collect(his, los, rows, starts, lens, stream=stream)
@@ -347,13 +349,20 @@ class TeraSortSplitJob(SplitJob):
                 pb += 1
             groups.append((pa, pb))
             pa = pb
+        spl_hi = [int(h[:16], 16) for h in outs[0].get("splitters") or []] if nparts > 1 else []
         for pa, pb in groups:
             starts = offs[:, pa]
             lens = offs[:, pb] - offs[:, pa]
             m = int(lens.sum())
             if m == 0:
                 continue
-            recs, hs, ls = self._sorted_partition(his, los, rows, starts, lens, bases, dev)
+            # the group's keys lie between its partitions' splitters (inclusive
+            # in hi): the bits above their highest differing bit need no pass
+            hr = (spl_hi[pa - 1] if pa > 0 else 0,
+                  spl_hi[pb - 1] if pb < nparts else (1 << 64) - 1) \
+                if len(spl_hi) == nparts - 1 else None
+            recs, hs, ls = self._sorted_partition(his, los, rows, starts, lens, bases, dev,
+                                                  hi_range=hr)
             bad = bad + S.count_unsorted_dev(hs, ls)
             if prev_last is not None:
                 bad = bad + S.pair_greater(prev_last, (hs[:1], ls[:1]))

@@ -28,6 +28,26 @@ _SORT80 = __import__("os").environ.get("HBMR_TERA_SORT80") == "1"
 # TeraSort reduce v4: the radix sort covers hi >> TIE_SHIFT (the low bits of hi
 # and lo are ordered by the in-place tie fix); HBMR_TERA_TIE_SHIFT overrides
 TIE_SHIFT = int(os.environ.get("HBMR_TERA_TIE_SHIFT", "16"))
+# bits of hi the v4 reduce radix-sorts below a group's common key prefix (the
+# group is a key range: its splitters fix the top bits).  48 = 6 passes.
+# TeraGen keys are printable bytes (95 values of 256), so a 32-bit window
+# leaves runs of equal prefixes longer than the in-place tie fix takes and
+# the group falls back to the full-key path: 0.76 s per 100 GB instead of
+# 0.25 (profiles/r03_terasort_window.json)
+SORT_BITS = int(os.environ.get("HBMR_TERA_SORT_BITS", "48"))
+
+
+def sort_window(hi_range=None):
+    """[begin, end) bits of hi the v4 reduce sorts.  Without a range: the top
+    64 - TIE_SHIFT bits.  With the group's inclusive (low, high) hi bounds (as
+    unsigned ints): the bits above their highest differing bit are the same in
+    every key of the group, so the sort takes the SORT_BITS below that (ties on
+    the sorted prefix are ordered by the full key afterwards)."""
+    if hi_range is None or SORT_BITS <= 0:
+        return TIE_SHIFT, 64
+    lo, up = hi_range
+    end = max(8, min(64, (int(lo) ^ int(up)).bit_length()))
+    return max(0, end - SORT_BITS), end
 
 def _ptr(t):
     return None if t is None else t.data_ptr()
@@ -479,17 +499,20 @@ def gather_records_gid(bases, gid: torch.Tensor, stream=None, keys=None) -> torc
     return res
 
 
-def sort_gathered(his, rows, starts, lens, bases, stream=None):
+def sort_gathered(his, rows, starts, lens, bases, stream=None, hi_range=None):
     """TeraSort reduce v4 for one group: (hi, gid) collect, radix passes over
     the top 64 - TIE_SHIFT bits of hi carrying the gid, ONE record gather by
     gid, the low key words read back from the sorted records, and runs of an
     equal sorted prefix ordered by the full key in place.  Returns (records,
     hi, lo), or None when such a run is too long for the in-place fix-up (the
-    caller takes the full-key path)."""
+    caller takes the full-key path).  ``hi_range`` (the group's hi bounds)
+    narrows the radix passes to the bits below the group's common prefix."""
     h, gid = tera_collect_gid(his, rows, starts, lens, stream=stream)
-    # the top 48 bits of hi (6 passes); the tie fix orders equal prefixes by
-    # the full key read back from the records
-    radix_sort_pairs(h, gid, TIE_SHIFT, 64, stream=stream)
+    # the window's bits of hi (by default the 48 below the group's common
+    # prefix: 6 passes); the tie fix orders equal sorted prefixes by the full
+    # key read back from the records
+    begin, end = sort_window(hi_range)
+    radix_sort_pairs(h, gid, begin, end, stream=stream)
     # the sorted keys come with the gather (lo is new; h is rewritten with the
     # same values): no second pass over the records
     lo = torch.empty_like(h)
@@ -501,7 +524,7 @@ def sort_gathered(his, rows, starts, lens, bases, stream=None):
         return recs[o], h[o], lo[o]
     flag = torch.zeros(1, dtype=torch.int32, device=recs.device)
     rc = _lib.load().hbmr_tera_tie_fix_records(_ptr(h), _ptr(lo), _ptr(recs), recs.shape[0],
-                                                recs.shape[1], TIE_SHIFT, _ptr(flag),
+                                                recs.shape[1], begin, _ptr(flag),
                                                 _lib.stream_handle(stream))
     _lib.check(rc, "hbmr_tera_tie_fix_records")
     if int(flag.item()):

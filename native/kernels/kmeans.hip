@@ -1870,6 +1870,14 @@ __device__ __forceinline__ void rows_dist2(const double (&xv)[8 * NM],
   for (int r = 0; r < R; ++r) out[r] = row_sum16(acc[r]);
 }
 
+// neighbours per Elkan step: 2 keeps v2 at 128 VGPRs (4 waves per SIMD; 4 rows
+// in flight take 134, 3 waves).  The exit bound refreshes every step, and the
+// minimum over any superset of the one-at-a-time walk is the same winner.
+#ifndef HBMR_ELKAN_STEP
+#define HBMR_ELKAN_STEP 2
+#endif
+constexpr int kElkanStep = HBMR_ELKAN_STEP;
+
 template <int NM>
 __global__ __launch_bounds__(256) void kmeans_refine_v2_kernel(
     const float* __restrict__ X32, long n, int d, int ldx, const float* __restrict__ xnorm,
@@ -1961,25 +1969,25 @@ __global__ __launch_bounds__(256) void kmeans_refine_v2_kernel(
       const float* nd = nbr_dist + (size_t)w0 * L;
       const float* cw0 = C32 + (size_t)w0 * d;
       int evals = 0;
-      for (int jj = 0; jj < L; jj += 4) {
+      for (int jj = 0; jj < L; jj += kElkanStep) {
         const double lim = (r0 + sqrt(dw)) * (1.0 + 0x1p-40);
         if ((double)nd[jj] > lim) {
           done = true;
           break;
         }
-        int jv[4];
-        const float* cp[4];
+        int jv[kElkanStep];
+        const float* cp[kElkanStep];
 #pragma unroll
-        for (int v = 0; v < 4; ++v) {
+        for (int v = 0; v < kElkanStep; ++v) {
           const bool ok = jj + v < L && (double)nd[jj + v] <= lim;
           jv[v] = ok ? ni[jj + v] : -1;
           cp[v] = ok ? C32 + (size_t)jv[v] * d : cw0;
         }
-        double dj[4];
-        rows_dist2<NM, 4>(xv, cp, d, sub, dj);
-        evals += 4;
+        double dj[kElkanStep];
+        rows_dist2<NM, kElkanStep>(xv, cp, d, sub, dj);
+        evals += kElkanStep;
 #pragma unroll
-        for (int v = 0; v < 4; ++v)
+        for (int v = 0; v < kElkanStep; ++v)
           if (jv[v] >= 0 && (dj[v] < dw || (dj[v] == dw && jv[v] < w))) { w = jv[v]; dw = dj[v]; }
       }
       if (sub == 0) {

@@ -339,14 +339,22 @@ def test_gpu_merge_runs_matches_cpu(sizes):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("window", [None, "full", "narrow"])
 @pytest.mark.parametrize("ties", [0, 5, 100, "prefix"])
-def test_gpu_sort_gathered_packed_ids(ties):
+def test_gpu_sort_gathered_packed_ids(ties, window):
     """Reduce v4 (hi + packed-id sort, one gather, lo from the gathered records,
     in-place tie fix-up): the records of three map outputs come out in key
     order; ties = equal 8-byte prefixes per run (100: longer than the fix-up
-    handles -> None, the caller's full-key path)."""
+    handles -> None, the caller's full-key path).  window: the group's hi
+    bounds given (full range, or every key under one top byte), so the radix
+    passes cover only the SORT_BITS below the common prefix and the tie fix-up
+    orders the longer equal-prefix runs."""
     parts_c = [torch.from_numpy(S.teragen_cpu(1000 * i, 20_000 + i)) for i in range(3)]
+    hi_range = {None: None, "full": (0, (1 << 64) - 1),
+                "narrow": (0x5A << 56, (0x5B << 56) - 1)}[window]
     for p in parts_c:
+        if window == "narrow":
+            p[:, 0] = 0x5A
         if ties == "prefix":
             # runs of 8 keys sharing the sorted 48-bit prefix (bytes 0-5) but
             # not bytes 6-9: the tie fix must order them by the full key
@@ -363,7 +371,7 @@ def test_gpu_sort_gathered_packed_ids(ties):
     his = [o[0] for o in outs]
     rows = [o[2] for o in outs]
     lens = [p.shape[0] for p in parts]
-    got = S.sort_gathered(his, rows, [0, 0, 0], lens, parts)
+    got = S.sort_gathered(his, rows, [0, 0, 0], lens, parts, hi_range=hi_range)
     if ties == 100:
         assert got is None
         return
