@@ -608,11 +608,8 @@ class KMeansSplitJob(SplitJob):
             need = km.delta_workspace_bytes(total, H, self.k)
             if scratch.get("dws") is None or scratch["dws"].numel() < need:
                 scratch["dws"] = torch.empty(need, dtype=torch.uint8, device=ctx.device)
-            off = 0
-            for i, n in zip(have, ns):
-                lab[off:off + n].copy_(km.assign_exact(datas[i], img, stats, scratch,
-                                                       stream=ctx.stream))
-                off += n
+            km.assign_exact_batch([datas[i] for i in have], img, stats, lab, scratch,
+                                  stream=ctx.stream)
             hb = [bases[i] for i in have]
             km.delta_combine([datas[i].x32 for i in have], lab, self.k, sums[:H], counts[:H],
                              scratch["dws"], hb, fx_shift=img.fx_shift, stream=ctx.stream)

@@ -318,6 +318,58 @@ def assign_exact(split: ExactSplit, img: CentroidImage, stats: torch.Tensor,
     return lab
 
 
+def assign_exact_batch(splits: list, img: CentroidImage, stats: torch.Tensor, out: torch.Tensor,
+                       scratch: dict | None = None, stream=None) -> None:
+    """Exact labels of a batch of splits, written back to back into ``out``
+    (int32 [sum n]): the top-3 assign and the certification per split, with
+    the centroid norms / neighbour lists fetched once, the batch's labels
+    written in place (no per-split copy) and the candidate / score / margin
+    scratch shared by every split (one stream orders the reuse)."""
+    if not splits:
+        return
+    dev = splits[0].xb.device
+    total = sum(sp.shape[0] for sp in splits)
+    if out.dtype != torch.int32 or out.numel() < total or not out.is_contiguous():
+        raise ValueError("out must be contiguous int32 with room for every split's labels")
+    if stats.dtype != torch.int64 or stats.numel() < 3:
+        raise ValueError("stats must be int64 [3]")
+    for sp in splits:
+        if sp.xb.dtype != torch.bfloat16 or sp.xb.shape[1] != img.dp or \
+                not sp.xb.is_contiguous() or not sp.x32.is_contiguous():
+            raise ValueError("exact splits must hold contiguous [n, dp] rows of the image's dp")
+    nmax = max(sp.shape[0] for sp in splits)
+    scratch = {} if scratch is None else scratch
+    key = ("exact-batch", nmax)
+    bufs = scratch.get(key)
+    if bufs is None:
+        for kk in [kk for kk in scratch if isinstance(kk, tuple) and kk[0] == "exact-batch"]:
+            del scratch[kk]
+        bufs = scratch[key] = (torch.empty(2 * nmax, dtype=torch.int32, device=dev),
+                               torch.empty(nmax, dtype=torch.float32, device=dev),
+                               torch.empty(2 * nmax, dtype=torch.float32, device=dev))
+    cand, sc, mg = bufs
+    with torch.cuda.stream(stream) if stream is not None else _nullctx():
+        cn, cmax, ce, cemax = img.norms()
+        ni, nd, L = img.neighbors()
+    lib = _lib.load()
+    st = _lib.stream_handle(stream)
+    pc, ps, pm, pst = _ptr(cand), _ptr(sc), _ptr(mg), _ptr(stats)
+    pcn, pcmax, pce, pcemax, pni, pnd = (_ptr(t) for t in (cn, cmax, ce, cemax, ni, nd))
+    base, off = out.data_ptr(), 0
+    for sp in splits:
+        n = sp.shape[0]
+        pl = ctypes.c_void_p(base + 4 * off)
+        rc = lib.hbmr_kmeans_assign_top3_bf16(_ptr(sp.xb), n, img.dp, _ptr(img.cbf),
+                                              _ptr(img.chalf), img.k_pad, pl, pc, ps, pm, st)
+        _lib.check(rc, "hbmr_kmeans_assign_top3_bf16")
+        rc = lib.hbmr_kmeans_refine_f32(
+            _ptr(sp.x32), n, img.d, sp.x32.shape[1], _ptr(sp.xnorm), _ptr(sp.xbn2),
+            _ptr(sp.xerr), _ptr(img.cen), img.k, img.k_pad, pcn, pcmax, pce, pcemax, pni, pnd, L,
+            pl, pc, ps, pm, pst, stats.numel(), st)
+        _lib.check(rc, "hbmr_kmeans_refine_f32")
+        off += n
+
+
 def map_split_exact(split: ExactSplit, img: CentroidImage, sums, counts, scratch: dict,
                     stats: torch.Tensor, stream=None) -> None:
     """One exact-mode GPU map task: top-3 assign, certification + fp64 re-score,

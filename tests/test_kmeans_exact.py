@@ -116,6 +116,25 @@ def test_exact_assign_agrees_with_fp64(d):
 
 
 @pytest.mark.gpu
+def test_assign_exact_batch_equals_per_split():
+    """The batched exact assign (labels written back to back, shared scratch)
+    gives each split the labels and stats the per-split call gives."""
+    from hbmr.ops import kmeans as km
+    d, k = 128, 256
+    x, c = _blobs(210_000, d, k, 5)
+    img = km.CentroidImage(c, "cuda")
+    cuts = [0, 50_000, 130_000, 210_000]           # splits of different sizes
+    sps = [km.ExactSplit(x[a:b].contiguous(), km.padded_dim(d)) for a, b in zip(cuts, cuts[1:])]
+    s1 = torch.zeros(5, dtype=torch.int64, device="cuda")
+    want = torch.cat([km.assign_exact(sp, img, s1).clone() for sp in sps])
+    s2 = torch.zeros(5, dtype=torch.int64, device="cuda")
+    got = torch.full((cuts[-1] + 7,), -1, dtype=torch.int32, device="cuda")
+    km.assign_exact_batch(sps, img, s2, got, {})
+    assert torch.equal(got[:cuts[-1]], want) and int((got[cuts[-1]:] != -1).sum()) == 0
+    assert s1.tolist() == s2.tolist()
+
+
+@pytest.mark.gpu
 def test_accum_f32_is_fixed_point_of_fp32_data():
     from hbmr.ops import kmeans as km
     n, d, k = 300000, 128, 1024
