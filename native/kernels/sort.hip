@@ -15,6 +15,7 @@
 //   key extraction, 100-byte record gather by permutation, splitter search for
 //   range partitioning (TeraSort.java:57-211's trie partitioner), and an
 //   order check (TeraValidate).
+#include <string>
 #include "common.h"
 #include "../include/hbmr/hbmr.h"
 
@@ -806,7 +807,7 @@ __global__ __launch_bounds__(256) void tera_collect_gid_kernel(
 // (with key outputs: the lanes holding words 0-2 of a record also store its
 // key — hi as two byte-swapped halves, lo from word 2 — so the sorted keys
 // need no second pass over the gathered records)
-template <int U>
+template <int U, bool NT = false>
 __global__ __launch_bounds__(256) void gather_records_gid_kernel(
     const uint32_t* const* __restrict__ bases, const uint32_t* __restrict__ gid, long n,
     int words, uint32_t* __restrict__ dst, uint32_t* __restrict__ khi,
@@ -834,7 +835,12 @@ __global__ __launch_bounds__(256) void gather_records_gid_kernel(
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       const long r = r0 + j * stride;
-      if (r < n) dst[r * words + w] = v[j];
+      if (r < n) {
+        if constexpr (NT)
+          __builtin_nontemporal_store(v[j], dst + r * words + w);  // streamed: no L2 reuse
+        else
+          dst[r * words + w] = v[j];
+      }
     }
     if (khi != nullptr && w < 3) {
 #pragma unroll
@@ -1096,9 +1102,21 @@ int hbmr_gather_records_gid(const void* const* bases, const uint32_t* gid, long 
   if ((hi == nullptr) != (lo == nullptr) || (hi != nullptr && record_bytes < 12))
     return (int)hipErrorInvalidValue;
   const int words = record_bytes / 4;
-  constexpr int U = 4;
+  // HBMR_GATHER=u8 / nt / u8nt: 8 records in flight per lane and/or streamed
+  // (non-temporal) stores of the gathered records, for A/B
+  static const int mode = [] {
+    const char* e = getenv("HBMR_GATHER");
+    if (!e) return 0;
+    const std::string m(e);
+    return (m.find("u8") != std::string::npos ? 1 : 0) | (m.find("nt") != std::string::npos ? 2 : 0);
+  }();
+  const int U = (mode & 1) ? 8 : 4;
+  auto kern = mode == 0 ? gather_records_gid_kernel<4, false>
+            : mode == 1 ? gather_records_gid_kernel<8, false>
+            : mode == 2 ? gather_records_gid_kernel<4, true>
+                        : gather_records_gid_kernel<8, true>;
   const long grid = std::min<long>(ceil_div(n, (256 / words) * U), 1L << 18);
-  hipLaunchKernelGGL(gather_records_gid_kernel<U>, dim3((unsigned)grid), dim3(256), 0, st,
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), 0, st,
                      reinterpret_cast<const uint32_t* const*>(bases), gid, n, words,
                      reinterpret_cast<uint32_t*>(dst), reinterpret_cast<uint32_t*>(hi), lo);
   return (int)hipGetLastError();
