@@ -179,7 +179,7 @@ class TaskInProgress:
 class JobInProgress:
     def __init__(self, jt, job_id: JobID, conf):
         self.jt = jt
-        self.fold_lock = threading.Lock()
+        self.fold_lock = threading.RLock()   # counters() holds it around fold_counters
         self.job_id = job_id
         self.conf = conf
         self.status = JobStatus(job_id, PREP)
@@ -306,7 +306,13 @@ class JobInProgress:
 
     def fold_counters(self) -> Counters:
         """Merge the counters of newly succeeded attempts (and the locality
-        levels counted by obtain_map) into the job's."""
+        levels counted by obtain_map) into the job's.  Under fold_lock: a
+        client reading counters while the job-finish path folds must not
+        return before the batch the other thread swapped out is merged."""
+        with self.fold_lock:
+            return self._fold_counters_locked()
+
+    def _fold_counters_locked(self) -> Counters:
         lc = self.loc_counts
         if any(lc):
             hbm, data, rack = lc
