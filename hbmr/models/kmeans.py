@@ -53,9 +53,12 @@ RETURN_KEY = "hbmr.kmeans.return.centroids"   # reduce result carries the new ce
 # so a tracker whose GPU worker restarted can re-localise the input centroids of
 # the next iteration (the DistributedCache role; the fast path stays in memory)
 CDIR_KEY = "hbmr.kmeans.centroids.dir"
-# exact mode: bf16 MFMA assign certified against the fp32 data (top-3 + fp64
+# exact mode: 16-bit MFMA assign certified against the fp32 data (top-3 + fp64
 # re-score of uncertain points) and fp32 fixed-point sums (ops.kmeans.ExactSplit)
 EXACT_KEY = "hbmr.kmeans.exact"
+# exact mode's MFMA operand type: "f16" (default: 11 significant bits, ~8x fewer
+# points to re-score than bf16) or "bf16"
+EXACT_MFMA_KEY = "hbmr.kmeans.exact.mfma"
 # GPU combiner: "delta" (default) sums only the points whose label changed
 # against the split's reference partition (ops.kmeans.Baseline) — bit-identical
 # to "sorted", the counting-sort combiner over every point
@@ -326,6 +329,8 @@ class KMeansSplitJob(SplitJob):
         self.fx_shift = conf.get_int("hbmr.kmeans.fx.shift", 24)
         self.cdir = conf.get(CDIR_KEY)
         self.exact = conf.get_boolean(EXACT_KEY, False)
+        self.exact_dtype = torch.bfloat16 if (conf.get(EXACT_MFMA_KEY) or "f16").lower() in (
+            "bf16", "bfloat16") else torch.float16
         self.combiner = (conf.get(COMBINER_KEY) or "delta").lower()
         if self.combiner not in ("delta", "sorted"):
             raise ValueError(f"{COMBINER_KEY} must be delta or sorted, not {self.combiner!r}")
@@ -435,7 +440,7 @@ class KMeansSplitJob(SplitJob):
         while _PINNED_INFLIGHT and _PINNED_INFLIGHT[0][0].query():
             _PINNED_INFLIGHT.pop(0)
         if self.exact:
-            return km.ExactSplit(x, km.padded_dim(self.d))
+            return km.ExactSplit(x, km.padded_dim(self.d), self.exact_dtype)
         xb = x.to(torch.bfloat16)
         dp = km.padded_dim(self.d)
         if dp == self.d:
@@ -483,7 +488,7 @@ class KMeansSplitJob(SplitJob):
             x = self._load_raw(spec, device)
             if str(device) == "cpu":
                 return x.contiguous()
-            return km.ExactSplit(x, km.padded_dim(self.d))
+            return km.ExactSplit(x, km.padded_dim(self.d), self.exact_dtype)
         xb = self._load_fp32(spec, device)
         if str(device) == "cpu":
             return xb.to(torch.float32)

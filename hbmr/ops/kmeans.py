@@ -86,7 +86,7 @@ class CentroidImage:
                                     _ptr(self.chalf), _ptr(self.shift2),
                                     _lib.stream_handle(stream))
         _lib.check(rc, "hbmr_kmeans_update")
-        self._norms = None     # exact mode's |c_j| and neighbour table: built on demand
+        self._img16 = {}       # exact mode's 16-bit images and neighbour table: on demand
         self._nbr = None
         if getattr(self, "_nbr_lock", None) is None:
             self._nbr_lock = threading.Lock()
@@ -95,21 +95,37 @@ class CentroidImage:
         self.cen.copy_(centroids.to(self.cen.device, torch.float32))
         self.refresh(stream=stream)
 
-    def norms(self):
-        """(|c_j| [k], max_j |c_j| [1], |c_j - c~_j| [k], max_j |c_j - c~_j| [1])
-        fp32 of the fp32 master centroids and their bf16 image (exact mode's
-        certification bound; the errors rounded up), computed in fp64 once per
-        image on the first caller's stream; other streams wait on it."""
+    def image16(self, dtype=torch.float16):
+        """Exact mode's 16-bit centroid image for MFMA operands of ``dtype``
+        (fp16, the default, or bf16): (c16 [k_pad, dp], chalf [k_pad] =
+        -|c~|²/2, |c_j| [k], max |c_j| [1], |c_j - c~_j| [k], max [1]) — norms
+        and rounding errors in fp64 rounded up (hbmr_kmeans_image16), built
+        once per image on the first caller's stream; other streams wait."""
         with self._nbr_lock:
-            if self._norms is None:
-                c64 = self.cen.double()
-                cn = c64.norm(dim=1).float()
-                ce = _f32_up((c64 - self.cbf[:self.k, :self.d].double()).norm(dim=1))
+            cache = self.__dict__.setdefault("_img16", {})
+            ent = cache.get(dtype)
+            if ent is None:
+                dev = self.cen.device
+                c16 = torch.empty(self.k_pad, self.dp, dtype=dtype, device=dev)
+                ch = torch.empty(self.k_pad, dtype=torch.float32, device=dev)
+                cn = torch.empty(self.k, dtype=torch.float32, device=dev)
+                ce = torch.empty(self.k, dtype=torch.float32, device=dev)
+                mx = torch.empty(2, dtype=torch.float32, device=dev)
+                rc = _lib.load().hbmr_kmeans_image16(
+                    _ptr(self.cen), self.k, self.d, self.dp, self.k_pad,
+                    int(dtype == torch.float16), _ptr(c16), _ptr(ch), _ptr(cn), _ptr(ce),
+                    _ptr(mx), _lib.stream_handle(None))
+                _lib.check(rc, "hbmr_kmeans_image16")
                 ev = torch.cuda.Event()
                 ev.record()
-                self._norms = (cn, cn.max().reshape(1), ce, ce.max().reshape(1), ev)
-        cn, cm, ce, cem, ev = self._norms
-        torch.cuda.current_stream().wait_event(ev)
+                ent = cache[dtype] = (c16, ch, cn, mx[0:1], ce, mx[1:2], ev)
+        torch.cuda.current_stream().wait_event(ent[6])
+        return ent[:6]
+
+    def norms(self, dtype=torch.float16):
+        """(|c_j| [k], max_j |c_j| [1], |c_j - c~_j| [k], max_j |c_j - c~_j| [1])
+        for the 16-bit image of ``dtype`` (exact mode's certification bound)."""
+        _, _, cn, cm, ce, cem = self.image16(dtype)
         return cn, cm, ce, cem
 
     def neighbors(self, L: int | None = None):
@@ -223,30 +239,42 @@ def _f32_up(v: torch.Tensor) -> torch.Tensor:
 
 
 class ExactSplit:
-    """A split held for exact mode (``hbmr.kmeans.exact``): the bf16 copy the
-    MFMA assign reads, the fp32 data (rows padded to dp) the certification
-    re-score and the combiner read, and per point |x| (fp32 data), |x~|²
-    (bf16 copy) and the rounding error |x - x~| (an upper bound), computed in
-    fp64 once when the split is made resident."""
+    """A split held for exact mode (``hbmr.kmeans.exact``): the 16-bit copy the
+    MFMA assign reads (``xb``: fp16 by default — 11 significant bits, so the
+    certification flags ~8x fewer points than with bf16's 8 — or bf16), the
+    fp32 data (rows padded to dp) the certification re-score and the combiner
+    read, and per point |x| (fp32 data), |x~|² (16-bit copy) and the rounding
+    error |x - x~| (an upper bound), computed in fp64 once when the split is
+    made resident (hbmr_kmeans_exact_prep)."""
     __slots__ = ("xb", "x32", "xnorm", "xbn2", "xerr", "d")
 
-    def __init__(self, x32: torch.Tensor, dp: int):
+    def __init__(self, x32: torch.Tensor, dp: int, dtype=torch.float16):
         n, d = x32.shape
         self.d = d
-        x64 = x32.double()
+        dev = x32.device
+        if dp == d:
+            self.x32 = x32.contiguous()
+        else:
+            self.x32 = torch.zeros(n, dp, dtype=torch.float32, device=dev)
+            self.x32[:, :d] = x32
+        if dev.type == "cuda":
+            self.xb = torch.empty(n, dp, dtype=dtype, device=dev)
+            self.xnorm = torch.empty(n, dtype=torch.float32, device=dev)
+            self.xbn2 = torch.empty(n, dtype=torch.float32, device=dev)
+            self.xerr = torch.empty(n, dtype=torch.float32, device=dev)
+            rc = _lib.load().hbmr_kmeans_exact_prep(
+                _ptr(self.x32), n, dp, dp, dp, int(dtype == torch.float16), _ptr(self.xb),
+                _ptr(self.xnorm), _ptr(self.xbn2), _ptr(self.xerr), _lib.stream_handle(None))
+            _lib.check(rc, "hbmr_kmeans_exact_prep")
+            return
+        x64 = self.x32.double()
         self.xnorm = x64.norm(dim=1).float()
-        xb = x32.to(torch.bfloat16)
+        lim = 65504.0 if dtype == torch.float16 else float("inf")
+        xb = self.x32.clamp(-lim, lim).to(dtype)
         xb64 = xb.double()
         self.xbn2 = xb64.pow(2).sum(1).float()
         self.xerr = _f32_up((x64 - xb64).norm(dim=1))
-        del x64, xb64
-        if dp == d:
-            self.xb, self.x32 = xb.contiguous(), x32.contiguous()
-        else:
-            self.xb = torch.zeros(n, dp, dtype=torch.bfloat16, device=x32.device)
-            self.xb[:, :d] = xb
-            self.x32 = torch.zeros(n, dp, dtype=torch.float32, device=x32.device)
-            self.x32[:, :d] = x32
+        self.xb = xb.contiguous()
 
     @property
     def shape(self):
@@ -263,38 +291,65 @@ def assign_top3(points: torch.Tensor, img: CentroidImage, labels, cand, scores, 
     cand [2n] (second | third), scores [n] (best score), margin [2n]
     (best - second | best - third)."""
     n, dp = points.shape
-    if points.dtype != torch.bfloat16 or dp != img.dp or not points.is_contiguous():
-        raise ValueError("points must be contiguous bf16 [n, dp] matching the centroid image")
+    if points.dtype not in (torch.bfloat16, torch.float16) or dp != img.dp or \
+            not points.is_contiguous():
+        raise ValueError("points must be contiguous bf16/fp16 [n, dp] matching the image")
     for t, dt, m in ((labels, torch.int32, 1), (cand, torch.int32, 2), (scores, torch.float32, 1),
                      (margin, torch.float32, 2)):
         if t.numel() != m * n or t.dtype != dt or not t.is_contiguous():
             raise ValueError("top-3 outputs: labels/scores [n], cand/margin [2n]")
-    rc = _lib.load().hbmr_kmeans_assign_top3_bf16(
-        _ptr(points), n, dp, _ptr(img.cbf), _ptr(img.chalf), img.k_pad, _ptr(labels),
+    f16 = points.dtype == torch.float16
+    with torch.cuda.stream(stream) if stream is not None else _nullctx():
+        c16, ch = img.image16(points.dtype)[:2]
+    fn = "hbmr_kmeans_assign_top3_f16" if f16 else "hbmr_kmeans_assign_top3_bf16"
+    rc = getattr(_lib.load(), fn)(
+        _ptr(points), n, dp, _ptr(c16), _ptr(ch), img.k_pad, _ptr(labels),
         _ptr(cand), _ptr(scores), _ptr(margin), _lib.stream_handle(stream))
-    _lib.check(rc, "hbmr_kmeans_assign_top3_bf16")
+    _lib.check(rc, fn)
+
+
+REFINE_VERSION = int(os.environ.get("HBMR_REFINE", "3"))
+
+
+def _refine_ws(n: int, device, scratch: dict | None):
+    """Queue workspace of refine v3 (hbmr_kmeans_refine_f32_q), kept in
+    ``scratch`` across calls (one stream orders the reuse)."""
+    need = int(_lib.load().hbmr_kmeans_refine_workspace_bytes(n))
+    ws = None if scratch is None else scratch.get("refine_ws")
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(need, dtype=torch.uint8, device=device)
+        if scratch is not None:
+            scratch["refine_ws"] = ws
+    return ws
 
 
 def refine_f32(split: ExactSplit, img: CentroidImage, labels, cand, scores, margin,
-               stats: torch.Tensor, stream=None) -> None:
-    """Certify the bf16 labels against the fp32 data; re-score the uncertain
-    points in fp64 (hbmr_kmeans_refine_f32).  stats (int64 [3]) += (flagged,
-    relabelled, points that needed the neighbour scan); a [5] stats also
-    counts the scan's neighbour distances and its full scans."""
+               stats: torch.Tensor, stream=None, scratch: dict | None = None) -> None:
+    """Certify the MFMA labels against the fp32 data; re-score the uncertain
+    points in fp64 (refine v3: the queue pipeline hbmr_kmeans_refine_f32_q;
+    HBMR_REFINE=1/2: the older single-kernel forms).  stats (int64 [3]) +=
+    (flagged, relabelled, points that needed the neighbour scan); a [5] stats
+    also counts the scan's neighbour distances and its full scans."""
     n = split.shape[0]
     if stats.dtype != torch.int64 or stats.numel() < 3:
         raise ValueError("stats must be int64 [3]")
     if labels.numel() != n or cand.numel() != 2 * n or margin.numel() != 2 * n:
         raise ValueError("labels [n], cand/margin [2n] from assign_top3 expected")
     with torch.cuda.stream(stream) if stream is not None else _nullctx():
-        cn, cmax, ce, cemax = img.norms()
+        cn, cmax, ce, cemax = img.norms(split.xb.dtype)
         ni, nd, L = img.neighbors()
-    rc = _lib.load().hbmr_kmeans_refine_f32(
-        _ptr(split.x32), n, img.d, split.x32.shape[1], _ptr(split.xnorm), _ptr(split.xbn2),
-        _ptr(split.xerr), _ptr(img.cen), img.k, img.k_pad, _ptr(cn), _ptr(cmax), _ptr(ce),
-        _ptr(cemax), _ptr(ni), _ptr(nd), L,
-        _ptr(labels), _ptr(cand), _ptr(scores), _ptr(margin), _ptr(stats), stats.numel(),
-        _lib.stream_handle(stream))
+    args = (_ptr(split.x32), n, img.d, split.x32.shape[1], _ptr(split.xnorm), _ptr(split.xbn2),
+            _ptr(split.xerr), _ptr(img.cen), img.k, img.k_pad, _ptr(cn), _ptr(cmax), _ptr(ce),
+            _ptr(cemax), _ptr(ni), _ptr(nd), L,
+            _ptr(labels), _ptr(cand), _ptr(scores), _ptr(margin), _ptr(stats), stats.numel())
+    lib = _lib.load()
+    if REFINE_VERSION >= 3:
+        ws = _refine_ws(n, split.x32.device, scratch)
+        rc = lib.hbmr_kmeans_refine_f32_q(*args, _ptr(ws), ws.numel(),
+                                          _lib.stream_handle(stream))
+        _lib.check(rc, "hbmr_kmeans_refine_f32_q")
+        return
+    rc = lib.hbmr_kmeans_refine_f32(*args, _lib.stream_handle(stream))
     _lib.check(rc, "hbmr_kmeans_refine_f32")
 
 
@@ -314,7 +369,7 @@ def assign_exact(split: ExactSplit, img: CentroidImage, stats: torch.Tensor,
                                torch.empty(2 * n, dtype=torch.float32, device=dev))
     lab, cand, sc, mg = bufs
     assign_top3(split.xb, img, lab, cand, sc, mg, stream=stream)
-    refine_f32(split, img, lab, cand, sc, mg, stats, stream=stream)
+    refine_f32(split, img, lab, cand, sc, mg, stats, stream=stream, scratch=scratch)
     return lab
 
 
@@ -333,10 +388,12 @@ def assign_exact_batch(splits: list, img: CentroidImage, stats: torch.Tensor, ou
         raise ValueError("out must be contiguous int32 with room for every split's labels")
     if stats.dtype != torch.int64 or stats.numel() < 3:
         raise ValueError("stats must be int64 [3]")
+    dt = splits[0].xb.dtype
     for sp in splits:
-        if sp.xb.dtype != torch.bfloat16 or sp.xb.shape[1] != img.dp or \
-                not sp.xb.is_contiguous() or not sp.x32.is_contiguous():
-            raise ValueError("exact splits must hold contiguous [n, dp] rows of the image's dp")
+        if sp.xb.dtype != dt or dt not in (torch.bfloat16, torch.float16) or \
+                sp.xb.shape[1] != img.dp or not sp.xb.is_contiguous() or \
+                not sp.x32.is_contiguous():
+            raise ValueError("exact splits must hold contiguous [n, dp] rows of one 16-bit type")
     nmax = max(sp.shape[0] for sp in splits)
     scratch = {} if scratch is None else scratch
     key = ("exact-batch", nmax)
@@ -349,23 +406,28 @@ def assign_exact_batch(splits: list, img: CentroidImage, stats: torch.Tensor, ou
                                torch.empty(2 * nmax, dtype=torch.float32, device=dev))
     cand, sc, mg = bufs
     with torch.cuda.stream(stream) if stream is not None else _nullctx():
-        cn, cmax, ce, cemax = img.norms()
+        c16, ch, cn, cmax, ce, cemax = img.image16(dt)
         ni, nd, L = img.neighbors()
     lib = _lib.load()
+    top3 = lib.hbmr_kmeans_assign_top3_f16 if dt == torch.float16 else \
+        lib.hbmr_kmeans_assign_top3_bf16
     st = _lib.stream_handle(stream)
     pc, ps, pm, pst = _ptr(cand), _ptr(sc), _ptr(mg), _ptr(stats)
     pcn, pcmax, pce, pcemax, pni, pnd = (_ptr(t) for t in (cn, cmax, ce, cemax, ni, nd))
+    ws = _refine_ws(nmax, dev, scratch) if REFINE_VERSION >= 3 else None
     base, off = out.data_ptr(), 0
     for sp in splits:
         n = sp.shape[0]
         pl = ctypes.c_void_p(base + 4 * off)
-        rc = lib.hbmr_kmeans_assign_top3_bf16(_ptr(sp.xb), n, img.dp, _ptr(img.cbf),
-                                              _ptr(img.chalf), img.k_pad, pl, pc, ps, pm, st)
-        _lib.check(rc, "hbmr_kmeans_assign_top3_bf16")
-        rc = lib.hbmr_kmeans_refine_f32(
-            _ptr(sp.x32), n, img.d, sp.x32.shape[1], _ptr(sp.xnorm), _ptr(sp.xbn2),
-            _ptr(sp.xerr), _ptr(img.cen), img.k, img.k_pad, pcn, pcmax, pce, pcemax, pni, pnd, L,
-            pl, pc, ps, pm, pst, stats.numel(), st)
+        rc = top3(_ptr(sp.xb), n, img.dp, _ptr(c16), _ptr(ch), img.k_pad, pl, pc, ps, pm, st)
+        _lib.check(rc, "hbmr_kmeans_assign_top3")
+        args = (_ptr(sp.x32), n, img.d, sp.x32.shape[1], _ptr(sp.xnorm), _ptr(sp.xbn2),
+                _ptr(sp.xerr), _ptr(img.cen), img.k, img.k_pad, pcn, pcmax, pce, pcemax, pni,
+                pnd, L, pl, pc, ps, pm, pst, stats.numel())
+        if ws is not None:
+            rc = lib.hbmr_kmeans_refine_f32_q(*args, _ptr(ws), ws.numel(), st)
+        else:
+            rc = lib.hbmr_kmeans_refine_f32(*args, st)
         _lib.check(rc, "hbmr_kmeans_refine_f32")
         off += n
 

@@ -32,6 +32,15 @@ int hbmr_kmeans_accum_f32(const float* X, long n, int dp, const int32_t* labels,
 int hbmr_kmeans_assign_top3_bf16(const void* X, long n, int dp, const void* C, const float* chalf,
                                  int k_pad, int32_t* labels, int32_t* cand, float* scores,
                                  float* margin, hipStream_t st);
+int hbmr_kmeans_assign_top3_f16(const void* X, long n, int dp, const void* C, const float* chalf,
+                                int k_pad, int32_t* labels, int32_t* cand, float* scores,
+                                float* margin, hipStream_t st);
+// exact-mode staging: 16-bit MFMA copy (f16 = 1: fp16, else bf16) + |x|, |x~|^2, |x - x~|
+int hbmr_kmeans_exact_prep(const float* x, long n, int d, int ldx, int dp, int f16, void* x16,
+                           float* xnorm, float* xn2, float* xerr, hipStream_t st);
+// 16-bit centroid image + chalf, |c|, |c - c~|, maxima[2]
+int hbmr_kmeans_image16(const float* cen, int k, int d, int dp, int k_pad, int f16, void* c16,
+                        float* chalf, float* cnorm, float* cerr, float* maxima, hipStream_t st);
 int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float* xnorm,
                            const float* xbn2, const float* xerr, const float* C32, int k,
                            int k_pad, const float* cnorm, const float* cmax, const float* cerr,
@@ -39,6 +48,14 @@ int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float
                            const float* nbr_dist, int L, int32_t* labels, const int32_t* cand,
                            const float* scores, const float* margin, unsigned long long* stats,
                            int nstats, hipStream_t st);
+long hbmr_kmeans_refine_workspace_bytes(long n);
+int hbmr_kmeans_refine_f32_q(const float* X32, long n, int d, int ldx, const float* xnorm,
+                             const float* xbn2, const float* xerr, const float* C32, int k,
+                             int k_pad, const float* cnorm, const float* cmax, const float* cerr,
+                             const float* cerrmax, const int32_t* nbr_idx, const float* nbr_dist,
+                             int L, int32_t* labels, const int32_t* cand, const float* scores,
+                             const float* margin, unsigned long long* stats, int nstats,
+                             void* ws, long ws_bytes, hipStream_t st);
 int hbmr_kmeans_update(const long long* sums, const long long* counts, int fx_shift, int k, int d,
                        int dp, int k_pad, float* cen, void* cbf, float* chalf, float* shift2,
                        hipStream_t st);

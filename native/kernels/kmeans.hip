@@ -35,6 +35,19 @@ constexpr int kWaves = 4;
 constexpr int kThreads = kWaves * HBMR_WAVE;
 constexpr int kCK = 64;  // clusters per LDS chunk (two 32-row MFMA blocks)
 
+// One 32x32x16 MFMA on 16-bit operands held as bf16x8 bit patterns: bf16, or
+// fp16 (F16) — exact mode's default, whose 11 significant bits round the
+// points and centroids 8x closer than bf16's 8 at the same matrix-core rate,
+// so 8x fewer points fail the certification (kmeans_refine_*).
+template <bool F16>
+__device__ __forceinline__ f32x16 mfma32x32x16(bf16x8 a, bf16x8 b, f32x16 c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
 template <int D> struct AssignCfg {
   static constexpr int KS = D / 16;             // MFMA k-steps (K=16 each)
   static constexpr int CPR = D / 8;             // 16-byte pieces per row
@@ -254,7 +267,7 @@ __device__ __forceinline__ void finish_point(const AM& am, int h, long p, long n
 }
 
 // One workgroup's tile of points [blk*PTS, (blk+1)*PTS) of one split.
-template <int D, bool EXACT = false>
+template <int D, bool EXACT = false, bool F16 = false>
 __device__ __forceinline__ void assign_tile(const __bf16* __restrict__ X, long n,
                                             const __bf16* __restrict__ C,
                                             const float* __restrict__ chalf, int nchunks,
@@ -335,7 +348,7 @@ __device__ __forceinline__ void assign_tile(const __bf16* __restrict__ X, long n
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(abase + ((q ^ aswz) << 4));
 #pragma unroll
         for (int pb = 0; pb < PB; ++pb)
-          acc[pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfrag[pb][s], acc[pb], 0, 0, 0);
+          acc[pb] = mfma32x32x16<F16>(a, bfrag[pb][s], acc[pb]);
       }
 #pragma unroll
       for (int pb = 0; pb < PB; ++pb) am[pb].update(acc[pb], c * (kCK / 32) + cb);
@@ -440,7 +453,7 @@ __device__ __forceinline__ void read_tile32(const char* buf, int col, int h, bf1
   }
 }
 
-template <int D, int PB, bool EXACT = false>
+template <int D, int PB, bool EXACT = false, bool F16 = false>
 __device__ __forceinline__ void assign_tile_v2(const __bf16* __restrict__ X, long n,
                                                const __bf16* __restrict__ C,
                                                const float* __restrict__ chalf, int ntiles,
@@ -510,8 +523,7 @@ __device__ __forceinline__ void assign_tile_v2(const __bf16* __restrict__ X, lon
     for (int s = 0; s < KS; ++s) {
 #pragma unroll
       for (int pb = 0; pb < PB; ++pb)
-        acc[pb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[s], bfrag[pb][s],
-                                                          s == 0 ? bias : acc[pb], 0, 0, 0);
+        acc[pb] = mfma32x32x16<F16>(a[s], bfrag[pb][s], s == 0 ? bias : acc[pb]);
       a[s] = *reinterpret_cast<const bf16x8*>(nrow + (((2 * s + h) ^ aswz) << 4));
     }
     {
@@ -554,25 +566,26 @@ __global__ __launch_bounds__(AssignV2<D>::THREADS, AssignV2<D>::MINB) void kmean
                     hbmr_xcd_remap(blockIdx.x, gridDim.x), smem);
 }
 
-// Exact mode: the same kernels with the top-3 epilogue.
-template <int D>
+// Exact mode: the same kernels with the top-3 epilogue (bf16 or fp16 operands;
+// the 16-bit rows travel as bf16 bit patterns either way).
+template <int D, bool F16>
 __global__ __launch_bounds__(kThreads, 2) void kmeans_assign_top3_kernel(
     const __bf16* __restrict__ X, long n, const __bf16* __restrict__ C,
     const float* __restrict__ chalf, int nchunks, int32_t* __restrict__ labels,
     int32_t* __restrict__ cand, float* __restrict__ scores, float* __restrict__ margin) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  assign_tile<D, true>(X, n, C, chalf, nchunks, labels, scores, nullptr,
-                       hbmr_xcd_remap(blockIdx.x, gridDim.x), smem, cand, margin);
+  assign_tile<D, true, F16>(X, n, C, chalf, nchunks, labels, scores, nullptr,
+                            hbmr_xcd_remap(blockIdx.x, gridDim.x), smem, cand, margin);
 }
 
-template <int D, int PB>
+template <int D, int PB, bool F16>
 __global__ __launch_bounds__(AssignV2<D>::THREADS, AssignV2<D>::MINB) void kmeans_assign_top3_v2_kernel(
     const __bf16* __restrict__ X, long n, const __bf16* __restrict__ C,
     const float* __restrict__ chalf, int ntiles, int32_t* __restrict__ labels,
     int32_t* __restrict__ cand, float* __restrict__ scores, float* __restrict__ margin) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  assign_tile_v2<D, PB, true>(X, n, C, chalf, ntiles, labels, scores,
-                              hbmr_xcd_remap(blockIdx.x, gridDim.x), smem, cand, margin);
+  assign_tile_v2<D, PB, true, F16>(X, n, C, chalf, ntiles, labels, scores,
+                                   hbmr_xcd_remap(blockIdx.x, gridDim.x), smem, cand, margin);
 }
 
 // 1 = the chunked kernel above, 2 = the pipelined v2 (D ≤ 128); HBMR_KMEANS_ASSIGN
@@ -1564,10 +1577,12 @@ constexpr int kRefinePer = kRefineMaxDp / kRefineGroup;  // features per lane
 // Error bound E of a kernel score sc (point norm xn, |x~|^2 = x2) against a
 // centroid of norm cn whose distance vector carries rounding error <= a, and a
 // lower bound of sqrt(D~) for the monotonicity test.
-__device__ __forceinline__ void exact_bound(double sc, double cn, double xn, double x2, double a,
-                                            double u, double gam, double pack_rel, double& e,
+__device__ __forceinline__ void exact_bound(double sc, double ct, double xt, double x2, double a,
+                                            double gam, double pack_rel, double& e,
                                             double& dlo) {
-  const double eacc = gam * (1.0 + u) * (1.0 + u) * (xn * cn + 0.5 * cn * cn);
+  // ct, xt: upper bounds of |c~| and |x~| (|c| + |c - c~|, |x| + |x - x~|: no
+  // relative-rounding assumption, so fp16 subnormals and saturation are covered)
+  const double eacc = gam * (xt * ct + 0.5 * ct * ct);
   const double epack = fabs(sc) * pack_rel;
   const double slack = 2.0 * (eacc + epack) + x2 * 0x1p-22;
   const double dhi = fmax(0.0, x2 - 2.0 * sc) + slack;
@@ -1676,11 +1691,10 @@ __global__ __launch_bounds__(256) void kmeans_refine_kernel(
   __shared__ unsigned long long cnt[5];
   if (threadIdx.x < 5) cnt[threadIdx.x] = 0;
   __syncthreads();
-  const double u = 0x1.004p-8;  // bf16 keeps 8 significant bits: unit roundoff 2^-8
   const double inflate = 1.0 + 0x1p-20;
   const double gam = (double)(d + 2) * 0x1p-23 * 1.01;
-  const double cm = (double)cmax[0] * inflate;
   const double cem = (double)cerrmax[0] * inflate;
+  const double cm = (double)cmax[0] * inflate + cem;  // bound of |c~_j| for every j
   bool flag = false;
   int b = 0, s2 = 0, s3 = 0;
   double xn = 0.0, x2 = 0.0, sb = 0.0, m3 = 0.0, amax = 0.0;
@@ -1689,7 +1703,7 @@ __global__ __launch_bounds__(256) void kmeans_refine_kernel(
     s2 = cand[p];
     s3 = cand[n + p];
     if (s2 < k) {  // a padded runner-up (-1e30) is never close: k == 1
-      xn = (double)xnorm[p] * inflate;
+      xn = ((double)xnorm[p] + (double)xerr[p]) * inflate;  // bound of |x~|
       x2 = (double)xbn2[p];
       sb = score[p];
       const double m2 = margin[p];
@@ -1697,9 +1711,9 @@ __global__ __launch_bounds__(256) void kmeans_refine_kernel(
       const double xe = (double)xerr[p];
       amax = (xe + cem) * inflate;
       double eb, es, dl_b, dl_s;
-      exact_bound(sb, (double)cnorm[b] * inflate, xn, x2, (xe + (double)cerr[b]) * inflate, u,
+      exact_bound(sb, ((double)cnorm[b] + (double)cerr[b]) * inflate, xn, x2, (xe + (double)cerr[b]) * inflate,
                   gam, pack_rel, eb, dl_b);
-      exact_bound(sb - m2, cm, xn, x2, amax, u, gam, pack_rel, es, dl_s);
+      exact_bound(sb - m2, cm, xn, x2, amax, gam, pack_rel, es, dl_s);
       flag = !(m2 > eb + es && dl_s >= 2.0 * amax);
     }
   }
@@ -1738,7 +1752,7 @@ __global__ __launch_bounds__(256) void kmeans_refine_kernel(
     bool certified = !t_real;
     if (t_real) {
       double et, dl_t;
-      exact_bound(qsb - qm3, cm, qxn, qx2, qamax, u, gam, pack_rel, et, dl_t);
+      exact_bound(qsb - qm3, cm, qxn, qx2, qamax, gam, pack_rel, et, dl_t);
       // scores are on the bf16 point's baseline: s_t = (|x~|^2 - D_t)/2 with
       // exact D; |x~|^2 (qx2) was stored in fp32, hence the 2^-23 margin.
       // (|x|^2 of the fp32 row would differ by ~|x| e_x, a shift the bound
@@ -1894,11 +1908,10 @@ __global__ __launch_bounds__(256) void kmeans_refine_v2_kernel(
   __shared__ unsigned long long cnt[5];
   if (threadIdx.x < 5) cnt[threadIdx.x] = 0;
   __syncthreads();
-  const double u = 0x1.004p-8;
   const double inflate = 1.0 + 0x1p-20;
   const double gam = (double)(d + 2) * 0x1p-23 * 1.01;
-  const double cm = (double)cmax[0] * inflate;
   const double cem = (double)cerrmax[0] * inflate;
+  const double cm = (double)cmax[0] * inflate + cem;  // bound of |c~_j| for every j
   bool flag = false;
   int b = 0, s2 = 0, s3 = 0;
   double xn = 0.0, x2 = 0.0, sb = 0.0, m3 = 0.0, amax = 0.0;
@@ -1907,7 +1920,7 @@ __global__ __launch_bounds__(256) void kmeans_refine_v2_kernel(
     s2 = cand[p];
     s3 = cand[n + p];
     if (s2 < k) {
-      xn = (double)xnorm[p] * inflate;
+      xn = ((double)xnorm[p] + (double)xerr[p]) * inflate;  // bound of |x~|
       x2 = (double)xbn2[p];
       sb = score[p];
       const double m2 = margin[p];
@@ -1915,9 +1928,9 @@ __global__ __launch_bounds__(256) void kmeans_refine_v2_kernel(
       const double xe = (double)xerr[p];
       amax = (xe + cem) * inflate;
       double eb, es, dl_b, dl_s;
-      exact_bound(sb, (double)cnorm[b] * inflate, xn, x2, (xe + (double)cerr[b]) * inflate, u,
+      exact_bound(sb, ((double)cnorm[b] + (double)cerr[b]) * inflate, xn, x2, (xe + (double)cerr[b]) * inflate,
                   gam, pack_rel, eb, dl_b);
-      exact_bound(sb - m2, cm, xn, x2, amax, u, gam, pack_rel, es, dl_s);
+      exact_bound(sb - m2, cm, xn, x2, amax, gam, pack_rel, es, dl_s);
       flag = !(m2 > eb + es && dl_s >= 2.0 * amax);
     }
   }
@@ -1956,7 +1969,7 @@ __global__ __launch_bounds__(256) void kmeans_refine_v2_kernel(
     bool certified = !t_real;
     if (t_real) {
       double et, dl_t;
-      exact_bound(qsb - qm3, cm, qxn, qx2, qamax, u, gam, pack_rel, et, dl_t);
+      exact_bound(qsb - qm3, cm, qxn, qx2, qamax, gam, pack_rel, et, dl_t);
       certified = 0.5 * (qx2 - dw) - qx2 * 0x1p-23 > (qsb - qm3) + et &&
                   dl_t >= 2.0 * qamax;
     }
@@ -2017,6 +2030,391 @@ __global__ __launch_bounds__(256) void kmeans_refine_v2_kernel(
     atomicAdd(stats + threadIdx.x, cnt[threadIdx.x]);
 }
 
+// ---------------------------------------------------------------------------
+// Exact mode staging.  A split's fp32 rows become the 16-bit MFMA copy (fp16 by
+// default, saturated at ±65504; or bf16) plus, per point, |x| (fp64 → fp32),
+// |x~|^2 (fp64 → fp32) and the rounding error |x - x~| (fp64, rounded UP):
+// the certification's inputs.  16 lanes per row, 8 features per lane.
+__device__ __forceinline__ uint16_t hbmr_f32_to_f16_sat(float v) {
+  const _Float16 h = (_Float16)fminf(fmaxf(v, -65504.f), 65504.f);
+  return __builtin_bit_cast(uint16_t, h);
+}
+__device__ __forceinline__ float hbmr_f16_to_f32(uint16_t b) {
+  return (float)__builtin_bit_cast(_Float16, b);
+}
+
+__global__ __launch_bounds__(256) void kmeans_exact_prep_kernel(
+    const float* __restrict__ x, long n, int d, int ldx, int dp, int f16,
+    uint16_t* __restrict__ x16, float* __restrict__ xnorm, float* __restrict__ xn2,
+    float* __restrict__ xerr) {
+  const long row = (long)blockIdx.x * 16 + threadIdx.x / kRefineGroup;
+  const int sub = threadIdx.x % kRefineGroup;
+  const bool ok = row < n;
+  const long r = ok ? row : n - 1;
+  double a = 0.0, q = 0.0, e = 0.0;
+  for (int i0 = 8 * sub; i0 < dp; i0 += 8 * kRefineGroup) {
+    uint16_t hb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = i0 + j;
+      const float v = i < d ? x[r * ldx + i] : 0.f;
+      const uint16_t b = f16 ? hbmr_f32_to_f16_sat(v) : hbmr_f32_to_bf16(v);
+      const float vt = f16 ? hbmr_f16_to_f32(b) : hbmr_bf16_to_f32(b);
+      hb[j] = b;
+      a = fma((double)v, (double)v, a);
+      q = fma((double)vt, (double)vt, q);
+      const double df = (double)v - (double)vt;
+      e = fma(df, df, e);
+    }
+    if (ok) {
+      uint4 w;
+      w.x = hb[0] | ((uint32_t)hb[1] << 16);
+      w.y = hb[2] | ((uint32_t)hb[3] << 16);
+      w.z = hb[4] | ((uint32_t)hb[5] << 16);
+      w.w = hb[6] | ((uint32_t)hb[7] << 16);
+      *reinterpret_cast<uint4*>(x16 + r * dp + i0) = w;
+    }
+  }
+  a = row_sum16(a);
+  q = row_sum16(q);
+  e = row_sum16(e);
+  if (ok && sub == 0) {
+    xnorm[r] = (float)sqrt(a);
+    xn2[r] = (float)q;
+    xerr[r] = __double2float_ru(sqrt(e) * (1.0 + 0x1p-50));
+  }
+}
+
+// The 16-bit image of the fp32 centroids for exact mode (fp16 by default):
+// c16 [k_pad, dp], chalf = -|c~|^2/2 (fp32, summed as kmeans_update sums the
+// bf16 image's), |c| and |c - c~| (fp64, rounded up) and their maxima (as
+// float bits: non-negative floats order as unsigned).  One workgroup per row.
+__global__ __launch_bounds__(128) void kmeans_image16_kernel(
+    const float* __restrict__ cen, int k, int d, int dp, int f16, uint16_t* __restrict__ c16,
+    float* __restrict__ chalf, float* __restrict__ cnorm, float* __restrict__ cerr,
+    unsigned* __restrict__ maxbits) {
+  const int j = blockIdx.x;
+  const int tid = threadIdx.x;
+  __shared__ float red[128];
+  __shared__ double red64[2][128];
+  float nrm = 0.f;
+  double a = 0.0, e = 0.0;
+  for (int i = tid; i < dp; i += 128) {
+    const float v = (j < k && i < d) ? cen[(size_t)j * d + i] : 0.f;
+    const uint16_t b = f16 ? hbmr_f32_to_f16_sat(v) : hbmr_f32_to_bf16(v);
+    const float vt = f16 ? hbmr_f16_to_f32(b) : hbmr_bf16_to_f32(b);
+    c16[(size_t)j * dp + i] = b;
+    nrm += vt * vt;
+    a = fma((double)v, (double)v, a);
+    const double df = (double)v - (double)vt;
+    e = fma(df, df, e);
+  }
+  red[tid] = nrm;
+  red64[0][tid] = a;
+  red64[1][tid] = e;
+  __syncthreads();
+  for (int s = 64; s > 0; s >>= 1) {
+    if (tid < s) {
+      red[tid] += red[tid + s];
+      red64[0][tid] += red64[0][tid + s];
+      red64[1][tid] += red64[1][tid + s];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    chalf[j] = j < k ? -0.5f * red[0] : -1.0e30f;
+    if (j < k) {
+      const float cn = __double2float_ru(sqrt(red64[0][0]) * (1.0 + 0x1p-50));
+      const float ce = __double2float_ru(sqrt(red64[1][0]) * (1.0 + 0x1p-50));
+      cnorm[j] = cn;
+      cerr[j] = ce;
+      atomicMax(maxbits + 0, __float_as_uint(cn));
+      atomicMax(maxbits + 1, __float_as_uint(ce));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Refine v3: the certification as a compacted queue pipeline.  v2 certifies
+// each point in the thread that scanned it and then walks the wave's ~10-20 %
+// flagged points four at a time, each round a dependent row-load chain, so a
+// wave waits out several L2/HBM round trips serially (87 µs per 781k-point
+// split).  v3 splits it by what each step needs:
+//   q1: step 1 (margins vs bounds) streams every point; the flagged ones are
+//       compacted into queue Q1 (wave ballots, one global atomic per block of
+//       1024 points);
+//   q2: step 2 over Q1 on a persistent grid, 16 lanes per entry and 2 × 4
+//       entries per wave in flight, every row load issued before the first FMA;
+//       winners the top three cannot certify go to queue Q2;
+//   q3: the Elkan neighbour scan over Q2 (≈1 % of points with fp16 operands).
+// Same bounds, same fp64 sums and ties as v1/v2: identical labels.
+struct ExactQ1 {
+  uint32_t row;
+  int32_t b, s, t;
+  float sb, m3, x2, xn, xe, pad0, pad1, pad2;
+};
+struct ExactQ2 {
+  uint32_t row;
+  int32_t w;
+  double dw;
+};
+static_assert(sizeof(ExactQ1) == 48 && sizeof(ExactQ2) == 16, "queue entry layout");
+
+constexpr int kQ1Per = 4;            // points per thread in the step-1 scan
+constexpr int kQ2Rounds = 2;         // 4-entry rounds per wave kept in flight
+constexpr int kRefineGrid = 2048;    // persistent grid of q2 / q3 (8 blocks per CU)
+
+// workspace: counters [4] (u32: |Q1|, |Q2|) | Q1 [n] | Q2 [n]
+__host__ __device__ inline size_t refine_q_off1() { return 256; }
+__host__ __device__ inline size_t refine_q_off2(long n) {
+  return 256 + (((size_t)n * sizeof(ExactQ1) + 255) & ~(size_t)255);
+}
+
+__global__ __launch_bounds__(256) void kmeans_refine_q1_kernel(
+    long n, int d, int k, const float* __restrict__ xnorm, const float* __restrict__ xbn2,
+    const float* __restrict__ xerr, const float* __restrict__ cnorm,
+    const float* __restrict__ cmax, const float* __restrict__ cerr,
+    const float* __restrict__ cerrmax, double pack_rel, const int32_t* __restrict__ labels,
+    const int32_t* __restrict__ cand, const float* __restrict__ score,
+    const float* __restrict__ margin, uint32_t* __restrict__ qcount, ExactQ1* __restrict__ q1,
+    unsigned long long* __restrict__ stats) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ uint32_t wcnt[4][kQ1Per];
+  __shared__ uint32_t base_s;
+  const double inflate = 1.0 + 0x1p-20;
+  const double gam = (double)(d + 2) * 0x1p-23 * 1.01;
+  const double cem = (double)cerrmax[0] * inflate;
+  const double cm = (double)cmax[0] * inflate + cem;
+  ExactQ1 e[kQ1Per];
+  bool flag[kQ1Per];
+  uint32_t rank[kQ1Per];
+#pragma unroll
+  for (int i = 0; i < kQ1Per; ++i) {
+    const long p = (long)blockIdx.x * (256 * kQ1Per) + i * 256 + tid;
+    flag[i] = false;
+    if (p < n) {
+      const int b = labels[p], s2 = cand[p];
+      if (s2 < k) {
+        const float xnf = xnorm[p], xef = xerr[p], x2f = xbn2[p];
+        const double xn = ((double)xnf + (double)xef) * inflate;
+        const double x2 = (double)x2f;
+        const double sb = score[p];
+        const double m2 = margin[p];
+        const double amax = ((double)xef + cem) * inflate;
+        double eb, es, dl_b, dl_s;
+        exact_bound(sb, ((double)cnorm[b] + (double)cerr[b]) * inflate, xn, x2,
+                    ((double)xef + (double)cerr[b]) * inflate, gam, pack_rel, eb, dl_b);
+        exact_bound(sb - m2, cm, xn, x2, amax, gam, pack_rel, es, dl_s);
+        flag[i] = !(m2 > eb + es && dl_s >= 2.0 * amax);
+        e[i].row = (uint32_t)p;
+        e[i].b = b;
+        e[i].s = s2;
+        e[i].t = cand[n + p];
+        e[i].sb = score[p];
+        e[i].m3 = margin[n + p];
+        e[i].x2 = x2f;
+        e[i].xn = xnf;
+        e[i].xe = xef;
+      }
+    }
+    const unsigned long long m = __ballot(flag[i]);
+    rank[i] = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (lane == 0) wcnt[wave][i] = (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+      for (int i = 0; i < kQ1Per; ++i) {
+        const uint32_t c = wcnt[w][i];
+        wcnt[w][i] = tot;
+        tot += c;
+      }
+    base_s = tot ? atomicAdd(qcount, tot) : 0u;
+    if (tot) atomicAdd(stats, (unsigned long long)tot);
+  }
+  __syncthreads();
+  const uint32_t base = base_s;
+#pragma unroll
+  for (int i = 0; i < kQ1Per; ++i)
+    if (flag[i]) q1[base + wcnt[wave][i] + rank[i]] = e[i];
+}
+
+template <int NM>
+__global__ __launch_bounds__(256) void kmeans_refine_q2_kernel(
+    const float* __restrict__ X32, int d, int ldx, const float* __restrict__ C32, int k,
+    const float* __restrict__ cmax, const float* __restrict__ cerrmax, double pack_rel,
+    int32_t* __restrict__ labels, const uint32_t* __restrict__ qcount,
+    const ExactQ1* __restrict__ q1, uint32_t* __restrict__ q2count, ExactQ2* __restrict__ q2,
+    unsigned long long* __restrict__ stats) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int grp = lane / kRefineGroup, sub = lane % kRefineGroup;
+  __shared__ unsigned long long cnt[2];
+  if (tid < 2) cnt[tid] = 0;
+  __syncthreads();
+  const double inflate = 1.0 + 0x1p-20;
+  const double gam = (double)(d + 2) * 0x1p-23 * 1.01;
+  const double cem = (double)cerrmax[0] * inflate;
+  const double cm = (double)cmax[0] * inflate + cem;
+  const uint32_t total = *qcount;
+  const uint32_t nwaves = gridDim.x * 4;
+  const uint32_t gw = blockIdx.x * 4 + (tid >> 6);
+  constexpr int PER = 4 * kQ2Rounds;
+  for (uint32_t base = gw * PER; base < total; base += nwaves * PER) {
+    ExactQ1 e[kQ2Rounds];
+    bool have[kQ2Rounds];
+    float xf[kQ2Rounds][8 * NM];
+    float cv[kQ2Rounds][3][8 * NM];
+#pragma unroll
+    for (int r = 0; r < kQ2Rounds; ++r) {
+      const uint32_t idx = base + r * 4 + grp;
+      have[r] = idx < total;
+      e[r] = q1[have[r] ? idx : base];
+      const bool t_real = e[r].t < k;
+      load_row8<NM>(X32 + (size_t)e[r].row * ldx, d, sub, xf[r]);
+      load_row8<NM>(C32 + (size_t)e[r].b * d, d, sub, cv[r][0]);
+      load_row8<NM>(C32 + (size_t)e[r].s * d, d, sub, cv[r][1]);
+      load_row8<NM>(C32 + (size_t)(t_real ? e[r].t : e[r].b) * d, d, sub, cv[r][2]);
+    }
+#pragma unroll
+    for (int r = 0; r < kQ2Rounds; ++r) {
+      double acc[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+      for (int i = 0; i < 8 * NM; ++i) {
+        const double x = (double)xf[r][i];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const double df = x - (double)cv[r][c][i];
+          acc[c] = fma(df, df, acc[c]);
+        }
+      }
+      double d3[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) d3[c] = row_sum16(acc[c]);
+      if (!have[r]) continue;
+      const ExactQ1& q = e[r];
+      const bool t_real = q.t < k;
+      int w = q.b;
+      double dw = d3[0];
+      if (d3[1] < dw || (d3[1] == dw && q.s < w)) { w = q.s; dw = d3[1]; }
+      if (t_real && (d3[2] < dw || (d3[2] == dw && q.t < w))) { w = q.t; dw = d3[2]; }
+      bool certified = !t_real;
+      if (t_real) {
+        const double xn = ((double)q.xn + (double)q.xe) * inflate;
+        const double x2 = (double)q.x2;
+        const double amax = ((double)q.xe + cem) * inflate;
+        const double st = (double)q.sb - (double)q.m3;
+        double et, dl_t;
+        exact_bound(st, cm, xn, x2, amax, gam, pack_rel, et, dl_t);
+        certified = 0.5 * (x2 - dw) - x2 * 0x1p-23 > st + et && dl_t >= 2.0 * amax;
+      }
+      if (sub == 0) {
+        if (certified) {
+          if (w != q.b) {
+            labels[q.row] = w;
+            atomicAdd(&cnt[0], 1ull);
+          }
+        } else {
+          const uint32_t slot = atomicAdd(q2count, 1u);
+          ExactQ2 o;
+          o.row = q.row;
+          o.w = w;
+          o.dw = dw;
+          q2[slot] = o;
+          atomicAdd(&cnt[1], 1ull);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0 && cnt[0]) atomicAdd(stats + 1, cnt[0]);
+  if (tid == 1 && cnt[1]) atomicAdd(stats + 2, cnt[1]);
+}
+
+template <int NM>
+__global__ __launch_bounds__(256) void kmeans_refine_q3_kernel(
+    const float* __restrict__ X32, int d, int ldx, const float* __restrict__ C32, int k,
+    const int32_t* __restrict__ nbr_idx, const float* __restrict__ nbr_dist, int L,
+    int32_t* __restrict__ labels, const uint32_t* __restrict__ q2count,
+    const ExactQ2* __restrict__ q2, unsigned long long* __restrict__ stats, int nstats) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int grp = lane / kRefineGroup, sub = lane % kRefineGroup;
+  __shared__ unsigned long long cnt[3];
+  if (tid < 3) cnt[tid] = 0;
+  __syncthreads();
+  const uint32_t total = *q2count;
+  const uint32_t nwaves = gridDim.x * 4;
+  const uint32_t gw = blockIdx.x * 4 + (tid >> 6);
+  for (uint32_t base = gw * 4; base < total; base += nwaves * 4) {
+    const uint32_t idx = base + grp;
+    const bool have = idx < total;
+    const ExactQ2 q = q2[have ? idx : base];
+    const int b0 = labels[q.row];   // the MFMA pick: step 2 left it in place
+    double xv[8 * NM];
+    {
+      float xf[8 * NM];
+      load_row8<NM>(X32 + (size_t)q.row * ldx, d, sub, xf);
+#pragma unroll
+      for (int i = 0; i < 8 * NM; ++i) xv[i] = (double)xf[i];
+    }
+    const int w0 = q.w;
+    int w = w0;
+    double dw = q.dw;
+    const double r0 = sqrt(dw);
+    bool done = false;
+    const int32_t* ni = nbr_idx + (size_t)w0 * L;
+    const float* nd = nbr_dist + (size_t)w0 * L;
+    const float* cw0 = C32 + (size_t)w0 * d;
+    int evals = 0;
+    for (int jj = 0; jj < L; jj += kElkanStep) {
+      const double lim = (r0 + sqrt(dw)) * (1.0 + 0x1p-40);
+      if ((double)nd[jj] > lim) {
+        done = true;
+        break;
+      }
+      int jv[kElkanStep];
+      const float* cp[kElkanStep];
+#pragma unroll
+      for (int v = 0; v < kElkanStep; ++v) {
+        const bool ok = jj + v < L && (double)nd[jj + v] <= lim;
+        jv[v] = ok ? ni[jj + v] : -1;
+        cp[v] = ok ? C32 + (size_t)jv[v] * d : cw0;
+      }
+      double dj[kElkanStep];
+      rows_dist2<NM, kElkanStep>(xv, cp, d, sub, dj);
+      evals += kElkanStep;
+#pragma unroll
+      for (int v = 0; v < kElkanStep; ++v)
+        if (jv[v] >= 0 && (dj[v] < dw || (dj[v] == dw && jv[v] < w))) { w = jv[v]; dw = dj[v]; }
+    }
+    const bool full = !done && L < k;
+    if (full) {
+      for (int j = 0; j < k; j += 4) {
+        const float* cp[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) cp[v] = C32 + (size_t)(j + v < k ? j + v : j) * d;
+        double dj[4];
+        rows_dist2<NM, 4>(xv, cp, d, sub, dj);
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          if (j + v < k && (dj[v] < dw || (dj[v] == dw && j + v < w))) { w = j + v; dw = dj[v]; }
+      }
+    }
+    if (have && sub == 0) {
+      atomicAdd(&cnt[1], (unsigned long long)evals);
+      if (full) atomicAdd(&cnt[2], 1ull);
+      if (w != b0) atomicAdd(&cnt[0], 1ull);
+      labels[q.row] = w;
+    }
+  }
+  __syncthreads();
+  if (tid == 0 && cnt[0]) atomicAdd(stats + 1, cnt[0]);
+  if (nstats >= 5 && tid >= 1 && tid < 3 && cnt[tid]) atomicAdd(stats + 2 + tid, cnt[tid]);
+}
+
 int refine_version() {
   static int v = 0;
   if (!v) {
@@ -2026,7 +2424,7 @@ int refine_version() {
   return v;
 }
 
-template <int D>
+template <int D, bool F16>
 int launch_assign_top3(const void* X, long n, const void* C, const float* chalf, int k_pad,
                        int32_t* labels, int32_t* cand, float* scores, float* margin,
                        hipStream_t st) {
@@ -2037,7 +2435,7 @@ int launch_assign_top3(const void* X, long n, const void* C, const float* chalf,
       const int pts = AssignV2<D>::WAVES * 2 * 32;
       const long nblk = (n + pts - 1) / pts;
       if (nblk > 0x7fffffffL) return (int)hipErrorInvalidValue;
-      hipLaunchKernelGGL((kmeans_assign_top3_v2_kernel<D, 2>), dim3((unsigned)nblk),
+      hipLaunchKernelGGL((kmeans_assign_top3_v2_kernel<D, 2, F16>), dim3((unsigned)nblk),
                          dim3(AssignV2<D>::THREADS), AssignV2<D>::LDS_BYTES, st,
                          reinterpret_cast<const __bf16*>(X), n, reinterpret_cast<const __bf16*>(C),
                          chalf, k_pad / 32, labels, cand, scores, margin);
@@ -2046,7 +2444,7 @@ int launch_assign_top3(const void* X, long n, const void* C, const float* chalf,
   }
   const long nblk = (n + AssignCfg<D>::PTS - 1) / AssignCfg<D>::PTS;
   if (nblk > 0x7fffffffL) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(kmeans_assign_top3_kernel<D>, dim3((unsigned)nblk), dim3(kThreads),
+  hipLaunchKernelGGL((kmeans_assign_top3_kernel<D, F16>), dim3((unsigned)nblk), dim3(kThreads),
                      AssignCfg<D>::LDS_BYTES, st, reinterpret_cast<const __bf16*>(X), n,
                      reinterpret_cast<const __bf16*>(C), chalf, k_pad / kCK, labels, cand, scores,
                      margin);
@@ -2498,9 +2896,23 @@ int hbmr_kmeans_assign_top3_bf16(const void* X, long n, int dp, const void* C, c
                                  float* margin, hipStream_t st) {
   if (!labels || !cand || !scores || !margin) return (int)hipErrorInvalidValue;
   switch (dp) {
-    case 64: return launch_assign_top3<64>(X, n, C, chalf, k_pad, labels, cand, scores, margin, st);
-    case 128: return launch_assign_top3<128>(X, n, C, chalf, k_pad, labels, cand, scores, margin, st);
-    case 256: return launch_assign_top3<256>(X, n, C, chalf, k_pad, labels, cand, scores, margin, st);
+    case 64: return launch_assign_top3<64, false>(X, n, C, chalf, k_pad, labels, cand, scores, margin, st);
+    case 128: return launch_assign_top3<128, false>(X, n, C, chalf, k_pad, labels, cand, scores, margin, st);
+    case 256: return launch_assign_top3<256, false>(X, n, C, chalf, k_pad, labels, cand, scores, margin, st);
+    default: return (int)hipErrorInvalidValue;
+  }
+}
+
+// exact mode's default: fp16 operands (rows of fp16 bit patterns, C the fp16
+// centroid image of hbmr_kmeans_image_f16, chalf its -|c~|^2/2)
+int hbmr_kmeans_assign_top3_f16(const void* X, long n, int dp, const void* C, const float* chalf,
+                                int k_pad, int32_t* labels, int32_t* cand, float* scores,
+                                float* margin, hipStream_t st) {
+  if (!labels || !cand || !scores || !margin) return (int)hipErrorInvalidValue;
+  switch (dp) {
+    case 64: return launch_assign_top3<64, true>(X, n, C, chalf, k_pad, labels, cand, scores, margin, st);
+    case 128: return launch_assign_top3<128, true>(X, n, C, chalf, k_pad, labels, cand, scores, margin, st);
+    case 256: return launch_assign_top3<256, true>(X, n, C, chalf, k_pad, labels, cand, scores, margin, st);
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -2534,6 +2946,83 @@ int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float
                      ldx, xnorm, xbn2, xerr, C32, k, cnorm, cmax, cerr, cerrmax, pack_rel,
                      nbr_idx, nbr_dist, L,
                      labels, cand, scores, margin, stats, nstats);
+  return (int)hipGetLastError();
+}
+
+
+int hbmr_kmeans_exact_prep(const float* x, long n, int d, int ldx, int dp, int f16, void* x16,
+                           float* xnorm, float* xn2, float* xerr, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (d > ldx || d > dp || dp % 8 || !x16 || !xnorm || !xn2 || !xerr)
+    return (int)hipErrorInvalidValue;
+  const long blocks = (n + 15) / 16;
+  if (blocks > 0x7fffffffL) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kmeans_exact_prep_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, n, d,
+                     ldx, dp, f16, reinterpret_cast<uint16_t*>(x16), xnorm, xn2, xerr);
+  return (int)hipGetLastError();
+}
+
+// maxima: float [2] = (max |c_j|, max |c_j - c~_j|), written by the kernel
+int hbmr_kmeans_image16(const float* cen, int k, int d, int dp, int k_pad, int f16, void* c16,
+                        float* chalf, float* cnorm, float* cerr, float* maxima, hipStream_t st) {
+  if (k <= 0 || k_pad < k || d > dp) return (int)hipErrorInvalidValue;
+  HBMR_RETURN_IF_ERROR(hipMemsetAsync(maxima, 0, 2 * sizeof(float), st));
+  hipLaunchKernelGGL(kmeans_image16_kernel, dim3((unsigned)k_pad), dim3(128), 0, st, cen, k, d,
+                     dp, f16, reinterpret_cast<uint16_t*>(c16), chalf, cnorm, cerr,
+                     reinterpret_cast<unsigned*>(maxima));
+  return (int)hipGetLastError();
+}
+
+
+long hbmr_kmeans_refine_workspace_bytes(long n) {
+  return (long)(refine_q_off2(n) + (size_t)n * sizeof(ExactQ2));
+}
+
+// refine v3 (the queue pipeline of kmeans_refine_q*): same contract as
+// hbmr_kmeans_refine_f32 plus a workspace of hbmr_kmeans_refine_workspace_bytes(n)
+int hbmr_kmeans_refine_f32_q(const float* X32, long n, int d, int ldx, const float* xnorm,
+                             const float* xbn2, const float* xerr, const float* C32, int k,
+                             int k_pad, const float* cnorm, const float* cmax, const float* cerr,
+                             const float* cerrmax, const int32_t* nbr_idx, const float* nbr_dist,
+                             int L, int32_t* labels, const int32_t* cand, const float* scores,
+                             const float* margin, unsigned long long* stats, int nstats,
+                             void* ws, long ws_bytes, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (d > ldx || d > kRefineMaxDp || k <= 0 || k_pad < k || L < 1 || L > k || nstats < 3 ||
+      n > 0xffffffffL || ws_bytes < hbmr_kmeans_refine_workspace_bytes(n))
+    return (int)hipErrorInvalidValue;
+  if (d % 8 || ldx % 4 || ((uintptr_t)X32 & 15) || ((uintptr_t)C32 & 15) || ((uintptr_t)ws & 255))
+    return (int)hipErrorInvalidValue;
+  int tb = 0;
+  while ((1 << tb) < k_pad / 32) ++tb;
+  const double pack_rel = ldexp(1.0, 4 + tb - 23);
+  char* w = static_cast<char*>(ws);
+  uint32_t* counts = reinterpret_cast<uint32_t*>(w);
+  ExactQ1* q1 = reinterpret_cast<ExactQ1*>(w + refine_q_off1());
+  ExactQ2* q2 = reinterpret_cast<ExactQ2*>(w + refine_q_off2(n));
+  HBMR_RETURN_IF_ERROR(hipMemsetAsync(counts, 0, 16, st));
+  const long b1 = (n + 256 * kQ1Per - 1) / (256 * kQ1Per);
+  hipLaunchKernelGGL(kmeans_refine_q1_kernel, dim3((unsigned)b1), dim3(256), 0, st, n, d, k,
+                     xnorm, xbn2, xerr, cnorm, cmax, cerr, cerrmax, pack_rel, labels, cand,
+                     scores, margin, counts, q1, stats);
+  HBMR_RETURN_IF_ERROR(hipGetLastError());
+  // persistent grids, never larger than the worst case needs
+  const long need2 = (n + 4 * 4 * kQ2Rounds - 1) / (4 * 4 * kQ2Rounds);
+  const unsigned g2 = (unsigned)std::min<long>(kRefineGrid, need2);
+  const unsigned g3 = (unsigned)std::min<long>(kRefineGrid / 4, (n + 15) / 16);
+  if (d <= 128) {
+    hipLaunchKernelGGL(kmeans_refine_q2_kernel<1>, dim3(g2), dim3(256), 0, st, X32, d, ldx, C32,
+                       k, cmax, cerrmax, pack_rel, labels, counts, q1, counts + 1, q2, stats);
+    HBMR_RETURN_IF_ERROR(hipGetLastError());
+    hipLaunchKernelGGL(kmeans_refine_q3_kernel<1>, dim3(g3), dim3(256), 0, st, X32, d, ldx, C32,
+                       k, nbr_idx, nbr_dist, L, labels, counts + 1, q2, stats, nstats);
+  } else {
+    hipLaunchKernelGGL(kmeans_refine_q2_kernel<2>, dim3(g2), dim3(256), 0, st, X32, d, ldx, C32,
+                       k, cmax, cerrmax, pack_rel, labels, counts, q1, counts + 1, q2, stats);
+    HBMR_RETURN_IF_ERROR(hipGetLastError());
+    hipLaunchKernelGGL(kmeans_refine_q3_kernel<2>, dim3(g3), dim3(256), 0, st, X32, d, ldx, C32,
+                       k, nbr_idx, nbr_dist, L, labels, counts + 1, q2, stats, nstats);
+  }
   return (int)hipGetLastError();
 }
 

@@ -1,6 +1,6 @@
-"""Exact K-Means mode (hbmr.kmeans.exact): top-2 MFMA assign, certification of
-the bf16 arg-max against the fp32 data with fp64 re-scoring of uncertain
-points, and the fp32-input fixed-point combiner.  GPU numerics are checked
+"""Exact K-Means mode (hbmr.kmeans.exact): top-3 MFMA assign on fp16 (default)
+or bf16 operands, certification of the arg-max against the fp32 data with
+fp64 re-scoring of uncertain points, and the fp32-input fixed-point combiner.  GPU numerics are checked
 against fp64 (the "exact" assignment of the fp32 data) and a plain fp32
 PyTorch reference; the CPU test runs an exact-mode job on CPU slots."""
 import pytest
@@ -64,20 +64,24 @@ def _blobs(n, d, k, seed, dup=2):
 
 
 @pytest.mark.gpu
-def test_top3_assign_matches_fp32_reference():
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_top3_assign_matches_fp32_reference(dtype):
     from hbmr.ops import kmeans as km
+    dt = torch.float16 if dtype == "f16" else torch.bfloat16
     n, d, k = 40000, 128, 256
     x, c = _blobs(n, d, k, 3)
     img = km.CentroidImage(c, "cuda")
-    sp = km.ExactSplit(x, km.padded_dim(d))
+    sp = km.ExactSplit(x, km.padded_dim(d), dt)
+    assert sp.xb.dtype == dt
     lab = torch.empty(n, dtype=torch.int32, device="cuda")
     cand = torch.empty(2 * n, dtype=torch.int32, device="cuda")
     sc, mg = torch.empty(n, device="cuda"), torch.empty(2 * n, device="cuda")
     km.assign_top3(sp.xb, img, lab, cand, sc, mg)
-    # reference: fp32 scores of the bf16 operands (what the MFMA computes)
+    # reference: fp32 scores of the 16-bit operands (what the MFMA computes)
+    c16, ch = img.image16(dt)[:2]
     xb = sp.xb[:, :d].float()
-    cb = img.cbf[:k, :d].float()
-    s = xb @ cb.T + img.chalf[:k][None, :]
+    cb = c16[:k, :d].float()
+    s = xb @ cb.T + ch[:k][None, :]
     top = s.topk(3, dim=1)
     got = torch.stack([lab.long(), cand[:n].long(), cand[n:].long()], 1)
     # scores of the kernel's picks must equal the reference top-3 scores up to
@@ -91,28 +95,85 @@ def test_top3_assign_matches_fp32_reference():
     ref_m = top.values[:, :1] - top.values[:, 1:]
     got_m = torch.stack([mg[:n], mg[n:]], 1)
     assert ((got_m - ref_m).abs() <= tol + 1e-2).all(1).float().mean().item() > 0.999
-    assert torch.equal(lab, km.assign(sp.xb, img))       # same winner as the plain kernel
+    if dt == torch.bfloat16:
+        assert torch.equal(lab, km.assign(sp.xb, img))   # same winner as the plain kernel
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("d", [64, 128])
-def test_exact_assign_agrees_with_fp64(d):
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_exact_prep_and_image16_match_fp64(dtype):
+    """The native staging kernels: the 16-bit copies are round-to-nearest of the
+    fp32 data (fp16 saturated at ±65504), and |x|, |x~|², |x - x~|, |c|,
+    |c - c~| match fp64 (the errors as upper bounds)."""
     from hbmr.ops import kmeans as km
+    dt = torch.float16 if dtype == "f16" else torch.bfloat16
+    n, d, k = 5000, 120, 70
+    x = torch.randn(n, d, device="cuda") * 20
+    x[0, 0] = 1e6          # saturates in fp16
+    x[1, :] = 1e-6         # fp16 subnormals
+    sp = km.ExactSplit(x, km.padded_dim(d), dt)
+    dp = km.padded_dim(d)
+    lim = 65504.0 if dt == torch.float16 else float("inf")
+    want = x.clamp(-lim, lim).to(dt)
+    assert torch.equal(sp.xb[:, :d], want) and int((sp.xb[:, d:] != 0).sum()) == 0
+    x64, w64 = x.double(), want.double()
+    assert torch.allclose(sp.xnorm.double(), x64.norm(dim=1), rtol=1e-6)
+    assert torch.allclose(sp.xbn2.double(), w64.pow(2).sum(1), rtol=1e-6)
+    e = (x64 - w64).norm(dim=1)
+    assert (sp.xerr.double() >= e).all() and torch.allclose(sp.xerr.double(), e, rtol=1e-6)
+    img = km.CentroidImage(x[:k] * 0.5, "cuda")
+    c16, ch, cn, cm, ce, cem = img.image16(dt)
+    cw = (x[:k] * 0.5).clamp(-lim, lim).to(dt)
+    assert torch.equal(c16[:k, :d], cw) and c16.shape == (img.k_pad, dp)
+    c64 = (x[:k] * 0.5).double()
+    assert (cn.double() >= c64.norm(dim=1)).all() and torch.allclose(cn.double(), c64.norm(dim=1))
+    ee = (c64 - cw.double()).norm(dim=1)
+    assert (ce.double() >= ee).all() and torch.allclose(ce.double(), ee, rtol=1e-6)
+    assert cm.item() == cn.max().item() and cem.item() == ce.max().item()
+    assert torch.allclose(ch[:k].double(), -0.5 * cw.double().pow(2).sum(1), rtol=1e-5)
+    assert (ch[k:] < -1e29).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,dtype", [(64, "f16"), (128, "f16"), (128, "bf16")])
+def test_exact_assign_agrees_with_fp64(d, dtype):
+    from hbmr.ops import kmeans as km
+    dt = torch.float16 if dtype == "f16" else torch.bfloat16
     n, k = 1_000_000, 256
     x, c = _blobs(n, d, k, 11)
     img = km.CentroidImage(c, "cuda")
-    sp = km.ExactSplit(x, km.padded_dim(d))
+    sp = km.ExactSplit(x, km.padded_dim(d), dt)
     truth = truth_labels(x, c)
-    bf16 = km.assign(sp.xb, img)
+    first = torch.empty(n, dtype=torch.int32, device="cuda")
+    cand = torch.empty(2 * n, dtype=torch.int32, device="cuda")
+    sc, mg = torch.empty(n, device="cuda"), torch.empty(2 * n, device="cuda")
+    km.assign_top3(sp.xb, img, first, cand, sc, mg)
     stats = torch.zeros(3, dtype=torch.int64, device="cuda")
     lab = km.assign_exact(sp, img, stats)
     agree_exact = (lab == truth).float().mean().item()
-    agree_bf16 = (bf16 == truth).float().mean().item()
+    agree_first = (first == truth).float().mean().item()
     flagged, relabelled, rescans = stats.tolist()
-    print(f"d={d}: bf16 agreement {agree_bf16:.6f}, exact {agree_exact:.7f}, "
+    print(f"d={d} {dtype}: MFMA arg-max agreement {agree_first:.6f}, exact {agree_exact:.7f}, "
           f"flagged {flagged / n:.4f}, relabelled {relabelled}, neighbour scans {rescans}")
     assert int((lab != truth).sum()) <= 1          # fp64 ties aside: the exact assignment
-    assert 0 < flagged < n and relabelled == int((bf16 != lab).sum())
+    assert 0 < flagged < n and relabelled == int((first != lab).sum())
+
+
+@pytest.mark.gpu
+def test_exact_assign_with_saturated_fp16_data():
+    """Data beyond fp16 range: the saturated copy is still certified against
+    the fp32 rows (its rounding error enters the bound), so the labels stay
+    the fp64 truth — more of them re-scored."""
+    from hbmr.ops import kmeans as km
+    n, d, k = 200_000, 64, 128
+    x, c = _blobs(n, d, k, 17)
+    x = x * 3000.0           # |x_i| up to ~1.5e5 > 65504
+    c = c * 3000.0
+    img = km.CentroidImage(c, "cuda")
+    sp = km.ExactSplit(x, km.padded_dim(d))
+    stats = torch.zeros(3, dtype=torch.int64, device="cuda")
+    lab = km.assign_exact(sp, img, stats)
+    assert int((lab != truth_labels(x, c)).sum()) <= 1
 
 
 @pytest.mark.gpu
@@ -234,3 +295,25 @@ def test_prefetched_iterations_match_and_wait_for_their_dependency():
         assert held.waitForCompletion(10)
         assert held.status().state == "KILLED"   # (released and running by then)
     assert torch.equal(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["f16", "bf16"])
+def test_refine_queue_pipeline_equals_single_kernel(dtype, monkeypatch):
+    """Refine v3 (step 1 / step 2 / Elkan as compacted queues) gives the same
+    labels and the same flagged / relabelled / scan counts as the v2 kernel."""
+    from hbmr.ops import kmeans as km
+    dt = torch.float16 if dtype == "f16" else torch.bfloat16
+    n, d, k = 600_000, 128, 512
+    x, c = _blobs(n, d, k, 23)
+    img = km.CentroidImage(c, "cuda")
+    sp = km.ExactSplit(x, km.padded_dim(d), dt)
+    out = {}
+    for v in (2, 3):
+        monkeypatch.setattr(km, "REFINE_VERSION", v)
+        st = torch.zeros(5, dtype=torch.int64, device="cuda")
+        lab = km.assign_exact(sp, img, st, {}).clone()
+        out[v] = (lab, st.tolist())
+    assert torch.equal(out[2][0], out[3][0])
+    assert out[2][1][:3] == out[3][1][:3] and out[3][1][0] > 0
+    assert int((out[3][0] != truth_labels(x, c)).sum()) <= 1

@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--iters", type=int, default=3, help="Lloyd iterations before timing")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--nbr", type=int, default=0, help="neighbour list length (0: default)")
+    ap.add_argument("--dtypes", default="f16,bf16", help="MFMA operand types to time")
     a = ap.parse_args()
     dev = torch.device("cuda")
     if a.nbr:
@@ -59,7 +60,16 @@ def main():
         km.assign(xb, img, labels=lab)
         km.accumulate(xb, lab, k, sums, cnt)
         img.refresh(sums, cnt)
-    splits = [km.ExactSplit(x32[s:s + a.split], dp) for s in range(0, n, a.split)]
+    for name in a.dtypes.split(","):
+        dt = torch.float16 if name == "f16" else torch.bfloat16
+        r = run_dtype(a, n, k, d, dp, x32, img, xb, lab, dt)
+        r["mfma_dtype"] = name
+        print(json.dumps(r), flush=True)
+
+
+def run_dtype(a, n, k, d, dp, x32, img, xb, lab, dt):
+    dev = x32.device
+    splits = [km.ExactSplit(x32[s:s + a.split], dp, dt) for s in range(0, n, a.split)]
     bsplits = [xb[s:s + a.split] for s in range(0, n, a.split)]
     torch.cuda.synchronize()
     stats = torch.zeros(5, dtype=torch.int64, device=dev)
@@ -112,7 +122,8 @@ def main():
              full_scan_frac=round(full / max(1, sc), 4))
     r["accum_f32_ms"] = timeit(acc32, a.reps)
     r["accum_bf16_ms"] = timeit(acc16, a.reps)
-    print(json.dumps(r), flush=True)
+    del splits
+    return r
 
 
 if __name__ == "__main__":
