@@ -45,12 +45,16 @@ _SIGS = {
                                        c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                        c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                        c_void_p]),
-    "hbmr_kmeans_refine_f32_q": (c_int, [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p,
-                                         c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
-                                         c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
-                                         c_void_p, c_void_p, c_void_p, c_void_p, c_int,
-                                         c_void_p, c_long, c_void_p]),
-    "hbmr_kmeans_refine_workspace_bytes": (c_long, [c_long]),
+    "hbmr_kmeans_refine_batch_bytes": (c_long, [c_int, c_void_p]),
+    "hbmr_kmeans_refine_batch_q1": (c_int, [c_int, c_void_p, c_int, c_int, c_int, c_int,
+                                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                            c_void_p, c_void_p, c_void_p, c_long, c_int,
+                                            c_void_p]),
+    "hbmr_kmeans_refine_batch_finish": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int,
+                                                c_int, c_void_p, c_int, c_int, c_void_p,
+                                                c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                                c_int, c_void_p, c_long, c_void_p]),
     "hbmr_kmeans_accum_workspace_bytes": (c_long, [c_long, c_int]),
     "hbmr_kmeans_batch_workspace_bytes": (c_long, [c_long, c_int, c_int]),
     "hbmr_kmeans_map_batch": (c_int, [c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,

@@ -309,47 +309,93 @@ def assign_top3(points: torch.Tensor, img: CentroidImage, labels, cand, scores, 
 
 
 REFINE_VERSION = int(os.environ.get("HBMR_REFINE", "3"))
+MAX_REFINE_BATCH = 64     # splits per refine v3 batch (the kernels' split table)
 
 
-def _refine_ws(n: int, device, scratch: dict | None):
-    """Queue workspace of refine v3 (hbmr_kmeans_refine_f32_q), kept in
-    ``scratch`` across calls (one stream orders the reuse)."""
-    need = int(_lib.load().hbmr_kmeans_refine_workspace_bytes(n))
+def _refine_ws(ns: list, device, scratch: dict | None):
+    """Queue workspace of a refine v3 batch, kept in ``scratch`` across calls
+    (one stream orders the reuse)."""
+    arr = (ctypes.c_long * len(ns))(*ns)
+    need = int(_lib.load().hbmr_kmeans_refine_batch_bytes(len(ns), arr))
+    if need < 0:
+        raise ValueError("refine batch of 1..64 splits expected")
     ws = None if scratch is None else scratch.get("refine_ws")
     if ws is None or ws.numel() < need:
         ws = torch.empty(need, dtype=torch.uint8, device=device)
         if scratch is not None:
             scratch["refine_ws"] = ws
-    return ws
+    return arr, ws
+
+
+class _RefineBatch:
+    """Refine v3 over a batch of splits: ``q1`` right after each split's top-3
+    assign (its candidate scratch may be reused by the next split), ``finish``
+    once (step 2 + Elkan scan over the batch's queues)."""
+
+    def __init__(self, splits: list, img: "CentroidImage", stats, scratch, stream):
+        self.splits, self.img, self.stats, self.stream = splits, img, stats, stream
+        self.dt = splits[0].xb.dtype
+        self.ns, self.ws = _refine_ws([sp.shape[0] for sp in splits], splits[0].x32.device,
+                                      scratch)
+        with torch.cuda.stream(stream) if stream is not None else _nullctx():
+            self.norms = img.norms(self.dt)
+            self.nbr = img.neighbors()
+        self.labels = [None] * len(splits)
+        self.lib = _lib.load()
+        self.st = _lib.stream_handle(stream)
+
+    def q1(self, i, labels_ptr, cand, scores, margin):
+        sp, img = self.splits[i], self.img
+        cn, cmax, ce, cemax = self.norms
+        self.labels[i] = labels_ptr
+        rc = self.lib.hbmr_kmeans_refine_batch_q1(
+            len(self.splits), self.ns, i, img.d, img.k, img.k_pad, _ptr(sp.xnorm),
+            _ptr(sp.xbn2), _ptr(sp.xerr), _ptr(cn), _ptr(cmax), _ptr(ce), _ptr(cemax),
+            labels_ptr, _ptr(cand), _ptr(scores), _ptr(margin), _ptr(self.stats),
+            _ptr(self.ws), self.ws.numel(), int(i == 0), self.st)
+        _lib.check(rc, "hbmr_kmeans_refine_batch_q1")
+
+    def finish(self):
+        B = len(self.splits)
+        img = self.img
+        _, cmax, _, cemax = self.norms
+        ni, nd, L = self.nbr
+        xs = (ctypes.c_void_p * B)(*[sp.x32.data_ptr() for sp in self.splits])
+        ls = (ctypes.c_void_p * B)(*[(lp.value if isinstance(lp, ctypes.c_void_p) else lp)
+                                     for lp in self.labels])
+        rc = self.lib.hbmr_kmeans_refine_batch_finish(
+            B, self.ns, xs, ls, img.d, self.splits[0].x32.shape[1], _ptr(img.cen), img.k,
+            img.k_pad, _ptr(cmax), _ptr(cemax), _ptr(ni), _ptr(nd), L, _ptr(self.stats),
+            self.stats.numel(), _ptr(self.ws), self.ws.numel(), self.st)
+        _lib.check(rc, "hbmr_kmeans_refine_batch_finish")
 
 
 def refine_f32(split: ExactSplit, img: CentroidImage, labels, cand, scores, margin,
                stats: torch.Tensor, stream=None, scratch: dict | None = None) -> None:
     """Certify the MFMA labels against the fp32 data; re-score the uncertain
-    points in fp64 (refine v3: the queue pipeline hbmr_kmeans_refine_f32_q;
-    HBMR_REFINE=1/2: the older single-kernel forms).  stats (int64 [3]) +=
-    (flagged, relabelled, points that needed the neighbour scan); a [5] stats
-    also counts the scan's neighbour distances and its full scans."""
+    points in fp64 (refine v3, the queue pipeline; HBMR_REFINE=1/2: the older
+    single-kernel forms).  stats (int64 [3]) += (flagged, relabelled, points
+    that needed the neighbour scan); a [5] stats also counts the scan's
+    neighbour distances and its full scans."""
     n = split.shape[0]
     if stats.dtype != torch.int64 or stats.numel() < 3:
         raise ValueError("stats must be int64 [3]")
     if labels.numel() != n or cand.numel() != 2 * n or margin.numel() != 2 * n:
         raise ValueError("labels [n], cand/margin [2n] from assign_top3 expected")
+    if REFINE_VERSION >= 3:
+        rb = _RefineBatch([split], img, stats, scratch, stream)
+        rb.q1(0, labels.data_ptr(), cand, scores, margin)
+        rb.finish()
+        return
     with torch.cuda.stream(stream) if stream is not None else _nullctx():
         cn, cmax, ce, cemax = img.norms(split.xb.dtype)
         ni, nd, L = img.neighbors()
-    args = (_ptr(split.x32), n, img.d, split.x32.shape[1], _ptr(split.xnorm), _ptr(split.xbn2),
-            _ptr(split.xerr), _ptr(img.cen), img.k, img.k_pad, _ptr(cn), _ptr(cmax), _ptr(ce),
-            _ptr(cemax), _ptr(ni), _ptr(nd), L,
-            _ptr(labels), _ptr(cand), _ptr(scores), _ptr(margin), _ptr(stats), stats.numel())
-    lib = _lib.load()
-    if REFINE_VERSION >= 3:
-        ws = _refine_ws(n, split.x32.device, scratch)
-        rc = lib.hbmr_kmeans_refine_f32_q(*args, _ptr(ws), ws.numel(),
-                                          _lib.stream_handle(stream))
-        _lib.check(rc, "hbmr_kmeans_refine_f32_q")
-        return
-    rc = lib.hbmr_kmeans_refine_f32(*args, _lib.stream_handle(stream))
+    rc = _lib.load().hbmr_kmeans_refine_f32(
+        _ptr(split.x32), n, img.d, split.x32.shape[1], _ptr(split.xnorm), _ptr(split.xbn2),
+        _ptr(split.xerr), _ptr(img.cen), img.k, img.k_pad, _ptr(cn), _ptr(cmax), _ptr(ce),
+        _ptr(cemax), _ptr(ni), _ptr(nd), L,
+        _ptr(labels), _ptr(cand), _ptr(scores), _ptr(margin), _ptr(stats), stats.numel(),
+        _lib.stream_handle(stream))
     _lib.check(rc, "hbmr_kmeans_refine_f32")
 
 
@@ -376,10 +422,11 @@ def assign_exact(split: ExactSplit, img: CentroidImage, stats: torch.Tensor,
 def assign_exact_batch(splits: list, img: CentroidImage, stats: torch.Tensor, out: torch.Tensor,
                        scratch: dict | None = None, stream=None) -> None:
     """Exact labels of a batch of splits, written back to back into ``out``
-    (int32 [sum n]): the top-3 assign and the certification per split, with
-    the centroid norms / neighbour lists fetched once, the batch's labels
-    written in place (no per-split copy) and the candidate / score / margin
-    scratch shared by every split (one stream orders the reuse)."""
+    (int32 [sum n]): the top-3 assign and the step-1 certification per split
+    (the candidate / score / margin scratch shared by every split: one stream
+    orders the reuse), then step 2 and the neighbour scan once per up to 64
+    splits (refine v3), with the centroid norms / neighbour lists fetched once
+    and the labels written in place."""
     if not splits:
         return
     dev = splits[0].xb.device
@@ -414,22 +461,26 @@ def assign_exact_batch(splits: list, img: CentroidImage, stats: torch.Tensor, ou
     st = _lib.stream_handle(stream)
     pc, ps, pm, pst = _ptr(cand), _ptr(sc), _ptr(mg), _ptr(stats)
     pcn, pcmax, pce, pcemax, pni, pnd = (_ptr(t) for t in (cn, cmax, ce, cemax, ni, nd))
-    ws = _refine_ws(nmax, dev, scratch) if REFINE_VERSION >= 3 else None
     base, off = out.data_ptr(), 0
-    for sp in splits:
-        n = sp.shape[0]
-        pl = ctypes.c_void_p(base + 4 * off)
-        rc = top3(_ptr(sp.xb), n, img.dp, _ptr(c16), _ptr(ch), img.k_pad, pl, pc, ps, pm, st)
-        _lib.check(rc, "hbmr_kmeans_assign_top3")
-        args = (_ptr(sp.x32), n, img.d, sp.x32.shape[1], _ptr(sp.xnorm), _ptr(sp.xbn2),
-                _ptr(sp.xerr), _ptr(img.cen), img.k, img.k_pad, pcn, pcmax, pce, pcemax, pni,
-                pnd, L, pl, pc, ps, pm, pst, stats.numel())
-        if ws is not None:
-            rc = lib.hbmr_kmeans_refine_f32_q(*args, _ptr(ws), ws.numel(), st)
-        else:
-            rc = lib.hbmr_kmeans_refine_f32(*args, st)
-        _lib.check(rc, "hbmr_kmeans_refine_f32")
-        off += n
+    for g0 in range(0, len(splits), MAX_REFINE_BATCH):
+        group = splits[g0:g0 + MAX_REFINE_BATCH]
+        rb = _RefineBatch(group, img, stats, scratch, stream) if REFINE_VERSION >= 3 else None
+        for i, sp in enumerate(group):
+            n = sp.shape[0]
+            pl = ctypes.c_void_p(base + 4 * off)
+            rc = top3(_ptr(sp.xb), n, img.dp, _ptr(c16), _ptr(ch), img.k_pad, pl, pc, ps, pm, st)
+            _lib.check(rc, "hbmr_kmeans_assign_top3")
+            if rb is not None:
+                rb.q1(i, pl, cand, sc, mg)
+            else:
+                rc = lib.hbmr_kmeans_refine_f32(
+                    _ptr(sp.x32), n, img.d, sp.x32.shape[1], _ptr(sp.xnorm), _ptr(sp.xbn2),
+                    _ptr(sp.xerr), _ptr(img.cen), img.k, img.k_pad, pcn, pcmax, pce, pcemax,
+                    pni, pnd, L, pl, pc, ps, pm, pst, stats.numel(), st)
+                _lib.check(rc, "hbmr_kmeans_refine_f32")
+            off += n
+        if rb is not None:
+            rb.finish()
 
 
 def map_split_exact(split: ExactSplit, img: CentroidImage, sums, counts, scratch: dict,

@@ -48,14 +48,21 @@ int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float
                            const float* nbr_dist, int L, int32_t* labels, const int32_t* cand,
                            const float* scores, const float* margin, unsigned long long* stats,
                            int nstats, hipStream_t st);
-long hbmr_kmeans_refine_workspace_bytes(long n);
-int hbmr_kmeans_refine_f32_q(const float* X32, long n, int d, int ldx, const float* xnorm,
-                             const float* xbn2, const float* xerr, const float* C32, int k,
-                             int k_pad, const float* cnorm, const float* cmax, const float* cerr,
-                             const float* cerrmax, const int32_t* nbr_idx, const float* nbr_dist,
-                             int L, int32_t* labels, const int32_t* cand, const float* scores,
-                             const float* margin, unsigned long long* stats, int nstats,
-                             void* ws, long ws_bytes, hipStream_t st);
+// refine v3 over a batch of splits (see kmeans.hip): q1 per split, finish once
+long hbmr_kmeans_refine_batch_bytes(int nsplit, const long* ns);
+int hbmr_kmeans_refine_batch_q1(int nsplit, const long* ns, int s, int d, int k, int k_pad,
+                                const float* xnorm, const float* xbn2, const float* xerr,
+                                const float* cnorm, const float* cmax, const float* cerr,
+                                const float* cerrmax, const int32_t* labels, const int32_t* cand,
+                                const float* scores, const float* margin,
+                                unsigned long long* stats, void* ws, long ws_bytes, int reset,
+                                hipStream_t st);
+int hbmr_kmeans_refine_batch_finish(int nsplit, const long* ns, const float* const* x32,
+                                    int32_t* const* labels, int d, int ldx, const float* C32,
+                                    int k, int k_pad, const float* cmax, const float* cerrmax,
+                                    const int32_t* nbr_idx, const float* nbr_dist, int L,
+                                    unsigned long long* stats, int nstats, void* ws,
+                                    long ws_bytes, hipStream_t st);
 int hbmr_kmeans_update(const long long* sums, const long long* counts, int fx_shift, int k, int d,
                        int dp, int k_pad, float* cen, void* cbf, float* chalf, float* shift2,
                        hipStream_t st);

@@ -1849,16 +1849,18 @@ __device__ __forceinline__ double row_sum16(double v) {
 template <int NM>
 __device__ __forceinline__ void load_row8(const float* __restrict__ r, int d, int sub,
                                           float (&v)[8 * NM]) {
+  // branch-free (see load_row16): clamped address + select, no per-load wait
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
     const int b = 8 * sub + 8 * kRefineGroup * m;
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), c = a;
-    if (b < d) {
-      a = *reinterpret_cast<const float4*>(r + b);
-      c = *reinterpret_cast<const float4*>(r + b + 4);
-    }
-    v[8 * m + 0] = a.x; v[8 * m + 1] = a.y; v[8 * m + 2] = a.z; v[8 * m + 3] = a.w;
-    v[8 * m + 4] = c.x; v[8 * m + 5] = c.y; v[8 * m + 6] = c.z; v[8 * m + 7] = c.w;
+    const bool ok = b < d;
+    const float* src = r + (ok ? b : 0);
+    const float4 a = *reinterpret_cast<const float4*>(src);
+    const float4 c = *reinterpret_cast<const float4*>(src + 4);
+    v[8 * m + 0] = ok ? a.x : 0.f; v[8 * m + 1] = ok ? a.y : 0.f;
+    v[8 * m + 2] = ok ? a.z : 0.f; v[8 * m + 3] = ok ? a.w : 0.f;
+    v[8 * m + 4] = ok ? c.x : 0.f; v[8 * m + 5] = ok ? c.y : 0.f;
+    v[8 * m + 6] = ok ? c.z : 0.f; v[8 * m + 7] = ok ? c.w : 0.f;
   }
 }
 
@@ -2135,91 +2137,153 @@ __global__ __launch_bounds__(128) void kmeans_image16_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Refine v3: the certification as a compacted queue pipeline.  v2 certifies
-// each point in the thread that scanned it and then walks the wave's ~10-20 %
-// flagged points four at a time, each round a dependent row-load chain, so a
-// wave waits out several L2/HBM round trips serially (87 µs per 781k-point
-// split).  v3 splits it by what each step needs:
-//   q1: step 1 (margins vs bounds) streams every point; the flagged ones are
-//       compacted into queue Q1 (wave ballots, one global atomic per block of
-//       1024 points);
-//   q2: step 2 over Q1 on a persistent grid, 16 lanes per entry and 2 × 4
-//       entries per wave in flight, every row load issued before the first FMA;
-//       winners the top three cannot certify go to queue Q2;
-//   q3: the Elkan neighbour scan over Q2 (≈1 % of points with fp16 operands).
-// Same bounds, same fp64 sums and ties as v1/v2: identical labels.
+// Refine v3: the certification as a compacted queue pipeline over a BATCH of
+// splits.  v2 certifies each point in the thread that scanned it and then walks
+// the wave's flagged points four at a time, each round a dependent row-load
+// chain, so a wave waits out several L2/HBM round trips serially.  v3 splits
+// the work by what each step needs:
+//   q1 (per split, right after its top-3 assign): step 1 (margins vs bounds)
+//       streams every point; the flagged ones are compacted into queue Q1;
+//   q2 (once per batch): step 2 over Q1 on a persistent grid, 8 lanes per entry
+//       (16 features each), 8 entries per wave, the next entries prefetched and
+//       every row load issued before the first FMA; winners that the top three
+//       cannot certify go to queue Q2;
+//   q3 (once per batch): the Elkan neighbour scan over Q2 (≈1 % of points with
+//       fp16 operands).
+// The batch pays q2/q3's latency chains once instead of once per split.  Same
+// bounds and ties as v1/v2; the fp64 distance sums differ only in summation
+// order (labels can differ only on exact fp64 ties).
+// Both queues are sharded 8 ways (by blockIdx % 8, i.e. per XCD under the
+// round-robin placement): one counter word takes ≈88 atomics/µs
+// (MI355X_MICROARCH.md, dequeue row).  Shard j holds its entries contiguously
+// at [j * cap, j * cap + count_j).
 struct ExactQ1 {
-  uint32_t row;
+  uint32_t row, split;
   int32_t b, s, t;
-  float sb, m3, x2, xn, xe, pad0, pad1, pad2;
+  float sb, m3, x2, xn, xe, pad0, pad1;
 };
 struct ExactQ2 {
-  uint32_t row;
-  int32_t w;
+  uint32_t row, split;
+  int32_t w, pad;
   double dw;
 };
-static_assert(sizeof(ExactQ1) == 48 && sizeof(ExactQ2) == 16, "queue entry layout");
+static_assert(sizeof(ExactQ1) == 48 && sizeof(ExactQ2) == 24, "queue entry layout");
 
+constexpr int kQShards = 8;
 constexpr int kQ1Per = 4;            // points per thread in the step-1 scan
-constexpr int kQ2Rounds = 2;         // 4-entry rounds per wave kept in flight
-constexpr int kRefineGrid = 2048;    // persistent grid of q2 / q3 (8 blocks per CU)
+constexpr int kQ2Lanes = 8;          // lanes per Q1 entry in step 2
+constexpr int kQ2Per = HBMR_WAVE / kQ2Lanes;
+constexpr int kRefineGrid = 2048;    // persistent grid of q2 (q3: a quarter)
 
-// workspace: counters [4] (u32: |Q1|, |Q2|) | Q1 [n] | Q2 [n]
-__host__ __device__ inline size_t refine_q_off1() { return 256; }
-__host__ __device__ inline size_t refine_q_off2(long n) {
-  return 256 + (((size_t)n * sizeof(ExactQ1) + 255) & ~(size_t)255);
+struct RefineTable {                 // the batch's splits, by value
+  int nsplit;
+  const float* x32[kMaxGroup];
+  int32_t* labels[kMaxGroup];
+};
+
+__host__ __device__ inline long ceil_div(long a, long b) { return (a + b - 1) / b; }
+
+struct RefineLayout {
+  long cap1, cap2;                   // entries per shard
+  unsigned g2;
+  size_t off1, off2, bytes;
+};
+inline RefineLayout refine_layout(int nsplit, const long* ns) {
+  RefineLayout L;
+  long total = 0, cap1 = 0;
+  for (int i = 0; i < nsplit; ++i) {
+    total += ns[i];
+    cap1 += ceil_div(ceil_div(ns[i], 256 * kQ1Per), kQShards) * 256 * kQ1Per;
+  }
+  L.cap1 = cap1;
+  L.g2 = (unsigned)std::max<long>(1, std::min<long>(kRefineGrid, ceil_div(total, 4 * kQ2Per)));
+  const long per_iter = (long)L.g2 * 4 * kQ2Per;           // Q1 entries per grid iteration
+  L.cap2 = ceil_div(L.g2, kQShards) * 4 * kQ2Per * std::max<long>(1, ceil_div(total, per_iter));
+  L.off1 = 256;
+  L.off2 = L.off1 + ((kQShards * (size_t)L.cap1 * sizeof(ExactQ1) + 255) & ~(size_t)255);
+  L.bytes = L.off2 + kQShards * (size_t)L.cap2 * sizeof(ExactQ2);
+  return L;
+}
+
+// item i of the flattened sharded queue → its slot (counts of the 8 shards)
+__device__ __forceinline__ long shard_slot(const uint32_t (&c)[kQShards], long cap, uint32_t i) {
+  uint32_t acc = 0;
+  long slot = 0;
+#pragma unroll
+  for (int j = 0; j < kQShards; ++j) {
+    if (i >= acc && i < acc + c[j]) slot = (long)j * cap + (i - acc);
+    acc += c[j];
+  }
+  return slot;
+}
+
+__device__ __forceinline__ uint32_t lane_rank(unsigned long long m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
 __global__ __launch_bounds__(256) void kmeans_refine_q1_kernel(
-    long n, int d, int k, const float* __restrict__ xnorm, const float* __restrict__ xbn2,
-    const float* __restrict__ xerr, const float* __restrict__ cnorm,
-    const float* __restrict__ cmax, const float* __restrict__ cerr,
-    const float* __restrict__ cerrmax, double pack_rel, const int32_t* __restrict__ labels,
-    const int32_t* __restrict__ cand, const float* __restrict__ score,
-    const float* __restrict__ margin, uint32_t* __restrict__ qcount, ExactQ1* __restrict__ q1,
+    long n, int sidx, int d, int k, const float* __restrict__ xnorm,
+    const float* __restrict__ xbn2, const float* __restrict__ xerr,
+    const float* __restrict__ cnorm, const float* __restrict__ cmax,
+    const float* __restrict__ cerr, const float* __restrict__ cerrmax, double pack_rel,
+    const int32_t* __restrict__ labels, const int32_t* __restrict__ cand,
+    const float* __restrict__ score, const float* __restrict__ margin,
+    uint32_t* __restrict__ qcount, ExactQ1* __restrict__ q1, long cap1,
     unsigned long long* __restrict__ stats) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int shard = blockIdx.x % kQShards;
   __shared__ uint32_t wcnt[4][kQ1Per];
   __shared__ uint32_t base_s;
   const double inflate = 1.0 + 0x1p-20;
   const double gam = (double)(d + 2) * 0x1p-23 * 1.01;
   const double cem = (double)cerrmax[0] * inflate;
   const double cm = (double)cmax[0] * inflate + cem;
+  // every load of the four points first, then the dependent gathers, then math
   ExactQ1 e[kQ1Per];
+  bool in[kQ1Per];
+  float m2[kQ1Per];
+#pragma unroll
+  for (int i = 0; i < kQ1Per; ++i) {
+    const long p = (long)blockIdx.x * (256 * kQ1Per) + i * 256 + tid;
+    in[i] = p < n;
+    const long q = in[i] ? p : n - 1;
+    e[i].row = (uint32_t)q;
+    e[i].split = (uint32_t)sidx;
+    e[i].b = labels[q];
+    e[i].s = cand[q];
+    e[i].t = cand[n + q];
+    e[i].sb = score[q];
+    m2[i] = margin[q];
+    e[i].m3 = margin[n + q];
+    e[i].x2 = xbn2[q];
+    e[i].xn = xnorm[q];
+    e[i].xe = xerr[q];
+  }
+  float cnb[kQ1Per], ceb[kQ1Per];
+#pragma unroll
+  for (int i = 0; i < kQ1Per; ++i) {
+    cnb[i] = cnorm[e[i].b];
+    ceb[i] = cerr[e[i].b];
+  }
   bool flag[kQ1Per];
   uint32_t rank[kQ1Per];
 #pragma unroll
   for (int i = 0; i < kQ1Per; ++i) {
-    const long p = (long)blockIdx.x * (256 * kQ1Per) + i * 256 + tid;
     flag[i] = false;
-    if (p < n) {
-      const int b = labels[p], s2 = cand[p];
-      if (s2 < k) {
-        const float xnf = xnorm[p], xef = xerr[p], x2f = xbn2[p];
-        const double xn = ((double)xnf + (double)xef) * inflate;
-        const double x2 = (double)x2f;
-        const double sb = score[p];
-        const double m2 = margin[p];
-        const double amax = ((double)xef + cem) * inflate;
-        double eb, es, dl_b, dl_s;
-        exact_bound(sb, ((double)cnorm[b] + (double)cerr[b]) * inflate, xn, x2,
-                    ((double)xef + (double)cerr[b]) * inflate, gam, pack_rel, eb, dl_b);
-        exact_bound(sb - m2, cm, xn, x2, amax, gam, pack_rel, es, dl_s);
-        flag[i] = !(m2 > eb + es && dl_s >= 2.0 * amax);
-        e[i].row = (uint32_t)p;
-        e[i].b = b;
-        e[i].s = s2;
-        e[i].t = cand[n + p];
-        e[i].sb = score[p];
-        e[i].m3 = margin[n + p];
-        e[i].x2 = x2f;
-        e[i].xn = xnf;
-        e[i].xe = xef;
-      }
+    if (in[i] && e[i].s < k) {
+      const double xn = ((double)e[i].xn + (double)e[i].xe) * inflate;
+      const double x2 = (double)e[i].x2;
+      const double sb = e[i].sb;
+      const double mm = m2[i];
+      const double amax = ((double)e[i].xe + cem) * inflate;
+      double eb, es, dl_b, dl_s;
+      exact_bound(sb, ((double)cnb[i] + (double)ceb[i]) * inflate, xn, x2,
+                  ((double)e[i].xe + (double)ceb[i]) * inflate, gam, pack_rel, eb, dl_b);
+      exact_bound(sb - mm, cm, xn, x2, amax, gam, pack_rel, es, dl_s);
+      flag[i] = !(mm > eb + es && dl_s >= 2.0 * amax);
     }
     const unsigned long long m = __ballot(flag[i]);
-    rank[i] = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    rank[i] = lane_rank(m);
     if (lane == 0) wcnt[wave][i] = (uint32_t)__popcll(m);
   }
   __syncthreads();
@@ -2233,25 +2297,55 @@ __global__ __launch_bounds__(256) void kmeans_refine_q1_kernel(
         wcnt[w][i] = tot;
         tot += c;
       }
-    base_s = tot ? atomicAdd(qcount, tot) : 0u;
+    base_s = tot ? atomicAdd(qcount + shard, tot) : 0u;
     if (tot) atomicAdd(stats, (unsigned long long)tot);
   }
   __syncthreads();
-  const uint32_t base = base_s;
+  ExactQ1* out = q1 + (long)shard * cap1 + base_s;
 #pragma unroll
   for (int i = 0; i < kQ1Per; ++i)
-    if (flag[i]) q1[base + wcnt[wave][i] + rank[i]] = e[i];
+    if (flag[i]) out[wcnt[wave][i] + rank[i]] = e[i];
+}
+
+// 16 consecutive features 16*sub + 128*m (+0..15) of a row (0 past d; d % 8 == 0)
+template <int NM>
+__device__ __forceinline__ void load_row16(const float* __restrict__ r, int d, int sub,
+                                           float (&v)[16 * NM]) {
+  // branch-free: every load is issued (address clamped into the row) and the
+  // features past d are zeroed by a select, so all of a round's loads stay in
+  // flight together (a guarded load made hipcc wait on each one in turn)
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int b = 16 * sub + 128 * m + 8 * h;
+      const bool ok = b < d;
+      const float* src = r + (ok ? b : 0);
+      const float4 a = *reinterpret_cast<const float4*>(src);
+      const float4 c = *reinterpret_cast<const float4*>(src + 4);
+      float* o = v + 16 * m + 8 * h;
+      o[0] = ok ? a.x : 0.f; o[1] = ok ? a.y : 0.f; o[2] = ok ? a.z : 0.f; o[3] = ok ? a.w : 0.f;
+      o[4] = ok ? c.x : 0.f; o[5] = ok ? c.y : 0.f; o[6] = ok ? c.z : 0.f; o[7] = ok ? c.w : 0.f;
+    }
+  }
+}
+
+__device__ __forceinline__ double row_sum8(double v) {
+  v += dpp_f64<0xB1>(v);   // xor 1
+  v += dpp_f64<0x4E>(v);   // xor 2
+  v += dpp_f64<0x141>(v);  // row_half_mirror: the other quad of the 8-lane group
+  return v;
 }
 
 template <int NM>
 __global__ __launch_bounds__(256) void kmeans_refine_q2_kernel(
-    const float* __restrict__ X32, int d, int ldx, const float* __restrict__ C32, int k,
+    const RefineTable tbl, int d, int ldx, const float* __restrict__ C32, int k,
     const float* __restrict__ cmax, const float* __restrict__ cerrmax, double pack_rel,
-    int32_t* __restrict__ labels, const uint32_t* __restrict__ qcount,
-    const ExactQ1* __restrict__ q1, uint32_t* __restrict__ q2count, ExactQ2* __restrict__ q2,
+    const uint32_t* __restrict__ qcount, const ExactQ1* __restrict__ q1, long cap1,
+    uint32_t* __restrict__ q2count, ExactQ2* __restrict__ q2, long cap2,
     unsigned long long* __restrict__ stats) {
   const int tid = threadIdx.x, lane = tid & 63;
-  const int grp = lane / kRefineGroup, sub = lane % kRefineGroup;
+  const int grp = lane / kQ2Lanes, sub = lane % kQ2Lanes;
   __shared__ unsigned long long cnt[2];
   if (tid < 2) cnt[tid] = 0;
   __syncthreads();
@@ -2259,73 +2353,75 @@ __global__ __launch_bounds__(256) void kmeans_refine_q2_kernel(
   const double gam = (double)(d + 2) * 0x1p-23 * 1.01;
   const double cem = (double)cerrmax[0] * inflate;
   const double cm = (double)cmax[0] * inflate + cem;
-  const uint32_t total = *qcount;
-  const uint32_t nwaves = gridDim.x * 4;
-  const uint32_t gw = blockIdx.x * 4 + (tid >> 6);
-  constexpr int PER = 4 * kQ2Rounds;
-  for (uint32_t base = gw * PER; base < total; base += nwaves * PER) {
-    ExactQ1 e[kQ2Rounds];
-    bool have[kQ2Rounds];
-    float xf[kQ2Rounds][8 * NM];
-    float cv[kQ2Rounds][3][8 * NM];
+  uint32_t c1[kQShards];
+  uint32_t total = 0;
 #pragma unroll
-    for (int r = 0; r < kQ2Rounds; ++r) {
-      const uint32_t idx = base + r * 4 + grp;
-      have[r] = idx < total;
-      e[r] = q1[have[r] ? idx : base];
-      const bool t_real = e[r].t < k;
-      load_row8<NM>(X32 + (size_t)e[r].row * ldx, d, sub, xf[r]);
-      load_row8<NM>(C32 + (size_t)e[r].b * d, d, sub, cv[r][0]);
-      load_row8<NM>(C32 + (size_t)e[r].s * d, d, sub, cv[r][1]);
-      load_row8<NM>(C32 + (size_t)(t_real ? e[r].t : e[r].b) * d, d, sub, cv[r][2]);
+  for (int j = 0; j < kQShards; ++j) {
+    c1[j] = qcount[j];
+    total += c1[j];
+  }
+  const int shard = blockIdx.x % kQShards;
+  const uint32_t stride = gridDim.x * 4 * kQ2Per;
+  uint32_t base = (blockIdx.x * 4 + (tid >> 6)) * kQ2Per;
+  ExactQ1 e;
+  if (base < total) e = q1[shard_slot(c1, cap1, min(base + grp, total - 1))];
+  for (; base < total; base += stride) {
+    const ExactQ1 q = e;
+    const bool have = base + grp < total;
+    // prefetch the next round's entry while this round's rows are in flight
+    const uint32_t nb = base + stride;
+    if (nb < total) e = q1[shard_slot(c1, cap1, min(nb + grp, total - 1))];
+    const bool t_real = q.t < k;
+    const float* xr = tbl.x32[q.split] + (size_t)q.row * ldx;
+    float xf[16 * NM], c0[16 * NM], c1r[16 * NM], c2[16 * NM];
+    load_row16<NM>(xr, d, sub, xf);
+    load_row16<NM>(C32 + (size_t)q.b * d, d, sub, c0);
+    load_row16<NM>(C32 + (size_t)q.s * d, d, sub, c1r);
+    load_row16<NM>(C32 + (size_t)(t_real ? q.t : q.b) * d, d, sub, c2);
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16 * NM; ++i) {
+      const double x = (double)xf[i];
+      const double e0 = x - (double)c0[i], e1 = x - (double)c1r[i], e2 = x - (double)c2[i];
+      a0 = fma(e0, e0, a0);
+      a1 = fma(e1, e1, a1);
+      a2 = fma(e2, e2, a2);
     }
-#pragma unroll
-    for (int r = 0; r < kQ2Rounds; ++r) {
-      double acc[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-      for (int i = 0; i < 8 * NM; ++i) {
-        const double x = (double)xf[r][i];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          const double df = x - (double)cv[r][c][i];
-          acc[c] = fma(df, df, acc[c]);
-        }
-      }
-      double d3[3];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) d3[c] = row_sum16(acc[c]);
-      if (!have[r]) continue;
-      const ExactQ1& q = e[r];
-      const bool t_real = q.t < k;
-      int w = q.b;
-      double dw = d3[0];
-      if (d3[1] < dw || (d3[1] == dw && q.s < w)) { w = q.s; dw = d3[1]; }
-      if (t_real && (d3[2] < dw || (d3[2] == dw && q.t < w))) { w = q.t; dw = d3[2]; }
-      bool certified = !t_real;
-      if (t_real) {
-        const double xn = ((double)q.xn + (double)q.xe) * inflate;
-        const double x2 = (double)q.x2;
-        const double amax = ((double)q.xe + cem) * inflate;
-        const double st = (double)q.sb - (double)q.m3;
-        double et, dl_t;
-        exact_bound(st, cm, xn, x2, amax, gam, pack_rel, et, dl_t);
-        certified = 0.5 * (x2 - dw) - x2 * 0x1p-23 > st + et && dl_t >= 2.0 * amax;
-      }
-      if (sub == 0) {
-        if (certified) {
-          if (w != q.b) {
-            labels[q.row] = w;
-            atomicAdd(&cnt[0], 1ull);
-          }
-        } else {
-          const uint32_t slot = atomicAdd(q2count, 1u);
-          ExactQ2 o;
-          o.row = q.row;
-          o.w = w;
-          o.dw = dw;
-          q2[slot] = o;
-          atomicAdd(&cnt[1], 1ull);
-        }
+    const double d0 = row_sum8(a0), d1 = row_sum8(a1), d2 = row_sum8(a2);
+    int w = q.b;
+    double dw = d0;
+    if (d1 < dw || (d1 == dw && q.s < w)) { w = q.s; dw = d1; }
+    if (t_real && (d2 < dw || (d2 == dw && q.t < w))) { w = q.t; dw = d2; }
+    bool certified = !t_real;
+    if (t_real) {
+      const double xn = ((double)q.xn + (double)q.xe) * inflate;
+      const double x2 = (double)q.x2;
+      const double amax = ((double)q.xe + cem) * inflate;
+      const double st = (double)q.sb - (double)q.m3;
+      double et, dl_t;
+      exact_bound(st, cm, xn, x2, amax, gam, pack_rel, et, dl_t);
+      certified = 0.5 * (x2 - dw) - x2 * 0x1p-23 > st + et && dl_t >= 2.0 * amax;
+    }
+    if (have && sub == 0 && certified && w != q.b) {
+      tbl.labels[q.split][q.row] = w;
+      atomicAdd(&cnt[0], 1ull);
+    }
+    // one sharded atomic per wave and round for its Q2 entries
+    const bool spill = have && sub == 0 && !certified;
+    const unsigned long long m = __ballot(spill);
+    if (m) {
+      uint32_t b2 = 0;
+      if (lane == 0) b2 = atomicAdd(q2count + shard, (uint32_t)__popcll(m));
+      b2 = __shfl(b2, 0);
+      if (spill) {
+        ExactQ2 o;
+        o.row = q.row;
+        o.split = q.split;
+        o.w = w;
+        o.pad = 0;
+        o.dw = dw;
+        q2[(long)shard * cap2 + b2 + lane_rank(m)] = o;
+        atomicAdd(&cnt[1], 1ull);
       }
     }
   }
@@ -2336,27 +2432,34 @@ __global__ __launch_bounds__(256) void kmeans_refine_q2_kernel(
 
 template <int NM>
 __global__ __launch_bounds__(256) void kmeans_refine_q3_kernel(
-    const float* __restrict__ X32, int d, int ldx, const float* __restrict__ C32, int k,
+    const RefineTable tbl, int d, int ldx, const float* __restrict__ C32, int k,
     const int32_t* __restrict__ nbr_idx, const float* __restrict__ nbr_dist, int L,
-    int32_t* __restrict__ labels, const uint32_t* __restrict__ q2count,
-    const ExactQ2* __restrict__ q2, unsigned long long* __restrict__ stats, int nstats) {
+    const uint32_t* __restrict__ q2count, const ExactQ2* __restrict__ q2, long cap2,
+    unsigned long long* __restrict__ stats, int nstats) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int grp = lane / kRefineGroup, sub = lane % kRefineGroup;
   __shared__ unsigned long long cnt[3];
   if (tid < 3) cnt[tid] = 0;
   __syncthreads();
-  const uint32_t total = *q2count;
+  uint32_t c2[kQShards];
+  uint32_t total = 0;
+#pragma unroll
+  for (int j = 0; j < kQShards; ++j) {
+    c2[j] = q2count[j];
+    total += c2[j];
+  }
   const uint32_t nwaves = gridDim.x * 4;
   const uint32_t gw = blockIdx.x * 4 + (tid >> 6);
   for (uint32_t base = gw * 4; base < total; base += nwaves * 4) {
     const uint32_t idx = base + grp;
     const bool have = idx < total;
-    const ExactQ2 q = q2[have ? idx : base];
-    const int b0 = labels[q.row];   // the MFMA pick: step 2 left it in place
+    const ExactQ2 q = q2[shard_slot(c2, cap2, have ? idx : base)];
+    int32_t* lab = tbl.labels[q.split];
+    const int b0 = lab[q.row];   // the MFMA pick: step 2 left it in place
     double xv[8 * NM];
     {
       float xf[8 * NM];
-      load_row8<NM>(X32 + (size_t)q.row * ldx, d, sub, xf);
+      load_row8<NM>(tbl.x32[q.split] + (size_t)q.row * ldx, d, sub, xf);
 #pragma unroll
       for (int i = 0; i < 8 * NM; ++i) xv[i] = (double)xf[i];
     }
@@ -2407,7 +2510,7 @@ __global__ __launch_bounds__(256) void kmeans_refine_q3_kernel(
       atomicAdd(&cnt[1], (unsigned long long)evals);
       if (full) atomicAdd(&cnt[2], 1ull);
       if (w != b0) atomicAdd(&cnt[0], 1ull);
-      labels[q.row] = w;
+      lab[q.row] = w;
     }
   }
   __syncthreads();
@@ -2974,54 +3077,85 @@ int hbmr_kmeans_image16(const float* cen, int k, int d, int dp, int k_pad, int f
 }
 
 
-long hbmr_kmeans_refine_workspace_bytes(long n) {
-  return (long)(refine_q_off2(n) + (size_t)n * sizeof(ExactQ2));
+// Refine v3 over a batch of splits (ns[nsplit]; at most 64): per split, right
+// after its top-3 assign, hbmr_kmeans_refine_batch_q1 (reset = 1 for the
+// first split); then hbmr_kmeans_refine_batch_finish once.  The workspace
+// holds the two sharded queues (hbmr_kmeans_refine_batch_bytes).
+long hbmr_kmeans_refine_batch_bytes(int nsplit, const long* ns) {
+  if (nsplit <= 0 || nsplit > kMaxGroup) return -1;
+  return (long)refine_layout(nsplit, ns).bytes;
 }
 
-// refine v3 (the queue pipeline of kmeans_refine_q*): same contract as
-// hbmr_kmeans_refine_f32 plus a workspace of hbmr_kmeans_refine_workspace_bytes(n)
-int hbmr_kmeans_refine_f32_q(const float* X32, long n, int d, int ldx, const float* xnorm,
-                             const float* xbn2, const float* xerr, const float* C32, int k,
-                             int k_pad, const float* cnorm, const float* cmax, const float* cerr,
-                             const float* cerrmax, const int32_t* nbr_idx, const float* nbr_dist,
-                             int L, int32_t* labels, const int32_t* cand, const float* scores,
-                             const float* margin, unsigned long long* stats, int nstats,
-                             void* ws, long ws_bytes, hipStream_t st) {
-  if (n <= 0) return 0;
-  if (d > ldx || d > kRefineMaxDp || k <= 0 || k_pad < k || L < 1 || L > k || nstats < 3 ||
-      n > 0xffffffffL || ws_bytes < hbmr_kmeans_refine_workspace_bytes(n))
+int hbmr_kmeans_refine_batch_q1(int nsplit, const long* ns, int s, int d, int k, int k_pad,
+                                const float* xnorm, const float* xbn2, const float* xerr,
+                                const float* cnorm, const float* cmax, const float* cerr,
+                                const float* cerrmax, const int32_t* labels, const int32_t* cand,
+                                const float* scores, const float* margin,
+                                unsigned long long* stats, void* ws, long ws_bytes, int reset,
+                                hipStream_t st) {
+  if (nsplit <= 0 || nsplit > kMaxGroup || s < 0 || s >= nsplit || k <= 0 || k_pad < k ||
+      d > kRefineMaxDp || ((uintptr_t)ws & 255))
     return (int)hipErrorInvalidValue;
-  if (d % 8 || ldx % 4 || ((uintptr_t)X32 & 15) || ((uintptr_t)C32 & 15) || ((uintptr_t)ws & 255))
+  for (int i = 0; i < nsplit; ++i)
+    if (ns[i] < 0 || ns[i] > 0x7fffffffL) return (int)hipErrorInvalidValue;
+  const RefineLayout Ly = refine_layout(nsplit, ns);
+  if (ws_bytes < (long)Ly.bytes) return (int)hipErrorInvalidValue;
+  char* w = static_cast<char*>(ws);
+  uint32_t* c1 = reinterpret_cast<uint32_t*>(w);
+  if (reset) HBMR_RETURN_IF_ERROR(hipMemsetAsync(c1, 0, 2 * kQShards * sizeof(uint32_t), st));
+  const long n = ns[s];
+  if (n == 0) return 0;
+  int tb = 0;
+  while ((1 << tb) < k_pad / 32) ++tb;
+  const double pack_rel = ldexp(1.0, 4 + tb - 23);
+  const long b1 = ceil_div(n, 256 * kQ1Per);
+  hipLaunchKernelGGL(kmeans_refine_q1_kernel, dim3((unsigned)b1), dim3(256), 0, st, n, s, d, k,
+                     xnorm, xbn2, xerr, cnorm, cmax, cerr, cerrmax, pack_rel, labels, cand,
+                     scores, margin, c1, reinterpret_cast<ExactQ1*>(w + Ly.off1), Ly.cap1, stats);
+  return (int)hipGetLastError();
+}
+
+int hbmr_kmeans_refine_batch_finish(int nsplit, const long* ns, const float* const* x32,
+                                    int32_t* const* labels, int d, int ldx, const float* C32,
+                                    int k, int k_pad, const float* cmax, const float* cerrmax,
+                                    const int32_t* nbr_idx, const float* nbr_dist, int L,
+                                    unsigned long long* stats, int nstats, void* ws,
+                                    long ws_bytes, hipStream_t st) {
+  if (nsplit <= 0 || nsplit > kMaxGroup || d > ldx || d > kRefineMaxDp || d % 8 || ldx % 4 ||
+      k <= 0 || k_pad < k || L < 1 || L > k || nstats < 3 || ((uintptr_t)C32 & 15) ||
+      ((uintptr_t)ws & 255))
     return (int)hipErrorInvalidValue;
+  const RefineLayout Ly = refine_layout(nsplit, ns);
+  if (ws_bytes < (long)Ly.bytes) return (int)hipErrorInvalidValue;
+  RefineTable tbl;
+  std::memset(&tbl, 0, sizeof(tbl));
+  tbl.nsplit = nsplit;
+  for (int i = 0; i < nsplit; ++i) {
+    if ((uintptr_t)x32[i] & 15) return (int)hipErrorInvalidValue;
+    tbl.x32[i] = x32[i];
+    tbl.labels[i] = labels[i];
+  }
   int tb = 0;
   while ((1 << tb) < k_pad / 32) ++tb;
   const double pack_rel = ldexp(1.0, 4 + tb - 23);
   char* w = static_cast<char*>(ws);
-  uint32_t* counts = reinterpret_cast<uint32_t*>(w);
-  ExactQ1* q1 = reinterpret_cast<ExactQ1*>(w + refine_q_off1());
-  ExactQ2* q2 = reinterpret_cast<ExactQ2*>(w + refine_q_off2(n));
-  HBMR_RETURN_IF_ERROR(hipMemsetAsync(counts, 0, 16, st));
-  const long b1 = (n + 256 * kQ1Per - 1) / (256 * kQ1Per);
-  hipLaunchKernelGGL(kmeans_refine_q1_kernel, dim3((unsigned)b1), dim3(256), 0, st, n, d, k,
-                     xnorm, xbn2, xerr, cnorm, cmax, cerr, cerrmax, pack_rel, labels, cand,
-                     scores, margin, counts, q1, stats);
-  HBMR_RETURN_IF_ERROR(hipGetLastError());
-  // persistent grids, never larger than the worst case needs
-  const long need2 = (n + 4 * 4 * kQ2Rounds - 1) / (4 * 4 * kQ2Rounds);
-  const unsigned g2 = (unsigned)std::min<long>(kRefineGrid, need2);
-  const unsigned g3 = (unsigned)std::min<long>(kRefineGrid / 4, (n + 15) / 16);
+  uint32_t* c1 = reinterpret_cast<uint32_t*>(w);
+  uint32_t* c2 = c1 + kQShards;
+  const ExactQ1* q1 = reinterpret_cast<const ExactQ1*>(w + Ly.off1);
+  ExactQ2* q2 = reinterpret_cast<ExactQ2*>(w + Ly.off2);
+  const unsigned g3 = std::max(1u, std::min(Ly.g2, (unsigned)(kRefineGrid / 4)));
   if (d <= 128) {
-    hipLaunchKernelGGL(kmeans_refine_q2_kernel<1>, dim3(g2), dim3(256), 0, st, X32, d, ldx, C32,
-                       k, cmax, cerrmax, pack_rel, labels, counts, q1, counts + 1, q2, stats);
+    hipLaunchKernelGGL(kmeans_refine_q2_kernel<1>, dim3(Ly.g2), dim3(256), 0, st, tbl, d, ldx,
+                       C32, k, cmax, cerrmax, pack_rel, c1, q1, Ly.cap1, c2, q2, Ly.cap2, stats);
     HBMR_RETURN_IF_ERROR(hipGetLastError());
-    hipLaunchKernelGGL(kmeans_refine_q3_kernel<1>, dim3(g3), dim3(256), 0, st, X32, d, ldx, C32,
-                       k, nbr_idx, nbr_dist, L, labels, counts + 1, q2, stats, nstats);
+    hipLaunchKernelGGL(kmeans_refine_q3_kernel<1>, dim3(g3), dim3(256), 0, st, tbl, d, ldx, C32,
+                       k, nbr_idx, nbr_dist, L, c2, q2, Ly.cap2, stats, nstats);
   } else {
-    hipLaunchKernelGGL(kmeans_refine_q2_kernel<2>, dim3(g2), dim3(256), 0, st, X32, d, ldx, C32,
-                       k, cmax, cerrmax, pack_rel, labels, counts, q1, counts + 1, q2, stats);
+    hipLaunchKernelGGL(kmeans_refine_q2_kernel<2>, dim3(Ly.g2), dim3(256), 0, st, tbl, d, ldx,
+                       C32, k, cmax, cerrmax, pack_rel, c1, q1, Ly.cap1, c2, q2, Ly.cap2, stats);
     HBMR_RETURN_IF_ERROR(hipGetLastError());
-    hipLaunchKernelGGL(kmeans_refine_q3_kernel<2>, dim3(g3), dim3(256), 0, st, X32, d, ldx, C32,
-                       k, nbr_idx, nbr_dist, L, labels, counts + 1, q2, stats, nstats);
+    hipLaunchKernelGGL(kmeans_refine_q3_kernel<2>, dim3(g3), dim3(256), 0, st, tbl, d, ldx, C32,
+                       k, nbr_idx, nbr_dist, L, c2, q2, Ly.cap2, stats, nstats);
   }
   return (int)hipGetLastError();
 }

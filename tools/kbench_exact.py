@@ -97,6 +97,12 @@ def run_dtype(a, n, k, d, dp, x32, img, xb, lab, dt):
             km.assign_top3(s.xb, img, *b)
             km.refine_f32(s, img, *b, stats)
 
+    bscratch = {}
+    labcat = torch.empty(n, dtype=torch.int32, device=dev)
+
+    def batch():
+        km.assign_exact_batch(splits, img, stats, labcat, bscratch)
+
     sums, cnt = km.new_partials(k, dp, dev)
 
     def acc32():
@@ -120,6 +126,7 @@ def run_dtype(a, n, k, d, dp, x32, img, xb, lab, dt):
              neighbour_scan_frac=round(sc / n, 6),
              neighbours_per_scan=round(ev / max(1, sc), 1),
              full_scan_frac=round(full / max(1, sc), 4))
+    r["exact_batch_ms"] = timeit(batch, a.reps)
     r["accum_f32_ms"] = timeit(acc32, a.reps)
     r["accum_bf16_ms"] = timeit(acc16, a.reps)
     del splits
