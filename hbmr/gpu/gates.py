@@ -30,6 +30,7 @@ class Gates:
         self._lock = threading.Lock()
         self._held: dict = {}
         self._open: dict = {}
+        self._epoch: dict = {}      # job id → times its gate was closed
         self._keep = keep
 
     def admit(self, runs):
@@ -48,10 +49,18 @@ class Gates:
                     self._held.setdefault(g, []).append(r)
         return now
 
-    def open(self, job_id, event=None):
+    def epoch(self, job_id) -> int:
+        """Taken by a reduce attempt when it starts; its ``open`` is ignored if
+        the gate was closed since (a killed attempt of a restarted gang)."""
+        with self._lock:
+            return self._epoch.get(job_id, 0)
+
+    def open(self, job_id, event=None, epoch=None):
         """Job ``job_id``'s result is enqueued (``event`` marks it on the
         device): returns the runs that were held for it, each with ``wait``."""
         with self._lock:
+            if epoch is not None and epoch != self._epoch.get(job_id, 0):
+                return []
             self._open.pop(job_id, None)
             self._open[job_id] = event
             while len(self._open) > self._keep:
@@ -60,6 +69,15 @@ class Gates:
         for r in held:
             r.wait = event
         return held
+
+    def close(self, job_id):
+        """Job ``job_id``'s reduce is re-run (its gang failed after opening
+        the gate): runs gated on it are held again until the new reduce opens."""
+        with self._lock:
+            self._open.pop(job_id, None)
+            self._epoch[job_id] = self._epoch.get(job_id, 0) + 1
+            while len(self._epoch) > self._keep:
+                self._epoch.pop(next(iter(self._epoch)))
 
     def is_open(self, job_id) -> bool:
         with self._lock:

@@ -261,6 +261,12 @@ class RemoteGpuRuntime:
         except OSError:
             pass
 
+    def close_gate(self, jid):
+        try:
+            send_msg(self.sock, ("close_gate", jid), self._send_lock)
+        except OSError:
+            pass
+
     def drop_job(self, jid):
         """The job is finished or killed (KillJobAction): the worker frees its
         state (map outputs held on the device), and its attempts no longer count

@@ -130,15 +130,18 @@ class GpuRuntime:
         return self.devices[d].torch_device
 
     # -- staged maps (hbmr/gpu/gates.py) ---------------------------------------------------
-    def open_gate(self, job_id, event=None):
+    def open_gate(self, job_id, event=None, epoch=None):
         """Job ``job_id``'s reduce result is enqueued on the device (``event``):
         its staged dependents' held maps go to the slots, behind the event."""
-        held = self.gates.open(job_id, event)
+        held = self.gates.open(job_id, event, epoch)
         if held:
             self.submit_many(held)
 
     def drop_held(self, job_id):
         return self.gates.drop(job_id)
+
+    def close_gate(self, job_id):
+        self.gates.close(job_id)
 
     def device_status(self):
         out = []

@@ -85,15 +85,18 @@ class SimulatedGpuRuntime:
     def torch_device(self, d):
         return torch.device("cpu")
 
-    def open_gate(self, job_id, event=None):
+    def open_gate(self, job_id, event=None, epoch=None):
         """Staged maps held for ``job_id`` go to the device queue; a simulated
         device runs them after its earlier work (busy_until), as a stream would."""
-        held = self.gates.open(job_id, event)
+        held = self.gates.open(job_id, event, epoch)
         if held:
             self.submit_many(held)
 
     def drop_held(self, job_id):
         return self.gates.drop(job_id)
+
+    def close_gate(self, job_id):
+        self.gates.close(job_id)
 
     def device_status(self):
         return [P.GpuDeviceStatus(device=d, max_slots=len(dev.slots),

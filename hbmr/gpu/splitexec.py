@@ -43,6 +43,11 @@ def run_split_cpu_map(host, run):
             host._finish(run, P.KILLED, "killed before start")
             return
         host._maybe_inject_fault(run)
+        # a failure AFTER the gates opened (tests of staged-job restarts): the
+        # attempt publishes a poisoned result (split_job.poison_result), lets
+        # the staged maps run on it, then fails
+        late = js.conf.get("hbmr.faultinject.reduce.fail.after.release.attempt")
+        late = bool(late) and late in spec.attempt_id
         rep = TaskReporter()
         run.task = SplitTaskShim(rep, run.kill)
         ctx = TaskContext(host, js, spec, rep, device="cpu")
@@ -142,6 +147,11 @@ def run_split_reduce(host, run, device=None):
             # an ordinary task failure (not a crash): the attempt FAILS and the
             # JobTracker re-runs the collective gang on the same worker
             raise RuntimeError(f"injected reduce failure ({spec.attempt_id})")
+        # a failure AFTER the gates opened (tests of staged-job restarts): the
+        # attempt publishes a poisoned result (split_job.poison_result), lets
+        # the staged maps run on it, then fails
+        late = js.conf.get("hbmr.faultinject.reduce.fail.after.release.attempt")
+        late = bool(late) and late in spec.attempt_id
         rep = TaskReporter()
         run.task = SplitTaskShim(rep, run.kill)
         ctx = TaskContext(host, js, spec, rep)
@@ -162,11 +172,15 @@ def run_split_reduce(host, run, device=None):
         cuda = device is not None and device.type == "cuda"
         rt = getattr(host, "gpu_runtime", None)
         released = [False]
+        gates = getattr(rt, "gates", None)
+        gate_epoch = gates.epoch(spec.job_id) if gates is not None else None
 
         def release_dependents():
             if released[0]:
                 return
             released[0] = True
+            if late and hasattr(js.split_job, "poison_result"):
+                js.split_job.poison_result(ctx)
             if rt is None or not hasattr(rt, "open_gate"):
                 return
             ev = getattr(ctx, "sim_ready", None)   # simulated device: a ready time
@@ -174,7 +188,7 @@ def run_split_reduce(host, run, device=None):
                 import torch
                 ev = torch.cuda.Event()
                 ev.record()
-            rt.open_gate(spec.job_id, ev)
+            rt.open_gate(spec.job_id, ev, gate_epoch)
             if TRACE.on:
                 TRACE.instant("tt.reduce.gate_open", job=spec.job_id)
         ctx.release_dependents = release_dependents
@@ -214,6 +228,8 @@ def run_split_reduce(host, run, device=None):
                 TRACE.instant("tt.reduce.combined", attempt=spec.attempt_id)
             js.result = js.split_job.reduce(ctx, combined)
             release_dependents()
+        if late:
+            raise RuntimeError(f"injected reduce failure after release ({spec.attempt_id})")
         if TRACE.on:
             TRACE.instant("tt.reduce.done", attempt=spec.attempt_id)
         with js.lock:

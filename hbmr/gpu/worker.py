@@ -347,6 +347,9 @@ def serve(sock):
             host.jobs.pop(msg[1], None)
             for r in runtime.drop_held(msg[1]) if hasattr(runtime, "drop_held") else ():
                 host._finish(r, P.KILLED, "job purged", wake=False)
+        elif typ == "close_gate":
+            if hasattr(runtime, "close_gate"):
+                runtime.close_gate(msg[1])
         elif typ == "probe":
             reason = runtime.probe(msg[1]) if hasattr(runtime, "probe") else None
             send_msg(sock, ("probe", msg[1], reason), host.send_lock)

@@ -180,6 +180,7 @@ class JobInProgress:
     def __init__(self, jt, job_id: JobID, conf):
         self.jt = jt
         self.fold_lock = threading.RLock()   # counters() holds it around fold_counters
+        self.acc_lock = threading.Lock()     # loc_counts / pending_counters writers + swap
         self.job_id = job_id
         self.conf = conf
         self.status = JobStatus(job_id, PREP)
@@ -312,16 +313,23 @@ class JobInProgress:
         with self.fold_lock:
             return self._fold_counters_locked()
 
+    def add_counters(self, d):
+        """A succeeded attempt's counters, folded lazily (fold_counters)."""
+        with self.acc_lock:
+            self.pending_counters.append(d)
+
     def _fold_counters_locked(self) -> Counters:
-        lc = self.loc_counts
+        # swap both accumulators under acc_lock (the lock their writers take),
+        # merge outside it: no increment or append can land in a swapped-out one
+        with self.acc_lock:
+            lc, self.loc_counts = self.loc_counts, [0, 0, 0]
+            pend, self.pending_counters = self.pending_counters, []
         if any(lc):
             hbm, data, rack = lc
-            self.loc_counts = [0, 0, 0]
             for name, v in (("HBM_LOCAL_MAPS", hbm), ("DATA_LOCAL_MAPS", data),
                             ("RACK_LOCAL_MAPS", rack)):
                 if v:
                     self.counters.incr(C.JOB_GROUP, name, v)
-        pend, self.pending_counters = self.pending_counters, []
         for d in pend:
             if d:
                 self.counters.incr_all(Counters.from_dict(d))
@@ -411,13 +419,14 @@ class JobInProgress:
     def _count_locality(self, level):
         # JobInProgress.Counter DATA_LOCAL_MAPS / RACK_LOCAL_MAPS (+ hbmr's
         # HBM-resident level): plain ints, folded into the counters on read
-        lc = self.loc_counts
-        if level == 0:
-            lc[0] += 1
-        if level <= 2:
-            lc[1] += 1
-        elif level == 3:
-            lc[2] += 1
+        with self.acc_lock:
+            lc = self.loc_counts
+            if level == 0:
+                lc[0] += 1
+            if level <= 2:
+                lc[1] += 1
+            elif level == 3:
+                lc[2] += 1
 
     def _take(self, tip):
         del self.pending_maps[tip]
@@ -1087,7 +1096,11 @@ class JobTracker:
             if st.gpu_worker_lost:
                 self._restart_gpu_gang(tr)
             if tr.extra_actions:
-                actions += tr.extra_actions
+                # a closed gate goes before this response's launches: a staged
+                # map launched here must not pass the gate of a restarted job
+                pre = [x for x in tr.extra_actions if x["type"] == "close_gate"]
+                actions = pre + actions + [x for x in tr.extra_actions
+                                           if x["type"] != "close_gate"]
                 tr.extra_actions = []
         return {"actions": actions, "interval": self.heartbeat_interval, "more": tr.more}
 
@@ -1172,7 +1185,7 @@ class JobTracker:
             jip.maps_done += 1
         else:
             jip.reduces_done += 1
-        jip.pending_counters.append(a.counters)   # folded lazily (fold_counters)
+        jip.add_counters(a.counters)
         if not tip.is_map and isinstance(a.output, dict) and a.output.get("result") is not None:
             if jip.result is None:
                 jip.result = {}
@@ -1277,7 +1290,7 @@ class JobTracker:
             done_ids = [a.aid for a in done]
             self.cost_model.tasks_finished(jip.signature, done_ids, True, dt)
             if rep.get("counters"):
-                jip.pending_counters.append(rep["counters"])
+                jip.add_counters(rep["counters"])
             self.history.log("TASKS_FINISHED", attempts=done_ids, tracker=tr.name,
                              gpu=True, device=done[0].device, finish=fin, device_time=dt)
             METRICS.inc("hbmr_tasks_succeeded_total", n, help="successful task attempts",
@@ -1311,13 +1324,29 @@ class JobTracker:
                 t.extra_actions.append(P.restart_gpu_worker_action(g))
         self._kick()
 
-    def _restart_collective(self, jip: JobInProgress, diag):
+    def _restart_collective(self, jip: JobInProgress, diag, kill_maps=False):
         """Re-run a split job's collective reduce gang: kill the running members,
         forget finished ones and re-execute the maps (their outputs were consumed
-        by finished members or died with a worker)."""
+        by finished members or died with a worker).
+
+        Jobs staged on this one (``_maybe_stage``) may already have run maps on
+        the failed gang's result — its reduce opens their gates as soon as it has
+        enqueued that result, before it finishes: they restart too, their held
+        or running map attempts killed (``kill_maps``), and every GPU tracker
+        closes this job's gate, so the re-launched maps wait for the new reduce."""
         self.history.log("COLLECTIVE_RESTART", job=str(jip.job_id), diag=diag[:500])
         jip.expect_mode = False
         jip.pending_finish = False
+        if kill_maps:
+            for tip in jip.maps:
+                for a in tip.running_attempts():
+                    a.state = P.KILLED
+                    self._release(a)
+                    t = self.trackers.get(a.tracker)
+                    if t is not None:
+                        t.kills.add(a.aid)
+                if tip.successful is None:
+                    jip.add_pending(tip)
         for r in jip.reduces:
             for a in r.running_attempts():
                 a.state = P.KILLED
@@ -1343,6 +1372,15 @@ class JobTracker:
             jip.add_pending(tip)
         jip.t_maps_done = 0.0
         self._update_progress(jip)
+        jid = str(jip.job_id)
+        staged = [w for w in self.staged if w.staged_on == jid and not w.completed()]
+        if staged or kill_maps:
+            for t in self.trackers.values():
+                if t.status.gpus:
+                    t.extra_actions.append(P.close_gate_action(jid))
+        for w in staged:
+            self.history.log("STAGED_JOB_RESTART", job=str(w.job_id), gate=jid)
+            self._restart_collective(w, f"job {jid} it is staged on restarted", kill_maps=True)
         self._kick()
 
     def preempt_attempt(self, a: Attempt, why="preempted"):

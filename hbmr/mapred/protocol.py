@@ -170,6 +170,12 @@ def restart_gpu_worker_action(generation: int):
     return {"type": "restart_gpu_worker", "generation": generation}
 
 
+def close_gate_action(job_id: str):
+    """Job ``job_id``'s collective reduce restarts: forget its opened gate, so
+    re-launched staged maps wait for the new reduce (hbmr/gpu/gates.py)."""
+    return {"type": "close_gate", "job_id": job_id}
+
+
 def reinit_action():
     return {"type": "reinit"}
 

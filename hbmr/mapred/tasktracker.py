@@ -577,6 +577,9 @@ class TaskTracker:
                     r.task.kill_event.set()
                 if getattr(self.gpu_runtime, "remote", False):
                     self.gpu_runtime.kill(act["attempt_id"])
+        elif typ == "close_gate":
+            if self.gpu_runtime is not None and hasattr(self.gpu_runtime, "close_gate"):
+                self.gpu_runtime.close_gate(act["job_id"])
         elif typ == "restart_gpu_worker":
             if getattr(self.gpu_runtime, "remote", False):
                 self.gpu_runtime.restart(act["generation"])

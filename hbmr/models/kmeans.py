@@ -776,6 +776,19 @@ class KMeansSplitJob(SplitJob):
             TRACE.instant("kmeans.reduce_return")
         return res
 
+    def poison_result(self, ctx):
+        """Fault injection (hbmr.faultinject.reduce.fail.after.release.attempt):
+        publish wrong centroids under this job's output key, as a gang that dies
+        mid-update would, before the staged maps are released on them."""
+        with STORE.lock:
+            host = STORE.host.get(self.cout)
+            if host is not None:
+                STORE.host[self.cout] = host + 1.0
+            for key, img in list(STORE.images.items()):
+                if key[0] == self.cout:
+                    STORE.images.pop(key)
+                    STORE.host[self.cout] = img.cen.detach().to("cpu")[:, :self.d] + 1.0
+
     def _write_output(self, ctx, counts, new_cen):
         out = self.conf.get("mapred.output.dir")
         if not out:

@@ -273,8 +273,12 @@ class TeraSortSplitJob(SplitJob):
                 stats = self._reduce_local(ctx, outs, combined["offsets"], nparts or 1, dev)
             else:
                 stats = self._reduce_shuffle(ctx, outs, combined["offsets"], nparts, dev)
-        finally:
-            self._close_output(ctx)
+        except BaseException:
+            # a failed or killed attempt: its partial part files never reach the
+            # output directory (FileOutputCommitter.abortTask)
+            self._close_output(ctx, commit=False)
+            raise
+        self._close_output(ctx, commit=True)
         # one device->host copy of this rank's statistics (no per-value syncs)
         n, st = stats
         if not torch.is_tensor(csum_in):
@@ -623,14 +627,22 @@ class TeraSortSplitJob(SplitJob):
         _com, _att, workdir, pw = ctx.tera_out
         pw.write(os.path.join(workdir, f"part-{p:05d}"), recs)
 
-    def _close_output(self, ctx):
+    def _close_output(self, ctx, commit=True):
+        """Close the part writer; commit the attempt's work directory only on
+        success, else abort it (rmtree of the work path)."""
         out = getattr(ctx, "tera_out", None)
         if out is None:
             return
         ctx.tera_out = None
         com, attempt, _wd, pw = out
-        pw.close()
-        if com.needs_task_commit(self.conf, attempt):
+        try:
+            pw.close()
+        except BaseException:
+            com.abort_task(self.conf, attempt)
+            raise
+        if not commit:
+            com.abort_task(self.conf, attempt)
+        elif com.needs_task_commit(self.conf, attempt):
             com.commit_task(self.conf, attempt)
 
     def job_succeeded(self, jip):
@@ -666,13 +678,22 @@ class _PartWriter:
             self.pending[i].result()
             self.pending[i] = None
 
+    def _finish_file(self, f):
+        f.flush()
+        if self.sync:
+            os.fsync(f.fileno())
+        f.close()
+
     def write(self, path, recs):
+        """Queue one part file; the writer thread closes (and syncs) it after
+        its last chunk, so at most the files in flight are open at once (a rank
+        may own thousands of partitions)."""
         os.makedirs(os.path.dirname(path), exist_ok=True)
         f = open(path, "wb")
-        self.files.append(f)
         flat = recs.reshape(-1)
         if not self.cuda or not flat.is_cuda:
-            self.pool.submit(lambda a=flat.numpy().copy(): a.tofile(f)).result()
+            a = flat.numpy().copy()
+            self.files.append(self.pool.submit(lambda: (a.tofile(f), self._finish_file(f))))
             return
         self.stream.wait_stream(torch.cuda.current_stream(flat.device))
         flat.record_stream(self.stream)
@@ -691,20 +712,18 @@ class _PartWriter:
                 ev.synchronize()
                 f.write(memoryview(view.numpy()))
             self.pending[i] = self.pool.submit(put)
+        # FIFO writer thread: runs after this file's last chunk
+        self.files.append(self.pool.submit(self._finish_file, f))
 
     def close(self):
         for i in range(2):
             self._wait(i)
-
-        def fin():
-            for f in self.files:
-                f.flush()
-                if self.sync:
-                    os.fsync(f.fileno())
-                f.close()
-        self.pool.submit(fin).result()
-        self.pool.shutdown()
-        self.files = []
+        try:
+            for fut in self.files:
+                fut.result()
+        finally:
+            self.pool.shutdown()
+            self.files = []
 
 
 def terasort_conf(base=None, rows=1_000_000, split_rows=None, output=None, inp=None,

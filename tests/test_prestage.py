@@ -111,3 +111,19 @@ def test_staged_maps_do_not_take_the_queue_their_gate_waits_on(worker, tmp_path)
     got, jobs, events, _ = _run(conf, tmp_path / "staged", steps=4)
     assert torch.equal(got, want)
     assert sum(e["event"] == "JOB_STAGED" for e in events) >= 2
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("worker", [False, True])
+def test_predecessor_reduce_failing_after_release_restarts_its_staged_job(worker, tmp_path):
+    """Iteration 2's reduce opens the gate of staged iteration 3 on poisoned
+    centroids and then FAILS: iteration 2 re-runs its gang, iteration 3's maps
+    that ran on the poisoned result re-run behind the new gate, and the
+    answer equals the unstaged run's."""
+    want, _, _, _ = _run(_conf(worker, prestage=False), tmp_path / "plain", steps=4)
+    conf = _conf(worker, **{"hbmr.faultinject.reduce.fail.after.release.attempt":
+                            "_0002_r_000000_0"})
+    got, jobs, events, _ = _run(conf, tmp_path / "late", steps=4)
+    names = [e["event"] for e in events]
+    assert "COLLECTIVE_RESTART" in names
+    assert torch.equal(got, want)
