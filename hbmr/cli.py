@@ -4,6 +4,7 @@ jar/pipes/job/fs/version/... dispatch).
   hbmr examples <program> [args]      example programs (ExampleDriver)
   hbmr pipes -input I -output O -cpubin C -gpubin G ...
   hbmr streaming -input I -output O -mapper CMD -reducer CMD ...
+  hbmr dumptb PATH | hbmr loadtb PATH   typed bytes out of / into SequenceFiles
   hbmr job -jt host:port -list [all] | -status ID | -kill ID | -counter ID GROUP NAME
            | -tasks ID map|reduce | -history FILE
   hbmr fs -ls|-lsr|-cat|-text|-put|-get|-cp|-mv|-rm|-rmr|-mkdir|-du|-count [-q]|-setrep PATH...
@@ -396,6 +397,9 @@ def main(argv=None):
     if cmd == "streaming":
         from . import streaming
         return streaming.main(rest)
+    if cmd in ("dumptb", "loadtb"):
+        from .streaming import dumptb
+        return (dumptb.dump_main if cmd == "dumptb" else dumptb.load_main)(rest)
     if cmd == "job":
         return _job(rest)
     if cmd in ("fs", "dfs"):

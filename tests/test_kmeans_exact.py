@@ -88,13 +88,25 @@ def test_top3_assign_matches_fp32_reference(dtype):
     # the accumulation-order / packing tolerance (ties may swap indices)
     picked = s.gather(1, got)
     tol = 1e-3 * top.values[:, :1].abs().clamp(min=1)
-    assert ((picked - top.values).abs() <= tol).all(1).float().mean().item() > 0.9999
+    # the default epilogue keeps the top two of 16 tracks (cluster bits 0-3):
+    # when the best and the second share a track the third is not known and
+    # the kernel reports t = b with a zero margin (certification step 2 then
+    # defers the point to the neighbour scan)
+    same = got[:, 2] == got[:, 0]
+    assert ((got[same, 0] ^ got[same, 1]) & 15 == 0).all()
+    assert (mg[n:][same] == 0).all()
+    assert same.float().mean().item() < 0.15
+    cols = torch.ones_like(got, dtype=torch.bool)
+    cols[same, 2] = False
+    ok = ((picked - top.values).abs() <= tol) | ~cols
+    assert ok.all(1).float().mean().item() > 0.9999
     # (the packed arg-max truncates 4 + log2(k/32) mantissa bits: near-equal
     # scores may swap, which the score check above already bounds)
-    assert (got == top.indices).all(1).float().mean().item() > 0.995
+    assert ((got == top.indices) | ~cols).all(1).float().mean().item() > 0.995
     ref_m = top.values[:, :1] - top.values[:, 1:]
     got_m = torch.stack([mg[:n], mg[n:]], 1)
-    assert ((got_m - ref_m).abs() <= tol + 1e-2).all(1).float().mean().item() > 0.999
+    okm = ((got_m - ref_m).abs() <= tol + 1e-2) | ~cols[:, 1:]
+    assert okm.all(1).float().mean().item() > 0.999
     if dt == torch.bfloat16:
         assert torch.equal(lab, km.assign(sp.xb, img))   # same winner as the plain kernel
 
