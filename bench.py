@@ -206,9 +206,19 @@ def main():
         def _avg(key):
             v = [t[key] for t in tls if t.get(key) is not None]
             return round(1e3 * sum(v) / len(v), 3) if v else None
-        phases_ms = {"submit_to_first_map": _avg("first_map"), "submit_to_maps_done": _avg(
-            "maps_done"), "submit_to_first_reduce": _avg("first_reduce"),
-            "submit_to_finish": _avg("finish")}
+        # phases from the job's release (its predecessor's finish, when the
+        # JobTracker lets a dependent job complete; its submission otherwise).
+        # Pre-staged maps and early collective reduces are launched BEFORE the
+        # release: reported as how far ahead they went, never as a negative time
+        lead = lambda v: None if v is None else round(max(0.0, -v), 3)  # noqa: E731
+        phases_ms = {"release_to_maps_done": _avg("maps_done"),
+                     "release_to_finish": _avg("finish"),
+                     "maps_launched_ahead_of_release": lead(_avg("first_map")),
+                     "reduce_launched_ahead_of_release": lead(_avg("first_reduce"))}
+        gk = [h["counters"].get("hbmr.GpuCounters", "GPU_KERNEL_US") for h in hist]
+        # device time of the map kernels per job, de-overlapped across the
+        # slot streams (hbmr.gpu.runtime._busy_ms), summed over the GPUs
+        map_device_ms = round(sum(gk) / len(gk) / 1e3, 3) if gk else None
         splits = -(-a.points // a.split_points)
         value = splits * a.steps / dt
         cm = node.jt.cost_model.snapshot()
@@ -240,6 +250,7 @@ def main():
                        "combiner": conf.get("hbmr.kmeans.combiner") or "delta"},
             "job_makespan_ms": round(ms, 3),
             "phases_ms": phases_ms,
+            "map_device_ms_per_job": map_device_ms,
             "points_per_sec": round(a.points * a.steps / dt, 1),
             "maps_launched": n_maps, "gpu_maps": gpu_maps, "cpu_maps": cpu_maps,
             "warmup_seconds": round(t_warm, 2),

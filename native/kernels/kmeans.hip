@@ -197,8 +197,64 @@ struct PackedTop3 : PackedArgMax {
   }
 };
 
+// Packed running TOP-2 per TRACK (exact mode default): the 16 accumulator
+// registers of a lane form 8 tracks (register r -> track r & 7), each keeping
+// its best two: s = med3(b, s, u), b = max(b, u) — 2 VALU ops per score (+ the
+// and_or that packs the code) instead of PackedTop3's 3.  With K = 128 one
+// 32x32 output tile is 8 MFMAs (256 MFMA cycles per SIMD, 64 of them blocking
+// vector issue): the top-3 epilogue's 4 issue slots per score did not fit the
+// remaining 192 cycles (top-3 assign ran 20 % behind the plain arg-max), 3 do.
+// Together with the lane half h, a cluster's track is its index bits 0-3
+// (cluster = tile*32 + (r&3) + 8(r>>2) + 4h).  The top 3 of a point are the
+// top 3 of the 32 track candidates; every cluster that is not a candidate
+// scores <= its track's second, which is <= the third — unless the best and
+// the second share a track, which finish_point flags (t = b, margin 0: step 2
+// of the certification then defers the point to the neighbour scan).
+struct PackedTop2x8 : PackedArgMax {
+  float tb[8], ts[8];
+  __device__ __forceinline__ void init(int ntiles) {
+    PackedArgMax::init(ntiles);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) tb[i] = ts[i] = -3.0e38f;
+  }
+  __device__ __forceinline__ void update(const f32x16& acc, int tt) {
+    const uint32_t base = top - ((uint32_t)tt << 4);
+    uint32_t code[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      code[r] = base | (15u - r);
+      asm("" : "+s"(code[r]));
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float u = __uint_as_float((__float_as_uint(acc[r]) & vmask) | code[r]);
+      ts[r & 7] = vmed3(tb[r & 7], ts[r & 7], u);
+      tb[r & 7] = vmax3(tb[r & 7], u, u);
+    }
+  }
+  __device__ __forceinline__ void top3(float& b, float& s, float& t) const {
+    b = s = t = -3.0e38f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      PackedTop3::insert(b, s, t, tb[i]);
+      PackedTop3::insert(b, s, t, ts[i]);
+    }
+  }
+  static constexpr bool kTracks = true;
+};
+
+template <class AM, class = void> struct HasTracks { static constexpr bool value = false; };
+template <class AM> struct HasTracks<AM, std::void_t<decltype(AM::kTracks)>> {
+  static constexpr bool value = AM::kTracks;
+};
+
+#ifndef HBMR_EXACT_TOP3
+#define HBMR_EXACT_TOP3 0   // 1: the full running top-3 (PackedTop3)
+#endif
 template <bool EXACT>
-using ArgMaxT = typename std::conditional<EXACT, PackedTop3, PackedArgMax>::type;
+using ArgMaxT = typename std::conditional<
+    EXACT, typename std::conditional<HBMR_EXACT_TOP3 != 0, PackedTop3, PackedTop2x8>::type,
+    PackedArgMax>::type;
 
 // (score, cluster) insertion into a sorted triple; ties to the lower cluster
 __device__ __forceinline__ void insert3(float (&v)[3], int (&c)[3], float u, int cu) {
@@ -253,6 +309,13 @@ __device__ __forceinline__ void finish_point(const AM& am, int h, long p, long n
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) insert3(v, c, ov[i], oc[i]);
+    if constexpr (HasTracks<AM>::value) {
+      // best and second in one track: the rest is bounded only by the second
+      if (((c[0] ^ c[1]) & 15) == 0) {
+        v[2] = v[0];
+        c[2] = c[0];
+      }
+    }
     if (h == 0 && p < n) {
       labels[p] = c[0];
       cand[p] = c[1];
@@ -453,7 +516,7 @@ __device__ __forceinline__ void read_tile32(const char* buf, int col, int h, bf1
   }
 }
 
-template <int D, int PB, bool EXACT = false, bool F16 = false>
+template <int D, int PB, bool EXACT = false, bool F16 = false, bool TOP3 = false>
 __device__ __forceinline__ void assign_tile_v2(const __bf16* __restrict__ X, long n,
                                                const __bf16* __restrict__ C,
                                                const float* __restrict__ chalf, int ntiles,
@@ -484,7 +547,8 @@ __device__ __forceinline__ void assign_tile_v2(const __bf16* __restrict__ X, lon
 #pragma unroll
     for (int s = 0; s < KS; ++s) bfrag[pb][s] = __builtin_bit_cast(bf16x8, row[2 * s + h]);
   }
-  ArgMaxT<EXACT> am[PB];
+  typename std::conditional<EXACT, typename std::conditional<TOP3, PackedTop3, PackedTop2x8>::type,
+                            PackedArgMax>::type am[PB];
 #pragma unroll
   for (int pb = 0; pb < PB; ++pb) am[pb].init(ntiles);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -578,14 +642,15 @@ __global__ __launch_bounds__(kThreads, 2) void kmeans_assign_top3_kernel(
                             hbmr_xcd_remap(blockIdx.x, gridDim.x), smem, cand, margin);
 }
 
-template <int D, int PB, bool F16>
+template <int D, int PB, bool F16, bool TOP3 = false>
 __global__ __launch_bounds__(AssignV2<D>::THREADS, AssignV2<D>::MINB) void kmeans_assign_top3_v2_kernel(
     const __bf16* __restrict__ X, long n, const __bf16* __restrict__ C,
     const float* __restrict__ chalf, int ntiles, int32_t* __restrict__ labels,
     int32_t* __restrict__ cand, float* __restrict__ scores, float* __restrict__ margin) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  assign_tile_v2<D, PB, true, F16>(X, n, C, chalf, ntiles, labels, scores,
-                                   hbmr_xcd_remap(blockIdx.x, gridDim.x), smem, cand, margin);
+  assign_tile_v2<D, PB, true, F16, TOP3>(X, n, C, chalf, ntiles, labels, scores,
+                                         hbmr_xcd_remap(blockIdx.x, gridDim.x), smem, cand,
+                                         margin);
 }
 
 // 1 = the chunked kernel above, 2 = the pipelined v2 (D ≤ 128); HBMR_KMEANS_ASSIGN
@@ -1849,18 +1914,19 @@ __device__ __forceinline__ double row_sum16(double v) {
 template <int NM>
 __device__ __forceinline__ void load_row8(const float* __restrict__ r, int d, int sub,
                                           float (&v)[8 * NM]) {
-  // branch-free (see load_row16): clamped address + select, no per-load wait
+  // branch-free (see load_row16): clamped address + select, no per-load wait.
+  // Lane sub of the 16-lane group owns features 128m + 64h + 4sub + (0..3):
+  // each float4 load of the group reads 256 contiguous bytes of the row
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
-    const int b = 8 * sub + 8 * kRefineGroup * m;
-    const bool ok = b < d;
-    const float* src = r + (ok ? b : 0);
-    const float4 a = *reinterpret_cast<const float4*>(src);
-    const float4 c = *reinterpret_cast<const float4*>(src + 4);
-    v[8 * m + 0] = ok ? a.x : 0.f; v[8 * m + 1] = ok ? a.y : 0.f;
-    v[8 * m + 2] = ok ? a.z : 0.f; v[8 * m + 3] = ok ? a.w : 0.f;
-    v[8 * m + 4] = ok ? c.x : 0.f; v[8 * m + 5] = ok ? c.y : 0.f;
-    v[8 * m + 6] = ok ? c.z : 0.f; v[8 * m + 7] = ok ? c.w : 0.f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int b = 128 * m + 64 * h + 4 * sub;
+      const bool ok = b < d;
+      const float4 a = *reinterpret_cast<const float4*>(r + (ok ? b : 0));
+      float* o = v + 8 * m + 4 * h;
+      o[0] = ok ? a.x : 0.f; o[1] = ok ? a.y : 0.f; o[2] = ok ? a.z : 0.f; o[3] = ok ? a.w : 0.f;
+    }
   }
 }
 
@@ -2174,6 +2240,12 @@ constexpr int kQ1Per = 4;            // points per thread in the step-1 scan
 constexpr int kQ2Lanes = 8;          // lanes per Q1 entry in step 2
 constexpr int kQ2Per = HBMR_WAVE / kQ2Lanes;
 constexpr int kRefineGrid = 2048;    // persistent grid of q2 (q3: a quarter)
+// workspace header: Q1 / Q2 shard counts (8 + 8 u32) and the sharded stats
+// (8 shards x 4 u64 at kStatsOff): one word per stat took every block's
+// atomic at the kernels' tails; kmeans_refine_stats_kernel folds them
+constexpr int kStatsOff = 64;
+constexpr int kRefineHdr = 512;
+constexpr int kHdrClear = kStatsOff + kQShards * 4 * 8;
 
 struct RefineTable {                 // the batch's splits, by value
   int nsplit;
@@ -2199,7 +2271,7 @@ inline RefineLayout refine_layout(int nsplit, const long* ns) {
   L.g2 = (unsigned)std::max<long>(1, std::min<long>(kRefineGrid, ceil_div(total, 4 * kQ2Per)));
   const long per_iter = (long)L.g2 * 4 * kQ2Per;           // Q1 entries per grid iteration
   L.cap2 = ceil_div(L.g2, kQShards) * 4 * kQ2Per * std::max<long>(1, ceil_div(total, per_iter));
-  L.off1 = 256;
+  L.off1 = kRefineHdr;
   L.off2 = L.off1 + ((kQShards * (size_t)L.cap1 * sizeof(ExactQ1) + 255) & ~(size_t)255);
   L.bytes = L.off2 + kQShards * (size_t)L.cap2 * sizeof(ExactQ2);
   return L;
@@ -2298,7 +2370,7 @@ __global__ __launch_bounds__(256) void kmeans_refine_q1_kernel(
         tot += c;
       }
     base_s = tot ? atomicAdd(qcount + shard, tot) : 0u;
-    if (tot) atomicAdd(stats, (unsigned long long)tot);
+    if (tot) atomicAdd(stats + 4 * shard, (unsigned long long)tot);
   }
   __syncthreads();
   ExactQ1* out = q1 + (long)shard * cap1 + base_s;
@@ -2307,7 +2379,9 @@ __global__ __launch_bounds__(256) void kmeans_refine_q1_kernel(
     if (flag[i]) out[wcnt[wave][i] + rank[i]] = e[i];
 }
 
-// 16 consecutive features 16*sub + 128*m (+0..15) of a row (0 past d; d % 8 == 0)
+// 16 features of a row per lane of an 8-lane group: 128m + 32h + 4sub + (0..3)
+// (0 past d; d % 4 == 0): each float4 load of the group reads 128 contiguous
+// bytes of the row
 template <int NM>
 __device__ __forceinline__ void load_row16(const float* __restrict__ r, int d, int sub,
                                            float (&v)[16 * NM]) {
@@ -2317,15 +2391,12 @@ __device__ __forceinline__ void load_row16(const float* __restrict__ r, int d, i
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int b = 16 * sub + 128 * m + 8 * h;
+    for (int h = 0; h < 4; ++h) {
+      const int b = 128 * m + 32 * h + 4 * sub;
       const bool ok = b < d;
-      const float* src = r + (ok ? b : 0);
-      const float4 a = *reinterpret_cast<const float4*>(src);
-      const float4 c = *reinterpret_cast<const float4*>(src + 4);
-      float* o = v + 16 * m + 8 * h;
+      const float4 a = *reinterpret_cast<const float4*>(r + (ok ? b : 0));
+      float* o = v + 16 * m + 4 * h;
       o[0] = ok ? a.x : 0.f; o[1] = ok ? a.y : 0.f; o[2] = ok ? a.z : 0.f; o[3] = ok ? a.w : 0.f;
-      o[4] = ok ? c.x : 0.f; o[5] = ok ? c.y : 0.f; o[6] = ok ? c.z : 0.f; o[7] = ok ? c.w : 0.f;
     }
   }
 }
@@ -2343,11 +2414,21 @@ __global__ __launch_bounds__(256) void kmeans_refine_q2_kernel(
     const float* __restrict__ cmax, const float* __restrict__ cerrmax, double pack_rel,
     const uint32_t* __restrict__ qcount, const ExactQ1* __restrict__ q1, long cap1,
     uint32_t* __restrict__ q2count, ExactQ2* __restrict__ q2, long cap2,
-    unsigned long long* __restrict__ stats) {
-  const int tid = threadIdx.x, lane = tid & 63;
+    unsigned long long* __restrict__ sstats) {
+  // Q2 entries are staged in LDS and written out with ONE global atomic per
+  // block (at the end, or when the buffer nears full): an atomic-with-return
+  // per wave and round on the 8 shard counters, whose latency every spilling
+  // wave waited out, was half of this kernel's time (diagnostic variant
+  // without it: refine 1.71 -> 0.82 ms per 12.5M points)
+  constexpr uint32_t kPerBlk = 4 * kQ2Per;        // entries per block round
+  constexpr uint32_t kBuf = 256;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int grp = lane / kQ2Lanes, sub = lane % kQ2Lanes;
+  __shared__ ExactQ2 sbuf[kBuf];
+  __shared__ uint32_t sn, sbase;
   __shared__ unsigned long long cnt[2];
   if (tid < 2) cnt[tid] = 0;
+  if (tid == 0) sn = 0;
   __syncthreads();
   const double inflate = 1.0 + 0x1p-20;
   const double gam = (double)(d + 2) * 0x1p-23 * 1.01;
@@ -2361,16 +2442,29 @@ __global__ __launch_bounds__(256) void kmeans_refine_q2_kernel(
     total += c1[j];
   }
   const int shard = blockIdx.x % kQShards;
-  const uint32_t stride = gridDim.x * 4 * kQ2Per;
-  uint32_t base = (blockIdx.x * 4 + (tid >> 6)) * kQ2Per;
+  const uint32_t stride = gridDim.x * kPerBlk;
+  const uint32_t off = wave * kQ2Per + grp;
+  auto flush = [&]() {            // block-uniform call sites only
+    if (tid == 0) {
+      sbase = atomicAdd(q2count + shard, sn);
+      cnt[1] += sn;
+    }
+    __syncthreads();
+    const uint32_t m = sn;
+    for (uint32_t i = tid; i < m; i += 256) q2[(long)shard * cap2 + sbase + i] = sbuf[i];
+    __syncthreads();
+    if (tid == 0) sn = 0;
+    __syncthreads();
+  };
+  uint32_t bb = blockIdx.x * kPerBlk;
   ExactQ1 e;
-  if (base < total) e = q1[shard_slot(c1, cap1, min(base + grp, total - 1))];
-  for (; base < total; base += stride) {
+  if (bb < total) e = q1[shard_slot(c1, cap1, min(bb + off, total - 1))];
+  for (; bb < total; bb += stride) {             // same trip count in every wave
     const ExactQ1 q = e;
-    const bool have = base + grp < total;
+    const bool have = bb + off < total;
     // prefetch the next round's entry while this round's rows are in flight
-    const uint32_t nb = base + stride;
-    if (nb < total) e = q1[shard_slot(c1, cap1, min(nb + grp, total - 1))];
+    const uint32_t nb = bb + stride;
+    if (nb < total) e = q1[shard_slot(c1, cap1, min(nb + off, total - 1))];
     const bool t_real = q.t < k;
     const float* xr = tbl.x32[q.split] + (size_t)q.row * ldx;
     float xf[16 * NM], c0[16 * NM], c1r[16 * NM], c2[16 * NM];
@@ -2406,12 +2500,11 @@ __global__ __launch_bounds__(256) void kmeans_refine_q2_kernel(
       tbl.labels[q.split][q.row] = w;
       atomicAdd(&cnt[0], 1ull);
     }
-    // one sharded atomic per wave and round for its Q2 entries
     const bool spill = have && sub == 0 && !certified;
     const unsigned long long m = __ballot(spill);
     if (m) {
       uint32_t b2 = 0;
-      if (lane == 0) b2 = atomicAdd(q2count + shard, (uint32_t)__popcll(m));
+      if (lane == 0) b2 = atomicAdd(&sn, (uint32_t)__popcll(m));    // LDS
       b2 = __shfl(b2, 0);
       if (spill) {
         ExactQ2 o;
@@ -2420,14 +2513,15 @@ __global__ __launch_bounds__(256) void kmeans_refine_q2_kernel(
         o.w = w;
         o.pad = 0;
         o.dw = dw;
-        q2[(long)shard * cap2 + b2 + lane_rank(m)] = o;
-        atomicAdd(&cnt[1], 1ull);
+        sbuf[b2 + lane_rank(m)] = o;
       }
     }
+    __syncthreads();
+    if (sn > kBuf - kPerBlk) flush();
   }
   __syncthreads();
-  if (tid == 0 && cnt[0]) atomicAdd(stats + 1, cnt[0]);
-  if (tid == 1 && cnt[1]) atomicAdd(stats + 2, cnt[1]);
+  if (sn) flush();
+  if (tid < 2 && cnt[tid]) atomicAdd(sstats + 4 * shard + 1 + tid, cnt[tid]);
 }
 
 template <int NM>
@@ -2435,7 +2529,7 @@ __global__ __launch_bounds__(256) void kmeans_refine_q3_kernel(
     const RefineTable tbl, int d, int ldx, const float* __restrict__ C32, int k,
     const int32_t* __restrict__ nbr_idx, const float* __restrict__ nbr_dist, int L,
     const uint32_t* __restrict__ q2count, const ExactQ2* __restrict__ q2, long cap2,
-    unsigned long long* __restrict__ stats, int nstats) {
+    unsigned long long* __restrict__ sstats, int nstats) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int grp = lane / kRefineGroup, sub = lane % kRefineGroup;
   __shared__ unsigned long long cnt[3];
@@ -2514,8 +2608,27 @@ __global__ __launch_bounds__(256) void kmeans_refine_q3_kernel(
     }
   }
   __syncthreads();
-  if (tid == 0 && cnt[0]) atomicAdd(stats + 1, cnt[0]);
-  if (nstats >= 5 && tid >= 1 && tid < 3 && cnt[tid]) atomicAdd(stats + 2 + tid, cnt[tid]);
+  // sharded stats (kmeans_refine_stats_kernel folds them): word 1 of a shard
+  // counts relabels; word 3 counts the scan's neighbour distances in shards
+  // 0-3 and its full scans in shards 4-7
+  const int sh = blockIdx.x % (kQShards / 2);
+  if (tid == 0 && cnt[0]) atomicAdd(sstats + 4 * sh + 1, cnt[0]);
+  if (tid == 1 && cnt[1]) atomicAdd(sstats + 4 * sh + 3, cnt[1]);
+  if (tid == 2 && cnt[2]) atomicAdd(sstats + 4 * (sh + kQShards / 2) + 3, cnt[2]);
+}
+
+// stats[0..2] (+3, 4 when nstats >= 5) += the shards of a refine batch
+__global__ void kmeans_refine_stats_kernel(const unsigned long long* __restrict__ ss,
+                                           unsigned long long* __restrict__ stats, int nstats) {
+  const int t = threadIdx.x;
+  if (t >= 5 || (t >= 3 && nstats < 5)) return;
+  unsigned long long v = 0;
+  if (t < 3) {
+    for (int j = 0; j < kQShards; ++j) v += ss[4 * j + t];
+  } else {
+    for (int j = 0; j < kQShards / 2; ++j) v += ss[4 * (j + (t - 3) * (kQShards / 2)) + 3];
+  }
+  if (v) stats[t] += v;
 }
 
 int refine_version() {
@@ -2538,7 +2651,14 @@ int launch_assign_top3(const void* X, long n, const void* C, const float* chalf,
       const int pts = AssignV2<D>::WAVES * 2 * 32;
       const long nblk = (n + pts - 1) / pts;
       if (nblk > 0x7fffffffL) return (int)hipErrorInvalidValue;
-      hipLaunchKernelGGL((kmeans_assign_top3_v2_kernel<D, 2, F16>), dim3((unsigned)nblk),
+      // HBMR_EXACT_EPI=top3: the full running top-3 epilogue (PackedTop3)
+      static const bool top3 = [] {
+        const char* e = getenv("HBMR_EXACT_EPI");
+        return e && strcmp(e, "top3") == 0;
+      }();
+      auto kern = top3 ? kmeans_assign_top3_v2_kernel<D, 2, F16, true>
+                       : kmeans_assign_top3_v2_kernel<D, 2, F16, false>;
+      hipLaunchKernelGGL(kern, dim3((unsigned)nblk),
                          dim3(AssignV2<D>::THREADS), AssignV2<D>::LDS_BYTES, st,
                          reinterpret_cast<const __bf16*>(X), n, reinterpret_cast<const __bf16*>(C),
                          chalf, k_pad / 32, labels, cand, scores, margin);
@@ -3102,7 +3222,7 @@ int hbmr_kmeans_refine_batch_q1(int nsplit, const long* ns, int s, int d, int k,
   if (ws_bytes < (long)Ly.bytes) return (int)hipErrorInvalidValue;
   char* w = static_cast<char*>(ws);
   uint32_t* c1 = reinterpret_cast<uint32_t*>(w);
-  if (reset) HBMR_RETURN_IF_ERROR(hipMemsetAsync(c1, 0, 2 * kQShards * sizeof(uint32_t), st));
+  if (reset) HBMR_RETURN_IF_ERROR(hipMemsetAsync(c1, 0, kHdrClear, st));
   const long n = ns[s];
   if (n == 0) return 0;
   int tb = 0;
@@ -3111,7 +3231,8 @@ int hbmr_kmeans_refine_batch_q1(int nsplit, const long* ns, int s, int d, int k,
   const long b1 = ceil_div(n, 256 * kQ1Per);
   hipLaunchKernelGGL(kmeans_refine_q1_kernel, dim3((unsigned)b1), dim3(256), 0, st, n, s, d, k,
                      xnorm, xbn2, xerr, cnorm, cmax, cerr, cerrmax, pack_rel, labels, cand,
-                     scores, margin, c1, reinterpret_cast<ExactQ1*>(w + Ly.off1), Ly.cap1, stats);
+                     scores, margin, c1, reinterpret_cast<ExactQ1*>(w + Ly.off1), Ly.cap1,
+                     reinterpret_cast<unsigned long long*>(w + kStatsOff));
   return (int)hipGetLastError();
 }
 
@@ -3143,20 +3264,23 @@ int hbmr_kmeans_refine_batch_finish(int nsplit, const long* ns, const float* con
   uint32_t* c2 = c1 + kQShards;
   const ExactQ1* q1 = reinterpret_cast<const ExactQ1*>(w + Ly.off1);
   ExactQ2* q2 = reinterpret_cast<ExactQ2*>(w + Ly.off2);
+  unsigned long long* ss = reinterpret_cast<unsigned long long*>(w + kStatsOff);
   const unsigned g3 = std::max(1u, std::min(Ly.g2, (unsigned)(kRefineGrid / 4)));
   if (d <= 128) {
     hipLaunchKernelGGL(kmeans_refine_q2_kernel<1>, dim3(Ly.g2), dim3(256), 0, st, tbl, d, ldx,
-                       C32, k, cmax, cerrmax, pack_rel, c1, q1, Ly.cap1, c2, q2, Ly.cap2, stats);
+                       C32, k, cmax, cerrmax, pack_rel, c1, q1, Ly.cap1, c2, q2, Ly.cap2, ss);
     HBMR_RETURN_IF_ERROR(hipGetLastError());
     hipLaunchKernelGGL(kmeans_refine_q3_kernel<1>, dim3(g3), dim3(256), 0, st, tbl, d, ldx, C32,
-                       k, nbr_idx, nbr_dist, L, c2, q2, Ly.cap2, stats, nstats);
+                       k, nbr_idx, nbr_dist, L, c2, q2, Ly.cap2, ss, nstats);
   } else {
     hipLaunchKernelGGL(kmeans_refine_q2_kernel<2>, dim3(Ly.g2), dim3(256), 0, st, tbl, d, ldx,
-                       C32, k, cmax, cerrmax, pack_rel, c1, q1, Ly.cap1, c2, q2, Ly.cap2, stats);
+                       C32, k, cmax, cerrmax, pack_rel, c1, q1, Ly.cap1, c2, q2, Ly.cap2, ss);
     HBMR_RETURN_IF_ERROR(hipGetLastError());
     hipLaunchKernelGGL(kmeans_refine_q3_kernel<2>, dim3(g3), dim3(256), 0, st, tbl, d, ldx, C32,
-                       k, nbr_idx, nbr_dist, L, c2, q2, Ly.cap2, stats, nstats);
+                       k, nbr_idx, nbr_dist, L, c2, q2, Ly.cap2, ss, nstats);
   }
+  HBMR_RETURN_IF_ERROR(hipGetLastError());
+  hipLaunchKernelGGL(kmeans_refine_stats_kernel, dim3(1), dim3(64), 0, st, ss, stats, nstats);
   return (int)hipGetLastError();
 }
 
