@@ -293,7 +293,8 @@ class GpuRuntime:
                         else:
                             loader = (lambda s=sspec: sj.load_split(s, dev.torch_device))
                         data, hit = tracker.split_cache.get_or_load(
-                            sspec.key, dev.index, loader, sj.split_nbytes)
+                            sspec.key, dev.index, loader, sj.split_nbytes,
+                            cache=getattr(sj, "cache_inputs", True))
                     except BaseException as e:  # noqa: BLE001
                         tracker._finish(r, P.FAILED, f"{type(e).__name__}: {e}\n"
                                                      f"{traceback.format_exc()[-2000:]}")

@@ -197,7 +197,7 @@ class SimulatedGpuRuntime:
                     else:
                         data, hit = tracker.split_cache.get_or_load(
                             sspec.key, dev.index, lambda s=sspec: sj.load_split(s, "cpu"),
-                            sj.split_nbytes)
+                            sj.split_nbytes, cache=getattr(sj, "cache_inputs", True))
                     rep.incrCounter("hbmr.GpuCounters",
                                     "GPU_SPLIT_CACHE_HITS" if hit else "GPU_SPLIT_CACHE_MISSES")
                     r.status.start_time = now

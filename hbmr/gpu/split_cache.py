@@ -32,6 +32,44 @@ class SplitCache:
         self.hits = 0
         self.misses = 0
         self.bypassed = 0       # splits streamed through without being cached (scan policy)
+        # eviction listeners fn(key, device): device state derived from a
+        # split (e.g. the K-Means delta combiner's reference partitions)
+        # goes with it; charge() counts that state against the capacity
+        self._listeners: list = []
+
+    def add_listener(self, fn):
+        with self._lock:
+            if fn not in self._listeners:
+                self._listeners.append(fn)
+
+    def charge(self, key, device, nbytes: int) -> bool:
+        """Count ``nbytes`` of device memory that belongs to the resident split
+        (key, device) against the cache capacity (evicting other splits if
+        that overfills it).  False if the split is not resident."""
+        evicted = []
+        with self._lock:
+            k = (key, device)
+            e = self._entries.get(k)
+            if e is None:
+                return False
+            self._entries[k] = (e[0], e[1] + int(nbytes))
+            self._bytes[device] += int(nbytes)
+            cap = self.capacity.get(device)
+            if cap is not None:
+                while self._bytes[device] > cap:
+                    victim = next((kk for kk in self._entries
+                                   if kk[1] == device and kk != k), None)
+                    if victim is None:
+                        break
+                    _, vb = self._entries.pop(victim)
+                    self._bytes[device] -= vb
+                    self.removed.append(list(victim))
+                    evicted.append(victim)
+            listeners = list(self._listeners)
+        for vk, vd in evicted:
+            for fn in listeners:
+                fn(vk, vd)
+        return True
 
     def get(self, key, device):
         with self._lock:
@@ -58,6 +96,7 @@ class SplitCache:
                 # resident set stays and the overflow streams through
                 self.bypassed += 1
                 return
+            evicted = []
             if cap is not None:
                 while self._bytes[device] + nbytes > cap:
                     victim = next((kk for kk in self._entries if kk[1] == device), None)
@@ -66,16 +105,28 @@ class SplitCache:
                     _, vb = self._entries.pop(victim)
                     self._bytes[device] -= vb
                     self.removed.append(list(victim))
+                    evicted.append(victim)
             self._entries[k] = (data, nbytes)
             self._bytes[device] += nbytes
             self.added.append([key, device])
+            listeners = list(self._listeners) if evicted else ()
+        for vk, vd in evicted:
+            for fn in listeners:
+                fn(vk, vd)
 
-    def get_or_load(self, key, device, loader, nbytes_fn):
+    def get_or_load(self, key, device, loader, nbytes_fn, cache=True):
+        """``cache=False``: the split job streams its inputs (e.g. an
+        out-of-core TeraSort): a resident copy is used, a loaded one is not
+        kept."""
         data = self.get(key, device)
         if data is not None:
             return data, True
         data = loader()
-        self.put(key, device, data, nbytes_fn(data))
+        if cache:
+            self.put(key, device, data, nbytes_fn(data))
+        else:
+            with self._lock:
+                self.bypassed += 1
         return data, False
 
     def drain_changes(self):
@@ -99,12 +150,18 @@ class SplitCache:
         return self._bytes[device]
 
     def clear(self, device=None):
+        gone = []
         with self._lock:
             for k in list(self._entries):
                 if device is None or k[1] == device:
                     _, b = self._entries.pop(k)
                     self._bytes[k[1]] -= b
                     self.removed.append(list(k))
+                    gone.append(k)
+            listeners = list(self._listeners)
+        for vk, vd in gone:
+            for fn in listeners:
+                fn(vk, vd)
 
 
 def configure(tracker):

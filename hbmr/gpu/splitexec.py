@@ -69,7 +69,7 @@ def run_split_cpu_map(host, run):
             return
         data, _hit = host.split_cache.get_or_load(
             sspec.key, "cpu", lambda: js.split_job.load_split(sspec, "cpu"),
-            js.split_job.split_nbytes)
+            js.split_job.split_nbytes, cache=getattr(js.split_job, "cache_inputs", True))
         out = js.split_job.map_cpu(ctx, data)
         with js.lock:
             js.map_outputs[spec.attempt_id] = out

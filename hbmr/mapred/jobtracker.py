@@ -944,18 +944,28 @@ class JobTracker:
                 tr.wake_seq = seq
             tr.bell.set()
 
-    def report(self, status: dict):
+    def report(self, status: dict, assign: bool = False):
         """A tracker's news (finished attempts, lost outputs, cache changes)
-        while its heartbeat long-polls: processed like a heartbeat without
-        assignment, then the long-poll is rung so it assigns into any freed
-        slots and returns what that yields (and any actions the report left,
-        e.g. commit approvals or kills).  One call instead of wakeup → the
-        long-poll returning empty → a heartbeat with the news → a new
-        long-poll; per-tracker heartbeat work is what bounds multi-rank jobs."""
+        while its heartbeat long-polls.
+
+        ``assign`` (hbmr.tracker.report.assign): processed like a heartbeat
+        WITH assignment, and the actions (new launches, commit approvals,
+        kills) return in this call's response — the long-poll stays parked.
+        One RPC per tracker and job in the steady state of chained jobs
+        (the reduce's report, carrying its deferred map completions, gets the
+        next staged job's launches back), where the ring-the-long-poll form
+        cost the report, the long-poll's return and a new long-poll; the
+        JobTracker's per-tracker work is what bounds multi-rank jobs.
+
+        Otherwise: processed without assignment and the long-poll is rung to
+        assign into any freed slots and return what that yields."""
         name = status["tracker_name"] if isinstance(status, dict) else status.tracker_name
         tr = self.trackers.get(name)
         if tr is None:
             return {"reinit": True}
+        if assign:
+            resp = self._heartbeat(status, False, True)
+            return {"actions": resp["actions"]}
         resp = self._heartbeat(status, False, False)
         if resp["actions"]:
             with self.lock:

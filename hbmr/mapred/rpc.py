@@ -246,8 +246,8 @@ class JobTrackerProxy:
     def wakeup(self, tracker_name, seq=None):
         return self.rpc.call("wakeup", tracker_name, seq)
 
-    def report(self, status):
-        return self.rpc.call("report", status)
+    def report(self, status, assign=False):
+        return self.rpc.call("report", status, assign)
 
     def map_completion_events(self, job_id, start=0, wait=0.0):
         return self.rpc.call("map_completion_events", job_id, start, wait)

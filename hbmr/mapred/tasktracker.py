@@ -147,6 +147,8 @@ class TaskTracker:
         # thread can wait that long for the interpreter while another one
         # runs bookkeeping, idling the GPU.  0.2 ms keeps hand-offs prompt.
         self.defer_map_reports = conf.get_boolean("hbmr.tracker.defer.map.reports", True)
+        # JobTracker.report assigns and returns actions (no long-poll wake-up)
+        self.report_assign = conf.get_boolean("hbmr.tracker.report.assign", True)
         # news reaches a long-polling JobTracker as one report call
         self.report_news = conf.get_boolean("hbmr.tracker.report.news", True)
         si = conf.get_float("hbmr.python.switchinterval.ms", 0.2)
@@ -451,8 +453,13 @@ class TaskTracker:
         if self.report_news and getattr(self.jt, "report", None) is not None:
             st = self.status()
             try:
-                r = self.jt.report(st.to_dict())
+                r = self.jt.report(st.to_dict(), self.report_assign) if self.report_assign \
+                    else self.jt.report(st.to_dict())
                 if not (isinstance(r, dict) and r.get("reinit")):
+                    # (assign form) the response carries this tracker's new
+                    # work: handled here, the long-poll stays parked
+                    for act in (r or {}).get("actions", ()):
+                        self._handle(act)
                     return
             except Exception:  # noqa: BLE001
                 pass

@@ -289,18 +289,47 @@ def _baseline_plan(ctxs, datas, k, dp, fx, exact, enabled):
     return have, new, plain, bases, keys
 
 
-def _install_baselines(entries, stream):
+def _baseline_bytes(b) -> int:
+    return sum(t.numel() * t.element_size() for t in (b.g, b.S0, b.N0) if t is not None)
+
+
+def _drop_baselines(split_key, device):
+    """Split-cache eviction listener: the split's reference partitions go with
+    it (their HBM was charged to the split's cache entry)."""
+    dev = f"cuda:{device}" if isinstance(device, int) else str(device)
+    with _BASE_LOCK:
+        for key in [kk for kk in _BASELINES if kk[0] == split_key and kk[1] == dev]:
+            _BASELINES.pop(key)
+
+
+def _install_baselines(entries, stream, cache=None):
     """entries: (key, Baseline) updated or created by a batch just enqueued on
-    ``stream``; their event marks its end."""
+    ``stream``; their event marks its end.  A NEW baseline's device memory is
+    charged to its split's entry in the tracker's split cache (``cache``), so
+    it counts against hbmr.gpu.hbm.reserve.gb's capacity and is dropped when
+    the split is evicted."""
     ev = torch.cuda.Event()
     ev.record(stream)
+    charge = []
     with _BASE_LOCK:
         for key, b in entries:
             b.event, b.stream = ev, stream
-            _BASELINES.pop(key, None)
+            old = _BASELINES.pop(key, None)
             _BASELINES[key] = b
+            if old is not b:
+                charge.append((key, b))
         while len(_BASELINES) > _BASE_MAX:
             _BASELINES.pop(next(iter(_BASELINES)))
+    if cache is not None and charge:
+        cache.add_listener(_drop_baselines)
+        idx = stream.device.index if stream is not None else 0
+        for key, b in charge:
+            if not cache.charge(key[0], idx, _baseline_bytes(b)):
+                # the split is not cache-resident (streamed through): keep no
+                # reference partition HBM the cache cannot account for
+                with _BASE_LOCK:
+                    if _BASELINES.get(key) is b:
+                        _BASELINES.pop(key)
 
 
 def _exact_stats(cin, device):
@@ -579,7 +608,7 @@ class KMeansSplitJob(SplitJob):
                                                                 datas[i].data_ptr(), n)))
                     off += n
         if installed:
-            _install_baselines(installed, ctx.stream)
+            _install_baselines(installed, ctx.stream, getattr(ctx, "split_cache", None))
         for c, d in zip(ctxs, datas):
             c.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, d.shape[0])
         return out
@@ -637,7 +666,7 @@ class KMeansSplitJob(SplitJob):
                 b = km.Baseline(lab.clone(), s, c, d.xb.data_ptr(), d.shape[0])
                 installed.append((keys[i], b))
         if installed:
-            _install_baselines(installed, ctx.stream)
+            _install_baselines(installed, ctx.stream, getattr(ctx, "split_cache", None))
         for c, d in zip(ctxs, datas):
             c.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, d.shape[0])
         return [(sums[pos[i]], counts[pos[i]]) for i in range(B)]

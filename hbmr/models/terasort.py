@@ -120,6 +120,20 @@ class TeraSortSplitJob(SplitJob):
         # same box, profiles/r03_terasort_100gb_v4_1gpu.json); false = the v3
         # path, sort keys then gather through a permutation
         self.gid = conf.get_boolean("hbmr.terasort.reduce.gid", True)
+        # out-of-core sort (MapTask.sortAndSpill / mergeParts): with an HBM
+        # budget below the input size (or hbmr.terasort.spill=true) each map
+        # sorts its split, spills the sorted run to host memory and drops the
+        # split; the reduce brings back, per group of partitions sized to the
+        # budget, every map's run slice and merges the runs (K8 merge path)
+        self.budget = int(conf.get_float("hbmr.terasort.hbm.budget.gb", 0.0) * (1 << 30))
+        self.spill = conf.get_boolean("hbmr.terasort.spill", False)
+        if not self.spill and self.budget > 0:
+            self.spill = sum(r[2] for r in self._ranges()) * S.RECORD > self.budget
+
+    @property
+    def cache_inputs(self):
+        """Spill mode streams the input: a split is dropped after its map."""
+        return not self.spill
 
     # -- splits + sampling (JobTracker side) -----------------------------------------
     def _ranges(self):
@@ -219,14 +233,42 @@ class TeraSortSplitJob(SplitJob):
         return {"records": recs, "hi": hp, "lo": lp, "row": row, "offsets": offs,
                 "checksum": csum, "nparts": nparts, "splitters": data["splitters"]}
 
+    def _map_spill(self, ctx, data):
+        """Spill mode: sort the whole split by key (a range partition is a key
+        range, so the sorted split is partition-ordered too), cut it at the
+        splitters and copy the sorted run to (pinned) host memory on the task's
+        stream; the device copies die with the task."""
+        recs = data["records"]
+        stream = getattr(ctx, "stream", None)
+        nparts = data["nparts"]
+        shi, slo = _parse_keys(data["splitters"]) if nparts > 1 else (
+            torch.zeros(0, dtype=torch.int64), torch.zeros(0, dtype=torch.int64))
+        n = recs.shape[0]
+        srt, hs, ls = S.sort_records(recs, stream=stream)
+        cuda = srt.is_cuda
+        if cuda:
+            shi, slo = shi.to(srt.device), slo.to(srt.device)
+        offs = S.split_offsets(hs, ls, shi, slo, stream=stream)
+        csum = hs.sum() + ls.sum()
+        if cuda:
+            host = torch.empty(srt.shape, dtype=torch.uint8, pin_memory=True)
+            host.copy_(srt, non_blocking=True)
+        else:
+            host = srt
+        ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, n)
+        ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_OUTPUT_RECORDS, n)
+        ctx.reporter.incrCounter(C.TASK_GROUP, "MAP_SPILLED_RECORDS", n)
+        return {"spill": host, "offsets": offs, "checksum": csum, "nparts": nparts,
+                "splitters": data["splitters"], "rows": n}
+
     def map_gpu(self, ctx, data):
-        return self._map(ctx, data)
+        return self._map_spill(ctx, data) if self.spill else self._map(ctx, data)
 
     def map_cpu(self, ctx, data):
-        return self._map(ctx, data)
+        return self._map_spill(ctx, data) if self.spill else self._map(ctx, data)
 
     def map_gpu_batch(self, ctxs, datas):
-        return [self._map(c, d) for c, d in zip(ctxs, datas)]
+        return [self.map_gpu(c, d) for c, d in zip(ctxs, datas)]
 
     # -- shuffle + reduce -------------------------------------------------------------
     @staticmethod
@@ -269,6 +311,11 @@ class TeraSortSplitJob(SplitJob):
             if combined.get("waves"):
                 stats, csum_in = self._reduce_shuffle_waves(ctx, outs, combined["marks"], nparts,
                                                             dev)
+            elif outs and outs[0].get("spill") is not None:
+                if comm.world_size > 1:
+                    raise NotImplementedError(
+                        "out-of-core TeraSort (spill mode) runs its reduce on one rank")
+                stats = self._reduce_spill(ctx, outs, combined["offsets"], nparts or 1, dev)
             elif comm.world_size == 1:
                 stats = self._reduce_local(ctx, outs, combined["offsets"], nparts or 1, dev)
             else:
@@ -367,6 +414,73 @@ class TeraSortSplitJob(SplitJob):
                 if len(spl_hi) == nparts - 1 else None
             recs, hs, ls = self._sorted_partition(his, los, rows, starts, lens, bases, dev,
                                                   hi_range=hr)
+            bad = bad + S.count_unsorted_dev(hs, ls)
+            if prev_last is not None:
+                bad = bad + S.pair_greater(prev_last, (hs[:1], ls[:1]))
+            prev_last = (hs[-1:], ls[-1:])
+            if first is None:
+                first = (hs[:1], ls[:1])
+            last = (hs[-1:], ls[-1:])
+            csum = csum + hs.sum() + ls.sum()
+            n += m
+            if self.out:
+                at = 0
+                for p in range(pa, pb):
+                    self._write_part(ctx, p, recs[at:at + int(sizes[p])])
+                    at += int(sizes[p])
+            del recs, hs, ls
+        if first is None:
+            return 0, None
+        return n, torch.cat([bad.reshape(1), csum.reshape(1), first[0], first[1], last[0],
+                             last[1]])
+
+    def _groups(self, sizes, nparts, limit):
+        """Consecutive partitions in groups of at most ``limit`` record bytes
+        (a single larger partition forms its own group)."""
+        groups, pa = [], 0
+        while pa < nparts:
+            pb, acc = pa, 0
+            while pb < nparts and (pb == pa or (acc + int(sizes[pb])) * S.RECORD <= limit):
+                acc += int(sizes[pb])
+                pb += 1
+            groups.append((pa, pb))
+            pa = pb
+        return groups
+
+    def _reduce_spill(self, ctx, outs, offs, nparts, dev):
+        """Out-of-core reduce (ReduceTask's merge of spilled map outputs,
+        ReduceTask.java:2421-2514, in-memory limit :1102-1111): per group of
+        partitions no larger than a third of the HBM budget, every map's sorted
+        run slice comes back from host memory, the runs are merged on their
+        keys (merge path, log2 #runs passes) and the records gathered in
+        merged order; peak HBM is about 2.3x the group."""
+        sizes = (offs[:, 1:] - offs[:, :-1]).sum(axis=0)
+        limit = self.budget // 3 if self.budget > 0 else self.group_bytes
+        cuda = dev is not None and getattr(dev, "type", "") == "cuda"
+        zero = torch.zeros((), dtype=torch.int64, device=dev)
+        bad, csum = zero.clone(), zero.clone()
+        prev_last = first = last = None
+        n = 0
+        for pa, pb in self._groups(sizes, nparts, limit):
+            lens = offs[:, pb] - offs[:, pa]
+            m = int(lens.sum())
+            if m == 0:
+                continue
+            buf = torch.empty((m, S.RECORD), dtype=torch.uint8, device=dev)
+            runs, at = [], 0
+            for i, o in enumerate(outs):
+                a, b = int(offs[i, pa]), int(offs[i, pb])
+                if b <= a:
+                    continue
+                piece = buf[at:at + b - a]
+                piece.copy_(o["spill"][a:b], non_blocking=cuda)
+                h, lw = S.tera_keys(piece)
+                runs.append((h, lw, torch.arange(at, at + b - a, dtype=torch.int32, device=dev)))
+                at += b - a
+            hs, ls, idx = S.merge_runs(runs)
+            del runs
+            recs = S.gather_records(buf, idx)
+            del buf, idx
             bad = bad + S.count_unsorted_dev(hs, ls)
             if prev_last is not None:
                 bad = bad + S.pair_greater(prev_last, (hs[:1], ls[:1]))
@@ -621,7 +735,8 @@ class TeraSortSplitJob(SplitJob):
         com.setup_task(self.conf, attempt)
         dev = getattr(ctx, "device", None)
         ctx.tera_out = (com, attempt, com.work_path(self.conf, attempt),
-                        _PartWriter(dev, self.conf.get_boolean("terasort.final.sync", True)))
+                        _PartWriter(dev, self.conf.get_boolean("terasort.final.sync", True),
+                                    self.conf.get_int("hbmr.terasort.output.writers", 8)))
 
     def _write_part(self, ctx, p, recs):
         _com, _att, workdir, pw = ctx.tera_out
@@ -651,73 +766,99 @@ class TeraSortSplitJob(SplitJob):
             FileOutputCommitter().commit_job(jip.conf)
 
 
+_PINNED: dict = {}      # (nbuf, chunk) -> pinned host buffers, reused across jobs
+
+
 class _PartWriter:
-    """Streams device record runs to files: chunks are copied into two pinned
-    host buffers on a copy stream while a writer thread writes the previous
-    chunk, so D2H (≈50 GB/s) and file writes overlap; CPU tensors are written
-    directly."""
+    """Streams device record runs to part files (TeraOutputFormat's writes).
 
-    CHUNK = 256 << 20
+    Each run is cut into CHUNK-byte pieces; a piece is copied device -> host
+    into a free buffer of a ring of pinned buffers on a copy stream (≈50 GB/s),
+    and a pool of writer threads ``pwrite``s it at its offset in the file —
+    pieces of one file may land in any order, several files are written at
+    once — so D2H and file writes overlap and a fast filesystem sees
+    ``hbmr.terasort.output.writers`` concurrent writers.  The piece that
+    completes a file flushes it, fsyncs it (``terasort.final.sync``) and
+    closes it: at most the files in flight are open.  CPU tensors are written
+    by the same pool.  The pinned ring is allocated once per process."""
 
-    def __init__(self, device, final_sync):
+    CHUNK = 64 << 20
+
+    def __init__(self, device, final_sync, writers=8):
         import concurrent.futures as cf
+        import threading
         self.sync = final_sync
-        self.pool = cf.ThreadPoolExecutor(1, thread_name_prefix="tera-out")
+        self.writers = max(1, int(writers))
+        self.pool = cf.ThreadPoolExecutor(self.writers, thread_name_prefix="tera-out")
         self.cuda = device is not None and getattr(device, "type", "") == "cuda"
-        self.bufs = self.events = None
-        self.pending = [None, None]
+        self.lock = threading.Lock()
+        self.files = []              # futures of every piece
         self.k = 0
+        self.errors = []
         if self.cuda:
-            self.bufs = [torch.empty(self.CHUNK, dtype=torch.uint8, pin_memory=True)
-                         for _ in range(2)]
+            nbuf = 2 * self.writers
+            key = (nbuf, self.CHUNK)
+            bufs = _PINNED.get(key)
+            if bufs is None:
+                bufs = _PINNED[key] = [torch.empty(self.CHUNK, dtype=torch.uint8,
+                                                   pin_memory=True) for _ in range(nbuf)]
+            self.bufs = bufs
+            self.pending = [None] * nbuf
             self.stream = torch.cuda.Stream(device)
-        self.files = []
 
-    def _wait(self, i):
-        if self.pending[i] is not None:
-            self.pending[i].result()
-            self.pending[i] = None
-
-    def _finish_file(self, f):
-        f.flush()
-        if self.sync:
-            os.fsync(f.fileno())
-        f.close()
+    def _piece(self, fd, st, view, off, ev=None):
+        try:
+            if ev is not None:
+                ev.synchronize()
+            mv = memoryview(view)
+            done = 0
+            while done < len(mv):
+                done += os.pwrite(fd, mv[done:], off + done)
+        finally:
+            with self.lock:
+                st[0] -= 1
+                last = st[0] == 0
+            if last:
+                if self.sync:
+                    os.fsync(fd)
+                os.close(fd)
 
     def write(self, path, recs):
-        """Queue one part file; the writer thread closes (and syncs) it after
-        its last chunk, so at most the files in flight are open at once (a rank
-        may own thousands of partitions)."""
         os.makedirs(os.path.dirname(path), exist_ok=True)
-        f = open(path, "wb")
+        fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
         flat = recs.reshape(-1)
+        n = flat.numel()
+        pieces = max(1, -(-n // self.CHUNK))
+        st = [pieces]
+        if n == 0:
+            self.files.append(self.pool.submit(self._piece, fd, st, b"", 0))
+            return
         if not self.cuda or not flat.is_cuda:
-            a = flat.numpy().copy()
-            self.files.append(self.pool.submit(lambda: (a.tofile(f), self._finish_file(f))))
+            a = flat.numpy()
+            for i in range(pieces):
+                o = i * self.CHUNK
+                self.files.append(self.pool.submit(self._piece, fd, st,
+                                                   a[o:o + self.CHUNK], o))
             return
         self.stream.wait_stream(torch.cuda.current_stream(flat.device))
         flat.record_stream(self.stream)
-        for off in range(0, flat.numel(), self.CHUNK):
-            c = min(self.CHUNK, flat.numel() - off)
-            i = self.k % 2
+        for i in range(pieces):
+            o = i * self.CHUNK
+            c = min(self.CHUNK, n - o)
+            j = self.k % len(self.bufs)
             self.k += 1
-            self._wait(i)
-            buf = self.bufs[i]
+            if self.pending[j] is not None:
+                self.pending[j].result()          # the buffer's previous piece is out
+            buf = self.bufs[j]
             with torch.cuda.stream(self.stream):
-                buf[:c].copy_(flat[off:off + c], non_blocking=True)
+                buf[:c].copy_(flat[o:o + c], non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(self.stream)
-
-            def put(ev=ev, view=buf[:c], f=f):
-                ev.synchronize()
-                f.write(memoryview(view.numpy()))
-            self.pending[i] = self.pool.submit(put)
-        # FIFO writer thread: runs after this file's last chunk
-        self.files.append(self.pool.submit(self._finish_file, f))
+            fut = self.pool.submit(self._piece, fd, st, buf[:c].numpy(), o, ev)
+            self.pending[j] = fut
+            self.files.append(fut)
 
     def close(self):
-        for i in range(2):
-            self._wait(i)
         try:
             for fut in self.files:
                 fut.result()

@@ -46,6 +46,13 @@ _SIGS = {
                                        c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                        c_void_p]),
     "hbmr_kmeans_refine_batch_bytes": (c_long, [c_int, c_void_p]),
+    "hbmr_kmeans_assign_top3_grouped": (c_int, [c_int, c_void_p, c_void_p, c_int, c_int,
+                                                c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                                                c_void_p, c_void_p, c_void_p]),
+    "hbmr_kmeans_refine_batch_q1g": (c_int, [c_int, c_void_p, c_int, c_int, c_int, c_void_p,
+                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                             c_void_p, c_long, c_void_p]),
     "hbmr_kmeans_refine_batch_q1": (c_int, [c_int, c_void_p, c_int, c_int, c_int, c_int,
                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

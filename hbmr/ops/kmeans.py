@@ -462,8 +462,13 @@ def assign_exact_batch(splits: list, img: CentroidImage, stats: torch.Tensor, ou
     pc, ps, pm, pst = _ptr(cand), _ptr(sc), _ptr(mg), _ptr(stats)
     pcn, pcmax, pce, pcemax, pni, pnd = (_ptr(t) for t in (cn, cmax, ce, cemax, ni, nd))
     base, off = out.data_ptr(), 0
+    grouped = REFINE_VERSION >= 3 and img.dp <= 128 and GROUPED_EXACT
     for g0 in range(0, len(splits), MAX_REFINE_BATCH):
         group = splits[g0:g0 + MAX_REFINE_BATCH]
+        if grouped:
+            off += _exact_group(group, img, stats, base + 4 * off, c16, ch, (cn, cmax, ce, cemax),
+                                dt, scratch, stream, lib, st)
+            continue
         rb = _RefineBatch(group, img, stats, scratch, stream) if REFINE_VERSION >= 3 else None
         for i, sp in enumerate(group):
             n = sp.shape[0]
@@ -481,6 +486,51 @@ def assign_exact_batch(splits: list, img: CentroidImage, stats: torch.Tensor, ou
             off += n
         if rb is not None:
             rb.finish()
+
+
+# exact batches: one top-3 launch + one step-1 launch per up to 64 splits
+# (HBMR_EXACT_GROUPED=0: a launch of each per split)
+GROUPED_EXACT = os.environ.get("HBMR_EXACT_GROUPED", "1") != "0"
+
+
+def _exact_group(group, img, stats, labels_ptr, c16, ch, norms, dt, scratch, stream, lib, st):
+    """Top-3 assign and certification of up to 64 splits with grouped launches
+    (hbmr_kmeans_assign_top3_grouped, hbmr_kmeans_refine_batch_q1g); labels of
+    the group written back to back at ``labels_ptr``.  Returns the row count."""
+    B = len(group)
+    ns = [sp.shape[0] for sp in group]
+    N = sum(ns)
+    dev = group[0].xb.device
+    key = ("exact-group", N)
+    bufs = scratch.get(key)
+    if bufs is None:
+        for kk in [kk for kk in scratch if isinstance(kk, tuple) and kk[0] == "exact-group"]:
+            del scratch[kk]
+        bufs = scratch[key] = (torch.empty(2 * N, dtype=torch.int32, device=dev),
+                               torch.empty(N, dtype=torch.float32, device=dev),
+                               torch.empty(2 * N, dtype=torch.float32, device=dev))
+    cand, sc, mg = bufs
+    P = ctypes.c_void_p * B
+    xs = P(*[sp.xb.data_ptr() for sp in group])
+    nsa = (ctypes.c_long * B)(*ns)
+    rc = lib.hbmr_kmeans_assign_top3_grouped(B, xs, nsa, img.dp, int(dt == torch.float16),
+                                             _ptr(c16), _ptr(ch), img.k_pad, labels_ptr,
+                                             _ptr(cand), _ptr(sc), _ptr(mg), st)
+    _lib.check(rc, "hbmr_kmeans_assign_top3_grouped")
+    rb = _RefineBatch(group, img, stats, scratch, stream)
+    cn, cmax, ce, cemax = norms
+    rc = lib.hbmr_kmeans_refine_batch_q1g(
+        B, nsa, img.d, img.k, img.k_pad, P(*[sp.xnorm.data_ptr() for sp in group]),
+        P(*[sp.xbn2.data_ptr() for sp in group]), P(*[sp.xerr.data_ptr() for sp in group]),
+        _ptr(cn), _ptr(cmax), _ptr(ce), _ptr(cemax), labels_ptr, _ptr(cand), _ptr(sc), _ptr(mg),
+        _ptr(rb.ws), rb.ws.numel(), st)
+    _lib.check(rc, "hbmr_kmeans_refine_batch_q1g")
+    o = 0
+    for i in range(B):
+        rb.labels[i] = labels_ptr + 4 * o
+        o += ns[i]
+    rb.finish()
+    return N
 
 
 def map_split_exact(split: ExactSplit, img: CentroidImage, sums, counts, scratch: dict,

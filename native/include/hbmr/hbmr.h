@@ -48,6 +48,16 @@ int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float
                            const float* nbr_dist, int L, int32_t* labels, const int32_t* cand,
                            const float* scores, const float* margin, unsigned long long* stats,
                            int nstats, hipStream_t st);
+int hbmr_kmeans_assign_top3_grouped(int nsplit, const void* const* X, const long* n, int dp,
+                                    int f16, const void* C, const float* chalf, int k_pad,
+                                    int32_t* labels, int32_t* cand, float* scores, float* margin,
+                                    hipStream_t st);
+int hbmr_kmeans_refine_batch_q1g(int nsplit, const long* ns, int d, int k, int k_pad,
+                                 const float* const* xnorm, const float* const* xbn2,
+                                 const float* const* xerr, const float* cnorm, const float* cmax,
+                                 const float* cerr, const float* cerrmax, const int32_t* labels,
+                                 const int32_t* cand, const float* scores, const float* margin,
+                                 void* ws, long ws_bytes, hipStream_t st);
 // refine v3 over a batch of splits (see kmeans.hip): q1 per split, finish once
 long hbmr_kmeans_refine_batch_bytes(int nsplit, const long* ns);
 int hbmr_kmeans_refine_batch_q1(int nsplit, const long* ns, int s, int d, int k, int k_pad,

@@ -204,18 +204,29 @@ struct PackedTop3 : PackedArgMax {
 // 32x32 output tile is 8 MFMAs (256 MFMA cycles per SIMD, 64 of them blocking
 // vector issue): the top-3 epilogue's 4 issue slots per score did not fit the
 // remaining 192 cycles (top-3 assign ran 20 % behind the plain arg-max), 3 do.
-// Together with the lane half h, a cluster's track is its index bits 0-3
-// (cluster = tile*32 + (r&3) + 8(r>>2) + 4h).  The top 3 of a point are the
+// Together with the lane half h, a cluster's track is its index bits 0-2 (4
+// tracks, r & 3) or 0-3 (8 tracks, r & 7): cluster = tile*32 + (r&3) +
+// 8(r>>2) + 4h.  The top 3 of a point are the
 // top 3 of the 32 track candidates; every cluster that is not a candidate
 // scores <= its track's second, which is <= the third — unless the best and
 // the second share a track, which finish_point flags (t = b, margin 0: step 2
 // of the certification then defers the point to the neighbour scan).
+// workgroups per CU the exact (top-3) assign kernels are built for: 3 keeps
+// them at <= 168 VGPRs, i.e. 3 waves per SIMD like the plain arg-max kernel
+#ifndef HBMR_EXACT_MINB
+#define HBMR_EXACT_MINB 3
+#endif
+#ifndef HBMR_EXACT_TRACKS
+#define HBMR_EXACT_TRACKS 4   // register tracks per lane (4: r & 3; 8: r & 7)
+#endif
 struct PackedTop2x8 : PackedArgMax {
-  float tb[8], ts[8];
+  static constexpr int NT = HBMR_EXACT_TRACKS;
+  static constexpr uint32_t TMASK = NT == 8 ? 15u : 7u;   // cluster bits of a track
+  float tb[NT], ts[NT];
   __device__ __forceinline__ void init(int ntiles) {
     PackedArgMax::init(ntiles);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) tb[i] = ts[i] = -3.0e38f;
+    for (int i = 0; i < NT; ++i) tb[i] = ts[i] = -3.0e38f;
   }
   __device__ __forceinline__ void update(const f32x16& acc, int tt) {
     const uint32_t base = top - ((uint32_t)tt << 4);
@@ -228,14 +239,14 @@ struct PackedTop2x8 : PackedArgMax {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float u = __uint_as_float((__float_as_uint(acc[r]) & vmask) | code[r]);
-      ts[r & 7] = vmed3(tb[r & 7], ts[r & 7], u);
-      tb[r & 7] = vmax3(tb[r & 7], u, u);
+      ts[r % NT] = vmed3(tb[r % NT], ts[r % NT], u);
+      tb[r % NT] = vmax3(tb[r % NT], u, u);
     }
   }
   __device__ __forceinline__ void top3(float& b, float& s, float& t) const {
     b = s = t = -3.0e38f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < NT; ++i) {
       PackedTop3::insert(b, s, t, tb[i]);
       PackedTop3::insert(b, s, t, ts[i]);
     }
@@ -282,7 +293,10 @@ __device__ __forceinline__ void finish_point(const AM& am, int h, long p, long n
                                              int32_t* __restrict__ cand,
                                              float* __restrict__ scores,
                                              float* __restrict__ margin,
-                                             uint32_t* __restrict__ hist) {
+                                             uint32_t* __restrict__ hist, long cs = -1) {
+  // cs: stride of the second candidate / margin (n for one split; the batch
+  // size when a grouped launch writes a batch's arrays)
+  if (cs < 0) cs = n;
   if constexpr (!EXACT) {
     float bv = am.best();
     int cluster = am.cluster(bv, h);
@@ -311,7 +325,7 @@ __device__ __forceinline__ void finish_point(const AM& am, int h, long p, long n
     for (int i = 0; i < 3; ++i) insert3(v, c, ov[i], oc[i]);
     if constexpr (HasTracks<AM>::value) {
       // best and second in one track: the rest is bounded only by the second
-      if (((c[0] ^ c[1]) & 15) == 0) {
+      if (((c[0] ^ c[1]) & AM::TMASK) == 0) {
         v[2] = v[0];
         c[2] = c[0];
       }
@@ -319,11 +333,11 @@ __device__ __forceinline__ void finish_point(const AM& am, int h, long p, long n
     if (h == 0 && p < n) {
       labels[p] = c[0];
       cand[p] = c[1];
-      cand[n + p] = c[2];
+      cand[cs + p] = c[2];
       const float bs = am.score(v[0]);
       scores[p] = bs;
       margin[p] = bs - am.score(v[1]);
-      margin[n + p] = bs - am.score(v[2]);
+      margin[cs + p] = bs - am.score(v[2]);
       if (hist) atomicAdd(hist + c[0], 1u);
     }
   }
@@ -523,7 +537,8 @@ __device__ __forceinline__ void assign_tile_v2(const __bf16* __restrict__ X, lon
                                                int32_t* __restrict__ labels,
                                                float* __restrict__ scores, long blk, char* smem,
                                                int32_t* __restrict__ cand = nullptr,
-                                               float* __restrict__ margin = nullptr) {
+                                               float* __restrict__ margin = nullptr,
+                                               long cs = -1) {
   static_assert(D <= 128, "v2 keeps PB point blocks of D ≤ 128 in registers");
   using V = AssignV2<D>;
   constexpr int KS = V::KS;
@@ -607,7 +622,8 @@ __device__ __forceinline__ void assign_tile_v2(const __bf16* __restrict__ X, lon
 
 #pragma unroll
   for (int pb = 0; pb < PB; ++pb)
-    finish_point<EXACT>(am[pb], h, p0 + pb * 32 + col, n, labels, cand, scores, margin, nullptr);
+    finish_point<EXACT>(am[pb], h, p0 + pb * 32 + col, n, labels, cand, scores, margin, nullptr,
+                        cs);
 }
 
 template <int D>
@@ -643,7 +659,7 @@ __global__ __launch_bounds__(kThreads, 2) void kmeans_assign_top3_kernel(
 }
 
 template <int D, int PB, bool F16, bool TOP3 = false>
-__global__ __launch_bounds__(AssignV2<D>::THREADS, AssignV2<D>::MINB) void kmeans_assign_top3_v2_kernel(
+__global__ __launch_bounds__(AssignV2<D>::THREADS, HBMR_EXACT_MINB) void kmeans_assign_top3_v2_kernel(
     const __bf16* __restrict__ X, long n, const __bf16* __restrict__ C,
     const float* __restrict__ chalf, int ntiles, int32_t* __restrict__ labels,
     int32_t* __restrict__ cand, float* __restrict__ scores, float* __restrict__ margin) {
@@ -721,6 +737,26 @@ __global__ __launch_bounds__(AssignV2<D>::THREADS, AssignV2<D>::MINB) void kmean
   const int s = __builtin_amdgcn_readfirstlane(find_split(tbl, b));
   assign_tile_v2<D, PB>(tbl.X[s], tbl.n[s], C, chalf, ntiles, labels + tbl.off[s], nullptr,
                     b - tbl.blk[s], smem);
+}
+
+// Exact mode over a batch of splits in ONE launch (a per-split launch of the
+// top-3 assign ran at 57 % MFMA busy against 67 % for a long dispatch): the
+// batch's labels / scores and the two-row cand / margin arrays are indexed by
+// the batch position (split offset + row), second rows at stride tbl.off[nsplit]
+template <int D, int PB, bool F16, bool TOP3>
+__global__ __launch_bounds__(AssignV2<D>::THREADS, HBMR_EXACT_MINB) void
+kmeans_assign_top3_grouped_v2_kernel(const SplitTable tbl, const __bf16* __restrict__ C,
+                                     const float* __restrict__ chalf, int ntiles,
+                                     int32_t* __restrict__ labels, int32_t* __restrict__ cand,
+                                     float* __restrict__ scores, float* __restrict__ margin,
+                                     long total) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const long b = hbmr_xcd_remap(blockIdx.x, gridDim.x);
+  const int s = __builtin_amdgcn_readfirstlane(find_split(tbl, b));
+  const long o = tbl.off[s];
+  assign_tile_v2<D, PB, true, F16, TOP3>(tbl.X[s], tbl.n[s], C, chalf, ntiles, labels + o,
+                                         scores + o, b - tbl.blk[s], smem, cand + o, margin + o,
+                                         total);
 }
 
 // ---------------------------------------------------------------------------
@@ -2293,13 +2329,15 @@ __device__ __forceinline__ uint32_t lane_rank(unsigned long long m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-__global__ __launch_bounds__(256) void kmeans_refine_q1_kernel(
-    long n, int sidx, int d, int k, const float* __restrict__ xnorm,
+// Step 1 over one block of 256 * kQ1Per points of split sidx (block index blk
+// within the split); cand / margin second rows at stride cs.
+__device__ __forceinline__ void refine_q1_block(
+    long n, int sidx, long blk, int d, int k, const float* __restrict__ xnorm,
     const float* __restrict__ xbn2, const float* __restrict__ xerr,
     const float* __restrict__ cnorm, const float* __restrict__ cmax,
     const float* __restrict__ cerr, const float* __restrict__ cerrmax, double pack_rel,
     const int32_t* __restrict__ labels, const int32_t* __restrict__ cand,
-    const float* __restrict__ score, const float* __restrict__ margin,
+    const float* __restrict__ score, const float* __restrict__ margin, long cs,
     uint32_t* __restrict__ qcount, ExactQ1* __restrict__ q1, long cap1,
     unsigned long long* __restrict__ stats) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2316,17 +2354,17 @@ __global__ __launch_bounds__(256) void kmeans_refine_q1_kernel(
   float m2[kQ1Per];
 #pragma unroll
   for (int i = 0; i < kQ1Per; ++i) {
-    const long p = (long)blockIdx.x * (256 * kQ1Per) + i * 256 + tid;
+    const long p = blk * (256 * kQ1Per) + i * 256 + tid;
     in[i] = p < n;
     const long q = in[i] ? p : n - 1;
     e[i].row = (uint32_t)q;
     e[i].split = (uint32_t)sidx;
     e[i].b = labels[q];
     e[i].s = cand[q];
-    e[i].t = cand[n + q];
+    e[i].t = cand[cs + q];
     e[i].sb = score[q];
     m2[i] = margin[q];
-    e[i].m3 = margin[n + q];
+    e[i].m3 = margin[cs + q];
     e[i].x2 = xbn2[q];
     e[i].xn = xnorm[q];
     e[i].xe = xerr[q];
@@ -2377,6 +2415,52 @@ __global__ __launch_bounds__(256) void kmeans_refine_q1_kernel(
 #pragma unroll
   for (int i = 0; i < kQ1Per; ++i)
     if (flag[i]) out[wcnt[wave][i] + rank[i]] = e[i];
+}
+
+__global__ __launch_bounds__(256) void kmeans_refine_q1_kernel(
+    long n, int sidx, int d, int k, const float* __restrict__ xnorm,
+    const float* __restrict__ xbn2, const float* __restrict__ xerr,
+    const float* __restrict__ cnorm, const float* __restrict__ cmax,
+    const float* __restrict__ cerr, const float* __restrict__ cerrmax, double pack_rel,
+    const int32_t* __restrict__ labels, const int32_t* __restrict__ cand,
+    const float* __restrict__ score, const float* __restrict__ margin,
+    uint32_t* __restrict__ qcount, ExactQ1* __restrict__ q1, long cap1,
+    unsigned long long* __restrict__ stats) {
+  refine_q1_block(n, sidx, blockIdx.x, d, k, xnorm, xbn2, xerr, cnorm, cmax, cerr, cerrmax,
+                  pack_rel, labels, cand, score, margin, n, qcount, q1, cap1, stats);
+}
+
+// the splits of a batch in one launch (after the grouped top-3 assign): the
+// batch arrays hold split s at offset off[s], second rows at stride total
+struct Q1Table {
+  int nsplit;
+  long total;
+  long n[kMaxGroup];
+  long off[kMaxGroup];
+  long blk[kMaxGroup + 1];
+  const float* xnorm[kMaxGroup];
+  const float* xbn2[kMaxGroup];
+  const float* xerr[kMaxGroup];
+};
+
+__global__ __launch_bounds__(256) void kmeans_refine_q1_grouped_kernel(
+    const Q1Table tbl, int d, int k, const float* __restrict__ cnorm,
+    const float* __restrict__ cmax, const float* __restrict__ cerr,
+    const float* __restrict__ cerrmax, double pack_rel, const int32_t* __restrict__ labels,
+    const int32_t* __restrict__ cand, const float* __restrict__ score,
+    const float* __restrict__ margin, uint32_t* __restrict__ qcount, ExactQ1* __restrict__ q1,
+    long cap1, unsigned long long* __restrict__ stats) {
+  const long b = blockIdx.x;
+  int lo = 0, hi = tbl.nsplit;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (tbl.blk[mid] <= b) lo = mid; else hi = mid;
+  }
+  const int s = __builtin_amdgcn_readfirstlane(lo);
+  const long o = tbl.off[s];
+  refine_q1_block(tbl.n[s], s, b - tbl.blk[s], d, k, tbl.xnorm[s], tbl.xbn2[s], tbl.xerr[s],
+                  cnorm, cmax, cerr, cerrmax, pack_rel, labels + o, cand + o, score + o,
+                  margin + o, tbl.total, qcount, q1, cap1, stats);
 }
 
 // 16 features of a row per lane of an 8-lane group: 128m + 32h + 4sub + (0..3)
@@ -2638,6 +2722,44 @@ int refine_version() {
     v = (e && atoi(e) == 1) ? 1 : 2;
   }
   return v;
+}
+
+template <int D, bool F16>
+int launch_assign_top3_grouped(int nsplit, const void* const* X, const long* n, const void* C,
+                               const float* chalf, int k_pad, int32_t* labels, int32_t* cand,
+                               float* scores, float* margin, hipStream_t st) {
+  if constexpr (D > 128) {
+    return (int)hipErrorNotSupported;      // the caller launches per split
+  } else {
+    if (nsplit <= 0 || nsplit > kMaxGroup || k_pad % 32) return (int)hipErrorInvalidValue;
+    SplitTable t;
+    memset(&t, 0, sizeof(t));
+    t.nsplit = nsplit;
+    constexpr int pts = AssignV2<D>::WAVES * 2 * 32;
+    long total = 0, nb = 0;
+    for (int i = 0; i < nsplit; ++i) {
+      if (n[i] < 0) return (int)hipErrorInvalidValue;
+      t.X[i] = reinterpret_cast<const __bf16*>(X[i]);
+      t.n[i] = n[i];
+      t.off[i] = total;
+      t.blk[i] = nb;
+      total += n[i];
+      nb += (n[i] + pts - 1) / pts;
+    }
+    t.blk[nsplit] = nb;
+    if (nb == 0) return 0;
+    if (nb > 0x7fffffffL) return (int)hipErrorInvalidValue;
+    static const bool top3 = [] {
+      const char* e = getenv("HBMR_EXACT_EPI");
+      return e && strcmp(e, "top3") == 0;
+    }();
+    auto kern = top3 ? kmeans_assign_top3_grouped_v2_kernel<D, 2, F16, true>
+                     : kmeans_assign_top3_grouped_v2_kernel<D, 2, F16, false>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(AssignV2<D>::THREADS),
+                       AssignV2<D>::LDS_BYTES, st, t, reinterpret_cast<const __bf16*>(C), chalf,
+                       k_pad / 32, labels, cand, scores, margin, total);
+    return (int)hipGetLastError();
+  }
 }
 
 template <int D, bool F16>
@@ -3140,6 +3262,28 @@ int hbmr_kmeans_assign_top3_f16(const void* X, long n, int dp, const void* C, co
   }
 }
 
+// the top-3 assign of a batch of splits in one launch (dp <= 128; else
+// hipErrorNotSupported): labels / scores [N], cand / margin [2N] of the batch,
+// N = sum n, split i at offset n[0] + ... + n[i-1]
+int hbmr_kmeans_assign_top3_grouped(int nsplit, const void* const* X, const long* n, int dp,
+                                    int f16, const void* C, const float* chalf, int k_pad,
+                                    int32_t* labels, int32_t* cand, float* scores, float* margin,
+                                    hipStream_t st) {
+  if (!labels || !cand || !scores || !margin) return (int)hipErrorInvalidValue;
+#define HBMR_TOP3G(D)                                                                      \
+  return f16 ? launch_assign_top3_grouped<D, true>(nsplit, X, n, C, chalf, k_pad, labels,  \
+                                                   cand, scores, margin, st)               \
+             : launch_assign_top3_grouped<D, false>(nsplit, X, n, C, chalf, k_pad, labels, \
+                                                    cand, scores, margin, st)
+  switch (dp) {
+    case 64: HBMR_TOP3G(64);
+    case 128: HBMR_TOP3G(128);
+    case 256: HBMR_TOP3G(256);
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef HBMR_TOP3G
+}
+
 int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float* xnorm,
                            const float* xbn2, const float* xerr, const float* C32, int k,
                            int k_pad, const float* cnorm, const float* cmax, const float* cerr,
@@ -3232,6 +3376,50 @@ int hbmr_kmeans_refine_batch_q1(int nsplit, const long* ns, int s, int d, int k,
   hipLaunchKernelGGL(kmeans_refine_q1_kernel, dim3((unsigned)b1), dim3(256), 0, st, n, s, d, k,
                      xnorm, xbn2, xerr, cnorm, cmax, cerr, cerrmax, pack_rel, labels, cand,
                      scores, margin, c1, reinterpret_cast<ExactQ1*>(w + Ly.off1), Ly.cap1,
+                     reinterpret_cast<unsigned long long*>(w + kStatsOff));
+  return (int)hipGetLastError();
+}
+
+// step 1 of a whole batch after hbmr_kmeans_assign_top3_grouped (resets the
+// batch's queues): the batch arrays as that call wrote them
+int hbmr_kmeans_refine_batch_q1g(int nsplit, const long* ns, int d, int k, int k_pad,
+                                 const float* const* xnorm, const float* const* xbn2,
+                                 const float* const* xerr, const float* cnorm, const float* cmax,
+                                 const float* cerr, const float* cerrmax, const int32_t* labels,
+                                 const int32_t* cand, const float* scores, const float* margin,
+                                 void* ws, long ws_bytes, hipStream_t st) {
+  if (nsplit <= 0 || nsplit > kMaxGroup || k <= 0 || k_pad < k || d > kRefineMaxDp ||
+      ((uintptr_t)ws & 255))
+    return (int)hipErrorInvalidValue;
+  Q1Table t;
+  memset(&t, 0, sizeof(t));
+  t.nsplit = nsplit;
+  long total = 0, nb = 0;
+  for (int i = 0; i < nsplit; ++i) {
+    if (ns[i] < 0 || ns[i] > 0x7fffffffL) return (int)hipErrorInvalidValue;
+    t.n[i] = ns[i];
+    t.off[i] = total;
+    t.blk[i] = nb;
+    t.xnorm[i] = xnorm[i];
+    t.xbn2[i] = xbn2[i];
+    t.xerr[i] = xerr[i];
+    total += ns[i];
+    nb += ceil_div(ns[i], 256 * kQ1Per);
+  }
+  t.blk[nsplit] = nb;
+  t.total = total;
+  const RefineLayout Ly = refine_layout(nsplit, ns);
+  if (ws_bytes < (long)Ly.bytes) return (int)hipErrorInvalidValue;
+  char* w = static_cast<char*>(ws);
+  uint32_t* c1 = reinterpret_cast<uint32_t*>(w);
+  HBMR_RETURN_IF_ERROR(hipMemsetAsync(c1, 0, kHdrClear, st));
+  if (nb == 0) return 0;
+  int tb = 0;
+  while ((1 << tb) < k_pad / 32) ++tb;
+  const double pack_rel = ldexp(1.0, 4 + tb - 23);
+  hipLaunchKernelGGL(kmeans_refine_q1_grouped_kernel, dim3((unsigned)nb), dim3(256), 0, st, t, d,
+                     k, cnorm, cmax, cerr, cerrmax, pack_rel, labels, cand, scores, margin, c1,
+                     reinterpret_cast<ExactQ1*>(w + Ly.off1), Ly.cap1,
                      reinterpret_cast<unsigned long long*>(w + kStatsOff));
   return (int)hipGetLastError();
 }

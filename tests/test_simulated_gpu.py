@@ -138,3 +138,23 @@ def test_kmeans_beyond_hbm_streams_splits_with_scan_cache():
     with LocalCluster(plain, num_trackers=1, cpu_slots=2) as cl:
         c_cpu = _kmeans(cl, plain, iters=4).centroids()
     assert torch.equal(c_small, c_cpu)
+
+
+def test_split_cache_charges_derived_state_and_notifies_evictions():
+    """Device state derived from a split (the delta combiner's reference
+    partitions) is charged to its cache entry and dropped with it."""
+    from hbmr.gpu.split_cache import SplitCache
+    c = SplitCache({0: 100})
+    gone = []
+    c.add_listener(lambda k, d: gone.append((k, d)))
+    c.put("a", 0, "A", 40)
+    c.put("b", 0, "B", 40)
+    assert c.charge("a", 0, 10) and c.bytes_on(0) == 90
+    assert not c.charge("zz", 0, 5)            # not resident: nothing charged
+    c.get("a", 0)                               # a is the most recent
+    c.charge("a", 0, 20)                        # 110 > 100: b goes, a stays
+    assert gone == [("b", 0)] and c.bytes_on(0) == 70
+    c.put("c", 0, "C", 50)                      # evicts a (70 + 50 > 100)
+    assert ("a", 0) in gone and c.bytes_on(0) == 50
+    c.clear(0)
+    assert ("c", 0) in gone and c.bytes_on(0) == 0

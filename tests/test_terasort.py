@@ -385,3 +385,52 @@ def test_gpu_sort_gathered_packed_ids(ties, window):
     assert S.count_unsorted(hs, ls) == 0
     # the same multiset of records (equal keys may come in either order)
     assert sorted(map(bytes, r)) == sorted(map(bytes, want))
+
+
+@pytest.mark.parametrize("budget_rows", [4000, 11000])
+def test_terasort_out_of_core_spill_and_merge(tmp_path, budget_rows):
+    """Out-of-core TeraSort (MapTask.sortAndSpill / mergeParts): an HBM budget
+    below the input size makes every map sort and spill its run to host
+    memory (its split not kept) and the reduce merge the runs back in groups
+    of partitions sized to the budget; output and order equal the in-memory
+    sort's, and TeraValidate passes."""
+    rows = 12000
+    out = tmp_path / "out"
+    conf = T.terasort_conf(rows=rows, split_rows=2500, output=str(out), partitions=10)
+    conf.set("hbmr.terasort.hbm.budget.gb", str(budget_rows * 100 / (1 << 30)))
+    with LocalCluster(JobConf(), num_trackers=1, cpu_slots=2) as cl:
+        rj = cl.submit_job(conf)
+        rj.waitForCompletion(120)
+        assert rj.isSuccessful(), rj.getFailureInfo()
+        res = rj._impl.jip.result[0]
+        spilled = rj.getCounters().get("org.apache.hadoop.mapred.Task$Counter",
+                                       "MAP_SPILLED_RECORDS")
+    assert spilled == rows                       # rows * 100 B > budget: spill mode
+    assert res["unsorted"] == 0 and res["checksum_ok"] and res["records"] == rows
+    parts = sorted(f for f in os.listdir(out) if f.startswith("part-"))
+    assert parts == [f"part-{i:05d}" for i in range(10)]
+    got = np.concatenate([np.fromfile(out / p, dtype=np.uint8).reshape(-1, 100) for p in parts])
+    assert np.array_equal(got, _ref_sorted(rows))
+    assert T.teravalidate(str(out))["misordered"] == 0
+
+
+@pytest.mark.gpu
+def test_gpu_terasort_out_of_core(tmp_path):
+    """On the GPU: data 3x a deliberately small HBM budget sorts through the
+    spill path (pinned host runs, merge-path reduce) and validates."""
+    rows = 3_000_000                      # 300 MB of records, budget 100 MB
+    out = tmp_path / "out"
+    conf = T.terasort_conf(rows=rows, split_rows=400_000, output=str(out), partitions=6)
+    conf.set("hbmr.terasort.hbm.budget.gb", str(100e6 / (1 << 30)))
+    with LocalCluster(JobConf(), num_trackers=1, gpus=[[0]], cpu_slots=0) as cl:
+        rj = cl.submit_job(conf)
+        rj.waitForCompletion(300)
+        assert rj.isSuccessful(), rj.getFailureInfo()
+        res = rj._impl.jip.result[0]
+        cnt = rj.getCounters()
+    assert cnt.get("org.apache.hadoop.mapred.Task$Counter", "MAP_SPILLED_RECORDS") == rows
+    assert res["records"] == rows and res["unsorted"] == 0 and res["checksum_ok"]
+    v = T.teravalidate(str(out))
+    assert v["files"] == 6 and v["records"] == rows and v["misordered"] == 0
+    got = np.fromfile(out / "part-00000", dtype=np.uint8).reshape(-1, 100)
+    assert np.array_equal(got[:1000], _ref_sorted(rows)[:1000])
