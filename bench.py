@@ -7,8 +7,12 @@ framework: JobTracker scheduling (hybrid cost model, CPU slots enabled), map
 tasks on the TaskTrackers' GPU slots (MFMA assign + fixed-point combiner on
 HBM-resident splits), the collective reduce (exact int64 all-reduce over
 RCCL/xGMI) and the centroid update.  The total problem (100M points) is fixed
-as N grows (strong scaling); splits are 781,250 points (200 MB bf16) → 128 map
-tasks per job.  Data: synthetic Gaussian mixture generated in HBM by the
+as N grows (strong scaling); splits are 781,250 points → 128 map tasks per job.
+Precision (default, ``--exact``): the points stay fp32 and every label is the
+exact arg-min over the fp32 data — f16 MFMA top candidates, certified against
+an error bound, the uncertain points re-scored in fp64 — and the centroid sums
+are exact int64 fixed point of the fp32 rows (dtype "fp32"); ``--no-exact``
+runs the bf16-input variant.  Data: synthetic Gaussian mixture generated in HBM by the
 framework's own split loader; centroids initialised from the first k points.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -67,9 +71,12 @@ def main():
     ap.add_argument("--prestage", action=argparse.BooleanOptionalAction, default=True,
                     help="let the JobTracker stage held iteration jobs: their GPU maps wait "
                          "on the device behind the predecessor's reduce (hbmr.job.prestage)")
-    ap.add_argument("--exact", action="store_true",
-                    help="fp32-faithful assignment (hbmr.kmeans.exact: bf16 MFMA top-3, "
-                         "certified, fp64 re-score of uncertain points); dtype bf16-certified-fp32")
+    ap.add_argument("--exact", action=argparse.BooleanOptionalAction, default=True,
+                    help="fp32-faithful assignment (default; hbmr.kmeans.exact: the points stay "
+                         "fp32, f16 MFMA candidates certified against the fp32 data, fp64 "
+                         "re-score of the uncertain points, fp32 rows summed in exact fixed "
+                         "point): dtype fp32.  --no-exact: the bf16-input variant (points "
+                         "stored and summed in bf16)")
     ap.add_argument("--input", default=None, metavar="DIR",
                     help="SequenceFile input (tools/write_kmeans_input.py writes the synthetic "
                          "set as files) instead of points generated in HBM")
@@ -233,8 +240,12 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "bf16-certified-fp32" if conf.get_boolean("hbmr.kmeans.exact", False)
-                     else "bf16",
+            "dtype": "fp32" if conf.get_boolean("hbmr.kmeans.exact", False) else "bf16",
+            "precision": ("exact: labels = the fp64 arg-min over the fp32 points and centroids "
+                          "(f16 MFMA top candidates, certified by an error bound, uncertain "
+                          "points re-scored in fp64); centroid sums of the fp32 rows in int64 "
+                          "fixed point") if conf.get_boolean("hbmr.kmeans.exact", False) else
+                         "bf16 points (storage and sums), bf16 MFMA assign",
             "data": (f"sequencefile input {a.input} (the synthetic set written to disk)"
                      if a.input else "synthetic") if a.simulate_ms is None else
                     f"simulated GPU slots ({a.simulate_ms} ms/split), CPU only",

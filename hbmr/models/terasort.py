@@ -945,16 +945,19 @@ def teragen_conf(base=None, rows=1000, output=None, split_rows=None):
     return job
 
 
-def teravalidate(path) -> dict:
+def teravalidate(path, progress=None) -> dict:
     """TeraValidate over the part files of ``path`` in name order: records out of
     order within a file or across file boundaries, total records and an
-    order-independent key checksum (sum of the 10-byte keys mod 2^64)."""
+    order-independent key checksum (sum of the 10-byte keys mod 2^64).
+    ``progress(i, nfiles)`` is called before each file."""
     files = sorted(f for f in os.listdir(path) if f.startswith("part-"))
     bad = 0
     total = 0
     csum = 0
     prev_last = None
-    for fn in files:
+    for i, fn in enumerate(files):
+        if progress is not None:
+            progress(i, len(files))
         recs = np.fromfile(os.path.join(path, fn), dtype=np.uint8)
         if recs.size % S.RECORD:
             raise ValueError(f"{fn}: not a whole number of 100-byte records")

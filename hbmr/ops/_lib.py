@@ -52,12 +52,12 @@ _SIGS = {
     "hbmr_kmeans_refine_batch_q1g": (c_int, [c_int, c_void_p, c_int, c_int, c_int, c_void_p,
                                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                             c_void_p, c_long, c_void_p]),
+                                             c_void_p, c_long, c_void_p, c_void_p]),
     "hbmr_kmeans_refine_batch_q1": (c_int, [c_int, c_void_p, c_int, c_int, c_int, c_int,
                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                             c_void_p, c_void_p, c_void_p, c_long, c_int,
-                                            c_void_p]),
+                                            c_void_p, c_void_p]),
     "hbmr_kmeans_refine_batch_finish": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int,
                                                 c_int, c_void_p, c_int, c_int, c_void_p,
                                                 c_void_p, c_void_p, c_void_p, c_int, c_void_p,

@@ -137,19 +137,44 @@ class CentroidImage:
                 if L is None:
                     L = int(os.environ.get("HBMR_KMEANS_NBR_L", NBR_L))
                 L = max(1, min(L, self.k))
+                # squared distances by the Gram form in fp64 (one DGEMM instead
+                # of a pairwise kernel: ~0.8 ms per image at k = 1024), with
+                # the form's rounding error bounded explicitly: |D2 - D| <=
+                # (d + 4) 2^-53 (|a|^2 + |b|^2) for fp32 inputs, so the lower
+                # bounds (Elkan's scan order and stop rule) and upper bounds
+                # (the pair rule) stay rigorous
                 c = self.cen.double()
-                dist = torch.cdist(c, c, compute_mode="donot_use_mm_for_euclid_dist")
-                dist.fill_diagonal_(0.0)
-                dv, di = dist.sort(dim=1, stable=True)
+                n2 = (c * c).sum(1)
+                nsum = n2[:, None] + n2[None, :]
+                d2 = torch.addmm(nsum, c, c.T, beta=1.0, alpha=-2.0)
+                err = nsum * ((self.d + 4) * 2.0 ** -53 * 1.01)
+                lo = (d2 - err).clamp_(min=0.0).sqrt_()
+                lo.fill_diagonal_(0.0)
+                dv, di = lo.sort(dim=1, stable=True)
                 dv, di = dv[:, :L].contiguous(), di[:, :L].to(torch.int32).contiguous()
                 f = dv.float()
                 f = torch.where(f.double() > dv, torch.nextafter(f, torch.full_like(f, -1.0)), f)
+                # the full matrix of upper bounds rounded UP (the pair rule of
+                # the certification's step 1); k <= PAIR_DIST_MAX_K
+                pd = None
+                if self.k <= PAIR_DIST_MAX_K:
+                    hi = (d2 + err).clamp_(min=0.0).sqrt_()
+                    hi.fill_diagonal_(0.0)
+                    pd = hi.float()
+                    pd = torch.where(pd.double() < hi, torch.nextafter(
+                        pd, torch.full_like(pd, float("inf"))), pd).contiguous()
                 ev = torch.cuda.Event()
                 ev.record()
-                self._nbr = (di, f.contiguous(), L, ev)
-        di, f, L, ev = self._nbr
+                self._nbr = (di, f.contiguous(), L, ev, pd)
+        di, f, L, ev, _ = self._nbr
         torch.cuda.current_stream().wait_event(ev)
         return di, f, L
+
+    def pair_dist(self):
+        """|c_a - c_b| for every pair, fp64 rounded up to fp32 [k, k] (None past
+        PAIR_DIST_MAX_K clusters): the certification's pair rule."""
+        self.neighbors()
+        return self._nbr[4]
 
     def max_shift(self) -> float:
         return float(self.shift2.max().sqrt().item()) if self.k else 0.0
@@ -340,6 +365,7 @@ class _RefineBatch:
         with torch.cuda.stream(stream) if stream is not None else _nullctx():
             self.norms = img.norms(self.dt)
             self.nbr = img.neighbors()
+            self.pd = img.pair_dist()
         self.labels = [None] * len(splits)
         self.lib = _lib.load()
         self.st = _lib.stream_handle(stream)
@@ -352,7 +378,7 @@ class _RefineBatch:
             len(self.splits), self.ns, i, img.d, img.k, img.k_pad, _ptr(sp.xnorm),
             _ptr(sp.xbn2), _ptr(sp.xerr), _ptr(cn), _ptr(cmax), _ptr(ce), _ptr(cemax),
             labels_ptr, _ptr(cand), _ptr(scores), _ptr(margin), _ptr(self.stats),
-            _ptr(self.ws), self.ws.numel(), int(i == 0), self.st)
+            _ptr(self.ws), self.ws.numel(), int(i == 0), _ptr(self.pd), self.st)
         _lib.check(rc, "hbmr_kmeans_refine_batch_q1")
 
     def finish(self):
@@ -488,6 +514,8 @@ def assign_exact_batch(splits: list, img: CentroidImage, stats: torch.Tensor, ou
             rb.finish()
 
 
+# the pair rule of the certification keeps a [k, k] centroid distance matrix
+PAIR_DIST_MAX_K = int(os.environ.get("HBMR_PAIR_DIST_MAX_K", "8192"))
 # exact batches: one top-3 launch + one step-1 launch per up to 64 splits
 # (HBMR_EXACT_GROUPED=0: a launch of each per split)
 GROUPED_EXACT = os.environ.get("HBMR_EXACT_GROUPED", "1") != "0"
@@ -523,7 +551,7 @@ def _exact_group(group, img, stats, labels_ptr, c16, ch, norms, dt, scratch, str
         B, nsa, img.d, img.k, img.k_pad, P(*[sp.xnorm.data_ptr() for sp in group]),
         P(*[sp.xbn2.data_ptr() for sp in group]), P(*[sp.xerr.data_ptr() for sp in group]),
         _ptr(cn), _ptr(cmax), _ptr(ce), _ptr(cemax), labels_ptr, _ptr(cand), _ptr(sc), _ptr(mg),
-        _ptr(rb.ws), rb.ws.numel(), st)
+        _ptr(rb.ws), rb.ws.numel(), _ptr(rb.pd), st)
     _lib.check(rc, "hbmr_kmeans_refine_batch_q1g")
     o = 0
     for i in range(B):

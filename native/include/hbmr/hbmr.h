@@ -57,7 +57,7 @@ int hbmr_kmeans_refine_batch_q1g(int nsplit, const long* ns, int d, int k, int k
                                  const float* const* xerr, const float* cnorm, const float* cmax,
                                  const float* cerr, const float* cerrmax, const int32_t* labels,
                                  const int32_t* cand, const float* scores, const float* margin,
-                                 void* ws, long ws_bytes, hipStream_t st);
+                                 void* ws, long ws_bytes, const float* dcc, hipStream_t st);
 // refine v3 over a batch of splits (see kmeans.hip): q1 per split, finish once
 long hbmr_kmeans_refine_batch_bytes(int nsplit, const long* ns);
 int hbmr_kmeans_refine_batch_q1(int nsplit, const long* ns, int s, int d, int k, int k_pad,
@@ -66,7 +66,7 @@ int hbmr_kmeans_refine_batch_q1(int nsplit, const long* ns, int s, int d, int k,
                                 const float* cerrmax, const int32_t* labels, const int32_t* cand,
                                 const float* scores, const float* margin,
                                 unsigned long long* stats, void* ws, long ws_bytes, int reset,
-                                hipStream_t st);
+                                const float* dcc, hipStream_t st);
 int hbmr_kmeans_refine_batch_finish(int nsplit, const long* ns, const float* const* x32,
                                     int32_t* const* labels, int d, int ldx, const float* C32,
                                     int k, int k_pad, const float* cmax, const float* cerrmax,

@@ -1691,6 +1691,16 @@ __device__ __forceinline__ void exact_bound(double sc, double ct, double xt, dou
   e = a * (2.0 * sqrt(dhi) + a) * 0.5 + eacc + epack;
 }
 
+// Error of a kernel score sc against the exact rounded-operand score
+// (accumulation + packing, eap) and an upper bound of sqrt(D~) (rdhi), for a
+// centroid with |c~| <= ct and |x~| <= xt (see exact_bound).
+__device__ __forceinline__ void score_err(double sc, double ct, double xt, double x2, double gam,
+                                          double pack_rel, double& eap, double& rdhi) {
+  const double eacc = gam * (xt * ct + 0.5 * ct * ct);
+  eap = eacc + fabs(sc) * pack_rel;
+  rdhi = sqrt(fmax(0.0, x2 - 2.0 * sc) + 2.0 * eap + x2 * 0x1p-22);
+}
+
 __device__ __forceinline__ double group_sum16(double v) {
 #pragma unroll
   for (int off = 1; off < kRefineGroup; off <<= 1) v += __shfl_xor(v, off);
@@ -2339,7 +2349,7 @@ __device__ __forceinline__ void refine_q1_block(
     const int32_t* __restrict__ labels, const int32_t* __restrict__ cand,
     const float* __restrict__ score, const float* __restrict__ margin, long cs,
     uint32_t* __restrict__ qcount, ExactQ1* __restrict__ q1, long cap1,
-    unsigned long long* __restrict__ stats) {
+    unsigned long long* __restrict__ stats, const float* __restrict__ dcc) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int shard = blockIdx.x % kQShards;
   __shared__ uint32_t wcnt[4][kQ1Per];
@@ -2391,6 +2401,32 @@ __device__ __forceinline__ void refine_q1_block(
                   ((double)e[i].xe + (double)ceb[i]) * inflate, gam, pack_rel, eb, dl_b);
       exact_bound(sb - mm, cm, xn, x2, amax, gam, pack_rel, es, dl_s);
       flag[i] = !(mm > eb + es && dl_s >= 2.0 * amax);
+      const int b = e[i].b, sc = e[i].s, t = e[i].t;
+      if (flag[i] && dcc != nullptr && t < k && t != b) {
+        // Pair rule: D_s - D_b >= (D~_s - D~_b) - 2|c~_b - c~_s| e_x
+        //   - 2 sqrt(D~_s) e_s - 2 sqrt(D~_b) e_b - (e_x + e_b)^2
+        // (x - c_j = (x~ - c~_j) + (dx - dc_j); the dx terms of b and s
+        // cancel up to (c~_b - c~_s).dx), with |c~_b - c~_s| <= |c_b - c_s|
+        // + e_b + e_s — tighter than E_b + E_s where the two centroids are
+        // close and the point is not.  Everything ranked at or below t is
+        // beaten by the generic rule at t (margin b-t against E_b + E_max(t)).
+        const double ex = (double)e[i].xe * inflate;
+        const double ebb = (double)ceb[i] * inflate;
+        const double ess = (double)cerr[sc] * inflate;
+        const double dbs = ((double)dcc[(size_t)b * k + sc] + (double)ceb[i] +
+                            (double)cerr[sc]) * inflate;
+        double eap_b, rb, eap_s, rs;
+        score_err(sb, ((double)cnb[i] + (double)ceb[i]) * inflate, xn, x2, gam, pack_rel,
+                  eap_b, rb);
+        score_err(sb - mm, ((double)cnorm[sc] + (double)cerr[sc]) * inflate, xn, x2, gam,
+                  pack_rel, eap_s, rs);
+        const double ep = dbs * ex + rs * ess + rb * ebb + 0.5 * (ex + ebb) * (ex + ebb) +
+                          eap_b + eap_s;
+        double et, dl_t;
+        const double m3 = e[i].m3;
+        exact_bound(sb - m3, cm, xn, x2, amax, gam, pack_rel, et, dl_t);
+        if (mm > ep && m3 > eb + et && dl_t >= 2.0 * amax) flag[i] = false;
+      }
     }
     const unsigned long long m = __ballot(flag[i]);
     rank[i] = lane_rank(m);
@@ -2425,9 +2461,9 @@ __global__ __launch_bounds__(256) void kmeans_refine_q1_kernel(
     const int32_t* __restrict__ labels, const int32_t* __restrict__ cand,
     const float* __restrict__ score, const float* __restrict__ margin,
     uint32_t* __restrict__ qcount, ExactQ1* __restrict__ q1, long cap1,
-    unsigned long long* __restrict__ stats) {
+    unsigned long long* __restrict__ stats, const float* __restrict__ dcc) {
   refine_q1_block(n, sidx, blockIdx.x, d, k, xnorm, xbn2, xerr, cnorm, cmax, cerr, cerrmax,
-                  pack_rel, labels, cand, score, margin, n, qcount, q1, cap1, stats);
+                  pack_rel, labels, cand, score, margin, n, qcount, q1, cap1, stats, dcc);
 }
 
 // the splits of a batch in one launch (after the grouped top-3 assign): the
@@ -2449,7 +2485,7 @@ __global__ __launch_bounds__(256) void kmeans_refine_q1_grouped_kernel(
     const float* __restrict__ cerrmax, double pack_rel, const int32_t* __restrict__ labels,
     const int32_t* __restrict__ cand, const float* __restrict__ score,
     const float* __restrict__ margin, uint32_t* __restrict__ qcount, ExactQ1* __restrict__ q1,
-    long cap1, unsigned long long* __restrict__ stats) {
+    long cap1, unsigned long long* __restrict__ stats, const float* __restrict__ dcc) {
   const long b = blockIdx.x;
   int lo = 0, hi = tbl.nsplit;
   while (hi - lo > 1) {
@@ -2460,7 +2496,7 @@ __global__ __launch_bounds__(256) void kmeans_refine_q1_grouped_kernel(
   const long o = tbl.off[s];
   refine_q1_block(tbl.n[s], s, b - tbl.blk[s], d, k, tbl.xnorm[s], tbl.xbn2[s], tbl.xerr[s],
                   cnorm, cmax, cerr, cerrmax, pack_rel, labels + o, cand + o, score + o,
-                  margin + o, tbl.total, qcount, q1, cap1, stats);
+                  margin + o, tbl.total, qcount, q1, cap1, stats, dcc);
 }
 
 // 16 features of a row per lane of an 8-lane group: 128m + 32h + 4sub + (0..3)
@@ -2483,6 +2519,13 @@ __device__ __forceinline__ void load_row16(const float* __restrict__ r, int d, i
       o[0] = ok ? a.x : 0.f; o[1] = ok ? a.y : 0.f; o[2] = ok ? a.z : 0.f; o[3] = ok ? a.w : 0.f;
     }
   }
+}
+
+__device__ __forceinline__ float row_sum8f(float v) {
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  return v;
 }
 
 __device__ __forceinline__ double row_sum8(double v) {
@@ -2556,22 +2599,35 @@ __global__ __launch_bounds__(256) void kmeans_refine_q2_kernel(
     load_row16<NM>(C32 + (size_t)q.b * d, d, sub, c0);
     load_row16<NM>(C32 + (size_t)q.s * d, d, sub, c1r);
     load_row16<NM>(C32 + (size_t)(t_real ? q.t : q.b) * d, d, sub, c2);
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+    // fp32 distances (a third of the fp64 form's VALU work, which bound this
+    // kernel): every term goes through at most 16*NM + 3 roundings (lane fma
+    // chain + the 8-lane tree), so |D^ - D| <= rel * D + abs_eps; the winner is
+    // decided only where the three bands do not overlap, else the point goes
+    // to the neighbour scan, which restarts from w's exact fp64 distance
+    float f0 = 0.f, f1 = 0.f, f2 = 0.f;
 #pragma unroll
     for (int i = 0; i < 16 * NM; ++i) {
-      const double x = (double)xf[i];
-      const double e0 = x - (double)c0[i], e1 = x - (double)c1r[i], e2 = x - (double)c2[i];
-      a0 = fma(e0, e0, a0);
-      a1 = fma(e1, e1, a1);
-      a2 = fma(e2, e2, a2);
+      const float e0 = xf[i] - c0[i], e1 = xf[i] - c1r[i], e2 = xf[i] - c2[i];
+      f0 = fmaf(e0, e0, f0);
+      f1 = fmaf(e1, e1, f1);
+      f2 = fmaf(e2, e2, f2);
     }
-    const double d0 = row_sum8(a0), d1 = row_sum8(a1), d2 = row_sum8(a2);
+    f0 = row_sum8f(f0);
+    f1 = row_sum8f(f1);
+    f2 = row_sum8f(f2);
+    const double rel = (double)(16 * NM + 8) * 0x1p-24 * 1.01, aeps = 0x1p-120;
     int w = q.b;
-    double dw = d0;
-    if (d1 < dw || (d1 == dw && q.s < w)) { w = q.s; dw = d1; }
-    if (t_real && (d2 < dw || (d2 == dw && q.t < w))) { w = q.t; dw = d2; }
-    bool certified = !t_real;
-    if (t_real) {
+    double dw = f0;
+    if ((double)f1 < dw || ((double)f1 == dw && q.s < w)) { w = q.s; dw = f1; }
+    if (t_real && ((double)f2 < dw || ((double)f2 == dw && q.t < w))) { w = q.t; dw = f2; }
+    const double whi = dw * (1.0 + rel) + aeps;            // >= D_w
+    auto beats = [&](double dj) { return dj * (1.0 - rel) - aeps > whi; };
+    bool separated = isfinite(whi) &&
+                     (w == q.b || beats(f0)) && (w == q.s || beats(f1)) &&
+                     (!t_real || w == q.t || beats(f2));
+    dw = whi;
+    bool certified = !t_real && separated;
+    if (t_real && separated) {
       const double xn = ((double)q.xn + (double)q.xe) * inflate;
       const double x2 = (double)q.x2;
       const double amax = ((double)q.xe + cem) * inflate;
@@ -2643,7 +2699,15 @@ __global__ __launch_bounds__(256) void kmeans_refine_q3_kernel(
     }
     const int w0 = q.w;
     int w = w0;
-    double dw = q.dw;
+    // step 2 hands over its winner with an fp32 distance (an upper bound):
+    // the scan starts from w0's exact fp64 distance
+    double dw;
+    {
+      const float* c0p[1] = {C32 + (size_t)w0 * d};
+      double d0[1];
+      rows_dist2<NM, 1>(xv, c0p, d, sub, d0);
+      dw = d0[0];
+    }
     const double r0 = sqrt(dw);
     bool done = false;
     const int32_t* ni = nbr_idx + (size_t)w0 * L;
@@ -3356,7 +3420,7 @@ int hbmr_kmeans_refine_batch_q1(int nsplit, const long* ns, int s, int d, int k,
                                 const float* cerrmax, const int32_t* labels, const int32_t* cand,
                                 const float* scores, const float* margin,
                                 unsigned long long* stats, void* ws, long ws_bytes, int reset,
-                                hipStream_t st) {
+                                const float* dcc, hipStream_t st) {
   if (nsplit <= 0 || nsplit > kMaxGroup || s < 0 || s >= nsplit || k <= 0 || k_pad < k ||
       d > kRefineMaxDp || ((uintptr_t)ws & 255))
     return (int)hipErrorInvalidValue;
@@ -3376,7 +3440,7 @@ int hbmr_kmeans_refine_batch_q1(int nsplit, const long* ns, int s, int d, int k,
   hipLaunchKernelGGL(kmeans_refine_q1_kernel, dim3((unsigned)b1), dim3(256), 0, st, n, s, d, k,
                      xnorm, xbn2, xerr, cnorm, cmax, cerr, cerrmax, pack_rel, labels, cand,
                      scores, margin, c1, reinterpret_cast<ExactQ1*>(w + Ly.off1), Ly.cap1,
-                     reinterpret_cast<unsigned long long*>(w + kStatsOff));
+                     reinterpret_cast<unsigned long long*>(w + kStatsOff), dcc);
   return (int)hipGetLastError();
 }
 
@@ -3387,7 +3451,7 @@ int hbmr_kmeans_refine_batch_q1g(int nsplit, const long* ns, int d, int k, int k
                                  const float* const* xerr, const float* cnorm, const float* cmax,
                                  const float* cerr, const float* cerrmax, const int32_t* labels,
                                  const int32_t* cand, const float* scores, const float* margin,
-                                 void* ws, long ws_bytes, hipStream_t st) {
+                                 void* ws, long ws_bytes, const float* dcc, hipStream_t st) {
   if (nsplit <= 0 || nsplit > kMaxGroup || k <= 0 || k_pad < k || d > kRefineMaxDp ||
       ((uintptr_t)ws & 255))
     return (int)hipErrorInvalidValue;
@@ -3420,7 +3484,7 @@ int hbmr_kmeans_refine_batch_q1g(int nsplit, const long* ns, int d, int k, int k
   hipLaunchKernelGGL(kmeans_refine_q1_grouped_kernel, dim3((unsigned)nb), dim3(256), 0, st, t, d,
                      k, cnorm, cmax, cerr, cerrmax, pack_rel, labels, cand, scores, margin, c1,
                      reinterpret_cast<ExactQ1*>(w + Ly.off1), Ly.cap1,
-                     reinterpret_cast<unsigned long long*>(w + kStatsOff));
+                     reinterpret_cast<unsigned long long*>(w + kStatsOff), dcc);
   return (int)hipGetLastError();
 }
 
@@ -3453,7 +3517,9 @@ int hbmr_kmeans_refine_batch_finish(int nsplit, const long* ns, const float* con
   const ExactQ1* q1 = reinterpret_cast<const ExactQ1*>(w + Ly.off1);
   ExactQ2* q2 = reinterpret_cast<ExactQ2*>(w + Ly.off2);
   unsigned long long* ss = reinterpret_cast<unsigned long long*>(w + kStatsOff);
-  const unsigned g3 = std::max(1u, std::min(Ly.g2, (unsigned)(kRefineGrid / 4)));
+  // (q3 walks each point's neighbours through a chain of dependent loads:
+  // a full grid keeps 4x more points in flight than the quarter grid did)
+  const unsigned g3 = std::max(1u, Ly.g2);
   if (d <= 128) {
     hipLaunchKernelGGL(kmeans_refine_q2_kernel<1>, dim3(Ly.g2), dim3(256), 0, st, tbl, d, ldx,
                        C32, k, cmax, cerrmax, pack_rel, c1, q1, Ly.cap1, c2, q2, Ly.cap2, ss);

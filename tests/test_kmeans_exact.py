@@ -330,5 +330,11 @@ def test_refine_queue_pipeline_equals_single_kernel(dtype, monkeypatch):
         lab = km.assign_exact(sp, img, st, {}).clone()
         out[v] = (lab, st.tolist())
     assert torch.equal(out[2][0], out[3][0])
-    assert out[2][1][:3] == out[3][1][:3] and out[3][1][0] > 0
+    # v3 flags fewer points (step 1's pair rule) and relabels the same ones;
+    # its step 2 decides in fp32 with error bands and defers the (rare) points
+    # inside a band to the neighbour scan
+    f2, r2, n2 = out[2][1][:3]
+    f3, r3, n3 = out[3][1][:3]
+    assert 0 < f3 <= f2 and r2 == r3
+    assert n3 <= n2 + max(16, f3 // 1000)
     assert int((out[3][0] != truth_labels(x, c)).sum()) <= 1

@@ -66,14 +66,19 @@ def main():
         job, the output directory cleared outside the timed region."""
         import shutil
         total = 0.0
-        for _ in range(a.steps):
+        for i in range(a.steps):
+            print(f"bench_terasort: sort with output {i + 1}/{a.steps}", file=sys.stderr,
+                  flush=True)
             shutil.rmtree(a.output, ignore_errors=True)
             node.submit_job(sync_conf(conf)).waitForCompletion()
             t0 = time.perf_counter()
             job(a.output)
             node.submit_job(sync_conf(conf)).waitForCompletion()
             total += time.perf_counter() - t0
-        v = T.teravalidate(a.output)
+        def prog(i, nf):
+            if i % 8 == 0:
+                print(f"bench_terasort: validating part {i}/{nf}", file=sys.stderr, flush=True)
+        v = T.teravalidate(a.output, progress=prog)
         return total / a.steps, v
 
     try:
@@ -106,6 +111,10 @@ def main():
                           "peak_hbm_gb_per_gpu": round(max(r.get("peak_hbm_bytes", 0)
                                                            for r in res.values()) / 1e9, 2),
                           "defines": a.defines,
+                          "hbm_budget_gb": conf.get_float("hbmr.terasort.hbm.budget.gb", 0.0)
+                          or None,
+                          "spilled_records": rj.getCounters().get(
+                              "org.apache.hadoop.mapred.Task$Counter", "MAP_SPILLED_RECORDS"),
                           "timeline": rj._impl.jip.timeline(), **out_extra}))
     finally:
         node.shutdown()
