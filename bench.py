@@ -306,6 +306,18 @@ def spawn_ranks(n):
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
                                       env=env, start_new_session=True))
     rc = 0
+
+    def _term(signum, _frame):
+        # the ranks run in sessions of their own: a SIGTERM to this launcher
+        # (timeout, the driver) must not leave them behind
+        for q in procs:
+            try:
+                os.killpg(q.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+        raise SystemExit(128 + signum)
+    signal.signal(signal.SIGTERM, _term)
+    signal.signal(signal.SIGHUP, _term)
     try:
         live = list(procs)
         while live:

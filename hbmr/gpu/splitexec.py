@@ -155,6 +155,10 @@ def run_split_reduce(host, run, device=None):
         rep = TaskReporter()
         run.task = SplitTaskShim(rep, run.kill)
         ctx = TaskContext(host, js, spec, rep)
+        # a reduce killed by a gang restart must not publish its result (the
+        # restarted gang's attempt publishes the same key): the split job
+        # checks this right before it does
+        ctx.killed = run.kill.is_set
         hconf = getattr(host, "conf", None)
         if hconf is not None and hconf.get_boolean("hbmr.gpu.simulate.nodata", False) and \
                 (hconf.get("hbmr.gpu.simulate.collective") or "device") == "device":

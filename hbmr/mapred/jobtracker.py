@@ -71,6 +71,9 @@ class TrackerInfo:
         # _kick() when new work may exist for every tracker
         self.bell = threading.Event()
         self.more = False    # the last assignment stopped at the per-heartbeat cap
+        # responses carrying actions are numbered (under the JobTracker lock):
+        # the tracker applies them in this order whichever thread receives them
+        self.resp_seq = 0
         self.rack = DEFAULT_RACK
         self.kills: set[str] = set()   # attempts to kill on the next heartbeat
         self.kill_epoch = -1           # JobTracker.kill_epoch this tracker was last scanned at
@@ -521,6 +524,9 @@ class JobTracker:
         self.kill_epoch = 0    # bumped when attempts may have become killable
         self.prestage = conf.get_boolean("hbmr.job.prestage", True)
         self.prestage_depth = max(1, conf.get_int("hbmr.job.prestage.depth", 2))
+        # trackers get their new work back in the report of a finished task
+        # (TaskTracker.report_assign, the same cluster key)
+        self.report_assign_expected = conf.get_boolean("hbmr.tracker.report.assign", True)
         self.trackers: dict[str, TrackerInfo] = {}
         self.attempt_index: dict[str, Attempt] = {}
         self.cost_model = CostModel(conf.get_float("hbmr.costmodel.ewma.alpha", 0.3))
@@ -808,7 +814,11 @@ class JobTracker:
         w.staged_on = str(j.job_id)
         self.staged.append(w)
         self.history.log("JOB_STAGED", job=str(w.job_id), gate=str(j.job_id))
-        self._kick()
+        # staged behind a job that is itself staged: its maps cannot run before
+        # two reduces have completed, and every tracker of the gang reports
+        # each completion (JobTracker.report assigns): no long-poll wake-up
+        if j.staged_on is None or not self.report_assign_expected:
+            self._kick()
 
     def _memory_violation(self, conf):
         """JobTracker.checkMemoryRequirements: a job asking for more memory per
@@ -925,10 +935,19 @@ class JobTracker:
                     self._maybe_stage(x, w)
             else:
                 self._finish_job(w, FAILED, f"job {jip.job_id} it depends on {state}")
-        if state == SUCCEEDED:
+        if state == SUCCEEDED and self._assignable():
             self._kick()
         for cb in self.listeners:
             cb("finished", jip)
+
+    def _assignable(self) -> bool:
+        """Work a long-polling tracker could be handed now: a queued job with
+        pending maps or reduces not yet running (staged jobs' maps are already
+        launched; their trackers report before those maps can run)."""
+        for jip in self.job_queue:
+            if jip.pending_maps or (jip.reduces and self._reduces_waiting(jip)):
+                return True
+        return False
 
     # -- heartbeat ----------------------------------------------------------------------
     def wakeup(self, tracker_name: str, seq: int | None = None):
@@ -965,7 +984,7 @@ class JobTracker:
             return {"reinit": True}
         if assign:
             resp = self._heartbeat(status, False, True)
-            return {"actions": resp["actions"]}
+            return {"actions": resp["actions"], "seq": resp.get("seq")}
         resp = self._heartbeat(status, False, False)
         if resp["actions"]:
             with self.lock:
@@ -1037,6 +1056,9 @@ class JobTracker:
                     resp["actions"] += self.scheduler.assign_tasks(tr)
                     if TRACE.on:
                         TRACE.instant("jt.assigned", n=len(resp["actions"]))
+                if resp["actions"]:
+                    tr.resp_seq += 1
+                    resp["seq"] = tr.resp_seq
         tr.wake = False
         resp["more"] = tr.more
         return self._with_lazy(tr, resp)
@@ -1046,6 +1068,9 @@ class JobTracker:
             with self.lock:
                 resp["actions"] += tr.lazy_actions
                 tr.lazy_actions = []
+                if "seq" not in resp:
+                    tr.resp_seq += 1
+                    resp["seq"] = tr.resp_seq
         return resp
 
     def _heartbeat(self, status, initial, accept_new_tasks):
@@ -1112,7 +1137,13 @@ class JobTracker:
                 actions = pre + actions + [x for x in tr.extra_actions
                                            if x["type"] != "close_gate"]
                 tr.extra_actions = []
-        return {"actions": actions, "interval": self.heartbeat_interval, "more": tr.more}
+            resp = {"actions": actions, "interval": self.heartbeat_interval, "more": tr.more}
+            if actions:
+                # numbered under the lock that drained the tracker's queues:
+                # the numbering is the order the actions were produced in
+                tr.resp_seq += 1
+                resp["seq"] = tr.resp_seq
+        return resp
 
     def _update_task_status(self, tr: TrackerInfo, ts: P.TaskStatus, actions):
         a = self.attempt_index.get(ts.attempt_id)

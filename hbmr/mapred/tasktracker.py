@@ -147,6 +147,11 @@ class TaskTracker:
         # thread can wait that long for the interpreter while another one
         # runs bookkeeping, idling the GPU.  0.2 ms keeps hand-offs prompt.
         self.defer_map_reports = conf.get_boolean("hbmr.tracker.defer.map.reports", True)
+        self._act_lock = threading.RLock()   # JobTracker actions, applied one at a time
+        self._resp_cond = threading.Condition()
+        self._next_seq = 1                   # JobTracker response order (resp["seq"])
+        self._deferred: dict = {}            # job id -> launches that came before its conf
+        self._early_kills: dict = {}         # attempts killed before their launch arrived
         # JobTracker.report assigns and returns actions (no long-poll wake-up)
         self.report_assign = conf.get_boolean("hbmr.tracker.report.assign", True)
         # news reaches a long-polling JobTracker as one report call
@@ -458,8 +463,7 @@ class TaskTracker:
                 if not (isinstance(r, dict) and r.get("reinit")):
                     # (assign form) the response carries this tracker's new
                     # work: handled here, the long-poll stays parked
-                    for act in (r or {}).get("actions", ()):
-                        self._handle(act)
+                    self._apply(r or {})
                     return
             except Exception:  # noqa: BLE001
                 pass
@@ -519,6 +523,7 @@ class TaskTracker:
                         self._polling = False
                 if TRACE.on:
                     TRACE.instant("tt.heartbeat.send", reports=len(st.task_reports), block=block)
+                initial_sent = initial
                 try:
                     resp = self.jt.heartbeat(st.to_dict(), initial=initial,
                                              accept_new_tasks=True, block=block)
@@ -530,8 +535,11 @@ class TaskTracker:
                 self.heartbeats += 1
                 initial = False
                 more = bool(resp.get("more"))
-                for act in resp.get("actions", []):
-                    self._handle(act)
+                if initial_sent:
+                    with self._resp_cond:
+                        self._next_seq = 1       # a (re-)registered tracker: new numbering
+                        self._resp_cond.notify_all()
+                self._apply(resp)
                 if self._reinit:
                     self._reinit = False
                     initial = True
@@ -569,15 +577,64 @@ class TaskTracker:
                                           f"for {limit:g} seconds. Killing!")
 
     # -- actions -------------------------------------------------------------------------
+    def _apply(self, resp):
+        """Apply a JobTracker response's actions in the JobTracker's order: a
+        response numbered ``seq`` waits (up to 2 s) until every earlier one has
+        been applied by whichever thread received it — a report's response and
+        the long-poll's can come back in either order."""
+        acts = resp.get("actions") or ()
+        seq = resp.get("seq")
+        if seq is None:
+            for act in acts:
+                self._handle(act)
+            return
+        with self._resp_cond:
+            deadline = time.time() + 2.0
+            while seq > self._next_seq and time.time() < deadline:
+                self._resp_cond.wait(deadline - time.time())
+            try:
+                for act in acts:
+                    self._handle(act)
+            finally:
+                self._next_seq = max(self._next_seq, seq + 1)
+                self._resp_cond.notify_all()
+
     def _handle(self, act):
+        """Apply one JobTracker action.  Actions arrive from the heartbeat
+        thread and (JobTracker.report with assign) from the thread that
+        reported finished tasks, so two responses may be applied out of the
+        order the JobTracker built them in: the first launch of a job on this
+        tracker carries the job's configuration, and a launch of a job not yet
+        known here without it is held until that one arrives."""
+        with self._act_lock:
+            self._handle_locked(act)
+
+    def _handle_locked(self, act):
         typ = act["type"]
-        if typ == "launch_batch":
-            self._launch_batch(act)
-        elif typ == "launch":
-            self._launch(P.TaskSpec.from_dict(act["task"]))
+        if typ in ("launch_batch", "launch"):
+            jid = act["job_id"] if typ == "launch_batch" else act["task"]["job_id"]
+            conf = act.get("conf") if typ == "launch_batch" else act["task"].get("conf")
+            if jid not in self.jobs and not conf:
+                self._deferred.setdefault(jid, []).append(act)
+                return
+            if typ == "launch_batch":
+                self._launch_batch(act)
+            else:
+                self._launch(P.TaskSpec.from_dict(act["task"]))
+            for later in self._deferred.pop(jid, ()):
+                self._handle_locked(later)
+        elif typ == "kill_job" and act["job_id"] in self._deferred:
+            self._deferred.pop(act["job_id"], None)
+            self._handle_kill_job(act)
         elif typ == "kill_task":
             with self._lock:
                 r = self.running.get(act["attempt_id"])
+                if r is None:
+                    # not launched here yet (its launch may still be held):
+                    # the launch is dropped when it comes
+                    self._early_kills[act["attempt_id"]] = None
+                    while len(self._early_kills) > 4096:
+                        self._early_kills.pop(next(iter(self._early_kills)))
             if r is not None:
                 r.kill.set()
                 if r.task is not None and getattr(r.task, "kill_event", None) is not None:
@@ -596,18 +653,7 @@ class TaskTracker:
             if r is not None:
                 r.status.commit_granted = True  # picked up by the waiting task
         elif typ == "kill_job":
-            # KillJobAction: the job is finished or killed; purge its state here
-            # and in the GPU worker (held device map outputs, worker JobState)
-            jid = act["job_id"]
-            js = self.jobs.pop(jid, None)
-            if js is not None and js.result is not None:
-                self._results[jid] = js.result
-                while len(self._results) > 64:
-                    self._results.pop(next(iter(self._results)))
-            if getattr(self.gpu_runtime, "remote", False):
-                self.gpu_runtime.drop_job(jid)
-            if self.child_manager is not None:
-                self.child_manager.job_done(jid)
+            self._handle_kill_job(act)
         elif typ == "reinit":
             # the JobTracker does not know us (it restarted, or expired us):
             # drop every attempt and job, re-advertise the HBM-resident splits
@@ -629,6 +675,20 @@ class TaskTracker:
         elif typ == "shutdown":
             self._stop.set()
 
+    def _handle_kill_job(self, act):
+        """KillJobAction: the job is finished or killed; purge its state here
+        and in the GPU worker (held device map outputs, worker JobState)."""
+        jid = act["job_id"]
+        js = self.jobs.pop(jid, None)
+        if js is not None and js.result is not None:
+            self._results[jid] = js.result
+            while len(self._results) > 64:
+                self._results.pop(next(iter(self._results)))
+        if getattr(self.gpu_runtime, "remote", False):
+            self.gpu_runtime.drop_job(jid)
+        if self.child_manager is not None:
+            self.child_manager.job_done(jid)
+
     def _job(self, spec: P.TaskSpec) -> JobState:
         js = self.jobs.get(spec.job_id)
         if js is None:
@@ -643,6 +703,8 @@ class TaskTracker:
         return js
 
     def _launch(self, spec: P.TaskSpec):
+        if self._early_kills.pop(spec.attempt_id, 0) is None:
+            return          # killed before it got here (the JobTracker already knows)
         js = self._job(spec)
         st = P.TaskStatus(attempt_id=spec.attempt_id, is_map=spec.is_map, state=P.RUNNING,
                           run_on_gpu=spec.run_on_gpu, gpu_device_id=spec.gpu_device_id,
@@ -701,6 +763,8 @@ class TaskTracker:
             runs = []
             gate = act.get("gate")
             for aid, part, split in tasks[lo:hi]:
+                if self._early_kills.pop(aid, 0) is None:
+                    continue    # killed before its launch arrived
                 spec = P.TaskSpec(aid, jid, True, part, True, dev, split, nm, nr, (), coll,
                                   gate=gate)
                 st = P.TaskStatus(aid, True, P.RUNNING, 0.0, True, dev, now)

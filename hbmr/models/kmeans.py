@@ -135,12 +135,20 @@ class CentroidStore:
         self.keep = 4
 
     def put_host(self, key, cen):
+        """New host centroids of ``key``: device images of an earlier version
+        of the key (a restarted reduce re-publishing it) are dropped."""
         with self.lock:
             self.host[key] = cen
+            for k in [k for k in self.images if k[0] == key]:
+                self.images.pop(k)
             self._touch(key)
 
     def put_image(self, key, device, img):
+        """A device image of ``key``; a host copy of an earlier version is
+        dropped (re-derived from the images on demand).  Every device's image
+        of one key comes from the same all-reduced sums."""
         with self.lock:
+            self.host.pop(key, None)
             self.images[(key, str(device))] = img
             self._touch(key)
 
@@ -743,6 +751,9 @@ class KMeansSplitJob(SplitJob):
                 ctx.reporter.incrCounter("KMEANS", "EXACT_FLAGGED_POINTS", flagged)
                 ctx.reporter.incrCounter("KMEANS", "EXACT_RELABELLED_POINTS", relabelled)
                 ctx.reporter.incrCounter("KMEANS", "EXACT_NEIGHBOUR_SCANS", rescans)
+        killed = getattr(ctx, "killed", None)
+        if killed is not None and killed():
+            raise RuntimeError("reduce killed (collective restart): result not published")
         if sums.device.type == "cuda":
             old = STORE.image(self.cin, sums.device)
             img = km.CentroidImage.__new__(km.CentroidImage)

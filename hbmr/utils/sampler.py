@@ -184,6 +184,17 @@ def maybe_watch_jobtracker(jt):
                             f"done={j.maps_done} reduces_done="
                             f"{sum(1 for r in j.reduces if r.successful)}/{len(j.reduces)} "
                             f"staged_on={j.staged_on} expect={j.expect_mode}")
+                        for r in j.reduces:
+                            if r.successful is None:
+                                lines.append("    reduce " + str(r.tid) + " attempts " + ", ".join(
+                                    f"{a.aid[-12:]}@{a.tracker[-3:]}:{a.state}"
+                                    for a in r.attempts.values()))
+                    evs = [e for e in list(getattr(jt.history, "events", []))
+                           if any(w in e.get("event", "") for w in ("FAILED", "RESTART", "LOST",
+                                                                     "KILLED"))]
+                    for e in evs[-6:]:
+                        lines.append(f"  event {e.get('event')} {e.get('attempt') or e.get('job')}"
+                                     f" {str(e.get('diag', ''))[:300]!r}")
                     for name, tr in jt.trackers.items():
                         lines.append(f"  tracker {name}: running={len(tr.running)} "
                                      f"gpu={dict(tr.running_gpu)} cpu={tr.running_cpu} "
