@@ -366,8 +366,13 @@ def serve(sock):
 
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
-    from ..utils.sampler import maybe_arm_stackdump
+    from ..utils.sampler import dump_profiles, maybe_arm_stackdump, maybe_profile_threads, \
+        maybe_start
     maybe_arm_stackdump()
+    # the bench's control-plane profilers (HBMR_CPROFILE / HBMR_SAMPLE_PROF)
+    # cover the worker too: its per-map bookkeeping is on the job's critical path
+    cprof = maybe_profile_threads()
+    sampler = maybe_start()
     sock = socket.socket(fileno=int(argv[0]))
     try:
         rc = serve(sock)
@@ -376,11 +381,28 @@ def main(argv=None):
             sock.close()
         except OSError:
             pass
+        if cprof:
+            dump_profiles(cprof)
+        if sampler is not None:
+            sampler.dump()
     sys.stdout.flush()
     sys.stderr.flush()
     if os.environ.get("HBMR_WORKER_CLEAN_EXIT") or \
             any(k.startswith("ROCPROF") for k in os.environ):
-        # a normal exit, so a profiler's exit handlers write this process's trace
+        # a normal exit, so a profiler's exit handlers write this process's
+        # trace.  Threads still inside HIP calls while the interpreter and the
+        # HIP runtime tear down ended the worker in std::terminate under the
+        # tracer: let them drain first (reduce threads, pools), bounded.
+        deadline = time.time() + 10.0
+        for t in threading.enumerate():
+            if t is not threading.current_thread() and t.is_alive():
+                t.join(timeout=max(0.0, deadline - time.time()))
+        try:
+            import torch
+            if torch.cuda.is_initialized():
+                torch.cuda.synchronize()
+        except Exception:  # noqa: BLE001
+            pass
         sys.exit(rc)
     # skip interpreter teardown of the HIP runtime / process group (the parent
     # only needs the exit status; the grid has drained in serve())

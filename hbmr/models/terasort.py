@@ -114,7 +114,15 @@ class TeraSortSplitJob(SplitJob):
         # outputs (in launch order), each wave's all-to-all-v issued as soon as
         # its maps are done — with an early reduce (expect mode,
         # hbmr.job.prestage) it overlaps the later maps (map ∥ shuffle)
-        self.waves = max(1, conf.get_int("hbmr.terasort.shuffle.waves", 1))
+        # (0, the default: 4 when the job runs on several ranks, else 1)
+        self.waves_conf = max(0, conf.get_int("hbmr.terasort.shuffle.waves", 0))
+        # the waves' all-to-alls are static-shape: each destination slot is
+        # sized from the split sizes and the partition share (x this slack),
+        # the counts travel as a tensor and are read on the device, so no wave
+        # waits on the host for its maps; one count check after the last wave
+        # (an overflowing slot re-runs the shuffle with exact sizes)
+        self.static_a2a = conf.get_boolean("hbmr.terasort.shuffle.static", True)
+        self.slot_slack = conf.get_float("hbmr.terasort.shuffle.slot.slack", 1.08)
         # one-rank reduce: sort (high key word, packed record id) and gather by
         # the id (v4, default: 0.284 s per 100 GB sort vs 0.341 s for v3 on the
         # same box, profiles/r03_terasort_100gb_v4_1gpu.json); false = the v3
@@ -275,13 +283,21 @@ class TeraSortSplitJob(SplitJob):
     def owner_range(rank, world, nparts):
         return rank * nparts // world, (rank + 1) * nparts // world
 
+    def waves_for(self, world):
+        """Shuffle waves for a job on ``world`` ranks (the same on every rank:
+        the collective sequence must match)."""
+        if self.waves_conf:
+            return self.waves_conf
+        return 4 if world > 1 else 1
+
     @property
     def orders_own_outputs(self):
-        """Wave mode waits on each map output's event itself."""
-        return self.waves > 1
+        """Wave mode waits on each map output's event itself (combine() waits
+        on all of them when one rank runs the job)."""
+        return self.waves_conf != 1
 
     def combine(self, ctx, outputs):
-        if self.waves > 1 and ctx.comm.world_size > 1:
+        if self.waves_for(ctx.comm.world_size) > 1 and ctx.comm.world_size > 1:
             marks = getattr(ctx, "output_marks", None) or [None] * len(outputs)
             keep = [(o, m) for o, m in zip(outputs, marks) if o is not None]
             return {"outs": [o for o, _ in keep], "marks": [m for _, m in keep], "waves": True,
@@ -565,11 +581,21 @@ class TeraSortSplitJob(SplitJob):
         nparts, spl = self._agree_parts(comm, outs, nparts)
         cuda = dev.type == "cuda"
         cur = torch.cuda.current_stream() if cuda else None
+        waves = self.waves_for(W)
+        if self.static_a2a and not self.sorted_runs:
+            got = self._shuffle_static(comm, outs, marks, nparts, waves, dev)
+            if got is not None:
+                recv, csum = got
+                return self._sort_received(ctx, recv, spl, nparts, W, me, dev), csum
+            # a slot overflowed on some rank: every rank re-runs the shuffle
+            # with exact sizes (the maps' outputs are still held)
+            if TRACE.on:
+                TRACE.instant("tera.shuffle.static_overflow")
         n_local = len(outs)
-        bounds = [n_local * g // self.waves for g in range(self.waves + 1)]
+        bounds = [n_local * g // waves for g in range(waves + 1)]
         csum = torch.zeros((), dtype=torch.int64, device=dev)
         recvs, rcs = [], []
-        for g in range(self.waves):
+        for g in range(waves):
             grp = outs[bounds[g]:bounds[g + 1]]
             if cuda:
                 for m in {id(m): m for m in marks[bounds[g]:bounds[g + 1]]
@@ -596,15 +622,109 @@ class TeraSortSplitJob(SplitJob):
             return (0, None), csum
         if self.sorted_runs:
             srt, hs, ls = self._merge_received(recv, runs_counts)
-        else:
-            srt, hs, ls = S.sort_records(recv)
+            del recv
+            return self._owned_stats(ctx, srt, hs, ls, spl, nparts, W, me, dev), csum
+        return self._sort_received(ctx, recv, spl, nparts, W, me, dev), csum
+
+    def _sort_received(self, ctx, recv, spl, nparts, W, me, dev):
+        if recv.shape[0] == 0:
+            return 0, None
+        srt, hs, ls = S.sort_records(recv)
         del recv
+        return self._owned_stats(ctx, srt, hs, ls, spl, nparts, W, me, dev)
+
+    def _owned_stats(self, ctx, srt, hs, ls, spl, nparts, W, me, dev):
         n = int(srt.shape[0])
         st = torch.cat([S.count_unsorted_dev(hs, ls).reshape(1),
                         (hs.sum() + ls.sum()).reshape(1), hs[:1], ls[:1], hs[-1:], ls[-1:]])
         if self.out:
             self._write_owned(ctx, srt, hs, ls, spl, nparts, W, me, n, dev)
-        return (n, st), csum
+        return n, st
+
+    def _slot_capacity(self, grp, nparts, W):
+        """Records per destination slot of one wave: the wave's records times
+        the largest destination's share of the partitions (sampled splitters
+        cut near-equal partitions), times the slack, plus a floor.  Host-side
+        shapes only — no device value is read."""
+        rows = sum(int(o["row"].shape[0]) for o in grp)
+        share = max(self.owner_range(d, W, nparts)[1] - self.owner_range(d, W, nparts)[0]
+                    for d in range(W)) / max(1, nparts)
+        return max(1024, int(rows * share * self.slot_slack) + 1024)
+
+    def _shuffle_static(self, comm, outs, marks, nparts, waves, dev):
+        """The shuffle waves as static-shape all-to-alls (see ``static_a2a``).
+        Wave g: wait (on the device) for its maps' events; per-destination
+        piece starts, lengths and slot prefixes from the maps' device offsets;
+        one collect + gather into W slots of ``cap`` records; one all-to-all
+        of the slots and one of the counts.  After the last wave ONE host read
+        (the received counts and an all-reduced overflow flag) compacts the
+        received slots.  Returns (received records, input checksum), or None
+        if any rank's slot overflowed (the caller falls back, collectively)."""
+        W = comm.world_size
+        cuda = dev.type == "cuda"
+        cur = torch.cuda.current_stream() if cuda else None
+        n_local = len(outs)
+        bounds = [n_local * g // waves for g in range(waves + 1)]
+        own = [self.owner_range(d, W, nparts) for d in range(W)]
+        ia = torch.tensor([a for a, _ in own], dtype=torch.int64, device=dev)
+        ib = torch.tensor([b for _, b in own], dtype=torch.int64, device=dev)
+        # the capacity must be the same on every rank (equal-split all-to-all):
+        # the largest wave of any rank decides it (one small host collective
+        # before any map output is read)
+        caps = [self._slot_capacity(outs[bounds[g]:bounds[g + 1]], nparts, W) if
+                bounds[g + 1] > bounds[g] else 0 for g in range(waves)]
+        capt = torch.stack(comm.all_gather(torch.tensor(caps, dtype=torch.int64)))
+        caps = [int(c) for c in capt.cpu().max(0).values.tolist()]
+        csum = torch.zeros((), dtype=torch.int64, device=dev)
+        over = torch.zeros((), dtype=torch.int64, device=dev)
+        recvs, rcnts = [], []
+        for g in range(waves):
+            grp = outs[bounds[g]:bounds[g + 1]]
+            cap = caps[g]
+            if cap == 0:
+                continue          # no rank has maps in this wave: nothing moves
+            if cuda:
+                for m in {id(m): m for m in marks[bounds[g]:bounds[g + 1]]
+                          if m is not None}.values():
+                    cur.wait_event(m)
+            if grp:
+                offs = torch.stack([o["offsets"].to(dev) for o in grp])      # [S, R+1]
+                csum = csum + torch.stack([o["checksum"].reshape(()).to(dev)
+                                           for o in grp]).sum()
+                starts = offs.index_select(1, ia)                              # [S, W]
+                lens = offs.index_select(1, ib) - starts
+                pre = torch.cat([torch.zeros(W, 1, dtype=torch.int64, device=dev),
+                                 lens.t().cumsum(1)], 1)                       # [W, S+1]
+                cnt = pre[:, -1]
+                over = over + (cnt > cap).sum()
+                split, row = S.tera_collect_slots([o["row"] for o in grp], starts, pre, cap)
+                send = S.gather_records_multi([o["records"] for o in grp], split, row)
+                del split, row
+                sent = torch.clamp(cnt, max=cap)
+            else:
+                send = torch.empty(W * cap, S.RECORD, dtype=torch.uint8, device=dev)
+                sent = torch.zeros(W, dtype=torch.int64, device=dev)
+            if TRACE.on:
+                TRACE.instant("tera.wave.send_static", wave=g, cap=cap)
+            recvs.append((comm.all_to_all_fixed(send), cap))
+            rcnts.append(comm.all_to_all_fixed(sent))
+            del send
+        over = comm.all_reduce(over.reshape(1))
+        if not recvs:
+            return torch.empty(0, S.RECORD, dtype=torch.uint8, device=dev), csum
+        # the one host read of the shuffle: received counts + the overflow flag
+        host = torch.cat([over.reshape(1).to(dev)] + [r.to(dev) for r in rcnts]).cpu().tolist()
+        if host[0]:
+            return None
+        pieces, at = [], 1
+        for recv, cap in recvs:
+            for src in range(W):
+                c = int(host[at + src])
+                if c:
+                    pieces.append(recv[src * cap:src * cap + c])
+            at += W
+        recv = torch.cat(pieces) if pieces else recvs[0][0][:0]
+        return recv, csum
 
     def _write_owned(self, ctx, srt, hs, ls, spl, nparts, W, me, n, dev):
         a, b = self.owner_range(me, W, nparts)

@@ -100,6 +100,8 @@ _SIGS = {
                                     c_void_p, c_void_p, c_void_p]),
     "hbmr_tera_collect": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_long,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "hbmr_tera_collect_slots": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_long,
+                                        c_void_p, c_void_p, c_void_p]),
     "hbmr_gather_records_multi": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int,
                                           c_void_p, c_void_p]),
     "hbmr_tera_partition_workspace_bytes": (c_long, [c_long, c_int]),

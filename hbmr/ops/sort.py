@@ -441,6 +441,42 @@ def tera_collect(his, los, rows, starts, lens, with_keys=True, stream=None):
     return ohi, olo, split, row
 
 
+NO_SPLIT = 0xFFFFFFFF
+
+
+def tera_collect_slots(rows, starts: torch.Tensor, pre: torch.Tensor, cap: int, stream=None):
+    """Static-shape shuffle send layout: (split, row) int32 [W * cap] — slot d
+    holds destination d's pieces in split order (piece s = rows[s][starts[s, d]
+    + i] for i < pre[d, s+1] - pre[d, s], at pre[d, s] + i), entries past
+    min(pre[d, S], cap) carry split = NO_SPLIT (gather_records_multi leaves
+    those records unwritten).  ``starts`` [S, W] and ``pre`` [W, S+1] (int64)
+    stay on the device: nothing here waits for the maps that produced them."""
+    S = len(rows)
+    W = pre.shape[0]
+    dev = rows[0].device
+    if not _on_gpu(rows[0]):
+        split = torch.full((W * cap,), -1, dtype=torch.int32)   # NO_SPLIT's bits
+        row = torch.zeros(W * cap, dtype=torch.int32)
+        st, pr = starts.tolist(), pre.tolist()
+        for d in range(W):
+            for s in range(S):
+                a, b = pr[d][s], min(pr[d][s + 1], cap)
+                if b <= a:
+                    continue
+                split[d * cap + a:d * cap + b] = s
+                row[d * cap + a:d * cap + b] = rows[s][st[s][d]:st[s][d] + (b - a)]
+        return split, row
+    split = torch.empty(W * cap, dtype=torch.int32, device=dev)
+    row = torch.empty(W * cap, dtype=torch.int32, device=dev)
+    starts = starts.to(dev, torch.int64).contiguous()
+    pre = pre.to(dev, torch.int64).contiguous()
+    tr = _ptr_table(rows, dev)
+    rc = _lib.load().hbmr_tera_collect_slots(_ptr(tr), _ptr(starts), _ptr(pre), S, W, cap,
+                                              _ptr(split), _ptr(row), _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_tera_collect_slots")
+    return split, row
+
+
 GID_MAX_SPLITS = 256
 GID_MAX_ROWS = 1 << 24
 

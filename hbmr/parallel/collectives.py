@@ -61,6 +61,16 @@ class Comm:
         ins = self.all_to_all(outs)
         return (torch.cat(ins) if ins else send[:0]), [int(t.shape[0]) for t in ins]
 
+    def all_to_all_fixed(self, send: torch.Tensor) -> torch.Tensor:
+        """Static-shape all-to-all: ``send`` is W equal slots along dim 0, slot j
+        goes to rank j; returns the W slots received, ordered by source.  No
+        sizes are exchanged first, so nothing waits on the host: the caller
+        sends the valid counts as another fixed-shape tensor and reads them on
+        the device (TeraSort's shuffle waves)."""
+        self._note("all_to_all_fixed", send)
+        ins = self.all_to_all(list(torch.chunk(send, self.world_size)))
+        return torch.cat(ins)
+
     def reduce_scatter(self, t: torch.Tensor) -> torch.Tensor:
         """Sum over ranks, rank r keeps rows [r*n/W, (r+1)*n/W) (dim 0 padded by caller)."""
         full = self.all_reduce(t)
@@ -234,6 +244,20 @@ class TorchComm(Comm):
         self.dist.all_to_all_single(recv, send.contiguous(), output_split_sizes=rcounts,
                                     input_split_sizes=[int(c) for c in counts], group=group)
         return recv, rcounts
+
+    def all_to_all_fixed(self, send):
+        if send.shape[0] % self.world_size:
+            raise ValueError("all_to_all_fixed: dim 0 must be W equal slots")
+        if self._staged("all_to_all_fixed", send):
+            h = send.contiguous().cpu()
+            out = torch.empty_like(h)
+            self.dist.all_to_all_single(out, h, group=self.cpu_group or self.group)
+            return out.to(send.device)
+        out = torch.empty_like(send)
+        # one RCCL alltoall of equal slots: enqueued on the current stream
+        # behind the kernels that filled ``send``, no host round trip
+        self.dist.all_to_all_single(out, send.contiguous(), group=self._grp(send))
+        return out
 
     def all_to_all_v(self, send, counts):
         if self._staged("all_to_all_v", send):

@@ -112,6 +112,11 @@ int hbmr_tera_collect(const uint64_t* const* his, const uint64_t* const* los,
                       const uint32_t* const* rows, const long* starts, const long* prefix, int S,
                       long n, uint64_t* ohi, uint64_t* olo, uint32_t* osplit, uint32_t* orow,
                       hipStream_t st);
+// static-shape shuffle slots: W x C (split, row) entries from device offsets
+// (split 0xFFFFFFFF past a slot's count; hbmr_gather_records_multi skips those)
+int hbmr_tera_collect_slots(const uint32_t* const* rows, const long* starts, const long* pre,
+                            int S, int W, long C, uint32_t* osplit, uint32_t* orow,
+                            hipStream_t st);
 int hbmr_gather_records_multi(const void* const* bases, const uint32_t* split, const uint32_t* row,
                               const uint32_t* perm, long n, int record_bytes, void* dst,
                               hipStream_t st);

@@ -523,7 +523,41 @@ __global__ __launch_bounds__(256) void tera_collect_kernel(
   }
 }
 
-// dst record i = record row[k] of split split[k], k = perm ? perm[i] : i; records
+// Static-shape shuffle send layout (the TeraSort shuffle waves): W destination
+// slots of C entries.  Entry j of slot d is element j of destination d's pieces
+// — piece s is [starts[s*W + d], +len) of split s's partition-ordered rows,
+// placed at [pre[d*(S+1) + s], pre[d*(S+1) + s + 1]) — while j < min(pre[d*(S+1)
+// + S], C); entries past the count get split = kNoSplit (the gather skips them).
+// Every offset is read on the device: no host round trip between the maps'
+// partition offsets and the all-to-all that sends the slots.
+constexpr uint32_t kNoSplit = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(256) void tera_collect_slots_kernel(
+    const uint32_t* const* __restrict__ rows, const long* __restrict__ starts,
+    const long* __restrict__ pre, int S, int W, long C, uint32_t* __restrict__ osplit,
+    uint32_t* __restrict__ orow) {
+  const long n = (long)W * C;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const int d = (int)(i / C);
+    const long j = i - (long)d * C;
+    const long* pd = pre + (long)d * (S + 1);
+    if (j >= pd[S]) {
+      osplit[i] = kNoSplit;
+      orow[i] = 0u;
+      continue;
+    }
+    int a = 0, b = S;          // largest s with pd[s] <= j
+    while (b - a > 1) {
+      const int m = (a + b) >> 1;
+      if (pd[m] <= j) a = m; else b = m;
+    }
+    osplit[i] = (uint32_t)a;
+    orow[i] = rows[a][starts[(long)a * W + d] + (j - pd[a])];
+  }
+}
+
+// dst record i = record row[k] of split split[k], k = perm ? perm[i] : i
+// (split kNoSplit: record i is left unwritten); records
 // of `words` 4-byte words, one word per lane (25 lanes cover a 100-byte record)
 // A workgroup copies 256 / words whole records per step: lane t moves word
 // t % words of record t / words (one 32-bit division per thread, not one
@@ -540,7 +574,8 @@ __global__ __launch_bounds__(256) void gather_records_multi_kernel(
   const int w = t - lr * words;
   for (long r = (long)blockIdx.x * rpb + lr; r < n; r += (long)gridDim.x * rpb) {
     const long k = perm ? (long)perm[r] : r;
-    dst[r * words + w] = bases[split[k]][(long)row[k] * words + w];
+    const uint32_t sp = split[k];
+    if (sp != kNoSplit) dst[r * words + w] = bases[sp][(long)row[k] * words + w];
   }
 }
 
@@ -685,7 +720,8 @@ __global__ __launch_bounds__(256) void gather_records_multi_v3_kernel(
       src[j] = nullptr;
       if (r < n) {
         const long k = perm ? (long)perm[r] : r;
-        src[j] = bases[split[k]] + (long)row[k] * words;
+        const uint32_t sp = split[k];
+        if (sp != kNoSplit) src[j] = bases[sp] + (long)row[k] * words;
       }
     }
     uint32_t v[U];
@@ -694,7 +730,7 @@ __global__ __launch_bounds__(256) void gather_records_multi_v3_kernel(
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       const long r = r0 + j * stride;
-      if (r < n) dst[r * words + w] = v[j];
+      if (src[j]) dst[r * words + w] = v[j];
     }
   }
 }
@@ -1013,6 +1049,17 @@ int hbmr_tera_keys_part(const void* records, long n, int stride, const uint64_t*
   hipLaunchKernelGGL(tera_keys_part_kernel, dim3((unsigned)grid), dim3(256), 0, st,
                      reinterpret_cast<const uint8_t*>(records), n, stride, shi, slo, nsplit, hi,
                      lo, pid);
+  return (int)hipGetLastError();
+}
+
+int hbmr_tera_collect_slots(const uint32_t* const* rows, const long* starts, const long* pre,
+                            int S, int W, long C, uint32_t* osplit, uint32_t* orow,
+                            hipStream_t st) {
+  if (W <= 0 || C <= 0) return 0;
+  if (S <= 0) return (int)hipErrorInvalidValue;
+  const long grid = std::min<long>(ceil_div((long)W * C, 256), 256L * 256);
+  hipLaunchKernelGGL(tera_collect_slots_kernel, dim3((unsigned)grid), dim3(256), 0, st, rows,
+                     starts, pre, S, W, C, osplit, orow);
   return (int)hipGetLastError();
 }
 

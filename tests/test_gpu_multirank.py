@@ -56,7 +56,9 @@ def test_two_ranks_one_gpu_device_collectives_match_in_process(tmp_path):
     # the device paths really ran, staged through the host over gloo
     assert mp["kmeans_counters"].get("ALL_REDUCE_CUDA", 0) >= 2
     assert mp["kmeans_counters"].get("ALL_REDUCE_STAGED", 0) >= 2
-    assert mp["terasort_counters"].get("ALL_TO_ALL_V_CUDA", 0) >= 2
+    # default TeraSort shuffle on 2 ranks: 4 waves of static-shape all-to-alls
+    # (records + counts, device-side counts, no host read between waves)
+    assert mp["terasort_counters"].get("ALL_TO_ALL_FIXED_CUDA", 0) >= 8
     assert mp["wordcount_counters"].get("ALL_TO_ALL_V_CUDA", 0) >= 4
     # waves: 3 all-to-all-v rounds (plus R/splitter agreement), same bytes
     assert mp["terasort_waves_counters"].get("ALL_TO_ALL_V_CUDA", 0) >= 6
@@ -71,4 +73,4 @@ def test_two_ranks_one_gpu_device_collectives_match_in_process(tmp_path):
     assert ip["terasort"] == mp["terasort"] and len(mp["terasort"]) == 2
     assert ip["terasort_waves"] == mp["terasort"]
     assert ip["wordcount"] == mp["wordcount"] and len(mp["wordcount"]) == 2
-    assert ip["terasort_counters"].get("ALL_TO_ALL_V_CUDA", 0) >= 2   # InProcessComm, device
+    assert ip["terasort_counters"].get("ALL_TO_ALL_FIXED_CUDA", 0) >= 8   # InProcessComm, device

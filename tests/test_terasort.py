@@ -11,6 +11,7 @@ from hbmr.mapred.cluster import LocalCluster
 from hbmr.mapred.jobconf import JobConf
 from hbmr.models import terasort as T
 from hbmr.ops import sort as S
+from hbmr.parallel.collectives import COLLECTIVE_GROUP
 
 
 def _ref_sorted(rows):
@@ -37,24 +38,38 @@ def test_create_partitions_rule():
     assert sp[:, 0].tolist() == [5, 10, 15]
 
 
-@pytest.mark.parametrize("trackers,merge,waves", [(1, False, 1), (2, False, 1), (3, False, 1),
-                                                  (3, True, 1), (3, False, 3), (2, True, 4)])
-def test_terasort_on_cluster_sorts_and_validates(tmp_path, trackers, merge, waves):
+@pytest.mark.parametrize("trackers,merge,waves,static,slack", [
+    (1, False, 1, True, None), (2, False, 1, True, None), (3, False, 1, True, None),
+    (3, True, 1, True, None), (3, False, 3, False, None), (2, True, 4, True, None),
+    (2, False, 0, True, None), (3, False, 0, True, None), (3, False, 2, True, 0.05)])
+def test_terasort_on_cluster_sorts_and_validates(tmp_path, trackers, merge, waves, static, slack):
     """merge: senders sort each destination's run and receivers merge the
     runs (K8 merge path) instead of re-sorting; waves: the shuffle runs in
-    rounds over each rank's map outputs — the same output bytes."""
+    rounds over each rank's map outputs (0: the default, 4 waves on several
+    ranks) — static-shape all-to-alls with device-side counts unless
+    ``static`` is off; a slot slack far too small overflows and the shuffle
+    re-runs with exact sizes — the same output bytes every time."""
     rows = 20000
     out = tmp_path / "out"
     with LocalCluster(JobConf(), num_trackers=trackers, cpu_slots=2) as cl:
         conf = T.terasort_conf(rows=rows, split_rows=3000, output=str(out))
         conf.set_boolean("hbmr.terasort.shuffle.sorted.runs", merge)
         conf.set_int("hbmr.terasort.shuffle.waves", waves)
+        conf.set_boolean("hbmr.terasort.shuffle.static", static)
+        if slack is not None:
+            conf.set("hbmr.terasort.shuffle.slot.slack", str(slack))
         rj = cl.submit_job(conf)
         rj.waitForCompletion(120)
         assert rj.isSuccessful(), rj.getFailureInfo()
         res = rj._impl.jip.result
+        ctr = {c.name: c.getValue() for c in rj.getCounters().group(COLLECTIVE_GROUP)}
     assert all(r["unsorted"] == 0 and r["checksum_ok"] for r in res.values())
     assert sum(r["records"] for r in res.values()) == rows
+    if trackers > 1 and waves != 1 and static and not merge:
+        # the data moved in static-shape all-to-alls (records + counts per wave)
+        assert ctr.get("ALL_TO_ALL_FIXED_CPU", 0) >= 2 * trackers
+        # ... unless a slot overflowed: then the exact-size waves ran as well
+        assert (ctr.get("ALL_TO_ALL_V_CPU", 0) > 0) == (slack is not None), ctr
     parts = sorted(f for f in os.listdir(out) if f.startswith("part-"))
     assert len(parts) == trackers
     got = np.concatenate([np.fromfile(out / p, dtype=np.uint8).reshape(-1, 100) for p in parts])
