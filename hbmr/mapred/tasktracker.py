@@ -204,6 +204,14 @@ class TaskTracker:
         # ride on the reduce's completion heartbeat instead of one of their own
         # (maps_done_news)
         self._expect_jobs: set = set()
+        # jobs whose maps were launched here behind a gate (pre-staged): their
+        # collective reduce is coming (the JobTracker sends it once every map
+        # of the job is launched), so their finished batches wait for it too —
+        # at most defer_max_s, after which they are reported on their own
+        # (a reduce that does not come in time, e.g. a map re-run elsewhere)
+        self._gated_jobs: set = set()
+        self.defer_max_s = conf.get_float("hbmr.tracker.defer.map.reports.max.ms", 25.0) / 1e3
+        self._defer_timer = None
         self._polling = False       # the heartbeat thread is in a long-poll
         self._requeued: list = []   # drained statuses whose report failed
         self._notify_seq = 0                 # wakeup() notifications sent (notify_seq)
@@ -364,9 +372,11 @@ class TaskTracker:
         if state != P.SUCCEEDED and run.spec is not None and run.spec.is_map and \
                 run.job is not None:
             run.job.note_failed(run.spec.attempt_id)
-        if run.spec is not None and not run.spec.is_map and self._expect_jobs:
+        if run.spec is not None and not run.spec.is_map and (self._expect_jobs or
+                                                             self._gated_jobs):
             with self._lock:
                 self._expect_jobs.discard(run.spec.job_id)
+                self._gated_jobs.discard(run.spec.job_id)
         if state == P.FAILED:
             dbg = self._run_debug_script(run, diag)
             if dbg:
@@ -432,7 +442,31 @@ class TaskTracker:
         if self._expect_jobs and all(j in self._expect_jobs for j in job_ids):
             self._news.set()
             return
+        if self._gated_jobs and all(j in self._gated_jobs or j in self._expect_jobs
+                                    for j in job_ids):
+            # the job's reduce launch is on its way (it rides on this tracker's
+            # next response): report these with the reduce, not on their own
+            self._news.set()
+            self._arm_defer_flush()
+            return
         self.notify_jobtracker()
+
+    def _arm_defer_flush(self):
+        """Liveness bound of deferred map reports: unreported batches go out
+        after defer_max_s even if no reduce completion carried them."""
+        with self._lock:
+            if self._defer_timer is not None:
+                return
+            t = self._defer_timer = threading.Timer(self.defer_max_s, self._defer_flush)
+        t.daemon = True
+        t.start()
+
+    def _defer_flush(self):
+        with self._lock:
+            self._defer_timer = None
+            pending = bool(self._bulk)
+        if pending:
+            self.notify_jobtracker()
 
     def outputs_lost(self, aids, worker_lost=False):
         with self._lock:
@@ -680,6 +714,9 @@ class TaskTracker:
         and in the GPU worker (held device map outputs, worker JobState)."""
         jid = act["job_id"]
         js = self.jobs.pop(jid, None)
+        with self._lock:
+            self._gated_jobs.discard(jid)
+            self._expect_jobs.discard(jid)
         if js is not None and js.result is not None:
             self._results[jid] = js.result
             while len(self._results) > 64:
@@ -762,6 +799,10 @@ class TaskTracker:
                 continue
             runs = []
             gate = act.get("gate")
+            if gate is not None and coll and self.defer_map_reports and \
+                    jid not in self._gated_jobs:
+                with self._lock:
+                    self._gated_jobs.add(jid)
             for aid, part, split in tasks[lo:hi]:
                 if self._early_kills.pop(aid, 0) is None:
                     continue    # killed before its launch arrived

@@ -75,9 +75,9 @@ def _peak_running(cl, jobs, until):
 def test_capacity_user_limit_splits_a_queue_between_users():
     conf = _cap_conf(**{"mapred.capacity-scheduler.queue.default.minimum-user-limit-percent": 50})
     with LocalCluster(conf, num_trackers=1, cpu_slots=4) as cl:
-        a = split_sleep_conf(12, map_ms=60, base=conf)
+        a = split_sleep_conf(12, map_ms=150, base=conf)
         a.set("user.name", "alice")
-        b = split_sleep_conf(12, map_ms=60, base=conf)
+        b = split_sleep_conf(12, map_ms=150, base=conf)
         b.set("user.name", "bob")
         ra, rb = cl.submit_job(a), cl.submit_job(b)
         peak = _peak_running(cl, [ra, rb], lambda: rb.isComplete() and ra.isComplete())
