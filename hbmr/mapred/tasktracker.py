@@ -210,6 +210,8 @@ class TaskTracker:
         # at most defer_max_s, after which they are reported on their own
         # (a reduce that does not come in time, e.g. a map re-run elsewhere)
         self._gated_jobs: set = set()
+        self.defer_gated = self.defer_map_reports and conf.get_boolean(
+            "hbmr.tracker.defer.gated.map.reports", True)
         self.defer_max_s = conf.get_float("hbmr.tracker.defer.map.reports.max.ms", 25.0) / 1e3
         self._defer_timer = None
         self._polling = False       # the heartbeat thread is in a long-poll
@@ -799,7 +801,7 @@ class TaskTracker:
                 continue
             runs = []
             gate = act.get("gate")
-            if gate is not None and coll and self.defer_map_reports and \
+            if gate is not None and coll and self.defer_gated and \
                     jid not in self._gated_jobs:
                 with self._lock:
                     self._gated_jobs.add(jid)
