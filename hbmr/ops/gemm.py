@@ -2,7 +2,8 @@
 
 :func:`matmul_tn` computes ``alpha · A · Btᵀ`` for bf16 ``A[M, K]`` and
 ``Bt[N, K]`` (K-contiguous operands) with fp32 accumulation on the CDNA4
-matrix cores; other shapes are zero-padded to the 256×256×64 tile.  On CPU it
+matrix cores; any M and N (ragged edge tiles are zero-filled by the loads'
+range check), K padded only to a multiple of 8.  On CPU it
 falls back to a float32 torch matmul (CPU map slots).
 """
 from __future__ import annotations
@@ -36,19 +37,22 @@ def matmul_tn(a: torch.Tensor, bt: torch.Tensor, alpha: float = 1.0,
         return (c, c.sum(dtype=torch.float64)) if with_sum else c
     if a.dtype != torch.bfloat16 or bt.dtype != torch.bfloat16:
         raise ValueError("bf16 operands required on the GPU")
-    Mp, Np, Kp = -(-M // TM) * TM, -(-N // TN) * TN, -(-K // TK) * TK
-    ap, bp = _pad(a, Mp, Kp), _pad(bt, Np, Kp)
     if out_dtype not in (torch.float32, torch.bfloat16):
         raise ValueError("C must be fp32 or bf16")
-    c = torch.empty(Mp, Np, dtype=out_dtype, device=a.device)
-    part = torch.empty((Mp // TM) * (Np // TN), dtype=torch.float64, device=a.device) \
+    # ragged M and N run natively (zero-filled edge tiles, masked stores); K
+    # only needs whole 16-B pieces, so just a K % 8 tail is padded here
+    Kp = -(-K // 8) * 8
+    ap, bp = _pad(a, M, Kp), _pad(bt, N, Kp)
+    if ap.data_ptr() % 16 or bp.data_ptr() % 16:
+        ap, bp = ap.clone(), bp.clone()       # (views at odd offsets)
+    c = torch.empty(M, N, dtype=out_dtype, device=a.device)
+    part = torch.empty((-(-M // TM)) * (-(-N // TN)), dtype=torch.float64, device=a.device) \
         if with_sum else None
-    rc = _lib.load().hbmr_gemm_bf16_tn_ex(ap.data_ptr(), bp.data_ptr(), c.data_ptr(), Mp, Np, Kp,
+    rc = _lib.load().hbmr_gemm_bf16_tn_ex(ap.data_ptr(), bp.data_ptr(), c.data_ptr(), M, N, Kp,
                                            float(alpha), int(out_dtype == torch.bfloat16),
                                            part.data_ptr() if part is not None else None,
                                            _lib.stream_handle(stream))
     _lib.check(rc, "hbmr_gemm_bf16_tn_ex")
-    c = c if (Mp == M and Np == N) else c[:M, :N]
     return (c, part.sum()) if with_sum else c
 
 

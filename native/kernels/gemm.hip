@@ -15,8 +15,12 @@
 //   so the 16 rows a ds_read_b128 fragment load touches spread over the banks;
 // * one barrier per K-step; bijective XCD-aware tile order (each XCD's L2
 //   serves neighbouring tiles of the same A row-panel).
-// Shapes must be multiples of the tile (M, N % 256 == 0, K % 64 == 0); the
-// host wrapper (hbmr/ops/gemm.py) pads other shapes.
+// Ragged shapes run natively in v1 (any M, N; K % 8 == 0): operand tiles are
+// staged by buffer_load … lds through a per-tile buffer resource whose range
+// ends at the operand's last valid row, and a piece past K gets an offset
+// beyond the range, so the hardware's range check zero-fills every piece
+// outside the matrix (no padded copies, no predicated VGPR path); stores are
+// masked to M × N.  v2 (HBMR_GEMM=2) keeps the tile-multiple contract.
 #include "common.h"
 
 #include <cstdlib>
@@ -32,19 +36,31 @@ constexpr int kGemmLds = 2 * kStageBytes;            // double buffered: 128 KiB
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 
-// Stage one 256×64 bf16 tile (rows row0.., cols k0..) of a K-contiguous
-// operand into LDS.  512 threads × 4 rounds × 16 B = 32 KiB.
-__device__ __forceinline__ void stage_tile(char* lds, const __bf16* __restrict__ G, long ld,
-                                           long row0, long k0, int tid) {
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// Buffer resource over rows [row0, min(row0 + 256, rows)) of a K-contiguous
+// operand: reads past its last valid row return zero.  Built from
+// wave-uniform values only (kernel arguments and blockIdx).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const __bf16* G, long ld, long row0,
+                                                            long rows) {
+  const long nr = rows - row0 < kBM ? rows - row0 : kBM;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(G + row0 * ld), 0, (int)(nr * ld * 2),
+                                           0x00020000);
+}
+
+// stage_tile through a tile resource: piece (r, c) at k = k0 + 8 src_c; a
+// piece at k >= K is sent past the range (zero-filled) — K % 8 == 0 keeps
+// every 16-B piece wholly inside or outside the matrix.
+__device__ __forceinline__ void stage_tile_rs(char* lds, __amdgpu_buffer_rsrc_t rs, long ld,
+                                              long k0, long K, int tid) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int p = i * kGemmThreads + tid;  // 16-B piece index in the tile image
+    const int p = i * kGemmThreads + tid;
     const int r = p >> 3, c = p & 7;
-    const int src_c = c ^ (r & 7);
-    const __bf16* g = G + (row0 + r) * ld + k0 + src_c * 8;
-    // each wave's 64 lanes land in one contiguous KiB: base for lane 0 of the wave
+    const long k = k0 + ((c ^ (r & 7)) << 3);
+    const uint32_t off = k < K ? (uint32_t)((r * ld + k) * 2) : 0x80000000u;
     char* dst = lds + (size_t)(i * kGemmThreads + (tid & ~63)) * 16;
-    __builtin_amdgcn_global_load_lds((const void*)g, (void*)dst, 16, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)dst, 16, off, 0, 0, 0);
   }
 }
 
@@ -56,11 +72,13 @@ __global__ __launch_bounds__(kGemmThreads, 1) void gemm_bf16_tn_kernel(
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;  // 2 × 4 waves
-  const long tiles_n = N / kBN;
+  const long tiles_n = (N + kBN - 1) / kBN;
   const uint32_t t = hbmr_xcd_remap(blockIdx.x, gridDim.x);
   const long bm = t / tiles_n, bn = t % tiles_n;
   const long m0 = bm * kBM, n0 = bn * kBN;
-  const int nk = (int)(K / kBK);
+  const int nk = (int)((K + kBK - 1) / kBK);
+  const __amdgpu_buffer_rsrc_t ra = tile_rsrc(A, K, m0, M);
+  const __amdgpu_buffer_rsrc_t rb = tile_rsrc(Bt, K, n0, N);
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -68,8 +86,8 @@ __global__ __launch_bounds__(kGemmThreads, 1) void gemm_bf16_tn_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  stage_tile(smem, A, K, m0, 0, tid);
-  stage_tile(smem + kTileBytes, Bt, K, n0, 0, tid);
+  stage_tile_rs(smem, ra, K, 0, K, tid);
+  stage_tile_rs(smem + kTileBytes, rb, K, 0, K, tid);
 
   const int fr = lane & 15;    // fragment row (A) / column (B) within a 16-tile
   const int fq = lane >> 4;    // k-group: elements k = 8 fq .. 8 fq + 7 of a 32-wide k-step
@@ -80,8 +98,8 @@ __global__ __launch_bounds__(kGemmThreads, 1) void gemm_bf16_tn_kernel(
     __syncthreads();
     if (kt + 1 < nk) {
       char* nxt = smem + ((kt + 1) & 1) * kStageBytes;
-      stage_tile(nxt, A, K, m0, (long)(kt + 1) * kBK, tid);
-      stage_tile(nxt + kTileBytes, Bt, K, n0, (long)(kt + 1) * kBK, tid);
+      stage_tile_rs(nxt, ra, K, (long)(kt + 1) * kBK, K, tid);
+      stage_tile_rs(nxt + kTileBytes, rb, K, (long)(kt + 1) * kBK, K, tid);
     }
     const char* la = cur;
     const char* lb = cur + kTileBytes;
@@ -119,6 +137,7 @@ __global__ __launch_bounds__(kGemmThreads, 1) void gemm_bf16_tn_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const long row = m0 + wm * 128 + i * 16 + fq * 4 + r;
+        if (row >= M || col >= N) continue;        // ragged edge tile
         const float v = acc[i][j][r] * alpha;
         if (OUT_BF16) {
           const uint16_t h = hbmr_f32_to_bf16(v);
@@ -277,11 +296,14 @@ bool g_gemm_lds_set = false;
 extern "C" {
 
 // C = alpha · A · Btᵀ; out_bf16 selects a bf16 C (else fp32).  partials (may be
-// null): (M/256)·(N/256) doubles, each workgroup's sum of its stored C tile.
+// null): ceil(M/256)·ceil(N/256) doubles, each workgroup's sum of its stored
+// C tile.  Any M, N; K % 8 == 0.
 int hbmr_gemm_bf16_tn_ex(const void* A, const void* Bt, void* C, long M, long N, long K,
                          float alpha, int out_bf16, double* partials, hipStream_t st) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
-  if (M % kBM || N % kBN || K % kBK) return (int)hipErrorInvalidValue;
+  // 16-B pieces: K % 8 (and 16-B aligned operands); buffer offsets are 32-bit
+  if (K % 8 || ((uintptr_t)A | (uintptr_t)Bt) % 16 || (long)kBM * K * 2 >= (1L << 31))
+    return (int)hipErrorInvalidValue;
   if (!g_gemm_lds_set) {
     HBMR_RETURN_IF_ERROR(hipFuncSetAttribute((const void*)gemm_bf16_tn_kernel<false>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLds));
@@ -293,14 +315,15 @@ int hbmr_gemm_bf16_tn_ex(const void* A, const void* Bt, void* C, long M, long N,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLds));
     g_gemm_lds_set = true;
   }
-  const long tiles = (M / kBM) * (N / kBN);
+  const long tiles = ((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
   if (tiles > 0x7fffffffL) return (int)hipErrorInvalidValue;
+  const bool ragged = M % kBM || N % kBN || K % kBK;
   // HBMR_GEMM=2: the 4-wave 128x128 / 32x32x16 variant (A/B against v1)
   static const int ver = [] {
     const char* e = getenv("HBMR_GEMM");
     return e && *e == '2' ? 2 : 1;
   }();
-  if (ver == 2) {
+  if (ver == 2 && !ragged) {
     if (out_bf16)
       hipLaunchKernelGGL(gemm_bf16_tn_v2_kernel<true>, dim3((unsigned)tiles), dim3(kGemmThreads2),
                          kGemmLds, st, reinterpret_cast<const __bf16*>(A),

@@ -36,7 +36,11 @@ def test_matmul_job_cpu_checksum(trackers):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("m,k,n", [(256, 64, 256), (512, 192, 768), (1000, 300, 100),
-                                   (2048, 1024, 1536)])
+                                   (2048, 1024, 1536),
+                                   # ragged: edge tiles zero-filled in-kernel (K % 8 == 0
+                                   # runs without any host padding)
+                                   (300, 136, 520), (1, 8, 1), (257, 72, 255),
+                                   (4097, 200, 33), (640, 1000, 384)])
 def test_gemm_kernel_matches_fp32_reference(m, k, n):
     g = torch.Generator().manual_seed(m + k + n)
     a = torch.randn(m, k, generator=g).to(torch.bfloat16)
