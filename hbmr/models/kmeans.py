@@ -744,13 +744,12 @@ class KMeansSplitJob(SplitJob):
                 ctx.sim_ready = max(time.time(), getattr(ctx, "sim_base", 0.0)) + sim
         sums = packed[:k * dp].view(k, dp)
         counts = packed[k * dp:]
-        if self.exact and sums.device.type == "cuda":
-            st = _EXACT_STATS.pop((self.cin, str(sums.device)), None)
-            if st is not None:
-                flagged, relabelled, rescans = (int(v) for v in st.tolist())
-                ctx.reporter.incrCounter("KMEANS", "EXACT_FLAGGED_POINTS", flagged)
-                ctx.reporter.incrCounter("KMEANS", "EXACT_RELABELLED_POINTS", relabelled)
-                ctx.reporter.incrCounter("KMEANS", "EXACT_NEIGHBOUR_SCANS", rescans)
+        # exact mode's device counters are read with the shift, after the
+        # update is enqueued and the staged maps released (a host read here
+        # would wait for every map kernel and leave the device idle until the
+        # update and the next job's maps were launched)
+        est = _EXACT_STATS.pop((self.cin, str(sums.device)), None) \
+            if self.exact and sums.device.type == "cuda" else None
         killed = getattr(ctx, "killed", None)
         if killed is not None and killed():
             raise RuntimeError("reduce killed (collective restart): result not published")
@@ -771,9 +770,17 @@ class KMeansSplitJob(SplitJob):
             rel = getattr(ctx, "release_dependents", None)
             if rel is not None:
                 rel()
-            # the shift and the point count in one device->host copy (one sync)
-            shift, npts = torch.stack([img.shift2.max().double().sqrt(),
-                                       counts.sum().double()]).tolist()
+            # the shift, the point count (and exact mode's counters) in one
+            # device->host copy (one sync)
+            vals = [img.shift2.max().double().sqrt(), counts.sum().double()]
+            if est is not None:
+                vals += list(est.double().unbind(0))
+            got = torch.stack(vals).tolist()
+            shift, npts = got[0], got[1]
+            if est is not None:
+                for name, v in zip(("EXACT_FLAGGED_POINTS", "EXACT_RELABELLED_POINTS",
+                                    "EXACT_NEIGHBOUR_SCANS"), got[2:5]):
+                    ctx.reporter.incrCounter("KMEANS", name, int(v))
             if TRACE.on:
                 TRACE.instant("kmeans.shift_synced")
             new_cen = None
