@@ -478,9 +478,13 @@ def assign_exact_batch(splits: list, img: CentroidImage, stats: torch.Tensor, ou
                                torch.empty(nmax, dtype=torch.float32, device=dev),
                                torch.empty(2 * nmax, dtype=torch.float32, device=dev))
     cand, sc, mg = bufs
+    grouped = REFINE_VERSION >= 3 and img.dp <= 128 and GROUPED_EXACT
     with torch.cuda.stream(stream) if stream is not None else _nullctx():
         c16, ch, cn, cmax, ce, cemax = img.image16(dt)
-        ni, nd, L = img.neighbors()
+        # the neighbour table is waited for only where the certification
+        # needs it (after the first top-3 launch: the reduce builds it on its
+        # own stream while that assign runs)
+        ni, nd, L = (None, None, 0) if grouped else img.neighbors()
     lib = _lib.load()
     top3 = lib.hbmr_kmeans_assign_top3_f16 if dt == torch.float16 else \
         lib.hbmr_kmeans_assign_top3_bf16
@@ -488,7 +492,6 @@ def assign_exact_batch(splits: list, img: CentroidImage, stats: torch.Tensor, ou
     pc, ps, pm, pst = _ptr(cand), _ptr(sc), _ptr(mg), _ptr(stats)
     pcn, pcmax, pce, pcemax, pni, pnd = (_ptr(t) for t in (cn, cmax, ce, cemax, ni, nd))
     base, off = out.data_ptr(), 0
-    grouped = REFINE_VERSION >= 3 and img.dp <= 128 and GROUPED_EXACT
     for g0 in range(0, len(splits), MAX_REFINE_BATCH):
         group = splits[g0:g0 + MAX_REFINE_BATCH]
         if grouped:
