@@ -141,7 +141,7 @@ def main():
         k, _, v = kv.partition("=")
         conf.set(k.strip(), v.strip())
     node = Node(conf, use_gpu=has_gpu)
-    if node.is_master:
+    if node.is_master and not getattr(node, "jt_process", False):
         from hbmr.utils.sampler import maybe_watch_jobtracker
         maybe_watch_jobtracker(node.jt)
     if not node.is_master:
@@ -180,6 +180,8 @@ def main():
         if in_process:
             torch.cuda.synchronize()
         cpu0 = time.process_time()
+        jt_proc = getattr(node, "jt_process", False)
+        jt_cpu0 = node.jt.cpu_seconds() if jt_proc else 0.0
         if sampler is not None:
             sampler.mark()
         t0 = time.perf_counter()
@@ -192,6 +194,7 @@ def main():
             torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         cpu_rank0 = time.process_time() - cpu0
+        jt_cpu = node.jt.cpu_seconds() - jt_cpu0 if jt_proc else None
         hist = drv.history[a.warmup:]
         if a.verbose:
             J = "org.apache.hadoop.mapred.JobInProgress$Counter"
@@ -265,9 +268,15 @@ def main():
             "points_per_sec": round(a.points * a.steps / dt, 1),
             "maps_launched": n_maps, "gpu_maps": gpu_maps, "cpu_maps": cpu_maps,
             "warmup_seconds": round(t_warm, 2),
-            # CPU time of this (rank-0) process per timed job: the JobTracker,
-            # its RPC handlers, the local TaskTracker and the driver
+            # CPU time of this (rank-0) process per timed job: its TaskTracker,
+            # the driver (and the JobTracker with its RPC handlers, when it
+            # runs here: one rank, or hbmr.jobtracker.process=false)
             "rank0_cpu_ms_per_step": round(cpu_rank0 / a.steps * 1e3, 3),
+            # with several ranks the JobTracker is a process of its own
+            # (hbmr.jobtracker.process): its CPU per timed job, not in rank 0's
+            "jobtracker_process": bool(jt_proc),
+            "jobtracker_cpu_ms_per_step": None if jt_cpu is None else
+            round(jt_cpu / a.steps * 1e3, 3),
             "final_shift": hist[-1].get("shift") if hist else None,
             "maps_per_tracker_last_job": hist[-1].get("maps_per_tracker") if hist else None,
             # per job signature: completed-task mean seconds on each slot type and the

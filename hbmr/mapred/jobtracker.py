@@ -1729,6 +1729,50 @@ class JobTracker:
                     "jobs": {j: jip.status.state for j, jip in self.jobs.items()},
                     "cost_model": self.cost_model.snapshot()}
 
+    # -- JobTracker process (hbmr/mapred/jtprocess.py): the node's driver side --------
+    def rpc_wait_job(self, jid, timeout=30.0):
+        """Long-poll: True once the job is complete (or ``timeout`` passed)."""
+        jip = self.check_access(jid, "view")
+        return jip.done.wait(max(0.0, min(float(timeout), 60.0)))
+
+    def rpc_job_info(self, jid):
+        """Everything a driver reads about a job, in one call: status,
+        counters, the phase timeline, maps per tracker and the reduce result."""
+        jip = self.check_access(jid, "view")
+        st = jip.status
+        per = {}
+        with self.lock:
+            for t in jip.maps:
+                if t.successful is not None:
+                    per[t.successful.tracker] = per.get(t.successful.tracker, 0) + 1
+        return {"state": st.state, "map_progress": st.map_progress,
+                "reduce_progress": st.reduce_progress, "start_time": st.start_time,
+                "finish_time": st.finish_time, "failure_info": st.failure_info,
+                "counters": jip.fold_counters().to_dict(), "timeline": jip.timeline(),
+                "maps_per_tracker": per, "result": jip.result}
+
+    def rpc_wait_for_trackers(self, n, timeout=60.0):
+        return self.wait_for_trackers(int(n), float(timeout))
+
+    def rpc_start_expiry(self):
+        self.start_expiry_thread()
+
+    def rpc_broadcast_shutdown(self):
+        self.broadcast_shutdown()
+
+    def rpc_live_trackers(self, exclude="", window=0.5):
+        with self.lock:
+            now = time.time()
+            return sum(1 for t in self.trackers.values()
+                       if t.name != exclude and now - t.last_seen < window)
+
+    def rpc_cost_model(self):
+        return self.cost_model.snapshot()
+
+    def rpc_cpu_seconds(self):
+        """CPU seconds of this process (a JobTracker process's own cost)."""
+        return time.process_time()
+
     def broadcast_shutdown(self):
         """Tell every tracker to exit on its next heartbeat."""
         with self.lock:

@@ -80,7 +80,19 @@ class Node:
                 worker_comm = {"host": os.environ.get("MASTER_ADDR", "127.0.0.1"),
                                "port": int(os.environ["MASTER_PORT"]), "rank": self.rank,
                                "world": self.world, "backend": dev_backend}
-        if self.rank == 0:
+        # several ranks: the JobTracker runs in a process of its own (not
+        # under rank 0's interpreter lock with its tracker and the driver);
+        # hbmr.jobtracker.process=false keeps it in rank 0
+        self.jt_process = self.rank == 0 and self.conf.get_boolean(
+            "hbmr.jobtracker.process", False)
+        if self.jt_process:
+            from .jtprocess import RemoteJobTracker
+            self.jt = RemoteJobTracker(self.conf)
+            if self.world > 1:
+                host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+                self.store.set("hbmr/jobtracker", f"{host}:{self.jt.port}")
+            jt_handle = JobTrackerProxy(self.jt.address, self.conf)
+        elif self.rank == 0:
             self.jt = JobTracker(self.conf)
             if self.world > 1:
                 self.server = RpcServer(self.jt, JT_METHODS, secret=rpc_secret(self.conf)).start()
@@ -124,8 +136,10 @@ class Node:
         return self.jt.submit_job(job)
 
     def job_result(self, rj, partition=0):
-        r = rj._impl.jip.result
-        return None if r is None else r.get(partition)
+        r = rj._impl.result
+        if r is None:
+            return None
+        return r.get(partition, r.get(str(partition)))
 
     def serve_until_shutdown(self):
         """Non-master ranks: run the tracker until the JobTracker says shutdown."""
@@ -138,9 +152,12 @@ class Node:
             # wait for the other trackers to receive the shutdown action
             deadline = time.time() + 30
             while time.time() < deadline:
-                with self.jt.lock:
-                    others = [t for t in self.jt.trackers.values()
-                              if t.name != self.tt.name and time.time() - t.last_seen < 0.5]
+                if self.jt_process:
+                    others = self.jt.live_trackers(self.tt.name, 0.5)
+                else:
+                    with self.jt.lock:
+                        others = [t for t in self.jt.trackers.values()
+                                  if t.name != self.tt.name and time.time() - t.last_seen < 0.5]
                 if not others or time.time() > deadline:
                     break
                 time.sleep(0.1)

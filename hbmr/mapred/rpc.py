@@ -228,8 +228,13 @@ class RpcClient:
             self._tl.sock = None
 
 
-JT_METHODS = ("heartbeat", "wakeup", "report", "map_completion_events", "rpc_submit_job", "rpc_job_status", "rpc_kill_job",
-              "rpc_job_result", "rpc_cluster_status", "rpc_list_jobs", "rpc_task_reports")
+JT_METHODS = ("heartbeat", "wakeup", "report", "map_completion_events", "rpc_submit_job",
+              "rpc_job_status", "rpc_kill_job", "rpc_job_result", "rpc_cluster_status",
+              "rpc_list_jobs", "rpc_task_reports", "rpc_wait_job", "rpc_job_info")
+# served by a JobTracker process to the node that started it (hbmr/mapred/jtprocess.py)
+JT_PROCESS_METHODS = JT_METHODS + ("rpc_wait_for_trackers", "rpc_start_expiry",
+                                   "rpc_broadcast_shutdown", "rpc_live_trackers",
+                                   "rpc_cost_model", "rpc_cpu_seconds", "rpc_stop")
 
 
 class JobTrackerProxy:
