@@ -50,6 +50,11 @@ class _Device:
         props = torch.cuda.get_device_properties(index)
         self.name = props.name
         self.total_mem = props.total_memory
+        # maps of jobs with a cap on maps in flight (a split job's
+        # max_inflight_maps: TeraSort's out-of-core mode, whose inputs are not
+        # cached and whose per-map working set must stay inside its HBM budget)
+        self.cap_cond = threading.Condition()
+        self.capped = 0
         self.device_errors = 0      # consecutive failed batches with a device-level error
         self.last_error = ""
         # device-time accounting: batch intervals are placed on one timeline
@@ -248,6 +253,7 @@ class GpuRuntime:
                 sj = js.split_job
                 i = 0
                 if hasattr(sj, "map_gpu_batch") and len(runs) > 2 * self.first_chunk and \
+                        not getattr(sj, "max_inflight_maps", 0) and \
                         not any(s.inflight for s in dev.slots):
                     # idle device: start it on a few tasks while the rest are
                     # prepared (each task costs ~20 µs of host work to launch)
@@ -260,12 +266,37 @@ class GpuRuntime:
                 per = min(self.max_batch, self.batch_target, max(1, -(-rest // max(1, nslot))))
                 if rest <= self.first_chunk and hasattr(sj, "map_gpu_batch"):
                     per = max(1, rest)       # a first chunk: one launch, no split
+                cap = int(getattr(sj, "max_inflight_maps", 0) or 0)
+                if cap > 0:
+                    per = min(per, cap)
                 for j in range(i, len(runs), per):
-                    self._launch_batch(dev, runs[j:j + per], js, sj, SplitSpec, TaskContext)
+                    chunk = runs[j:j + per]
+                    if cap > 0:
+                        # the launcher waits for capped maps to complete (the
+                        # completer releases them): their device memory is
+                        # allocated at launch, not when the kernels run
+                        with dev.cap_cond:
+                            while dev.capped and dev.capped + len(chunk) > cap and \
+                                    not self._stop.is_set():
+                                dev.cap_cond.wait(0.5)
+                            dev.capped += len(chunk)
+                    n = self._launch_batch(dev, chunk, js, sj, SplitSpec, TaskContext,
+                                           capped=cap > 0)
+                    if cap > 0 and n < len(chunk):
+                        self._release_capped(dev, len(chunk) - n)
             for ev in picked:
                 ev.set()
 
-    def _launch_batch(self, dev, runs, js, sj, SplitSpec, TaskContext):  # noqa: N803
+    @staticmethod
+    def _release_capped(dev, n):
+        with dev.cap_cond:
+            dev.capped = max(0, dev.capped - n)
+            dev.cap_cond.notify_all()
+
+    def _launch_batch(self, dev, runs, js, sj, SplitSpec, TaskContext,  # noqa: N803
+                      capped=False):
+        """Launch one batch on the next slot; returns how many of its runs
+        went to the device (their completion is the completer's)."""
         tracker = self.tracker
         slot = dev.slots[dev.rr % len(dev.slots)]
         dev.rr += 1
@@ -307,7 +338,7 @@ class GpuRuntime:
                     datas.append(data)
                     live.append(r)
                 if not live:
-                    return
+                    return 0
                 # staged attempts: the job they depend on enqueued its reduce
                 # result; the kernels wait for it on the device, not the host
                 waits = {id(r.wait): r.wait for r in live if r.wait is not None}
@@ -333,13 +364,15 @@ class GpuRuntime:
                 by_job.setdefault(id(r.job), (r.job, []))[1].append((r.spec.attempt_id, out, ev1))
             for js, items in by_job.values():
                 js.note_launched(items)
-            slot.done_q.put((live, ev0, ev1, outs))
+            slot.done_q.put((live, ev0, ev1, outs, capped))
+            return len(live)
         except BaseException as e:  # noqa: BLE001
             self._note_error(dev.index, e)
             for r in (live or runs):
                 if r.status.state not in P.TERMINAL:
                     tracker._finish(r, P.FAILED,
                                     f"{type(e).__name__}: {e}\n{traceback.format_exc()[-2000:]}")
+            return 0
 
     def _prefetch_hosts(self, dev, runs, sj, SplitSpec):  # noqa: N803
         """Cold splits of a batch whose job can load them on the host
@@ -371,7 +404,7 @@ class GpuRuntime:
             item = slot.done_q.get()
             if item is None:
                 break
-            runs, ev0, ev1, outs = item
+            runs, ev0, ev1, outs, capped = item
             try:
                 ev1.synchronize()
                 if TRACE.on:
@@ -402,6 +435,8 @@ class GpuRuntime:
                                     f"{type(e).__name__}: {e}\n{traceback.format_exc()[-2000:]}")
             finally:
                 slot.inflight -= len(runs)
+                if capped:
+                    self._release_capped(self.devices[slot.device.index], len(runs))
 
     @staticmethod
     def _busy_ms(dev, ev0, ev1):

@@ -143,6 +143,17 @@ class TeraSortSplitJob(SplitJob):
         """Spill mode streams the input: a split is dropped after its map."""
         return not self.spill
 
+    @property
+    def max_inflight_maps(self):
+        """Spill mode: maps in flight per GPU such that their working sets
+        (the split, its sorted copy, keys and permutation: about 3.5x the
+        split) stay inside the HBM budget; 0 = no cap."""
+        if not self.spill:
+            return 0
+        split_bytes = max(1, self.split_rows * S.RECORD)
+        budget = self.budget if self.budget > 0 else self.group_bytes
+        return max(1, int(budget // (4 * split_bytes)))
+
     # -- splits + sampling (JobTracker side) -----------------------------------------
     def _ranges(self):
         """[(kind, params, rows)] covering the input."""
