@@ -451,10 +451,11 @@ class TeraSortSplitJob(SplitJob):
             csum = csum + hs.sum() + ls.sum()
             n += m
             if self.out:
-                at = 0
+                at, items = 0, []
                 for p in range(pa, pb):
-                    self._write_part(ctx, p, recs[at:at + int(sizes[p])])
+                    items.append((p, recs[at:at + int(sizes[p])]))
                     at += int(sizes[p])
+                self._write_parts(ctx, items)
             del recs, hs, ls
         if first is None:
             return 0, None
@@ -518,10 +519,11 @@ class TeraSortSplitJob(SplitJob):
             csum = csum + hs.sum() + ls.sum()
             n += m
             if self.out:
-                at = 0
+                at, items = 0, []
                 for p in range(pa, pb):
-                    self._write_part(ctx, p, recs[at:at + int(sizes[p])])
+                    items.append((p, recs[at:at + int(sizes[p])]))
                     at += int(sizes[p])
+                self._write_parts(ctx, items)
             del recs, hs, ls
         if first is None:
             return 0, None
@@ -748,8 +750,7 @@ class TeraSortSplitJob(SplitJob):
             cut = [0] + cut[1:-1] + [n]
         else:
             cut = [0, n]
-        for i, p in enumerate(range(a, b)):
-            self._write_part(ctx, p, srt[cut[i]:cut[i + 1]])
+        self._write_parts(ctx, [(p, srt[cut[i]:cut[i + 1]]) for i, p in enumerate(range(a, b))])
 
     def _reduce_shuffle(self, ctx, outs, offs, nparts, dev):
         """world > 1: every rank gathers the records of each destination's
@@ -832,8 +833,8 @@ class TeraSortSplitJob(SplitJob):
                 cut = [0] + cut[1:-1] + [n]
             else:
                 cut = [0, n]
-            for i, p in enumerate(range(a, b)):
-                self._write_part(ctx, p, srt[cut[i]:cut[i + 1]])
+            self._write_parts(ctx, [(p, srt[cut[i]:cut[i + 1]])
+                                    for i, p in enumerate(range(a, b))])
         return n, st
 
     @staticmethod
@@ -867,11 +868,17 @@ class TeraSortSplitJob(SplitJob):
         dev = getattr(ctx, "device", None)
         ctx.tera_out = (com, attempt, com.work_path(self.conf, attempt),
                         _PartWriter(dev, self.conf.get_boolean("terasort.final.sync", True),
-                                    self.conf.get_int("hbmr.terasort.output.writers", 8)))
+                                    self.conf.get_int("hbmr.terasort.output.writers", 16)))
 
     def _write_part(self, ctx, p, recs):
+        self._write_parts(ctx, [(p, recs)])
+
+    def _write_parts(self, ctx, items):
+        """Partitions [(p, records)] that are ready together (one sort group)
+        are written together: their pieces interleave, so the writers work
+        on different files (one file's writes serialise on its inode)."""
         _com, _att, workdir, pw = ctx.tera_out
-        pw.write(os.path.join(workdir, f"part-{p:05d}"), recs)
+        pw.write_many([(os.path.join(workdir, f"part-{p:05d}"), recs) for p, recs in items])
 
     def _close_output(self, ctx, commit=True):
         """Close the part writer; commit the attempt's work directory only on
@@ -955,39 +962,50 @@ class _PartWriter:
                 os.close(fd)
 
     def write(self, path, recs):
-        os.makedirs(os.path.dirname(path), exist_ok=True)
-        fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
-        flat = recs.reshape(-1)
-        n = flat.numel()
-        pieces = max(1, -(-n // self.CHUNK))
-        st = [pieces]
-        if n == 0:
-            self.files.append(self.pool.submit(self._piece, fd, st, b"", 0))
-            return
-        if not self.cuda or not flat.is_cuda:
-            a = flat.numpy()
-            for i in range(pieces):
+        self.write_many([(path, recs)])
+
+    def write_many(self, items):
+        """Several files at once: piece i of every file before piece i + 1 of
+        any, so the writers in flight hold different files."""
+        files = []
+        for path, recs in items:
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+            flat = recs.reshape(-1)
+            n = flat.numel()
+            pieces = max(1, -(-n // self.CHUNK))
+            st = [pieces]
+            if n == 0:
+                self.files.append(self.pool.submit(self._piece, fd, st, b"", 0))
+                continue
+            if not self.cuda or not flat.is_cuda:
+                a = flat.numpy()
+                for i in range(pieces):
+                    o = i * self.CHUNK
+                    self.files.append(self.pool.submit(self._piece, fd, st,
+                                                       a[o:o + self.CHUNK], o))
+                continue
+            self.stream.wait_stream(torch.cuda.current_stream(flat.device))
+            flat.record_stream(self.stream)
+            files.append((fd, st, flat, n, pieces))
+        for i in range(max((f[4] for f in files), default=0)):
+            for fd, st, flat, n, pieces in files:
+                if i >= pieces:
+                    continue
                 o = i * self.CHUNK
-                self.files.append(self.pool.submit(self._piece, fd, st,
-                                                   a[o:o + self.CHUNK], o))
-            return
-        self.stream.wait_stream(torch.cuda.current_stream(flat.device))
-        flat.record_stream(self.stream)
-        for i in range(pieces):
-            o = i * self.CHUNK
-            c = min(self.CHUNK, n - o)
-            j = self.k % len(self.bufs)
-            self.k += 1
-            if self.pending[j] is not None:
-                self.pending[j].result()          # the buffer's previous piece is out
-            buf = self.bufs[j]
-            with torch.cuda.stream(self.stream):
-                buf[:c].copy_(flat[o:o + c], non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(self.stream)
-            fut = self.pool.submit(self._piece, fd, st, buf[:c].numpy(), o, ev)
-            self.pending[j] = fut
-            self.files.append(fut)
+                c = min(self.CHUNK, n - o)
+                j = self.k % len(self.bufs)
+                self.k += 1
+                if self.pending[j] is not None:
+                    self.pending[j].result()          # the buffer's previous piece is out
+                buf = self.bufs[j]
+                with torch.cuda.stream(self.stream):
+                    buf[:c].copy_(flat[o:o + c], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(self.stream)
+                fut = self.pool.submit(self._piece, fd, st, buf[:c].numpy(), o, ev)
+                self.pending[j] = fut
+                self.files.append(fut)
 
     def close(self):
         try:
