@@ -137,6 +137,26 @@ class CentroidImage:
                 if L is None:
                     L = int(os.environ.get("HBMR_KMEANS_NBR_L", NBR_L))
                 L = max(1, min(L, self.k))
+                if self.cen.is_cuda and self.k <= NBR_NATIVE_MAX_K and self.d <= 256:
+                    # one kernel (hbmr_kmeans_centroid_nbr): pairwise fp64
+                    # distances, bounds rounded outward, per-row bitonic sort
+                    # in LDS — instead of ~40 small torch launches whose host
+                    # time held the interpreter lock at the iteration seam
+                    dev = self.cen.device
+                    di = torch.empty(self.k, L, dtype=torch.int32, device=dev)
+                    f = torch.empty(self.k, L, dtype=torch.float32, device=dev)
+                    pd = torch.empty(self.k, self.k, dtype=torch.float32, device=dev) \
+                        if self.k <= PAIR_DIST_MAX_K else None
+                    rc = _lib.load().hbmr_kmeans_centroid_nbr(
+                        _ptr(self.cen), self.k, self.d, L, _ptr(di), _ptr(f), _ptr(pd),
+                        _lib.stream_handle(None))
+                    _lib.check(rc, "hbmr_kmeans_centroid_nbr")
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    self._nbr = (di, f, L, ev, pd)
+                    di, f, L, ev, _ = self._nbr
+                    torch.cuda.current_stream().wait_event(ev)
+                    return di, f, L
                 # squared distances by the Gram form in fp64 (one DGEMM instead
                 # of a pairwise kernel: ~0.8 ms per image at k = 1024), with
                 # the form's rounding error bounded explicitly: |D2 - D| <=
@@ -519,6 +539,8 @@ def assign_exact_batch(splits: list, img: CentroidImage, stats: torch.Tensor, ou
 
 # the pair rule of the certification keeps a [k, k] centroid distance matrix
 PAIR_DIST_MAX_K = int(os.environ.get("HBMR_PAIR_DIST_MAX_K", "8192"))
+# the native neighbour table sorts a row of k keys in LDS (k <= 8192)
+NBR_NATIVE_MAX_K = int(os.environ.get("HBMR_NBR_NATIVE_MAX_K", "8192"))
 # exact batches: one top-3 launch + one step-1 launch per up to 64 splits
 # (HBMR_EXACT_GROUPED=0: a launch of each per split)
 GROUPED_EXACT = os.environ.get("HBMR_EXACT_GROUPED", "1") != "0"

@@ -39,6 +39,11 @@ int hbmr_kmeans_assign_top3_f16(const void* X, long n, int dp, const void* C, co
 int hbmr_kmeans_exact_prep(const float* x, long n, int d, int ldx, int dp, int f16, void* x16,
                            float* xnorm, float* xn2, float* xerr, hipStream_t st);
 // 16-bit centroid image + chalf, |c|, |c - c~|, maxima[2]
+// exact mode's centroid neighbour table: di/dv [k, L] (the L nearest by a
+// lower bound rounded down, ascending, itself first), pd [k, k] upper bounds
+// rounded up (may be null); k <= 8192, d <= 256
+int hbmr_kmeans_centroid_nbr(const float* cen, int k, int d, int L, int32_t* di, float* dv,
+                             float* pd, hipStream_t st);
 int hbmr_kmeans_image16(const float* cen, int k, int d, int dp, int k_pad, int f16, void* c16,
                         float* chalf, float* cnorm, float* cerr, float* maxima, hipStream_t st);
 int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float* xnorm,

@@ -3405,6 +3405,114 @@ int hbmr_kmeans_image16(const float* cen, int k, int d, int dp, int k_pad, int f
 }
 
 
+}  // extern "C"
+
+// One workgroup per centroid a: D(a, b) = sum_i (c_ai - c_bi)^2 in fp64 — one
+// rounded difference and d fused square-adds, |D~ - D| <= (d + 2) 2^-53 D —
+// then the lower bound sqrt(D~ (1 - rel)) rounded DOWN to fp32 and the upper
+// bound sqrt(D~ (1 + rel)) rounded UP (rel = (d + 4) 2^-53 * 1.01 also covers
+// the product and sqrt roundings).  The (lower bound, b) keys of the row are
+// bitonic-sorted in LDS — ties by index, i.e. a stable sort — and the L
+// first kept (di, dv: the scan order and its stop rule); pd[a][b] gets the
+// upper bounds.  The pairwise form (not the Gram form) bounds the error by D
+// itself, so near centroids keep tight bounds.
+constexpr int kNbrThreads = 256;
+constexpr int kNbrMaxD = 256;
+constexpr int kNbrMaxK = 8192;
+
+__global__ __launch_bounds__(kNbrThreads) void kmeans_centroid_nbr_kernel(
+    const float* __restrict__ cen, int k, int d, int L, int kp2, double rel,
+    int32_t* __restrict__ di, float* __restrict__ dv, float* __restrict__ pd) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long s_key[];   // kp2
+  __shared__ double s_ca[kNbrMaxD];
+  const int a = blockIdx.x, t = threadIdx.x;
+  for (int i = t; i < d; i += kNbrThreads) s_ca[i] = (double)cen[(long)a * d + i];
+  __syncthreads();
+  const bool vec4 = (d & 3) == 0;
+  for (int b = t; b < kp2; b += kNbrThreads) {
+    unsigned long long key = ~0ull;
+    if (b < k) {
+      float lo_f = 0.f, hi_f = 0.f;
+      if (b != a) {
+        const float* cb = cen + (long)b * d;
+        double acc = 0.0;
+        if (vec4) {
+          for (int i = 0; i < d; i += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(cb + i);
+            double e = s_ca[i] - (double)v.x;
+            acc = fma(e, e, acc);
+            e = s_ca[i + 1] - (double)v.y;
+            acc = fma(e, e, acc);
+            e = s_ca[i + 2] - (double)v.z;
+            acc = fma(e, e, acc);
+            e = s_ca[i + 3] - (double)v.w;
+            acc = fma(e, e, acc);
+          }
+        } else {
+          for (int i = 0; i < d; ++i) {
+            const double e = s_ca[i] - (double)cb[i];
+            acc = fma(e, e, acc);
+          }
+        }
+        const double lo = sqrt(fmax(0.0, acc * (1.0 - rel)));
+        const double hi = sqrt(acc * (1.0 + rel));
+        lo_f = (float)lo;
+        if ((double)lo_f > lo) lo_f = nextafterf(lo_f, 0.f);
+        hi_f = (float)hi;
+        if ((double)hi_f < hi) hi_f = nextafterf(hi_f, __builtin_inff());
+      }
+      if (pd) pd[(long)a * k + b] = hi_f;
+      key = ((unsigned long long)__float_as_uint(lo_f) << 32) | (unsigned)b;
+    }
+    s_key[b] = key;
+  }
+  __syncthreads();
+  for (int size = 2; size <= kp2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = t; i < kp2 / 2; i += kNbrThreads) {
+        const int pos = 2 * i - (i & (stride - 1));
+        const int q = pos + stride;
+        const bool up = (pos & size) == 0;
+        const unsigned long long x = s_key[pos], y = s_key[q];
+        if ((x > y) == up) {
+          s_key[pos] = y;
+          s_key[q] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int j = t; j < L; j += kNbrThreads) {
+    const unsigned long long key = s_key[j];
+    di[(long)a * L + j] = (int32_t)(uint32_t)(key & 0xffffffffull);
+    dv[(long)a * L + j] = __uint_as_float((uint32_t)(key >> 32));
+  }
+}
+
+extern "C" {
+
+int hbmr_kmeans_centroid_nbr(const float* cen, int k, int d, int L, int32_t* di, float* dv,
+                             float* pd, hipStream_t st) {
+  if (k <= 0 || k > kNbrMaxK || d <= 0 || d > kNbrMaxD || L <= 0 || L > k)
+    return (int)hipErrorInvalidValue;
+  if (((uintptr_t)cen & 15) != 0) return (int)hipErrorInvalidValue;
+  int kp2 = 1;
+  while (kp2 < k) kp2 <<= 1;
+  const size_t lds = (size_t)kp2 * sizeof(unsigned long long);
+  static bool lds_set = false;
+  if (!lds_set) {
+    HBMR_RETURN_IF_ERROR(hipFuncSetAttribute((const void*)kmeans_centroid_nbr_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)(kNbrMaxK * sizeof(unsigned long long))));
+    lds_set = true;
+  }
+  const double rel = (double)(d + 4) * 0x1p-53 * 1.01;
+  hipLaunchKernelGGL(kmeans_centroid_nbr_kernel, dim3((unsigned)k), dim3(kNbrThreads), lds, st,
+                     cen, k, d, L, kp2, rel, di, dv, pd);
+  return (int)hipGetLastError();
+}
+
+
 // Refine v3 over a batch of splits (ns[nsplit]; at most 64): per split, right
 // after its top-3 assign, hbmr_kmeans_refine_batch_q1 (reset = 1 for the
 // first split); then hbmr_kmeans_refine_batch_finish once.  The workspace

@@ -338,3 +338,33 @@ def test_refine_queue_pipeline_equals_single_kernel(dtype, monkeypatch):
     assert 0 < f3 <= f2 and r2 == r3
     assert n3 <= n2 + max(16, f3 // 1000)
     assert int((out[3][0] != truth_labels(x, c)).sum()) <= 1
+
+
+@pytest.mark.gpu
+def test_native_centroid_neighbour_table_bounds():
+    """hbmr_kmeans_centroid_nbr: per centroid the L nearest by a lower bound
+    rounded down (ascending, ties by index), and the [k, k] upper bounds
+    rounded up — checked against fp64 pairwise distances (a duplicated
+    centroid gives an off-diagonal zero)."""
+    from hbmr.ops import kmeans as km
+    g = torch.Generator().manual_seed(3)
+    k, d, L = 300, 40, 64
+    c = torch.randn(k, d, generator=g) * 3
+    c[7] = c[5]
+    img = km.CentroidImage(c, "cuda")
+    di, f, L2 = img.neighbors(L)
+    pd = img.pair_dist()
+    torch.cuda.synchronize()
+    cd = c.double()
+    exact = ((cd[:, None, :] - cd[None, :, :]) ** 2).sum(-1).sqrt()
+    di, f, pd = di.cpu().long(), f.cpu().double(), pd.cpu().double()
+    assert L2 == L and di.shape == (k, L)
+    true = exact[torch.arange(k)[:, None], di]
+    assert (f <= true).all() and (f >= true * (1 - 1e-6) - 1e-12).all()
+    assert (pd >= exact).all() and (pd <= exact * (1 + 1e-6) + 1e-12).all()
+    assert (f[:, 1:] >= f[:, :-1]).all()
+    assert di[5, 0].item() == 5 and di[5, 1].item() == 7 and di[7, 0].item() == 5
+    own = di[:, 0] == torch.arange(k)
+    assert own.sum().item() == k - 1           # every centroid first but 7 (5 ties first)
+    kth = exact.sort(dim=1).values[:, L - 1]
+    assert (true <= kth[:, None] * (1 + 1e-6) + 1e-9).all()
