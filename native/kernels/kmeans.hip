@@ -219,6 +219,9 @@ struct PackedTop3 : PackedArgMax {
 #ifndef HBMR_EXACT_TRACKS
 #define HBMR_EXACT_TRACKS 4   // register tracks per lane (4: r & 3; 8: r & 7)
 #endif
+#ifndef HBMR_EXACT_PAIRINS
+#define HBMR_EXACT_PAIRINS 1  // insert a track's two scores of a tile at once
+#endif
 struct PackedTop2x8 : PackedArgMax {
   static constexpr int NT = HBMR_EXACT_TRACKS;
   static constexpr uint32_t TMASK = NT == 8 ? 15u : 7u;   // cluster bits of a track
@@ -236,12 +239,27 @@ struct PackedTop2x8 : PackedArgMax {
       code[r] = base | (15u - r);
       asm("" : "+s"(code[r]));
     }
+#if HBMR_EXACT_PAIRINS
+    // registers r and r + NT belong to one track: both are inserted at once —
+    // the second of {b >= s, u, v} is max(med3(b, u, v), s) — 3 VALU ops per
+    // two scores instead of 4 (the epilogue is what bounds this kernel)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if ((r / NT) % 2) continue;
+      const float u = __uint_as_float((__float_as_uint(acc[r]) & vmask) | code[r]);
+      const float v = __uint_as_float((__float_as_uint(acc[r + NT]) & vmask) | code[r + NT]);
+      const float m = vmed3(tb[r % NT], u, v);
+      ts[r % NT] = vmax3(m, ts[r % NT], ts[r % NT]);
+      tb[r % NT] = vmax3(tb[r % NT], u, v);
+    }
+#else
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float u = __uint_as_float((__float_as_uint(acc[r]) & vmask) | code[r]);
       ts[r % NT] = vmed3(tb[r % NT], ts[r % NT], u);
       tb[r % NT] = vmax3(tb[r % NT], u, u);
     }
+#endif
   }
   __device__ __forceinline__ void top3(float& b, float& s, float& t) const {
     b = s = t = -3.0e38f;
