@@ -117,6 +117,8 @@ class GpuRuntime:
         # device sooner (each costs ~10-20 µs of host work per task to prepare),
         # larger ones amortise the per-launch kernels
         self.batch_target = max(1, tracker.conf.get_int("hbmr.gpu.batch.target", 16))
+        # a job's last batches halve in size (see _chunks)
+        self.taper = tracker.conf.get_boolean("hbmr.gpu.batch.taper", True)
         # > 0: the submitter of an idle device's first chunk waits (up to this
         # long) until it is launched.  In-process traces show the device
         # starting ~1 ms earlier, but same-box A/Bs of the bench measured no
@@ -269,8 +271,8 @@ class GpuRuntime:
                 cap = int(getattr(sj, "max_inflight_maps", 0) or 0)
                 if cap > 0:
                     per = min(per, cap)
-                for j in range(i, len(runs), per):
-                    chunk = runs[j:j + per]
+                for j, n in self._chunks(i, len(runs), per, cap == 0 and self.taper):
+                    chunk = runs[j:j + n]
                     if cap > 0:
                         # the launcher waits for capped maps to complete (the
                         # completer releases them): their device memory is
@@ -286,6 +288,25 @@ class GpuRuntime:
                         self._release_capped(dev, len(chunk) - n)
             for ev in picked:
                 ev.set()
+
+    @staticmethod
+    def _chunks(i, n, per, taper):
+        """(start, size) of the batches of runs[i:n].  Tapered: the last
+        2 x per runs go as halving batches, so the work left after a job's
+        last full batch — its certification and combiner kernels, which do
+        not fill the GPU — is short (the iteration tail)."""
+        out, j = [], i
+        while j < n:
+            r = n - j
+            if not taper or r > 2 * per:
+                c = min(per, r)
+            elif r > 4:
+                c = -(-r // 2)
+            else:
+                c = r
+            out.append((j, c))
+            j += c
+        return out
 
     @staticmethod
     def _release_capped(dev, n):

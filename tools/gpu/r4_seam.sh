@@ -10,4 +10,8 @@ timeout -k 10 300 python tools/kbench_exact.py --dtypes f16 > gpurun_out/${P}_kb
 cut -c1-600 gpurun_out/${P}_kbench_exact.json
 timeout -k 10 300 python bench.py > gpurun_out/${P}_bench.json 2> gpurun_out/${P}_bench.err || { tail -20 gpurun_out/${P}_bench.err; exit 1; }
 tail -1 gpurun_out/${P}_bench.json | cut -c1-300
+timeout -k 10 300 python bench.py --gpu-slots 1 --steps 10 --warmup 3 > gpurun_out/${P}_bench_1slot.json 2> gpurun_out/${P}_bench_1slot.err || { tail -20 gpurun_out/${P}_bench_1slot.err; exit 1; }
+tail -1 gpurun_out/${P}_bench_1slot.json | cut -c1-200
+timeout -k 10 300 python bench.py --steps 10 --warmup 3 -D hbmr.gpu.batch.taper=false > gpurun_out/${P}_bench_notaper.json 2> gpurun_out/${P}_bench_notaper.err || { tail -20 gpurun_out/${P}_bench_notaper.err; exit 1; }
+tail -1 gpurun_out/${P}_bench_notaper.json | cut -c1-200
 P=${P}p bash tools/gpu/r4_prof3.sh
