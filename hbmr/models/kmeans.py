@@ -763,9 +763,11 @@ class KMeansSplitJob(SplitJob):
             img.shift2 = torch.zeros_like(old.shift2)
             img.refresh(sums, counts)
             if self.exact:
-                # the 16-bit operand image the next job's first kernel reads:
-                # built here, behind the update, so the gate's event covers it
+                # the 16-bit operand image and the centroid neighbour table
+                # (one native kernel each) the next job's first kernels read:
+                # built here, behind the update, so the gate's event covers them
                 img.image16(self.exact_dtype)
+                img.neighbors()
             if TRACE.on:
                 TRACE.instant("kmeans.refresh_launched")
             STORE.put_image(self.cout, sums.device, img)
@@ -774,11 +776,6 @@ class KMeansSplitJob(SplitJob):
             rel = getattr(ctx, "release_dependents", None)
             if rel is not None:
                 rel()
-            if self.exact:
-                # the centroid neighbour table (Elkan scan, pair rule) on this
-                # stream while the next job's first top-3 assign runs on the
-                # slot streams: its certification waits on the table's event
-                img.neighbors()
             # the shift, the point count (and exact mode's counters) in one
             # device->host copy (one sync)
             vals = [img.shift2.max().double().sqrt(), counts.sum().double()]

@@ -38,6 +38,11 @@ _SIGS = {
                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "hbmr_kmeans_exact_prep": (c_int, [c_void_p, c_long, c_int, c_int, c_int, c_int, c_void_p,
                                        c_void_p, c_void_p, c_void_p, c_void_p]),
+    "hbmr_kmeans_assign_top3_q1_grouped": (c_int, [c_int, c_void_p, c_void_p, c_int, c_int,
+                                                   c_void_p, c_void_p, c_int, c_void_p,
+                                                   c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                                   c_void_p, c_void_p, c_void_p, c_void_p,
+                                                   c_void_p, c_long, c_void_p, c_void_p]),
     "hbmr_kmeans_centroid_nbr": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                                          c_void_p, c_void_p]),
     "hbmr_kmeans_image16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,

@@ -544,6 +544,9 @@ NBR_NATIVE_MAX_K = int(os.environ.get("HBMR_NBR_NATIVE_MAX_K", "8192"))
 # exact batches: one top-3 launch + one step-1 launch per up to 64 splits
 # (HBMR_EXACT_GROUPED=0: a launch of each per split)
 GROUPED_EXACT = os.environ.get("HBMR_EXACT_GROUPED", "1") != "0"
+# step 1 of the certification inside the grouped top-3 kernel's epilogue
+# (HBMR_EXACT_FUSED_Q1=0: the separate step-1 scan over materialised arrays)
+FUSED_Q1 = os.environ.get("HBMR_EXACT_FUSED_Q1", "1") != "0"
 
 
 def _exact_group(group, img, stats, labels_ptr, c16, ch, norms, dt, scratch, stream, lib, st):
@@ -566,6 +569,23 @@ def _exact_group(group, img, stats, labels_ptr, c16, ch, norms, dt, scratch, str
     P = ctypes.c_void_p * B
     xs = P(*[sp.xb.data_ptr() for sp in group])
     nsa = (ctypes.c_long * B)(*ns)
+    if FUSED_Q1 and img.dp <= 128:
+        # step 1 in the top-3 epilogue: no candidate / score / margin arrays
+        rb = _RefineBatch(group, img, stats, scratch, stream)
+        cn, cmax, ce, cemax = norms
+        rc = lib.hbmr_kmeans_assign_top3_q1_grouped(
+            B, xs, nsa, img.dp, int(dt == torch.float16), _ptr(c16), _ptr(ch), img.k_pad,
+            labels_ptr, P(*[sp.xnorm.data_ptr() for sp in group]),
+            P(*[sp.xbn2.data_ptr() for sp in group]), P(*[sp.xerr.data_ptr() for sp in group]),
+            img.d, img.k, _ptr(cn), _ptr(cmax), _ptr(ce), _ptr(cemax), _ptr(rb.ws),
+            rb.ws.numel(), _ptr(rb.pd), st)
+        _lib.check(rc, "hbmr_kmeans_assign_top3_q1_grouped")
+        o = 0
+        for i in range(B):
+            rb.labels[i] = labels_ptr + 4 * o
+            o += ns[i]
+        rb.finish()
+        return N
     rc = lib.hbmr_kmeans_assign_top3_grouped(B, xs, nsa, img.dp, int(dt == torch.float16),
                                              _ptr(c16), _ptr(ch), img.k_pad, labels_ptr,
                                              _ptr(cand), _ptr(sc), _ptr(mg), st)

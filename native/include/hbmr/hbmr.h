@@ -53,6 +53,13 @@ int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float
                            const float* nbr_dist, int L, int32_t* labels, const int32_t* cand,
                            const float* scores, const float* margin, unsigned long long* stats,
                            int nstats, hipStream_t st);
+int hbmr_kmeans_assign_top3_q1_grouped(int nsplit, const void* const* X, const long* n, int dp,
+                                       int f16, const void* C, const float* chalf, int k_pad,
+                                       int32_t* labels, const float* const* xnorm,
+                                       const float* const* xbn2, const float* const* xerr,
+                                       int d, int k, const float* cnorm, const float* cmax,
+                                       const float* cerr, const float* cerrmax, void* ws,
+                                       long ws_bytes, const float* dcc, hipStream_t st);
 int hbmr_kmeans_assign_top3_grouped(int nsplit, const void* const* X, const long* n, int dp,
                                     int f16, const void* C, const float* chalf, int k_pad,
                                     int32_t* labels, int32_t* cand, float* scores, float* margin,

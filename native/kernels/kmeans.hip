@@ -548,7 +548,10 @@ __device__ __forceinline__ void read_tile32(const char* buf, int col, int h, bf1
   }
 }
 
-template <int D, int PB, bool EXACT = false, bool F16 = false, bool TOP3 = false>
+struct NoFin {};   // assign_tile_v2's default finish (finish_point)
+
+template <int D, int PB, bool EXACT = false, bool F16 = false, bool TOP3 = false,
+          class Fin = NoFin>
 __device__ __forceinline__ void assign_tile_v2(const __bf16* __restrict__ X, long n,
                                                const __bf16* __restrict__ C,
                                                const float* __restrict__ chalf, int ntiles,
@@ -556,7 +559,7 @@ __device__ __forceinline__ void assign_tile_v2(const __bf16* __restrict__ X, lon
                                                float* __restrict__ scores, long blk, char* smem,
                                                int32_t* __restrict__ cand = nullptr,
                                                float* __restrict__ margin = nullptr,
-                                               long cs = -1) {
+                                               long cs = -1, const Fin* fin = nullptr) {
   static_assert(D <= 128, "v2 keeps PB point blocks of D ≤ 128 in registers");
   using V = AssignV2<D>;
   constexpr int KS = V::KS;
@@ -638,10 +641,14 @@ __device__ __forceinline__ void assign_tile_v2(const __bf16* __restrict__ X, lon
     for (int pb = 0; pb < PB; ++pb) am[pb].update(acc[pb], t);
   }
 
+  if constexpr (!std::is_same<Fin, NoFin>::value) {
+    (*fin)(am, h, p0, col, n, labels);        // e.g. the fused step-1 certification
+  } else {
 #pragma unroll
-  for (int pb = 0; pb < PB; ++pb)
-    finish_point<EXACT>(am[pb], h, p0 + pb * 32 + col, n, labels, cand, scores, margin, nullptr,
-                        cs);
+    for (int pb = 0; pb < PB; ++pb)
+      finish_point<EXACT>(am[pb], h, p0 + pb * 32 + col, n, labels, cand, scores, margin,
+                          nullptr, cs);
+  }
 }
 
 template <int D>
@@ -2326,12 +2333,15 @@ struct RefineLayout {
 };
 inline RefineLayout refine_layout(int nsplit, const long* ns) {
   RefineLayout L;
-  long total = 0, cap1 = 0;
+  long total = 0, cap1 = 0, nb_fused = 0;
   for (int i = 0; i < nsplit; ++i) {
     total += ns[i];
     cap1 += ceil_div(ceil_div(ns[i], 256 * kQ1Per), kQShards) * 256 * kQ1Per;
+    nb_fused += ceil_div(ns[i], 256);
   }
-  L.cap1 = cap1;
+  // the fused top-3 epilogue appends from 256-point workgroups, shard =
+  // blockIdx % kQShards: at most ceil(nb / kQShards) workgroups per shard
+  L.cap1 = std::max<long>(cap1, ceil_div(nb_fused, kQShards) * 256);
   L.g2 = (unsigned)std::max<long>(1, std::min<long>(kRefineGrid, ceil_div(total, 4 * kQ2Per)));
   const long per_iter = (long)L.g2 * 4 * kQ2Per;           // Q1 entries per grid iteration
   L.cap2 = ceil_div(L.g2, kQShards) * 4 * kQ2Per * std::max<long>(1, ceil_div(total, per_iter));
@@ -2355,6 +2365,53 @@ __device__ __forceinline__ long shard_slot(const uint32_t (&c)[kQShards], long c
 
 __device__ __forceinline__ uint32_t lane_rank(unsigned long long m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Step 1's certification of one point (its kernel top-3 in e, best - second
+// margin m2, cnb / ceb = |c_b|, |c_b - c~_b|): true = not certified, the point
+// goes to step 2.  Shared by the step-1 scan and the fused top-3 epilogue.
+__device__ __forceinline__ bool q1_flagged(const ExactQ1& e, float m2, float cnb, float ceb, int k,
+                                           double gam, double cm, double cem, double pack_rel,
+                                           const float* __restrict__ cnorm,
+                                           const float* __restrict__ cerr,
+                                           const float* __restrict__ dcc) {
+  const double inflate = 1.0 + 0x1p-20;
+  const double xn = ((double)e.xn + (double)e.xe) * inflate;
+  const double x2 = (double)e.x2;
+  const double sb = e.sb;
+  const double mm = m2;
+  const double amax = ((double)e.xe + cem) * inflate;
+  double eb, es, dl_b, dl_s;
+  exact_bound(sb, ((double)cnb + (double)ceb) * inflate, xn, x2,
+              ((double)e.xe + (double)ceb) * inflate, gam, pack_rel, eb, dl_b);
+  exact_bound(sb - mm, cm, xn, x2, amax, gam, pack_rel, es, dl_s);
+  bool flag = !(mm > eb + es && dl_s >= 2.0 * amax);
+  const int b = e.b, sc = e.s, t = e.t;
+  if (flag && dcc != nullptr && t < k && t != b) {
+    // Pair rule: D_s - D_b >= (D~_s - D~_b) - 2|c~_b - c~_s| e_x
+    //   - 2 sqrt(D~_s) e_s - 2 sqrt(D~_b) e_b - (e_x + e_b)^2
+    // (x - c_j = (x~ - c~_j) + (dx - dc_j); the dx terms of b and s
+    // cancel up to (c~_b - c~_s).dx), with |c~_b - c~_s| <= |c_b - c_s|
+    // + e_b + e_s — tighter than E_b + E_s where the two centroids are
+    // close and the point is not.  Everything ranked at or below t is
+    // beaten by the generic rule at t (margin b-t against E_b + E_max(t)).
+    const double ex = (double)e.xe * inflate;
+    const double ebb = (double)ceb * inflate;
+    const double ess = (double)cerr[sc] * inflate;
+    const double dbs = ((double)dcc[(size_t)b * k + sc] + (double)ceb + (double)cerr[sc]) *
+                       inflate;
+    double eap_b, rb, eap_s, rs;
+    score_err(sb, ((double)cnb + (double)ceb) * inflate, xn, x2, gam, pack_rel, eap_b, rb);
+    score_err(sb - mm, ((double)cnorm[sc] + (double)cerr[sc]) * inflate, xn, x2, gam,
+              pack_rel, eap_s, rs);
+    const double ep = dbs * ex + rs * ess + rb * ebb + 0.5 * (ex + ebb) * (ex + ebb) +
+                      eap_b + eap_s;
+    double et, dl_t;
+    const double m3 = e.m3;
+    exact_bound(sb - m3, cm, xn, x2, amax, gam, pack_rel, et, dl_t);
+    if (mm > ep && m3 > eb + et && dl_t >= 2.0 * amax) flag = false;
+  }
+  return flag;
 }
 
 // Step 1 over one block of 256 * kQ1Per points of split sidx (block index blk
@@ -2407,45 +2464,8 @@ __device__ __forceinline__ void refine_q1_block(
   uint32_t rank[kQ1Per];
 #pragma unroll
   for (int i = 0; i < kQ1Per; ++i) {
-    flag[i] = false;
-    if (in[i] && e[i].s < k) {
-      const double xn = ((double)e[i].xn + (double)e[i].xe) * inflate;
-      const double x2 = (double)e[i].x2;
-      const double sb = e[i].sb;
-      const double mm = m2[i];
-      const double amax = ((double)e[i].xe + cem) * inflate;
-      double eb, es, dl_b, dl_s;
-      exact_bound(sb, ((double)cnb[i] + (double)ceb[i]) * inflate, xn, x2,
-                  ((double)e[i].xe + (double)ceb[i]) * inflate, gam, pack_rel, eb, dl_b);
-      exact_bound(sb - mm, cm, xn, x2, amax, gam, pack_rel, es, dl_s);
-      flag[i] = !(mm > eb + es && dl_s >= 2.0 * amax);
-      const int b = e[i].b, sc = e[i].s, t = e[i].t;
-      if (flag[i] && dcc != nullptr && t < k && t != b) {
-        // Pair rule: D_s - D_b >= (D~_s - D~_b) - 2|c~_b - c~_s| e_x
-        //   - 2 sqrt(D~_s) e_s - 2 sqrt(D~_b) e_b - (e_x + e_b)^2
-        // (x - c_j = (x~ - c~_j) + (dx - dc_j); the dx terms of b and s
-        // cancel up to (c~_b - c~_s).dx), with |c~_b - c~_s| <= |c_b - c_s|
-        // + e_b + e_s — tighter than E_b + E_s where the two centroids are
-        // close and the point is not.  Everything ranked at or below t is
-        // beaten by the generic rule at t (margin b-t against E_b + E_max(t)).
-        const double ex = (double)e[i].xe * inflate;
-        const double ebb = (double)ceb[i] * inflate;
-        const double ess = (double)cerr[sc] * inflate;
-        const double dbs = ((double)dcc[(size_t)b * k + sc] + (double)ceb[i] +
-                            (double)cerr[sc]) * inflate;
-        double eap_b, rb, eap_s, rs;
-        score_err(sb, ((double)cnb[i] + (double)ceb[i]) * inflate, xn, x2, gam, pack_rel,
-                  eap_b, rb);
-        score_err(sb - mm, ((double)cnorm[sc] + (double)cerr[sc]) * inflate, xn, x2, gam,
-                  pack_rel, eap_s, rs);
-        const double ep = dbs * ex + rs * ess + rb * ebb + 0.5 * (ex + ebb) * (ex + ebb) +
-                          eap_b + eap_s;
-        double et, dl_t;
-        const double m3 = e[i].m3;
-        exact_bound(sb - m3, cm, xn, x2, amax, gam, pack_rel, et, dl_t);
-        if (mm > ep && m3 > eb + et && dl_t >= 2.0 * amax) flag[i] = false;
-      }
-    }
+    flag[i] = in[i] && e[i].s < k &&
+              q1_flagged(e[i], m2[i], cnb[i], ceb[i], k, gam, cm, cem, pack_rel, cnorm, cerr, dcc);
     const unsigned long long m = __ballot(flag[i]);
     rank[i] = lane_rank(m);
     if (lane == 0) wcnt[wave][i] = (uint32_t)__popcll(m);
@@ -2515,6 +2535,143 @@ __global__ __launch_bounds__(256) void kmeans_refine_q1_grouped_kernel(
   refine_q1_block(tbl.n[s], s, b - tbl.blk[s], d, k, tbl.xnorm[s], tbl.xbn2[s], tbl.xerr[s],
                   cnorm, cmax, cerr, cerrmax, pack_rel, labels + o, cand + o, score + o,
                   margin + o, tbl.total, qcount, q1, cap1, stats, dcc);
+}
+
+// ---------------------------------------------------------------------------
+// Top-3 assign with step 1 fused into its epilogue (HBMR_EXACT_FUSED_Q1, the
+// default): the lane that finishes a point holds its kernel top 3 and
+// margins in registers, certifies it there (q1_flagged) and appends only an
+// uncertain point to the step-2 queue — one atomic per workgroup — so the
+// candidate / score / margin arrays (20 B per point written, then read back
+// with the labels by the step-1 scan) are never materialised.
+struct FusedQ1Fin {
+  const float* xnorm;
+  const float* xbn2;
+  const float* xerr;
+  int sidx;
+  int k;
+  double gam, pack_rel;
+  const float* cmax_p;       // max |c_j| and max |c_j - c~_j| (device, 1 float each)
+  const float* cerrmax_p;
+  const float* cnorm;
+  const float* cerr;
+  const float* dcc;
+  uint32_t* qcount;
+  ExactQ1* q1;
+  long cap1;
+  unsigned long long* stats;
+
+  template <class AM, int PB>
+  __device__ __forceinline__ void operator()(const AM (&am)[PB], int h, long p0, int col, long n,
+                                             int32_t* __restrict__ labels) const {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ uint32_t fq_cnt[4 * PB];
+    __shared__ uint32_t fq_base;
+    const int shard = blockIdx.x % kQShards;
+    const double inflate = 1.0 + 0x1p-20;
+    const double cem = (double)cerrmax_p[0] * inflate;
+    const double cm = (double)cmax_p[0] * inflate + cem;
+    ExactQ1 e[PB];
+    bool flag[PB];
+    uint32_t rank[PB];
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb) {
+      float v[3];
+      int c[3];
+      am[pb].top3(v[0], v[1], v[2]);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) c[i] = am[pb].cluster(v[i], h);
+      float ov[3];
+      int oc[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        ov[i] = __shfl_xor(v[i], 32);
+        oc[i] = __shfl_xor(c[i], 32);
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) insert3(v, c, ov[i], oc[i]);
+      if constexpr (HasTracks<AM>::value) {
+        if (((c[0] ^ c[1]) & AM::TMASK) == 0) {
+          v[2] = v[0];
+          c[2] = c[0];
+        }
+      }
+      const long p = p0 + pb * 32 + col;
+      flag[pb] = false;
+      if (h == 0 && p < n) {
+        labels[p] = c[0];
+        const float bs = am[pb].score(v[0]);
+        const float m2 = bs - am[pb].score(v[1]);
+        ExactQ1& q = e[pb];
+        q.row = (uint32_t)p;
+        q.split = (uint32_t)sidx;
+        q.b = c[0];
+        q.s = c[1];
+        q.t = c[2];
+        q.sb = bs;
+        q.m3 = bs - am[pb].score(v[2]);
+        q.x2 = xbn2[p];
+        q.xn = xnorm[p];
+        q.xe = xerr[p];
+        q.pad0 = q.pad1 = 0.f;
+        flag[pb] = q.s < k && q1_flagged(q, m2, cnorm[q.b], cerr[q.b], k, gam, cm, cem,
+                                         pack_rel, cnorm, cerr, dcc);
+      }
+      const unsigned long long m = __ballot(flag[pb]);
+      rank[pb] = lane_rank(m);
+      if (lane == 0) fq_cnt[wave * PB + pb] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t tot = 0;
+#pragma unroll
+      for (int i = 0; i < 4 * PB; ++i) {
+        const uint32_t c = fq_cnt[i];
+        fq_cnt[i] = tot;
+        tot += c;
+      }
+      fq_base = tot ? atomicAdd(qcount + shard, tot) : 0u;
+      if (tot) atomicAdd(stats + 4 * shard, (unsigned long long)tot);
+    }
+    __syncthreads();
+    ExactQ1* out = q1 + (long)shard * cap1 + fq_base;
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb)
+      if (flag[pb]) out[fq_cnt[wave * PB + pb] + rank[pb]] = e[pb];
+  }
+};
+
+struct TopQ1Table {       // the batch's splits, by value (X, per-point norms)
+  int nsplit;
+  const __bf16* X[kMaxGroup];
+  const float* xnorm[kMaxGroup];
+  const float* xbn2[kMaxGroup];
+  const float* xerr[kMaxGroup];
+  long off[kMaxGroup + 1];
+  long blk[kMaxGroup + 1];
+};
+
+template <int D, bool F16>
+__global__ __launch_bounds__(AssignV2<D>::THREADS, HBMR_EXACT_MINB) void
+kmeans_assign_top3_q1_grouped_kernel(const TopQ1Table tbl, const __bf16* __restrict__ C,
+                                     const float* __restrict__ chalf, int ntiles,
+                                     int32_t* __restrict__ labels, FusedQ1Fin fin) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const long b = hbmr_xcd_remap(blockIdx.x, gridDim.x);
+  int lo = 0, hi = tbl.nsplit;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (tbl.blk[mid] <= b) lo = mid; else hi = mid;
+  }
+  const int s = __builtin_amdgcn_readfirstlane(lo);
+  const long o = tbl.off[s];
+  fin.xnorm = tbl.xnorm[s];
+  fin.xbn2 = tbl.xbn2[s];
+  fin.xerr = tbl.xerr[s];
+  fin.sidx = s;
+  assign_tile_v2<D, 2, true, F16, false, FusedQ1Fin>(tbl.X[s], tbl.off[s + 1] - o, C, chalf,
+                                                     ntiles, labels + o, nullptr, b - tbl.blk[s],
+                                                     smem, nullptr, nullptr, -1, &fin);
 }
 
 // 16 features of a row per lane of an 8-lane group: 128m + 32h + 4sub + (0..3)
@@ -3364,6 +3521,77 @@ int hbmr_kmeans_assign_top3_grouped(int nsplit, const void* const* X, const long
     default: return (int)hipErrorInvalidValue;
   }
 #undef HBMR_TOP3G
+}
+
+// Exact mode, one batch: top-3 assign with step 1 fused (FusedQ1Fin): labels
+// of every point, the batch's step-2 queue and flagged count in ws (as
+// hbmr_kmeans_refine_batch_q1g leaves them); dp <= 128
+int hbmr_kmeans_assign_top3_q1_grouped(int nsplit, const void* const* X, const long* n, int dp,
+                                       int f16, const void* C, const float* chalf, int k_pad,
+                                       int32_t* labels, const float* const* xnorm,
+                                       const float* const* xbn2, const float* const* xerr,
+                                       int d, int k, const float* cnorm, const float* cmax,
+                                       const float* cerr, const float* cerrmax, void* ws,
+                                       long ws_bytes, const float* dcc, hipStream_t st) {
+  if (nsplit <= 0 || nsplit > kMaxGroup || k_pad % 32 || k <= 0 || k_pad < k ||
+      d > kRefineMaxDp || !labels || ((uintptr_t)ws & 255) || (dp != 64 && dp != 128))
+    return (int)hipErrorInvalidValue;
+  TopQ1Table t;
+  memset(&t, 0, sizeof(t));
+  t.nsplit = nsplit;
+  constexpr int pts = 4 * 2 * 32;             // AssignV2<D>::WAVES * PB * 32
+  long total = 0, nb = 0;
+  for (int i = 0; i < nsplit; ++i) {
+    if (n[i] < 0 || n[i] > 0x7fffffffL) return (int)hipErrorInvalidValue;
+    t.X[i] = reinterpret_cast<const __bf16*>(X[i]);
+    t.xnorm[i] = xnorm[i];
+    t.xbn2[i] = xbn2[i];
+    t.xerr[i] = xerr[i];
+    t.off[i] = total;
+    t.blk[i] = nb;
+    total += n[i];
+    nb += ceil_div(n[i], pts);
+  }
+  t.off[nsplit] = total;
+  t.blk[nsplit] = nb;
+  const RefineLayout Ly = refine_layout(nsplit, n);
+  if (ws_bytes < (long)Ly.bytes) return (int)hipErrorInvalidValue;
+  char* w = static_cast<char*>(ws);
+  HBMR_RETURN_IF_ERROR(hipMemsetAsync(w, 0, kHdrClear, st));
+  if (nb == 0) return 0;
+  if (nb > 0x7fffffffL) return (int)hipErrorInvalidValue;
+  int tb = 0;
+  while ((1 << tb) < k_pad / 32) ++tb;
+  FusedQ1Fin fin;
+  memset(&fin, 0, sizeof(fin));
+  fin.k = k;
+  const double inflate = 1.0 + 0x1p-20;
+  fin.gam = (double)(d + 2) * 0x1p-23 * 1.01;
+  // cmax / cerrmax are device values: the kernel reads them through cnorm's
+  // image: pass pointers and let the kernel fold them (see below)
+  fin.pack_rel = ldexp(1.0, 4 + tb - 23);
+  fin.cnorm = cnorm;
+  fin.cerr = cerr;
+  fin.dcc = dcc;
+  fin.qcount = reinterpret_cast<uint32_t*>(w);
+  fin.q1 = reinterpret_cast<ExactQ1*>(w + Ly.off1);
+  fin.cap1 = Ly.cap1;
+  fin.stats = reinterpret_cast<unsigned long long*>(w + kStatsOff);
+  fin.cmax_p = cmax;
+  fin.cerrmax_p = cerrmax;
+  (void)inflate;
+#define HBMR_TOP3Q1(D)                                                                         \
+  {                                                                                            \
+    auto kern = f16 ? kmeans_assign_top3_q1_grouped_kernel<D, true>                            \
+                    : kmeans_assign_top3_q1_grouped_kernel<D, false>;                          \
+    hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(AssignV2<D>::THREADS),                   \
+                       AssignV2<D>::LDS_BYTES, st, t, reinterpret_cast<const __bf16*>(C),      \
+                       chalf, k_pad / 32, labels, fin);                                        \
+    return (int)hipGetLastError();                                                             \
+  }
+  if (dp == 64) HBMR_TOP3Q1(64)
+  HBMR_TOP3Q1(128)
+#undef HBMR_TOP3Q1
 }
 
 int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float* xnorm,

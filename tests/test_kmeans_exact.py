@@ -189,13 +189,15 @@ def test_exact_assign_with_saturated_fp16_data():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("grouped", [True, False])
-def test_assign_exact_batch_equals_per_split(grouped, monkeypatch):
+@pytest.mark.parametrize("grouped,fused", [(True, True), (True, False), (False, False)])
+def test_assign_exact_batch_equals_per_split(grouped, fused, monkeypatch):
     """The batched exact assign (labels written back to back, shared scratch;
-    grouped: one top-3 launch and one step-1 launch for the batch) gives each
-    split the labels and stats the per-split call gives."""
+    grouped: one top-3 launch and one step-1 launch for the batch; fused: step
+    1 inside the top-3 epilogue, no candidate arrays) gives each split the
+    labels and stats (flagged, relabelled, scanned) the per-split call gives."""
     from hbmr.ops import kmeans as km
     monkeypatch.setattr(km, "GROUPED_EXACT", grouped)
+    monkeypatch.setattr(km, "FUSED_Q1", fused)
     d, k = 128, 256
     x, c = _blobs(210_000, d, k, 5)
     img = km.CentroidImage(c, "cuda")
