@@ -341,34 +341,58 @@ class JobInProgress:
     def _index(self, tracker: TrackerInfo, on_gpu, device):
         """Per-(tracker, device) queues of pending TIPs by locality level, built
         once per job and consumed with lazy deletion: O(1) amortised per
-        assignment instead of the reference's scan of every TIP."""
+        assignment instead of the reference's scan of every TIP.  A build
+        visits only what is local to the tracker — its HBM-resident split keys
+        (by_split_key) and the job's TIPs naming it (_by_location) — not every
+        pending TIP, so a job's index costs O(maps) over all trackers, not
+        O(maps x trackers)."""
         key = (tracker.name, device if on_gpu else None)
         idx = self._loc_index.get(key)
         if idx is None or idx[4] != len(tracker.cached):
-            lv0, lv1, lv2, rest = [], [], [], []
-            cached_keys = {k for k, _ in tracker.cached}
-            host = tracker.status.host
-            for tip in self.pending_maps:
-                sk = tip.split_key()
-                locs = tip.locations()
-                if sk is not None and on_gpu and (sk, device) in tracker.cached:
-                    lv0.append(tip)
-                elif sk is not None and sk in cached_keys:
-                    lv1.append(tip)
-                elif tracker.name in locs or host in locs:
-                    lv2.append(tip)
-                elif locs:
-                    rest.append(tip)
-            # the rack-local level is resolved on first use (delay scheduling
-            # rarely gets there, and the topology lookups were most of a build)
-            idx = [lv0[::-1], lv1[::-1], lv2[::-1], None, len(tracker.cached), rest]
+            pend = self.pending_maps
+            byk = self.by_split_key
+            lv0, lv1, lv2, seen = [], [], [], set()
+            if byk and tracker.cached:
+                if on_gpu:
+                    for k, d in tracker.cached:
+                        tip = byk.get(k)
+                        if d == device and tip is not None and tip in pend and tip not in seen:
+                            lv0.append(tip)
+                            seen.add(tip)
+                for k, _d in tracker.cached:
+                    tip = byk.get(k)
+                    if tip is not None and tip in pend and tip not in seen:
+                        lv1.append(tip)
+                        seen.add(tip)
+            byloc = self._by_location()
+            for loc in (tracker.name, tracker.status.host):
+                for tip in byloc.get(loc, ()):
+                    if tip in pend and tip not in seen:
+                        lv2.append(tip)
+                        seen.add(tip)
+            # stacks popped from the end: pending (FIFO = map index) order
+            order = lambda lv: sorted(lv, key=lambda t: t.partition, reverse=True)  # noqa: E731
+            idx = [order(lv0), order(lv1), order(lv2), None, len(tracker.cached), seen]
             self._loc_index[key] = idx
         return idx
+
+    def _by_location(self):
+        """location (tracker name / host) -> the job's map TIPs naming it."""
+        bl = self.__dict__.get("_byloc")
+        if bl is None:
+            bl = {}
+            for tip in self.maps:
+                for loc in tip.locations():
+                    bl.setdefault(loc, []).append(tip)
+            self._byloc = bl
+        return bl
 
     def _rack_level(self, tracker, idx):
         if idx[3] is None:
             topo = self.jt.topology
-            idx[3] = [t for t in idx[5] if tracker.rack in topo.resolve(t.locations())][::-1]
+            seen = idx[5]
+            rest = [t for t in self.pending_maps if t not in seen and t.locations()]
+            idx[3] = [t for t in rest if tracker.rack in topo.resolve(t.locations())][::-1]
             idx[5] = None
         return idx[3]
 
