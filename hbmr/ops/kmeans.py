@@ -557,15 +557,6 @@ def _exact_group(group, img, stats, labels_ptr, c16, ch, norms, dt, scratch, str
     ns = [sp.shape[0] for sp in group]
     N = sum(ns)
     dev = group[0].xb.device
-    key = ("exact-group", N)
-    bufs = scratch.get(key)
-    if bufs is None:
-        for kk in [kk for kk in scratch if isinstance(kk, tuple) and kk[0] == "exact-group"]:
-            del scratch[kk]
-        bufs = scratch[key] = (torch.empty(2 * N, dtype=torch.int32, device=dev),
-                               torch.empty(N, dtype=torch.float32, device=dev),
-                               torch.empty(2 * N, dtype=torch.float32, device=dev))
-    cand, sc, mg = bufs
     P = ctypes.c_void_p * B
     xs = P(*[sp.xb.data_ptr() for sp in group])
     nsa = (ctypes.c_long * B)(*ns)
@@ -586,6 +577,15 @@ def _exact_group(group, img, stats, labels_ptr, c16, ch, norms, dt, scratch, str
             o += ns[i]
         rb.finish()
         return N
+    key = ("exact-group", N)
+    bufs = scratch.get(key)
+    if bufs is None:
+        for kk in [kk for kk in scratch if isinstance(kk, tuple) and kk[0] == "exact-group"]:
+            del scratch[kk]
+        bufs = scratch[key] = (torch.empty(2 * N, dtype=torch.int32, device=dev),
+                               torch.empty(N, dtype=torch.float32, device=dev),
+                               torch.empty(2 * N, dtype=torch.float32, device=dev))
+    cand, sc, mg = bufs
     rc = lib.hbmr_kmeans_assign_top3_grouped(B, xs, nsa, img.dp, int(dt == torch.float16),
                                              _ptr(c16), _ptr(ch), img.k_pad, labels_ptr,
                                              _ptr(cand), _ptr(sc), _ptr(mg), st)
