@@ -117,37 +117,54 @@ class InProcessComm(Comm):
         rv = _Rendezvous(n)
         return [cls(rv, r) for r in range(n)]
 
-    def _exchange(self, obj):
+    @staticmethod
+    def _sync(obj):
+        """Device tensors: the posting (or copying) stream has finished with
+        them — every rank's stream is its own, and the peers read on theirs."""
+        t = obj[0] if isinstance(obj, (list, tuple)) else obj
+        if torch.is_tensor(t) and t.is_cuda:
+            torch.cuda.current_stream(t.device).synchronize()
+
+    def _exchange(self, obj, take=None):
+        """Post ``obj``, read every rank's; ``take`` (optional) copies what this
+        rank needs out of the posted objects while the peers still hold them
+        (their streams may reuse the memory once the exchange returns)."""
         rv = self.rv
+        self._sync(obj)
         rv.slots[self.rank] = obj
         rv.barrier_obj.wait()
         got = list(rv.slots)
+        if take is not None:
+            got = take(got)
+            self._sync(got)
         rv.barrier_obj.wait()
         return got
 
     def all_reduce(self, t):
         self._note("all_reduce", t)
         # exchange snapshots: peers may still be reading while we write into t
-        got = self._exchange(t.detach().clone())
-        out = got[0].to(t.device).clone()
-        for g in got[1:]:
-            out += g.to(t.device)
-        t.copy_(out)
+        def take(got):
+            out = got[0].to(t.device).clone()
+            for g in got[1:]:
+                out += g.to(t.device)
+            return [out]
+        t.copy_(self._exchange(t.detach().clone(), take)[0])
         return t
 
     def all_gather(self, t):
         self._note("all_gather", t)
-        return [g.to(t.device) for g in self._exchange(t)]
+        return self._exchange(t, lambda got: [g.to(t.device, copy=True) for g in got])
 
     def all_to_all(self, outs):
         self._note("all_to_all", outs[0])
-        got = self._exchange(list(outs))
-        return [got[j][self.rank] for j in range(self.world_size)]
+        me = self.rank
+        return self._exchange(list(outs),
+                              lambda got: [got[j][me].clone() for j in range(self.world_size)])
 
     def broadcast(self, t, src=0):
         self._note("broadcast", t)
-        got = self._exchange(t.detach().clone())
-        t.copy_(got[src].to(t.device))
+        got = self._exchange(t.detach().clone(), lambda got: [got[src].to(t.device, copy=True)])
+        t.copy_(got[0])
         return t
 
     def barrier(self):
