@@ -904,7 +904,11 @@ class TeraSortSplitJob(SplitJob):
             FileOutputCommitter().commit_job(jip.conf)
 
 
-_PINNED: dict = {}      # (nbuf, chunk) -> pinned host buffers, reused across jobs
+# (nbuf, chunk) -> idle rings of pinned host buffers, reused across jobs: a
+# writer takes a ring of its own (two reduces of one process — trackers of a
+# LocalCluster — must never share one) and gives it back when it closes
+_PINNED: dict = {}
+_PINNED_LOCK = __import__("threading").Lock()
 
 
 class _PartWriter:
@@ -936,10 +940,13 @@ class _PartWriter:
         if self.cuda:
             nbuf = 2 * self.writers
             key = (nbuf, self.CHUNK)
-            bufs = _PINNED.get(key)
+            with _PINNED_LOCK:
+                idle = _PINNED.setdefault(key, [])
+                bufs = idle.pop() if idle else None
             if bufs is None:
-                bufs = _PINNED[key] = [torch.empty(self.CHUNK, dtype=torch.uint8,
-                                                   pin_memory=True) for _ in range(nbuf)]
+                bufs = [torch.empty(self.CHUNK, dtype=torch.uint8, pin_memory=True)
+                        for _ in range(nbuf)]
+            self.ring_key = key
             self.bufs = bufs
             self.pending = [None] * nbuf
             self.stream = torch.cuda.Stream(device)
@@ -1014,6 +1021,12 @@ class _PartWriter:
         finally:
             self.pool.shutdown()
             self.files = []
+            bufs = getattr(self, "bufs", None)
+            if bufs is not None:
+                # every piece is written (or failed): the ring is free again
+                self.bufs = None
+                with _PINNED_LOCK:
+                    _PINNED.setdefault(self.ring_key, []).append(bufs)
 
 
 def terasort_conf(base=None, rows=1_000_000, split_rows=None, output=None, inp=None,
