@@ -243,6 +243,8 @@ class GpuRuntime:
             run = dev.q.get()
             if run is None:
                 break
+            if TRACE.on:
+                TRACE.instant("gpu.wake", n=len(run) if isinstance(run, list) else 1)
             groups: dict = {}
             picked = [run.picked] if getattr(run, "picked", None) is not None else []
             for r in self._drain(dev, run, picked):

@@ -628,6 +628,9 @@ class KMeansSplitJob(SplitJob):
         relabelled counts accumulate on the device per (job, device) and are
         reported by the reduce (no host sync here)."""
         from ..ops import kmeans as km
+        from ..utils.trace import TRACE
+        if TRACE.on:
+            TRACE.instant("kmeans.map_exact", n=len(datas))
         ctx = ctxs[0]
         store = ctx.tracker.__dict__.setdefault("_scratch", {})
         scratch = store.setdefault(("kmeans-exact", str(ctx.device), id(ctx.stream)), {})

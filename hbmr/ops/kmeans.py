@@ -20,6 +20,7 @@ import threading
 import torch
 
 from . import _lib
+from ..utils.trace import TRACE
 
 SUPPORTED_DP = (64, 128, 256)
 
@@ -563,6 +564,8 @@ def _exact_group(group, img, stats, labels_ptr, c16, ch, norms, dt, scratch, str
     if FUSED_Q1 and img.dp <= 128:
         # step 1 in the top-3 epilogue: no candidate / score / margin arrays
         rb = _RefineBatch(group, img, stats, scratch, stream)
+        if TRACE.on:
+            TRACE.instant("kmeans.top3_launch", n=B)
         cn, cmax, ce, cemax = norms
         rc = lib.hbmr_kmeans_assign_top3_q1_grouped(
             B, xs, nsa, img.dp, int(dt == torch.float16), _ptr(c16), _ptr(ch), img.k_pad,
