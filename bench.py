@@ -264,6 +264,10 @@ def main():
                        "combiner": conf.get("hbmr.kmeans.combiner") or "delta"},
             "job_makespan_ms": round(ms, 3),
             "phases_ms": phases_ms,
+            # each timed job's finish after its predecessor's (the first: after
+            # its submission, which follows the opening barrier job)
+            "release_to_finish_ms_per_job": [round(1e3 * t["finish"], 2) for t in tls
+                                             if t.get("finish") is not None],
             "map_device_ms_per_job": map_device_ms,
             "points_per_sec": round(a.points * a.steps / dt, 1),
             "maps_launched": n_maps, "gpu_maps": gpu_maps, "cpu_maps": cpu_maps,

@@ -124,6 +124,12 @@ class GpuRuntime:
         # starting ~1 ms earlier, but same-box A/Bs of the bench measured no
         # end-to-end gain (worker process: 33.7 vs 35.5 ms median), so off
         self.handoff_s = tracker.conf.get_float("hbmr.gpu.first.chunk.handoff.ms", 0.0) / 1e3
+        # > 0: a slot's completer polls its batch's end event at this period
+        # instead of blocking in hipEventSynchronize, which (traced on the box)
+        # held up other threads' operations on the same stream — an early
+        # reduce's wait on the batch, the launcher's next batch — until the
+        # batch finished
+        self.poll_s = tracker.conf.get_float("hbmr.gpu.completion.poll.us", 100.0) / 1e6
         self._stop = threading.Event()
         reserve = tracker.conf.get_float("hbmr.gpu.hbm.reserve.gb", 16.0) * (1 << 30)
         for d, dev in self.devices.items():
@@ -377,14 +383,23 @@ class GpuRuntime:
                 else:
                     outs = [sj.map_gpu(c, d) for c, d in zip(ctxs, datas)]
                 ev1.record(slot.stream)
+                # the marker an early reduce orders itself behind: an event of
+                # its own, because HIP serialises operations on one event — a
+                # stream wait on ev1 blocked the reduce thread on the host for
+                # as long as the completer sat in ev1.synchronize() (traced on
+                # the box: the combine was enqueued only after the last map
+                # finished, ~1.5 ms of idle before each update and again
+                # before the next job's first assign)
+                evr = torch.cuda.Event()
+                evr.record(slot.stream)
             slot.inflight += len(live)
             if TRACE.on:
                 TRACE.instant("gpu.launch", n=len(live), slot=slot.index)
             # an early collective reduce may consume the outputs now, ordered
-            # behind ev1 on its own stream
+            # behind evr on its own stream
             by_job: dict = {}
             for r, out in zip(live, outs):
-                by_job.setdefault(id(r.job), (r.job, []))[1].append((r.spec.attempt_id, out, ev1))
+                by_job.setdefault(id(r.job), (r.job, []))[1].append((r.spec.attempt_id, out, evr))
             for js, items in by_job.values():
                 js.note_launched(items)
             slot.done_q.put((live, ev0, ev1, outs, capped))
@@ -429,7 +444,11 @@ class GpuRuntime:
                 break
             runs, ev0, ev1, outs, capped = item
             try:
-                ev1.synchronize()
+                if self.poll_s > 0:
+                    while not ev1.query():
+                        time.sleep(self.poll_s)
+                else:
+                    ev1.synchronize()
                 if TRACE.on:
                     TRACE.instant("gpu.complete", n=len(runs), slot=slot.index)
                 # a batch completes together; the busy time it adds to the

@@ -173,6 +173,8 @@ def run_split_reduce(host, run, device=None):
             outs, marks = _gather_outputs(js, spec, run)
         except RuntimeError as e:
             raise RuntimeError(f"{e} on {host.name}") from None
+        if TRACE.on:
+            TRACE.instant("tt.reduce.gathered", attempt=spec.attempt_id, n=len(outs))
         cuda = device is not None and device.type == "cuda"
         rt = getattr(host, "gpu_runtime", None)
         released = [False]
@@ -209,6 +211,8 @@ def run_split_reduce(host, run, device=None):
                 else:
                     for ev in {id(m): m for m in marks if m is not None}.values():
                         cur.wait_event(ev)
+                    if TRACE.on:
+                        TRACE.instant("tt.reduce.waited", attempt=spec.attempt_id)
                 combined = js.split_job.combine(ctx, outs)
                 if TRACE.on:
                     TRACE.instant("tt.reduce.combined", attempt=spec.attempt_id)

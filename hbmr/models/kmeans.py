@@ -719,6 +719,9 @@ class KMeansSplitJob(SplitJob):
                 if s.is_cuda:
                     s.record_stream(cur)
                     c.record_stream(cur)
+        from ..utils.trace import TRACE
+        if TRACE.on:
+            TRACE.instant("kmeans.combine.recorded", n=len(outputs))
         same = [(s, c) for s, c in outputs if s.device == dev and s.shape[1] == dp]
         other = [(s, c) for s, c in outputs if not (s.device == dev and s.shape[1] == dp)]
         if same:

@@ -185,8 +185,10 @@ TRACE = Tracer()
 
 _env = os.environ.get("HBMR_TRACE", "")
 if _env and _env != "0":
-    # "{rank}" in the path keeps the dumps of a multi-process node apart
-    TRACE.enable(None if _env == "1" else _env.replace("{rank}", os.environ.get("RANK", "0")))
+    # "{rank}" / "{pid}" in the path keep the dumps of a multi-process node
+    # (ranks, GPU worker processes) apart
+    TRACE.enable(None if _env == "1" else _env.replace("{rank}", os.environ.get("RANK", "0"))
+                 .replace("{pid}", str(os.getpid())))
 
 
 def configure(conf):

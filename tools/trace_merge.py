@@ -17,7 +17,7 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--iters", type=int, default=2)
     ap.add_argument("--names", default="gpu.native,gpu.launch,gpu.complete,tt.reduce.start,"
-                    "tt.reduce.combined,tt.reduce.gate_open,gpu.wake,gpu.prep,kmeans.map_exact,kmeans.top3_launch,kmeans.refresh_launched,"
+                    "tt.reduce.gathered,tt.reduce.waited,kmeans.combine.recorded,tt.reduce.combined,tt.reduce.gate_open,gpu.wake,gpu.prep,kmeans.map_exact,kmeans.top3_launch,kmeans.refresh_launched,"
                     "kmeans.shift_synced,tt.reduce.done,jt.job_finished,tt.launch_batch,"
                     "jt.assigned,tt.finish,kmeans.reduce_return")
     a = ap.parse_args()
