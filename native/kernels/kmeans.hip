@@ -1342,52 +1342,90 @@ __global__ __launch_bounds__(256) void kmeans_slab_copy_kernel(const SlabTable s
 }
 
 constexpr long kDiffPts = 8192;  // points per diff workgroup
+constexpr int kDiffPer = (int)(kDiffPts / 256);  // points per thread
 
+// Every thread loads its 32 (label, reference label) pairs up front (strided
+// by the workgroup width, so each load instruction is coalesced) — the loads
+// are in flight together instead of one dependent round trip per 64 points —
+// then the workgroup reserves room for all of its movers with ONE atomic on
+// the split's mover count (a prefix sum over the threads' mover counts places
+// each thread's movers).  Mover order is irrelevant downstream: the scatter
+// sorts entries by cluster and the row sums are integer.
 __global__ __launch_bounds__(256) void kmeans_delta_diff_kernel(
     const SplitTable tbl, const GTable gt, const int32_t* __restrict__ labels,
     uint2* __restrict__ movers, uint32_t* __restrict__ mcount, uint32_t* __restrict__ hist,
     long long* __restrict__ counts) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_bins[];  // in[k] | out[k]
+  __shared__ uint32_t s_wsum[4];
+  __shared__ uint32_t s_first;
   const int k = tbl.k;
   const int s = __builtin_amdgcn_readfirstlane(find_split(tbl, blockIdx.x));
   const long local = blockIdx.x - tbl.blk[s];
   const long n = tbl.n[s];
-  for (int i = threadIdx.x; i < 2 * k; i += 256) s_bins[i] = 0u;
-  __syncthreads();
+  const int t = threadIdx.x;
+  for (int i = t; i < 2 * k; i += 256) s_bins[i] = 0u;
   const int32_t* lab = labels + tbl.off[s];
   int32_t* g = gt.g[s];
   uint2* mv = movers + tbl.off[s];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const unsigned long long lt = (1ull << lane) - 1ull;
+  const int lane = t & 63, wave = t >> 6;
+  const long p0 = local * kDiffPts + t;
   const long p1 = min(n, (local + 1) * kDiffPts);
-  for (long base = local * kDiffPts + wave * 64; base < p1; base += 256) {
-    const long p = base + lane;
-    int l = 0, o = 0;
-    bool ch = false;
-    if (p < p1) {
-      l = lab[p];
-      o = g[p];
-      // (a label outside [0, k) would index past the bins and the slabs:
-      // such a point is never a mover — the bit-exactness tests catch it)
-      ch = l != o && (unsigned)l < (unsigned)k && (unsigned)o < (unsigned)k;
-    }
-    const unsigned long long m = __ballot(ch);
-    if (m == 0) continue;
-    uint32_t first = 0;
-    if (lane == 0) first = atomicAdd(mcount + s, (uint32_t)__popcll(m));
-    first = __shfl(first, 0);
-    if (ch) {
-      const uint32_t i = first + (uint32_t)__popcll(m & lt);
-      mv[i] = make_uint2((uint32_t)p, ((uint32_t)l << 16) | (uint32_t)o);
-      g[p] = l;
-      atomicAdd(s_bins + l, 1u);
-      atomicAdd(s_bins + k + o, 1u);
+  int32_t l[kDiffPer], o[kDiffPer];
+  // branch-free: every load is issued (index clamped into the workgroup's
+  // range, which holds at least one point) and out-of-range pairs zeroed by a
+  // select, so all 64 loads of a thread are in flight together
+#pragma unroll
+  for (int j = 0; j < kDiffPer; ++j) {
+    const long p = p0 + (long)j * 256;
+    const bool in = p < p1;
+    const long pc = in ? p : p1 - 1;
+    const int32_t a = lab[pc], b = g[pc];
+    l[j] = in ? a : 0;
+    o[j] = in ? b : 0;
+  }
+  // (a label outside [0, k) would index past the bins and the slabs: such a
+  // point is never a mover — the bit-exactness tests catch it)
+  uint32_t chm = 0u;
+  uint32_t pk[kDiffPer];  // new << 16 | old (k <= 8192)
+#pragma unroll
+  for (int j = 0; j < kDiffPer; ++j) {
+    const bool ch = l[j] != o[j] && (unsigned)l[j] < (unsigned)k && (unsigned)o[j] < (unsigned)k;
+    chm |= (uint32_t)ch << j;
+    pk[j] = ((uint32_t)l[j] << 16) | ((uint32_t)o[j] & 0xffffu);
+  }
+  const uint32_t cnt = (uint32_t)__popc(chm);
+  uint32_t x = cnt;  // inclusive prefix over the wave
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) s_wsum[wave] = x;
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t tot = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+    s_first = tot ? atomicAdd(mcount + s, tot) : 0u;
+  }
+  __syncthreads();
+  if (chm) {
+    uint32_t i = s_first + x - cnt;
+    for (int w = 0; w < wave; ++w) i += s_wsum[w];
+#pragma unroll
+    for (int j = 0; j < kDiffPer; ++j) {
+      if ((chm >> j) & 1u) {
+        const uint32_t p = (uint32_t)(p0 + (long)j * 256);
+        const uint32_t nl = pk[j] >> 16, ol = pk[j] & 0xffffu;
+        mv[i++] = make_uint2(p, pk[j]);
+        g[p] = (int32_t)nl;
+        atomicAdd(s_bins + nl, 1u);
+        atomicAdd(s_bins + k + ol, 1u);
+      }
     }
   }
   __syncthreads();
   uint32_t* hs = hist + (size_t)s * k;
   u64* cs = reinterpret_cast<u64*>(counts) + (size_t)s * k;
-  for (int c = threadIdx.x; c < k; c += 256) {
+  for (int c = t; c < k; c += 256) {
     const uint32_t in = s_bins[c], out = s_bins[k + c];
     if (in | out) {
       atomicAdd(hs + c, in + out);
