@@ -26,6 +26,7 @@
 #include "common.h"
 #include "../include/hbmr/hbmr.h"
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 
@@ -550,8 +551,18 @@ __device__ __forceinline__ void read_tile32(const char* buf, int col, int h, bf1
 
 struct NoFin {};   // assign_tile_v2's default finish (finish_point)
 
+// HBMR_EXACT_PIPE: the fused exact kernel overlaps each tile's arg-max
+// epilogue with the NEXT tile's MFMAs inside one wave (two accumulator sets,
+// scheduler-interleaved), at 2 waves per SIMD instead of 3.  PMC on the
+// non-pipelined kernel: MFMA pipes 51 % busy, 40 % of wave cycles stalled on
+// issue — the 16 MFMAs of a tile ran back to back and the ~100 epilogue VALU
+// ops after them, so only other waves could fill the MFMA gaps.
+#ifndef HBMR_EXACT_PIPE
+#define HBMR_EXACT_PIPE 0   // default of the runtime switch HBMR_EXACT_PIPE (env)
+#endif
+
 template <int D, int PB, bool EXACT = false, bool F16 = false, bool TOP3 = false,
-          class Fin = NoFin>
+          class Fin = NoFin, bool PIPE = false>
 __device__ __forceinline__ void assign_tile_v2(const __bf16* __restrict__ X, long n,
                                                const __bf16* __restrict__ C,
                                                const float* __restrict__ chalf, int ntiles,
@@ -606,6 +617,66 @@ __device__ __forceinline__ void assign_tile_v2(const __bf16* __restrict__ X, lon
 
   const bool w0 = wave == 0;
   int slot = 0;  // t % NS
+  if constexpr (PIPE) {
+    // MFMAs of tile t into `acc`, the epilogue of tile t-1 from `prev`
+    // (before tile 0: scores of -3e38, displaced by the real ones — every
+    // track sees >= 2 real scores per tile), interleaved by the scheduler
+    auto step = [&](int t, f32x16 (&acc)[PB], f32x16 (&prev)[PB])
+        __attribute__((always_inline)) {
+      wait_tile_dmas<V::P, V::NS - 2>(max(0, min(V::NS - 2, ntiles - 2 - t)), w0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t + V::NS < ntiles)
+        stage_tile32<D>(smem + slot * V::BUF, C, chalf, t + V::NS, wave, lane);
+      slot = slot + 1 == V::NS ? 0 : slot + 1;
+      const char* nbuf = smem + slot * V::BUF;
+      const char* nrow = nbuf + col * (D * 2);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+#pragma unroll
+        for (int pb = 0; pb < PB; ++pb)
+          acc[pb] = mfma32x32x16<F16>(a[s], bfrag[pb][s], s == 0 ? bias : acc[pb]);
+        a[s] = *reinterpret_cast<const bf16x8*>(nrow + (((2 * s + h) ^ aswz) << 4));
+      }
+      {
+        const float* ch = reinterpret_cast<const float*>(nbuf + V::TILE_BYTES);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(ch + 8 * g + 4 * h);
+          bias[4 * g + 0] = v[0];
+          bias[4 * g + 1] = v[1];
+          bias[4 * g + 2] = v[2];
+          bias[4 * g + 3] = v[3];
+        }
+      }
+#pragma unroll
+      for (int pb = 0; pb < PB; ++pb) am[pb].update(prev[pb], t - 1);
+#pragma unroll
+      for (int i = 0; i < KS * PB; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);   // then vector ALU
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // and an LDS read
+      }
+    };
+    f32x16 accA[PB], accB[PB];
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) accB[pb][r] = -3.0e38f;
+    int t = 0;
+    for (; t + 1 < ntiles; t += 2) {
+      step(t, accA, accB);
+      step(t + 1, accB, accA);
+    }
+    if (t < ntiles) {
+      step(t, accA, accB);
+#pragma unroll
+      for (int pb = 0; pb < PB; ++pb) am[pb].update(accA[pb], t);
+    } else if (ntiles > 0) {
+#pragma unroll
+      for (int pb = 0; pb < PB; ++pb) am[pb].update(accB[pb], ntiles - 1);
+    }
+  } else
   for (int t = 0; t < ntiles; ++t) {
     // tile t+1's DMA has landed for every wave (younger DMAs in flight: tiles
     // t+2 .. min(t+NS-1, ntiles-1)), and this wave's reads of tile t have
@@ -2689,8 +2760,8 @@ struct TopQ1Table {       // the batch's splits, by value (X, per-point norms)
   long blk[kMaxGroup + 1];
 };
 
-template <int D, bool F16>
-__global__ __launch_bounds__(AssignV2<D>::THREADS, HBMR_EXACT_MINB) void
+template <int D, bool F16, bool PIPE>
+__global__ __launch_bounds__(AssignV2<D>::THREADS, PIPE ? 2 : HBMR_EXACT_MINB) void
 kmeans_assign_top3_q1_grouped_kernel(const TopQ1Table tbl, const __bf16* __restrict__ C,
                                      const float* __restrict__ chalf, int ntiles,
                                      int32_t* __restrict__ labels, FusedQ1Fin fin) {
@@ -2707,7 +2778,8 @@ kmeans_assign_top3_q1_grouped_kernel(const TopQ1Table tbl, const __bf16* __restr
   fin.xbn2 = tbl.xbn2[s];
   fin.xerr = tbl.xerr[s];
   fin.sidx = s;
-  assign_tile_v2<D, 2, true, F16, false, FusedQ1Fin>(tbl.X[s], tbl.off[s + 1] - o, C, chalf,
+  assign_tile_v2<D, 2, true, F16, false, FusedQ1Fin, PIPE>(
+      tbl.X[s], tbl.off[s + 1] - o, C, chalf,
                                                      ntiles, labels + o, nullptr, b - tbl.blk[s],
                                                      smem, nullptr, nullptr, -1, &fin);
 }
@@ -3618,10 +3690,18 @@ int hbmr_kmeans_assign_top3_q1_grouped(int nsplit, const void* const* X, const l
   fin.cmax_p = cmax;
   fin.cerrmax_p = cerrmax;
   (void)inflate;
+  // the epilogue-pipelined kernel (HBMR_EXACT_PIPE, read once; env overrides
+  // the build default) or the 3-waves-per-SIMD one
+  static const bool pipe = [] {
+    const char* e = getenv("HBMR_EXACT_PIPE");
+    return e && *e ? atoi(e) != 0 : HBMR_EXACT_PIPE != 0;
+  }();
 #define HBMR_TOP3Q1(D)                                                                         \
   {                                                                                            \
-    auto kern = f16 ? kmeans_assign_top3_q1_grouped_kernel<D, true>                            \
-                    : kmeans_assign_top3_q1_grouped_kernel<D, false>;                          \
+    auto kern = pipe ? (f16 ? kmeans_assign_top3_q1_grouped_kernel<D, true, true>              \
+                            : kmeans_assign_top3_q1_grouped_kernel<D, false, true>)            \
+                     : (f16 ? kmeans_assign_top3_q1_grouped_kernel<D, true, false>             \
+                            : kmeans_assign_top3_q1_grouped_kernel<D, false, false>);          \
     hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(AssignV2<D>::THREADS),                   \
                        AssignV2<D>::LDS_BYTES, st, t, reinterpret_cast<const __bf16*>(C),      \
                        chalf, k_pad / 32, labels, fin);                                        \
