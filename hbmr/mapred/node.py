@@ -80,11 +80,13 @@ class Node:
                 worker_comm = {"host": os.environ.get("MASTER_ADDR", "127.0.0.1"),
                                "port": int(os.environ["MASTER_PORT"]), "rank": self.rank,
                                "world": self.world, "backend": dev_backend}
-        # several ranks: the JobTracker runs in a process of its own (not
-        # under rank 0's interpreter lock with its tracker and the driver);
-        # hbmr.jobtracker.process=false keeps it in rank 0
+        # 8+ ranks: the JobTracker runs in a process of its own (not under
+        # rank 0's interpreter lock with its tracker and the driver): the
+        # 16-CPU-host rehearsal measured 8.1 vs 9.0 ms per job at 8 ranks (rank
+        # 0's CPU 9.8 -> 1.6 ms per job) and no gain at 2-4 ranks
+        # (profiles/r04_final_b_terasort_rehearsal.json); the key overrides
         self.jt_process = self.rank == 0 and self.conf.get_boolean(
-            "hbmr.jobtracker.process", False)
+            "hbmr.jobtracker.process", self.world >= 8)
         if self.jt_process:
             from .jtprocess import RemoteJobTracker
             self.jt = RemoteJobTracker(self.conf)
