@@ -218,7 +218,7 @@ def maybe_profile_threads():
     orig = threading.Thread.run
 
     def run(self):
-        pr = cProfile.Profile()
+        pr = cProfile.Profile(time.thread_time)
         _PROFILES.append(pr)
         pr.enable()
         try:
@@ -226,7 +226,7 @@ def maybe_profile_threads():
         finally:
             pr.disable()
     threading.Thread.run = run
-    main = cProfile.Profile()
+    main = cProfile.Profile(time.thread_time)
     _PROFILES.append(main)
     main.enable()
     return path

@@ -4,6 +4,8 @@ time per split), the same pre-staged K-Means driver as bench.py.  Reports
 ms/job and, with --cprofile, the CPU per job by component (JobTracker +
 scheduler, TaskTracker, GPU runtime/split executor, model, RPC/other), which is
 what a JobTracker process of its own would have to sustain per job.
+The profiles measure per-thread CPU time (time.thread_time), so threads
+waiting for the interpreter lock or a Python lock are not charged.
 
 usage: python tools/jt_floor.py [--trackers 8] [--jobs 40] [--ms 0.01] [--cprofile]
 """
@@ -28,7 +30,7 @@ def _install_thread_profiler():
     orig = threading.Thread.run
 
     def run(self):
-        pr = cProfile.Profile()
+        pr = cProfile.Profile(time.thread_time)
         _PROFILES.append(pr)
         pr.enable()
         try:
@@ -36,7 +38,7 @@ def _install_thread_profiler():
         finally:
             pr.disable()
     threading.Thread.run = run
-    main_pr = cProfile.Profile()
+    main_pr = cProfile.Profile(time.thread_time)
     _PROFILES.append(main_pr)
     return main_pr
 
