@@ -360,4 +360,17 @@ def spawn_ranks(n):
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    rc = main()
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        # a rank leaves after its exit handlers (trace / profile dumps) without
+        # interpreter finalization: daemon threads still inside torch / gloo /
+        # RCCL C++ frames when the interpreter tears them down could abort the
+        # process ("terminate called without an active exception", seen on
+        # the box at 8 ranks with the stack sampler on) after the result line
+        # was printed, failing the run
+        import atexit
+        atexit._run_exitfuncs()
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(rc or 0)
+    sys.exit(rc)
