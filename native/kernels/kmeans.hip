@@ -469,9 +469,9 @@ __device__ __forceinline__ void assign_tile(const __bf16* __restrict__ X, long n
 //   MFMAs + arg-max epilogue of tile t.
 // A DMA thus has NS-1 tiles (≈(NS-1)·512 MFMA cycles) to land: with NS = 2 the
 // L2 latency under full-chip load was exposed every tile.
-template <int D> struct AssignV2 {
+template <int D, int NSV = 4> struct AssignV2 {
   static constexpr int KS = D / 16;
-  static constexpr int NS = 4;                           // ring depth
+  static constexpr int NS = NSV;                         // ring depth
   static constexpr int TILE_BYTES = 32 * D * 2;          // 32 clusters
   static constexpr int BUF = TILE_BYTES + 32 * 4;        // + -|c|²/2
   static constexpr int LDS_BYTES = NS * BUF;
@@ -562,7 +562,7 @@ struct NoFin {};   // assign_tile_v2's default finish (finish_point)
 #endif
 
 template <int D, int PB, bool EXACT = false, bool F16 = false, bool TOP3 = false,
-          class Fin = NoFin, bool PIPE = false>
+          class Fin = NoFin, bool PIPE = false, int NSV = 4>
 __device__ __forceinline__ void assign_tile_v2(const __bf16* __restrict__ X, long n,
                                                const __bf16* __restrict__ C,
                                                const float* __restrict__ chalf, int ntiles,
@@ -572,7 +572,7 @@ __device__ __forceinline__ void assign_tile_v2(const __bf16* __restrict__ X, lon
                                                float* __restrict__ margin = nullptr,
                                                long cs = -1, const Fin* fin = nullptr) {
   static_assert(D <= 128, "v2 keeps PB point blocks of D ≤ 128 in registers");
-  using V = AssignV2<D>;
+  using V = AssignV2<D, NSV>;
   constexpr int KS = V::KS;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid / HBMR_WAVE);
@@ -2760,7 +2760,7 @@ struct TopQ1Table {       // the batch's splits, by value (X, per-point norms)
   long blk[kMaxGroup + 1];
 };
 
-template <int D, bool F16, bool PIPE>
+template <int D, bool F16, bool PIPE, int NSV = 4>
 __global__ __launch_bounds__(AssignV2<D>::THREADS, PIPE ? 2 : HBMR_EXACT_MINB) void
 kmeans_assign_top3_q1_grouped_kernel(const TopQ1Table tbl, const __bf16* __restrict__ C,
                                      const float* __restrict__ chalf, int ntiles,
@@ -2778,7 +2778,7 @@ kmeans_assign_top3_q1_grouped_kernel(const TopQ1Table tbl, const __bf16* __restr
   fin.xbn2 = tbl.xbn2[s];
   fin.xerr = tbl.xerr[s];
   fin.sidx = s;
-  assign_tile_v2<D, 2, true, F16, false, FusedQ1Fin, PIPE>(
+  assign_tile_v2<D, 2, true, F16, false, FusedQ1Fin, PIPE, NSV>(
       tbl.X[s], tbl.off[s + 1] - o, C, chalf,
                                                      ntiles, labels + o, nullptr, b - tbl.blk[s],
                                                      smem, nullptr, nullptr, -1, &fin);
@@ -3696,14 +3696,23 @@ int hbmr_kmeans_assign_top3_q1_grouped(int nsplit, const void* const* X, const l
     const char* e = getenv("HBMR_EXACT_PIPE");
     return e && *e ? atoi(e) != 0 : HBMR_EXACT_PIPE != 0;
   }();
+  // centroid-tile ring depth of the fused kernel: 4, or 6 (HBMR_EXACT_NS=6:
+  // two more tiles of DMA lead, 50 KB of LDS per workgroup)
+  static const bool ns6 = [] {
+    const char* e = getenv("HBMR_EXACT_NS");
+    return e && atoi(e) == 6;
+  }();
 #define HBMR_TOP3Q1(D)                                                                         \
   {                                                                                            \
     auto kern = pipe ? (f16 ? kmeans_assign_top3_q1_grouped_kernel<D, true, true>              \
                             : kmeans_assign_top3_q1_grouped_kernel<D, false, true>)            \
+              : ns6  ? (f16 ? kmeans_assign_top3_q1_grouped_kernel<D, true, false, 6>          \
+                            : kmeans_assign_top3_q1_grouped_kernel<D, false, false, 6>)        \
                      : (f16 ? kmeans_assign_top3_q1_grouped_kernel<D, true, false>             \
                             : kmeans_assign_top3_q1_grouped_kernel<D, false, false>);          \
+    const size_t lds = ns6 && !pipe ? AssignV2<D, 6>::LDS_BYTES : AssignV2<D>::LDS_BYTES;      \
     hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(AssignV2<D>::THREADS),                   \
-                       AssignV2<D>::LDS_BYTES, st, t, reinterpret_cast<const __bf16*>(C),      \
+                       lds, st, t, reinterpret_cast<const __bf16*>(C),                         \
                        chalf, k_pad / 32, labels, fin);                                        \
     return (int)hipGetLastError();                                                             \
   }
