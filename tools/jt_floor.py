@@ -68,6 +68,7 @@ def main():
     ap.add_argument("--cprofile", action="store_true")
     ap.add_argument("--filter", default="", help="regex: print only matching functions")
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--sort", default="tottime")
     a = ap.parse_args()
     main_pr = _install_thread_profiler() if a.cprofile else None
     conf = JobConf()
@@ -124,7 +125,7 @@ def main():
               f"{1e3 * idle / a.jobs:.2f} ms/job are in python/libs):")
         for k, v in by.most_common():
             print(f"  {k:14s} {1e3 * v / a.jobs:8.2f}")
-        st.sort_stats("tottime").print_stats(*([a.filter] if a.filter else []), a.top)
+        st.sort_stats(a.sort).print_stats(*([a.filter] if a.filter else []), a.top)
 
 
 if __name__ == "__main__":
