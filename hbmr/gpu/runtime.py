@@ -117,6 +117,14 @@ class GpuRuntime:
         # device sooner (each costs ~10-20 µs of host work per task to prepare),
         # larger ones amortise the per-launch kernels
         self.batch_target = max(1, tracker.conf.get_int("hbmr.gpu.batch.target", 16))
+        # a job whose maps were not pre-staged (nothing to wait for: the
+        # device idles until they are launched) goes out in larger batches
+        # after its first chunk, so the launcher's ~1 ms of host work per batch
+        # stays ahead of the device (traced: a 16-task batch takes the launcher
+        # about as long as the device, and the first job of a chain ran ~30 %
+        # slower than the pre-staged ones behind it)
+        self.batch_target_unstaged = max(1, tracker.conf.get_int(
+            "hbmr.gpu.batch.target.unstaged", 32))
         # a job's last batches halve in size (see _chunks)
         self.taper = tracker.conf.get_boolean("hbmr.gpu.batch.taper", True)
         # > 0: the submitter of an idle device's first chunk waits (up to this
@@ -273,7 +281,9 @@ class GpuRuntime:
                 # split the rest of the job's batch over the slots so streams overlap
                 rest = len(runs) - i
                 nslot = len(dev.slots) if hasattr(sj, "map_gpu_batch") else rest
-                per = min(self.max_batch, self.batch_target, max(1, -(-rest // max(1, nslot))))
+                target = self.batch_target if any(r.wait is not None for r in runs) \
+                    else self.batch_target_unstaged
+                per = min(self.max_batch, target, max(1, -(-rest // max(1, nslot))))
                 if rest <= self.first_chunk and hasattr(sj, "map_gpu_batch"):
                     per = max(1, rest)       # a first chunk: one launch, no split
                 cap = int(getattr(sj, "max_inflight_maps", 0) or 0)
