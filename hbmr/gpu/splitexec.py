@@ -14,6 +14,7 @@ trackers' combined map outputs.
 """
 from __future__ import annotations
 
+import itertools
 import time
 import traceback
 
@@ -117,12 +118,27 @@ def _gather_outputs(js, spec, run):
     return outs, marks
 
 
+_REDUCE_STREAMS = 4
+
+
 def _reduce_stream(host, device):
+    """A stream for one reduce attempt, round robin over a small pool: the
+    early reduces of consecutive jobs must not share one.  With a single
+    shared stream, job J+1's combine (enqueued as soon as J+1's maps were
+    launched, waiting on them on the device) sat in front of job J's
+    centroid read-back (the saved version, the returned centroids), so J's
+    reduce finished a whole iteration late (traced on the box: 29 ms between
+    J's shift sync and its completion, and jobs completing in pairs).  Order
+    across jobs needs no shared stream: J+1's maps wait on J's gate event,
+    and J+1's reduce waits on those maps."""
     import torch
-    st = host.__dict__.get("_reduce_stream")
-    if st is None:
-        st = host.__dict__.setdefault("_reduce_stream", torch.cuda.Stream(device=device))
-    return st
+    d = host.__dict__
+    pool = d.get("_reduce_streams")
+    if pool is None:
+        pool = d.setdefault("_reduce_streams",
+                            [torch.cuda.Stream(device=device) for _ in range(_REDUCE_STREAMS)])
+        d.setdefault("_reduce_rr", itertools.count())
+    return pool[next(d["_reduce_rr"]) % len(pool)]
 
 
 def run_split_reduce(host, run, device=None):

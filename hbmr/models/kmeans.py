@@ -169,6 +169,9 @@ class CentroidStore:
                 return c
             for (k, _dev), img in self.images.items():
                 if k == key:
+                    ready = getattr(img, "ready", None)
+                    if ready is not None:
+                        ready.synchronize()     # built on a reduce's own stream
                     c = img.cen.detach().to("cpu")
                     self.host[key] = c
                     return c
@@ -184,6 +187,9 @@ class CentroidStore:
         if cen is None:
             raise KeyError(f"centroids {key!r} not resident on this tracker")
         img = km.CentroidImage(cen, device)
+        # built on the caller's stream: consumers on other streams wait on it
+        img.ready = torch.cuda.Event()
+        img.ready.record()
         self.put_image(key, device, img)
         return img
 
@@ -573,7 +579,11 @@ class KMeansSplitJob(SplitJob):
         from ..ops import kmeans as km
         ctx = ctxs[0]
         img = STORE.image(self.cin, ctx.device)
-        # the image may live on the reduce's stream (pipelined iterations)
+        # the image may live on a reduce's stream (pipelined iterations) or on
+        # another slot's stream (built from host centroids by its first batch)
+        ready = getattr(img, "ready", None)
+        if ready is not None:
+            torch.cuda.current_stream().wait_event(ready)
         for t in (img.cbf, img.chalf):
             t.record_stream(torch.cuda.current_stream())
         B = len(datas)
@@ -761,6 +771,12 @@ class KMeansSplitJob(SplitJob):
             raise RuntimeError("reduce killed (collective restart): result not published")
         if sums.device.type == "cuda":
             old = STORE.image(self.cin, sums.device)
+            # the previous job's reduce built it on a stream of its own
+            # (splitexec._reduce_stream): order the read behind it even where
+            # no local map output (which waited on that job's gate) orders it
+            ready = getattr(old, "ready", None)
+            if ready is not None:
+                torch.cuda.current_stream().wait_event(ready)
             img = km.CentroidImage.__new__(km.CentroidImage)
             img.__dict__.update(old.__dict__)
             img.cen = old.cen.clone()
@@ -774,6 +790,8 @@ class KMeansSplitJob(SplitJob):
                 # built here, behind the update, so the gate's event covers them
                 img.image16(self.exact_dtype)
                 img.neighbors()
+            img.ready = torch.cuda.Event()
+            img.ready.record()
             if TRACE.on:
                 TRACE.instant("kmeans.refresh_launched")
             STORE.put_image(self.cout, sums.device, img)
