@@ -14,7 +14,6 @@ trackers' combined map outputs.
 """
 from __future__ import annotations
 
-import itertools
 import time
 import traceback
 
@@ -118,27 +117,19 @@ def _gather_outputs(js, spec, run):
     return outs, marks
 
 
-_REDUCE_STREAMS = 4
-
-
 def _reduce_stream(host, device):
-    """A stream for one reduce attempt, round robin over a small pool: the
-    early reduces of consecutive jobs must not share one.  With a single
-    shared stream, job J+1's combine (enqueued as soon as J+1's maps were
-    launched, waiting on them on the device) sat in front of job J's
-    centroid read-back (the saved version, the returned centroids), so J's
-    reduce finished a whole iteration late (traced on the box: 29 ms between
-    J's shift sync and its completion, and jobs completing in pairs).  Order
-    across jobs needs no shared stream: J+1's maps wait on J's gate event,
-    and J+1's reduce waits on those maps."""
+    """The tracker's reduce stream, shared by its reduce attempts.  (A pool of
+    streams, one per attempt, measured worse: with 4 hardware queues per
+    process the streams share queues, and an early reduce's wait on maps not
+    yet finished blocks whatever follows it in its queue — consecutive jobs
+    then completed in threes instead of pairs.  What must not queue behind a
+    later job's waits is enqueued before them instead: see the KMeans reduce's
+    centroid read-back.)"""
     import torch
-    d = host.__dict__
-    pool = d.get("_reduce_streams")
-    if pool is None:
-        pool = d.setdefault("_reduce_streams",
-                            [torch.cuda.Stream(device=device) for _ in range(_REDUCE_STREAMS)])
-        d.setdefault("_reduce_rr", itertools.count())
-    return pool[next(d["_reduce_rr"]) % len(pool)]
+    st = host.__dict__.get("_reduce_stream")
+    if st is None:
+        st = host.__dict__.setdefault("_reduce_stream", torch.cuda.Stream(device=device))
+    return st
 
 
 def run_split_reduce(host, run, device=None):

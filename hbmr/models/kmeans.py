@@ -792,6 +792,18 @@ class KMeansSplitJob(SplitJob):
                 img.neighbors()
             img.ready = torch.cuda.Event()
             img.ready.record()
+            # the host copy of the new centroids (rank 0's saved version, the
+            # returned centroids) is enqueued now, right behind the update: on
+            # the tracker's shared reduce stream a later read-back would queue
+            # behind the next job's combine, which waits for that job's maps —
+            # this job then finished a whole iteration late
+            host_cen = cen_ev = None
+            if ctx.rank == 0 and (self.cdir or self.conf.get_boolean(RETURN_KEY, False)):
+                host_cen = torch.empty(tuple(img.cen.shape), dtype=torch.float32,
+                                       pin_memory=True)
+                host_cen.copy_(img.cen, non_blocking=True)
+                cen_ev = torch.cuda.Event()
+                cen_ev.record()
             if TRACE.on:
                 TRACE.instant("kmeans.refresh_launched")
             STORE.put_image(self.cout, sums.device, img)
@@ -815,6 +827,7 @@ class KMeansSplitJob(SplitJob):
                 TRACE.instant("kmeans.shift_synced")
             new_cen = None
         else:
+            host_cen = cen_ev = None
             old = STORE.host_centroids(self.cin)
             if sim is not None:
                 # no-data rehearsal: every partial is zero, the centroids stay
@@ -841,13 +854,15 @@ class KMeansSplitJob(SplitJob):
         if TRACE.on:
             TRACE.instant("kmeans.output_written")
         res = {"shift": shift, "points": int(npts), "centroids_key": self.cout}
+        if host_cen is not None:
+            cen_ev.synchronize()
         if ctx.rank == 0 and self.cdir:
-            cen = new_cen if new_cen is not None else STORE.image(self.cout, sums.device).cen
+            cen = new_cen if new_cen is not None else host_cen
             _save_centroids(self.cdir, self.cout, cen[:, :self.d])
         if ctx.rank == 0 and self.conf.get_boolean(RETURN_KEY, False):
             # the new centroids travel back with the result (the client may live
             # in another process than the reduce, e.g. with GPU worker processes)
-            cen = new_cen if new_cen is not None else STORE.image(self.cout, sums.device).cen
+            cen = new_cen if new_cen is not None else host_cen
             res["centroids"] = encode_centroids(cen[:, :self.d])
         if TRACE.on:
             TRACE.instant("kmeans.reduce_return")
