@@ -95,6 +95,14 @@ class RemoteGpuRuntime:
             env["HBMR_TRACE"] = env["HBMR_TRACE"].replace("{rank}", "{rank}_worker")
         env["PYTHONPATH"] = _ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH")
                                      else "")
+        hwq = tr.conf.get_int("hbmr.gpu.hw.queues", 8 if tr.world_size > 1 else 0)
+        if hwq > 0 and "GPU_MAX_HW_QUEUES" not in os.environ:
+            # a stream per hardware queue: HIP maps streams onto 4 queues by
+            # default, and a queue shared by two streams blocks one behind the
+            # other's waits on unfinished work (measured: a pool of reduce
+            # streams made jobs complete in threes).  One rank uses 4 streams
+            # (default, two slots, reduce); several ranks add RCCL's stream
+            env["GPU_MAX_HW_QUEUES"] = str(min(hwq, 32))
         self.proc = subprocess.Popen([sys.executable, "-m", "hbmr.gpu.worker",
                                       str(child.fileno())], pass_fds=(child.fileno(),),
                                      env=env, cwd=_ROOT)
