@@ -187,9 +187,10 @@ class CentroidStore:
         if cen is None:
             raise KeyError(f"centroids {key!r} not resident on this tracker")
         img = km.CentroidImage(cen, device)
-        # built on the caller's stream: consumers on other streams wait on it
-        img.ready = torch.cuda.Event()
-        img.ready.record()
+        if img.cen.is_cuda:
+            # built on the caller's stream: consumers on other streams wait on it
+            img.ready = torch.cuda.Event()
+            img.ready.record()
         self.put_image(key, device, img)
         return img
 
