@@ -281,8 +281,7 @@ class GpuRuntime:
                 # split the rest of the job's batch over the slots so streams overlap
                 rest = len(runs) - i
                 nslot = len(dev.slots) if hasattr(sj, "map_gpu_batch") else rest
-                target = self.batch_target if any(r.wait is not None for r in runs) \
-                    else self.batch_target_unstaged
+                target = self._batch_target(runs, self.batch_target, self.batch_target_unstaged)
                 per = min(self.max_batch, target, max(1, -(-rest // max(1, nslot))))
                 if rest <= self.first_chunk and hasattr(sj, "map_gpu_batch"):
                     per = max(1, rest)       # a first chunk: one launch, no split
@@ -306,6 +305,14 @@ class GpuRuntime:
                         self._release_capped(dev, len(chunk) - n)
             for ev in picked:
                 ev.set()
+
+    @staticmethod
+    def _batch_target(runs, staged, unstaged):
+        """Tasks per launch: pre-staged maps (released behind a gate event)
+        are launched while the job before them runs, so small batches reach
+        the device early; a job with nothing to wait for is on the critical
+        path of an idle device, where larger batches keep the launcher ahead."""
+        return staged if any(r.wait is not None for r in runs) else unstaged
 
     @staticmethod
     def _chunks(i, n, per, taper):
