@@ -18,6 +18,7 @@ Differences by design (SURVEY.md §2.1 bugs B1-B13):
 """
 from __future__ import annotations
 
+import collections
 import itertools
 import json
 import logging
@@ -74,6 +75,10 @@ class TrackerInfo:
         # responses carrying actions are numbered (under the JobTracker lock):
         # the tracker applies them in this order whichever thread receives them
         self.resp_seq = 0
+        # the last numbered responses (seq, actions): resent when a tracker
+        # lost a reply (JobTracker.resend; the reference resends its last
+        # heartbeat response by responseId, JobTracker.java:3308-3437)
+        self.sent: collections.deque = collections.deque(maxlen=32)
         self.rack = DEFAULT_RACK
         self.kills: set[str] = set()   # attempts to kill on the next heartbeat
         self.kill_epoch = -1           # JobTracker.kill_epoch this tracker was last scanned at
@@ -206,6 +211,8 @@ class JobInProgress:
         self.running_gpu = 0
         self.pending_counters: list = []
         self._loc_index: dict = {}
+        self._front: dict = {}          # re-queued TIPs (add_pending front) -> order key
+        self._front_seq = 0
         self.finished_cpu_maps = 0
         self.finished_gpu_maps = 0
         self.completion_events: list = []     # (map TaskID, attempt id, output)
@@ -370,8 +377,12 @@ class JobInProgress:
                     if tip in pend and tip not in seen:
                         lv2.append(tip)
                         seen.add(tip)
-            # stacks popped from the end: pending (FIFO = map index) order
-            order = lambda lv: sorted(lv, key=lambda t: t.partition, reverse=True)  # noqa: E731
+            # stacks popped from the end, in pending order: re-queued TIPs
+            # (failed / lost outputs, add_pending(front=True)) first, newest
+            # first, then map index order (findNewMapTask takes failed maps first)
+            front = self._front
+            order = lambda lv: sorted(lv, key=lambda t: front.get(t, t.partition),  # noqa: E731
+                                      reverse=True)
             idx = [order(lv0), order(lv1), order(lv2), None, len(tracker.cached), seen]
             self._loc_index[key] = idx
         return idx
@@ -457,12 +468,16 @@ class JobInProgress:
 
     def _take(self, tip):
         del self.pending_maps[tip]
+        if self._front:
+            self._front.pop(tip, None)
 
     def add_pending(self, tip, front=False):
         if tip in self.pending_maps:
             return
         if front:
             self.pending_maps = {tip: None, **self.pending_maps}
+            self._front_seq -= 1
+            self._front[tip] = self._front_seq      # (negative: before every index)
         else:
             self.pending_maps[tip] = None
         self._loc_index.clear()
@@ -1009,7 +1024,7 @@ class JobTracker:
         if assign:
             resp = self._heartbeat(status, False, True)
             return {"actions": resp["actions"], "seq": resp.get("seq")}
-        resp = self._heartbeat(status, False, False)
+        resp = self._heartbeat(status, False, False, number=False)
         if resp["actions"]:
             with self.lock:
                 tr.extra_actions += resp["actions"]
@@ -1081,11 +1096,30 @@ class JobTracker:
                     if TRACE.on:
                         TRACE.instant("jt.assigned", n=len(resp["actions"]))
                 if resp["actions"]:
-                    tr.resp_seq += 1
-                    resp["seq"] = tr.resp_seq
+                    self._number(tr, resp)
         tr.wake = False
         resp["more"] = tr.more
         return self._with_lazy(tr, resp)
+
+    @staticmethod
+    def _number(tr, resp):
+        """Give a response that goes back to its tracker the next sequence
+        number (the order its actions were produced in; callers hold the lock)
+        and keep it for a resend."""
+        tr.resp_seq += 1
+        resp["seq"] = tr.resp_seq
+        tr.sent.append((tr.resp_seq, list(resp["actions"])))
+
+    def resend(self, tracker_name, after_seq):
+        """The numbered responses after ``after_seq`` that this JobTracker
+        still holds — a tracker whose report reply was lost (the RPC failed
+        after the JobTracker processed it) takes back the launches, commit
+        approvals and kills it carried; the tracker skips any it applied."""
+        tr = self.trackers.get(tracker_name)
+        if tr is None:
+            return {"responses": []}
+        with self.lock:
+            return {"responses": [[q, acts] for q, acts in tr.sent if q > after_seq]}
 
     def _with_lazy(self, tr, resp):
         if tr is not None and tr.lazy_actions:
@@ -1093,11 +1127,16 @@ class JobTracker:
                 resp["actions"] += tr.lazy_actions
                 tr.lazy_actions = []
                 if "seq" not in resp:
-                    tr.resp_seq += 1
-                    resp["seq"] = tr.resp_seq
+                    self._number(tr, resp)
+                else:
+                    for i, (q, _a) in enumerate(tr.sent):
+                        if q == resp["seq"]:
+                            tr.sent[i] = (q, list(resp["actions"]))
         return resp
 
-    def _heartbeat(self, status, initial, accept_new_tasks):
+    def _heartbeat(self, status, initial, accept_new_tasks, number=True):
+        # number=False: the caller re-queues the actions (report without
+        # assignment) and they are numbered where they are finally returned
         st = P.TaskTrackerStatus.from_dict(status) if isinstance(status, dict) else status
         now = time.time()
         actions = []
@@ -1162,11 +1201,10 @@ class JobTracker:
                                            if x["type"] != "close_gate"]
                 tr.extra_actions = []
             resp = {"actions": actions, "interval": self.heartbeat_interval, "more": tr.more}
-            if actions:
+            if actions and number:
                 # numbered under the lock that drained the tracker's queues:
                 # the numbering is the order the actions were produced in
-                tr.resp_seq += 1
-                resp["seq"] = tr.resp_seq
+                self._number(tr, resp)
         return resp
 
     def _update_task_status(self, tr: TrackerInfo, ts: P.TaskStatus, actions):
@@ -1439,10 +1477,13 @@ class JobTracker:
         self._update_progress(jip)
         jid = str(jip.job_id)
         staged = [w for w in self.staged if w.staged_on == jid and not w.completed()]
-        if staged or kill_maps:
-            for t in self.trackers.values():
-                if t.status.gpus:
-                    t.extra_actions.append(P.close_gate_action(jid))
+        # always: a failed member of the gang may already have opened this job's
+        # gate on the trackers (release_dependents runs before its failure), and
+        # a job staged on this one AFTER the restart would otherwise launch its
+        # maps through that stale open gate onto the failed attempt's result
+        for t in self.trackers.values():
+            if t.status.gpus:
+                t.extra_actions.append(P.close_gate_action(jid))
         for w in staged:
             self.history.log("STAGED_JOB_RESTART", job=str(w.job_id), gate=jid)
             self._restart_collective(w, f"job {jid} it is staged on restarted", kill_maps=True)

@@ -228,7 +228,7 @@ class RpcClient:
             self._tl.sock = None
 
 
-JT_METHODS = ("heartbeat", "wakeup", "report", "map_completion_events", "rpc_submit_job",
+JT_METHODS = ("heartbeat", "wakeup", "report", "resend", "map_completion_events", "rpc_submit_job",
               "rpc_job_status", "rpc_kill_job", "rpc_job_result", "rpc_cluster_status",
               "rpc_list_jobs", "rpc_task_reports", "rpc_wait_job", "rpc_job_info")
 # served by a JobTracker process to the node that started it (hbmr/mapred/jtprocess.py)
@@ -250,6 +250,9 @@ class JobTrackerProxy:
 
     def wakeup(self, tracker_name, seq=None):
         return self.rpc.call("wakeup", tracker_name, seq)
+
+    def resend(self, tracker_name, after_seq):
+        return self.rpc.call("resend", tracker_name, after_seq)
 
     def report(self, status, assign=False):
         return self.rpc.call("report", status, assign)

@@ -150,6 +150,7 @@ class TaskTracker:
         self._act_lock = threading.RLock()   # JobTracker actions, applied one at a time
         self._resp_cond = threading.Condition()
         self._next_seq = 1                   # JobTracker response order (resp["seq"])
+        self._skipped: set = set()           # numbers passed over by a timed-out wait
         self._deferred: dict = {}            # job id -> launches that came before its conf
         self._early_kills: dict = {}         # attempts killed before their launch arrived
         # JobTracker.report assigns and returns actions (no long-poll wake-up)
@@ -502,7 +503,8 @@ class TaskTracker:
                     self._apply(r or {})
                     return
             except Exception:  # noqa: BLE001
-                pass
+                # the JobTracker may have processed it: take back its reply
+                self._recover_lost_reply()
             self._requeue(st)      # not delivered: the heartbeat thread sends it
         try:
             self.jt.wakeup(self.name, seq)
@@ -574,6 +576,7 @@ class TaskTracker:
                 if initial_sent:
                     with self._resp_cond:
                         self._next_seq = 1       # a (re-)registered tracker: new numbering
+                        self._skipped.clear()
                         self._resp_cond.notify_all()
                 self._apply(resp)
                 if self._reinit:
@@ -628,12 +631,39 @@ class TaskTracker:
             deadline = time.time() + 2.0
             while seq > self._next_seq and time.time() < deadline:
                 self._resp_cond.wait(deadline - time.time())
+            if seq < self._next_seq and seq not in self._skipped:
+                return                       # applied already (a resent response)
             try:
                 for act in acts:
                     self._handle(act)
             finally:
-                self._next_seq = max(self._next_seq, seq + 1)
+                if seq in self._skipped:
+                    self._skipped.discard(seq)           # a late one a wait gave up on
+                else:
+                    # (seq > _next_seq: the 2 s wait timed out; the numbers
+                    # passed over may still arrive and are applied then)
+                    self._skipped.update(range(self._next_seq, seq))
+                    self._next_seq = seq + 1
+                while len(self._skipped) > 256:
+                    self._skipped.discard(min(self._skipped))
                 self._resp_cond.notify_all()
+
+    def _recover_lost_reply(self):
+        """A report whose reply was lost after the JobTracker processed it: take
+        back the numbered responses after the last one applied here (their
+        launches / approvals / kills would otherwise be lost, and a later
+        response would wait 2 s for the missing number)."""
+        fn = getattr(self.jt, "resend", None)
+        if fn is None:
+            return
+        with self._resp_cond:
+            after = self._next_seq - 1
+        try:
+            r = fn(self.name, after)
+        except Exception:  # noqa: BLE001
+            return
+        for q, acts in (r or {}).get("responses", ()):
+            self._apply({"seq": q, "actions": acts})
 
     def _handle(self, act):
         """Apply one JobTracker action.  Actions arrive from the heartbeat

@@ -923,12 +923,16 @@ def make_iteration_conf(base, k, d, inp, split_points, cin, cout, init=None,
     return job
 
 
-def initial_centroids(inp, k, d, centers=None):
-    """First k points of the input (deterministic)."""
+def initial_centroids(inp, k, d, centers=None, exact=False):
+    """First k points of the input (deterministic).  The bf16 mode starts from
+    their bf16 roundings (the values its image holds); exact mode
+    (``hbmr.kmeans.exact``) from the fp32 points themselves."""
+    def rnd(x):
+        return x if exact else x.to(torch.bfloat16).to(torch.float32)
     if inp.startswith("synthetic:"):
         _, _n, seed = inp.split(":")
         x = synthetic_points(int(seed), 0, k, d, centers or k, "cpu")
-        return x.to(torch.bfloat16).to(torch.float32)
+        return rnd(x)
     from ..io import sequencefile as seqf
     import os
     path = inp
@@ -941,7 +945,7 @@ def initial_centroids(inp, k, d, centers=None):
             if raw is None:
                 break
             rows.append(np.frombuffer(raw[1][4:], dtype=">f4").astype(np.float32))
-    return torch.from_numpy(np.stack(rows)).to(torch.bfloat16).to(torch.float32)
+    return rnd(torch.from_numpy(np.stack(rows)))
 
 
 class KMeansDriver:
@@ -1018,7 +1022,9 @@ class KMeansDriver:
 
     def _job_conf(self, i, depends_on=None):
         centers = self.base.get_int(NCENTERS_KEY, self.k) if self.base is not None else None
-        init = initial_centroids(self.inp, self.k, self.d, centers) if i == 0 else None
+        exact = self.base.get_boolean(EXACT_KEY, False) if self.base is not None else False
+        init = initial_centroids(self.inp, self.k, self.d, centers, exact=exact) if i == 0 \
+            else None
         if init is not None:
             STORE.put_host(self.key(0), init)
         job = make_iteration_conf(self.base, self.k, self.d, self.inp, self.split_points,

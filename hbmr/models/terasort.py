@@ -193,6 +193,14 @@ class TeraSortSplitJob(SplitJob):
         return np.concatenate(keys)
 
     def get_splits(self, conf, trackers):
+        if self.spill and len(trackers) > 1 and self.needs_reduce:
+            # rejected at job setup, before any map runs: the spill reduce
+            # merges every map's run on one rank, and the several-rank paths
+            # (shuffle waves, all-to-all-v) read device-resident map outputs
+            raise ValueError(
+                f"out-of-core TeraSort (spill mode: hbmr.terasort.spill, or input above "
+                f"hbmr.terasort.hbm.budget.gb) runs its reduce on one rank; this job "
+                f"would run on {len(trackers)} trackers")
         ranges = self._ranges()
         # default R: one per tracker, and at least one per ~2 GB of input so a
         # single GPU sorts the output a partition at a time

@@ -39,7 +39,7 @@ _SIGS = {
     "hbmr_kmeans_exact_prep": (c_int, [c_void_p, c_long, c_int, c_int, c_int, c_int, c_void_p,
                                        c_void_p, c_void_p, c_void_p, c_void_p]),
     "hbmr_kmeans_assign_top3_q1_grouped": (c_int, [c_int, c_void_p, c_void_p, c_int, c_int,
-                                                   c_void_p, c_void_p, c_int, c_void_p,
+                                                   c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                                    c_void_p, c_void_p, c_void_p, c_int, c_int,
                                                    c_void_p, c_void_p, c_void_p, c_void_p,
                                                    c_void_p, c_long, c_void_p, c_void_p]),
@@ -47,6 +47,8 @@ _SIGS = {
                                          c_void_p, c_void_p]),
     "hbmr_kmeans_image16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "hbmr_kmeans_image16_tiled": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "hbmr_kmeans_set_stamps": (c_int, [c_void_p]),
     "hbmr_kmeans_refine_f32": (c_int, [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,

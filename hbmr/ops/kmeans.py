@@ -117,11 +117,24 @@ class CentroidImage:
                     int(dtype == torch.float16), _ptr(c16), _ptr(ch), _ptr(cn), _ptr(ce),
                     _ptr(mx), _lib.stream_handle(None))
                 _lib.check(rc, "hbmr_kmeans_image16")
+                c16t = None
+                if self.dp in (64, 128):
+                    # the v3 fused assign's tiled copy (hbmr_kmeans_image16_tiled)
+                    c16t = torch.empty_like(c16)
+                    rc = _lib.load().hbmr_kmeans_image16_tiled(
+                        _ptr(c16), self.k_pad, self.dp, _ptr(c16t), _lib.stream_handle(None))
+                    _lib.check(rc, "hbmr_kmeans_image16_tiled")
                 ev = torch.cuda.Event()
                 ev.record()
-                ent = cache[dtype] = (c16, ch, cn, mx[0:1], ce, mx[1:2], ev)
+                ent = cache[dtype] = (c16, ch, cn, mx[0:1], ce, mx[1:2], ev, c16t)
         torch.cuda.current_stream().wait_event(ent[6])
         return ent[:6]
+
+    def image16_tiled(self, dtype=torch.float16):
+        """The tiled copy of ``image16(dtype)[0]`` (32-row tiles, 16-byte pieces
+        piece-major) the v3 fused assign stages lane-linearly, or None (dp > 128)."""
+        self.image16(dtype)
+        return self._img16[dtype][7]
 
     def norms(self, dtype=torch.float16):
         """(|c_j| [k], max_j |c_j| [1], |c_j - c~_j| [k], max_j |c_j - c~_j| [1])
@@ -568,7 +581,8 @@ def _exact_group(group, img, stats, labels_ptr, c16, ch, norms, dt, scratch, str
             TRACE.instant("kmeans.top3_launch", n=B)
         cn, cmax, ce, cemax = norms
         rc = lib.hbmr_kmeans_assign_top3_q1_grouped(
-            B, xs, nsa, img.dp, int(dt == torch.float16), _ptr(c16), _ptr(ch), img.k_pad,
+            B, xs, nsa, img.dp, int(dt == torch.float16), _ptr(c16),
+            _ptr(img.image16_tiled(dt)), _ptr(ch), img.k_pad,
             labels_ptr, P(*[sp.xnorm.data_ptr() for sp in group]),
             P(*[sp.xbn2.data_ptr() for sp in group]), P(*[sp.xerr.data_ptr() for sp in group]),
             img.d, img.k, _ptr(cn), _ptr(cmax), _ptr(ce), _ptr(cemax), _ptr(rb.ws),

@@ -46,6 +46,9 @@ int hbmr_kmeans_centroid_nbr(const float* cen, int k, int d, int L, int32_t* di,
                              float* pd, hipStream_t st);
 int hbmr_kmeans_image16(const float* cen, int k, int d, int dp, int k_pad, int f16, void* c16,
                         float* chalf, float* cnorm, float* cerr, float* maxima, hipStream_t st);
+// tiled (piece-major per 32-row tile) copy of a 16-bit image for the v3 assign
+int hbmr_kmeans_image16_tiled(const void* c16, int k_pad, int dp, void* c16t, hipStream_t st);
+int hbmr_kmeans_set_stamps(void* p);
 int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float* xnorm,
                            const float* xbn2, const float* xerr, const float* C32, int k,
                            int k_pad, const float* cnorm, const float* cmax, const float* cerr,
@@ -54,7 +57,8 @@ int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float
                            const float* scores, const float* margin, unsigned long long* stats,
                            int nstats, hipStream_t st);
 int hbmr_kmeans_assign_top3_q1_grouped(int nsplit, const void* const* X, const long* n, int dp,
-                                       int f16, const void* C, const float* chalf, int k_pad,
+                                       int f16, const void* C, const void* Ct,
+                                       const float* chalf, int k_pad,
                                        int32_t* labels, const float* const* xnorm,
                                        const float* const* xbn2, const float* const* xerr,
                                        int d, int k, const float* cnorm, const float* cmax,

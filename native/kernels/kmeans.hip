@@ -560,6 +560,9 @@ struct NoFin {};   // assign_tile_v2's default finish (finish_point)
 #ifndef HBMR_EXACT_PIPE
 #define HBMR_EXACT_PIPE 0   // default of the runtime switch HBMR_EXACT_PIPE (env)
 #endif
+#ifndef HBMR_EXACT_V3_DEFAULT
+#define HBMR_EXACT_V3_DEFAULT 16   // fused exact kernel: -1 = v2, else a v3 mode (env HBMR_EXACT_V3)
+#endif
 
 template <int D, int PB, bool EXACT = false, bool F16 = false, bool TOP3 = false,
           class Fin = NoFin, bool PIPE = false, int NSV = 4>
@@ -2333,6 +2336,21 @@ __global__ __launch_bounds__(256) void kmeans_exact_prep_kernel(
   }
 }
 
+// Tiled copy of a 16-bit image [k_pad, dp] (dp = 64 / 128) for the v3 assign:
+// tile T (32 rows) holds its 16-byte pieces piece-major, (q, r) at
+// T * 32 * dp * 2 + q * 512 + r * 16 bytes (q = piece in the row, r = row).
+__global__ __launch_bounds__(256) void kmeans_image16_tiled_kernel(const uint4* __restrict__ c16,
+                                                                   int k_pad, int dp,
+                                                                   uint4* __restrict__ c16t) {
+  const long P = (long)blockIdx.x * 256 + threadIdx.x;
+  const int cpr = dp / 8;
+  if (P >= (long)k_pad * cpr) return;
+  const long T = P / (32 * cpr);
+  const int w = (int)(P % (32 * cpr));
+  const int q = w / 32, r = w % 32;
+  c16t[P] = c16[(T * 32 + r) * cpr + q];
+}
+
 // The 16-bit image of the fp32 centroids for exact mode (fp16 by default):
 // c16 [k_pad, dp], chalf = -|c~|^2/2 (fp32, summed as kmeans_update sums the
 // bf16 image's), |c| and |c - c~| (fp64, rounded up) and their maxima (as
@@ -2750,6 +2768,486 @@ struct FusedQ1Fin {
   }
 };
 
+// ---------------------------------------------------------------------------
+// v3 of the fused exact assign (PB = 2 point blocks per wave, D <= 128).  v2
+// issues ~100 VALU and ~48 SALU per 32-cluster tile and wave beside its 16
+// MFMAs (PMC: MFMA pipes 51 % busy, 40 % of wave cycles issue-stalled;
+// profiles/r04_exact_pipe_ab.json).  v3 trims that stream and the registers:
+//  * the 16 (tile, register) codes of a tile are made once, in SGPRs, and
+//    shared by both point blocks (v2 re-derived them per block: 39 s_add);
+//  * -|c|^2/2 is read from LDS straight into the accumulators (v2 kept a bias
+//    register set and copied it: 16 v_mov per tile);
+//  * kV3Jit: the A fragments are read from the CURRENT tile's ring slot two
+//    k-steps ahead of their MFMAs instead of a whole tile ahead — 8 VGPRs of A
+//    live instead of 32 (the slot refilled at the top of tile t is t-1's, so
+//    the DMA lead is NS-1 tiles);
+//  * kV3Prio: s_setprio 1 while a wave issues its MFMA chain and 0 for its
+//    epilogue, so the waves of a SIMD hand the matrix pipe to each other;
+//  * kV3Pipe: tile t-1's epilogue is interleaved with tile t's MFMAs in the
+//    wave (two accumulator sets; implies kV3Jit);
+//  * kV3Half: a half-tile pipeline with no extra accumulators — block 0's
+//    MFMA chain beside block 1's epilogue of the previous tile and vice versa;
+//  * kV3Pair: two tiles per barrier step (the per-step wait, barrier, loop and
+//    stamps measured ~830 of a tile's ~2240 cycles per wave); the ring slots
+//    are refilled from inside the epilogue (an LDS-DMA issued among VALU costs
+//    a fraction of one issued beside the barrier), and the next tile's
+//    -|c|^2/2 is read between the two blocks' epilogues so its latency hides
+//    behind the second (kV3Ns6: a 6-slot ring, one more step of DMA lead);
+//  * kV3Tiled: the centroid image in the tiled (piece-major) layout of
+//    hbmr_kmeans_image16_tiled: a tile's DMA is lane-linear on both sides and
+//    a lane's k-step s is at a fixed immediate offset (s * 1 KiB) from one
+//    base register — no XOR-swizzle offsets (8 VGPRs) or per-read address
+//    VALU; 16 lanes of one k-step read 256 contiguous bytes (conflict-free).
+constexpr int kV3Jit = 1, kV3Prio = 2, kV3Pipe = 4, kV3Half = 8, kV3Tiled = 16, kV3Stamp = 32,
+              kV3Pair = 64, kV3Ns6 = 128, kV3Reord = 256;
+// kV3Stamp (base path only): s_memtime stamps of 6 points of every tile, per
+// wave, kept in LDS and copied at the end to g_v3_stamps for workgroups < 64
+// (hbmr_kmeans_set_stamps) — where a tile's cycles go
+__device__ uint32_t* g_v3_stamps;
+constexpr int kV3StampBytes = 4 * 32 * 8 * 4;
+
+// tiled image: tile t is 32 * D * 2 contiguous bytes already in LDS order
+template <int D>
+__device__ __forceinline__ void stage_tile32t(char* buf, const __bf16* __restrict__ Ct,
+                                              const float* __restrict__ chalf, int tile, int wave,
+                                              int lane) {
+  using V = AssignV2<D>;
+  // wave-uniform bases + a 32-bit lane offset: the saddr form of the DMA (one
+  // VGPR of address, not a 64-bit pair per instruction)
+  const uint32_t loff = (uint32_t)lane * 16u;
+#pragma unroll
+  for (int i = 0; i < V::P; ++i) {
+    const int base = (i * V::WAVES + wave) * HBMR_WAVE;
+    const char* g = reinterpret_cast<const char*>(Ct) + (size_t)tile * V::TILE_BYTES +
+                    (size_t)base * 16;
+    __builtin_amdgcn_global_load_lds((const void*)(g + loff), (void*)(buf + base * 16), 16, 0, 0);
+  }
+  if (wave == 0 && lane < 32) {
+    const char* g = reinterpret_cast<const char*>(chalf + (size_t)tile * 32);
+    __builtin_amdgcn_global_load_lds((const void*)(g + loff / 4u), (void*)(buf + V::TILE_BYTES),
+                                     4, 0, 0);
+  }
+}
+
+// (tile, register) codes of tile t in SGPRs (see PackedArgMax)
+__device__ __forceinline__ void tile_codes(uint32_t top, int t, uint32_t (&code)[16]) {
+  const uint32_t base = top - ((uint32_t)t << 4);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    code[r] = base | (15u - r);
+    asm("" : "+s"(code[r]));
+  }
+}
+
+// PackedTop2x8::update with precomputed codes (pair insertion, NT tracks)
+__device__ __forceinline__ void top2_insert(PackedTop2x8& am, const f32x16& acc,
+                                            const uint32_t (&code)[16], uint32_t vmask) {
+  constexpr int NT = PackedTop2x8::NT;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    if ((r / NT) % 2) continue;
+    const float u = __uint_as_float((__float_as_uint(acc[r]) & vmask) | code[r]);
+    const float v = __uint_as_float((__float_as_uint(acc[r + NT]) & vmask) | code[r + NT]);
+    const float m = vmed3(am.tb[r % NT], u, v);
+    am.ts[r % NT] = vmax3(m, am.ts[r % NT], am.ts[r % NT]);
+    am.tb[r % NT] = vmax3(am.tb[r % NT], u, v);
+  }
+}
+
+template <int D, bool F16, int MODE, int NS = (MODE & kV3Ns6) ? 6 : 4>
+__device__ __forceinline__ void assign_tile_v3(const __bf16* __restrict__ X, long n,
+                                               const __bf16* __restrict__ C,
+                                               const float* __restrict__ chalf, int ntiles,
+                                               int32_t* __restrict__ labels, long blk, char* smem,
+                                               const FusedQ1Fin& fin) {
+  static_assert(D <= 128, "v3 keeps two 32-point blocks of D <= 128 in registers");
+  constexpr int PB = 2;
+  using V = AssignV2<D, NS>;
+  static_assert(V::WAVES == 4, "v3: 4 waves per workgroup");
+  constexpr int KS = V::KS;
+  constexpr bool PIPE = (MODE & kV3Pipe) != 0;
+  constexpr bool JIT = PIPE || (MODE & kV3Jit) != 0;
+  constexpr bool PRIO = (MODE & kV3Prio) != 0;
+  constexpr bool HALF = (MODE & kV3Half) != 0 && !JIT;
+  constexpr bool TILED = (MODE & kV3Tiled) != 0;
+  constexpr bool STAMP = (MODE & kV3Stamp) != 0;
+  constexpr bool PAIR = (MODE & kV3Pair) != 0 && !JIT && !HALF;
+  constexpr bool REORD = (MODE & kV3Reord) != 0;
+  constexpr int SWZ = AssignCfg<D>::SWZ;
+  // the bias sits right after the tile's rows whatever D is
+  static_assert(V::TILE_BYTES == 32 * D * 2, "tile layout");
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / HBMR_WAVE);
+  const int lane = tid & (HBMR_WAVE - 1);
+  const int h = lane >> 5;
+  const int col = lane & 31;
+  const long p0 = blk * (V::WAVES * PB * 32) + (long)wave * PB * 32;
+  const int aswz = col & SWZ;
+  // `row` is the tile buffer + rowoff: row-major rows (XOR-swizzled pieces)
+  // or the tiled layout (k-step s of this lane at s KiB)
+  const int rowoff = TILED ? h * 512 + col * 16 : col * (D * 2);
+  auto frag = [&](const char* row, int s) __attribute__((always_inline)) {
+    if constexpr (TILED)
+      return *reinterpret_cast<const bf16x8*>(row + s * 1024);
+    else
+      return *reinterpret_cast<const bf16x8*>(row + (((2 * s + h) ^ aswz) << 4));
+  };
+  auto stage = [&](char* buf, int tile) __attribute__((always_inline)) {
+    if constexpr (TILED) stage_tile32t<D>(buf, C, chalf, tile, wave, lane);
+    else stage_tile32<D>(buf, C, chalf, tile, wave, lane);
+  };
+  auto bias = [&](const char* buf, f32x16& acc) __attribute__((always_inline)) {
+    const float* ch = reinterpret_cast<const float*>(buf + V::TILE_BYTES);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(ch + 8 * g + 4 * h);
+      acc[4 * g + 0] = v[0];
+      acc[4 * g + 1] = v[1];
+      acc[4 * g + 2] = v[2];
+      acc[4 * g + 3] = v[3];
+    }
+  };
+
+  constexpr int LEAD = JIT || HALF || PAIR ? NS - 1 : NS;   // tiles staged before tile 0
+#pragma unroll
+  for (int i = 0; i < LEAD; ++i)
+    if (i < ntiles) stage(smem + i * V::BUF, i);
+
+  bf16x8 bfrag[PB][KS];
+#pragma unroll
+  for (int pb = 0; pb < PB; ++pb) {
+    long p = p0 + pb * 32 + col;
+    if (p >= n) p = n - 1;
+    const uint4* row = reinterpret_cast<const uint4*>(X + p * D);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) bfrag[pb][s] = __builtin_bit_cast(bf16x8, row[2 * s + h]);
+  }
+  PackedTop2x8 am[PB];
+#pragma unroll
+  for (int pb = 0; pb < PB; ++pb) am[pb].init(ntiles);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int pb = 0; pb < PB; ++pb)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(bfrag[pb][s]));
+  __syncthreads();
+  const bool w0 = wave == 0;
+  const uint32_t top = am[0].top;
+  const uint32_t vmask = am[0].vmask;   // one copy for both blocks
+
+  if constexpr (HALF) {
+    // half-tile software pipeline: block 0's MFMA chain of tile t runs beside
+    // block 1's epilogue of tile t-1, block 1's chain beside block 0's epilogue
+    // of tile t and the LDS reads of tile t+1 — each 8-MFMA chain (256 matrix
+    // cycles) carries 40 VALU, 5 per MFMA gap, with no extra accumulator set.
+    // -|c|^2/2 is read straight into an accumulator once its epilogue is done,
+    // so the slot refilled at the top of tile t is tile t-1's (every read of
+    // it retired): tile t+1 must have landed there, a DMA lead of NS-2 tiles.
+    bf16x8 a[KS];
+    f32x16 acc0, acc1;
+    {
+      const char* row = smem + rowoff;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) a[s] = frag(row, s);
+      bias(smem, acc0);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc1[r] = -3.0e38f;   // "tile -1": displaced
+    }
+    int slot = 0;                // t % NS
+    auto step = [&](int t, uint32_t (&code)[16], const uint32_t (&cprev)[16])
+        __attribute__((always_inline)) {
+      wait_tile_dmas<V::P, NS - 3>(max(0, min(NS - 3, ntiles - 2 - t)), w0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int pslot = slot == 0 ? NS - 1 : slot - 1;
+      if (t + NS - 1 < ntiles)
+        stage(smem + pslot * V::BUF, t + NS - 1);
+      const char* cbuf = smem + slot * V::BUF;
+      slot = slot + 1 == NS ? 0 : slot + 1;
+      const char* nbuf = smem + slot * V::BUF;   // tile t+1 (stale past the end)
+      const char* nrow = nbuf + rowoff;
+      tile_codes(top, t, code);
+      // phase A: block 0's chain of tile t, block 1's epilogue of tile t-1
+#pragma unroll
+      for (int s = 0; s < KS; ++s) acc0 = mfma32x32x16<F16>(a[s], bfrag[0][s], acc0);
+      top2_insert(am[1], acc1, cprev, vmask);
+      bias(cbuf, acc1);
+      // (the epilogue first, so the bias reads that follow it have the last
+      // MFMAs of the chain to land before phase B's first MFMA needs them)
+#pragma unroll
+      for (int i = 0; i < KS - 2; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      // phase B: block 1's chain of tile t, block 0's epilogue of tile t, and
+      // tile t+1's A fragments read as the chain frees their registers
+#pragma unroll
+      for (int s = 0; s < KS; ++s) acc1 = mfma32x32x16<F16>(a[s], bfrag[1][s], acc1);
+      top2_insert(am[0], acc0, code, vmask);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) a[s] = frag(nrow, s);
+      bias(nbuf, acc0);
+#pragma unroll
+      for (int i = 0; i < KS; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    };
+    uint32_t cA[16], cB[16];
+    tile_codes(top, -1, cB);
+    int t = 0;
+    for (; t + 1 < ntiles; t += 2) {
+      step(t, cA, cB);
+      step(t + 1, cB, cA);
+    }
+    if (t < ntiles) {
+      step(t, cA, cB);
+      top2_insert(am[1], acc1, cA, vmask);
+    } else if (ntiles > 0) {
+      top2_insert(am[1], acc1, cB, vmask);
+    }
+  } else if constexpr (PAIR) {
+    // step j: tiles 2j and 2j+1 behind one barrier.  Tile t's A fragments are
+    // read during tile t-1's MFMAs and its -|c|^2/2 between tile t-1's two
+    // epilogues, so after the barrier at the top of step j every read of the
+    // slots of tiles 2j-1 and 2j has retired: step j refills them with tiles
+    // 2j-1+NS and 2j+NS, and needs tiles 2j+1 and 2j+2 landed at its top.
+    static_assert(NS == 4 || NS == 6, "pair ring depth");
+    bf16x8 a[KS];
+    f32x16 bz;
+    {
+      const char* row = smem + rowoff;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) a[s] = frag(row, s);
+      bias(smem, bz);
+    }
+    uint32_t* stl = reinterpret_cast<uint32_t*>(smem + NS * V::BUF) + wave * 256;
+    auto stamp = [&](int j, int e) __attribute__((always_inline)) {
+      if constexpr (STAMP) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (lane == 0 && j < 32) stl[j * 8 + e] = (uint32_t)__builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    // one tile: MFMAs on A(t) (reading A(t+1) from nslot as each k-step frees
+    // its registers), block 1's epilogue, bias(t+1), the refill DMA, block 0's
+    auto tile = [&](int t, const char* nbuf, char* rbuf, int rtile)
+        __attribute__((always_inline)) {
+      const char* nrow = nbuf + rowoff;
+      f32x16 acc[PB];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+#pragma unroll
+        for (int pb = 0; pb < PB; ++pb)
+          acc[pb] = mfma32x32x16<F16>(a[s], bfrag[pb][s], s == 0 ? bz : acc[pb]);
+        a[s] = frag(nrow, s);
+      }
+      uint32_t code[16];
+      tile_codes(top, t, code);
+      top2_insert(am[1], acc[1], code, vmask);
+      bias(nbuf, bz);
+      if (rtile < ntiles) stage(rbuf, rtile);
+      top2_insert(am[0], acc[0], code, vmask);
+    };
+    for (int j = 0; 2 * j < ntiles; ++j) {
+      const int t0 = 2 * j;
+      stamp(j, 0);
+      if constexpr (NS == 4) {
+        vm_wait<0>();
+      } else {
+        const int y = max(0, min(2, ntiles - 3 - t0));
+        if (y == 2) { if (w0) vm_wait<2 * (V::P + 1)>(); else vm_wait<2 * V::P>(); }
+        else if (y == 1) { if (w0) vm_wait<V::P + 1>(); else vm_wait<V::P>(); }
+        else vm_wait<0>();
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      stamp(j, 1);
+      __syncthreads();
+      stamp(j, 2);
+      // slots: tile t lives in slot t % NS
+      char* s_m1 = smem + ((t0 + NS - 1) % NS) * V::BUF;   // tile 2j-1's slot
+      char* s_0 = smem + (t0 % NS) * V::BUF;               // tile 2j's
+      const char* s_1 = smem + ((t0 + 1) % NS) * V::BUF;   // tile 2j+1's
+      const char* s_2 = smem + ((t0 + 2) % NS) * V::BUF;   // tile 2j+2's
+      tile(t0, s_1, s_m1, t0 - 1 + NS);
+      stamp(j, 3);
+      if (t0 + 1 < ntiles) tile(t0 + 1, s_2, s_0, t0 + NS);
+      stamp(j, 4);
+    }
+    if constexpr (STAMP) {
+      __syncthreads();
+      if (blockIdx.x < 64 && g_v3_stamps)
+        for (int i = lane; i < 256; i += HBMR_WAVE)
+          g_v3_stamps[((size_t)blockIdx.x * 4 + wave) * 256 + i] = stl[i];
+    }
+  } else if constexpr (!JIT) {
+    // v2's ring (tile t+1's A read during tile t), codes shared, bias into acc
+    bf16x8 a[KS];
+    f32x16 bz;
+    {
+      const char* row = smem + rowoff;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) a[s] = frag(row, s);
+      bias(smem, bz);
+    }
+    int slot = 0;
+    uint32_t* stl = reinterpret_cast<uint32_t*>(smem + NS * V::BUF) + wave * 256;
+    auto stamp = [&](int t, int e) __attribute__((always_inline)) {
+      if constexpr (STAMP) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (lane == 0 && t < 32) stl[t * 8 + e] = (uint32_t)__builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    for (int t = 0; t < ntiles; ++t) {
+      stamp(t, 0);
+      wait_tile_dmas<V::P, NS - 2>(max(0, min(NS - 2, ntiles - 2 - t)), w0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      stamp(t, 1);
+      __syncthreads();
+      stamp(t, 2);
+      char* rbuf = smem + slot * V::BUF;
+      if constexpr (!REORD)
+        if (t + NS < ntiles) stage(rbuf, t + NS);
+      slot = slot + 1 == NS ? 0 : slot + 1;
+      const char* nbuf = smem + slot * V::BUF;
+      const char* nrow = nbuf + rowoff;
+      stamp(t, 3);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+      f32x16 acc[PB];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+#pragma unroll
+        for (int pb = 0; pb < PB; ++pb)
+          acc[pb] = mfma32x32x16<F16>(a[s], bfrag[pb][s], s == 0 ? bz : acc[pb]);
+        a[s] = frag(nrow, s);
+      }
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+      stamp(t, 4);
+      uint32_t code[16];
+      tile_codes(top, t, code);
+      if constexpr (REORD) {
+        // block 1's epilogue frees bz's registers (block 1 accumulates in
+        // them), then bias(t+1) and the refill DMA go out among block 0's VALU
+        top2_insert(am[1], acc[1], code, vmask);
+        bias(nbuf, bz);
+        if (t + NS < ntiles) stage(rbuf, t + NS);
+        top2_insert(am[0], acc[0], code, vmask);
+        stamp(t, 5);
+      } else {
+#pragma unroll
+        for (int pb = 0; pb < PB; ++pb) top2_insert(am[pb], acc[pb], code, vmask);
+        stamp(t, 5);
+        bias(nbuf, bz);
+      }
+    }
+    if constexpr (STAMP) {
+      __syncthreads();
+      if (blockIdx.x < 64 && g_v3_stamps)
+        for (int i = lane; i < 256; i += HBMR_WAVE)
+          g_v3_stamps[((size_t)blockIdx.x * 4 + wave) * 256 + i] = stl[i];
+    }
+  } else if constexpr (!PIPE) {
+    int slot = 0;                // t % NS
+    for (int t = 0; t < ntiles; ++t) {
+      // tile t landed for every wave (younger DMAs: tiles t+1 .. t+NS-2), and
+      // every wave's reads of tile t-1's slot retired → that slot is free
+      wait_tile_dmas<V::P, NS - 2>(max(0, min(NS - 2, ntiles - 1 - t)), w0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int pslot = slot == 0 ? NS - 1 : slot - 1;
+      if (t + NS - 1 < ntiles)
+        stage(smem + pslot * V::BUF, t + NS - 1);
+      const char* buf = smem + slot * V::BUF;
+      const char* row = buf + rowoff;
+      slot = slot + 1 == NS ? 0 : slot + 1;
+      f32x16 bz;
+      bias(buf, bz);
+      bf16x8 a[2];
+      a[0] = frag(row, 0);
+      a[1] = frag(row, 1);
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+      f32x16 acc[PB];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+#pragma unroll
+        for (int pb = 0; pb < PB; ++pb)
+          acc[pb] = mfma32x32x16<F16>(a[s & 1], bfrag[pb][s], s == 0 ? bz : acc[pb]);
+        if (s + 2 < KS) a[s & 1] = frag(row, s + 2);
+      }
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+      uint32_t code[16];
+      tile_codes(top, t, code);
+#pragma unroll
+      for (int pb = 0; pb < PB; ++pb) top2_insert(am[pb], acc[pb], code, vmask);
+    }
+  } else {
+    // MFMAs of tile t into `acc`, the epilogue of tile t-1 from `prev`
+    int slot = 0;
+    auto step = [&](int t, f32x16 (&acc)[PB], f32x16 (&prev)[PB], bool epi)
+        __attribute__((always_inline)) {
+      wait_tile_dmas<V::P, NS - 2>(max(0, min(NS - 2, ntiles - 1 - t)), w0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int pslot = slot == 0 ? NS - 1 : slot - 1;
+      if (t + NS - 1 < ntiles)
+        stage(smem + pslot * V::BUF, t + NS - 1);
+      const char* buf = smem + slot * V::BUF;
+      const char* row = buf + rowoff;
+      slot = slot + 1 == NS ? 0 : slot + 1;
+      f32x16 bz;
+      bias(buf, bz);
+      bf16x8 a[2];
+      a[0] = frag(row, 0);
+      a[1] = frag(row, 1);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+#pragma unroll
+        for (int pb = 0; pb < PB; ++pb)
+          acc[pb] = mfma32x32x16<F16>(a[s & 1], bfrag[pb][s], s == 0 ? bz : acc[pb]);
+        if (s + 2 < KS) a[s & 1] = frag(row, s + 2);
+      }
+      if (epi) {
+        uint32_t code[16];
+        tile_codes(top, t - 1, code);
+#pragma unroll
+        for (int pb = 0; pb < PB; ++pb) top2_insert(am[pb], prev[pb], code, vmask);
+      }
+#pragma unroll
+      for (int i = 0; i < KS * PB; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);   // then vector ALU
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // and an LDS read
+      }
+    };
+    f32x16 accA[PB], accB[PB];
+    int t = 0;
+    if (ntiles > 0) {
+      step(0, accA, accB, false);
+      t = 1;
+    }
+    for (; t + 1 < ntiles; t += 2) {
+      step(t, accB, accA, true);
+      step(t + 1, accA, accB, true);
+    }
+    uint32_t code[16];
+    if (t < ntiles) {
+      step(t, accB, accA, true);
+      tile_codes(top, t, code);
+#pragma unroll
+      for (int pb = 0; pb < PB; ++pb) top2_insert(am[pb], accB[pb], code, vmask);
+    } else if (ntiles > 0) {
+      tile_codes(top, ntiles - 1, code);
+#pragma unroll
+      for (int pb = 0; pb < PB; ++pb) top2_insert(am[pb], accA[pb], code, vmask);
+    }
+  }
+  fin(am, h, p0, col, n, labels);
+}
+
 struct TopQ1Table {       // the batch's splits, by value (X, per-point norms)
   int nsplit;
   const __bf16* X[kMaxGroup];
@@ -2782,6 +3280,28 @@ kmeans_assign_top3_q1_grouped_kernel(const TopQ1Table tbl, const __bf16* __restr
       tbl.X[s], tbl.off[s + 1] - o, C, chalf,
                                                      ntiles, labels + o, nullptr, b - tbl.blk[s],
                                                      smem, nullptr, nullptr, -1, &fin);
+}
+
+// v3 (see assign_tile_v3): MINB workgroups of 4 waves per CU
+template <int D, bool F16, int MODE, int MINB>
+__global__ __launch_bounds__(256, MINB) void kmeans_assign_top3_q1_v3_kernel(
+    const TopQ1Table tbl, const __bf16* __restrict__ C, const float* __restrict__ chalf,
+    int ntiles, int32_t* __restrict__ labels, FusedQ1Fin fin) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const long b = hbmr_xcd_remap(blockIdx.x, gridDim.x);
+  int lo = 0, hi = tbl.nsplit;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (tbl.blk[mid] <= b) lo = mid; else hi = mid;
+  }
+  const int s = __builtin_amdgcn_readfirstlane(lo);
+  const long o = tbl.off[s];
+  fin.xnorm = tbl.xnorm[s];
+  fin.xbn2 = tbl.xbn2[s];
+  fin.xerr = tbl.xerr[s];
+  fin.sidx = s;
+  assign_tile_v3<D, F16, MODE>(tbl.X[s], tbl.off[s + 1] - o, C, chalf, ntiles, labels + o,
+                               b - tbl.blk[s], smem, fin);
 }
 
 // 16 features of a row per lane of an 8-lane group: 128m + 32h + 4sub + (0..3)
@@ -3637,7 +4157,8 @@ int hbmr_kmeans_assign_top3_grouped(int nsplit, const void* const* X, const long
 // of every point, the batch's step-2 queue and flagged count in ws (as
 // hbmr_kmeans_refine_batch_q1g leaves them); dp <= 128
 int hbmr_kmeans_assign_top3_q1_grouped(int nsplit, const void* const* X, const long* n, int dp,
-                                       int f16, const void* C, const float* chalf, int k_pad,
+                                       int f16, const void* C, const void* Ct,
+                                       const float* chalf, int k_pad,
                                        int32_t* labels, const float* const* xnorm,
                                        const float* const* xbn2, const float* const* xerr,
                                        int d, int k, const float* cnorm, const float* cmax,
@@ -3702,6 +4223,59 @@ int hbmr_kmeans_assign_top3_q1_grouped(int nsplit, const void* const* X, const l
     const char* e = getenv("HBMR_EXACT_NS");
     return e && atoi(e) == 6;
   }();
+  // HBMR_EXACT_V3: the v3 fused kernel (assign_tile_v3) in mode M (bits kV3*:
+  // 1 just-in-time A reads at 4 waves per SIMD, 2 MFMA-chain priority, 4 epilogue
+  // pipelining, 8 half-tile pipeline, 16 tiled image); "v2": v2
+  // (read per launch: an A/B harness flips it within one process)
+  const int v3 = [] {
+    const char* e = getenv("HBMR_EXACT_V3");
+    if (!e || !*e) return HBMR_EXACT_V3_DEFAULT;
+    if (strcmp(e, "v2") == 0) return -1;
+    return atoi(e);
+  }();
+#define HBMR_V3_CASE(D, F, M)                                                                  \
+  case M:                                                                                      \
+    kern = kmeans_assign_top3_q1_v3_kernel<D, F, M,                                            \
+                                           (M & kV3Jit) && !(M & kV3Pipe) ? 4 : 3>;            \
+    break;
+#define HBMR_TOP3Q1_V3(D, F)                                                                   \
+  {                                                                                            \
+    decltype(&kmeans_assign_top3_q1_v3_kernel<D, F, 0, 3>) kern = nullptr;                     \
+    switch (v3) {                                                                              \
+      HBMR_V3_CASE(D, F, 0)                                                                    \
+      HBMR_V3_CASE(D, F, 16)                                                                   \
+      HBMR_V3_CASE(D, F, 18)                                                                   \
+      HBMR_V3_CASE(D, F, 24)                                                                   \
+      HBMR_V3_CASE(D, F, 17)                                                                   \
+      HBMR_V3_CASE(D, F, 19)                                                                   \
+      HBMR_V3_CASE(D, F, 20)                                                                   \
+      HBMR_V3_CASE(D, F, 48)                                                                   \
+      HBMR_V3_CASE(D, F, 80)                                                                   \
+      HBMR_V3_CASE(D, F, 208)                                                                  \
+      HBMR_V3_CASE(D, F, 112)                                                                  \
+      HBMR_V3_CASE(D, F, 272)                                                                  \
+      HBMR_V3_CASE(D, F, 274)                                                                  \
+      HBMR_V3_CASE(D, F, 304)                                                                  \
+      default: return (int)hipErrorInvalidValue;                                               \
+    }                                                                                          \
+    if ((v3 & kV3Tiled) && !Ct) return (int)hipErrorInvalidValue;                             \
+    const size_t lds = ((v3 & kV3Ns6) ? AssignV2<D, 6>::LDS_BYTES : AssignV2<D>::LDS_BYTES) + \
+                       ((v3 & kV3Stamp) ? kV3StampBytes : 0);                                  \
+    hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), lds, st, t,                        \
+                       reinterpret_cast<const __bf16*>((v3 & kV3Tiled) ? Ct : C), chalf,       \
+                       k_pad / 32, labels, fin);                                               \
+    return (int)hipGetLastError();                                                             \
+  }
+  if (v3 >= 0) {
+    if (dp == 64) {
+      if (f16) HBMR_TOP3Q1_V3(64, true)
+      HBMR_TOP3Q1_V3(64, false)
+    }
+    if (f16) HBMR_TOP3Q1_V3(128, true)
+    HBMR_TOP3Q1_V3(128, false)
+  }
+#undef HBMR_V3_CASE
+#undef HBMR_TOP3Q1_V3
 #define HBMR_TOP3Q1(D)                                                                         \
   {                                                                                            \
     auto kern = pipe ? (f16 ? kmeans_assign_top3_q1_grouped_kernel<D, true, true>              \
@@ -3763,6 +4337,21 @@ int hbmr_kmeans_exact_prep(const float* x, long n, int d, int ldx, int dp, int f
   if (blocks > 0x7fffffffL) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(kmeans_exact_prep_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, n, d,
                      ldx, dp, f16, reinterpret_cast<uint16_t*>(x16), xnorm, xn2, xerr);
+  return (int)hipGetLastError();
+}
+
+// the v3 kernel's stamp buffer (kV3Stamp): u32 [64 workgroups][4 waves][32 tiles][8]
+int hbmr_kmeans_set_stamps(void* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_v3_stamps), &p, sizeof(p));
+}
+
+int hbmr_kmeans_image16_tiled(const void* c16, int k_pad, int dp, void* c16t, hipStream_t st) {
+  if (k_pad <= 0 || k_pad % 32 || (dp != 64 && dp != 128) || !c16 || !c16t)
+    return (int)hipErrorInvalidValue;
+  const long pieces = (long)k_pad * dp / 8;
+  hipLaunchKernelGGL(kmeans_image16_tiled_kernel, dim3((unsigned)((pieces + 255) / 256)),
+                     dim3(256), 0, st, reinterpret_cast<const uint4*>(c16), k_pad, dp,
+                     reinterpret_cast<uint4*>(c16t));
   return (int)hipGetLastError();
 }
 

@@ -48,7 +48,7 @@ def test_exact_mode_job_on_cpu_slots_matches_fp64_lloyd():
             drv.step()
         got = drv.centroids()
     x = K.synthetic_points(9, 0, n, d, k, "cpu")
-    ref = lloyd64(x, K.initial_centroids(inp, k, d), 3)
+    ref = lloyd64(x, K.initial_centroids(inp, k, d, exact=True), 3)
     err = (got.double() - ref).abs().max().item()
     assert err < 1e-4, err
 
@@ -242,7 +242,7 @@ def test_exact_mode_job_matches_fp64_lloyd():
         got = drv.centroids()
         flagged = r["counters"].get("KMEANS", "EXACT_FLAGGED_POINTS")
     x = K.synthetic_points(5, 0, n, d, k // 2, "cuda")
-    ref = lloyd64(x, K.initial_centroids(inp, k, d, centers=k // 2).cuda(), 3)
+    ref = lloyd64(x, K.initial_centroids(inp, k, d, centers=k // 2, exact=True).cuda(), 3)
     # identical assignments: centroids differ only by the 2^-24 fixed-point rounding
     assert (got.cuda().double() - ref).abs().max().item() < 1e-5
     assert flagged > 0
@@ -370,3 +370,81 @@ def test_native_centroid_neighbour_table_bounds():
     assert own.sum().item() == k - 1           # every centroid first but 7 (5 ties first)
     kth = exact.sort(dim=1).values[:, L - 1]
     assert (true <= kth[:, None] * (1 + 1e-6) + 1e-9).all()
+
+
+def test_exact_mode_starts_from_the_fp32_points():
+    """Exact mode's first centroids are the fp32 first-k points; the bf16 mode
+    keeps their bf16 roundings (what its image holds)."""
+    inp = "synthetic:1000:5"
+    x = K.synthetic_points(5, 0, 16, 24, 16, "cpu")
+    assert torch.equal(K.initial_centroids(inp, 16, 24, exact=True), x)
+    assert torch.equal(K.initial_centroids(inp, 16, 24), x.to(torch.bfloat16).float())
+
+
+def _only_ties(x, c, got, want):
+    """Every label that differs from the fp64 arg-min is an exact fp64 tie."""
+    bad = (got != want).nonzero().flatten()
+    if bad.numel() == 0:
+        return 0
+    xb = x[bad].double()
+    cd = c.double()
+    dg = ((xb - cd[got[bad].long()]) ** 2).sum(1)
+    dw = ((xb - cd[want[bad].long()]) ** 2).sum(1)
+    assert torch.equal(dg, dw), (bad[:8].tolist(), (dg - dw)[:8].tolist())
+    return bad.numel()
+
+
+@pytest.mark.gpu
+def test_exact_batch_labels_at_bench_shape():
+    """The bench's shape and distribution (k = 1024 centers, d = 128): the
+    packed arg-max keeps 9 fewer mantissa bits at k = 1024 (4 + log2(k/32)),
+    yet every certified label is the fp64 arg-min of the fp32 data (up to fp64
+    ties), for the default fused kernel and the round-4 one."""
+    import os
+    from hbmr.ops import kmeans as km
+    n, d, k, split = 2_000_000, 128, 1024, 250_000
+    x = K.synthetic_points(7, 0, n, d, k, "cuda")
+    c = K.initial_centroids(f"synthetic:{n}:7", k, d, exact=True).cuda()
+    for _ in range(3):                                   # centroids of a few Lloyd steps
+        lab = truth_labels(x, c).long()
+        s = torch.zeros(k, d, dtype=torch.float64, device="cuda").index_add_(0, lab, x.double())
+        cnt = torch.bincount(lab, minlength=k).double()[:, None]
+        c = torch.where(cnt > 0, s / cnt.clamp(min=1), c.double()).float()
+    img = km.CentroidImage(c, "cuda")
+    sps = [km.ExactSplit(x[a:a + split].contiguous(), km.padded_dim(d))
+           for a in range(0, n, split)]
+    want = truth_labels(x, c)
+    old = os.environ.get("HBMR_EXACT_V3")
+    try:
+        for mode in ("", "v2"):
+            os.environ["HBMR_EXACT_V3"] = mode
+            st = torch.zeros(5, dtype=torch.int64, device="cuda")
+            got = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+            km.assign_exact_batch(sps, img, st, got, {})
+            assert _only_ties(x, c, got, want) <= 4
+            assert st[0].item() > 0                      # the certification had work
+    finally:
+        if old is None:
+            os.environ.pop("HBMR_EXACT_V3", None)
+        else:
+            os.environ["HBMR_EXACT_V3"] = old
+
+
+@pytest.mark.gpu
+def test_exact_mode_job_at_bench_shape_matches_fp64_lloyd():
+    """Three iteration jobs at k = 1024, d = 128 on 2M points of the bench
+    distribution, through the JobTracker / GPU slots: the centroids equal
+    fp64-assignment Lloyd's with the framework's 2^-24 fixed-point sums."""
+    n, k, d, sp = 2_000_000, 1024, 128, 250_000
+    inp = f"synthetic:{n}:7"
+    conf = JobConf()
+    conf.set_boolean(K.EXACT_KEY, True)
+    with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=0) as cl:
+        drv = K.KMeansDriver(cl.submit_job, lambda rj: rj._impl.jip.result[0], conf=conf, k=k,
+                             d=d, inp=inp, split_points=sp)
+        for _ in range(3):
+            drv.step()
+        got = drv.centroids()
+    x = K.synthetic_points(7, 0, n, d, k, "cuda")
+    ref = lloyd64(x, K.initial_centroids(inp, k, d, exact=True).cuda(), 3)
+    assert (got.cuda().double() - ref).abs().max().item() < 1e-5

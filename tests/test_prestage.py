@@ -127,3 +127,73 @@ def test_predecessor_reduce_failing_after_release_restarts_its_staged_job(worker
     names = [e["event"] for e in events]
     assert "COLLECTIVE_RESTART" in names
     assert torch.equal(got, want)
+
+
+@pytest.mark.timeout(60)
+def test_collective_restart_closes_the_gate_on_every_gpu_tracker(tmp_path):
+    """A gang restarted with no job staged on it yet still closes its gate on
+    every GPU tracker: a failed member may have opened it already, and a job
+    staged on the restarted job later must wait for the new reduce instead of
+    passing that stale open gate (the close was sent only when a
+    staged job already existed)."""
+    conf = _conf(False, task_ms=50.0)
+    conf.set("mapred.local.dir", str(tmp_path))
+    with LocalCluster(conf, num_trackers=2, gpus=[[0], [1]], cpu_slots=0) as cl:
+        drv = K.KMeansDriver(cl.submit_job, lambda rj: rj._impl.jip.result[0], conf=conf, k=5,
+                             d=8, inp="synthetic:8000:3", split_points=1000)
+        rj = drv.submit(drv._job_conf(0))
+        jt = cl.jt
+        jid = str(rj.getID())
+        with jt.lock:
+            jip = jt.jobs[jid]
+            for t in jt.trackers.values():
+                t.extra_actions = [x for x in t.extra_actions if x.get("type") != "close_gate"]
+            jt._restart_collective(jip, "test")
+            closes = {name: [x for x in t.extra_actions
+                             if x.get("type") == "close_gate" and x.get("job_id") == jid]
+                      for name, t in jt.trackers.items() if t.status.gpus}
+        assert len(closes) == 2 and all(len(v) == 1 for v in closes.values()), closes
+        assert rj.waitForCompletion(60)
+        assert rj.status().state == "SUCCEEDED"
+
+
+@pytest.mark.timeout(120)
+def test_job_staged_after_a_collective_restart_waits_for_the_new_reduce(tmp_path):
+    """Iteration 2's reduce opens its gate on poisoned centroids and fails;
+    iteration 3 is submitted (and staged on iteration 2) only AFTER that
+    restart.  The restart closed the gate on every GPU tracker, so iteration
+    3's maps wait for the re-run reduce instead of passing the stale open gate
+    (the gate was closed only when a staged job already existed)."""
+    want, _, _, _ = _run(_conf(False, prestage=False, task_ms=20.0), tmp_path / "plain", steps=4)
+    conf = _conf(False, task_ms=20.0, **{"hbmr.faultinject.reduce.fail.after.release.attempt":
+                                         "_0002_r_000000_0"})
+    conf.set("mapred.local.dir", str(tmp_path / "late"))
+    with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=0) as cl:
+        drv = K.KMeansDriver(cl.submit_job, lambda rj: rj._impl.jip.result[0], conf=conf, k=5,
+                             d=8, inp="synthetic:8000:3", split_points=1000)
+        drv.step()                                 # iteration 1
+        jt = cl.jt
+        real_submit = drv.submit
+
+        def submit_after_restart(job):
+            # iteration 3 (depends on iteration 2): hold its submission until
+            # iteration 2's gang has failed and restarted
+            if job.get("hbmr.job.depends.on"):
+                for _ in range(2000):
+                    if any(e["event"] == "COLLECTIVE_RESTART" for e in jt.history.events):
+                        break
+                    import time as _t
+                    _t.sleep(0.005)
+            return real_submit(job)
+
+        drv.submit = submit_after_restart
+        drv.prefetch_delay = 0.0
+        drv.step(prefetch=1)                       # iteration 2, iteration 3 staged late
+        drv.step()
+        drv.step()
+        got = drv.centroids()
+        names = [e["event"] for e in jt.history.events]
+    assert "COLLECTIVE_RESTART" in names
+    restart = names.index("COLLECTIVE_RESTART")
+    assert "JOB_STAGED" in names[restart:], names
+    assert torch.equal(got, want)

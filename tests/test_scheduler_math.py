@@ -174,3 +174,49 @@ def test_split_jobs_plan_gpu_capacity_in_devices_not_slots():
     # 40 maps, CPU 10x slower: one device gives CPUs 10 maps, two "servers" only 4
     assert min_makespan_cpu_tasks(40, 4, 1, 0.2, 0.02) == 10
     assert min_makespan_cpu_tasks(40, 4, 2, 0.2, 0.02) < 10
+
+
+def test_requeued_maps_are_taken_first_at_local_levels():
+    """obtain_map's per-tracker locality stacks keep pending order: a TIP
+    re-queued at the front (a failed map / lost output, add_pending(front=
+    True)) is taken before lower-index local TIPs, as findNewMapTask takes
+    failed maps first (the stacks were sorted by map index)."""
+    import threading
+    import types
+
+    from hbmr.mapred.jobtracker import JobInProgress
+
+    class Tip:
+        def __init__(self, i):
+            self.partition = i
+            self.failed_trackers = set()
+
+        def locations(self):
+            return ["tt0"]
+
+        def split_key(self):
+            return None
+
+    class Job:
+        pass
+
+    for name in ("_index", "_by_location", "_rack_level", "obtain_map", "_take", "add_pending",
+                 "_count_locality"):
+        setattr(Job, name, getattr(JobInProgress, name))
+    job = Job()
+    tips = [Tip(i) for i in range(6)]
+    job.maps = tips
+    job.pending_maps = {t: None for t in tips}
+    job.by_split_key = {}
+    job._loc_index, job._front, job._front_seq = {}, {}, 0
+    job.acc_lock, job.loc_counts = threading.Lock(), [0, 0, 0]
+    tr = types.SimpleNamespace(name="tt0", cached=set(), rack="/r",
+                               status=types.SimpleNamespace(host="h0"))
+    job.jt = types.SimpleNamespace(trackers={"tt0": tr}, topology=None)
+    assert [job.obtain_map(tr, False, 0)[0].partition for _ in range(6)] == list(range(6))
+    job.add_pending(tips[1])                    # map 1 killed: back at the end
+    job.add_pending(tips[4], front=True)        # map 4 failed: re-run first
+    job.add_pending(tips[5], front=True)        # map 5 failed after it: newest first
+    got = [job.obtain_map(tr, False, 0)[0].partition for _ in range(3)]
+    assert got == [5, 4, 1]
+    assert job.obtain_map(tr, False, 0) is None

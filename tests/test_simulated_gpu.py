@@ -7,6 +7,8 @@ GPU devices (src/test/org/apache/hadoop/mapred/TestJobQueueTaskScheduler.java:
 """
 import json
 
+import pytest
+
 import torch
 
 from hbmr.examples.sleepjob import sleep_job_conf, split_sleep_conf
@@ -158,3 +160,54 @@ def test_split_cache_charges_derived_state_and_notifies_evictions():
     assert ("a", 0) in gone and c.bytes_on(0) == 50
     c.clear(0)
     assert ("c", 0) in gone and c.bytes_on(0) == 0
+
+
+def _iteration_ms(conf, iters=6):
+    import time as _t
+    with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=0) as cl:
+        drv = K.KMeansDriver(cl.submit_job, lambda rj: rj._impl.jip.result[0], conf=conf, k=6,
+                             d=16, inp="synthetic:12000:5", split_points=2000)
+        drv.step()
+        t0 = _t.time()
+        for _ in range(iters):
+            assert drv.step()["points"] == 12000
+        return (_t.time() - t0) * 1e3 / iters, drv.centroids()
+
+
+def test_report_without_assignment_does_not_stall_on_response_numbers():
+    """hbmr.tracker.report.assign=false: a report's actions go back through the
+    long-poll, numbered only there — numbering them in the report (whose
+    reply carries nothing) left a gap the tracker waited 2 s on."""
+    ms, got = _iteration_ms(_sim_conf(**{"hbmr.tracker.report.assign": "false"}))
+    ms_ref, want = _iteration_ms(_sim_conf())
+    assert torch.equal(got, want)
+    assert ms < 1000, ms
+
+
+@pytest.mark.timeout(60)
+def test_lost_report_reply_is_resent():
+    """A report reply lost after the JobTracker processed it (the RPC raised):
+    the tracker takes the numbered responses back (JobTracker.resend) instead
+    of losing their launches / commit approvals and stalling 2 s on the gap."""
+    from hbmr.mapred.jobtracker import JobTracker
+    real = JobTracker.report
+    state = {"n": 0, "lost": 0}
+
+    def flaky(self, status, assign=False):
+        r = real(self, status, assign)
+        if assign and r.get("actions"):
+            state["n"] += 1
+        if assign and r.get("actions") and state["n"] % 3 == 1:
+            state["lost"] += 1
+            raise ConnectionError("reply lost")
+        return r
+
+    JobTracker.report = flaky
+    try:
+        ms, got = _iteration_ms(_sim_conf())
+    finally:
+        JobTracker.report = real
+    _, want = _iteration_ms(_sim_conf())
+    assert state["lost"] > 0
+    assert torch.equal(got, want)
+    assert ms < 1000, ms

@@ -429,6 +429,22 @@ def test_terasort_out_of_core_spill_and_merge(tmp_path, budget_rows):
     assert T.teravalidate(str(out))["misordered"] == 0
 
 
+def test_terasort_spill_mode_on_several_ranks_fails_at_setup(tmp_path):
+    """Spill mode merges every map's run on one rank: a job it would put on two
+    trackers fails at job setup, before any map runs (it failed
+    with a KeyError in the shuffle after every map had run)."""
+    conf = T.terasort_conf(rows=12000, split_rows=2500, output=str(tmp_path / "out"),
+                           partitions=4)
+    conf.set("hbmr.terasort.hbm.budget.gb", str(4000 * 100 / (1 << 30)))
+    with LocalCluster(JobConf(), num_trackers=2, cpu_slots=2) as cl:
+        rj = cl.submit_job(conf)
+        rj.waitForCompletion(60)
+        assert not rj.isSuccessful()
+        assert "one rank" in (rj.getFailureInfo() or "")
+        jip = rj._impl.jip
+        assert all(t.successful is None for t in jip.maps)
+
+
 @pytest.mark.gpu
 def test_gpu_terasort_out_of_core(tmp_path):
     """On the GPU: data 3x a deliberately small HBM budget sorts through the
