@@ -82,6 +82,10 @@ class TrackerInfo:
         self.rack = DEFAULT_RACK
         self.kills: set[str] = set()   # attempts to kill on the next heartbeat
         self.kill_epoch = -1           # JobTracker.kill_epoch this tracker was last scanned at
+        self.cap_sig = None            # slot capacities last reported (JobTracker.cap_epoch)
+        # running attempt ids by job id: a job ending scans only its own
+        # attempts here for kills, not every running attempt of the tracker
+        self.running_by_job: dict = {}
         self.extra_actions: list = []  # e.g. restart_gpu_worker, sent on the next heartbeat
         # not worth ending a long-poll for (KillJobAction purges of finished
         # jobs): they ride on the next response the tracker gets anyway
@@ -211,6 +215,7 @@ class JobInProgress:
         self.running_gpu = 0
         self.pending_counters: list = []
         self._loc_index: dict = {}
+        self.reduce_by_tracker: dict = {}   # collective gang: tracker -> its pinned reduce
         self._front: dict = {}          # re-queued TIPs (add_pending front) -> order key
         self._front_seq = 0
         self.finished_cpu_maps = 0
@@ -293,6 +298,7 @@ class JobInProgress:
             for r in range(nred):
                 self.reduces.append(TaskInProgress(self, TaskID(self.job_id, False, r),
                                                    partition=r, pinned_tracker=trackers[r]))
+                self.reduce_by_tracker[trackers[r]] = self.reduces[-1]
         else:
             for r in range(conf.get_num_reduce_tasks()):
                 self.reduces.append(TaskInProgress(self, TaskID(self.job_id, False, r),
@@ -371,21 +377,34 @@ class JobInProgress:
                     if tip is not None and tip in pend and tip not in seen:
                         lv1.append(tip)
                         seen.add(tip)
-            byloc = self._by_location()
-            for loc in (tracker.name, tracker.status.host):
-                for tip in byloc.get(loc, ()):
-                    if tip in pend and tip not in seen:
-                        lv2.append(tip)
-                        seen.add(tip)
             # stacks popped from the end, in pending order: re-queued TIPs
             # (failed / lost outputs, add_pending(front=True)) first, newest
             # first, then map index order (findNewMapTask takes failed maps first)
             front = self._front
             order = lambda lv: sorted(lv, key=lambda t: front.get(t, t.partition),  # noqa: E731
                                       reverse=True)
-            idx = [order(lv0), order(lv1), order(lv2), None, len(tracker.cached), seen]
+            # level 2 (node-local by split location) is built on first use: on
+            # one host every split names this node, so building it eagerly
+            # visited every map of the job per (tracker, device) even when the
+            # HBM-resident level 0 serves them all
+            idx = [order(lv0), order(lv1), None, None, len(tracker.cached), seen]
             self._loc_index[key] = idx
         return idx
+
+    def _node_level(self, tracker, idx):
+        if idx[2] is None:
+            pend = self.pending_maps
+            seen = idx[5]
+            lv2 = []
+            byloc = self._by_location()
+            for loc in (tracker.name, tracker.status.host):
+                for tip in byloc.get(loc, ()):
+                    if tip in pend and tip not in seen:
+                        lv2.append(tip)
+                        seen.add(tip)
+            front = self._front
+            idx[2] = sorted(lv2, key=lambda t: front.get(t, t.partition), reverse=True)
+        return idx[2]
 
     def _by_location(self):
         """location (tracker name / host) -> the job's map TIPs naming it."""
@@ -426,7 +445,8 @@ class JobInProgress:
         for level in (0, 1, 2, 3):
             if level == 3 and not allow_nonlocal:
                 return None
-            stack = idx[level] if level < 3 else self._rack_level(tracker, idx)
+            stack = idx[level] if level < 2 else self._node_level(tracker, idx) if level == 2 \
+                else self._rack_level(tracker, idx)
             while stack:
                 tip = stack.pop()
                 if tip in self.pending_maps and not avoid(tip):
@@ -440,6 +460,56 @@ class JobInProgress:
             self._count_locality(4)
             return tip, 4
         return None
+
+    def obtain_maps(self, tracker: TrackerInfo, on_gpu: bool, device: int, n: int,
+                    allow_nonlocal=True):
+        """Up to ``n`` maps for one device in one call — obtain_map's levels
+        and order, with the index looked up once and the stacks drained in a
+        loop (a bulk launch takes a device's whole queue depth at once)."""
+        out = []
+        pend = self.pending_maps
+        if n <= 0 or not pend:
+            return out
+        ntr = len(self.jt.trackers)
+        multi = ntr > 1
+        name = tracker.name
+        idx = self._index(tracker, on_gpu, device)
+        for level in (0, 1, 2, 3):
+            if level == 3 and not allow_nonlocal:
+                break
+            stack = idx[level] if level < 2 else self._node_level(tracker, idx) if level == 2 \
+                else self._rack_level(tracker, idx)
+            while stack and len(out) < n:
+                tip = stack.pop()
+                if tip in pend and not (multi and name in tip.failed_trackers and
+                                        len(tip.failed_trackers) < ntr):
+                    self._take(tip)
+                    out.append((tip, level))
+            if len(out) >= n:
+                break
+        else:
+            for tip in list(pend):
+                if len(out) >= n:
+                    break
+                if multi and name in tip.failed_trackers and len(tip.failed_trackers) < ntr:
+                    continue
+                self._take(tip)
+                out.append((tip, 4))
+        if out:
+            counts = [0, 0, 0]
+            for _t, lv in out:
+                if lv == 0:
+                    counts[0] += 1
+                if lv <= 2:
+                    counts[1] += 1
+                elif lv == 3:
+                    counts[2] += 1
+            with self.acc_lock:
+                lc = self.loc_counts
+                lc[0] += counts[0]
+                lc[1] += counts[1]
+                lc[2] += counts[2]
+        return out
 
     def locality_possible(self) -> bool:
         """Does any split name a live tracker (by tracker name, host or rack)?
@@ -561,11 +631,18 @@ class JobTracker:
         # job they wait for (hbmr/gpu/gates.py); chains up to prestage.depth
         self.staged: list[JobInProgress] = []
         self.kill_epoch = 0    # bumped when attempts may have become killable
+        # bumped when the cluster's slot capacity may have changed (a tracker
+        # joined / was lost / blacklisted, or reported other slot counts): the
+        # scheduler's capacity totals are recomputed only then, not per call
+        self.cap_epoch = 0
         self.prestage = conf.get_boolean("hbmr.job.prestage", True)
         self.prestage_depth = max(1, conf.get_int("hbmr.job.prestage.depth", 2))
         # trackers get their new work back in the report of a finished task
         # (TaskTracker.report_assign, the same cluster key)
         self.report_assign_expected = conf.get_boolean("hbmr.tracker.report.assign", True)
+        # a staged split job is placed on every tracker at once (maps + reduce
+        # gang member per tracker: HybridScheduler.plan_staged)
+        self.plan_staged = conf.get_boolean("hbmr.scheduler.plan.staged", True)
         self.trackers: dict[str, TrackerInfo] = {}
         self.attempt_index: dict[str, Attempt] = {}
         self.cost_model = CostModel(conf.get_float("hbmr.costmodel.ewma.alpha", 0.3))
@@ -656,6 +733,7 @@ class JobTracker:
         re-execute its completed maps whose output lived on it."""
         with self.lock:
             tr = self.trackers.pop(name, None)
+            self.cap_epoch += 1
             if tr is None:
                 return
             log.warning("tracker %s %s", name, why)
@@ -853,6 +931,9 @@ class JobTracker:
         w.staged_on = str(j.job_id)
         self.staged.append(w)
         self.history.log("JOB_STAGED", job=str(w.job_id), gate=str(j.job_id))
+        plan = getattr(self.scheduler, "plan_staged", None)
+        if plan is not None and self.plan_staged:
+            plan(w)
         # staged behind a job that is itself staged: its maps cannot run before
         # two reduces have completed, and every tracker of the gang reports
         # each completion (JobTracker.report assigns): no long-poll wake-up
@@ -1156,6 +1237,11 @@ class JobTracker:
                                  gpus=[g["device"] for g in st.gpus])
             tr.status = st
             tr.last_seen = now
+            cap = (st.max_cpu_map_slots, st.max_reduce_slots,
+                   tuple((g["device"], g["max_slots"]) for g in st.gpus))
+            if cap != tr.cap_sig:
+                tr.cap_sig = cap
+                self.cap_epoch += 1
             for k in st.cached_splits_added:
                 tr.cached.add(tuple(k))
             for k in st.cached_splits_removed:
@@ -1565,6 +1651,7 @@ class JobTracker:
                 tr.failures += 1
                 if tr.failures >= self.max_tracker_failures * 4 and len(self.trackers) > 1:
                     tr.blacklisted = True
+                    self.cap_epoch += 1
                     self.history.log("TRACKER_BLACKLISTED", tracker=tr.name)
         limit = jip.max_map_attempts if tip.is_map else jip.max_reduce_attempts
         if tip.failures >= limit:

@@ -169,9 +169,13 @@ class RemoteJobTracker:
 
     def __init__(self, conf):
         env = dict(os.environ, HBMR_JT_PROCESS="1")
+        # the package root on the child's path whatever the caller's cwd
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH")
+                                    else "")
         self.proc = subprocess.Popen([sys.executable, "-m", "hbmr.mapred.jtprocess"],
                                      stdin=subprocess.PIPE, stdout=subprocess.PIPE,
-                                     env=env, text=True)
+                                     env=env, text=True, cwd=root)
         self.proc.stdin.write(json.dumps(conf.to_dict()) + "\n")
         self.proc.stdin.flush()
         line = self.proc.stdout.readline()

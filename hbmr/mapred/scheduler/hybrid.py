@@ -71,6 +71,11 @@ class HybridTaskScheduler(TaskScheduler):
 
     # -- cluster capacity ----------------------------------------------------------------
     def _totals(self):
+        # cached until the cluster's capacity changes (JobTracker.cap_epoch):
+        # this ran on every assignment call, O(trackers) each
+        ep = getattr(self.jt, "cap_epoch", None)
+        if ep is not None and getattr(self, "_tot_epoch", None) == ep:
+            return self._tot
         cpu = gpu = ndev = 0
         for t in self.jt.trackers.values():
             if t.blacklisted:
@@ -79,6 +84,8 @@ class HybridTaskScheduler(TaskScheduler):
             gpu += sum(g["max_slots"] for g in t.status.gpus)
             ndev += len(t.status.gpus)
         self._devices = ndev
+        self._tot = (cpu, gpu)
+        self._tot_epoch = ep
         return cpu, gpu
 
     def _gpu_servers(self, jip, total_gpu):
@@ -201,6 +208,11 @@ class HybridTaskScheduler(TaskScheduler):
                 bulk = jip.split_job is not None   # split jobs: one bulk launch per device
                 for dev in sorted(gpu_free):
                     batch = []
+                    if bulk:
+                        # one obtain_maps call takes the device's share at once
+                        budget, glim = self._bulk_gpu(tr, jip, dev, gpu_free, reserve, budget,
+                                                      glim, now, actions)
+                        continue
                     # the min-makespan plan's later CPU waves stay pending: a deep GPU
                     # queue must not swallow them (they free the GPUs' tail)
                     while gpu_free[dev] > 0 and len(jip.pending_maps) > max(0, reserve) and \
@@ -250,11 +262,47 @@ class HybridTaskScheduler(TaskScheduler):
                 reduce_free = self._assign_reduces(tr, jip, reduce_free, actions)
         return actions
 
+    def _bulk_gpu(self, tr, jip, dev, gpu_free, reserve, budget, glim, now, actions):
+        """A split job's maps for one device in one bulk launch: as many as
+        the device's free queue, the plan's CPU reserve, the job's GPU limit
+        and the response budget allow, local levels first (delay scheduling:
+        a device waits up to locality_wait before it takes non-local splits)."""
+        want = min(gpu_free[dev], len(jip.pending_maps) - max(0, reserve), glim)
+        if want <= 0:
+            return budget, glim
+        if budget < want:
+            tr.more = True
+            want = budget
+            if want <= 0:
+                return budget, glim
+        key = (str(jip.job_id), tr.name, dev)
+        first = self._skips.get(key)
+        allow_nonlocal = self.policy == "stock" or (
+            first is not None and now - first >= self.locality_wait) or \
+            not jip.locality_possible()
+        got = jip.obtain_maps(tr, True, dev, want, allow_nonlocal=allow_nonlocal)
+        if any(lv < 3 for _t, lv in got):
+            self._skips.pop(key, None)
+        if len(got) < want and key not in self._skips:
+            self._skips[key] = now
+        n = len(got)
+        if n:
+            actions.append(self.jt.launch_gpu_batch(tr, [t for t, _lv in got], dev))
+            gpu_free[dev] -= n
+            self.decisions += n
+        return budget - n, glim - n
+
     def _assign_reduces(self, tr, jip, reduce_free, actions):
         jt = self.jt
         n_red = 0
         expect = jip.expect_mode and not jip.maps_complete()
-        for tip in jip.reduces:
+        if jip.collective_reduce and jip.reduce_by_tracker:
+            # a gang member per tracker: only this tracker's pinned reduce
+            mine = jip.reduce_by_tracker.get(tr.name)
+            tips = () if mine is None else (mine,)
+        else:
+            tips = jip.reduces
+        for tip in tips:
             if jip.collective_reduce and tip.pinned_tracker != tr.name:
                 continue
             if tip.is_complete() or tip.is_running():
@@ -274,6 +322,33 @@ class HybridTaskScheduler(TaskScheduler):
             reduce_free -= spt
         return reduce_free
 
+    def plan_staged(self, jip):
+        """Whole-job placement of a just-staged split job: every GPU tracker's
+        HBM-resident / node-local maps in one bulk launch per device, and —
+        once no map is left pending — each tracker's collective reduce member
+        (expect mode) in the same per-tracker record.  The records ride on
+        each tracker's next response (tr.extra_actions) instead of being
+        pulled one tracker heartbeat at a time, where a tracker whose maps
+        were staged before the job's last ones needed a heartbeat of its own
+        for its reduce.  What cannot be placed locally now stays pending for
+        the per-heartbeat path (_stage_maps / assign_tasks)."""
+        jt = self.jt
+        if not jip.gpu_capable or jip.staged_on is None:
+            return
+        depth = 1 if self.policy == "stock" else self.queue_depth
+        trackers = [t for _n, t in sorted(jt.trackers.items())
+                    if t.status.gpus and t.status.healthy and not t.blacklisted]
+        for tr in trackers:
+            acts = []
+            self._stage_maps(tr, jip, depth, acts)
+            tr.extra_actions += acts
+        if jip.pending_maps or not jip.reduces or not self._reduces_may_start(jip):
+            return
+        for tr in trackers:
+            acts = []
+            self._assign_reduces(tr, jip, tr.status.max_reduce_slots - tr.running_reduce, acts)
+            tr.extra_actions += acts
+
     def _stage_maps(self, tr, jip, depth, actions):
         """Launch a staged job's pending maps that are local to this tracker's
         GPUs (HBM-resident / node-local splits), gated on the job it waits for;
@@ -281,13 +356,8 @@ class HybridTaskScheduler(TaskScheduler):
         for g in tr.status.gpus:
             dev = g["device"]
             cap = g["max_slots"] * depth - jip.staged_launched.get((tr.name, dev), 0)
-            batch = []
-            while cap > 0 and jip.pending_maps:
-                got = jip.obtain_map(tr, True, dev, allow_nonlocal=False)
-                if got is None:
-                    break
-                batch.append(got[0])
-                cap -= 1
+            batch = [t for t, _lv in jip.obtain_maps(tr, True, dev, cap, allow_nonlocal=False)] \
+                if cap > 0 and jip.pending_maps else []
             if batch:
                 actions.append(self.jt.launch_gpu_batch(tr, batch, dev, gate=jip.staged_on))
 

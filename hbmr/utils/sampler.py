@@ -257,6 +257,7 @@ def dump_profiles(path):
     st.sort_stats("cumulative").print_stats(60)
     with open(f"{path}_{os.getpid()}.txt", "w") as f:
         f.write(buf.getvalue())
+    st.dump_stats(f"{path}_{os.getpid()}.prof")     # raw, for pstats diffs
 
 
 def maybe_start():

@@ -200,7 +200,8 @@ def test_requeued_maps_are_taken_first_at_local_levels():
     class Job:
         pass
 
-    for name in ("_index", "_by_location", "_rack_level", "obtain_map", "_take", "add_pending",
+    for name in ("_index", "_by_location", "_node_level", "_rack_level", "obtain_map", "_take",
+                 "add_pending",
                  "_count_locality"):
         setattr(Job, name, getattr(JobInProgress, name))
     job = Job()
