@@ -22,6 +22,7 @@ import traceback
 import torch
 
 from ..mapred import protocol as P
+from .busy import BusyTimeline, batch_interval
 from ..mapred.task import TaskReporter
 from ..utils.trace import TRACE
 
@@ -62,8 +63,7 @@ class _Device:
         # adds beyond the frontier, so overlapping slot streams are not
         # double-counted in the tasks' device time (the cost model's t_gpu)
         self.ref = None
-        self.busy_frontier = 0.0
-        self.busy_lock = threading.Lock()
+        self.busy = BusyTimeline()      # union of this device's charged batch intervals
 
 
 class _Batch(list):
@@ -419,7 +419,7 @@ class GpuRuntime:
                 by_job.setdefault(id(r.job), (r.job, []))[1].append((r.spec.attempt_id, out, evr))
             for js, items in by_job.values():
                 js.note_launched(items)
-            slot.done_q.put((live, ev0, ev1, outs, capped))
+            slot.done_q.put((live, ev0, ev1, outs, capped, list(waits.values())))
             return len(live)
         except BaseException as e:  # noqa: BLE001
             self._note_error(dev.index, e)
@@ -459,7 +459,7 @@ class GpuRuntime:
             item = slot.done_q.get()
             if item is None:
                 break
-            runs, ev0, ev1, outs, capped = item
+            runs, ev0, ev1, outs, capped, gates = item
             try:
                 if self.poll_s > 0:
                     while not ev1.query():
@@ -470,8 +470,9 @@ class GpuRuntime:
                     TRACE.instant("gpu.complete", n=len(runs), slot=slot.index)
                 # a batch completes together; the busy time it adds to the
                 # device (beyond what overlapping batches on the other slots
-                # already account for) is shared evenly by its tasks
-                dt = self._busy_ms(self.devices[slot.device.index], ev0, ev1) / 1000.0 / \
+                # already account for, from when its gates let it start) is
+                # shared evenly by its tasks
+                dt = self._busy_ms(self.devices[slot.device.index], ev0, ev1, gates) / 1000.0 / \
                     max(1, len(runs))
                 for r, out in zip(runs, outs):   # a batch may mix jobs
                     with r.job.lock:
@@ -498,19 +499,21 @@ class GpuRuntime:
                     self._release_capped(self.devices[slot.device.index], len(runs))
 
     @staticmethod
-    def _busy_ms(dev, ev0, ev1):
+    def _busy_ms(dev, ev0, ev1, gates=()):
+        """The device time a batch adds (hbmr/gpu/busy.py): its [start, end)
+        on the device clock — start no earlier than the gate events its
+        stream waited on — charged against the union of the device's batches."""
         elapsed = ev0.elapsed_time(ev1)
         if dev.ref is None:
             return elapsed
-        start = dev.ref.elapsed_time(ev0)
-        end = start + elapsed
-        with dev.busy_lock:
-            busy = max(0.0, end - max(start, dev.busy_frontier))
-            dev.busy_frontier = max(dev.busy_frontier, end)
-        # completers of the slot streams may process batches out of device
-        # order, and a batch that overlaps an already-charged one would be
-        # charged ~0; it shares the device with at most len(slots) streams
-        return max(busy, elapsed / max(1, len(dev.slots)))
+        gate_ms = []
+        for g in gates or ():
+            try:
+                gate_ms.append(dev.ref.elapsed_time(g))
+            except RuntimeError:        # an event without timing: start at ev0
+                pass
+        start, end = batch_interval(dev.ref.elapsed_time(ev0), elapsed, gate_ms)
+        return dev.busy.charge(start, end)
 
     # -- device health (NodeHealthChecker probes) --------------------------------------
     def _note_error(self, d, exc):

@@ -199,7 +199,9 @@ def run_split_reduce(host, run, device=None):
             ev = getattr(ctx, "sim_ready", None)   # simulated device: a ready time
             if cuda:
                 import torch
-                ev = torch.cuda.Event()
+                # timed: a staged batch's device time starts when this fires
+                # (hbmr/gpu/busy.py batch_interval), not at its stream's wait
+                ev = torch.cuda.Event(enable_timing=True)
                 ev.record()
             rt.open_gate(spec.job_id, ev, gate_epoch)
             if TRACE.on:

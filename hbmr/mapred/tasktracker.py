@@ -238,6 +238,10 @@ class TaskTracker:
         # round trip overlap another's device work (a lone child serialises
         # them: about 1.5 ms per map against ~50 us of GPU time)
         conc = max(1, conf.get_int("hbmr.gpu.pipes.concurrency", 2))
+        if conf.get_boolean("hbmr.pipes.gpu.mux", True):
+            # one shared child per device takes up to its queue depth of maps
+            # (hbmr/pipes/mux.py): a thread per map in flight
+            conc = max(conc, conf.get_int("hbmr.pipes.gpu.queue.depth", 8))
         self.gpu_pipes_pool = cf.ThreadPoolExecutor(
             max(1, len(self.gpu_devices) * max(1, self.gpu_slots_per_device) * conc),
             thread_name_prefix=f"{self.name}-gpupipes")

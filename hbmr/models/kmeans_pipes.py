@@ -80,23 +80,28 @@ def write_centroids(path, cen: torch.Tensor):
 
 
 def read_centroids(outdir, old: torch.Tensor) -> torch.Tensor:
-    new = old.detach().to("cpu", torch.float32).clone()
+    """The reducers' ``cluster \t c0,c1,...`` lines folded into the next
+    centroids (clusters without a line keep theirs).  One numpy parse of all
+    the values (the reducer prints %.9g: every fp32 round-trips exactly)."""
+    new = old.detach().to("cpu", torch.float32).numpy().copy()
+    keys, vals = [], []
     for fn in sorted(os.listdir(outdir)):
         if not fn.startswith("part-"):
             continue
         with open(os.path.join(outdir, fn)) as f:
             for line in f:
-                line = line.rstrip("\n")
-                if not line:
-                    continue
-                k, v = line.split("\t", 1)
-                new[int(k)] = torch.from_numpy(np.array([float(t) for t in v.split(",")],
-                                                        dtype=np.float32))
-    return new
+                k, sep, v = line.rstrip("\n").partition("\t")
+                if sep:
+                    keys.append(int(k))
+                    vals.append(v)
+    if keys:
+        arr = np.array(",".join(vals).split(","), dtype=np.float64).astype(np.float32)
+        new[np.asarray(keys)] = arr.reshape(len(keys), -1)
+    return torch.from_numpy(new)
 
 
 def iteration_conf(base, inp, out, cen_file, k, d, cpubin=None, gpubin=None, reduces=1,
-                   maps=None, reuse=True) -> JobConf:
+                   maps=None, reuse=True, exact=True) -> JobConf:
     from ..pipes import submitter
     job = JobConf(base)
     job.set_job_name(f"kmeans-pipes {os.path.basename(out)}")
@@ -108,6 +113,11 @@ def iteration_conf(base, inp, out, cen_file, k, d, cpubin=None, gpubin=None, red
     job.set_int("hbmr.kmeans.k", k)
     job.set_int("hbmr.kmeans.dims", d)
     job.set("hbmr.kmeans.centroids.file", os.path.abspath(cen_file))
+    # exact mode (hbmr.kmeans.exact): both binaries give the fp64 arg-min of the
+    # fp32 points and the fixed point of the fp32 rows — the same partials
+    # whichever slots ran a map, so a hybrid job's centroids do not depend on
+    # the placement (the bf16 GPU mode differs from the CPU binary on near-ties)
+    job.set_boolean("hbmr.kmeans.exact", exact)
     # keep the task binaries alive across tasks and iteration jobs: the GPU
     # binary keeps its HIP context and the HBM-resident splits
     job.set_boolean("hbmr.pipes.child.reuse", reuse)
@@ -126,10 +136,11 @@ class KMeansPipesDriver:
 
     def __init__(self, workdir, inp, k, d, init: torch.Tensor, base=None, cluster=None,
                  cpubin=os.path.join(BIN, "kmeans_cpu"), gpubin=os.path.join(BIN, "kmeans_gpu"),
-                 reduces=1, maps=None):
+                 reduces=1, maps=None, exact=True):
         self.workdir, self.inp, self.k, self.d = workdir, inp, k, d
         self.base, self.cluster = base, cluster
         self.cpubin, self.gpubin, self.reduces, self.maps = cpubin, gpubin, reduces, maps
+        self.exact = exact
         self.centroids = init.detach().to("cpu", torch.float32)
         self.iteration = 0
         self.history = []
@@ -142,7 +153,7 @@ class KMeansPipesDriver:
                                    self.centroids)
         out = os.path.join(self.workdir, f"iter-{i:03d}")
         job = iteration_conf(self.base, self.inp, out, cen_file, self.k, self.d, self.cpubin,
-                             self.gpubin, self.reduces, self.maps)
+                             self.gpubin, self.reduces, self.maps, exact=self.exact)
         from ..utils.trace import TRACE
         if TRACE.on:
             TRACE.instant("kmeans_pipes.submit")
@@ -176,10 +187,12 @@ def main(argv=None, cluster=None):
     ap.add_argument("--dims", type=int, default=128)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--reduces", type=int, default=1)
+    ap.add_argument("--exact", action=argparse.BooleanOptionalAction, default=True,
+                    help="fp64-exact labels on both binaries (default; --no-exact: bf16 GPU maps)")
     a = ap.parse_args(argv)
-    init = K.initial_centroids(a.input, a.k, a.dims)
+    init = K.initial_centroids(a.input, a.k, a.dims, exact=a.exact)
     drv = KMeansPipesDriver(a.workdir, a.input, a.k, a.dims, init, cluster=cluster,
-                            reduces=a.reduces)
+                            reduces=a.reduces, exact=a.exact)
     for _ in range(a.iters):
         r = drv.step()
         print(f"iteration {r['iteration']}: shift {r['shift']:.6f}")

@@ -127,7 +127,10 @@ class PipesMapRunner(MapRunnable):
 
 
 class PipesGPUMapRunner(PipesMapRunner):
-    """GPU attempt: the GPU executable, told which device the scheduler chose."""
+    """GPU attempt: the GPU executable, told which device the scheduler chose.
+    Child-read input (the common GPU shape: the binary loads its split) goes
+    to the device's shared child with several maps in flight (hbmr/pipes/
+    mux.py, ``hbmr.pipes.gpu.mux``); Java-fed input keeps a child per map."""
     run_on_gpu = True
 
     def executable(self):
@@ -135,6 +138,21 @@ class PipesGPUMapRunner(PipesMapRunner):
 
     def device(self):
         return self.job.get_int("hbmr.task.gpu.device", 0)
+
+    def run(self, reader, output, reporter):
+        from . import mux
+        job = self.job
+        if job.get_boolean(JAVA_RR, False) or not job.get_boolean(mux.MUX, True):
+            return super().run(reader, output, reporter)
+        part = getattr(output, "partitioner", None)
+        partitioner = part if isinstance(part, PipesPartitioner) else None
+        child = mux.REGISTRY.get(job, self.executable(), self.device(),
+                                 _work_dir(job, f"gpumux{self.device()}"),
+                                 job.get_int(mux.DEPTH, 8))
+        t = child.submit(job, output, reporter, job.get_map_output_key_class(),
+                         job.get_map_output_value_class(), partitioner, _split_bytes(reporter),
+                         job.get_num_reduce_tasks())
+        child.wait(t)
 
 
 class PipesReducer(Reducer):

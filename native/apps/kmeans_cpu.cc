@@ -1,6 +1,7 @@
 // K-Means Pipes CPU task binary (the CPU half of a hybrid K-Means job; see
-// kmeans_pipes.h).  The map runs the native multi-threaded fp32 assignment +
-// int64 fixed-point combiner of native/cpu/kmeans_cpu.cc over the whole split.
+// kmeans_pipes.h).  The map runs the native multi-threaded fp32 assignment
+// (exact mode: certified, uncertain points re-scored in fp64) + int64
+// fixed-point combiner of native/cpu/kmeans_cpu.cc over the whole split.
 #include <stdexcept>
 #include <thread>
 
@@ -15,7 +16,12 @@ class KMeansCpuMapper : public HadoopPipes::Mapper {
     const HadoopPipes::JobConf* conf = ctx.getJobConf();
     threads_ = conf->hasKey("hbmr.cpu.threads.per.slot") ? conf->getInt("hbmr.cpu.threads.per.slot")
                                                           : 1;
+    // exact mode (hbmr.kmeans.exact): fp32 scores certified against their
+    // error bound, uncertain points re-scored in fp64 — the fp64 arg-min the
+    // GPU binary's exact pipeline also gives, so both emit the same partials
+    exact_ = conf->hasKey("hbmr.kmeans.exact") && conf->getBoolean("hbmr.kmeans.exact");
     points_ = ctx.getCounter("KMEANS", "POINTS");
+    cpu_ = ctx.getCounter("KMEANS", "CPU_MAPS");
   }
   void map(HadoopPipes::MapContext& ctx) override {
     const std::string& v = ctx.getInputValue();
@@ -23,10 +29,13 @@ class KMeansCpuMapper : public HadoopPipes::Mapper {
     std::vector<int32_t> labels((size_t)n);
     std::vector<long long> sums((size_t)p_.k * p_.d, 0), counts((size_t)p_.k, 0);
     double cost = 0;
-    const int rc = hbmr_kmeans_map_cpu_f32(reinterpret_cast<const float*>(v.data()), n, p_.d,
-                                           cen_.data(), p_.k, labels.data(), sums.data(),
-                                           counts.data(), &cost, p_.fx, threads_);
-    if (rc) throw std::runtime_error("hbmr_kmeans_map_cpu_f32 failed");
+    long rescored = 0;
+    const int rc = hbmr_kmeans_map_cpu_f32_ex(reinterpret_cast<const float*>(v.data()), n, p_.d,
+                                              cen_.data(), p_.k, labels.data(), sums.data(),
+                                              counts.data(), &cost, p_.fx, threads_,
+                                              exact_ ? 1 : 0, &rescored);
+    if (rc) throw std::runtime_error("hbmr_kmeans_map_cpu_f32_ex failed");
+    ctx.incrementCounter(cpu_, 1);
     kmp::emit_partials(ctx, p_.k, p_.d, reinterpret_cast<const int64_t*>(sums.data()), p_.d,
                        reinterpret_cast<const int64_t*>(counts.data()));
     ctx.incrementCounter(points_, (uint64_t)n);
@@ -36,7 +45,9 @@ class KMeansCpuMapper : public HadoopPipes::Mapper {
   kmp::Params p_;
   std::vector<float> cen_;
   int threads_ = 1;
+  bool exact_ = false;
   HadoopPipes::TaskContext::Counter* points_;
+  HadoopPipes::TaskContext::Counter* cpu_;
 };
 
 int main(int argc, char** argv) {

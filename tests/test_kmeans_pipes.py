@@ -38,6 +38,67 @@ def _split_job_centroids(iters):
         return drv.centroids()
 
 
+def _exact_split_job_centroids(iters):
+    conf = JobConf()
+    conf.set_boolean(K.EXACT_KEY, True)
+    with LocalCluster(conf, num_trackers=1, cpu_slots=2) as cl:
+        drv = K.KMeansDriver(cl.submit_job, lambda rj: rj._impl.jip.result[0], conf=conf, k=KC,
+                             d=D, inp=f"synthetic:{N}:3", split_points=4000)
+        for _ in range(iters):
+            drv.step()
+        return drv.centroids()
+
+
+def _pipes_exact(tmp_path, name, conf, gpus, cpu_slots, files=6):
+    pts = tmp_path / "pts"
+    if not pts.exists():
+        KP.write_points(str(pts), N, D, seed=3, centers=KC, files=files, bf16_exact=False)
+    init = K.initial_centroids(f"synthetic:{N}:3", KC, D, exact=True)
+    with LocalCluster(conf, num_trackers=1, gpus=gpus, cpu_slots=cpu_slots,
+                      gpu_slots_per_device=1) as cl:
+        drv = KP.KMeansPipesDriver(str(tmp_path / name), str(pts), KC, D, init, cluster=cl,
+                                   reduces=1, gpubin=None if not gpus else KP.os.path.join(
+                                       KP.BIN, "kmeans_gpu"), exact=True)
+        cen = drv.run(3)
+    return cen, drv.history
+
+
+def test_pipes_kmeans_exact_cpu_binary_matches_exact_split_job(tmp_path):
+    """Exact mode (hbmr.kmeans.exact) through the CPU Pipes binary: the fp64
+    arg-min of the fp32 points and fixed-point sums of the fp32 rows — the
+    exact split job's centroids, bit for bit."""
+    cen, hist = _pipes_exact(tmp_path, "cpu", JobConf(), None, 2)
+    assert hist[-1]["counters"].get("KMEANS", "POINTS") == N
+    assert torch.equal(cen, _exact_split_job_centroids(3))
+
+
+@pytest.mark.gpu
+def test_pipes_kmeans_exact_gpu_and_hybrid_are_placement_independent(tmp_path):
+    """The GPU binary's exact mode (fp16 MFMA top-3 + certification + fp64
+    re-score, fp32 fixed-point sums) emits the CPU binary's partials: an
+    all-GPU job, a hybrid job whose maps ran on both kinds of slots, and the
+    exact split job give identical centroids.  The GPU maps of a device run
+    in one shared child with several maps in flight (hbmr/pipes/mux.py)."""
+    from hbmr.pipes import mux
+    ref = _exact_split_job_centroids(3)
+    mux.REGISTRY.close_all()
+    gpu, hg = _pipes_exact(tmp_path, "gpu", JobConf(), [[0]], 0)
+    assert torch.equal(gpu, ref)
+    assert all(h["counters"].get("KMEANS", "GPU_MAPS") == 6 for h in hg)
+    # the shared child kept every split resident after the first iteration
+    assert [h["counters"].get("KMEANS", "GPU_SPLIT_CACHE_HITS") for h in hg] == [0, 6, 6]
+    children = list(mux.REGISTRY._children.values())
+    assert len(children) == 1 and children[0].maps == 18
+    conf = JobConf()
+    conf.set("hbmr.scheduler.policy", "stock")     # CPU slots take maps too
+    hyb, hh = _pipes_exact(tmp_path, "hyb", conf, [[0]], 2)
+    cpu_maps = sum(h["counters"].get("KMEANS", "CPU_MAPS") for h in hh)
+    gpu_maps = sum(h["counters"].get("KMEANS", "GPU_MAPS") for h in hh)
+    assert cpu_maps > 0 and gpu_maps > 0 and cpu_maps + gpu_maps == 18
+    assert torch.equal(hyb, ref)
+    mux.REGISTRY.close_all()
+
+
 @pytest.mark.parametrize("compression", ["NONE", "RECORD", "BLOCK"])
 def test_pipes_kmeans_cpu_binary_matches_split_job(tmp_path, compression):
     KP.write_points(str(tmp_path / "pts"), N, D, seed=3, centers=KC, files=2,
@@ -45,7 +106,7 @@ def test_pipes_kmeans_cpu_binary_matches_split_job(tmp_path, compression):
     init = K.initial_centroids(f"synthetic:{N}:3", KC, D)
     with LocalCluster(JobConf(), num_trackers=2, cpu_slots=2) as cl:
         drv = KP.KMeansPipesDriver(str(tmp_path / "work"), str(tmp_path / "pts"), KC, D, init,
-                                   cluster=cl, gpubin=None, reduces=2)
+                                   cluster=cl, gpubin=None, reduces=2, exact=False)
         cen = drv.run(3)
     cs = drv.history[-1]["counters"]
     assert cs.get("KMEANS", "POINTS") == N
@@ -59,7 +120,7 @@ def test_pipes_kmeans_gpu_binary_on_gpu_slots(tmp_path):
     with LocalCluster(JobConf(), num_trackers=1, gpus=[[0]], cpu_slots=0,
                       gpu_slots_per_device=1) as cl:
         drv = KP.KMeansPipesDriver(str(tmp_path / "work"), str(tmp_path / "pts"), KC, D, init,
-                                   cluster=cl, reduces=1)
+                                   cluster=cl, reduces=1, exact=False)
         cen = drv.run(3)
     cs = drv.history[-1]["counters"]
     assert cs.get("org.apache.hadoop.mapred.JobInProgress$Counter", "GPU_MAP_TASKS") == 3
@@ -143,10 +204,11 @@ def test_gpu_pipes_binary_is_reused_and_keeps_splits_in_hbm(tmp_path):
     # so every-split hit counts are exact only here
     conf = JobConf()
     conf.set_int("hbmr.gpu.pipes.concurrency", 1)
+    conf.set_boolean("hbmr.pipes.gpu.mux", False)       # the per-map child pool path
     with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=0,
                       gpu_slots_per_device=1) as cl:
         drv = KP.KMeansPipesDriver(str(tmp_path / "work"), str(tmp_path / "pts"), KC, D, init,
-                                   cluster=cl, reduces=1)
+                                   cluster=cl, reduces=1, exact=False)
         drv.run(3)
         assert POOL.size() >= 1             # the children wait for the next job
     hits = [h["counters"].get("KMEANS", "GPU_SPLIT_CACHE_HITS") for h in drv.history]

@@ -150,7 +150,8 @@ def kmeans_pipes(a):
         init = K.initial_centroids(os.path.join(tmp, "pts"), a.k, a.dims)
         res = {"config": f"K-Means {a.points} pts x {a.dims}-d, k={a.k}, 1 GPU map slot via "
                          f"HIP Pipes (BASELINE config 2)", "points": a.points, "dims": a.dims,
-               "k": a.k, "map_tasks": a.files, "write_input_s": round(t_write, 2)}
+               "k": a.k, "map_tasks": a.files, "write_input_s": round(t_write, 2),
+               "exact": a.exact}
         gpu = torch.cuda.is_available()
         conf = JobConf()
         with LocalCluster(conf, num_trackers=1, gpus=[[0]] if gpu else None,
@@ -158,7 +159,7 @@ def kmeans_pipes(a):
             drv = KP.KMeansPipesDriver(os.path.join(tmp, "work"), os.path.join(tmp, "pts"),
                                        a.k, a.dims, init, cluster=cl,
                                        gpubin=KP.os.path.join(KP.BIN, "kmeans_gpu") if gpu
-                                       else None, maps=a.files)
+                                       else None, maps=a.files, exact=a.exact)
             times = []
             for _ in range(a.steps):
                 t = time.perf_counter()
@@ -253,6 +254,8 @@ def main():
     ap.add_argument("--lines", type=int, default=100)
     ap.add_argument("--procs", type=int, default=1, help="wordcount: parallel map processes")
     ap.add_argument("--cpu-slots", type=int, default=0)
+    ap.add_argument("--exact", action=argparse.BooleanOptionalAction, default=True,
+                    help="kmeans-pipes: fp64-exact labels on both binaries (hbmr.kmeans.exact)")
     a = ap.parse_args()
     {"wordcount": wordcount, "wordcount-gpu": wordcount_gpu, "kmeans-pipes": kmeans_pipes,
      "mrbench": mrbench}[a.which](a)
