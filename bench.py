@@ -283,9 +283,12 @@ def main():
             round(jt_cpu / a.steps * 1e3, 3),
             "final_shift": hist[-1].get("shift") if hist else None,
             "maps_per_tracker_last_job": hist[-1].get("maps_per_tracker") if hist else None,
-            # per job signature: completed-task mean seconds on each slot type and the
+            # per job signature: completed-task mean seconds on each slot type (over
+            # every job, warm-up included), the live estimate the scheduler uses
+            # (EWMA of the device time each batch adds, hbmr/gpu/busy.py) and the
             # number of tasks behind it (the CPU probe may still be running)
-            "cost_model": {k: {s: {"mean_s": round(v["mean"], 6), "n": v["n"],
+            "cost_model": {k: {s: {"mean_s": round(v["mean"], 6),
+                                   "estimate_s": round(v["ewma"], 6), "n": v["n"],
                                    "running": v["running"]} for s, v in d.items()}
                            for k, d in cm.items()},
             "baseline_note": "BASELINE.md publishes only a ratio (hybrid 1.93x faster than stock "
