@@ -315,8 +315,7 @@ class WordCountSplitJob(SplitJob):
         from ..mapred import counters as C
         from ..ops import text
         blob, counts, part_bytes, part_words = combined
-        rblob, _ = ctx.comm.all_to_all_v(blob, part_bytes)
-        rcounts, _ = ctx.comm.all_to_all_v(counts, part_words)
+        rblob, rcounts = self._shuffle(ctx, blob, counts, part_bytes, part_words)
         mblob, mcounts, _, _ = text.merge_tables(rblob, rcounts, 1)
         items = text.sorted_items(mblob, mcounts)
         total = sum(n for _, n in items)
@@ -331,6 +330,33 @@ class WordCountSplitJob(SplitJob):
                 f.write(b"".join(w + b"\t" + str(n).encode() + b"\n" for w, n in items))
             os.replace(os.path.join(tmp, name), os.path.join(self.out, name))
         return {"distinct": len(items), "words": total}
+
+    @staticmethod
+    def _shuffle(ctx, blob, counts, part_bytes, part_words):
+        """The word tables' shuffle: two static-shape all-to-alls (bytes, then
+        counts) whose slot sizes every rank agrees on through a HOST all-reduce
+        of the largest per-destination sizes (the sizes are host values
+        already: merge_tables returns them), so no collective here waits for
+        the device; the one host read is the compaction after both exchanges
+        are enqueued.  An overflowing slot (impossible with exact maxima, kept
+        as a guard) falls back to all_to_all_v."""
+        import torch
+
+        from ..parallel.collectives import compact_static
+        comm = ctx.comm
+        W = comm.world_size
+        if W <= 1 or not hasattr(comm, "all_to_all_v_static"):
+            return comm.all_to_all_v(blob, part_bytes)[0], comm.all_to_all_v(counts, part_words)[0]
+        mx = torch.tensor([max(part_bytes or [0]), max(part_words or [0])], dtype=torch.int64)
+        mx = comm.all_reduce_max(mx) if hasattr(comm, "all_reduce_max") else mx
+        cap_b, cap_w = max(1, int(mx[0])), max(1, int(mx[1]))
+        rb, rcb = comm.all_to_all_v_static(blob, part_bytes, cap_b)
+        rc, rcw = comm.all_to_all_v_static(counts, part_words, cap_w)
+        got_b = compact_static(rb, rcb, cap_b)
+        got_w = compact_static(rc, rcw, cap_w)
+        if got_b is None or got_w is None:
+            return comm.all_to_all_v(blob, part_bytes)[0], comm.all_to_all_v(counts, part_words)[0]
+        return got_b[0], got_w[0]
 
     def job_succeeded(self, jip):
         import os

@@ -61,6 +61,43 @@ class Comm:
         ins = self.all_to_all(outs)
         return (torch.cat(ins) if ins else send[:0]), [int(t.shape[0]) for t in ins]
 
+    def all_reduce_max(self, t: torch.Tensor) -> torch.Tensor:
+        """Element-wise maximum over ranks of a small tensor (host tensors go
+        over the host group: a shape agreement that never waits for a device)."""
+        if self.world_size <= 1:
+            return t
+        return torch.stack([x.to(t.device) for x in self.all_gather(t)]).amax(0)
+
+    def all_to_all_v_static(self, send: torch.Tensor, counts: list, cap: int):
+        """Variable all-to-all with static shapes: rows [sum(counts[:j]),
+        +counts[j]) of ``send`` go to rank j through a slot of ``cap`` rows
+        (the same ``cap`` on every rank).  Returns (recv, rcounts): the W
+        received slots ``[W * cap, ...]`` ordered by source and their valid
+        row counts as a DEVICE tensor — no size exchange is read on the host,
+        so nothing here waits for the device (TorchComm.all_to_all_v reads
+        the incoming sizes before it can allocate).  A count above ``cap`` is
+        truncated in the slot and shows as rcounts > cap: the caller checks
+        when it next reads host data (:func:`compact_static`) and re-runs the
+        exchange with all_to_all_v."""
+        self._note("all_to_all_v_static", send)
+        W = self.world_size
+        cap = max(1, int(cap))
+        rest = tuple(send.shape[1:])
+        slots = send.new_zeros((W * cap,) + rest)
+        off = 0
+        for j, c in enumerate(counts):
+            c = int(c)
+            n = min(c, cap)
+            if n:
+                slots[j * cap:j * cap + n] = send[off:off + n]
+            off += c
+        ct = torch.tensor([int(c) for c in counts], dtype=torch.int64)
+        if send.device.type != "cpu":
+            ct = ct.pin_memory().to(send.device, non_blocking=True)
+        recv = self.all_to_all_fixed(slots)
+        rc = self.all_to_all_fixed(ct)
+        return recv, rc
+
     def all_to_all_fixed(self, send: torch.Tensor) -> torch.Tensor:
         """Static-shape all-to-all: ``send`` is W equal slots along dim 0, slot j
         goes to rank j; returns the W slots received, ordered by source.  No
@@ -230,6 +267,8 @@ class TorchComm(Comm):
         sizes = torch.tensor([o.shape[0] for o in outs], dtype=torch.int64, device=dev)
         in_sizes = torch.empty_like(sizes)
         self.dist.all_to_all_single(in_sizes, sizes, group=self._grp(outs[0]))
+        if self.stats is not None:
+            self.stats["ALL_TO_ALL_HOST_READS"] += dev.type != "cpu"
         ins = [torch.empty((int(n),) + tuple(outs[0].shape[1:]), dtype=outs[0].dtype, device=dev)
                for n in in_sizes.tolist()]
         self.dist.all_to_all(ins, [o.contiguous() for o in outs], group=self._grp(outs[0]))
@@ -256,6 +295,8 @@ class TorchComm(Comm):
         sc = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=dev)
         rc = torch.empty_like(sc)
         self.dist.all_to_all_single(rc, sc, group=group)
+        if self.stats is not None:
+            self.stats["ALL_TO_ALL_V_HOST_READS"] += dev.type != "cpu"
         rcounts = [int(x) for x in rc.tolist()]
         recv = torch.empty((sum(rcounts),) + tuple(send.shape[1:]), dtype=send.dtype, device=dev)
         self.dist.all_to_all_single(recv, send.contiguous(), output_split_sizes=rcounts,
@@ -300,3 +341,15 @@ class TorchComm(Comm):
         self.dist.reduce_scatter_tensor(out, t.contiguous(), group=self._grp(t))
         lo = self.rank * per
         return out[:max(0, min(per, n - lo))]
+
+
+def compact_static(recv: torch.Tensor, rcounts: torch.Tensor, cap: int):
+    """The valid rows of all_to_all_v_static's slots, back to back by source,
+    and their counts (a host list) — the one host read of the exchange.
+    Returns None when a slot overflowed (a count above ``cap``): re-run the
+    exchange with all_to_all_v."""
+    rc = [int(x) for x in rcounts.tolist()]
+    if any(c > cap for c in rc):
+        return None
+    parts = [recv[j * cap:j * cap + c] for j, c in enumerate(rc)]
+    return (torch.cat(parts) if parts else recv[:0]), rc
