@@ -1887,6 +1887,12 @@ class JobTracker:
         jip = self.check_access(jid, "view")
         return jip.done.wait(max(0.0, min(float(timeout), 60.0)))
 
+    def rpc_wait_job_info(self, jid, timeout=30.0):
+        """rpc_wait_job and rpc_job_info in one call: the job's information
+        once it is complete, None if ``timeout`` passed first (a driver waiting
+        for each iteration job spends one RPC on it, not two)."""
+        return self.rpc_job_info(jid) if self.rpc_wait_job(jid, timeout) else None
+
     def rpc_job_info(self, jid):
         """Everything a driver reads about a job, in one call: status,
         counters, the phase timeline, maps per tracker and the reduce result."""

@@ -113,8 +113,9 @@ class _ProcJobHandle:
         self.jid = jid
         self._info = None
 
-    def _fetch(self):
-        info = self.rpc.call("rpc_job_info", self.jid)
+    def _fetch(self, info=None):
+        if info is None:
+            info = self.rpc.call("rpc_job_info", self.jid)
         st = JobStatus(self.jid, info["state"])
         for k in ("map_progress", "reduce_progress", "start_time", "finish_time",
                   "failure_info"):
@@ -138,8 +139,9 @@ class _ProcJobHandle:
         deadline = None if timeout is None else time.time() + timeout
         while True:
             left = 60.0 if deadline is None else max(0.0, deadline - time.time())
-            if self.rpc.call("rpc_wait_job", self.jid, min(left, 60.0)):
-                self._fetch()
+            info = self.rpc.call("rpc_wait_job_info", self.jid, min(left, 60.0))
+            if info is not None:
+                self._fetch(info)
                 return True
             if deadline is not None and time.time() >= deadline:
                 return False

@@ -21,7 +21,9 @@ from __future__ import annotations
 
 import contextlib
 import hmac
+import json
 import logging
+import os
 import secrets as _secrets
 import socket
 import socketserver
@@ -37,7 +39,31 @@ _LEN = struct.Struct(">I")
 
 # per-method (calls, seconds in the handler incl. the reply) of this process's
 # RPC servers; on with HBMR_SAMPLE_PROF (reported by hbmr.utils.sampler)
-RPC_STATS: dict | None = {} if __import__("os").environ.get("HBMR_SAMPLE_PROF") else None
+# HBMR_RPC_TRACE=prefix: one JSON line per served call (time, method, the
+# tracker, its reports and bulk completions, the kinds of action returned) in
+# prefix_<pid>.jsonl — the control plane's message flow, call by call
+_TR = (open(f"{os.environ['HBMR_RPC_TRACE']}_{os.getpid()}.jsonl", "w", buffering=1)
+       if os.environ.get("HBMR_RPC_TRACE") else None)
+
+
+def _trace(m, req, res):
+    args = req.get("a") or [None]
+    st = args[0]
+    info = {}
+    if isinstance(st, dict) and "tracker_name" in st:
+        info = {"tracker": st["tracker_name"], "kw": req.get("k", {}),
+                "reports": [[r.get("attempt_id"), r.get("state")]
+                            for r in st.get("task_reports") or ()],
+                "bulk": [len(b["attempts"]) for b in st.get("bulk_reports") or ()]}
+    elif args[0] is not None:
+        info = {"args": [a for a in args if isinstance(a, (str, int, float, bool))]}
+    if isinstance(res, dict) and "actions" in res:
+        info["actions"] = [[x.get("type"), x.get("job_id") or
+                            (x.get("task") or {}).get("attempt_id")] for x in res["actions"]]
+    _TR.write(json.dumps([round(time.time(), 5), m, info]) + "\n")
+
+
+RPC_STATS: dict | None = {} if os.environ.get("HBMR_SAMPLE_PROF") else None
 
 
 def _send(sock, obj):
@@ -125,7 +151,13 @@ class RpcServer:
                             res = getattr(outer.target, m)(*req.get("a", ()),
                                                            **req.get("k", {}))
                         _send(s, {"r": res})
+                        if _TR is not None:
+                            _trace(m, req, res)
                         if RPC_STATS is not None:
+                            if isinstance(res, dict) and "actions" in res:
+                                # heartbeat / report: by the kinds of action returned
+                                m = m + ":" + ("+".join(sorted({a.get("type", "?") for a in
+                                                                res["actions"]})) or "-")
                             st = RPC_STATS.setdefault(m, [0, 0.0])
                             st[0] += 1
                             st[1] += time.perf_counter() - t0
@@ -230,7 +262,8 @@ class RpcClient:
 
 JT_METHODS = ("heartbeat", "wakeup", "report", "resend", "map_completion_events", "rpc_submit_job",
               "rpc_job_status", "rpc_kill_job", "rpc_job_result", "rpc_cluster_status",
-              "rpc_list_jobs", "rpc_task_reports", "rpc_wait_job", "rpc_job_info")
+              "rpc_list_jobs", "rpc_task_reports", "rpc_wait_job", "rpc_job_info",
+              "rpc_wait_job_info")
 # served by a JobTracker process to the node that started it (hbmr/mapred/jtprocess.py)
 JT_PROCESS_METHODS = JT_METHODS + ("rpc_wait_for_trackers", "rpc_start_expiry",
                                    "rpc_broadcast_shutdown", "rpc_live_trackers",

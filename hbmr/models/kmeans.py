@@ -1048,11 +1048,15 @@ class KMeansDriver:
         if not self._manifest_written:
             self._write_manifest()
         t0 = time.time()
-        rj = self._ahead.pop(0) if self._ahead else self.submit(self._job_conf(i))
+        ahead = bool(self._ahead)
+        rj = self._ahead.pop(0) if ahead else self.submit(self._job_conf(i))
         depth = int(prefetch)
+        # a job submitted ahead is staged and launched already: the next one
+        # goes in at once (a wait here, as long as a whole job at 8 GPUs, let
+        # the chain drain); a job submitted just now gets its own launch under
+        # way first, the next one's submission not in its path
         if depth > 0 and len(self._ahead) < depth and \
-                not rj.waitForCompletion(self.prefetch_delay):
-            # submitted once this job's own launch is under way, not in its path
+                (ahead or not rj.waitForCompletion(self.prefetch_delay)):
             last = self._ahead[-1] if self._ahead else rj
             while len(self._ahead) < depth:
                 nxt = self.submit(self._job_conf(i + 1 + len(self._ahead),
