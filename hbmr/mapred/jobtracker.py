@@ -23,6 +23,7 @@ import itertools
 import json
 import logging
 import math
+import operator
 import os
 import shutil
 import threading
@@ -101,32 +102,36 @@ class TrackerInfo:
         return 0
 
 
-class Attempt:
-    __slots__ = ("aid", "tip", "tracker", "run_on_gpu", "device", "state", "progress",
-                 "start", "finish", "counters", "output", "diagnostic", "speculative",
-                 "device_time", "_released", "profile_only", "profile_fraction", "slots",
-                 "gated")
+_PARTITION = operator.attrgetter("partition")
 
-    def __init__(self, aid, tip, tracker, run_on_gpu, device, speculative=False):
+
+class Attempt:
+    """One attempt of a TIP.  The fields most attempts never change are class
+    defaults (an instance sets only its own): a bulk launch builds one per map
+    of every job on the JobTracker's critical path."""
+    progress = 0.0
+    finish = 0.0
+    counters: dict = {}          # replaced (never mutated) when a report carries them
+    output: dict = {}
+    diagnostic = ""
+    speculative = False
+    device_time = 0.0
+    _released = False
+    profile_only = False         # a CPU profiling probe left running after its TIP won
+    profile_fraction = 0.0       # >0: sampled probe, timed on this fraction of a split
+    slots = 1                    # CPU / reduce slots held (memory matching)
+    gated = False                # launched staged, behind another job's reduce
+    state = P.RUNNING
+
+    def __init__(self, aid, tip, tracker, run_on_gpu, device, speculative=False, start=None):
         self.aid = aid
         self.tip = tip
         self.tracker = tracker
         self.run_on_gpu = run_on_gpu
         self.device = device
-        self.state = P.RUNNING
-        self.progress = 0.0
-        self.start = time.time()
-        self.finish = 0.0
-        self.counters = {}
-        self.output = {}
-        self.diagnostic = ""
-        self.speculative = speculative
-        self.device_time = 0.0
-        self._released = False
-        self.slots = 1              # CPU / reduce slots held (memory matching)
-        self.profile_only = False   # a CPU profiling probe left running after its TIP won
-        self.profile_fraction = 0.0  # >0: sampled probe, timed on this fraction of a split
-        self.gated = False          # launched staged, behind another job's reduce
+        if speculative:
+            self.speculative = True
+        self.start = time.time() if start is None else start
 
 
 class TaskInProgress:
@@ -224,7 +229,6 @@ class JobInProgress:
         # notified when completion events are added or the job ends: reduces
         # long-poll map_completion_events on it instead of sleeping
         self.events_cond = threading.Condition(threading.Lock())
-        self.map_index: dict[str, TaskInProgress] = {}
         self.pending_maps: dict = {}   # TIP -> None: not yet started, insertion (FIFO) order
         self.by_split_key: dict = {}
         self.signature = conf.get("hbmr.job.signature") or self._signature(conf)
@@ -251,6 +255,8 @@ class JobInProgress:
         self.loc_counts = [0, 0, 0]     # HBM-local, data-local, rack-local maps
         self.pending_finish = False
         self.expect_mode = False
+        self.probe_aids: list = []      # sampled CPU probes (attempts of no TIP)
+        self.retired = None             # its summary once its task state is dropped
 
     @staticmethod
     def _signature(conf):
@@ -275,7 +281,9 @@ class JobInProgress:
             from ..gpu.splitjob import SplitJob
             if type(self.split_job).map_gpu is not SplitJob.map_gpu:
                 self.gpu_capable = True   # the split job has a device map
-            split_dicts = [s.to_dict() for s in splits]
+            # a split list memoised across iteration jobs keeps its dicts too
+            split_dicts = [s.__dict__.get("_wire") or s.__dict__.setdefault("_wire", s.to_dict())
+                           for s in splits]
         else:
             # job setup (the reference's setup task: FileOutputCommitter.setupJob)
             self.committer().setup_job(conf)
@@ -285,13 +293,12 @@ class JobInProgress:
                             "data": s.serialize().hex(),
                             "locations": list(s.getLocations() or []),
                             "length": s.getLength()} for s in splits]
-        for i, sd in enumerate(split_dicts):
-            tip = TaskInProgress(self, TaskID(self.job_id, True, i), split=sd, partition=i)
-            self.maps.append(tip)
-            self.map_index[str(tip.tid)] = tip
-            self.pending_maps[tip] = None
-            if sd.get("key"):
-                self.by_split_key[sd["key"]] = tip
+        jid = self.job_id
+        maps = self.maps = [TaskInProgress(self, TaskID(jid, True, i), split=sd, partition=i)
+                            for i, sd in enumerate(split_dicts)]
+        self.pending_maps = dict.fromkeys(maps)
+        self.by_split_key = {sd["key"]: tip for tip, sd in zip(maps, split_dicts)
+                             if sd.get("key")}
         if self.collective_reduce and self.split_job is not None:
             # one pinned reduce per tracker: the collective (RCCL) reduce gang
             nred = len(trackers) if getattr(self.split_job, "needs_reduce", True) else 0
@@ -381,8 +388,9 @@ class JobInProgress:
             # (failed / lost outputs, add_pending(front=True)) first, newest
             # first, then map index order (findNewMapTask takes failed maps first)
             front = self._front
-            order = lambda lv: sorted(lv, key=lambda t: front.get(t, t.partition),  # noqa: E731
-                                      reverse=True)
+            order = (lambda lv: sorted(lv, key=_PARTITION, reverse=True)) if not front else \
+                (lambda lv: sorted(lv, key=lambda t: front.get(t, t.partition),  # noqa: E731
+                                   reverse=True))
             # level 2 (node-local by split location) is built on first use: on
             # one host every split names this node, so building it eagerly
             # visited every map of the job per (tracker, device) even when the
@@ -403,7 +411,8 @@ class JobInProgress:
                         lv2.append(tip)
                         seen.add(tip)
             front = self._front
-            idx[2] = sorted(lv2, key=lambda t: front.get(t, t.partition), reverse=True)
+            idx[2] = sorted(lv2, key=(lambda t: front.get(t, t.partition)) if front else _PARTITION,
+                            reverse=True)
         return idx[2]
 
     def _by_location(self):
@@ -555,6 +564,35 @@ class JobInProgress:
     def completed(self):
         return self.status.is_complete()
 
+    def maps_per_tracker(self) -> dict:
+        """Succeeded maps per tracker (kept past retirement)."""
+        if self.retired is not None:
+            return dict(self.retired["maps_per_tracker"])
+        per = {}
+        for t in self.maps:
+            if t.successful is not None:
+                per[t.successful.tracker] = per.get(t.successful.tracker, 0) + 1
+        return per
+
+    def retire(self):
+        """Drop a completed job's task state (JobTracker._retire_jobs); its
+        attempt ids go to ``retired_aids`` for the JobTracker's index."""
+        if self.retired is not None:
+            return
+        self.retired = {"maps_per_tracker": self.maps_per_tracker(),
+                        "maps": len(self.maps), "reduces": len(self.reduces)}
+        aids = list(self.probe_aids)
+        for tip in self.maps:
+            aids.extend(tip.attempts)
+        for tip in self.reduces:
+            aids.extend(tip.attempts)
+        self.retired_aids = aids
+        self.maps, self.reduces = [], []
+        self.pending_maps, self.by_split_key, self.reduce_by_tracker = {}, {}, {}
+        self.completion_events, self.launched_on, self._loc_index = [], {}, {}
+        self.staged_launched, self._front, self.probe_aids = {}, {}, []
+        self.__dict__.pop("_byloc", None)
+
     def timeline(self) -> dict:
         """Phase breakdown in seconds (submit → first map launch → last map done
         → first reduce launch → finish); a dependent job counts from its release."""
@@ -658,6 +696,18 @@ class JobTracker:
         self._expire_thread = None
         self._stop = threading.Event()
         self.listeners = []
+        # job retirement (JobTracker.RetireJobs, mapred.jobtracker.completeuserjobs
+        # .maximum): the newest completed jobs keep their task state; older ones
+        # drop it (TIPs, attempts, completion events: a long K-Means run adds
+        # ~1,500 objects per iteration job that every full collection would
+        # walk and every attempt lookup would index), keeping status, counters,
+        # result and a per-tracker map summary; beyond hbmr.jobtracker.retired
+        # .jobs.maximum they are forgotten
+        self.keep_completed = max(1, conf.get_int("mapred.jobtracker.completeuserjobs.maximum",
+                                                  100))
+        self.keep_retired = max(0, conf.get_int("hbmr.jobtracker.retired.jobs.maximum", 1000))
+        self._completed: collections.deque = collections.deque()
+        self._retired: collections.deque = collections.deque()
         self.start_time = time.time()
         self.system_dir = conf.get("mapred.system.dir")
         # job files exist for restart recovery only: without it a submit does
@@ -980,7 +1030,10 @@ class JobTracker:
     def _finish_job(self, jip: JobInProgress, state, info=""):
         if jip.completed():
             return
-        self.kill_epoch += 1          # its attempts still running anywhere get killed
+        if jip.running_cpu or jip.running_gpu or any(r.is_running() for r in jip.reduces):
+            # its attempts still running anywhere get killed (a job that
+            # succeeded has none: no tracker need scan its running attempts)
+            self.kill_epoch += 1
         st = jip.status
         st.state = state
         st.failure_info = info
@@ -1059,6 +1112,21 @@ class JobTracker:
             self._kick()
         for cb in self.listeners:
             cb("finished", jip)
+        self._retire_jobs(jip)
+
+    def _retire_jobs(self, jip):
+        self._completed.append(jip)
+        while len(self._completed) > self.keep_completed:
+            old = self._completed.popleft()
+            old.retire()
+            index = self.attempt_index
+            for aid in old.retired_aids:
+                index.pop(aid, None)
+            old.retired_aids = ()
+            self._retired.append(str(old.job_id))
+            self.history.log("JOB_RETIRED", job=str(old.job_id))
+        while len(self._retired) > self.keep_retired:
+            self.jobs.pop(self._retired.popleft(), None)
 
     def _assignable(self) -> bool:
         """Work a long-polling tracker could be handed now: a queued job with
@@ -1441,57 +1509,68 @@ class JobTracker:
         succeeded = P.SUCCEEDED
         running = tr.running
         running_gpu = tr.running_gpu
+        # per attempt only what is its own; the counts (job, tracker, device,
+        # staged budget) are folded once per batch below
+        jp = dev = ev = None
+        ungated = gated = 0
         for aid in aids:
             a = index.get(aid)
             if a is None or a.state in terminal:
                 continue
             tip = a.tip
             if a.profile_fraction or tip.successful is not None or tip.killed or \
-                    len(tip.attempts) > 1:
-                odd.append(a)        # speculative twins etc.: the general path
+                    len(tip.attempts) > 1 or \
+                    (jp is not None and (tip.job is not jp or a.device != dev)):
+                # speculative twins etc. (and anything not of the batch's job
+                # and device): the general path
+                odd.append(a)
                 continue
+            if jp is None:
+                jp, dev = tip.job, a.device
+                ev = jp.completion_events
             a.progress = 1.0
             a.finish = fin
             a.output = out
             a.device_time = dt
             a.state = succeeded
-            jp = tip.job
             if not a._released:
                 a._released = True
-                if a.gated:
-                    key = (a.tracker, a.device)
-                    jp.staged_launched[key] = max(0, jp.staged_launched.get(key, 1) - 1)
-                jp.running_gpu = max(0, jp.running_gpu - 1)
                 running.discard(aid)
-                running_gpu[a.device] = max(0, running_gpu.get(a.device, 1) - 1)
+                if a.gated:
+                    gated += 1
+                else:
+                    ungated += 1
             tip.successful = a
-            jp.maps_done += 1
-            jp.finished_gpu_maps += 1
             # (map id, attempt, output): map_completion_events renders them
-            jp.completion_events.append((tip.tid, aid, out))
+            ev.append((tip.tid, aid, out))
             done.append(a)
         if done:
-            jip = done[0].tip.job
-            for jp in {a.tip.job for a in done}:
-                with jp.events_cond:
-                    jp.events_cond.notify_all()
             n = len(done)
+            rel = gated + ungated
+            if gated:
+                key = (tr.name, dev)
+                jp.staged_launched[key] = max(0, jp.staged_launched.get(key, gated) - gated)
+            jp.running_gpu = max(0, jp.running_gpu - rel)
+            running_gpu[dev] = max(0, running_gpu.get(dev, rel) - rel)
+            jp.maps_done += n
+            jp.finished_gpu_maps += n
+            jip = jp
+            with jp.events_cond:
+                jp.events_cond.notify_all()
             done_ids = [a.aid for a in done]
             self.cost_model.tasks_finished(jip.signature, done_ids, True, dt)
             if rep.get("counters"):
                 jip.add_counters(rep["counters"])
             self.history.log("TASKS_FINISHED", attempts=done_ids, tracker=tr.name,
-                             gpu=True, device=done[0].device, finish=fin, device_time=dt)
+                             gpu=True, device=dev, finish=fin, device_time=dt)
             METRICS.inc("hbmr_tasks_succeeded_total", n, help="successful task attempts",
                         type="map", where="gpu")
-            jobs = {a.tip.job for a in done}
-            for jp in jobs:
-                self._update_progress(jp)
-                if jp.maps_complete():
-                    jp.t_maps_done = time.time()
-                self._check_job_done(jp)
-                if jp.reduces and jp.maps_complete() and self._reduces_waiting(jp):
-                    self._kick()
+            self._update_progress(jp)
+            if jp.maps_complete():
+                jp.t_maps_done = time.time()
+            self._check_job_done(jp)
+            if jp.reduces and jp.maps_complete() and self._reduces_waiting(jp):
+                self._kick()
         for a in odd:
             self._update_task_status(tr, P.TaskStatus(
                 attempt_id=a.aid, is_map=True, state=P.SUCCEEDED, progress=1.0,
@@ -1698,6 +1777,7 @@ class JobTracker:
             # the TIP stays pending for real execution
             a.profile_fraction = profile_fraction
             a.profile_only = True
+            jip.probe_aids.append(a.aid)
             jip.counters.incr(C.JOB_GROUP, "PROFILE_TASKS")
         else:
             tip.attempts[a.aid] = a
@@ -1749,13 +1829,15 @@ class JobTracker:
         aids = []
         index = self.attempt_index
         running = tr.running
-        jip.launched_on.setdefault(tr.name, []).extend(tips)
+        name = tr.name
+        gated = gate is not None
+        jip.launched_on.setdefault(name, []).extend(tips)
         for tip in tips:
             aid = tip._aid_prefix + str(tip.next_attempt)
             tip.next_attempt += 1
-            a = Attempt(aid, tip, tr.name, True, device)
-            a.start = now
-            a.gated = gate is not None
+            a = Attempt(aid, tip, name, True, device, start=now)
+            if gated:
+                a.gated = True
             tip.attempts[aid] = a
             index[aid] = a
             running.add(aid)
@@ -1793,7 +1875,7 @@ class JobTracker:
             # only maps launched on this tracker can have outputs here (a TIP
             # re-run elsewhere is listed under that tracker too); map order
             tips = jip.launched_on.get(tracker_name, ())
-            for t in sorted(set(tips), key=lambda t: t.partition):
+            for t in sorted(dict.fromkeys(tips), key=_PARTITION):
                 a = t.successful
                 if a is None and expect:
                     ra = t.running_attempts()
@@ -1898,11 +1980,8 @@ class JobTracker:
         counters, the phase timeline, maps per tracker and the reduce result."""
         jip = self.check_access(jid, "view")
         st = jip.status
-        per = {}
         with self.lock:
-            for t in jip.maps:
-                if t.successful is not None:
-                    per[t.successful.tracker] = per.get(t.successful.tracker, 0) + 1
+            per = jip.maps_per_tracker()
         return {"state": st.state, "map_progress": st.map_progress,
                 "reduce_progress": st.reduce_progress, "start_time": st.start_time,
                 "finish_time": st.finish_time, "failure_info": st.failure_info,

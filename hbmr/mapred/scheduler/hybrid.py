@@ -389,10 +389,16 @@ class HybridTaskScheduler(TaskScheduler):
         # it holds): one running GPU attempt per unfinished map
         if jip.running_gpu != len(jip.maps) - jip.maps_done:
             return False
+        # the map scan once per state of those counts (this runs per tracker
+        # per heartbeat for every staged job)
+        sig = (jip.running_gpu, jip.maps_done, jip.jt.kill_epoch)
+        if jip.__dict__.get("_expect_sig") == sig:
+            return False
         for t in jip.maps:
             if t.successful is None:
                 ra = t.running_attempts()
                 if len(ra) != 1 or not ra[0].run_on_gpu:
+                    jip._expect_sig = sig
                     return False
         return True
 

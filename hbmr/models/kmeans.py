@@ -1070,14 +1070,7 @@ class KMeansDriver:
         jip = getattr(rj._impl, "jip", None)
         if jip is not None:
             res["timeline"] = jip.timeline()
-            if hasattr(jip, "maps_per_tracker"):      # a JobTracker process's job view
-                per = jip.maps_per_tracker()
-            else:
-                per = {}
-                for t in jip.maps:
-                    if t.successful is not None:
-                        per[t.successful.tracker] = per.get(t.successful.tracker, 0) + 1
-            res["maps_per_tracker"] = per
+            res["maps_per_tracker"] = jip.maps_per_tracker()
         res.update(iteration=i, seconds=time.time() - t0, job=str(rj.getID()),
                    counters=rj.getCounters())
         self.history.append(res)
