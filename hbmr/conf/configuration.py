@@ -298,7 +298,8 @@ class Configuration:
         return list(iter(self))
 
     def to_dict(self) -> dict:
-        return dict(iter(self))
+        sub = self._substitute
+        return {k: (sub(v) if "${" in v else v) for k, v in sorted(self._props.items())}
 
     def write_xml(self, out):
         root = ET.Element("configuration")

@@ -134,6 +134,26 @@ class Counters:
 
     incrAllCounters = incr_all  # noqa: N815
 
+    def incr_dicts(self, dicts):
+        """Add counters given as ``{group: {name: value}}`` dicts (the wire
+        form), without building a Counters object per dict."""
+        with self._lock:
+            groups = self.groups
+            for d in dicts:
+                if not d:
+                    continue
+                for gname, cs in d.items():
+                    g = groups.get(gname)
+                    if g is None:
+                        g = groups[gname] = Group(gname)
+                    gc = g.counters
+                    for n, v in cs.items():
+                        c = gc.get(n)
+                        if c is None:
+                            gc[n] = Counter(n, value=v)
+                        else:
+                            c.value += v
+
     def to_dict(self) -> dict:
         return {g: {c.name: c.value for c in grp} for g, grp in self.groups.items()}
 

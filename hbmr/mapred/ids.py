@@ -74,12 +74,14 @@ class JobID(_ID):
 class TaskID(_ID):
     __slots__ = ("job", "is_map", "id", "_s")
 
-    def __init__(self, job: JobID, is_map: bool, id: int):  # noqa: A002
-        object.__setattr__(self, "job", job)
-        object.__setattr__(self, "is_map", is_map)
-        object.__setattr__(self, "id", id)
-        object.__setattr__(self, "_s", f"task_{job.jt}_{job.id:04d}_"
-                                       f"{'m' if is_map else 'r'}_{id:06d}")
+    def __init__(self, job: JobID, is_map: bool, id: int, s: str | None = None):  # noqa: A002
+        # ``s``: the string form when the caller has it (a job's TIPs are
+        # built from one prefix)
+        _set = object.__setattr__
+        _set(self, "job", job)
+        _set(self, "is_map", is_map)
+        _set(self, "id", id)
+        _set(self, "_s", s or f"task_{job.jt}_{job.id:04d}_{'m' if is_map else 'r'}_{id:06d}")
 
     def _key(self):
         return (self.job, self.is_map, self.id)

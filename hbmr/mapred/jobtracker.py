@@ -103,6 +103,7 @@ class TrackerInfo:
 
 
 _PARTITION = operator.attrgetter("partition")
+_LIVE = (P.RUNNING, P.COMMIT_PENDING)
 
 
 class Attempt:
@@ -135,24 +136,27 @@ class Attempt:
 
 
 class TaskInProgress:
-    __slots__ = ("job", "tid", "split", "partition", "pinned_tracker", "attempts", "next_attempt",
-                 "failures", "failed_trackers", "successful", "commit_granted", "killed",
-                 "_aid_prefix", "__weakref__")
+    """A task (map or reduce) of a job and its attempts.  As with Attempt,
+    the fields most TIPs never change are class defaults: init_tasks builds
+    one per split of every job."""
+    pinned_tracker = None
+    next_attempt = 0
+    failures = 0
+    failed_trackers: frozenset | set = frozenset()   # a set once an attempt fails
+    successful = None            # the winning Attempt
+    commit_granted = None
+    killed = False
 
-    def __init__(self, job, tid: TaskID, split=None, partition=0, pinned_tracker=None):
+    def __init__(self, job, tid: TaskID, split=None, partition=0, pinned_tracker=None,
+                 aid_prefix=None):
         self.job = job
         self.tid = tid
         self.split = split
         self.partition = partition
-        self.pinned_tracker = pinned_tracker
+        if pinned_tracker is not None:
+            self.pinned_tracker = pinned_tracker
         self.attempts: dict[str, Attempt] = {}
-        self.next_attempt = 0
-        self.failures = 0
-        self.failed_trackers: set[str] = set()
-        self.successful: Attempt | None = None
-        self.commit_granted: str | None = None
-        self.killed = False
-        self._aid_prefix = "attempt" + str(tid)[4:] + "_"
+        self._aid_prefix = aid_prefix or ("attempt" + tid._s[4:] + "_")
 
     @property
     def is_map(self):
@@ -162,7 +166,11 @@ class TaskInProgress:
         return self.successful is not None
 
     def running_attempts(self):
-        return [a for a in self.attempts.values() if a.state in (P.RUNNING, P.COMMIT_PENDING)]
+        at = self.attempts
+        if len(at) == 1:                 # the common case: one attempt
+            for a in at.values():
+                return [a] if a.state in _LIVE else []
+        return [a for a in at.values() if a.state in _LIVE]
 
     def is_running(self):
         return bool(self.running_attempts())
@@ -294,7 +302,11 @@ class JobInProgress:
                             "locations": list(s.getLocations() or []),
                             "length": s.getLength()} for s in splits]
         jid = self.job_id
-        maps = self.maps = [TaskInProgress(self, TaskID(jid, True, i), split=sd, partition=i)
+        tpre = f"task_{jid.jt}_{jid.id:04d}_m_"
+        apre = f"attempt_{jid.jt}_{jid.id:04d}_m_"
+        maps = self.maps = [TaskInProgress(self, TaskID(jid, True, i, tpre + f"{i:06d}"),
+                                           split=sd, partition=i,
+                                           aid_prefix=apre + f"{i:06d}_")
                             for i, sd in enumerate(split_dicts)]
         self.pending_maps = dict.fromkeys(maps)
         self.by_split_key = {sd["key"]: tip for tip, sd in zip(maps, split_dicts)
@@ -353,9 +365,8 @@ class JobInProgress:
                             ("RACK_LOCAL_MAPS", rack)):
                 if v:
                     self.counters.incr(C.JOB_GROUP, name, v)
-        for d in pend:
-            if d:
-                self.counters.incr_all(Counters.from_dict(d))
+        if pend:
+            self.counters.incr_dicts(pend)
         return self.counters
 
     def _index(self, tracker: TrackerInfo, on_gpu, device):
@@ -371,19 +382,21 @@ class JobInProgress:
         if idx is None or idx[4] != len(tracker.cached):
             pend = self.pending_maps
             byk = self.by_split_key
-            lv0, lv1, lv2, seen = [], [], [], set()
+            lv0, lv1 = [], []
             if byk and tracker.cached:
-                if on_gpu:
-                    for k, d in tracker.cached:
-                        tip = byk.get(k)
-                        if d == device and tip is not None and tip in pend and tip not in seen:
-                            lv0.append(tip)
-                            seen.add(tip)
-                for k, _d in tracker.cached:
+                # one pass: a split cached on this device is level 0, on
+                # another of the tracker's devices level 1 (once: a split may
+                # be cached on several)
+                dev0 = device if on_gpu else None
+                for k, d in tracker.cached:
                     tip = byk.get(k)
-                    if tip is not None and tip in pend and tip not in seen:
-                        lv1.append(tip)
-                        seen.add(tip)
+                    if tip is not None and tip in pend:
+                        (lv0 if d == dev0 else lv1).append(tip)
+                if len(tracker.status.gpus) > 1 or not on_gpu:
+                    s0 = set(lv0)
+                    lv1 = [t for t in dict.fromkeys(lv1) if t not in s0]
+            seen = set(lv0)
+            seen.update(lv1)
             # stacks popped from the end, in pending order: re-queued TIPs
             # (failed / lost outputs, add_pending(front=True)) first, newest
             # first, then map index order (findNewMapTask takes failed maps first)
@@ -421,8 +434,14 @@ class JobInProgress:
         if bl is None:
             bl = {}
             for tip in self.maps:
-                for loc in tip.locations():
-                    bl.setdefault(loc, []).append(tip)
+                sp = tip.split
+                if sp.__class__ is dict:
+                    for loc in sp.get("locations") or ():
+                        got = bl.get(loc)
+                        if got is None:
+                            bl[loc] = [tip]
+                        else:
+                            got.append(tip)
             self._byloc = bl
         return bl
 
@@ -488,11 +507,15 @@ class JobInProgress:
                 break
             stack = idx[level] if level < 2 else self._node_level(tracker, idx) if level == 2 \
                 else self._rack_level(tracker, idx)
+            front = self._front
             while stack and len(out) < n:
                 tip = stack.pop()
-                if tip in pend and not (multi and name in tip.failed_trackers and
+                if tip in pend and not (multi and tip.failed_trackers and
+                                        name in tip.failed_trackers and
                                         len(tip.failed_trackers) < ntr):
-                    self._take(tip)
+                    del pend[tip]
+                    if front:
+                        front.pop(tip, None)
                     out.append((tip, level))
             if len(out) >= n:
                 break
@@ -1722,6 +1745,8 @@ class JobTracker:
             return
         if not killed:
             tip.failures += 1
+            if not isinstance(tip.failed_trackers, set):
+                tip.failed_trackers = set()
             tip.failed_trackers.add(a.tracker)
             jip.counters.incr(C.JOB_GROUP, C.NUM_FAILED_MAPS if tip.is_map else
                               C.NUM_FAILED_REDUCES)
@@ -1757,7 +1782,8 @@ class JobTracker:
         # O(1) on the counters; the TIP scan only confirms the rare final case
         if jip.maps_done < len(jip.maps) or jip.reduces_done < len(jip.reduces):
             return
-        if all(t.is_complete() for t in jip.maps) and all(t.is_complete() for t in jip.reduces):
+        if all(t.successful is not None for t in jip.maps) and \
+                all(t.successful is not None for t in jip.reduces):
             if jip.staged_on is not None:
                 # a staged job ran ahead of the job it depends on: it succeeds
                 # when that one does (or fails with it)
@@ -1833,16 +1859,15 @@ class JobTracker:
         gated = gate is not None
         jip.launched_on.setdefault(name, []).extend(tips)
         for tip in tips:
-            aid = tip._aid_prefix + str(tip.next_attempt)
-            tip.next_attempt += 1
-            a = Attempt(aid, tip, name, True, device, start=now)
+            k = tip.next_attempt
+            aid = tip._aid_prefix + str(k)
+            tip.next_attempt = k + 1
+            a = tip.attempts[aid] = index[aid] = Attempt(aid, tip, name, True, device, False, now)
             if gated:
                 a.gated = True
-            tip.attempts[aid] = a
-            index[aid] = a
-            running.add(aid)
             tasks.append([aid, tip.partition, tip.split])
             aids.append(aid)
+        running.update(aids)
         n = len(tips)
         tr.running_gpu[device] = tr.running_gpu.get(device, 0) + n
         jip.running_gpu += n
@@ -1881,7 +1906,7 @@ class JobTracker:
                     ra = t.running_attempts()
                     a = ra[0] if len(ra) == 1 else None
                 if a is not None and a.tracker == tracker_name:
-                    out.append([str(t.tid), a.aid, a.output or {}])
+                    out.append([t.tid._s, a.aid, a.output or {}])
             return out
         return [[str(t.tid), t.successful.aid, t.successful.output] for t in jip.maps
                 if t.successful is not None]

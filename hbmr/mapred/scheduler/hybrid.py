@@ -150,10 +150,13 @@ class HybridTaskScheduler(TaskScheduler):
         # beyond one queue's worth would otherwise never launch, and whose
         # reduce the gate waits on
         held = {}
-        for j in jt.staged:
-            for (tname, dev), n in j.staged_launched.items():
-                if tname == tr.name and n:
-                    held[dev] = held.get(dev, 0) + n
+        if jt.staged:
+            name = tr.name
+            for g in tr.status.gpus:
+                dev = g["device"]
+                n = sum(j.staged_launched.get((name, dev), 0) for j in jt.staged)
+                if n:
+                    held[dev] = n
         gpu_free = {g["device"]: g["max_slots"] * depth - tr.running_gpu.get(g["device"], 0) +
                     held.get(g["device"], 0) for g in tr.status.gpus}
         budget = self.max_maps_per_hb

@@ -190,9 +190,10 @@ def test_requeued_maps_are_taken_first_at_local_levels():
         def __init__(self, i):
             self.partition = i
             self.failed_trackers = set()
+            self.split = {"locations": ["tt0"]}
 
         def locations(self):
-            return ["tt0"]
+            return self.split["locations"]
 
         def split_key(self):
             return None

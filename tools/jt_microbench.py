@@ -90,8 +90,9 @@ class Harness:
                                     f"mb:{i}", f"mb:{i + 1}")
         if self.submitted:
             job.set(DEPENDS_KEY, self.submitted[-1])
+        wire = msgpack.packb(job.to_dict())        # the driver's side
         t0 = time.thread_time()
-        d = msgpack.unpackb(msgpack.packb(job.to_dict()), raw=False)
+        d = msgpack.unpackb(wire, raw=False)
         jid = self.jt.rpc_submit_job(d)
         self.cpu += time.thread_time() - t0
         self.calls += 1
