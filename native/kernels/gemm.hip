@@ -289,6 +289,233 @@ __global__ __launch_bounds__(kGemmThreads2, 1) void gemm_bf16_tn_v2_kernel(
   }
 }
 
+
+// Ring kernels (HBMR_GEMM=3 / 4 / 5 / 6): WM × WN waves, each owning a
+// (256/WM) × (256/WN) block of 32×32 tiles (v_mfma_f32_32x32x16_bf16), over a
+// 4-slot ring of K-steps of 32 (4 × 32 KiB of LDS): the loads of K-step k+4
+// are issued in the middle of step k (into step k's slot, once every wave
+// holds its last fragments of it), so a step's operands have three steps to
+// arrive from L2 / HBM instead of one, and a step waits only for its own
+// pieces (a counted vmcnt: the younger steps stay in flight across the
+// barrier, which is a bare s_barrier — __syncthreads()'s release fence waits
+// for every outstanding LDS-DMA, vmcnt(0), and would drain the ring).
+// Fragments are software-pipelined: the second 16-wide half of a K-step
+// loads while the first half's MFMAs run, the next K-step's first half while
+// the second half's run.  PRIO: s_setprio(1) over the MFMA blocks.
+// LDS image of a 256×32 operand tile: rows r and r+1 share a 128-B line
+// L = r/2 (16-B chunk q = 4 (r & 1) + c), chunk q at slot q ^ ((L >> 1) & 3):
+// the 16 lanes of a ds_read_b128 pass (16 consecutive rows, one k-chunk) hit
+// 16 distinct bank groups.
+constexpr int kBKr = 32;
+constexpr int kTiler = kBM * kBKr * 2;    // 16 KiB
+constexpr int kStager = 2 * kTiler;       // A + B: 32 KiB
+constexpr int kRingr = 4;
+constexpr int kLdsr = kRingr * kStager;   // 128 KiB
+
+template <int THREADS>
+__device__ __forceinline__ void stage_ring(char* lds, const __bf16* __restrict__ G, long ld,
+                                           long row0, long k0, int tid) {
+#pragma unroll
+  for (int i = 0; i < kTiler / 16 / THREADS; ++i) {
+    const int p = i * THREADS + tid;        // 16-B slot in the image (line-major)
+    const int L = p >> 3, slot = p & 7;
+    const int q = slot ^ ((L >> 1) & 3);
+    const int r = 2 * L + (q >> 2), c = q & 3;
+    const __bf16* g = G + (row0 + r) * ld + k0 + c * 8;
+    char* dst = lds + (size_t)(i * THREADS + (tid & ~63)) * 16;
+    __builtin_amdgcn_global_load_lds((const void*)g, (void*)dst, 16, 0, 0);
+  }
+}
+
+// s_waitcnt vmcnt(PER · n) for n in 0..3 (the count is an immediate)
+template <int PER>
+__device__ __forceinline__ void vmcnt_steps(int n) {
+  if (n >= 3)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * PER) : "memory");
+  else if (n == 2)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PER) : "memory");
+  else if (n == 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// a fragment read in inline asm: hipcc's own lgkmcnt for compiler-visible
+// ds_reads is conservative at the loop head (it waited for the half-step
+// loaded behind the one the MFMAs need); these are counted by hand
+// (lgkm_wait + sched_barrier: the MFMAs are register-only and would be
+// scheduled past a bare asm wait)
+__device__ __forceinline__ bf16x8_t frag_ring(const char* t, int r, int c) {
+  const int L = r >> 1;
+  const int slot = (((r & 1) << 2) | c) ^ ((L >> 1) & 3);
+  const __attribute__((address_space(3))) char* p =
+      (const __attribute__((address_space(3))) char*)(t + L * 128 + slot * 16);
+  bf16x8_t v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)p));
+  return v;
+}
+
+template <int N>
+__device__ __forceinline__ void lgkm_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool OUT_BF16, int WM, int WN, bool PRIO>
+__global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_tn_ring_kernel(
+    const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void* __restrict__ Cv, long M,
+    long N, long K, float alpha, double* __restrict__ partials) {
+  constexpr int THREADS = 64 * WM * WN;
+  constexpr int TI = kBM / WM / 32, TJ = kBN / WN / 32;   // 32×32 tiles per wave
+  constexpr int PER = 2 * (kTiler / 16 / THREADS);        // pieces per thread per K-step
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const long tiles_n = N / kBN;
+  const uint32_t t = hbmr_xcd_remap(blockIdx.x, gridDim.x);
+  const long bm = t / tiles_n, bn = t % tiles_n;
+  const long m0 = bm * kBM, n0 = bn * kBN;
+  const int nk = (int)(K / kBKr);
+
+  f32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+#pragma unroll
+  for (int s = 0; s < kRingr; ++s) {
+    if (s < nk) {
+      stage_ring<THREADS>(smem + s * kStager, A, K, m0, (long)s * kBKr, tid);
+      stage_ring<THREADS>(smem + s * kStager + kTiler, Bt, K, n0, (long)s * kBKr, tid);
+    }
+  }
+  const int fr = lane & 31;
+  const int h = lane >> 5;
+  const int ra = wm * (kBM / WM) + fr, rb = wn * (kBN / WN) + fr;
+
+  bf16x8_t a0[TI], b0[TJ], a1[TI], b1[TJ];
+  {
+    vmcnt_steps<PER>(nk - 1 < 3 ? nk - 1 : 3);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < TI; ++i) a0[i] = frag_ring(smem, ra + i * 32, h);
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) b0[j] = frag_ring(smem + kTiler, rb + j * 32, h);
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* la = smem + (kt & (kRingr - 1)) * kStager;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) a1[i] = frag_ring(la, ra + i * 32, 2 + h);
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) b1[j] = frag_ring(la + kTiler, rb + j * 32, 2 + h);
+    lgkm_wait<TI + TJ>();        // F0 landed (F1's reads may be in flight)
+    if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[i], b0[j], acc[i][j], 0, 0, 0);
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
+    if (kt + 1 < nk) {
+      lgkm_wait<0>();
+      vmcnt_steps<PER>(nk - 2 - kt < 2 ? nk - 2 - kt : 2);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kt + kRingr < nk) {
+        char* nxt = smem + (kt & (kRingr - 1)) * kStager;
+        stage_ring<THREADS>(nxt, A, K, m0, (long)(kt + kRingr) * kBKr, tid);
+        stage_ring<THREADS>(nxt + kTiler, Bt, K, n0, (long)(kt + kRingr) * kBKr, tid);
+      }
+      const char* ln = smem + ((kt + 1) & (kRingr - 1)) * kStager;
+#pragma unroll
+      for (int i = 0; i < TI; ++i) a0[i] = frag_ring(ln, ra + i * 32, h);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) b0[j] = frag_ring(ln + kTiler, rb + j * 32, h);
+    } else {
+      lgkm_wait<0>();            // F1 landed (the branch above waited before its barrier)
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
+  }
+
+  double csum = 0.0;
+  const long lane_off = (m0 + wm * (kBM / WM) + 4 * h) * N + n0 + wn * (kBN / WN) + fr;
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const long base = lane_off + (long)(i * 32) * N + j * 32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long off = base + (long)((r & 3) + 8 * (r >> 2)) * N;
+        const float v = acc[i][j][r] * alpha;
+        if (OUT_BF16) {
+          const uint16_t hv = hbmr_f32_to_bf16(v);
+          reinterpret_cast<uint16_t*>(Cv)[off] = hv;
+          csum += (double)__uint_as_float((uint32_t)hv << 16);
+        } else {
+          reinterpret_cast<float*>(Cv)[off] = v;
+          csum += (double)v;
+        }
+      }
+    }
+  }
+  if (partials) {
+    // (reuses the staging array: a second __shared__ object can make hipcc
+    // wait vmcnt(0) before the loop's first ds_read)
+    __syncthreads();
+    double* red = reinterpret_cast<double*>(smem);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) csum += __shfl_xor(csum, o);
+    if (lane == 0) red[wave] = csum;
+    __syncthreads();
+    if (tid == 0) {
+      double sum = 0.0;
+#pragma unroll
+      for (int w = 0; w < WM * WN; ++w) sum += red[w];
+      partials[blockIdx.x] = sum;
+    }
+  }
+}
+
+template <bool OUT_BF16, int WM, int WN, bool PRIO>
+int launch_ring(const void* A, const void* Bt, void* C, long M, long N, long K, float alpha,
+                double* partials, long tiles, hipStream_t st) {
+  static bool set = false;
+  if (!set) {
+    HBMR_RETURN_IF_ERROR(hipFuncSetAttribute(
+        (const void*)gemm_bf16_tn_ring_kernel<OUT_BF16, WM, WN, PRIO>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsr));
+    set = true;
+  }
+  hipLaunchKernelGGL((gemm_bf16_tn_ring_kernel<OUT_BF16, WM, WN, PRIO>), dim3((unsigned)tiles),
+                     dim3(64 * WM * WN), kLdsr, st, reinterpret_cast<const __bf16*>(A),
+                     reinterpret_cast<const __bf16*>(Bt), C, M, N, K, alpha, partials);
+  return (int)hipGetLastError();
+}
+
+template <bool OUT_BF16>
+int launch_ring_ver(int ver, const void* A, const void* Bt, void* C, long M, long N, long K,
+                    float alpha, double* partials, long tiles, hipStream_t st) {
+  switch (ver) {
+    case 3: return launch_ring<OUT_BF16, 2, 2, false>(A, Bt, C, M, N, K, alpha, partials, tiles, st);
+    case 4: return launch_ring<OUT_BF16, 2, 2, true>(A, Bt, C, M, N, K, alpha, partials, tiles, st);
+    case 5: return launch_ring<OUT_BF16, 2, 4, false>(A, Bt, C, M, N, K, alpha, partials, tiles, st);
+    default: return launch_ring<OUT_BF16, 2, 4, true>(A, Bt, C, M, N, K, alpha, partials, tiles, st);
+  }
+}
+
 bool g_gemm_lds_set = false;
 
 }  // namespace
@@ -318,11 +545,14 @@ int hbmr_gemm_bf16_tn_ex(const void* A, const void* Bt, void* C, long M, long N,
   const long tiles = ((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
   if (tiles > 0x7fffffffL) return (int)hipErrorInvalidValue;
   const bool ragged = M % kBM || N % kBN || K % kBK;
-  // HBMR_GEMM=2: the 4-wave 128x128 / 32x32x16 variant (A/B against v1)
-  static const int ver = [] {
-    const char* e = getenv("HBMR_GEMM");
-    return e && *e == '2' ? 2 : 1;
-  }();
+  // HBMR_GEMM=2: the 4-wave 128x128 / 32x32x16 double-buffered variant;
+  // 3..6: the ring kernels (A/B against v1), read per call (a bench switches
+  // between them in one process)
+  const char* ev = getenv("HBMR_GEMM");
+  const int ver = ev && *ev >= '2' && *ev <= '6' ? *ev - '0' : 1;
+  if (ver >= 3 && !ragged && K % kBKr == 0)
+    return out_bf16 ? launch_ring_ver<true>(ver, A, Bt, C, M, N, K, alpha, partials, tiles, st)
+                    : launch_ring_ver<false>(ver, A, Bt, C, M, N, K, alpha, partials, tiles, st);
   if (ver == 2 && !ragged) {
     if (out_bf16)
       hipLaunchKernelGGL(gemm_bf16_tn_v2_kernel<true>, dim3((unsigned)tiles), dim3(kGemmThreads2),
