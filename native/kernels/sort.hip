@@ -893,6 +893,87 @@ __global__ __launch_bounds__(256) void gather_records_gid_kernel(
   }
 }
 
+// The record gather in 16-B pieces (v2, default): a record of W words is
+// moved by L = ceil(W / 4) lanes, lane c the 16 B at word 4c (the last lane
+// the remaining 1-4 words) — 7 lanes per 100-B TeraSort record instead of 25,
+// so a wave keeps 9 records x U in flight per round instead of 2.5 x U, with
+// 16-B loads/stores at the record's 4-B alignment (global memory takes
+// dword-aligned vector accesses).  The lane holding words 0-3 also writes the
+// record's key (hi byte-swapped from words 0-1, lo from word 2's bytes 8-9).
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef u32x4_t __attribute__((aligned(4))) u32x4_a4;
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+typedef u32x2_t __attribute__((aligned(4))) u32x2_a4;
+
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void gather_records_gid16_kernel(
+    const uint32_t* const* __restrict__ bases, const uint32_t* __restrict__ gid, long n,
+    int words, uint32_t* __restrict__ dst, uint32_t* __restrict__ khi,
+    uint64_t* __restrict__ klo) {
+  const int L = (words + 3) >> 2;            // lanes per record
+  const int rpw = HBMR_WAVE / L;             // records per wave
+  const int lane = threadIdx.x & (HBMR_WAVE - 1), wave = threadIdx.x / HBMR_WAVE;
+  if (lane >= rpw * L) return;               // (no barrier in this kernel)
+  const int lr = lane / L;
+  const int c = lane - lr * L;
+  const int w0 = 4 * c;                      // first word of this lane's piece
+  const int nw = words - w0 < 4 ? words - w0 : 4;
+  const long rpb = (long)rpw * (256 / HBMR_WAVE);
+  const long stride = (long)gridDim.x * rpb;
+  for (long r0 = (long)blockIdx.x * rpb + wave * rpw + lr; r0 < n; r0 += stride * U) {
+    const uint32_t* src[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const long r = r0 + j * stride;
+      src[j] = nullptr;
+      if (r < n) {
+        const uint32_t g = gid[r];
+        src[j] = bases[g >> 24] + (long)(g & 0xFFFFFFu) * words + w0;
+      }
+    }
+    u32x4_t v[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      v[j] = u32x4_t{0u, 0u, 0u, 0u};
+      if (!src[j]) continue;
+      if (nw == 4) {
+        v[j] = *reinterpret_cast<const u32x4_a4*>(src[j]);
+      } else if (nw == 2) {
+        const u32x2_t t = *reinterpret_cast<const u32x2_a4*>(src[j]);
+        v[j].x = t.x;
+        v[j].y = t.y;
+      } else {
+        v[j].x = src[j][0];
+        if (nw > 1) v[j].y = src[j][1];
+        if (nw > 2) v[j].z = src[j][2];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const long r = r0 + j * stride;
+      if (r >= n) continue;
+      uint32_t* d = dst + r * words + w0;
+      if (nw == 4) {
+        if constexpr (NT)
+          __builtin_nontemporal_store(v[j], reinterpret_cast<u32x4_a4*>(d));
+        else
+          *reinterpret_cast<u32x4_a4*>(d) = v[j];
+      } else if (nw == 2) {
+        *reinterpret_cast<u32x2_a4*>(d) = u32x2_t{v[j].x, v[j].y};
+      } else {
+        d[0] = v[j].x;
+        if (nw > 1) d[1] = v[j].y;
+        if (nw > 2) d[2] = v[j].z;
+      }
+      if (khi != nullptr && c == 0) {
+        khi[2 * r + 1] = __builtin_bswap32(v[j].x);   // hi = bytes 0-7, big-endian
+        khi[2 * r] = __builtin_bswap32(v[j].y);
+        klo[r] = ((uint64_t)(v[j].z & 0xFFu) << 8) | ((v[j].z >> 8) & 0xFFu);   // bytes 8-9
+      }
+    }
+  }
+}
+
 // After the sort on the high key word's top 64 - shift bits and the record
 // gather: order each run of an equal sorted prefix (hi >> shift) by the full
 // key (hi, lo), moving hi, lo and the (already gathered) records themselves;
@@ -1158,6 +1239,23 @@ int hbmr_gather_records_gid(const void* const* bases, const uint32_t* gid, long 
     return (m.find("u8") != std::string::npos ? 1 : 0) | (m.find("nt") != std::string::npos ? 2 : 0);
   }();
   const int U = (mode & 1) ? 8 : 4;
+  // HBMR_GATHER=w1...: the word-per-lane kernel (round 3-4) for A/B
+  static const bool word_lanes = [] {
+    const char* e = getenv("HBMR_GATHER");
+    return e && std::string(e).find("w1") != std::string::npos;
+  }();
+  if (!word_lanes && words >= 3) {
+    auto k16 = mode == 0 ? gather_records_gid16_kernel<4, false>
+             : mode == 1 ? gather_records_gid16_kernel<8, false>
+             : mode == 2 ? gather_records_gid16_kernel<4, true>
+                         : gather_records_gid16_kernel<8, true>;
+    const long rpb = (long)(HBMR_WAVE / ((words + 3) / 4)) * (256 / HBMR_WAVE);
+    const long grid16 = std::min<long>(ceil_div(n, rpb * U), 1L << 18);
+    hipLaunchKernelGGL(k16, dim3((unsigned)grid16), dim3(256), 0, st,
+                       reinterpret_cast<const uint32_t* const*>(bases), gid, n, words,
+                       reinterpret_cast<uint32_t*>(dst), reinterpret_cast<uint32_t*>(hi), lo);
+    return (int)hipGetLastError();
+  }
   auto kern = mode == 0 ? gather_records_gid_kernel<4, false>
             : mode == 1 ? gather_records_gid_kernel<8, false>
             : mode == 2 ? gather_records_gid_kernel<4, true>

@@ -471,3 +471,27 @@ def test_gpu_terasort_out_of_core(tmp_path):
     assert v["files"] == 6 and v["records"] == rows and v["misordered"] == 0
     got = np.fromfile(out / "part-00000", dtype=np.uint8).reshape(-1, 100)
     assert np.array_equal(got[:1000], _ref_sorted(rows)[:1000])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rb", [100, 12, 16, 20, 28, 36, 8, 4])
+def test_gpu_record_gather_pieces_match_cpu(rb):
+    """The 16-B-piece record gather (7 lanes per 100-B record; other sizes:
+    a last piece of 1-3 words) and its key outputs against the CPU gather,
+    from several base splits at random rows (record sizes below 12 B take the
+    word-per-lane kernel)."""
+    g = torch.Generator().manual_seed(rb)
+    bases = [torch.randint(0, 256, (n, rb), generator=g, dtype=torch.uint8) for n in (1000, 37, 4099)]
+    split = torch.randint(0, 3, (20000,), generator=g)
+    row = torch.cat([torch.randint(0, bases[s].shape[0], (1,), generator=g) for s in split.tolist()])
+    gid = ((split << 24) | row).to(torch.int32)
+    want = S.gather_records_gid(bases, gid)
+    keys = None
+    if rb >= 12:
+        keys = (torch.empty(20000, dtype=torch.int64, device="cuda"),
+                torch.empty(20000, dtype=torch.int64, device="cuda"))
+    got = S.gather_records_gid([b.cuda() for b in bases], gid.cuda(), keys=keys)
+    assert torch.equal(got.cpu(), want)
+    if keys is not None:
+        h, lo = S.tera_keys(want)
+        assert torch.equal(keys[0].cpu(), h) and torch.equal(keys[1].cpu(), lo)
