@@ -695,6 +695,122 @@ __global__ __launch_bounds__(kSortThreads) void tera_part_scatter_kernel(
   }
 }
 
+// (A') key / partition / count with the key read as 3 dwords (the record
+// stride is a multiple of 4: bytes 0-11 of every record are 4-B aligned)
+// instead of 10 byte loads per record.
+__global__ __launch_bounds__(256) void tera_part_count_w_kernel(
+    const uint32_t* __restrict__ rec, long n, int stride_words, const uint64_t* __restrict__ shi,
+    const uint64_t* __restrict__ slo, int nsplit, uint64_t* __restrict__ hi,
+    uint64_t* __restrict__ lo, uint16_t* __restrict__ pid, unsigned int* __restrict__ counts) {
+  __shared__ uint64_t s_hi[kMaxSplitters];
+  __shared__ uint16_t s_lo[kMaxSplitters];
+  __shared__ unsigned int s_cnt[kMaxSplitters + 1];
+  const int nparts = nsplit + 1;
+  for (int j = threadIdx.x; j < nsplit; j += 256) {
+    s_hi[j] = shi[j];
+    s_lo[j] = (uint16_t)slo[j];
+  }
+  for (int j = threadIdx.x; j < nparts; j += 256) s_cnt[j] = 0u;
+  __syncthreads();
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const uint32_t* r = rec + i * stride_words;
+    const uint32_t w0 = r[0], w1 = r[1], w2 = r[2];
+    const uint64_t h = ((uint64_t)__builtin_bswap32(w0) << 32) | __builtin_bswap32(w1);
+    const uint32_t l = ((w2 & 0xFFu) << 8) | ((w2 >> 8) & 0xFFu);
+    int a = 0, b = nsplit;
+    while (a < b) {
+      const int m = (a + b) >> 1;
+      const bool le = s_hi[m] < h || (s_hi[m] == h && s_lo[m] <= l);
+      if (le) a = m + 1; else b = m;
+    }
+    hi[i] = h;
+    lo[i] = l;
+    pid[i] = (uint16_t)a;
+    atomicAdd(&s_cnt[a], 1u);
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < nparts; j += 256)
+    if (s_cnt[j]) atomicAdd(&counts[j], s_cnt[j]);
+}
+
+// (B') the scatter with the tile staged in partition order in LDS, so the
+// global writes go out as contiguous runs per partition (consecutive threads,
+// consecutive addresses) instead of every item to its own place: a tile of
+// kPartTile items ranks them per partition (LDS atomics), scans the tile's
+// partition counts, reserves each touched partition's range from the global
+// cursor, lays the items out in LDS by (partition, rank) and streams them out.
+constexpr int kPartTile = 2048;
+constexpr int kPartMax = 1025;     // partitions this kernel takes (else tera_part_scatter)
+__global__ __launch_bounds__(256) void tera_part_scatter_lds_kernel(
+    const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo,
+    const uint16_t* __restrict__ pid, long n, int nparts, unsigned int* __restrict__ cursor,
+    uint64_t* __restrict__ ohi, uint64_t* __restrict__ olo, uint32_t* __restrict__ orow) {
+  constexpr int kItems = kPartTile / 256;
+  constexpr int kPer = (kPartMax + 255) / 256;
+  __shared__ uint64_t s_hi[kPartTile];
+  __shared__ uint32_t s_row[kPartTile];
+  __shared__ uint16_t s_lo[kPartTile];
+  __shared__ uint16_t s_p[kPartTile];
+  __shared__ unsigned int s_cnt[kPartMax];
+  __shared__ unsigned int s_off[kPartMax];
+  __shared__ unsigned int s_gb[kPartMax];
+  __shared__ uint32_t s_w[4];
+  const int t = threadIdx.x;
+  const long base = (long)blockIdx.x * kPartTile;
+  const int tile_n = (int)min((long)kPartTile, n - base);
+  for (int j = t; j < nparts; j += 256) s_cnt[j] = 0u;
+  __syncthreads();
+  unsigned int loc[kItems];
+  uint16_t p[kItems];
+#pragma unroll
+  for (int i = 0; i < kItems; ++i) {
+    const int k = i * 256 + t;
+    if (k < tile_n) {
+      p[i] = pid[base + k];
+      loc[i] = atomicAdd(&s_cnt[p[i]], 1u);
+    }
+  }
+  __syncthreads();
+  // thread t owns partitions t*kPer .. t*kPer+kPer-1
+  unsigned int c[kPer], sum = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int q = t * kPer + j;
+    c[j] = q < nparts ? s_cnt[q] : 0u;
+    sum += c[j];
+  }
+  unsigned int run = block_excl_scan256(sum, s_w);
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int q = t * kPer + j;
+    if (q < nparts) {
+      s_off[q] = run;
+      s_gb[q] = c[j] ? atomicAdd(&cursor[q], c[j]) : 0u;
+    }
+    run += c[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kItems; ++i) {
+    const int k = i * 256 + t;
+    if (k < tile_n) {
+      const unsigned int slot = s_off[p[i]] + loc[i];
+      s_hi[slot] = hi[base + k];
+      s_lo[slot] = (uint16_t)lo[base + k];
+      s_row[slot] = (uint32_t)(base + k);
+      s_p[slot] = p[i];
+    }
+  }
+  __syncthreads();
+  for (int j = t; j < tile_n; j += 256) {
+    const int q = s_p[j];
+    const long d = (long)s_gb[q] + (j - (long)s_off[q]);
+    ohi[d] = s_hi[j];
+    olo[d] = s_lo[j];
+    orow[d] = s_row[j];
+  }
+}
+
 // dst record i = record row[k] of split split[k], k = perm ? perm[i] : i, with
 // U records per lane in flight: the index loads of all U records are issued,
 // then their words, then the stores, so each lane keeps U independent random
@@ -1178,17 +1294,34 @@ int hbmr_tera_partition(const void* records, long n, int stride, const uint64_t*
       (reinterpret_cast<uintptr_t>(pid + n) + 15) & ~uintptr_t(15));
   unsigned int* cursor = counts + (nparts + 1);
   HBMR_RETURN_IF_ERROR(hipMemsetAsync(counts, 0, (size_t)(nparts + 1) * 4, st));
+  // HBMR_TERA_PART=v1: the byte-load count and item-wise scatter (rounds 3-4)
+  static const bool v1 = [] {
+    const char* e = getenv("HBMR_TERA_PART");
+    return e && std::string(e) == "v1";
+  }();
+  const bool words = !v1 && stride % 4 == 0 && stride >= 12 &&
+                     reinterpret_cast<uintptr_t>(records) % 4 == 0;
   if (n > 0) {
     const long grid = std::min<long>(ceil_div(n, 256), 256L * 64);
-    hipLaunchKernelGGL(tera_part_count_kernel, dim3((unsigned)grid), dim3(256), 0, st,
-                       reinterpret_cast<const uint8_t*>(records), n, stride, shi, slo, nsplit, hi,
-                       lo, pid, counts);
+    if (words)
+      hipLaunchKernelGGL(tera_part_count_w_kernel, dim3((unsigned)grid), dim3(256), 0, st,
+                         reinterpret_cast<const uint32_t*>(records), n, stride / 4, shi, slo,
+                         nsplit, hi, lo, pid, counts);
+    else
+      hipLaunchKernelGGL(tera_part_count_kernel, dim3((unsigned)grid), dim3(256), 0, st,
+                         reinterpret_cast<const uint8_t*>(records), n, stride, shi, slo, nsplit,
+                         hi, lo, pid, counts);
   }
   hipLaunchKernelGGL(tera_part_offsets_kernel, dim3(1), dim3(1024), 0, st, counts, nparts, cursor,
                      offsets);
-  if (n > 0)
-    hipLaunchKernelGGL(tera_part_scatter_kernel, dim3((unsigned)ceil_div(n, kSortTile)),
-                       dim3(kSortThreads), 0, st, hi, lo, pid, n, nparts, cursor, ohi, olo, orow);
+  if (n > 0) {
+    if (!v1 && nparts <= kPartMax)
+      hipLaunchKernelGGL(tera_part_scatter_lds_kernel, dim3((unsigned)ceil_div(n, kPartTile)),
+                         dim3(256), 0, st, hi, lo, pid, n, nparts, cursor, ohi, olo, orow);
+    else
+      hipLaunchKernelGGL(tera_part_scatter_kernel, dim3((unsigned)ceil_div(n, kSortTile)),
+                         dim3(kSortThreads), 0, st, hi, lo, pid, n, nparts, cursor, ohi, olo, orow);
+  }
   return (int)hipGetLastError();
 }
 

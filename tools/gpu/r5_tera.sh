@@ -6,10 +6,10 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 P=${P:-r5ts}
 df -h /tmp $GRAFT_REPO_ROOT $HOME /dev/shm > gpurun_out/${P}_df.txt 2>&1
-timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_terasort.py -m gpu -k "gather or terasort_job or commits_output or many_partitions" > gpurun_out/${P}_tests.log 2>&1 || { tail -20 gpurun_out/${P}_tests.log; exit 1; }
+timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_terasort.py -m gpu -k "gather or terasort_job or commits_output or many_partitions or partition or radix" > gpurun_out/${P}_tests.log 2>&1 || { tail -20 gpurun_out/${P}_tests.log; exit 1; }
 tail -1 gpurun_out/${P}_tests.log
-for mode in default w1 default; do
-  if [ $mode = default ]; then unset HBMR_GATHER; else export HBMR_GATHER=$mode; fi
+for mode in default v1 default; do
+  if [ $mode = default ]; then unset HBMR_GATHER HBMR_TERA_PART; else export HBMR_GATHER=w1 HBMR_TERA_PART=v1; fi
   timeout -k 10 600 python3 tools/bench_terasort.py --rows 1000000000 --steps 2 > gpurun_out/${P}_100g_$mode.json 2> gpurun_out/${P}_100g_$mode.err || { tail -5 gpurun_out/${P}_100g_$mode.err; exit 1; }
   python3 -c "import json;d=json.loads(open('gpurun_out/${P}_100g_$mode.json').read().strip().splitlines()[-1]);print('$mode', d['seconds_per_sort'], d['gb_per_s'], d['validated'])"
 done
