@@ -27,8 +27,11 @@ M_KEY, K_KEY, N_KEY = "hbmr.matmul.m", "hbmr.matmul.k", "hbmr.matmul.n"
 ROWS_KEY = "hbmr.matmul.split.rows"
 SEED_KEY = "hbmr.matmul.seed"
 OUTC_KEY = "hbmr.matmul.output.dtype"   # float32 | bfloat16
-# GPU GEMM of a map task: "hbmr" = native/kernels/gemm.hip (MFMA, hand-written);
-# "hipblaslt" = torch.matmul (the vendor library, for comparison: a plain GEMM)
+# GPU GEMM of a map task: "hipblaslt" (default) = torch.matmul, the vendor
+# library — a map task's GEMM is a plain library GEMM, and hipBLASLt runs it at
+# 1.4x the hand-written kernel (profiles/r05_gemm_ring_ab.json); its checksum
+# is one extra read of C.  "hbmr" = native/kernels/gemm.hip (MFMA, hand-written,
+# the checksum fused into its epilogue)
 GEMM_KEY = "hbmr.matmul.gemm"
 
 _M32 = 0xFFFFFFFF
@@ -94,7 +97,7 @@ class MatmulSplitJob(SplitJob):
         self.out_dtype = torch.bfloat16 if conf.get(OUTC_KEY, "float32") == "bfloat16" \
             else torch.float32
         self.out = conf.get("mapred.output.dir")
-        self.gemm = conf.get(GEMM_KEY, "hbmr")
+        self.gemm = conf.get(GEMM_KEY, "hipblaslt")
         if self.gemm not in ("hbmr", "hipblaslt"):
             raise ValueError(f"{GEMM_KEY} must be hbmr or hipblaslt, not {self.gemm!r}")
 

@@ -68,10 +68,13 @@ def test_gemm_layout_identity_with_asymmetric_b():
 
 
 @pytest.mark.gpu
-def test_matmul_job_gpu():
+@pytest.mark.parametrize("gemm", ["hipblaslt", "hbmr"])
+def test_matmul_job_gpu(gemm):
     m, k, n = 4096, 512, 1024
-    with LocalCluster(JobConf(), num_trackers=1, gpus=[[0]], cpu_slots=0) as cl:
-        rj = cl.submit_job(MM.matmul_conf(m=m, k=k, n=n, split_rows=1024))
+    conf = JobConf()
+    conf.set(MM.GEMM_KEY, gemm)
+    with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=0) as cl:
+        rj = cl.submit_job(MM.matmul_conf(conf, m=m, k=k, n=n, split_rows=1024))
         rj.waitForCompletion(120)
         assert rj.isSuccessful(), rj.getFailureInfo()
         res = rj._impl.jip.result[0]
