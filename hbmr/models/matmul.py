@@ -124,9 +124,10 @@ class MatmulSplitJob(SplitJob):
         a = data["a"]
         bt = SIDE.bt(self.seed, self.k, self.n, a.device)
         if a.device.type == "cuda" and self.gemm == "hipblaslt":
-            c = torch.matmul(a, bt.t())
-            if self.out_dtype != torch.bfloat16:
-                c = c.float()
+            # fp32 C straight from the fp32 accumulators (aten::mm.dtype), not
+            # a bf16 C widened afterwards
+            c = torch.mm(a, bt.t()) if self.out_dtype == torch.bfloat16 else \
+                torch.mm(a, bt.t(), out_dtype=torch.float32)
             cs = c.sum(dtype=torch.float64)
         else:
             # the checksum comes out of the GEMM epilogue (no second pass over C)
