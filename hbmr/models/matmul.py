@@ -27,11 +27,12 @@ M_KEY, K_KEY, N_KEY = "hbmr.matmul.m", "hbmr.matmul.k", "hbmr.matmul.n"
 ROWS_KEY = "hbmr.matmul.split.rows"
 SEED_KEY = "hbmr.matmul.seed"
 OUTC_KEY = "hbmr.matmul.output.dtype"   # float32 | bfloat16
-# GPU GEMM of a map task: "hipblaslt" (default) = torch.matmul, the vendor
-# library — a map task's GEMM is a plain library GEMM, and hipBLASLt runs it at
-# 1.4x the hand-written kernel (profiles/r05_gemm_ring_ab.json); its checksum
-# is one extra read of C.  "hbmr" = native/kernels/gemm.hip (MFMA, hand-written,
-# the checksum fused into its epilogue)
+# GPU GEMM of a map task: "hbmr" (default) = native/kernels/gemm.hip (MFMA,
+# hand-written, the checksum fused into its epilogue); "hipblaslt" =
+# torch.mm, the vendor library — faster as a bare GEMM (1,366 vs 1,130 TF/s at
+# 8192^3 on one box) but slower as the map task (806 vs 899 TF/s for the
+# 65536x8192x8192 job: its checksum is a second pass over C,
+# profiles/r05_matmul_job_1gpu.json)
 GEMM_KEY = "hbmr.matmul.gemm"
 
 _M32 = 0xFFFFFFFF
@@ -97,7 +98,7 @@ class MatmulSplitJob(SplitJob):
         self.out_dtype = torch.bfloat16 if conf.get(OUTC_KEY, "float32") == "bfloat16" \
             else torch.float32
         self.out = conf.get("mapred.output.dir")
-        self.gemm = conf.get(GEMM_KEY, "hipblaslt")
+        self.gemm = conf.get(GEMM_KEY, "hbmr")
         if self.gemm not in ("hbmr", "hipblaslt"):
             raise ValueError(f"{GEMM_KEY} must be hbmr or hipblaslt, not {self.gemm!r}")
 

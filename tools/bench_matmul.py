@@ -35,7 +35,7 @@ def main():
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--split-rows", type=int, default=8192)
     ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--gemm", default="hipblaslt", choices=["hbmr", "hipblaslt"],
+    ap.add_argument("--gemm", default="hbmr", choices=["hbmr", "hipblaslt"],
                     help="map-task GEMM (hbmr.matmul.gemm)")
     a = ap.parse_args()
     import torch
