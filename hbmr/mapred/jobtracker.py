@@ -1008,10 +1008,17 @@ class JobTracker:
         if plan is not None and self.plan_staged:
             plan(w)
         # staged behind a job that is itself staged: its maps cannot run before
-        # two reduces have completed, and every tracker of the gang reports
-        # each completion (JobTracker.report assigns): no long-poll wake-up
+        # two reduces have completed, and a tracker with work running reports
+        # each completion (JobTracker.report assigns), which carries the plan:
+        # only the trackers with nothing running are rung — they have no report
+        # coming (one that ran its share of the chain ahead of the others would
+        # otherwise hold the new job's launches until its long-poll expired)
         if j.staged_on is None or not self.report_assign_expected:
             self._kick()
+        else:
+            for tr in list(self.trackers.values()):
+                if not tr.running and tr.extra_actions:
+                    tr.bell.set()
 
     def _memory_violation(self, conf):
         """JobTracker.checkMemoryRequirements: a job asking for more memory per
