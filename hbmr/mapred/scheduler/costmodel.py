@@ -38,11 +38,25 @@ class TimeStats:
     probe: str | None = None   # the first attempt on this slot type (profiling probe)
     queued: bool = False       # attempts wait in a queue (GPU): age is not run time
     scale: dict = field(default_factory=dict)     # attempt -> 1/fraction (sampled probes)
+    # the estimate is a ratio of decayed sums (time / tasks), one decay step
+    # per completion event: a single task or a whole batch of GPU tasks (whose
+    # device time is the part of the batch's interval no other batch covered —
+    # hbmr/gpu/busy.py — so the batches of two slot streams alternate large and
+    # small shares; a per-task EWMA that a batch of n tasks stepped n times
+    # tracked the last batch's share alone: 15 µs against 0.25 ms per split)
+    wnum: float = 0.0
+    wden: float = 0.0
+
+    def _decay(self, dt_total: float, n: int, alpha: float):
+        keep = 1.0 - alpha
+        self.wnum = keep * self.wnum + dt_total
+        self.wden = keep * self.wden + n
+        self.ewma = self.wnum / self.wden if self.wden > 0 else 0.0
 
     def add(self, dt: float, alpha: float):
         self.n += 1
         self.total += dt
-        self.ewma = dt if self.n == 1 else (alpha * dt + (1 - alpha) * self.ewma)
+        self._decay(dt, 1, alpha)
         self.min = min(self.min, dt)
         self.max = max(self.max, dt)
 
@@ -114,13 +128,8 @@ class CostModel:
             for a in attempts:
                 pop(a, None)
             if dt_each >= 0 and attempts:
-                # n EWMA steps with the same sample, in closed form
                 n = len(attempts)
-                if st.n == 0:
-                    st.ewma = dt_each
-                else:
-                    keep = (1 - self.alpha) ** n
-                    st.ewma = keep * st.ewma + (1 - keep) * dt_each
+                st._decay(dt_each * n, n, self.alpha)
                 st.n += n
                 st.total += dt_each * n
                 st.min = min(st.min, dt_each)

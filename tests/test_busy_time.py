@@ -65,3 +65,21 @@ def test_old_intervals_are_pruned_but_charges_stay_exact_in_order():
     for k in range(1000):
         total += tl.charge(2 * k, 2 * k + 1)
     assert total == 1000.0 and len(tl._starts) <= 8
+
+
+def test_cost_model_estimate_averages_the_slot_streams_batches():
+    """Two slot streams' batches get alternately most and little of the device
+    time (the union charges each its uncovered part): the estimate must follow
+    the device's throughput per task, not the last batch's share (a per-task
+    EWMA stepped once per task of a batch did)."""
+    from hbmr.mapred.scheduler.costmodel import CostModel
+    cm = CostModel(alpha=0.3)
+    for i in range(20):
+        big = i % 2 == 0
+        ids = [f"b{i}_{j}" for j in range(16)]
+        cm.tasks_started("s", ids, True, 0.0)
+        cm.tasks_finished("s", ids, True, (0.0076 if big else 0.0004) / 16)
+    est, lb = cm.stats("s", True).estimate(0.0)
+    assert not lb
+    per_task = (0.0076 + 0.0004) / 32
+    assert abs(est - per_task) < 0.25 * per_task, (est, per_task)
