@@ -26,6 +26,9 @@ import threading
 from dataclasses import dataclass, field
 
 
+GPU_WINDOW = 64      # tasks per decay step of a batched (GPU) estimate
+
+
 @dataclass
 class TimeStats:
     n: int = 0
@@ -47,8 +50,9 @@ class TimeStats:
     wnum: float = 0.0
     wden: float = 0.0
 
-    def _decay(self, dt_total: float, n: int, alpha: float):
-        keep = 1.0 - alpha
+    def _decay(self, dt_total: float, n: int, alpha: float, per: float = 1.0):
+        # one step of (1 - alpha) per ``per`` tasks
+        keep = (1.0 - alpha) ** (n / per)
         self.wnum = keep * self.wnum + dt_total
         self.wden = keep * self.wden + n
         self.ewma = self.wnum / self.wden if self.wden > 0 else 0.0
@@ -129,7 +133,10 @@ class CostModel:
                 pop(a, None)
             if dt_each >= 0 and attempts:
                 n = len(attempts)
-                st._decay(dt_each * n, n, self.alpha)
+                # a step per GPU_WINDOW tasks: the window spans about a
+                # 128-split job, whose batches' shares sum to its busy time
+                # (a job's last batches alone are charged little)
+                st._decay(dt_each * n, n, self.alpha, GPU_WINDOW)
                 st.n += n
                 st.total += dt_each * n
                 st.min = min(st.min, dt_each)
