@@ -154,6 +154,9 @@ def kmeans_pipes(a):
                "exact": a.exact}
         gpu = torch.cuda.is_available()
         conf = JobConf()
+        # every map of an iteration in flight on the GPU slot (the Pipes child
+        # runs them back to back; 4 = the default left half for a second round)
+        conf.set_int("hbmr.gpu.queue.depth", max(16, a.files))
         with LocalCluster(conf, num_trackers=1, gpus=[[0]] if gpu else None,
                           cpu_slots=0 if gpu else 2, gpu_slots_per_device=1) as cl:
             drv = KP.KMeansPipesDriver(os.path.join(tmp, "work"), os.path.join(tmp, "pts"),

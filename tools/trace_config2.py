@@ -28,6 +28,7 @@ def main():
     KP.write_points(os.path.join(tmp, "pts"), a.points, 128, seed=5, centers=64, files=a.files)
     init = K.initial_centroids(os.path.join(tmp, "pts"), 64, 128)
     conf = JobConf()
+    conf.set_int("hbmr.gpu.queue.depth", max(16, a.files))
     for kv in a.defines:
         k, _, v = kv.partition("=")
         conf.set(k, v)
