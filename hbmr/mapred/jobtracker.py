@@ -88,6 +88,9 @@ class TrackerInfo:
         # attempts here for kills, not every running attempt of the tracker
         self.running_by_job: dict = {}
         self.extra_actions: list = []  # e.g. restart_gpu_worker, sent on the next heartbeat
+        # attempts launched into extra_actions (a staged job's plan) and not yet
+        # delivered: they count in ``running`` but the tracker knows nothing of them
+        self.planned = 0
         # not worth ending a long-poll for (KillJobAction purges of finished
         # jobs): they ride on the next response the tracker gets anyway
         self.lazy_actions: list = []
@@ -1010,14 +1013,16 @@ class JobTracker:
         # staged behind a job that is itself staged: its maps cannot run before
         # two reduces have completed, and a tracker with work running reports
         # each completion (JobTracker.report assigns), which carries the plan:
-        # only the trackers with nothing running are rung — they have no report
-        # coming (one that ran its share of the chain ahead of the others would
-        # otherwise hold the new job's launches until its long-poll expired)
+        # only the trackers with nothing delivered running are rung — they have
+        # no report coming (one that ran its share of the chain ahead of the
+        # others would otherwise hold the new job's launches until its
+        # long-poll expired); attempts of plans still queued for a tracker count
+        # in its running set but not as work it knows of
         if j.staged_on is None or not self.report_assign_expected:
             self._kick()
         else:
             for tr in list(self.trackers.values()):
-                if not tr.running and tr.extra_actions:
+                if tr.extra_actions and len(tr.running) <= tr.planned:
                     tr.bell.set()
 
     def _memory_violation(self, conf):
@@ -1267,6 +1272,7 @@ class JobTracker:
                 if tr.extra_actions:
                     resp["actions"] += tr.extra_actions
                     tr.extra_actions = []
+                    tr.planned = 0
                 if tr.kills:
                     resp["actions"] += [P.kill_task_action(aid) for aid in sorted(tr.kills)]
                     tr.kills.clear()
@@ -1384,6 +1390,7 @@ class JobTracker:
                 actions = pre + actions + [x for x in tr.extra_actions
                                            if x["type"] != "close_gate"]
                 tr.extra_actions = []
+                tr.planned = 0
             resp = {"actions": actions, "interval": self.heartbeat_interval, "more": tr.more}
             if actions and number:
                 # numbered under the lock that drained the tracker's queues:

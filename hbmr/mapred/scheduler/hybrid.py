@@ -345,12 +345,14 @@ class HybridTaskScheduler(TaskScheduler):
             acts = []
             self._stage_maps(tr, jip, depth, acts)
             tr.extra_actions += acts
+            tr.planned += _attempts_in(acts)
         if jip.pending_maps or not jip.reduces or not self._reduces_may_start(jip):
             return
         for tr in trackers:
             acts = []
             self._assign_reduces(tr, jip, tr.status.max_reduce_slots - tr.running_reduce, acts)
             tr.extra_actions += acts
+            tr.planned += _attempts_in(acts)
 
     def _stage_maps(self, tr, jip, depth, actions):
         """Launch a staged job's pending maps that are local to this tracker's
@@ -476,6 +478,12 @@ class HybridTaskScheduler(TaskScheduler):
             next_check = min(next_check, a.start + limit)
         jip._no_straggler_until = next_check
         return None
+
+
+def _attempts_in(acts) -> int:
+    """Attempts a list of launch actions carries."""
+    return sum(len(a["tasks"]) if a["type"] == "launch_batch" else 1 for a in acts
+               if a["type"] in ("launch", "launch_batch"))
 
 
 def _prio(p):

@@ -66,6 +66,10 @@ class Harness:
         self.cached = {nm: [] for nm in self.names}
         self.cpu = 0.0
         self.calls = 0
+        self.park = False
+        self.parked_steps = 0
+        self.rng = None                 # random.Random: trackers step at self.speed[r]
+        self.speed = [1.0] * n
         self.submitted: list[str] = []
         self.finished = 0
         for r, nm in enumerate(self.names):
@@ -124,11 +128,20 @@ class Harness:
 
     def step(self, r):
         """Tracker ``r`` finishes the oldest job it holds work of (its maps'
-        batch and its reduce) and reports it; with nothing held it polls."""
+        batch and its reduce) and reports it; with nothing held it polls —
+        or, with ``park`` (a long-poll modelled), it waits for its bell and
+        only then heartbeats: work left in a parked tracker's queues with its
+        bell unrung is a lost wake-up (the real long-poll would sit it out)."""
         nm = self.names[r]
         jid, w = self._oldest(nm)
         now = time.time()
         if w is None or (not w["maps"] and w["reduce"] is None):
+            tr = self.jt.trackers[nm]
+            if self.park:
+                if not tr.bell.is_set():
+                    self.parked_steps += 1
+                    return
+                tr.bell.clear()
             resp = self._call(self.jt.heartbeat, _status(nm, r, self.n), block=0.0)
             self._apply(nm, resp)
             return
@@ -162,7 +175,8 @@ class Harness:
             if guard > 200 * (jobs + warmup) * self.n:
                 raise RuntimeError("no progress")
             for r in range(self.n):
-                self.step(r)
+                if self.rng is None or self.rng.random() < self.speed[r]:
+                    self.step(r)
             while done < len(self.submitted) and self.jt.jobs[self.submitted[done]].done.is_set():
                 st = self.jt.jobs[self.submitted[done]].status.state
                 if st != "SUCCEEDED":
