@@ -64,10 +64,13 @@ def main():
                     help="CPU rehearsal: simulated GPU slots with this device time per split")
     ap.add_argument("--in-process", action="store_true",
                     help="run the GPU slots inside the tracker process (no worker process)")
-    ap.add_argument("--prefetch", type=int, default=2, metavar="N",
+    ap.add_argument("--prefetch", type=int, default=3, metavar="N",
                     help="keep N iteration jobs submitted ahead, each held by the JobTracker "
                          "until its predecessor succeeds (hbmr.job.depends.on), as a "
-                         "JobControl driver would; 0 submits each after the previous finished")
+                         "JobControl driver would; 0 submits each after the previous finished. "
+                         "3: a new job is staged behind a staged one, so its plan rides on "
+                         "the trackers' reports (no long-poll ring per tracker per job: "
+                         "profiles/r05_control_plane_rehearsal.json)")
     ap.add_argument("--prestage", action=argparse.BooleanOptionalAction, default=True,
                     help="let the JobTracker stage held iteration jobs: their GPU maps wait "
                          "on the device behind the predecessor's reduce (hbmr.job.prestage)")
