@@ -29,12 +29,14 @@ _SORT80 = __import__("os").environ.get("HBMR_TERA_SORT80") == "1"
 # and lo are ordered by the in-place tie fix); HBMR_TERA_TIE_SHIFT overrides
 TIE_SHIFT = int(os.environ.get("HBMR_TERA_TIE_SHIFT", "16"))
 # bits of hi the v4 reduce radix-sorts below a group's common key prefix (the
-# group is a key range: its splitters fix the top bits).  48 = 6 passes.
-# TeraGen keys are printable bytes (95 values of 256), so a 32-bit window
-# leaves runs of equal prefixes longer than the in-place tie fix takes and
-# the group falls back to the full-key path: 0.76 s per 100 GB instead of
-# 0.25 (profiles/r03_terasort_window.json)
-SORT_BITS = int(os.environ.get("HBMR_TERA_SORT_BITS", "48"))
+# group is a key range: its splitters fix the top bits).  40 = 5 passes of 8
+# bits: equal 40-bit prefixes come in pairs or triples among the ~2.5e8 keys of
+# a group even for TeraGen's printable bytes (95 values of 256), ordered by the
+# in-place tie fix — 0.229-0.231 s per 100 GB vs 0.237-0.242 s with 48 bits
+# (profiles/r05_terasort_1gpu.json).  A 32-bit window leaves runs of equal
+# prefixes longer than the tie fix takes and the group falls back to the
+# full-key path: 0.76 s (profiles/r03_terasort_window.json)
+SORT_BITS = int(os.environ.get("HBMR_TERA_SORT_BITS", "40"))
 
 
 def sort_window(hi_range=None):
