@@ -435,3 +435,28 @@ def writable_from(value):
     if isinstance(value, np.ndarray):
         return FloatVectorWritable(value)
     raise TypeError(f"cannot wrap {type(value)} as a Writable")
+
+
+_I32 = struct.Struct(">i")
+
+
+def _text_payload(raw: bytes) -> bytes:
+    n = len(raw)
+    return (_VINT1[n] if n < 128 else encode_vint(n)) + raw
+
+
+def _bytes_payload(raw: bytes) -> bytes:
+    return _I32.pack(len(raw)) + raw
+
+
+def payload_serializer(cls):
+    """raw payload bytes -> ``cls``'s serialised form, for the classes whose
+    Pipes wire form is the bare payload (Text, BytesWritable; BinaryProtocol.
+    writeObject, BinaryProtocol.java:349-369), so a Pipes child's output can be
+    collected without building Writables; None for any other class."""
+    if cls is Text:
+        return _text_payload
+    if cls is BytesWritable:
+        return _bytes_payload
+    return None
+

@@ -860,7 +860,7 @@ class JobTracker:
         if d is None:
             return
         os.makedirs(d, exist_ok=True)
-        tmp = os.path.join(d, "job.json.tmp")
+        tmp = os.path.join(d, f"job.json.{os.getpid()}.{threading.get_ident()}.tmp")
         with open(tmp, "w") as f:
             json.dump({"conf": conf.to_dict(), "submit_time": time.time()}, f)
         os.replace(tmp, os.path.join(d, "job.json"))
@@ -875,7 +875,10 @@ class JobTracker:
         if d is None:
             return
         os.makedirs(d, exist_ok=True)
-        tmp = os.path.join(d, "jobtracker.json.tmp")
+        # a temp name of this writer's own: two JobTrackers (processes, or the
+        # heartbeat threads of one) sharing a system dir must not rename each
+        # other's file away
+        tmp = os.path.join(d, f"jobtracker.json.{os.getpid()}.{threading.get_ident()}.tmp")
         with open(tmp, "w") as f:
             json.dump({"restart_count": self.restart_count, "trackers": len(self.trackers)}, f)
         os.replace(tmp, os.path.join(d, "jobtracker.json"))

@@ -31,6 +31,7 @@ import numpy as np
 from ..io.compress import get_codec
 from ..io.ifile import IFileWriter, SpillRecord, read_segment
 from ..io.serializer import to_bytes
+from ..io.writable import payload_serializer
 from ..utils.reflection import new_instance
 from . import counters as C
 from . import sortbuf
@@ -303,6 +304,42 @@ class MapOutputBuffer(OutputCollector):
         self.buf_bytes += n + 16   # 16 B accounting per record (MapTask.java:890-903)
         if self.buf_bytes >= self.soft_limit:
             self._spill_full()
+
+    def raw_sink(self):
+        """A ``sink(k, v, part)`` taking a Pipes child's OUTPUT frames as they
+        came off the wire (``part``: a PARTITIONED_OUTPUT's partition, else
+        None) and appending their serialised form without building Writables
+        (the uplink's per-record cost) — or None when the key or value class
+        is not one whose wire form is its payload (Text, BytesWritable)."""
+        kser, vser = payload_serializer(self.kcls), payload_serializer(self.vcls)
+        if kser is None or vser is None:
+            return None
+        R, native_hash, kind = self.R, self.native_hash, self.kind
+
+        def sink(k, v, part):
+            kb, vb = kser(k), vser(v)
+            if native_hash:
+                self.keys.append(kb)
+                self.vals.append(vb)
+            else:
+                if part is None:
+                    part = 0 if R == 1 else self.partitioner.getPartition(
+                        self.kcls.deserialize(kb), self.vcls.deserialize(vb), R)
+                if not 0 <= part < R:
+                    raise ValueError(f"Illegal partition for {k!r} ({part})")
+                if kind is not None:
+                    self.keys.append(kb)
+                    self.vals.append(vb)
+                    self.parts.append(part)
+                else:
+                    self.buf.append((part, self.sort_key(kb), kb, vb))
+                self.n_out += 1
+            n = len(kb) + len(vb)
+            self.bytes_out += n
+            self.buf_bytes += n + 16
+            if self.buf_bytes >= self.soft_limit:
+                self._spill_full()
+        return sink
 
     def _spill_full(self):
         """The buffer passed io.sort.spill.percent: hand it to the spill thread."""
@@ -835,12 +872,20 @@ class ReduceTask(Task):
         ends = b.group_ends(kind, perm, 0, b.n).tolist()
         pl = perm.tolist()
         kdes, vdes = kcls.deserialize, vcls.deserialize
+        # a reducer that takes serialised groups (PipesReducer.raw_reduce)
+        # gets them without a Writable built per record
+        rr = getattr(reducer, "raw_reduce", None)
+        rr = rr(kcls, vcls) if rr is not None else None
         try:
             a = 0
             for g, e in enumerate(ends):
                 if (g & 1023) == 1023:
                     self.check_killed()
-                reducer.reduce(kdes(b.key(pl[a])), (vdes(b.value(r)) for r in pl[a:e]), out, rep)
+                if rr is not None:
+                    rr(b.key(pl[a]), [b.value(r) for r in pl[a:e]], out, rep)
+                else:
+                    reducer.reduce(kdes(b.key(pl[a])), (vdes(b.value(r)) for r in pl[a:e]), out,
+                                   rep)
                 a = e
         finally:
             reducer.close()

@@ -869,6 +869,8 @@ class TaskTracker:
     def _run_cpu_map(self, run: _Running):
         spec, js = run.spec, run.job
         run.status.start_time = time.time()
+        if TRACE.on:
+            TRACE.instant("tt.map.start", attempt=spec.attempt_id)
         try:
             if run.kill.is_set():
                 self._finish(run, P.KILLED, "killed before start")

@@ -21,6 +21,7 @@ import tempfile
 import threading
 
 from ..mapred import counters as C
+from . import protocol as _protocol
 from .protocol import DownwardProtocol, UplinkReader, create_digest, from_wire
 
 log = logging.getLogger("hbmr.pipes")
@@ -43,12 +44,23 @@ class OutputHandler:
         self.error = None
         self.progress_value = 0.0
         self.records = 0
+        # a map's output buffer takes the frames as they are (MapOutputBuffer.
+        # raw_sink): no Writable built and re-serialised per record
+        rs = getattr(collector, "raw_sink", None) if _protocol.RAW_FRAMES else None
+        self.sink = rs() if rs is not None else None
 
     def output(self, k, v):
-        self.collector.collect(from_wire(k, self.kcls), from_wire(v, self.vcls))
+        if self.sink is not None:
+            self.sink(k, v, None)
+        else:
+            self.collector.collect(from_wire(k, self.kcls), from_wire(v, self.vcls))
         self.records += 1
 
     def partitioned_output(self, part, k, v):
+        if self.sink is not None:
+            self.sink(k, v, part)
+            self.records += 1
+            return
         if self.partitioner is not None:
             self.partitioner.set_next(part)
         self.output(k, v)

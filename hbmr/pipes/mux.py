@@ -24,6 +24,7 @@ import collections
 import logging
 import threading
 
+from ..utils.trace import TRACE
 from .application import Application, OutputHandler
 
 log = logging.getLogger("hbmr.pipes")
@@ -84,6 +85,8 @@ class _FifoHandler:
         self.boot.authenticate(digest)
 
     def done(self):
+        if TRACE.on:
+            TRACE.instant("pipes.mux.done")
         with self.mux.cond:
             t = self.mux.fifo.popleft() if self.mux.fifo else None
             self.mux.cond.notify_all()
@@ -127,6 +130,8 @@ class MuxChild:
                num_reduces):
         """Queue one map (blocks while ``depth`` maps are in flight)."""
         h = OutputHandler(collector, reporter, key_class, value_class, partitioner)
+        if TRACE.on:
+            TRACE.instant("pipes.mux.submit")
         with self.cond:
             while len(self.fifo) >= self.depth and self.dead is None:
                 self.cond.wait()
@@ -143,8 +148,12 @@ class MuxChild:
                 job.set_boolean("hbmr.pipes.child.reuse", True)
                 self.app.downlink.set_job_conf(job)
                 self.conf_job = jid
+                if TRACE.on:
+                    TRACE.instant("pipes.mux.conf_sent")
             self.app.downlink.run_map(split, num_reduces, False)
             self.maps += 1
+            if TRACE.on:
+                TRACE.instant("pipes.mux.run_map_sent", fifo=len(self.fifo))
         return t
 
     def wait(self, ticket):

@@ -17,6 +17,7 @@ import hashlib
 import hmac
 import io
 import logging
+import os
 import struct
 import threading
 
@@ -62,6 +63,26 @@ def from_wire(raw: bytes, cls):
 
 
 _SMALL_VINTS = [bytes((n,)) for n in range(128)]
+
+# HBMR_PIPES_RAW=0: records go through Writable objects both ways (the byte
+# paths below off; for A/B measurement)
+RAW_FRAMES = os.environ.get("HBMR_PIPES_RAW", "1") != "0"
+
+
+def frame_of_serialized(cls):
+    """``cls``'s serialised bytes -> the VInt-length-prefixed frame its object
+    goes down the pipe as (``_bytes(to_wire(obj))``), without building the
+    object; None for subclasses of Text/BytesWritable (their to_wire differs)."""
+    if not RAW_FRAMES:
+        return None
+    if cls is Text:
+        return lambda s: s          # VInt length + UTF-8 already
+    if cls is BytesWritable:
+        return lambda s: encode_vint(len(s) - 4) + s[4:]
+    if issubclass(cls, (Text, BytesWritable)) or not issubclass(cls, Writable):
+        return None
+    return lambda s: encode_vint(len(s)) + s
+
 
 class DownwardProtocol:
     def __init__(self, sock):
@@ -139,6 +160,16 @@ class DownwardProtocol:
         with self._lock:
             self._int(REDUCE_VALUE)
             self._bytes(to_wire(value))
+
+    def reduce_group(self, key_frame: bytes, value_frames: list):
+        """REDUCE_KEY and the REDUCE_VALUEs of one key group in one write
+        (frames as made by :func:`frame_of_serialized`)."""
+        sep = _SMALL_VINTS[REDUCE_VALUE]
+        msg = _SMALL_VINTS[REDUCE_KEY] + key_frame
+        if value_frames:
+            msg += sep + sep.join(value_frames)
+        with self._lock:
+            self.out.write(msg)
 
     def end_of_input(self):
         with self._lock:

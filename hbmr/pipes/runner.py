@@ -22,6 +22,7 @@ from ..mapred.api import InputFormat, MapRunnable, Partitioner, RecordReader, Re
 from ..mapred.formats import FileSplit
 from ..utils.reflection import load_class, new_instance
 from .application import POOL, Application
+from .protocol import frame_of_serialized
 
 JAVA_RR = "hadoop.pipes.java.recordreader"
 JAVA_MAPPER = "hadoop.pipes.java.mapper"
@@ -188,6 +189,22 @@ class PipesReducer(Reducer):
         for v in values:
             d.reduce_value(v)
         reporter.progress()
+
+    def raw_reduce(self, key_class, value_class):
+        """``reduce`` over serialised records (ReduceTask's native merge path):
+        each key group goes down as one write of ready-made frames, no
+        Writable built per value; None when a class's frame needs its object."""
+        kf, vf = frame_of_serialized(key_class), frame_of_serialized(value_class)
+        if kf is None or vf is None:
+            return None
+
+        def reduce_raw(kb, vbs, output, reporter):
+            if self.app is None:
+                self.reporter = reporter
+                self._start(output, reporter)
+            self.app.downlink.reduce_group(kf(kb), [vf(v) for v in vbs])
+            reporter.progress()
+        return reduce_raw
 
     def close(self):
         if self.app is None:

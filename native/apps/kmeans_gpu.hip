@@ -29,7 +29,9 @@
 
 #include <sys/stat.h>
 
+#include <cstdio>
 #include <cstdlib>
+#include <ctime>
 #include <map>
 #include <stdexcept>
 
@@ -53,6 +55,20 @@
 namespace {
 
 constexpr int kNbrL = 256;     // exact mode's neighbour lists (hbmr.ops.kmeans.NBR_L)
+
+// HBMR_PIPES_TRACE=<file>: "<wall seconds> <event>" lines appended per map
+// phase (tools/trace_config2.py merges them into the tracker's timeline)
+void tmark(const char* what) {
+  static FILE* f = [] {
+    const char* p = std::getenv("HBMR_PIPES_TRACE");
+    return p && *p ? std::fopen(p, "a") : nullptr;
+  }();
+  if (!f) return;
+  timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  std::fprintf(f, "%lld.%09ld child.%s\n", (long long)ts.tv_sec, ts.tv_nsec, what);
+  std::fflush(f);
+}
 
 // A device buffer that only grows.
 struct DevBuf {
@@ -178,6 +194,7 @@ class SplitDescReader : public HadoopPipes::RecordReader {
 class KMeansGpuMapper : public HadoopPipes::Mapper {
  public:
   explicit KMeansGpuMapper(HadoopPipes::TaskContext& ctx) : p_(ctx.getJobConf()) {
+    tmark("mapper.ctor");
     int device = HadoopPipes::getGPUDeviceId();
     if (device < 0) device = 0;
     DeviceState& S = state();
@@ -190,6 +207,7 @@ class KMeansGpuMapper : public HadoopPipes::Mapper {
       throw std::runtime_error("exact mode wants d % 8 == 0 and d <= 128");
     kpad_ = hbmr_kmeans_padded_k(p_.k);
     image(S);
+    tmark("mapper.ready");
     points_ = ctx.getCounter("KMEANS", "POINTS");
     gpu_ = ctx.getCounter("KMEANS", "GPU_MAPS");
     hits_ = ctx.getCounter("KMEANS", "GPU_SPLIT_CACHE_HITS");
@@ -197,42 +215,56 @@ class KMeansGpuMapper : public HadoopPipes::Mapper {
     relabelled_ = ctx.getCounter("KMEANS", "EXACT_RELABELLED_POINTS");
   }
 
-  // The job's centroid image, built on the first map of the job.
+  // The job's centroid image, built on the first map of the job — into the
+  // previous job's buffers when the shapes match (an iteration chain): a
+  // hipFree synchronises the device, and freeing and re-allocating the eleven
+  // buffers per job cost milliseconds before the job's first map
   void image(DeviceState& S) {
     const std::string key = file_key(p_.centroids) + (exact_ ? "|x" : "|b");
     CentroidImage& I = S.img;
     if (I.key == key) return;
-    I.release();
     const std::vector<float> c = kmp::load_centroids(p_.centroids, p_.k, p_.d);
-    I.k = p_.k;
-    I.d = p_.d;
-    I.dp = dp_;
-    I.kpad = kpad_;
-    I.exact = exact_;
-    I.cen = static_cast<float*>(dalloc(sizeof(float) * c.size()));
+    tmark("image.loaded");
+    const bool reuse = I.cen != nullptr && I.k == p_.k && I.d == p_.d && I.dp == dp_ &&
+                       I.kpad == kpad_ && I.exact == exact_;
+    if (!reuse) {
+      I.release();
+      I.k = p_.k;
+      I.d = p_.d;
+      I.dp = dp_;
+      I.kpad = kpad_;
+      I.exact = exact_;
+      I.cen = static_cast<float*>(dalloc(sizeof(float) * c.size()));
+      I.chalf = static_cast<float*>(dalloc(sizeof(float) * kpad_));
+      if (!exact_) {
+        I.cbf = dalloc(2 * (size_t)kpad_ * dp_);
+      } else {
+        I.c16 = dalloc(2 * (size_t)kpad_ * dp_);
+        I.c16t = dalloc(2 * (size_t)kpad_ * dp_);
+        I.cnorm = static_cast<float*>(dalloc(sizeof(float) * p_.k));
+        I.cerr = static_cast<float*>(dalloc(sizeof(float) * p_.k));
+        I.maxima = static_cast<float*>(dalloc(sizeof(float) * 2));
+        I.L = std::min(kNbrL, p_.k);
+        I.nbr_i = static_cast<int32_t*>(dalloc(sizeof(int32_t) * (size_t)p_.k * I.L));
+        I.nbr_d = static_cast<float*>(dalloc(sizeof(float) * (size_t)p_.k * I.L));
+        I.pd = static_cast<float*>(dalloc(sizeof(float) * (size_t)p_.k * p_.k));
+      }
+    }
+    I.key.clear();
     HIP_OK(hipMemcpyAsync(I.cen, c.data(), sizeof(float) * c.size(), hipMemcpyHostToDevice, S.st));
-    I.chalf = static_cast<float*>(dalloc(sizeof(float) * kpad_));
     if (!exact_) {
-      I.cbf = dalloc(2 * (size_t)kpad_ * dp_);
       HIP_OK(hipMemsetAsync(I.cbf, 0, 2 * (size_t)kpad_ * dp_, S.st));
       // sums/counts == NULL: rebuild the bf16 image and -|c|²/2 from cen
       LIB_OK(hbmr_kmeans_update(nullptr, nullptr, p_.fx, p_.k, p_.d, dp_, kpad_, I.cen, I.cbf,
                                 I.chalf, nullptr, S.st));
     } else {
-      I.c16 = dalloc(2 * (size_t)kpad_ * dp_);
-      I.c16t = dalloc(2 * (size_t)kpad_ * dp_);
-      I.cnorm = static_cast<float*>(dalloc(sizeof(float) * p_.k));
-      I.cerr = static_cast<float*>(dalloc(sizeof(float) * p_.k));
-      I.maxima = static_cast<float*>(dalloc(sizeof(float) * 2));
       LIB_OK(hbmr_kmeans_image16(I.cen, p_.k, p_.d, dp_, kpad_, 1, I.c16, I.chalf, I.cnorm,
                                  I.cerr, I.maxima, S.st));
       LIB_OK(hbmr_kmeans_image16_tiled(I.c16, kpad_, dp_, I.c16t, S.st));
-      I.L = std::min(kNbrL, p_.k);
-      I.nbr_i = static_cast<int32_t*>(dalloc(sizeof(int32_t) * (size_t)p_.k * I.L));
-      I.nbr_d = static_cast<float*>(dalloc(sizeof(float) * (size_t)p_.k * I.L));
-      I.pd = static_cast<float*>(dalloc(sizeof(float) * (size_t)p_.k * p_.k));
       LIB_OK(hbmr_kmeans_centroid_nbr(I.cen, p_.k, p_.d, I.L, I.nbr_i, I.nbr_d, I.pd, S.st));
     }
+    // (the host vector c dies at return: the copy must have left it)
+    HIP_OK(hipStreamSynchronize(S.st));
     I.key = key;
   }
 
@@ -295,6 +327,7 @@ class KMeansGpuMapper : public HadoopPipes::Mapper {
   void map(HadoopPipes::MapContext& ctx) override {
     DeviceState& S = state();
     const CentroidImage& I = S.img;
+    tmark("map.start");
     const CachedSplit& cs = split(ctx.getInputKey());
     const long n = cs.n;
     std::vector<long long> sums((size_t)p_.k * dp_), counts((size_t)p_.k);
@@ -343,6 +376,7 @@ class KMeansGpuMapper : public HadoopPipes::Mapper {
                             S.st));
       HIP_OK(hipStreamSynchronize(S.st));
     }
+    tmark("map.device_done");
     if (tmp_.n || tmp_.xb || tmp_.x32) tmp_.release();   // an uncached split
     kmp::emit_partials(ctx, p_.k, p_.d, reinterpret_cast<const int64_t*>(sums.data()), dp_,
                        reinterpret_cast<const int64_t*>(counts.data()));

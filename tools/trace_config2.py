@@ -25,6 +25,8 @@ def main():
     from hbmr.models import kmeans_pipes as KP
     from hbmr.utils.trace import TRACE
     tmp = tempfile.mkdtemp(prefix="hbmr-trace2-")
+    child_trace = os.path.join(tmp, "child.trace")
+    os.environ["HBMR_PIPES_TRACE"] = child_trace      # the GPU child's phase marks
     KP.write_points(os.path.join(tmp, "pts"), a.points, 128, seed=5, centers=64, files=a.files)
     init = K.initial_centroids(os.path.join(tmp, "pts"), 64, 128)
     conf = JobConf()
@@ -43,12 +45,23 @@ def main():
             print("warm-up iteration", round(time.perf_counter() - t, 4), flush=True)
         TRACE.enable()
         TRACE.clear()
+        skip = os.path.getsize(child_trace) if os.path.exists(child_trace) else 0
         t = time.perf_counter()
         drv.step()
         print("traced iteration", round(time.perf_counter() - t, 4), flush=True)
         TRACE.disable()
+    from hbmr.utils.trace import wall_ns
+    events = list(TRACE.events)
+    if os.path.exists(child_trace):
+        off = wall_ns(0)                  # child wall clock -> this process's perf clock
+        with open(child_trace) as f:
+            f.seek(skip)
+            for line in f:
+                w, _, name = line.strip().partition(" ")
+                events.append((int(float(w) * 1e9) - off, "pipes-child", "i", name, 0, {}))
+    events.sort(key=lambda e: e[0])
     t0 = TRACE.events[0][0]
-    for ts, th, ph, name, dur, args in TRACE.events:
+    for ts, th, ph, name, dur, args in events:
         if name in ("jt.heartbeat",):
             continue
         print(f"{(ts - t0) / 1e6:9.3f} ms {dur / 1e6:7.3f} {th[:24]:>24} {name:<22} "
