@@ -98,7 +98,11 @@ class DataNode:
         out = []
         for fn in os.listdir(self.dir):
             if fn.startswith("blk_") and not fn.endswith((".meta", ".tmp")):
-                out.append([int(fn[4:]), os.path.getsize(os.path.join(self.dir, fn))])
+                try:
+                    size = os.path.getsize(os.path.join(self.dir, fn))
+                except FileNotFoundError:
+                    continue        # deleted (an invalidation) since the listing
+                out.append([int(fn[4:]), size])
         return out
 
     def _crcs(self, data: bytes) -> bytes:

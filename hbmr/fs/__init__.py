@@ -11,6 +11,7 @@ from __future__ import annotations
 import glob as _glob
 import os
 import shutil
+import stat
 from dataclasses import dataclass
 
 DEFAULT_BLOCK_SIZE = 64 * 1024 * 1024  # dfs.block.size default (hdfs-default.xml:259-260)
@@ -98,7 +99,7 @@ class LocalFileSystem:
     def get_file_status(self, path) -> FileStatus:
         p = strip_scheme(path)
         st = os.stat(p)
-        return FileStatus(p, st.st_size, os.path.isdir(p), self.block_size, st.st_mtime)
+        return FileStatus(p, st.st_size, stat.S_ISDIR(st.st_mode), self.block_size, st.st_mtime)
 
     getFileStatus = get_file_status  # noqa: N815
 
@@ -113,10 +114,15 @@ class LocalFileSystem:
         if not os.path.isdir(p):
             return [self.get_file_status(p)]
         out = []
-        for name in sorted(os.listdir(p)):
-            if filter_hidden and hidden(name):
+        # one stat per entry (DirEntry.stat follows links like os.stat)
+        with os.scandir(p) as it:
+            ents = sorted(it, key=lambda e: e.name)
+        for e in ents:
+            if filter_hidden and hidden(e.name):
                 continue
-            out.append(self.get_file_status(os.path.join(p, name)))
+            st = e.stat()
+            out.append(FileStatus(os.path.join(p, e.name), st.st_size, stat.S_ISDIR(st.st_mode),
+                                  self.block_size, st.st_mtime))
         return out
 
     listStatus = list_status  # noqa: N815
@@ -206,6 +212,27 @@ def fopen(path, mode="rb", buffering=-1, conf=None):
         fs = get_fs(path, conf)
         return fs.open(path) if "r" in mode else fs.create(path)
     return open(strip_scheme(path), mode, buffering=buffering)
+
+
+def mkdirs_fast(path):
+    """os.makedirs for the common case that only the last level or two are
+    missing: mkdir from the deepest level up as needed, no stat per level
+    (os.makedirs stats every parent first)."""
+    try:
+        os.mkdir(path)
+        return
+    except FileExistsError:
+        if os.path.isdir(path):
+            return
+        raise
+    except FileNotFoundError:
+        pass
+    mkdirs_fast(os.path.dirname(path))
+    try:
+        os.mkdir(path)
+    except FileExistsError:
+        if not os.path.isdir(path):
+            raise
 
 
 def makedirs(path):

@@ -13,8 +13,10 @@ three big-endian longs, followed by an 8-byte CRC32 of the index entries.
 """
 from __future__ import annotations
 
+import collections
 import io
 import struct
+import threading
 import zlib
 
 from .vint import decode_vint, encode_vint
@@ -101,6 +103,7 @@ class SpillRecord:
     def write(self, path):
         with open(path, "wb") as f:
             f.write(self.to_bytes())
+        _remember(path, self)
 
     @classmethod
     def from_bytes(cls, data: bytes) -> "SpillRecord":
@@ -113,8 +116,36 @@ class SpillRecord:
 
     @classmethod
     def read(cls, path) -> "SpillRecord":
+        got = _INDEX_CACHE.get(path)
+        if got is not None:
+            return got
         with open(path, "rb") as f:
             return cls.from_bytes(f.read())
+
+
+# The spill indexes this process wrote, by path: a reduce in the same process
+# as its maps (a tracker's reduce of its own maps' outputs) finds them here
+# instead of re-reading each map's .index file (map output paths are unique
+# per attempt and never rewritten in place).  Bounded by partition entries.
+_INDEX_CACHE: "collections.OrderedDict[str, SpillRecord]" = collections.OrderedDict()
+_INDEX_CACHE_ENTRIES = [0]
+_INDEX_CACHE_MAX = 1 << 18
+_INDEX_LOCK = threading.Lock()
+
+
+def _remember(path, rec):
+    n = len(rec.entries)
+    if n > _INDEX_CACHE_MAX // 64:
+        return
+    with _INDEX_LOCK:
+        old = _INDEX_CACHE.pop(path, None)
+        if old is not None:
+            _INDEX_CACHE_ENTRIES[0] -= len(old.entries)
+        _INDEX_CACHE[path] = rec
+        _INDEX_CACHE_ENTRIES[0] += n
+        while _INDEX_CACHE_ENTRIES[0] > _INDEX_CACHE_MAX:
+            _p, r = _INDEX_CACHE.popitem(last=False)
+            _INDEX_CACHE_ENTRIES[0] -= len(r.entries)
 
 
 def read_partition(path, index: SpillRecord, part: int, codec=None):

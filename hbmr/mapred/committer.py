@@ -69,9 +69,12 @@ class FileOutputCommitter(OutputCommitter):
             F.rmtree(os.path.join(out, TEMP_DIR))
 
     def setup_task(self, job, attempt):
-        wp = self.work_path(job, attempt)
-        if wp:
-            F.makedirs(wp)
+        # nothing, as in FileOutputCommitter.setupTask (FileOutputCommitter.java
+        # :115-119): the attempt's work dir is made on demand by the first writer
+        # (every RecordWriter makes its parent directories); a map whose output
+        # goes to its local map-output files never creates one, which saves the
+        # mkdir here and the listdir in needs_task_commit per map
+        pass
 
     def needs_task_commit(self, job, attempt) -> bool:
         wp = self.work_path(job, attempt)

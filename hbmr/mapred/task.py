@@ -28,13 +28,14 @@ import time
 
 import numpy as np
 
+from ..fs import mkdirs_fast
 from ..io.compress import get_codec
 from ..io.ifile import IFileWriter, SpillRecord, read_segment
 from ..io.serializer import to_bytes
 from ..io.writable import payload_serializer
 from ..utils.reflection import new_instance
 from . import counters as C
-from . import sortbuf
+from . import mapoutput, sortbuf
 from .api import OutputCollector, Reporter
 from .committer import FileOutputCommitter
 from .formats import FileSplit
@@ -234,7 +235,13 @@ class MapOutputBuffer(OutputCollector):
                                        "org.apache.hadoop.io.compress.DefaultCodec")) \
             if job.get_compress_map_output() else None
         self.out_dir = out_dir
-        os.makedirs(out_dir, exist_ok=True)
+        self._dir_made = False
+        # a small single-spill output stays in this process's memory when the
+        # tracker's reduces read here (hbmr/mapred/mapoutput.py)
+        self.mem_max = job.get_long(mapoutput.MAX_KEY, 4 << 20) \
+            if getattr(task, "memory_outputs", False) else 0
+        self.mem_total = job.get_long(mapoutput.TOTAL_KEY, 256 << 20)
+        self._to_memory = False
         # native sort path (hbmr/mapred/sortbuf.py): serialised records only,
         # partition + sort + group + IFile encode per spill in C++
         self.kind = sortbuf.key_kind(job)
@@ -255,6 +262,43 @@ class MapOutputBuffer(OutputCollector):
         self.spill_async = job.get_boolean("hbmr.map.spill.async", True)
         self._spill_thread = None
         self._spill_error = None
+        self._direct_final = False
+
+    def _spill_path(self, idx):
+        # a map's only spill is written under the final name (no rename pair)
+        return os.path.join(self.out_dir, "file.out" if self._direct_final else f"spill{idx}.out")
+
+    def _ensure_dir(self):
+        if not self._dir_made:
+            # the attempt's dir, then its output dir: two mkdirs (os.makedirs
+            # stats every level first)
+            mkdirs_fast(os.path.dirname(self.out_dir))
+            mkdirs_fast(self.out_dir)
+            self._dir_made = True
+
+    def _open_spill(self, path):
+        """A spill's target: its file, or a buffer for an in-memory output."""
+        if self._to_memory:
+            return io.BytesIO()
+        self._ensure_dir()
+        return open(path, "wb")
+
+    def _commit_spill(self, path, f, rec):
+        """Close a spill: its index file next to it, or both held in memory
+        (a store over its cap gets the files after all)."""
+        if self._to_memory:
+            data = f.getvalue()
+            if mapoutput.STORE.put(path, data, rec, self.mem_total):
+                return
+            self._ensure_dir()
+            with open(path, "wb") as out:
+                out.write(data)
+            size = len(data)
+        else:
+            size = f.tell()
+            f.close()
+        rec.write(path + ".index")
+        _fs_written(path, size)
 
     def collect(self, key, value):
         if not isinstance(key, self.kcls):
@@ -394,10 +438,11 @@ class MapOutputBuffer(OutputCollector):
         self.task.check_killed()
         parts = self._sorted_partitions(buf, self.R)
         idx = len(self.spills)
-        path = os.path.join(self.out_dir, f"spill{idx}.out")
+        path = self._spill_path(idx)
         rec = SpillRecord(self.R)
         spilled = 0
-        with open(path, "wb") as f:
+        f = self._open_spill(path)
+        try:
             for p in range(self.R):
                 recs = parts[p]
                 if self.combiner_cls is not None and recs:
@@ -408,9 +453,11 @@ class MapOutputBuffer(OutputCollector):
                     w.append(kb, vb)
                 spilled += len(recs)
                 rec.put(p, *w.close())
-        rec.write(path + ".index")
+        except BaseException:
+            f.close()
+            raise
+        self._commit_spill(path, f, rec)
         self.spills.append((path, rec))
-        _fs_written(path)
         self.reporter.incrCounter(C.TASK_GROUP, C.SPILLED_RECORDS, spilled)
 
     # -- native path ------------------------------------------------------------------------
@@ -448,10 +495,11 @@ class MapOutputBuffer(OutputCollector):
         starts = np.zeros(self.R + 1, np.int64)
         np.cumsum(np.bincount(part, minlength=self.R), out=starts[1:])
         idx = len(self.spills)
-        path = os.path.join(self.out_dir, f"spill{idx}.out")
+        path = self._spill_path(idx)
         rec = SpillRecord(self.R)
         spilled = 0
-        with open(path, "wb") as f:
+        f = self._open_spill(path)
+        try:
             for p in range(self.R):
                 lo, hi = int(starts[p]), int(starts[p + 1])
                 if self.combiner_cls is not None and hi > lo:
@@ -460,9 +508,11 @@ class MapOutputBuffer(OutputCollector):
                     body, nrec = b.ifile_body(perm, lo, hi), hi - lo
                 spilled += nrec
                 rec.put(p, *sortbuf.write_segment(f, body, self.codec))
-        rec.write(path + ".index")
+        except BaseException:
+            f.close()
+            raise
+        self._commit_spill(path, f, rec)
         self.spills.append((path, rec))
-        _fs_written(path)
         self.reporter.incrCounter(C.TASK_GROUP, C.SPILLED_RECORDS, spilled)
 
     def _merge_parts_native(self, final):
@@ -498,12 +548,20 @@ class MapOutputBuffer(OutputCollector):
 
     def flush(self):
         """Final spill + merge into file.out / file.out.index."""
-        self.sort_and_spill()      # waits for a running background spill first
+        self._wait_spill()
         final = os.path.join(self.out_dir, "file.out")
+        self._direct_final = not self.spills
+        self._to_memory = self._direct_final and 0 < self.mem_max and \
+            self.buf_bytes <= self.mem_max
+        try:
+            self.sort_and_spill()
+        finally:
+            self._direct_final = self._to_memory = False
         if len(self.spills) == 1:
             path, rec = self.spills[0]
-            os.replace(path, final)
-            os.replace(path + ".index", final + ".index")
+            if path != final:
+                os.replace(path, final)
+                os.replace(path + ".index", final + ".index")
         elif self.kind is not None:
             self._merge_parts_native(final)
         else:
@@ -546,11 +604,11 @@ class MapOutputBuffer(OutputCollector):
         self.reporter.incrCounter(C.TASK_GROUP, C.SPILLED_RECORDS, spilled)
 
 
-def _fs_written(path):
+def _fs_written(path, size=None):
     """Local bytes a task wrote (FILE_BYTES_WRITTEN via FileSystem statistics)."""
     from ..fs import STATS
     try:
-        STATS.add("file", written=os.path.getsize(path))
+        STATS.add("file", written=os.path.getsize(path) if size is None else size)
     except OSError:
         pass
 
@@ -696,6 +754,11 @@ class MapOutputLocation:
     def read_partition(self, part):
         if self.fetch is not None:
             return self.fetch(part)
+        held = mapoutput.STORE.get(self.path) if self.path else None
+        if held is not None:            # an in-memory map output of this process
+            data, idx = held
+            start, _raw, plen = idx.get(part)
+            return data[start:start + plen]
         idx = SpillRecord.read(self.path + ".index")
         start, _raw, plen = idx.get(part)
         with open(self.path, "rb") as f:

@@ -26,6 +26,7 @@ import os
 import queue
 import random
 import re
+import shutil
 import socket
 import sys
 import threading
@@ -34,6 +35,7 @@ import traceback
 
 from ..utils.reflection import load_class, new_instance
 from . import counters as C
+from . import mapoutput
 from . import protocol as P
 from .ids import TaskAttemptID
 from .jobconf import JobConf
@@ -745,11 +747,31 @@ class TaskTracker:
         elif typ == "shutdown":
             self._stop.set()
 
+    def _memory_outputs(self) -> bool:
+        """Map outputs may stay in memory (hbmr/mapred/mapoutput.py) when every
+        reduce that reads them runs in this process: the JobTracker is this
+        process's own (a LocalCluster's trackers share it), not an RPC proxy,
+        and the job's tasks run in this process (a job with child-process
+        tasks never reaches the in-process MapTask that asks)."""
+        m = self.__dict__.get("_mem_out")
+        if m is None:
+            from .jobtracker import JobTracker
+            m = self._mem_out = isinstance(self.jt, JobTracker)
+        return m
+
     def _handle_kill_job(self, act):
         """KillJobAction: the job is finished or killed; purge its state here
-        and in the GPU worker (held device map outputs, worker JobState)."""
+        and in the GPU worker (held device map outputs, worker JobState), its
+        in-memory map outputs and (purgeJob / removeJobFiles) its local dir."""
         jid = act["job_id"]
+        jdir = os.path.join(self.local_dir, jid)
+        mapoutput.STORE.drop_prefix(jdir + os.sep)
         js = self.jobs.pop(jid, None)
+        if js is not None and os.path.isdir(jdir) and \
+                not js.conf.get_boolean("keep.failed.task.files", False) and \
+                not js.conf.get("keep.task.files.pattern"):
+            threading.Thread(target=shutil.rmtree, args=(jdir, True), daemon=True,
+                             name=f"{self.name}-purge").start()
         with self._lock:
             self._gated_jobs.discard(jid)
             self._expect_jobs.discard(jid)
@@ -888,6 +910,7 @@ class TaskTracker:
             split = _split_from_dict(spec.split)
             aid = TaskAttemptID.for_name(spec.attempt_id)
             task = MapTask(js.conf, aid, spec.partition, split)
+            task.memory_outputs = self._memory_outputs()
             task.setRunOnGPU(spec.run_on_gpu)
             task.setGPUDeviceId(spec.gpu_device_id)
             task.kill_event = run.kill

@@ -184,7 +184,8 @@ class MuxRegistry:
                 m.close()
                 m = None
             if m is None:
-                m = self._children[key] = MuxChild(job, executable, device, work_dir, depth)
+                wd = work_dir() if callable(work_dir) else work_dir
+                m = self._children[key] = MuxChild(job, executable, device, wd, depth)
             return m
 
     def close_all(self):

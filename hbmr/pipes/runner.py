@@ -147,8 +147,10 @@ class PipesGPUMapRunner(PipesMapRunner):
             return super().run(reader, output, reporter)
         part = getattr(output, "partitioner", None)
         partitioner = part if isinstance(part, PipesPartitioner) else None
+        # (the work dir is made only when a child is started: one per child,
+        # not a directory per map)
         child = mux.REGISTRY.get(job, self.executable(), self.device(),
-                                 _work_dir(job, f"gpumux{self.device()}"),
+                                 lambda: _work_dir(job, f"gpumux{self.device()}"),
                                  job.get_int(mux.DEPTH, 8))
         t = child.submit(job, output, reporter, job.get_map_output_key_class(),
                          job.get_map_output_value_class(), partitioner, _split_bytes(reporter),

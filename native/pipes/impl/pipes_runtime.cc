@@ -18,6 +18,7 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <pthread.h>
+#include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -729,7 +730,10 @@ bool runTask(const Factory& factory) {
       const string outName = string(file) + ".out";
       out = fopen(outName.c_str(), "wb");
     } else {
-      // text protocol on stdin/stdout through the bridge threads
+      // text protocol on stdin/stdout through the bridge threads; a write to a
+      // bridge pipe whose other end has closed (the task ended while a bridge
+      // still had bytes in flight) must fail with EPIPE, not kill the process
+      signal(SIGPIPE, SIG_IGN);
       int down[2], up[2];
       HADOOP_ASSERT(pipe(down) == 0 && pipe(up) == 0, "pipe() failed");
       static BridgeFds fds;

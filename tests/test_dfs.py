@@ -147,7 +147,11 @@ def test_wordcount_over_hdfs_with_data_local_maps(tmp_path):
                 f.write(("\n".join(lines) + "\n").encode())
             for ln in lines:
                 cnt.update(ln.split())
-        with LocalCluster(JobConf(), num_trackers=2, cpu_slots=2, hosts=hosts) as cl:
+        cc = JobConf()
+        # delay scheduling long enough that a loaded host (pytest -n 8) does
+        # not hand a tracker the other node's blocks before that one asks
+        cc.set_int("hbmr.locality.wait.ms", 3000)
+        with LocalCluster(cc, num_trackers=2, cpu_slots=2, hosts=hosts) as cl:
             # the per-record mapper: maps long enough that each tracker is
             # offered its own blocks before the other could take them
             wc = JobConf()

@@ -21,14 +21,21 @@ PROFS = []
 _run = threading.Thread.run
 
 
-def _profiled_run(self):
-    pr = cProfile.Profile()
-    pr.enable()
-    try:
-        _run(self)
-    finally:
-        pr.disable()
+def _profiled(run):
+    def wrapped(self):
+        pr = cProfile.Profile()
+        # registered up front: pool workers outlive the cluster (their stats are
+        # read while they idle)
         PROFS.append(pr)
+        pr.enable()
+        try:
+            run(self)
+        finally:
+            pr.disable()
+    return wrapped
+
+
+_profiled_run = _profiled(_run)
 
 
 def main():
@@ -49,6 +56,8 @@ def main():
     conf = JobConf()
     conf.set_int("hbmr.gpu.queue.depth", max(16, a.files))
     threading.Thread.run = _profiled_run
+    from hbmr.pipes.protocol import UplinkReader
+    UplinkReader.run = _profiled(UplinkReader.run)     # overrides Thread.run
     main_pr = cProfile.Profile()
     with LocalCluster(conf, num_trackers=1, gpus=[[0]] if a.gpu else None,
                       cpu_slots=0 if a.gpu else 2, gpu_slots_per_device=1) as cl:
