@@ -45,6 +45,7 @@ class LocalCluster:
                              reduce_slots=reduce_slots, gpu_slots_per_device=gpu_slots_per_device,
                              comm=comms[i], local_dir=f"{self.local_dir}/tt{i}",
                              host=hosts[i] if hosts else None)
+            tt.all_trackers_local = True
             self.trackers.append(tt)
         for tt in self.trackers:
             tt.start()

@@ -109,6 +109,8 @@ class Node:
                               name=f"tracker_{socket.gethostname()}_r{self.rank}", rank=self.rank,
                               world_size=self.world, gpu_devices=gpus, comm=self.comm,
                               worker_comm=worker_comm)
+        # one rank with its JobTracker in this process: every reduce reads here
+        self.tt.all_trackers_local = self.world == 1 and not self.jt_process
         self.tt.start()
         if self.jt is not None:
             if not self.jt.wait_for_trackers(self.world, timeout=300):

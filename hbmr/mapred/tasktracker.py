@@ -747,17 +747,15 @@ class TaskTracker:
         elif typ == "shutdown":
             self._stop.set()
 
+    #: every tracker that can run a reduce of this tracker's maps lives in this
+    #: process (set by LocalCluster, and by a one-rank node): only then may map
+    #: outputs stay in memory (hbmr/mapred/mapoutput.py).  A tracker of a
+    #: multi-rank node has reduces in other processes reading its files, even
+    #: when its JobTracker is in-process (rank 0 below 8 ranks).
+    all_trackers_local = False
+
     def _memory_outputs(self) -> bool:
-        """Map outputs may stay in memory (hbmr/mapred/mapoutput.py) when every
-        reduce that reads them runs in this process: the JobTracker is this
-        process's own (a LocalCluster's trackers share it), not an RPC proxy,
-        and the job's tasks run in this process (a job with child-process
-        tasks never reaches the in-process MapTask that asks)."""
-        m = self.__dict__.get("_mem_out")
-        if m is None:
-            from .jobtracker import JobTracker
-            m = self._mem_out = isinstance(self.jt, JobTracker)
-        return m
+        return self.all_trackers_local
 
     def _handle_kill_job(self, act):
         """KillJobAction: the job is finished or killed; purge its state here

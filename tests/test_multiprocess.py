@@ -33,6 +33,8 @@ def test_two_process_kmeans_matches_single_process():
     res = json.loads(lines[0][7:])
     assert res["points"] == 6000 and res["trackers"] == 2
     assert len(res["map_trackers"]) == 2      # locality spread maps over both processes
+    # a classic job whose reduces (in both processes) read the other's map outputs
+    assert res["wordcount_ok"] and len(res["wordcount_reduce_trackers"]) == 2
     # same answer as one in-process tracker: fixed-point partials are exact
     conf = JobConf()
     with LocalCluster(conf, num_trackers=1) as cl:
