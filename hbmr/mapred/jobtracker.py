@@ -1917,11 +1917,20 @@ class JobTracker:
             # only maps launched on this tracker can have outputs here (a TIP
             # re-run elsewhere is listed under that tracker too); map order
             tips = jip.launched_on.get(tracker_name, ())
+            live = _LIVE
             for t in sorted(dict.fromkeys(tips), key=_PARTITION):
                 a = t.successful
                 if a is None and expect:
-                    ra = t.running_attempts()
-                    a = ra[0] if len(ra) == 1 else None
+                    # the single running attempt (running_attempts() inlined:
+                    # this runs per map of every staged job's plan)
+                    at = t.attempts
+                    if len(at) == 1:
+                        for a in at.values():
+                            if a.state not in live:
+                                a = None
+                    else:
+                        ra = [x for x in at.values() if x.state in live]
+                        a = ra[0] if len(ra) == 1 else None
                 if a is not None and a.tracker == tracker_name:
                     out.append([t.tid._s, a.aid, a.output or {}])
             return out
