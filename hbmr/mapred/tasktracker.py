@@ -220,6 +220,10 @@ class TaskTracker:
         self._polling = False       # the heartbeat thread is in a long-poll
         self._requeued: list = []   # drained statuses whose report failed
         self._notify_seq = 0                 # wakeup() notifications sent (notify_seq)
+        # one report in flight at a time: a task finishing meanwhile leaves its
+        # news to that reporter's next round (coalesced, not one call each)
+        self._reporting = False
+        self._report_again = False
         self._lost: list[str] = []           # succeeded attempts whose output was lost
         self._worker_lost = False            # GPU worker died: the gang must restart
         self._news = threading.Event()
@@ -495,27 +499,58 @@ class TaskTracker:
             self._notify_seq += 1
             seq = self._notify_seq
             polling = self._polling
+            if polling and self.report_news and self._reporting:
+                # a report is in flight: it goes again with this news
+                self._report_again = True
+                self._news.set()
+                return
+            if polling and self.report_news:
+                self._reporting = True
         self._news.set()
         if not polling:
             return
         if self.report_news and getattr(self.jt, "report", None) is not None:
-            st = self.status()
             try:
-                r = self.jt.report(st.to_dict(), self.report_assign) if self.report_assign \
-                    else self.jt.report(st.to_dict())
-                if not (isinstance(r, dict) and r.get("reinit")):
-                    # (assign form) the response carries this tracker's new
-                    # work: handled here, the long-poll stays parked
-                    self._apply(r or {})
-                    return
-            except Exception:  # noqa: BLE001
-                # the JobTracker may have processed it: take back its reply
-                self._recover_lost_reply()
-            self._requeue(st)      # not delivered: the heartbeat thread sends it
+                while True:
+                    if not self._report_once(seq):
+                        return
+                    with self._lock:
+                        if not self._report_again:
+                            return
+                        self._report_again = False
+                        seq = self._notify_seq
+            finally:
+                with self._lock:
+                    # (news left by a failed round went to the heartbeat: _news)
+                    self._reporting = self._report_again = False
+        elif self.report_news:
+            with self._lock:
+                self._reporting = False
         try:
             self.jt.wakeup(self.name, seq)
         except Exception:  # noqa: BLE001
             pass
+
+    def _report_once(self, seq) -> bool:
+        """One report of the drained news; True if it was delivered."""
+        st = self.status()
+        try:
+            r = self.jt.report(st.to_dict(), self.report_assign) if self.report_assign \
+                else self.jt.report(st.to_dict())
+            if not (isinstance(r, dict) and r.get("reinit")):
+                # (assign form) the response carries this tracker's new work:
+                # handled here, the long-poll stays parked
+                self._apply(r or {})
+                return True
+        except Exception:  # noqa: BLE001
+            # the JobTracker may have processed it: take back its reply
+            self._recover_lost_reply()
+        self._requeue(st)      # not delivered: the heartbeat thread sends it
+        try:
+            self.jt.wakeup(self.name, seq)
+        except Exception:  # noqa: BLE001
+            pass
+        return False
 
     def _requeue(self, st):
         """A drained status whose report did not reach the JobTracker: its

@@ -101,7 +101,7 @@ def read_centroids(outdir, old: torch.Tensor) -> torch.Tensor:
 
 
 def iteration_conf(base, inp, out, cen_file, k, d, cpubin=None, gpubin=None, reduces=1,
-                   maps=None, reuse=True, exact=True) -> JobConf:
+                   maps=None, reuse=True, exact=True, block=True) -> JobConf:
     from ..pipes import submitter
     job = JobConf(base)
     job.set_job_name(f"kmeans-pipes {os.path.basename(out)}")
@@ -118,6 +118,10 @@ def iteration_conf(base, inp, out, cen_file, k, d, cpubin=None, gpubin=None, red
     # whichever slots ran a map, so a hybrid job's centroids do not depend on
     # the placement (the bf16 GPU mode differs from the CPU binary on near-ties)
     job.set_boolean("hbmr.kmeans.exact", exact)
+    # block mode (kmeans_pipes.h): one record per map carrying every cluster's
+    # partial (in-mapper combining) instead of one record per cluster — the
+    # same int64 partials, a k-th of the frames through the parent
+    job.set_boolean("hbmr.kmeans.pipes.block", block)
     # keep the task binaries alive across tasks and iteration jobs: the GPU
     # binary keeps its HIP context and the HBM-resident splits
     job.set_boolean("hbmr.pipes.child.reuse", reuse)
@@ -136,8 +140,9 @@ class KMeansPipesDriver:
 
     def __init__(self, workdir, inp, k, d, init: torch.Tensor, base=None, cluster=None,
                  cpubin=os.path.join(BIN, "kmeans_cpu"), gpubin=os.path.join(BIN, "kmeans_gpu"),
-                 reduces=1, maps=None, exact=True):
+                 reduces=1, maps=None, exact=True, block=True):
         self.workdir, self.inp, self.k, self.d = workdir, inp, k, d
+        self.block = block
         self.base, self.cluster = base, cluster
         self.cpubin, self.gpubin, self.reduces, self.maps = cpubin, gpubin, reduces, maps
         self.exact = exact
@@ -153,7 +158,8 @@ class KMeansPipesDriver:
                                    self.centroids)
         out = os.path.join(self.workdir, f"iter-{i:03d}")
         job = iteration_conf(self.base, self.inp, out, cen_file, self.k, self.d, self.cpubin,
-                             self.gpubin, self.reduces, self.maps, exact=self.exact)
+                             self.gpubin, self.reduces, self.maps, exact=self.exact,
+                             block=self.block)
         from ..utils.trace import TRACE
         if TRACE.on:
             TRACE.instant("kmeans_pipes.submit")

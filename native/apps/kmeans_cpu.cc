@@ -36,7 +36,7 @@ class KMeansCpuMapper : public HadoopPipes::Mapper {
                                               exact_ ? 1 : 0, &rescored);
     if (rc) throw std::runtime_error("hbmr_kmeans_map_cpu_f32_ex failed");
     ctx.incrementCounter(cpu_, 1);
-    kmp::emit_partials(ctx, p_.k, p_.d, reinterpret_cast<const int64_t*>(sums.data()), p_.d,
+    kmp::emit_partials(ctx, p_, reinterpret_cast<const int64_t*>(sums.data()), p_.d,
                        reinterpret_cast<const int64_t*>(counts.data()));
     ctx.incrementCounter(points_, (uint64_t)n);
   }

@@ -378,7 +378,7 @@ class KMeansGpuMapper : public HadoopPipes::Mapper {
     }
     tmark("map.device_done");
     if (tmp_.n || tmp_.xb || tmp_.x32) tmp_.release();   // an uncached split
-    kmp::emit_partials(ctx, p_.k, p_.d, reinterpret_cast<const int64_t*>(sums.data()), dp_,
+    kmp::emit_partials(ctx, p_, reinterpret_cast<const int64_t*>(sums.data()), dp_,
                        reinterpret_cast<const int64_t*>(counts.data()));
     ctx.incrementCounter(points_, (uint64_t)n);
     ctx.incrementCounter(gpu_, 1);

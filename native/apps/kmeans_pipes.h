@@ -12,10 +12,17 @@
 //     d int64 fixed-point sums (Σ round(x·2^fx)), so partials combine exactly
 //     whatever CPU/GPU mix produced them;
 //   * KMeansReducer — sums the partials of a cluster and emits the new centroid
-//     as comma-separated floats (key = cluster id).
+//     as comma-separated floats (key = cluster id);
+//   * block mode (hbmr.kmeans.pipes.block): a map emits ONE record, key "*",
+//     whose value packs every non-empty cluster's (int32 id, int64 count,
+//     d int64 sums) — in-mapper combining: one frame per map through the
+//     parent instead of k (k = 1024 at the headline shape) — and the reducer,
+//     given the "*" group, sums the blocks and emits the same per-cluster
+//     centroid lines.  Same int64 partials, so the result is bit-identical.
 //
 // Job keys: hbmr.kmeans.k, hbmr.kmeans.dims, hbmr.kmeans.centroids.file
-// (SequenceFile<IntWritable, FloatVectorWritable>), hbmr.kmeans.fx.shift (24).
+// (SequenceFile<IntWritable, FloatVectorWritable>), hbmr.kmeans.fx.shift (24),
+// hbmr.kmeans.pipes.block (false).
 #pragma once
 
 #include <cmath>
@@ -31,13 +38,17 @@
 
 namespace kmp {
 
+constexpr const char* kBlockKey = "*";
+
 struct Params {
   int k = 0, d = 0, fx = 24;
+  bool block = false;
   std::string centroids;
   explicit Params(const HadoopPipes::JobConf* conf) {
     k = conf->getInt("hbmr.kmeans.k");
     d = conf->getInt("hbmr.kmeans.dims");
     if (conf->hasKey("hbmr.kmeans.fx.shift")) fx = conf->getInt("hbmr.kmeans.fx.shift");
+    block = conf->hasKey("hbmr.kmeans.pipes.block") && conf->getBoolean("hbmr.kmeans.pipes.block");
     centroids = conf->get("hbmr.kmeans.centroids.file");
     if (centroids.rfind("file:", 0) == 0) centroids = centroids.substr(5);
   }
@@ -98,17 +109,51 @@ inline std::string encode_partial(int64_t count, const int64_t* sums, int d) {
   return v;
 }
 
-inline void emit_partials(HadoopPipes::MapContext& ctx, int k, int d, const int64_t* sums,
+inline void emit_partials(HadoopPipes::MapContext& ctx, const Params& p, const int64_t* sums,
                           int sums_stride, const int64_t* counts) {
-  for (int j = 0; j < k; ++j)
-    if (counts[j] > 0)
-      ctx.emit(HadoopUtils::toString(j), encode_partial(counts[j], sums + (size_t)j * sums_stride, d));
+  const int k = p.k, d = p.d;
+  if (!p.block) {
+    for (int j = 0; j < k; ++j)
+      if (counts[j] > 0)
+        ctx.emit(HadoopUtils::toString(j),
+                 encode_partial(counts[j], sums + (size_t)j * sums_stride, d));
+    return;
+  }
+  const size_t rec = 4 + 8 * (size_t)(d + 1);
+  int used = 0;
+  for (int j = 0; j < k; ++j) used += counts[j] > 0;
+  std::string v(rec * (size_t)used, '\0');
+  char* o = &v[0];
+  for (int j = 0; j < k; ++j) {
+    if (counts[j] <= 0) continue;
+    const int32_t id = j;
+    memcpy(o, &id, 4);
+    memcpy(o + 4, &counts[j], 8);
+    memcpy(o + 12, sums + (size_t)j * sums_stride, 8 * (size_t)d);
+    o += rec;
+  }
+  ctx.emit(kBlockKey, v);
+}
+
+inline std::string centroid_text(const int64_t* s, int64_t cnt, int d, int fx) {
+  std::string out;
+  char buf[32];
+  const double inv = std::ldexp(1.0, -fx) / (double)cnt;
+  for (int i = 0; i < d; ++i) {
+    snprintf(buf, sizeof(buf), i ? ",%.9g" : "%.9g", (float)((double)s[i] * inv));
+    out += buf;
+  }
+  return out;
 }
 
 class KMeansReducer : public HadoopPipes::Reducer {
  public:
   explicit KMeansReducer(HadoopPipes::TaskContext& ctx) : p_(ctx.getJobConf()) {}
   void reduce(HadoopPipes::ReduceContext& ctx) override {
+    if (ctx.getInputKey() == kBlockKey) {
+      reduce_blocks(ctx);
+      return;
+    }
     int64_t cnt = 0;
     std::vector<int64_t> s((size_t)p_.d, 0), part((size_t)p_.d);
     while (ctx.nextValue()) {
@@ -120,14 +165,33 @@ class KMeansReducer : public HadoopPipes::Reducer {
       cnt += c;
       for (int i = 0; i < p_.d; ++i) s[i] += part[i];
     }
-    std::string out;
-    char buf[32];
-    const double inv = std::ldexp(1.0, -p_.fx) / (double)cnt;
-    for (int i = 0; i < p_.d; ++i) {
-      snprintf(buf, sizeof(buf), i ? ",%.9g" : "%.9g", (float)((double)s[i] * inv));
-      out += buf;
+    ctx.emit(ctx.getInputKey(), centroid_text(s.data(), cnt, p_.d, p_.fx));
+  }
+
+  // every map's block (block mode): per-cluster sums over all of them, then
+  // one centroid line per non-empty cluster, in cluster order
+  void reduce_blocks(HadoopPipes::ReduceContext& ctx) {
+    const int k = p_.k, d = p_.d;
+    const size_t rec = 4 + 8 * (size_t)(d + 1);
+    std::vector<int64_t> cnt((size_t)k, 0), s((size_t)k * d, 0), part((size_t)d);
+    while (ctx.nextValue()) {
+      const std::string& v = ctx.getInputValue();
+      if (v.size() % rec) throw std::runtime_error("bad partials block");
+      for (const char* o = v.data(); o < v.data() + v.size(); o += rec) {
+        int32_t j;
+        int64_t c;
+        memcpy(&j, o, 4);
+        memcpy(&c, o + 4, 8);
+        if (j < 0 || j >= k) throw std::runtime_error("bad cluster id in partials block");
+        memcpy(part.data(), o + 12, 8 * (size_t)d);
+        cnt[j] += c;
+        int64_t* sj = &s[(size_t)j * d];
+        for (int i = 0; i < d; ++i) sj[i] += part[i];
+      }
     }
-    ctx.emit(ctx.getInputKey(), out);
+    for (int j = 0; j < k; ++j)
+      if (cnt[j] > 0)
+        ctx.emit(HadoopUtils::toString(j), centroid_text(&s[(size_t)j * d], cnt[j], d, p_.fx));
   }
 
  private:

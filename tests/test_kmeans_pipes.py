@@ -49,7 +49,7 @@ def _exact_split_job_centroids(iters):
         return drv.centroids()
 
 
-def _pipes_exact(tmp_path, name, conf, gpus, cpu_slots, files=6):
+def _pipes_exact(tmp_path, name, conf, gpus, cpu_slots, files=6, block=True):
     pts = tmp_path / "pts"
     if not pts.exists():
         KP.write_points(str(pts), N, D, seed=3, centers=KC, files=files, bf16_exact=False)
@@ -58,7 +58,7 @@ def _pipes_exact(tmp_path, name, conf, gpus, cpu_slots, files=6):
                       gpu_slots_per_device=1) as cl:
         drv = KP.KMeansPipesDriver(str(tmp_path / name), str(pts), KC, D, init, cluster=cl,
                                    reduces=1, gpubin=None if not gpus else KP.os.path.join(
-                                       KP.BIN, "kmeans_gpu"), exact=True)
+                                       KP.BIN, "kmeans_gpu"), exact=True, block=block)
         cen = drv.run(3)
     return cen, drv.history
 
@@ -70,6 +70,18 @@ def test_pipes_kmeans_exact_cpu_binary_matches_exact_split_job(tmp_path):
     cen, hist = _pipes_exact(tmp_path, "cpu", JobConf(), None, 2)
     assert hist[-1]["counters"].get("KMEANS", "POINTS") == N
     assert torch.equal(cen, _exact_split_job_centroids(3))
+
+
+def test_pipes_kmeans_block_mode_matches_per_cluster_records(tmp_path):
+    """hbmr.kmeans.pipes.block: one partials record per map (in-mapper
+    combining) gives the per-cluster records' centroids, bit for bit, with a
+    k-th of the map output records."""
+    blk, hb = _pipes_exact(tmp_path, "blk", JobConf(), None, 2, block=True)
+    per, hp = _pipes_exact(tmp_path, "per", JobConf(), None, 2, block=False)
+    assert torch.equal(blk, per)
+    tc = "org.apache.hadoop.mapred.Task$Counter"
+    assert hb[-1]["counters"].get(tc, "MAP_OUTPUT_RECORDS") == 6
+    assert hp[-1]["counters"].get(tc, "MAP_OUTPUT_RECORDS") > 6
 
 
 @pytest.mark.gpu
