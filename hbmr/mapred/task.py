@@ -34,6 +34,7 @@ from ..io.ifile import IFileWriter, SpillRecord, read_segment
 from ..io.serializer import to_bytes
 from ..io.writable import payload_serializer
 from ..utils.reflection import new_instance
+from ..utils.trace import TRACE
 from . import counters as C
 from . import mapoutput, sortbuf
 from .api import OutputCollector, Reporter
@@ -758,7 +759,7 @@ class MapOutputLocation:
         if held is not None:            # an in-memory map output of this process
             data, idx = held
             start, _raw, plen = idx.get(part)
-            return data[start:start + plen]
+            return sortbuf.VerifiedSegment(memoryview(data)[start:start + plen])
         idx = SpillRecord.read(self.path + ".index")
         start, _raw, plen = idx.get(part)
         with open(self.path, "rb") as f:
@@ -846,6 +847,8 @@ class ReduceTask(Task):
             self.check_killed()
             merger.add(loc.read_partition(self.partition))
         rep.incrCounter(C.TASK_GROUP, C.REDUCE_SHUFFLE_BYTES, merger.shuffled)
+        if TRACE.on:
+            TRACE.instant("reduce.copied", bytes=merger.shuffled)
         rep.set_progress(1 / 3)
         # sort phase (merge)
         if not merger.on_disk:
@@ -939,6 +942,8 @@ class ReduceTask(Task):
         # gets them without a Writable built per record
         rr = getattr(reducer, "raw_reduce", None)
         rr = rr(kcls, vcls) if rr is not None else None
+        if TRACE.on:
+            TRACE.instant("reduce.sorted", groups=len(ends))
         try:
             a = 0
             for g, e in enumerate(ends):
@@ -950,14 +955,20 @@ class ReduceTask(Task):
                     reducer.reduce(kdes(b.key(pl[a])), (vdes(b.value(r)) for r in pl[a:e]), out,
                                    rep)
                 a = e
+            if TRACE.on:
+                TRACE.instant("reduce.fed")
         finally:
             reducer.close()
             writer.close(rep)
+        if TRACE.on:
+            TRACE.instant("reduce.closed")
         rep.incrCounter(C.TASK_GROUP, C.REDUCE_INPUT_GROUPS, len(ends))
         rep.incrCounter(C.TASK_GROUP, C.REDUCE_INPUT_RECORDS, b.n)
         rep.incrCounter(C.TASK_GROUP, C.REDUCE_OUTPUT_RECORDS, n_out[0])
         if committer.needs_task_commit(job, self.attempt_id):
             committer.commit_task(job, self.attempt_id)
+        if TRACE.on:
+            TRACE.instant("reduce.committed")
         rep.set_progress(1.0)
         self.finish_time = time.time()
 

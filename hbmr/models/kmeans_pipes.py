@@ -28,7 +28,7 @@ import numpy as np
 import torch
 
 from ..io import sequencefile as seqf
-from ..io.writable import FloatVectorWritable, IntWritable, LongWritable
+from ..io.writable import BytesWritable, FloatVectorWritable, IntWritable, LongWritable, Text
 from ..mapred import FileInputFormat, FileOutputFormat, JobConf
 from . import kmeans as K
 
@@ -82,12 +82,28 @@ def write_centroids(path, cen: torch.Tensor):
 def read_centroids(outdir, old: torch.Tensor) -> torch.Tensor:
     """The reducers' ``cluster \t c0,c1,...`` lines folded into the next
     centroids (clusters without a line keep theirs).  One numpy parse of all
-    the values (the reducer prints %.9g: every fp32 round-trips exactly)."""
+    the values (the reducer prints %.9g: every fp32 round-trips exactly).
+    Binary output (hbmr.kmeans.pipes.binary.output): SequenceFile parts of
+    (Text cluster, BytesWritable d little-endian fp32) — the same floats."""
     new = old.detach().to("cpu", torch.float32).numpy().copy()
     keys, vals = [], []
-    for fn in sorted(os.listdir(outdir)):
-        if not fn.startswith("part-"):
-            continue
+    parts = [fn for fn in sorted(os.listdir(outdir)) if fn.startswith("part-")]
+    if parts and _is_seqfile(os.path.join(outdir, parts[0])):
+        rows = []
+        for fn in parts:
+            with seqf.Reader(os.path.join(outdir, fn)) as r:
+                while True:
+                    raw = r.next_raw()
+                    if raw is None:
+                        break
+                    kb, vb = raw
+                    keys.append(int(Text.deserialize(kb).bytes))
+                    rows.append(BytesWritable.deserialize(vb).bytes)
+        if keys:
+            arr = np.frombuffer(b"".join(rows), dtype="<f4")
+            new[np.asarray(keys)] = arr.reshape(len(keys), -1)
+        return torch.from_numpy(new)
+    for fn in parts:
         with open(os.path.join(outdir, fn)) as f:
             for line in f:
                 k, sep, v = line.rstrip("\n").partition("\t")
@@ -100,8 +116,13 @@ def read_centroids(outdir, old: torch.Tensor) -> torch.Tensor:
     return torch.from_numpy(new)
 
 
+def _is_seqfile(path) -> bool:
+    with open(path, "rb") as f:
+        return f.read(3) == b"SEQ"
+
+
 def iteration_conf(base, inp, out, cen_file, k, d, cpubin=None, gpubin=None, reduces=1,
-                   maps=None, reuse=True, exact=True, block=True) -> JobConf:
+                   maps=None, reuse=True, exact=True, block=True, binary=True) -> JobConf:
     from ..pipes import submitter
     job = JobConf(base)
     job.set_job_name(f"kmeans-pipes {os.path.basename(out)}")
@@ -122,6 +143,17 @@ def iteration_conf(base, inp, out, cen_file, k, d, cpubin=None, gpubin=None, red
     # partial (in-mapper combining) instead of one record per cluster — the
     # same int64 partials, a k-th of the frames through the parent
     job.set_boolean("hbmr.kmeans.pipes.block", block)
+    # the new centroids as raw fp32 bytes in a SequenceFile (read_centroids),
+    # not %.9g text: the same floats without a format and a parse per value
+    job.set_boolean("hbmr.kmeans.pipes.binary.output", binary)
+    if binary:
+        job.set("mapred.output.format.class", "hbmr.mapred.formats:SequenceFileOutputFormat")
+        job.set_output_key_class(Text)
+        job.set_output_value_class(BytesWritable)
+    # every map's partials block stays in the reduce's memory (a 1,024-cluster
+    # block is ~1 MB per map)
+    job.set_int("hbmr.reduce.shuffle.memory.mb",
+                max(512, (4 * k * (d + 1) * 8 * max(maps or 0, 128)) >> 20))
     # keep the task binaries alive across tasks and iteration jobs: the GPU
     # binary keeps its HIP context and the HBM-resident splits
     job.set_boolean("hbmr.pipes.child.reuse", reuse)
@@ -140,9 +172,9 @@ class KMeansPipesDriver:
 
     def __init__(self, workdir, inp, k, d, init: torch.Tensor, base=None, cluster=None,
                  cpubin=os.path.join(BIN, "kmeans_cpu"), gpubin=os.path.join(BIN, "kmeans_gpu"),
-                 reduces=1, maps=None, exact=True, block=True):
+                 reduces=1, maps=None, exact=True, block=True, binary=True):
         self.workdir, self.inp, self.k, self.d = workdir, inp, k, d
-        self.block = block
+        self.block, self.binary = block, binary
         self.base, self.cluster = base, cluster
         self.cpubin, self.gpubin, self.reduces, self.maps = cpubin, gpubin, reduces, maps
         self.exact = exact
@@ -159,7 +191,7 @@ class KMeansPipesDriver:
         out = os.path.join(self.workdir, f"iter-{i:03d}")
         job = iteration_conf(self.base, self.inp, out, cen_file, self.k, self.d, self.cpubin,
                              self.gpubin, self.reduces, self.maps, exact=self.exact,
-                             block=self.block)
+                             block=self.block, binary=self.binary)
         from ..utils.trace import TRACE
         if TRACE.on:
             TRACE.instant("kmeans_pipes.submit")

@@ -49,7 +49,7 @@ def _exact_split_job_centroids(iters):
         return drv.centroids()
 
 
-def _pipes_exact(tmp_path, name, conf, gpus, cpu_slots, files=6, block=True):
+def _pipes_exact(tmp_path, name, conf, gpus, cpu_slots, files=6, block=True, binary=True):
     pts = tmp_path / "pts"
     if not pts.exists():
         KP.write_points(str(pts), N, D, seed=3, centers=KC, files=files, bf16_exact=False)
@@ -58,7 +58,8 @@ def _pipes_exact(tmp_path, name, conf, gpus, cpu_slots, files=6, block=True):
                       gpu_slots_per_device=1) as cl:
         drv = KP.KMeansPipesDriver(str(tmp_path / name), str(pts), KC, D, init, cluster=cl,
                                    reduces=1, gpubin=None if not gpus else KP.os.path.join(
-                                       KP.BIN, "kmeans_gpu"), exact=True, block=block)
+                                       KP.BIN, "kmeans_gpu"), exact=True, block=block,
+                                   binary=binary)
         cen = drv.run(3)
     return cen, drv.history
 
@@ -75,9 +76,10 @@ def test_pipes_kmeans_exact_cpu_binary_matches_exact_split_job(tmp_path):
 def test_pipes_kmeans_block_mode_matches_per_cluster_records(tmp_path):
     """hbmr.kmeans.pipes.block: one partials record per map (in-mapper
     combining) gives the per-cluster records' centroids, bit for bit, with a
-    k-th of the map output records."""
-    blk, hb = _pipes_exact(tmp_path, "blk", JobConf(), None, 2, block=True)
-    per, hp = _pipes_exact(tmp_path, "per", JobConf(), None, 2, block=False)
+    k-th of the map output records; the binary centroid output
+    (hbmr.kmeans.pipes.binary.output) reads back the text output's floats."""
+    blk, hb = _pipes_exact(tmp_path, "blk", JobConf(), None, 2, block=True, binary=True)
+    per, hp = _pipes_exact(tmp_path, "per", JobConf(), None, 2, block=False, binary=False)
     assert torch.equal(blk, per)
     tc = "org.apache.hadoop.mapred.Task$Counter"
     assert hb[-1]["counters"].get(tc, "MAP_OUTPUT_RECORDS") == 6

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--points", type=int, default=1_000_000)
     ap.add_argument("--files", type=int, default=8)
     ap.add_argument("--gpu", action="store_true")
+    ap.add_argument("--k", type=int, default=64)
     ap.add_argument("-D", dest="defines", action="append", default=[], metavar="KEY=VALUE")
     a = ap.parse_args()
     from hbmr.mapred.cluster import LocalCluster
@@ -27,8 +28,8 @@ def main():
     tmp = tempfile.mkdtemp(prefix="hbmr-trace2-")
     child_trace = os.path.join(tmp, "child.trace")
     os.environ["HBMR_PIPES_TRACE"] = child_trace      # the GPU child's phase marks
-    KP.write_points(os.path.join(tmp, "pts"), a.points, 128, seed=5, centers=64, files=a.files)
-    init = K.initial_centroids(os.path.join(tmp, "pts"), 64, 128)
+    KP.write_points(os.path.join(tmp, "pts"), a.points, 128, seed=5, centers=a.k, files=a.files)
+    init = K.initial_centroids(os.path.join(tmp, "pts"), a.k, 128)
     conf = JobConf()
     conf.set_int("hbmr.gpu.queue.depth", max(16, a.files))
     for kv in a.defines:
@@ -36,7 +37,7 @@ def main():
         conf.set(k, v)
     with LocalCluster(conf, num_trackers=1, gpus=[[0]] if a.gpu else None,
                       cpu_slots=0 if a.gpu else 2, gpu_slots_per_device=1) as cl:
-        drv = KP.KMeansPipesDriver(os.path.join(tmp, "work"), os.path.join(tmp, "pts"), 64, 128,
+        drv = KP.KMeansPipesDriver(os.path.join(tmp, "work"), os.path.join(tmp, "pts"), a.k, 128,
                                    init, cluster=cl, gpubin=os.path.join(KP.BIN, "kmeans_gpu")
                                    if a.gpu else None, maps=a.files)
         for _ in range(3):
