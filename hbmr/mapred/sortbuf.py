@@ -171,6 +171,11 @@ class Batch:
         p = int(self.vpos[r])
         return self.vbuf[p:p + int(self.vlen[r])]
 
+    def value_view(self, r) -> memoryview:
+        """value() without the copy (a view into the batch's buffer)."""
+        p = int(self.vpos[r])
+        return memoryview(self.vbuf)[p:p + int(self.vlen[r])]
+
 
 def write_segment(f, body: bytes, codec=None):
     """Append one IFile segment (body [+codec] + CRC32) to f; returns
@@ -194,8 +199,8 @@ class VerifiedSegment(bytes):
 
 def segment_body(data: bytes, codec=None, verify=True) -> bytes:
     """Stored IFile segment (incl. CRC) → decompressed body."""
-    body, crc = data[:-4], struct.unpack(">I", data[-4:])[0]
+    body, crc = memoryview(data)[:-4], struct.unpack(">I", data[-4:])[0]
     if verify and data.__class__ is not VerifiedSegment and \
             (zlib.crc32(body) & 0xFFFFFFFF) != crc:
         raise IOError("IFile checksum error")
-    return codec.decompress(body) if codec is not None else body
+    return codec.decompress(bytes(body)) if codec is not None else body

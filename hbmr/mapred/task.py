@@ -950,7 +950,7 @@ class ReduceTask(Task):
                 if (g & 1023) == 1023:
                     self.check_killed()
                 if rr is not None:
-                    rr(b.key(pl[a]), [b.value(r) for r in pl[a:e]], out, rep)
+                    rr(b.key(pl[a]), [b.value_view(r) for r in pl[a:e]], out, rep)
                 else:
                     reducer.reduce(kdes(b.key(pl[a])), (vdes(b.value(r)) for r in pl[a:e]), out,
                                    rep)

@@ -76,7 +76,7 @@ def frame_of_serialized(cls):
     if not RAW_FRAMES:
         return None
     if cls is Text:
-        return lambda s: s          # VInt length + UTF-8 already
+        return lambda s: s          # VInt length + UTF-8 already (bytes or memoryview)
     if cls is BytesWritable:
         return lambda s: encode_vint(len(s) - 4) + s[4:]
     if issubclass(cls, (Text, BytesWritable)) or not issubclass(cls, Writable):
@@ -165,11 +165,23 @@ class DownwardProtocol:
         """REDUCE_KEY and the REDUCE_VALUEs of one key group in one write
         (frames as made by :func:`frame_of_serialized`)."""
         sep = _SMALL_VINTS[REDUCE_VALUE]
-        msg = _SMALL_VINTS[REDUCE_KEY] + key_frame
-        if value_frames:
-            msg += sep + sep.join(value_frames)
         with self._lock:
-            self.out.write(msg)
+            if sum(map(len, value_frames)) < (1 << 16):
+                # small values: one joined write
+                msg = _SMALL_VINTS[REDUCE_KEY] + key_frame
+                if value_frames:
+                    msg += sep + sep.join(value_frames)
+                self.out.write(msg)
+                return
+            # big values (a K-Means partials block is ~1 MB): written as they
+            # are (memoryviews, no joined copy); the buffered writer passes
+            # writes above its buffer size straight to the socket
+            w = self.out.write
+            w(_SMALL_VINTS[REDUCE_KEY])
+            w(key_frame)
+            for f in value_frames:
+                w(sep)
+                w(f)
 
     def end_of_input(self):
         with self._lock:

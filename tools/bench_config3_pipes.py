@@ -60,6 +60,7 @@ def main():
     ap.add_argument("--dir", default=None)
     ap.add_argument("--out", default=None)
     ap.add_argument("--skip-split-job", action="store_true")
+    ap.add_argument("--trace", default=None, help="event timeline of the last Pipes iteration")
     a = ap.parse_args()
     import torch
 
@@ -99,20 +100,36 @@ def main():
             torch.cuda.empty_cache()
         conf = JobConf()
         conf.set_int("hbmr.gpu.queue.depth", max(16, a.files))
+        # one map per file, as the split job's 128 splits (FileInputFormat
+        # would cut each 420 MB file into 64 MB blocks: 7x the map tasks)
+        conf.set_long("mapred.min.split.size", 1 << 40)
         # every split resident in the GPU child's HBM cache (exact mode holds
         # the fp32 rows, their fp16 copy and per-point norms: ~78 GB here)
         os.environ["HBMR_PIPES_SPLIT_CACHE_MB"] = "200000"
         with LocalCluster(conf, num_trackers=1, gpus=[[0]], cpu_slots=0,
                           gpu_slots_per_device=1) as cl:
             drv = KP.KMeansPipesDriver(os.path.join(tmp, "work"), inp, a.k, a.dims, init,
-                                       cluster=cl, gpubin=os.path.join(KP.BIN, "kmeans_gpu"),
+                                       base=conf, cluster=cl,
+                                       gpubin=os.path.join(KP.BIN, "kmeans_gpu"),
                                        maps=a.files, exact=True)
             times = []
-            for _ in range(a.iters):
+            from hbmr.utils.trace import TRACE
+            for it in range(a.iters):
+                if a.trace and it == a.iters - 1:
+                    TRACE.enable()
+                    TRACE.clear()
                 t = time.perf_counter()
                 drv.step()
                 times.append(time.perf_counter() - t)
                 print(json.dumps({"pipes_iteration_s": round(times[-1], 4)}), flush=True)
+            if a.trace:
+                TRACE.disable()
+                ev = [e for e in TRACE.events if e[3] not in ("jt.heartbeat",)]
+                t0 = ev[0][0]
+                with open(a.trace, "w") as f:
+                    for ts, th, _ph, name, _dur, args in ev:
+                        f.write(f"{(ts - t0) / 1e6:9.3f} ms {th[:24]:>24} {name:<24} "
+                                f"{ {k: v for k, v in args.items() if k != 'attempt'} }\n")
             res["pipes_iteration_ms"] = [round(1e3 * x, 2) for x in times]
             cs = drv.history[-1]["counters"]
             res["pipes_gpu_maps"] = cs.get("KMEANS", "GPU_MAPS")
