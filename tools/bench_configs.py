@@ -157,10 +157,13 @@ def kmeans_pipes(a):
         # every map of an iteration in flight on the GPU slot (the Pipes child
         # runs them back to back; 4 = the default left half for a second round)
         conf.set_int("hbmr.gpu.queue.depth", max(16, a.files))
+        for kv in a.defines:
+            kk, _, vv = kv.partition("=")
+            conf.set(kk, vv)
         with LocalCluster(conf, num_trackers=1, gpus=[[0]] if gpu else None,
                           cpu_slots=0 if gpu else 2, gpu_slots_per_device=1) as cl:
             drv = KP.KMeansPipesDriver(os.path.join(tmp, "work"), os.path.join(tmp, "pts"),
-                                       a.k, a.dims, init, cluster=cl,
+                                       a.k, a.dims, init, base=conf, cluster=cl,
                                        gpubin=KP.os.path.join(KP.BIN, "kmeans_gpu") if gpu
                                        else None, maps=a.files, exact=a.exact)
             times = []
@@ -169,7 +172,7 @@ def kmeans_pipes(a):
                 drv.step()
                 times.append(time.perf_counter() - t)
             cs = drv.history[-1]["counters"]
-            res["pipes_iteration_s"] = [round(x, 3) for x in times]
+            res["pipes_iteration_s"] = [round(x, 4) for x in times]
             res["pipes_gpu_maps"] = cs.get("org.apache.hadoop.mapred.JobInProgress$Counter",
                                            "GPU_MAP_TASKS")
             res["pipes_points_per_s"] = round(a.points / min(times), 1)
@@ -257,6 +260,8 @@ def main():
     ap.add_argument("--lines", type=int, default=100)
     ap.add_argument("--procs", type=int, default=1, help="wordcount: parallel map processes")
     ap.add_argument("--cpu-slots", type=int, default=0)
+    ap.add_argument("-D", dest="defines", action="append", default=[], metavar="KEY=VALUE",
+                    help="kmeans-pipes: extra cluster/job conf")
     ap.add_argument("--exact", action=argparse.BooleanOptionalAction, default=True,
                     help="kmeans-pipes: fp64-exact labels on both binaries (hbmr.kmeans.exact)")
     a = ap.parse_args()
