@@ -91,12 +91,14 @@ class NativeWordCountRunner(MapRunner):
         try:
             max_words = self.job.get_int("hbmr.wordcount.inmapper.max.words", 1 << 20)
             for block in _owned_blocks(lr, self.BLOCK):
-                lines += block.count(b"\n") + (0 if block.endswith(b"\n") else 1)
+                # (the newlines are counted in the tokeniser's pass)
+                lines += 0 if block.endswith(b"\n") else 1
                 if lib.hbmr_wc_cpu_add(h, block, len(block)) >= max_words:
                     _emit(lib, h, output)
                 if reporter is not None:
                     reporter.progress()
             _emit(lib, h, output)
+            lines += lib.hbmr_wc_cpu_newlines(h)
         finally:
             lib.hbmr_wc_cpu_free(h)
         reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, lines)
@@ -169,7 +171,8 @@ def _wc_lib():
             L.hbmr_wc_cpu_free.argtypes = [P]
             L.hbmr_wc_cpu_add.argtypes = [P, ctypes.c_char_p, I64]
             L.hbmr_wc_cpu_add.restype = I64
-            for f in ("hbmr_wc_cpu_words", "hbmr_wc_cpu_bytes", "hbmr_wc_cpu_tokens"):
+            for f in ("hbmr_wc_cpu_words", "hbmr_wc_cpu_bytes", "hbmr_wc_cpu_tokens",
+                      "hbmr_wc_cpu_newlines"):
                 getattr(L, f).argtypes = [P]
                 getattr(L, f).restype = I64
             L.hbmr_wc_cpu_export.argtypes = [P, P, P, P]

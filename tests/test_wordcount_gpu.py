@@ -151,3 +151,44 @@ def test_gpu_wordcount_job_equals_classic(tmp_path):
     classic.set("mapred.job.tracker", "local")
     JobClient.runJob(classic, verbose=False)
     assert _outputs(tmp_path / "split") == _outputs(tmp_path / "classic")
+
+
+def test_native_cpu_tokeniser_matches_bytes_split():
+    """The native map runner's tokeniser (native/cpu/wordcount.cc: 64-byte
+    AVX2 whitespace masks, masked 16-byte word prefixes, newline count) gives
+    Python's bytes.split() counts on random text: every whitespace kind, words
+    longer than 16 bytes and across 64-byte chunks, leading/trailing blanks."""
+    import collections
+    import ctypes
+    import random
+
+    import numpy as np
+
+    from hbmr.models.wordcount import _wc_lib
+    lib = _wc_lib()
+    if lib is None:
+        pytest.skip("libhbmr_cpu not built")
+    rnd = random.Random(5)
+    for trial in range(80):
+        toks = [rnd.choice(["a", "bb", "xyz" * rnd.randint(1, 12), "q" * rnd.randint(1, 70),
+                            "été"]) for _ in range(rnd.randint(0, 400))]
+        seps = [rnd.choice([" ", "\t", "\n", "  ", "\r\n", "\x0b", "\x0c"]) for _ in toks]
+        text = "".join(a + b for a, b in zip(toks, seps)).encode()
+        if trial % 3 == 0:
+            text = text.rstrip()
+        if trial % 5 == 0:
+            text = b"  " + text
+        h = lib.hbmr_wc_cpu_new()
+        try:
+            lib.hbmr_wc_cpu_add(h, text, len(text))
+            assert lib.hbmr_wc_cpu_newlines(h) == text.count(b"\n")
+            w, nb = lib.hbmr_wc_cpu_words(h), lib.hbmr_wc_cpu_bytes(h)
+            words = ctypes.create_string_buffer(max(1, nb))
+            offs = np.empty(w + 1, np.int64)
+            cnts = np.empty(w, np.int64)
+            lib.hbmr_wc_cpu_export(h, words, offs.ctypes.data, cnts.ctypes.data)
+        finally:
+            lib.hbmr_wc_cpu_free(h)
+        raw = words.raw[:nb]
+        got = {raw[offs[j]:offs[j + 1]]: int(cnts[j]) for j in range(w)}
+        assert got == dict(collections.Counter(text.split())), trial
