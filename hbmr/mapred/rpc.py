@@ -19,7 +19,6 @@ authenticated handshake, not from the calls.
 """
 from __future__ import annotations
 
-import contextlib
 import hmac
 import json
 import logging
@@ -72,13 +71,31 @@ def _send(sock, obj):
 
 
 def _recv_exact(sock, n):
-    buf = bytearray()
+    data = sock.recv(n)             # the common case: all of it in one read
+    if len(data) == n:
+        return data
+    if not data:
+        raise ConnectionError("connection closed")
+    buf = bytearray(data)
     while len(buf) < n:
         chunk = sock.recv(n - len(buf))
         if not chunk:
             raise ConnectionError("connection closed")
         buf += chunk
     return bytes(buf)
+
+
+def _recv_buffered(f):
+    """One message from a connection's buffered reader (the length word and
+    the body usually arrive in one recv)."""
+    head = f.read(4)
+    if len(head) < 4:
+        raise ConnectionError("connection closed")
+    (n,) = _LEN.unpack(head)
+    body = f.read(n)
+    if len(body) < n:
+        raise ConnectionError("connection closed")
+    return msgpack.unpackb(body, raw=False, strict_map_key=False)
 
 
 def _recv(sock):
@@ -134,20 +151,30 @@ class RpcServer:
                         return
                     if authed is None:
                         return
+                # requests and replies alternate on a connection, so a
+                # buffered reader cannot read past the next request
+                rf = s.makefile("rb", buffering=1 << 16)
+                ugis = {}
                 while True:
                     try:
-                        req = _recv(s)
-                    except (ConnectionError, OSError):
+                        req = _recv_buffered(rf)
+                    except (ConnectionError, OSError, ValueError):
                         return
                     m = req.get("m")
                     user = authed or req.get("u")
-                    ctx = UserGroupInformation.create_remote_user(user).do_as() if user \
-                        else contextlib.nullcontext()
                     try:
                         if m not in outer.methods:
                             raise AttributeError(f"no RPC method {m!r}")
                         t0 = time.perf_counter() if RPC_STATS is not None else 0.0
-                        with ctx:
+                        if user:
+                            # doAs: the caller's identity on this thread's stack
+                            ugi = ugis.get(user)
+                            if ugi is None:
+                                ugi = ugis[user] = UserGroupInformation.create_remote_user(user)
+                            with ugi.do_as():
+                                res = getattr(outer.target, m)(*req.get("a", ()),
+                                                               **req.get("k", {}))
+                        else:
                             res = getattr(outer.target, m)(*req.get("a", ()),
                                                            **req.get("k", {}))
                         _send(s, {"r": res})
