@@ -185,6 +185,7 @@ def main():
         cpu0 = time.process_time()
         jt_proc = getattr(node, "jt_process", False)
         jt_cpu0 = node.jt.cpu_seconds() if jt_proc else 0.0
+        jt_thr0 = node.jt.thread_cpu() if jt_proc else {}
         if sampler is not None:
             sampler.mark()
         t0 = time.perf_counter()
@@ -198,6 +199,8 @@ def main():
         dt = time.perf_counter() - t0
         cpu_rank0 = time.process_time() - cpu0
         jt_cpu = node.jt.cpu_seconds() - jt_cpu0 if jt_proc else None
+        jt_thr = {k: round((v - jt_thr0.get(k, 0.0)) / a.steps * 1e3, 3)
+                  for k, v in node.jt.thread_cpu().items()} if jt_proc else None
         hist = drv.history[a.warmup:]
         if a.verbose:
             J = "org.apache.hadoop.mapred.JobInProgress$Counter"
@@ -284,6 +287,8 @@ def main():
             "jobtracker_process": bool(jt_proc),
             "jobtracker_cpu_ms_per_step": None if jt_cpu is None else
             round(jt_cpu / a.steps * 1e3, 3),
+            # the JobTracker process's CPU per timed job by thread group
+            "jobtracker_thread_cpu_ms_per_step": jt_thr,
             "final_shift": hist[-1].get("shift") if hist else None,
             "maps_per_tracker_last_job": hist[-1].get("maps_per_tracker") if hist else None,
             # per job signature: completed-task mean seconds on each slot type (over

@@ -2061,6 +2061,21 @@ class JobTracker:
         """CPU seconds of this process (a JobTracker process's own cost)."""
         return time.process_time()
 
+    def rpc_thread_cpu(self):
+        """CPU seconds per thread of this process, summed over threads whose
+        names differ only in digits (RPC handler threads, long-polls): where a
+        JobTracker process's CPU goes."""
+        import re as _re
+        out = {}
+        for t in threading.enumerate():
+            try:
+                sec = time.clock_gettime(time.pthread_getcpuclockid(t.ident))
+            except (OSError, AttributeError, TypeError):
+                continue
+            key = _re.sub(r"\d+", "#", t.name)
+            out[key] = out.get(key, 0.0) + sec
+        return out
+
     def broadcast_shutdown(self):
         """Tell every tracker to exit on its next heartbeat."""
         with self.lock:

@@ -209,6 +209,9 @@ class RemoteJobTracker:
     def cpu_seconds(self):
         return float(self.rpc.call("rpc_cpu_seconds"))
 
+    def thread_cpu(self):
+        return dict(self.rpc.call("rpc_thread_cpu"))
+
     def shutdown(self):
         try:
             self.rpc.call("rpc_stop")

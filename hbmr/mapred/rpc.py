@@ -165,7 +165,8 @@ class RpcServer:
                     try:
                         if m not in outer.methods:
                             raise AttributeError(f"no RPC method {m!r}")
-                        t0 = time.perf_counter() if RPC_STATS is not None else 0.0
+                        # (thread CPU, not wall: a long-poll's wait is not cost)
+                        t0 = time.thread_time() if RPC_STATS is not None else 0.0
                         if user:
                             # doAs: the caller's identity on this thread's stack
                             ugi = ugis.get(user)
@@ -187,7 +188,7 @@ class RpcServer:
                                                                 res["actions"]})) or "-")
                             st = RPC_STATS.setdefault(m, [0, 0.0])
                             st[0] += 1
-                            st[1] += time.perf_counter() - t0
+                            st[1] += time.thread_time() - t0
                     except Exception as e:  # noqa: BLE001
                         log.debug("rpc %s failed", m, exc_info=True)
                         try:
@@ -294,7 +295,8 @@ JT_METHODS = ("heartbeat", "wakeup", "report", "resend", "map_completion_events"
 # served by a JobTracker process to the node that started it (hbmr/mapred/jtprocess.py)
 JT_PROCESS_METHODS = JT_METHODS + ("rpc_wait_for_trackers", "rpc_start_expiry",
                                    "rpc_broadcast_shutdown", "rpc_live_trackers",
-                                   "rpc_cost_model", "rpc_cpu_seconds", "rpc_stop")
+                                   "rpc_cost_model", "rpc_cpu_seconds", "rpc_thread_cpu",
+                                   "rpc_stop")
 
 
 class JobTrackerProxy:
