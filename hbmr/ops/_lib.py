@@ -49,6 +49,8 @@ _SIGS = {
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "hbmr_kmeans_image16_tiled": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "hbmr_kmeans_set_stamps": (c_int, [c_void_p]),
+    "hbmr_kmeans_set_exact_v4": (c_int, [c_int]),
+    "hbmr_kmeans_set_v4_stamps": (c_int, [c_void_p]),
     "hbmr_kmeans_refine_f32": (c_int, [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,

@@ -3593,6 +3593,413 @@ int refine_version() {
   return v;
 }
 
+// ---------------------------------------------------------------------------
+// v4 of the exact top-3 assign: STATIONARY CENTROIDS, STREAMED POINTS
+// (D = 128, fp16/bf16 operands, k_pad = 256 * TPW, TPW = 1, 2 or 4).
+//
+// v2/v3 keep a wave's 64 points in registers and stream the k centroids through
+// an LDS ring, one workgroup barrier per 32-centroid tile: 16 MFMAs per wave
+// between barriers, and the stamps put ~830 of a tile's ~2240 cycles in the
+// DMA wait + barrier + refill (profiles/r05_exact_v3_ab.json).  v4 turns the
+// loop inside out.  One persistent 8-wave workgroup per CU holds the WHOLE
+// centroid image in registers — wave w owns centroids [32 TPW w, 32 TPW (w+1)),
+// 32 TPW VGPRs of A fragments, loaded once — and streams 32-point blocks
+// through a 4-slot LDS ring.  Per block every wave runs TPW tiles × 8 k-steps
+// = 32 MFMAs (TPW = 4) on the block's B fragments (8 ds_read_b128, shared by
+// all its tiles): ONE barrier per 32 MFMAs per wave (2× v3's), 4× fewer LDS
+// fragment bytes per MFMA, and no centroid DMA at all.  The block's DMA is one
+// 16-B global_load_lds per thread, issued NS-1 blocks ahead.
+//
+// The running top-2-per-track epilogue is v3's (PackedTop2x8, pair insertion);
+// the score's low 10 bits carry the code 2 (511 - (64 w + 16 t + r)) | (1 - h)
+// (wave, tile, register, lane half), so the top-3 of a lane, and the merge of
+// the 16 (wave, half) top-3s of a point, are plain med3 / max3 on packed
+// floats.  The merge runs one step later (its inputs complete at the next
+// barrier): 16 lanes per point, a 4-round butterfly.  Track rule as v3's: when
+// the best and the second share a (wave, half, register & 3) track, the third
+// is replaced by the best (margin 0: certification step 3 decides).
+//
+// vmcnt bookkeeping is explicit: the DMAs and the result stores are inline
+// asm (hipcc neither counts nor drains them), each step issues exactly one
+// DMA and (from step 1) one 4-byte store per lane — past the last block the
+// DMA reloads the last block into the free slot and a lane without a field of
+// its own rewrites its group's label — so "block j landed" is a fixed count.
+namespace v4 {
+constexpr int kNS = 4;                        // point-block ring slots
+constexpr int kRow = 256;                     // bytes of one 128-feature 16-bit row
+constexpr int kSlot = 32 * kRow;              // one 32-point block
+constexpr int kMaxK = 1024;
+constexpr int kMaxGrid = 256;
+// merge buffer: [source = 2 wave + half][point] f32x4 (b, s, t, -), rows padded
+// so the merge's ds_read_b128 lane groups hit distinct 16-byte bank slots
+template <int WAVES> struct Cfg {
+  static constexpr int kThreads = WAVES * HBMR_WAVE;
+  static constexpr int kSrc = 2 * WAVES;                  // sources per point
+  static constexpr int kMStr = WAVES == 8 ? 34 : 36;      // row stride, 16-B slots
+  static constexpr int kMrg = kSrc * kMStr * 16;
+  static constexpr int kP = 512 / kThreads;               // DMAs per thread per block
+  static constexpr int kOffMrg = kNS * kSlot;
+  static constexpr int kOffBias = kOffMrg + 2 * kMrg;
+  static constexpr int kLds = kOffBias + kMaxK * 4;
+};
+}  // namespace v4
+int g_exact_v4 = -1;   // hbmr_kmeans_set_exact_v4 (-1: HBMR_EXACT_V4 / default on)
+
+__device__ __forceinline__ void v4_glds16(uint32_t lds_base, const void* src) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds_base)
+      : "memory");
+}
+
+__device__ __forceinline__ void v4_store(void* p, uint32_t v) {
+  asm volatile("global_store_dword %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+
+__device__ __forceinline__ void v4_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+__device__ __forceinline__ void v4_ins3(float& b, float& s, float& t, float u) {
+  t = vmed3(s, t, u);
+  s = vmed3(b, s, u);
+  b = vmax3(b, u, u);
+}
+
+// packed code (low 10 bits): 2 (511 - 16 tile - r) | (1 - h), tile = the
+// global 32-centroid tile, r its accumulator register, h the lane half
+__device__ __forceinline__ int v4_cluster(float v) {
+  const uint32_t c = __float_as_uint(v) & 1023u;
+  const int idx = 511 - (int)(c >> 1);
+  const int r = idx & 15;
+  return (idx >> 4) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (int)(1u - (c & 1u));
+}
+
+// the value's track: (owning wave, lane half, register & (NT - 1))
+template <int TPW>
+__device__ __forceinline__ uint32_t v4_track(float v) {
+  const uint32_t c = __float_as_uint(v) & 1023u;
+  const uint32_t idx = 511u - (c >> 1);
+  return ((idx >> 4) / TPW) * 64u + (c & 1u) * 16u + (idx & (PackedTop2x8::NT - 1));
+}
+
+// A workgroup's blocks ascend (g0, g0 + G, ...): the current split's bounds
+// and pointers stay in SGPRs and are reloaded (a short chain of kernarg loads)
+// only when a block crosses into the next split — every ~100 steps here.
+struct V4Walk {
+  int s = 0;
+  long lo = 0, hi = -1, n = 0, off = 0;
+  const char* X = nullptr;
+  __device__ __forceinline__ void at(const SplitTable& t, long b) {
+    if (b >= hi) {
+      while (s + 1 < t.nsplit && t.blk[s + 1] <= b) ++s;
+      s = __builtin_amdgcn_readfirstlane(s);
+      lo = t.blk[s];
+      hi = t.blk[s + 1];
+      n = t.n[s];
+      off = t.off[s];
+      X = reinterpret_cast<const char*>(t.X[s]);
+    }
+  }
+};
+
+template <int N> __device__ __forceinline__ void v4_vmwait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int CTRL> __device__ __forceinline__ float v4_dpp(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+
+// one merge round: this lane's top 3 with the top 3 of a lane holding a
+// disjoint set of sources (the DPP partner)
+template <int CTRL> __device__ __forceinline__ void v4_round(float& b, float& s, float& t) {
+  const float o0 = v4_dpp<CTRL>(b), o1 = v4_dpp<CTRL>(s), o2 = v4_dpp<CTRL>(t);
+  v4_ins3(b, s, t, o0);
+  v4_ins3(b, s, t, o1);
+  v4_ins3(b, s, t, o2);
+}
+
+// the top 3 of a point's SRC sources, one source per lane of an aligned group
+template <int SRC> __device__ __forceinline__ void v4_merge_rounds(float& b, float& s, float& t) {
+  if constexpr (SRC == 16) {           // row_ror 1, 2, 4, 8: {i .. i+2R-1} (mod 16)
+    v4_round<0x121>(b, s, t);
+    v4_round<0x122>(b, s, t);
+    v4_round<0x124>(b, s, t);
+    v4_round<0x128>(b, s, t);
+  } else {                             // xor 1, xor 2 (quad), then the other quad
+    static_assert(SRC == 8, "8 or 16 sources");
+    v4_round<0xB1>(b, s, t);           // quad_perm [1,0,3,2]
+    v4_round<0x4E>(b, s, t);           // quad_perm [2,3,0,1]
+    v4_round<0x141>(b, s, t);          // row_half_mirror: lane i <-> 7 - i
+  }
+}
+
+// diagnostic build (STAMP): per wave, s_memtime sums of the DMA wait, the
+// barrier and the step's work, u64 [grid][waves][4] at g_v4_stamps
+__device__ unsigned long long* g_v4_stamps;
+__device__ __forceinline__ unsigned long long v4_time() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
+template <int WAVES, int TPW, bool F16, bool STAMP = false>
+__global__ __launch_bounds__(WAVES * HBMR_WAVE, WAVES / 4) void kmeans_assign_top3_v4_kernel(
+    const SplitTable tbl, long nblocks, const __bf16* __restrict__ C,
+    const float* __restrict__ chalf, int32_t* __restrict__ labels, int32_t* __restrict__ cand,
+    float* __restrict__ scores, float* __restrict__ margin, long cs) {
+  using Cf = v4::Cfg<WAVES>;
+  constexpr int K = 32 * WAVES * TPW;
+  static_assert(K <= v4::kMaxK, "k_pad <= 1024");
+  constexpr int D = 128, KS = D / 16, P = Cf::kP, SRC = Cf::kSrc;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, col = lane & 31;
+  const long g0 = blockIdx.x, G = gridDim.x;
+  if (g0 >= nblocks) return;
+  const long nsteps = (nblocks - 1 - g0) / G + 1;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+
+  // ---- DMA of step j's block into slot j % 4: P 16-byte pieces per thread
+  // (steps past the end reload the last block: the same count every step)
+  V4Walk wd;
+  auto dma = [&](long j) __attribute__((always_inline)) {
+    const long b = g0 + (j < nsteps ? j : nsteps - 1) * G;
+    wd.at(tbl, b);
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      const int row = i * (Cf::kThreads / 16) + wave * 4 + (lane >> 4);
+      long p = (b - wd.lo) * 32 + row;
+      if (p >= wd.n) p = wd.n - 1;
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(
+          lds0 + (uint32_t)(j & (v4::kNS - 1)) * v4::kSlot +
+          (uint32_t)(i * Cf::kThreads + wave * 64) * 16u);
+      v4_glds16(dst, wd.X + p * v4::kRow + (((lane & 15) ^ (row & 15)) * 16));
+    }
+  };
+#pragma unroll
+  for (int j = 0; j < v4::kNS - 1; ++j) dma(j);
+
+  // ---- stationary operands: -|c|^2/2 of every centroid in LDS, this wave's
+  // A fragments (TPW tiles) in registers
+  float* bias = reinterpret_cast<float*>(smem + Cf::kOffBias);
+  for (int i = tid; i < K; i += Cf::kThreads) bias[i] = chalf[i];
+  bf16x8 A[TPW][KS];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const uint4* row =
+        reinterpret_cast<const uint4*>(C + (size_t)((wave * TPW + t) * 32 + col) * D);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) A[t][s] = __builtin_bit_cast(bf16x8, row[2 * s + h]);
+  }
+  // wait for the A loads HERE (and mark the registers as defined by the asm):
+  // otherwise hipcc keeps them pending across the loop's back edge and waits
+  // vmcnt(0) — draining the ring's DMAs — in every step
+#pragma unroll
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(A[t][s]));
+  uint32_t vmask;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(vmask) : "s"(~1023u));
+  const uint32_t hbit = 1u - (uint32_t)h;
+
+  // ---- merge of step jm's block (inputs in merge buffer jm & 1) + its store.
+  // Step 0 merges buffer 1 (never written) into block g0's rows: garbage that
+  // step 1's merge of the same rows overwrites (same lane, same address, in
+  // order) — it keeps the step free of a branch and the store count uniform
+  V4Walk wm;
+  const int q = wave * (64 / SRC) + lane / SRC;       // point of this lane's group
+  const int sub = lane & (SRC - 1);                   // source (2 wave + half) / field
+  auto merge = [&](long jm) __attribute__((always_inline)) {
+    const char* mb = smem + Cf::kOffMrg + (jm & 1) * Cf::kMrg;
+    const f32x4 m = *reinterpret_cast<const f32x4*>(mb + (sub * Cf::kMStr + q) * 16);
+    float b = m[0], s = m[1], t = m[2];
+    v4_merge_rounds<SRC>(b, s, t);
+    if (v4_track<TPW>(b) == v4_track<TPW>(s)) t = b;
+    const long blk = g0 + (jm < 0 ? 0 : jm) * G;
+    wm.at(tbl, blk);
+    long p = (blk - wm.lo) * 32 + q;
+    if (p >= wm.n) p = wm.n - 1;
+    const long pos = wm.off + p;
+    const float bs = __uint_as_float(__float_as_uint(b) & ~1023u);
+    const float ss = __uint_as_float(__float_as_uint(s) & ~1023u);
+    const float ts = __uint_as_float(__float_as_uint(t) & ~1023u);
+    // field of this lane: 0 label, 1 / 2 second / third, 3 score, 4 / 5
+    // margins; the other lanes rewrite the label (selects, not branches)
+    const float fv = sub == 1 ? s : sub == 2 ? t : b;
+    const uint32_t cl = (uint32_t)v4_cluster(fv);
+    const uint32_t v = sub == 3 ? __float_as_uint(bs) : sub == 4 ? __float_as_uint(bs - ss)
+                     : sub == 5 ? __float_as_uint(bs - ts) : cl;
+    char* const fb = sub == 1 || sub == 2 ? reinterpret_cast<char*>(cand)
+                   : sub == 3 ? reinterpret_cast<char*>(scores)
+                   : sub == 4 || sub == 5 ? reinterpret_cast<char*>(margin)
+                   : reinterpret_cast<char*>(labels);
+    v4_store(fb + 4 * (pos + (sub == 2 || sub == 5 ? cs : 0)), v);
+  };
+  auto epilogue = [&](PackedTop2x8& am, const f32x16& acc, int t)
+      __attribute__((always_inline)) {
+    uint32_t code[16];
+    const uint32_t base = (uint32_t)(496 - (wave * TPW + t) * 16) << 1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      code[r] = base | ((15u - r) << 1);
+      asm("" : "+s"(code[r]));
+    }
+    top2_insert(am, acc, code, vmask);
+  };
+
+  unsigned long long st_vm = 0, st_bar = 0, st_work = 0, st_t0 = 0;
+  if constexpr (STAMP) st_t0 = v4_time();
+  const int bx = col & 15;
+  for (long j = 0; j < nsteps; ++j) {
+    unsigned long long t0 = 0, t1 = 0;
+    if constexpr (STAMP) t0 = v4_time();
+    // block j landed: y younger DMAs / stores of this wave,
+    // y = 2P + min(j, 3) (3 prologue blocks; then per step P DMAs, one store)
+    if (j >= 3) v4_vmwait<2 * P + 3>();
+    else if (j == 2) v4_vmwait<2 * P + 2>();
+    else if (j == 1) v4_vmwait<2 * P + 1>();
+    else v4_vmwait<2 * P>();
+    if constexpr (STAMP) t1 = v4_time();
+    v4_barrier();
+    if constexpr (STAMP) {
+      const unsigned long long t2 = v4_time();
+      st_vm += t1 - t0;
+      st_bar += t2 - t1;
+      st_work -= t2;
+    }
+    dma(j + v4::kNS - 1);
+    const char* slot = smem + (j & (v4::kNS - 1)) * v4::kSlot + col * v4::kRow;
+    bf16x8 B[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      B[s] = *reinterpret_cast<const bf16x8*>(slot + (((2 * s + h) ^ bx) << 4));
+    PackedTop2x8 am;
+#pragma unroll
+    for (int i = 0; i < PackedTop2x8::NT; ++i) am.tb[i] = am.ts[i] = -3.0e38f;
+    // tile t's MFMA chain beside tile t-1's epilogue (two accumulator sets);
+    // tile 0's chain beside the previous block's merge
+    f32x16 acc[2];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      f32x16& a = acc[t & 1];
+      const float* bb = bias + (wave * TPW + t) * 32 + 4 * h;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(bb + 8 * g);
+        a[4 * g + 0] = v[0];
+        a[4 * g + 1] = v[1];
+        a[4 * g + 2] = v[2];
+        a[4 * g + 3] = v[3];
+      }
+#pragma unroll
+      for (int s = 0; s < KS; ++s) a = mfma32x32x16<F16>(A[t][s], B[s], a);
+      if (t == 0) merge(j - 1);
+      else epilogue(am, acc[(t - 1) & 1], t - 1);
+    }
+    epilogue(am, acc[(TPW - 1) & 1], TPW - 1);
+    float b, s, t;
+    am.top3(b, s, t);
+    f32x4 o;
+    o[0] = __uint_as_float(__float_as_uint(b) | hbit);
+    o[1] = __uint_as_float(__float_as_uint(s) | hbit);
+    o[2] = __uint_as_float(__float_as_uint(t) | hbit);
+    o[3] = 0.f;
+    *reinterpret_cast<f32x4*>(smem + Cf::kOffMrg + (j & 1) * Cf::kMrg +
+                              ((wave * 2 + h) * Cf::kMStr + col) * 16) = o;
+    if constexpr (STAMP) st_work += v4_time();
+  }
+  v4_barrier();
+  merge(nsteps - 1);
+  // no LDS-DMA may land after the workgroup's LDS is released
+  v4_vmwait<0>();
+  if constexpr (STAMP) {
+    const unsigned long long tot = v4_time() - st_t0;
+    if (lane == 0 && g_v4_stamps) {
+      unsigned long long* o = g_v4_stamps + ((size_t)blockIdx.x * 8 + wave) * 4;
+      o[0] = st_vm;
+      o[1] = st_bar;
+      o[2] = st_work;
+      o[3] = tot;
+    }
+  }
+}
+
+template <int WAVES, int TPW, bool F16, bool STAMP>
+int launch_v4_kernel(unsigned grid, const SplitTable& t, long nb, const void* C,
+                     const float* chalf, int32_t* labels, int32_t* cand, float* scores,
+                     float* margin, long cs, hipStream_t st) {
+  using Cf = v4::Cfg<WAVES>;
+  static bool opt = [] {
+    (void)hipFuncSetAttribute((const void*)kmeans_assign_top3_v4_kernel<WAVES, TPW, F16, STAMP>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, Cf::kLds);
+    (void)hipGetLastError();
+    return true;
+  }();
+  (void)opt;
+  hipLaunchKernelGGL((kmeans_assign_top3_v4_kernel<WAVES, TPW, F16, STAMP>), dim3(grid),
+                     dim3(Cf::kThreads), Cf::kLds, st, t, nb, reinterpret_cast<const __bf16*>(C),
+                     chalf, labels, cand, scores, margin, cs);
+  return (int)hipGetLastError();
+}
+
+// k_pad = 256: 8 waves x 1 tile (two waves per SIMD); 512 / 1024: 4 waves x
+// 4 / 8 tiles at one wave per SIMD, the A fragments partly in AGPRs
+// (hbmr_kmeans_set_exact_v4(3): 8 waves x k_pad / 256 tiles instead)
+template <bool F16, bool STAMP>
+int launch_v4_shape(int k_pad, unsigned grid, const SplitTable& t, long nb, const void* C,
+                    const float* chalf, int32_t* labels, int32_t* cand, float* scores,
+                    float* margin, long cs, hipStream_t st) {
+  const bool eight = g_exact_v4 == 3;
+  switch (k_pad) {
+    case 256:
+      return launch_v4_kernel<8, 1, F16, STAMP>(grid, t, nb, C, chalf, labels, cand, scores, margin, cs, st);
+    case 512:
+      return eight ? launch_v4_kernel<8, 2, F16, STAMP>(grid, t, nb, C, chalf, labels, cand, scores, margin, cs, st)
+                   : launch_v4_kernel<4, 4, F16, STAMP>(grid, t, nb, C, chalf, labels, cand, scores, margin, cs, st);
+    default:
+      return eight ? launch_v4_kernel<8, 4, F16, STAMP>(grid, t, nb, C, chalf, labels, cand, scores, margin, cs, st)
+                   : launch_v4_kernel<4, 8, F16, STAMP>(grid, t, nb, C, chalf, labels, cand, scores, margin, cs, st);
+  }
+}
+
+template <bool F16>
+int launch_assign_top3_v4(int k_pad, const SplitTable& t, long nb, const void* C,
+                          const float* chalf, int32_t* labels, int32_t* cand, float* scores,
+                          float* margin, long cs, hipStream_t st) {
+  static int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = v4::kMaxGrid;
+    return std::max(1, std::min(n, v4::kMaxGrid));
+  }();
+  const unsigned grid = (unsigned)std::min<long>(nb, cus);
+  if (g_exact_v4 == 2)   // the stamped diagnostic build (hbmr_kmeans_set_exact_v4(2))
+    return launch_v4_shape<F16, true>(k_pad, grid, t, nb, C, chalf, labels, cand, scores, margin,
+                                      cs, st);
+  return launch_v4_shape<F16, false>(k_pad, grid, t, nb, C, chalf, labels, cand, scores, margin,
+                                     cs, st);
+}
+
+// v4 where it applies unless HBMR_EXACT_V4=0 (read once) or
+// hbmr_kmeans_set_exact_v4(0) (an A/B harness or a test flips it in-process)
+inline bool use_v4(int d, int k_pad) {
+  static const bool env_on = [] {
+    const char* e = getenv("HBMR_EXACT_V4");
+    return !(e && *e && atoi(e) == 0);
+  }();
+  const bool on = g_exact_v4 < 0 ? env_on : g_exact_v4 != 0;
+  return on && d == 128 && (k_pad == 256 || k_pad == 512 || k_pad == 1024);
+}
+
 template <int D, bool F16>
 int launch_assign_top3_grouped(int nsplit, const void* const* X, const long* n, const void* C,
                                const float* chalf, int k_pad, int32_t* labels, int32_t* cand,
@@ -3618,6 +4025,17 @@ int launch_assign_top3_grouped(int nsplit, const void* const* X, const long* n, 
     t.blk[nsplit] = nb;
     if (nb == 0) return 0;
     if (nb > 0x7fffffffL) return (int)hipErrorInvalidValue;
+    if (use_v4(D, k_pad)) {
+      // v4 walks 32-point blocks
+      long nb4 = 0;
+      for (int i = 0; i < nsplit; ++i) {
+        t.blk[i] = nb4;
+        nb4 += (n[i] + 31) / 32;
+      }
+      t.blk[nsplit] = nb4;
+      return launch_assign_top3_v4<F16>(k_pad, t, nb4, C, chalf, labels, cand, scores, margin,
+                                        total, st);
+    }
     static const bool top3 = [] {
       const char* e = getenv("HBMR_EXACT_EPI");
       return e && strcmp(e, "top3") == 0;
@@ -4338,6 +4756,18 @@ int hbmr_kmeans_exact_prep(const float* x, long n, int d, int ldx, int dp, int f
   hipLaunchKernelGGL(kmeans_exact_prep_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, n, d,
                      ldx, dp, f16, reinterpret_cast<uint16_t*>(x16), xnorm, xn2, xerr);
   return (int)hipGetLastError();
+}
+
+// the v4 exact top-3 kernel: 1 on (where it applies), 0 off, -1 the default
+// (HBMR_EXACT_V4, on); returns the previous setting
+int hbmr_kmeans_set_exact_v4(int v) {
+  const int old = g_exact_v4;
+  g_exact_v4 = v < 0 ? -1 : v;
+  return old;
+}
+
+int hbmr_kmeans_set_v4_stamps(void* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_v4_stamps), &p, sizeof(p));
 }
 
 // the v3 kernel's stamp buffer (kV3Stamp): u32 [64 workgroups][4 waves][32 tiles][8]
