@@ -48,9 +48,7 @@ _SIGS = {
     "hbmr_kmeans_image16": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "hbmr_kmeans_image16_tiled": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
-    "hbmr_kmeans_set_stamps": (c_int, [c_void_p]),
-    "hbmr_kmeans_set_exact_v4": (c_int, [c_int]),
-    "hbmr_kmeans_set_v4_stamps": (c_int, [c_void_p]),
+    "hbmr_kmeans_set_exact_kernel": (c_int, [c_int]),
     "hbmr_kmeans_refine_f32": (c_int, [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
@@ -142,6 +140,7 @@ _SIGS = {
     # GEMM (native/kernels/gemm.hip)
     "hbmr_gemm_bf16_tn": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_long, c_long,
                                   ctypes.c_float, c_int, c_void_p]),
+    "hbmr_gemm_set_kernel": (c_int, [c_int]),
     "hbmr_gemm_bf16_tn_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_long, c_long,
                                      ctypes.c_float, c_int, c_void_p, c_void_p]),
 }

@@ -20,7 +20,8 @@
 // ends at the operand's last valid row, and a piece past K gets an offset
 // beyond the range, so the hardware's range check zero-fills every piece
 // outside the matrix (no padded copies, no predicated VGPR path); stores are
-// masked to M × N.  v2 (HBMR_GEMM=2) keeps the tile-multiple contract.
+// masked to M × N.  Tile-multiple shapes (K % 128 == 0) take the 8-phase
+// kernel below.
 #include "common.h"
 
 #include <cstdlib>
@@ -165,357 +166,232 @@ __global__ __launch_bounds__(kGemmThreads, 1) void gemm_bf16_tn_kernel(
   }
 }
 
-// ---- v2: 4 waves of 128×128 (v_mfma_f32_32x32x16_bf16) ----------------------
-// Same 256×256 tile, K-step, LDS image (XOR-swizzled 128-B rows) and DMA
-// staging as v1, but 4 waves as 2 (M) × 2 (N), each owning a 128×128 block =
-// 4×4 tiles of 32×32: per K-step a wave reads its 128 A rows and 128 B rows
-// once (128 KiB of LDS reads per workgroup instead of v1's 192 KiB for the
-// same 8.4 MFLOP), and issues 64 MFMAs of 32x32x16 (256 accumulators per lane,
-// AGPR-resident).  32x32x16 fragments: lane l holds row (l & 31) at k-offset
-// 8 (l >> 5) of a 16-wide step; C register r of lane l is row
-// (r & 3) + 8 (r >> 2) + 4 (l >> 5), column l & 31.
-constexpr int kGemmThreads2 = 256;
+// ---- 8-phase kernel (tile-multiple shapes, K % 128 == 0) ------------------
+// cdna_hip_programming.md §5 "The 256² 8-phase template", T2-T5, rebuilt here:
+// the same 256×256 tile and 8 waves (2 M × 4 N, each 128×64 = 8×4 tiles of
+// v_mfma_f32_16x16x32_bf16), but each K-tile (BK = 64) is computed as four
+// C-quadrant phases of 16 MFMAs, and each operand tile is staged as two
+// 16 KiB SUB-tiles that follow the quadrants: A-sub h holds rows
+// {h·64 .. h·64+63} of both 128-row wave blocks, B-sub h columns
+// {h·32 .. h·32+31} of all four 64-column wave blocks.  A wave's quadrant
+// (mh, nh) reads A-sub mh and B-sub nh only, so a sub-tile is dead as soon as
+// its quadrants have read it and is restaged the next phase:
+//
+//   phase  reads (E = even K-tile buffer, O = odd)  stages (K-tile, sub)   MFMA quadrant
+//   1      E.A0 + E.B0                              (2i+1, A1)             (0,0)
+//   2      E.B1                                     (2i+2, A0)             (0,1)
+//   3      E.A1                                     (2i+2, B0)             (1,1)
+//   4      -             vmcnt(6): O landed         (2i+2, B1)             (1,0)
+//   5-8    the same on O                            (2i+2, A1), (2i+3, A0 / B0 / B1)
+//
+// Every phase: ds_reads, one sub-tile's DMA (2 × 16-B global_load_lds per
+// thread), barrier, lgkmcnt(0), s_setprio(1) + 16 MFMAs + s_setprio(0),
+// barrier.  The DMAs stay in flight across barriers: the only VM waits are
+// the counted vmcnt(6) of phases 4 and 8 (three sub-tiles, i.e. three phases
+// of lead), never 0 in the loop.  Past the last K-tile the DMAs reload the
+// last K-tile into the dead sub-tile (a uniform vmcnt count).  LDS rows are
+// 128 B; chunk c of sub-tile row r sits at chunk c ^ ((r >> 1) & 7): the 16
+// rows of a ds_read_b128 lane group hit 16 distinct bank slots.
+constexpr int kSub8 = 128 * kBK * 2;   // one sub-tile: 16 KiB
+constexpr int kBuf8 = 4 * kSub8;       // A0, A1, B0, B1 of one K-tile: 64 KiB
 
-__device__ __forceinline__ void stage_tile2(char* lds, const __bf16* __restrict__ G, long ld,
-                                            long row0, long k0, int tid) {
+__device__ __forceinline__ bf16x8_t ph8_frag(const char* sub, int lr, int c) {
+  return *reinterpret_cast<const bf16x8_t*>(sub + lr * 128 + ((c ^ ((lr >> 1) & 7)) << 4));
+}
+
+// one sub-tile's DMA through the operand panel's buffer resource: the
+// per-lane byte offsets (vo[i], loop-invariant) plus a scalar offset for the
+// K-tile and the sub-tile (A-sub 1 is 64 rows down, B-sub 1 32 columns)
+__device__ __forceinline__ void ph8_stage(char* sub, __amdgpu_buffer_rsrc_t rs,
+                                          const uint32_t (&vo)[2], uint32_t soff, int tid) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int p = i * kGemmThreads2 + tid;  // 16-B piece index in the tile image
-    const int r = p >> 3, c = p & 7;
-    const int src_c = c ^ (r & 7);
-    const __bf16* g = G + (row0 + r) * ld + k0 + src_c * 8;
-    char* dst = lds + (size_t)(i * kGemmThreads2 + (tid & ~63)) * 16;
-    __builtin_amdgcn_global_load_lds((const void*)g, (void*)dst, 16, 0, 0);
+  for (int i = 0; i < 2; ++i) {
+    char* dst = sub + (size_t)(i * kGemmThreads + (tid & ~63)) * 16;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)dst, 16, vo[i], soff, 0, 0);
   }
 }
 
-template <bool OUT_BF16>
-__global__ __launch_bounds__(kGemmThreads2, 1) void gemm_bf16_tn_v2_kernel(
+// tile order: XCD-contiguous (hbmr_xcd_remap), then GROUP rows at a time
+// (GROUP > 1): the ~32 tiles an XCD runs at once span GROUP A row-panels and
+// 32 / GROUP B column-panels instead of 1 and 32 — fewer distinct operand
+// panels per XCD L2
+template <int GROUP>
+__device__ __forceinline__ void ph8_tile(uint32_t t, long tiles_m, long tiles_n, long& bm,
+                                         long& bn) {
+  if constexpr (GROUP <= 1) {
+    bm = t / tiles_n;
+    bn = t % tiles_n;
+  } else {
+    const long per = (long)GROUP * tiles_n;
+    const long g = t / per, first = g * GROUP;
+    const long gs = tiles_m - first < GROUP ? tiles_m - first : GROUP;
+    const long r = t % per;
+    bm = first + r % gs;
+    bn = r / gs;
+  }
+}
+
+template <bool OUT_BF16, int GROUP>
+__global__ __launch_bounds__(kGemmThreads, 1) void gemm_bf16_tn_8ph_kernel(
     const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void* __restrict__ Cv, long M,
     long N, long K, float alpha, double* __restrict__ partials) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;   // 2 × 2 waves
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
   const long tiles_n = N / kBN;
   const uint32_t t = hbmr_xcd_remap(blockIdx.x, gridDim.x);
-  const long bm = t / tiles_n, bn = t % tiles_n;
+  long bm, bn;
+  ph8_tile<GROUP>(t, M / kBM, tiles_n, bm, bn);
   const long m0 = bm * kBM, n0 = bn * kBN;
-  const int nk = (int)(K / kBK);
+  const int nk = (int)(K / kBK);                    // even
+  auto sub = [&](int buf, int which) __attribute__((always_inline)) {
+    return smem + buf * kBuf8 + which * kSub8;      // which: A0, A1, B0, B1
+  };
+  // operand panels (256 rows x K) as buffer resources; a lane's two pieces of
+  // a sub-tile at byte offsets vo (sub-tile 0, K-tile 0)
+  const __amdgpu_buffer_rsrc_t ra = tile_rsrc(A, K, m0, M);
+  const __amdgpu_buffer_rsrc_t rb = tile_rsrc(Bt, K, n0, N);
+  uint32_t voa[2], vob[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int p = i * kGemmThreads + tid;            // 16-B piece of the sub-tile image
+    const int lr = p >> 3, pos = p & 7;
+    const uint32_t kb = (uint32_t)((pos ^ ((lr >> 1) & 7)) << 4);
+    voa[i] = (uint32_t)(((lr >> 6) * 128 + (lr & 63)) * K * 2) + kb;
+    vob[i] = (uint32_t)(((lr >> 5) * 64 + (lr & 31)) * K * 2) + kb;
+  }
+  auto stage = [&](int kt, int which) __attribute__((always_inline)) {
+    const uint32_t k0b = (uint32_t)((kt < nk ? kt : nk - 1) * kBK * 2);
+    char* dst = sub(kt & 1, which);
+    if (which < 2) ph8_stage(dst, ra, voa, k0b + (uint32_t)(which * 64 * K * 2), tid);
+    else ph8_stage(dst, rb, vob, k0b + (uint32_t)((which - 2) * 32 * K * 2), tid);
+  };
 
-  f32x16 acc[4][4];
+  f32x4 acc[8][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16x8_t a[4][2], b[2][2][2];                     // a[i][kk], b[nh][j][kk]
+  auto readA = [&](int buf, int mh) __attribute__((always_inline)) {
+    const char* s = sub(buf, mh);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  stage_tile2(smem, A, K, m0, 0, tid);
-  stage_tile2(smem + kTileBytes, Bt, K, n0, 0, tid);
-
-  const int fr = lane & 31;   // fragment row (A) / column (B) within a 32-tile
-  const int h = lane >> 5;    // k-offset 8h within a 16-wide step
-
-  for (int kt = 0; kt < nk; ++kt) {
-    char* cur = smem + (kt & 1) * kStageBytes;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kt + 1 < nk) {
-      char* nxt = smem + ((kt + 1) & 1) * kStageBytes;
-      stage_tile2(nxt, A, K, m0, (long)(kt + 1) * kBK, tid);
-      stage_tile2(nxt + kTileBytes, Bt, K, n0, (long)(kt + 1) * kBK, tid);
-    }
-    const char* la = cur;
-    const char* lb = cur + kTileBytes;
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int c = 2 * s + h;  // logical 16-B chunk of the 128-B row
-      bf16x8_t a[4], b[4];
+      for (int kk = 0; kk < 2; ++kk) a[i][kk] = ph8_frag(s, wm * 64 + i * 16 + fr, kk * 4 + fq);
+  };
+  auto readB = [&](int buf, int nh) __attribute__((always_inline)) {
+    const char* s = sub(buf, 2 + nh);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = wm * 128 + i * 32 + fr;
-        a[i] = *reinterpret_cast<const bf16x8_t*>(la + r * 128 + ((c ^ (r & 7)) << 4));
-      }
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r = wn * 128 + j * 32 + fr;
-        b[j] = *reinterpret_cast<const bf16x8_t*>(lb + r * 128 + ((c ^ (r & 7)) << 4));
-      }
+      for (int kk = 0; kk < 2; ++kk)
+        b[nh][j][kk] = ph8_frag(s, wn * 32 + j * 16 + fr, kk * 4 + fq);
+  };
+  auto mma = [&](int mh, int nh) __attribute__((always_inline)) {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
-  }
-
-  // per (i, j) one lane base pointer; the 16 rows of a register block are
-  // uniform multiples of N (scalar offsets)
-  double csum = 0.0;
-  const long lane_off = (m0 + wm * 128 + 4 * h) * N + n0 + wn * 128 + fr;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const long base = lane_off + (long)(i * 32) * N + j * 32;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const long off = base + (long)((r & 3) + 8 * (r >> 2)) * N;
-        const float v = acc[i][j][r] * alpha;
-        if (OUT_BF16) {
-          const uint16_t hv = hbmr_f32_to_bf16(v);
-          reinterpret_cast<uint16_t*>(Cv)[off] = hv;
-          csum += (double)__uint_as_float((uint32_t)hv << 16);
-        } else {
-          reinterpret_cast<float*>(Cv)[off] = v;
-          csum += (double)v;
-        }
-      }
-    }
-  }
-  if (partials) {
-    __shared__ double s_red2[kGemmThreads2 / 64];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) csum += __shfl_xor(csum, o);
-    if (lane == 0) s_red2[wave] = csum;
-    __syncthreads();
-    if (tid == 0) {
-      double sum = 0.0;
-#pragma unroll
-      for (int w = 0; w < kGemmThreads2 / 64; ++w) sum += s_red2[w];
-      partials[blockIdx.x] = sum;
-    }
-  }
-}
-
-
-// Ring kernels (HBMR_GEMM=3 / 4 / 5 / 6): WM × WN waves, each owning a
-// (256/WM) × (256/WN) block of 32×32 tiles (v_mfma_f32_32x32x16_bf16), over a
-// 4-slot ring of K-steps of 32 (4 × 32 KiB of LDS): the loads of K-step k+4
-// are issued in the middle of step k (into step k's slot, once every wave
-// holds its last fragments of it), so a step's operands have three steps to
-// arrive from L2 / HBM instead of one, and a step waits only for its own
-// pieces (a counted vmcnt: the younger steps stay in flight across the
-// barrier, which is a bare s_barrier — __syncthreads()'s release fence waits
-// for every outstanding LDS-DMA, vmcnt(0), and would drain the ring).
-// Fragments are software-pipelined: the second 16-wide half of a K-step
-// loads while the first half's MFMAs run, the next K-step's first half while
-// the second half's run.  PRIO: s_setprio(1) over the MFMA blocks.
-// LDS image of a 256×32 operand tile: rows r and r+1 share a 128-B line
-// L = r/2 (16-B chunk q = 4 (r & 1) + c), chunk q at slot q ^ ((L >> 1) & 3):
-// the 16 lanes of a ds_read_b128 pass (16 consecutive rows, one k-chunk) hit
-// 16 distinct bank groups.
-constexpr int kBKr = 32;
-constexpr int kTiler = kBM * kBKr * 2;    // 16 KiB
-constexpr int kStager = 2 * kTiler;       // A + B: 32 KiB
-constexpr int kRingr = 4;
-constexpr int kLdsr = kRingr * kStager;   // 128 KiB
-
-template <int THREADS>
-__device__ __forceinline__ void stage_ring(char* lds, const __bf16* __restrict__ G, long ld,
-                                           long row0, long k0, int tid) {
-#pragma unroll
-  for (int i = 0; i < kTiler / 16 / THREADS; ++i) {
-    const int p = i * THREADS + tid;        // 16-B slot in the image (line-major)
-    const int L = p >> 3, slot = p & 7;
-    const int q = slot ^ ((L >> 1) & 3);
-    const int r = 2 * L + (q >> 2), c = q & 3;
-    const __bf16* g = G + (row0 + r) * ld + k0 + c * 8;
-    char* dst = lds + (size_t)(i * THREADS + (tid & ~63)) * 16;
-    __builtin_amdgcn_global_load_lds((const void*)g, (void*)dst, 16, 0, 0);
-  }
-}
-
-// s_waitcnt vmcnt(PER · n) for n in 0..3 (the count is an immediate)
-template <int PER>
-__device__ __forceinline__ void vmcnt_steps(int n) {
-  if (n >= 3)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * PER) : "memory");
-  else if (n == 2)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PER) : "memory");
-  else if (n == 1)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PER) : "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// a fragment read in inline asm: hipcc's own lgkmcnt for compiler-visible
-// ds_reads is conservative at the loop head (it waited for the half-step
-// loaded behind the one the MFMAs need); these are counted by hand
-// (lgkm_wait + sched_barrier: the MFMAs are register-only and would be
-// scheduled past a bare asm wait)
-__device__ __forceinline__ bf16x8_t frag_ring(const char* t, int r, int c) {
-  const int L = r >> 1;
-  const int slot = (((r & 1) << 2) | c) ^ ((L >> 1) & 3);
-  const __attribute__((address_space(3))) char* p =
-      (const __attribute__((address_space(3))) char*)(t + L * 128 + slot * 16);
-  bf16x8_t v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)p));
-  return v;
-}
-
-template <int N>
-__device__ __forceinline__ void lgkm_wait() {
-  asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(N) : "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-template <bool OUT_BF16, int WM, int WN, bool PRIO>
-__global__ __launch_bounds__(64 * WM * WN, 1) void gemm_bf16_tn_ring_kernel(
-    const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, void* __restrict__ Cv, long M,
-    long N, long K, float alpha, double* __restrict__ partials) {
-  constexpr int THREADS = 64 * WM * WN;
-  constexpr int TI = kBM / WM / 32, TJ = kBN / WN / 32;   // 32×32 tiles per wave
-  constexpr int PER = 2 * (kTiler / 16 / THREADS);        // pieces per thread per K-step
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const long tiles_n = N / kBN;
-  const uint32_t t = hbmr_xcd_remap(blockIdx.x, gridDim.x);
-  const long bm = t / tiles_n, bn = t % tiles_n;
-  const long m0 = bm * kBM, n0 = bn * kBN;
-  const int nk = (int)(K / kBKr);
-
-  f32x16 acc[TI][TJ];
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-#pragma unroll
-  for (int s = 0; s < kRingr; ++s) {
-    if (s < nk) {
-      stage_ring<THREADS>(smem + s * kStager, A, K, m0, (long)s * kBKr, tid);
-      stage_ring<THREADS>(smem + s * kStager + kTiler, Bt, K, n0, (long)s * kBKr, tid);
-    }
-  }
-  const int fr = lane & 31;
-  const int h = lane >> 5;
-  const int ra = wm * (kBM / WM) + fr, rb = wn * (kBN / WN) + fr;
-
-  bf16x8_t a0[TI], b0[TJ], a1[TI], b1[TJ];
-  {
-    vmcnt_steps<PER>(nk - 1 < 3 ? nk - 1 : 3);
+        for (int j = 0; j < 2; ++j)
+          acc[mh * 4 + i][nh * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              a[i][kk], b[nh][j][kk], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int i = 0; i < TI; ++i) a0[i] = frag_ring(smem, ra + i * 32, h);
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) b0[j] = frag_ring(smem + kTiler, rb + j * 32, h);
-  }
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* la = smem + (kt & (kRingr - 1)) * kStager;
-#pragma unroll
-    for (int i = 0; i < TI; ++i) a1[i] = frag_ring(la, ra + i * 32, 2 + h);
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) b1[j] = frag_ring(la + kTiler, rb + j * 32, 2 + h);
-    lgkm_wait<TI + TJ>();        // F0 landed (F1's reads may be in flight)
-    if (PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[i], b0[j], acc[i][j], 0, 0, 0);
-    if (PRIO) __builtin_amdgcn_s_setprio(0);
-    if (kt + 1 < nk) {
-      lgkm_wait<0>();
-      vmcnt_steps<PER>(nk - 2 - kt < 2 ? nk - 2 - kt : 2);
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      if (kt + kRingr < nk) {
-        char* nxt = smem + (kt & (kRingr - 1)) * kStager;
-        stage_ring<THREADS>(nxt, A, K, m0, (long)(kt + kRingr) * kBKr, tid);
-        stage_ring<THREADS>(nxt + kTiler, Bt, K, n0, (long)(kt + kRingr) * kBKr, tid);
-      }
-      const char* ln = smem + ((kt + 1) & (kRingr - 1)) * kStager;
-#pragma unroll
-      for (int i = 0; i < TI; ++i) a0[i] = frag_ring(ln, ra + i * 32, h);
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) b0[j] = frag_ring(ln + kTiler, rb + j * 32, h);
-    } else {
-      lgkm_wait<0>();            // F1 landed (the branch above waited before its barrier)
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
-    if (PRIO) __builtin_amdgcn_s_setprio(0);
-  }
+  };
 
+  // prologue: K-tile 0 whole, K-tile 1 but its A1 (phase 1 stages it)
+  stage(0, 0);
+  stage(0, 2);
+  stage(0, 3);
+  stage(0, 1);
+  stage(1, 0);
+  stage(1, 2);
+  stage(1, 3);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nk; kt += 2) {
+    // phases 1-4: even K-tile (buffer 0)
+    readA(0, 0);
+    readB(0, 0);
+    stage(kt + 1, 1);
+    mma(0, 0);
+    readB(0, 1);
+    stage(kt + 2, 0);
+    mma(0, 1);
+    readA(0, 1);
+    stage(kt + 2, 2);
+    mma(1, 1);
+    stage(kt + 2, 3);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    mma(1, 0);
+    // phases 5-8: odd K-tile (buffer 1)
+    readA(1, 0);
+    readB(1, 0);
+    stage(kt + 2, 1);
+    mma(0, 0);
+    readB(1, 1);
+    stage(kt + 3, 0);
+    mma(0, 1);
+    readA(1, 1);
+    stage(kt + 3, 2);
+    mma(1, 1);
+    stage(kt + 3, 3);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    mma(1, 0);
+  }
+  // the DMAs past the last K-tile must land before the LDS is released
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // C/D map of 16x16x32: col = lane & 15, row = 4 (lane >> 4) + reg; wave
+  // accumulator [mh·4 + i][nh·2 + j] is rows wm·128 + mh·64 + 16 i, columns
+  // wn·64 + nh·32 + 16 j of the tile
   double csum = 0.0;
-  const long lane_off = (m0 + wm * (kBM / WM) + 4 * h) * N + n0 + wn * (kBN / WN) + fr;
 #pragma unroll
-  for (int i = 0; i < TI; ++i) {
+  for (int mi = 0; mi < 8; ++mi) {
 #pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const long base = lane_off + (long)(i * 32) * N + j * 32;
+    for (int nj = 0; nj < 4; ++nj) {
+      const long col = n0 + wn * 64 + (nj >> 1) * 32 + (nj & 1) * 16 + fr;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const long off = base + (long)((r & 3) + 8 * (r >> 2)) * N;
-        const float v = acc[i][j][r] * alpha;
+      for (int r = 0; r < 4; ++r) {
+        const long row = m0 + wm * 128 + (mi >> 2) * 64 + (mi & 3) * 16 + fq * 4 + r;
+        const float v = acc[mi][nj][r] * alpha;
         if (OUT_BF16) {
           const uint16_t hv = hbmr_f32_to_bf16(v);
-          reinterpret_cast<uint16_t*>(Cv)[off] = hv;
+          reinterpret_cast<uint16_t*>(Cv)[row * N + col] = hv;
           csum += (double)__uint_as_float((uint32_t)hv << 16);
         } else {
-          reinterpret_cast<float*>(Cv)[off] = v;
+          reinterpret_cast<float*>(Cv)[row * N + col] = v;
           csum += (double)v;
         }
       }
     }
   }
   if (partials) {
-    // (reuses the staging array: a second __shared__ object can make hipcc
-    // wait vmcnt(0) before the loop's first ds_read)
-    __syncthreads();
-    double* red = reinterpret_cast<double*>(smem);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) csum += __shfl_xor(csum, o);
-    if (lane == 0) red[wave] = csum;
+    // reuse the (drained) operand LDS for the 8 wave sums: one LDS object
+    double* s_red = reinterpret_cast<double*>(smem);
+    __syncthreads();
+    if (lane == 0) s_red[wave] = csum;
     __syncthreads();
     if (tid == 0) {
-      double sum = 0.0;
+      double s = 0.0;
 #pragma unroll
-      for (int w = 0; w < WM * WN; ++w) sum += red[w];
-      partials[blockIdx.x] = sum;
+      for (int w = 0; w < kGemmThreads / 64; ++w) s += s_red[w];
+      partials[blockIdx.x] = s;
     }
   }
 }
 
-template <bool OUT_BF16, int WM, int WN, bool PRIO>
-int launch_ring(const void* A, const void* Bt, void* C, long M, long N, long K, float alpha,
-                double* partials, long tiles, hipStream_t st) {
-  static bool set = false;
-  if (!set) {
-    HBMR_RETURN_IF_ERROR(hipFuncSetAttribute(
-        (const void*)gemm_bf16_tn_ring_kernel<OUT_BF16, WM, WN, PRIO>,
-        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsr));
-    set = true;
-  }
-  hipLaunchKernelGGL((gemm_bf16_tn_ring_kernel<OUT_BF16, WM, WN, PRIO>), dim3((unsigned)tiles),
-                     dim3(64 * WM * WN), kLdsr, st, reinterpret_cast<const __bf16*>(A),
-                     reinterpret_cast<const __bf16*>(Bt), C, M, N, K, alpha, partials);
-  return (int)hipGetLastError();
-}
-
-template <bool OUT_BF16>
-int launch_ring_ver(int ver, const void* A, const void* Bt, void* C, long M, long N, long K,
-                    float alpha, double* partials, long tiles, hipStream_t st) {
-  switch (ver) {
-    case 3: return launch_ring<OUT_BF16, 2, 2, false>(A, Bt, C, M, N, K, alpha, partials, tiles, st);
-    case 4: return launch_ring<OUT_BF16, 2, 2, true>(A, Bt, C, M, N, K, alpha, partials, tiles, st);
-    case 5: return launch_ring<OUT_BF16, 2, 4, false>(A, Bt, C, M, N, K, alpha, partials, tiles, st);
-    default: return launch_ring<OUT_BF16, 2, 4, true>(A, Bt, C, M, N, K, alpha, partials, tiles, st);
-  }
-}
-
+int g_gemm_kernel = -1;   // hbmr_gemm_set_kernel: 1 = v1, 8 = 8-phase, -1 = default
 bool g_gemm_lds_set = false;
 
 }  // namespace
@@ -536,32 +412,35 @@ int hbmr_gemm_bf16_tn_ex(const void* A, const void* Bt, void* C, long M, long N,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLds));
     HBMR_RETURN_IF_ERROR(hipFuncSetAttribute((const void*)gemm_bf16_tn_kernel<true>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLds));
-    HBMR_RETURN_IF_ERROR(hipFuncSetAttribute((const void*)gemm_bf16_tn_v2_kernel<false>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLds));
-    HBMR_RETURN_IF_ERROR(hipFuncSetAttribute((const void*)gemm_bf16_tn_v2_kernel<true>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLds));
     g_gemm_lds_set = true;
   }
   const long tiles = ((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
   if (tiles > 0x7fffffffL) return (int)hipErrorInvalidValue;
   const bool ragged = M % kBM || N % kBN || K % kBK;
-  // HBMR_GEMM=2: the 4-wave 128x128 / 32x32x16 double-buffered variant;
-  // 3..6: the ring kernels (A/B against v1), read per call (a bench switches
-  // between them in one process)
-  const char* ev = getenv("HBMR_GEMM");
-  const int ver = ev && *ev >= '2' && *ev <= '6' ? *ev - '0' : 1;
-  if (ver >= 3 && !ragged && K % kBKr == 0)
-    return out_bf16 ? launch_ring_ver<true>(ver, A, Bt, C, M, N, K, alpha, partials, tiles, st)
-                    : launch_ring_ver<false>(ver, A, Bt, C, M, N, K, alpha, partials, tiles, st);
-  if (ver == 2 && !ragged) {
-    if (out_bf16)
-      hipLaunchKernelGGL(gemm_bf16_tn_v2_kernel<true>, dim3((unsigned)tiles), dim3(kGemmThreads2),
-                         kGemmLds, st, reinterpret_cast<const __bf16*>(A),
-                         reinterpret_cast<const __bf16*>(Bt), C, M, N, K, alpha, partials);
-    else
-      hipLaunchKernelGGL(gemm_bf16_tn_v2_kernel<false>, dim3((unsigned)tiles),
-                         dim3(kGemmThreads2), kGemmLds, st, reinterpret_cast<const __bf16*>(A),
-                         reinterpret_cast<const __bf16*>(Bt), C, M, N, K, alpha, partials);
+  // the 8-phase kernel for tile-multiple shapes with an even K-tile count;
+  // v1 (any shape) otherwise or when hbmr_gemm_set_kernel(1) asks for it
+  if (!ragged && K % (2 * kBK) == 0 && g_gemm_kernel != 1) {
+    auto kern = out_bf16 ? (g_gemm_kernel == 8 ? gemm_bf16_tn_8ph_kernel<true, 1>
+                            : g_gemm_kernel == 10 ? gemm_bf16_tn_8ph_kernel<true, 4>
+                                                  : gemm_bf16_tn_8ph_kernel<true, 8>)
+                         : (g_gemm_kernel == 8 ? gemm_bf16_tn_8ph_kernel<false, 1>
+                            : g_gemm_kernel == 10 ? gemm_bf16_tn_8ph_kernel<false, 4>
+                                                  : gemm_bf16_tn_8ph_kernel<false, 8>);
+    static bool opt = [] {
+      for (const void* f : {(const void*)gemm_bf16_tn_8ph_kernel<true, 1>,
+                            (const void*)gemm_bf16_tn_8ph_kernel<true, 4>,
+                            (const void*)gemm_bf16_tn_8ph_kernel<true, 8>,
+                            (const void*)gemm_bf16_tn_8ph_kernel<false, 1>,
+                            (const void*)gemm_bf16_tn_8ph_kernel<false, 4>,
+                            (const void*)gemm_bf16_tn_8ph_kernel<false, 8>})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLds);
+      (void)hipGetLastError();
+      return true;
+    }();
+    (void)opt;
+    hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(kGemmThreads), kGemmLds, st,
+                       reinterpret_cast<const __bf16*>(A), reinterpret_cast<const __bf16*>(Bt), C,
+                       M, N, K, alpha, partials);
     return (int)hipGetLastError();
   }
   if (out_bf16)
@@ -573,6 +452,15 @@ int hbmr_gemm_bf16_tn_ex(const void* A, const void* Bt, void* C, long M, long N,
                        kGemmLds, st, reinterpret_cast<const __bf16*>(A),
                        reinterpret_cast<const __bf16*>(Bt), C, M, N, K, alpha, partials);
   return (int)hipGetLastError();
+}
+
+// the tile-multiple kernel: 1 = v1, 8 = the 8-phase kernel (default), -1
+// restores the default; returns the previous setting (an A/B harness flips
+// it in-process)
+int hbmr_gemm_set_kernel(int v) {
+  const int old = g_gemm_kernel;
+  g_gemm_kernel = v == 1 || v == 8 || v == 9 || v == 10 ? v : -1;
+  return old;
 }
 
 int hbmr_gemm_bf16_tn(const void* A, const void* Bt, void* C, long M, long N, long K, float alpha,

@@ -551,21 +551,19 @@ __device__ __forceinline__ void read_tile32(const char* buf, int col, int h, bf1
 
 struct NoFin {};   // assign_tile_v2's default finish (finish_point)
 
-// HBMR_EXACT_PIPE: the fused exact kernel overlaps each tile's arg-max
-// epilogue with the NEXT tile's MFMAs inside one wave (two accumulator sets,
-// scheduler-interleaved), at 2 waves per SIMD instead of 3.  PMC on the
-// non-pipelined kernel: MFMA pipes 51 % busy, 40 % of wave cycles stalled on
-// issue — the 16 MFMAs of a tile ran back to back and the ~100 epilogue VALU
-// ops after them, so only other waves could fill the MFMA gaps.
-#ifndef HBMR_EXACT_PIPE
-#define HBMR_EXACT_PIPE 0   // default of the runtime switch HBMR_EXACT_PIPE (env)
-#endif
-#ifndef HBMR_EXACT_V3_DEFAULT
-#define HBMR_EXACT_V3_DEFAULT 16   // fused exact kernel: -1 = v2, else a v3 mode (env HBMR_EXACT_V3)
-#endif
+// the fused exact kernel: 3 = v3 (default), 2 = v2 (HBMR_EXACT_V3=v2, read once;
+// hbmr_kmeans_set_exact_kernel overrides it in-process)
+int g_exact_kernel = -1;
+inline int exact_kernel() {
+  static const int env = [] {
+    const char* e = getenv("HBMR_EXACT_V3");
+    return e && strcmp(e, "v2") == 0 ? 2 : 3;
+  }();
+  return g_exact_kernel > 0 ? g_exact_kernel : env;
+}
 
 template <int D, int PB, bool EXACT = false, bool F16 = false, bool TOP3 = false,
-          class Fin = NoFin, bool PIPE = false, int NSV = 4>
+          class Fin = NoFin>
 __device__ __forceinline__ void assign_tile_v2(const __bf16* __restrict__ X, long n,
                                                const __bf16* __restrict__ C,
                                                const float* __restrict__ chalf, int ntiles,
@@ -575,7 +573,7 @@ __device__ __forceinline__ void assign_tile_v2(const __bf16* __restrict__ X, lon
                                                float* __restrict__ margin = nullptr,
                                                long cs = -1, const Fin* fin = nullptr) {
   static_assert(D <= 128, "v2 keeps PB point blocks of D ≤ 128 in registers");
-  using V = AssignV2<D, NSV>;
+  using V = AssignV2<D>;
   constexpr int KS = V::KS;
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid / HBMR_WAVE);
@@ -620,66 +618,6 @@ __device__ __forceinline__ void assign_tile_v2(const __bf16* __restrict__ X, lon
 
   const bool w0 = wave == 0;
   int slot = 0;  // t % NS
-  if constexpr (PIPE) {
-    // MFMAs of tile t into `acc`, the epilogue of tile t-1 from `prev`
-    // (before tile 0: scores of -3e38, displaced by the real ones — every
-    // track sees >= 2 real scores per tile), interleaved by the scheduler
-    auto step = [&](int t, f32x16 (&acc)[PB], f32x16 (&prev)[PB])
-        __attribute__((always_inline)) {
-      wait_tile_dmas<V::P, V::NS - 2>(max(0, min(V::NS - 2, ntiles - 2 - t)), w0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (t + V::NS < ntiles)
-        stage_tile32<D>(smem + slot * V::BUF, C, chalf, t + V::NS, wave, lane);
-      slot = slot + 1 == V::NS ? 0 : slot + 1;
-      const char* nbuf = smem + slot * V::BUF;
-      const char* nrow = nbuf + col * (D * 2);
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-#pragma unroll
-        for (int pb = 0; pb < PB; ++pb)
-          acc[pb] = mfma32x32x16<F16>(a[s], bfrag[pb][s], s == 0 ? bias : acc[pb]);
-        a[s] = *reinterpret_cast<const bf16x8*>(nrow + (((2 * s + h) ^ aswz) << 4));
-      }
-      {
-        const float* ch = reinterpret_cast<const float*>(nbuf + V::TILE_BYTES);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 v = *reinterpret_cast<const f32x4*>(ch + 8 * g + 4 * h);
-          bias[4 * g + 0] = v[0];
-          bias[4 * g + 1] = v[1];
-          bias[4 * g + 2] = v[2];
-          bias[4 * g + 3] = v[3];
-        }
-      }
-#pragma unroll
-      for (int pb = 0; pb < PB; ++pb) am[pb].update(prev[pb], t - 1);
-#pragma unroll
-      for (int i = 0; i < KS * PB; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);   // then vector ALU
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // and an LDS read
-      }
-    };
-    f32x16 accA[PB], accB[PB];
-#pragma unroll
-    for (int pb = 0; pb < PB; ++pb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) accB[pb][r] = -3.0e38f;
-    int t = 0;
-    for (; t + 1 < ntiles; t += 2) {
-      step(t, accA, accB);
-      step(t + 1, accB, accA);
-    }
-    if (t < ntiles) {
-      step(t, accA, accB);
-#pragma unroll
-      for (int pb = 0; pb < PB; ++pb) am[pb].update(accA[pb], t);
-    } else if (ntiles > 0) {
-#pragma unroll
-      for (int pb = 0; pb < PB; ++pb) am[pb].update(accB[pb], ntiles - 1);
-    }
-  } else
   for (int t = 0; t < ntiles; ++t) {
     // tile t+1's DMA has landed for every wave (younger DMAs in flight: tiles
     // t+2 .. min(t+NS-1, ntiles-1)), and this wave's reads of tile t have
@@ -2777,35 +2715,18 @@ struct FusedQ1Fin {
 //    shared by both point blocks (v2 re-derived them per block: 39 s_add);
 //  * -|c|^2/2 is read from LDS straight into the accumulators (v2 kept a bias
 //    register set and copied it: 16 v_mov per tile);
-//  * kV3Jit: the A fragments are read from the CURRENT tile's ring slot two
-//    k-steps ahead of their MFMAs instead of a whole tile ahead — 8 VGPRs of A
-//    live instead of 32 (the slot refilled at the top of tile t is t-1's, so
-//    the DMA lead is NS-1 tiles);
-//  * kV3Prio: s_setprio 1 while a wave issues its MFMA chain and 0 for its
-//    epilogue, so the waves of a SIMD hand the matrix pipe to each other;
-//  * kV3Pipe: tile t-1's epilogue is interleaved with tile t's MFMAs in the
-//    wave (two accumulator sets; implies kV3Jit);
-//  * kV3Half: a half-tile pipeline with no extra accumulators — block 0's
-//    MFMA chain beside block 1's epilogue of the previous tile and vice versa;
-//  * kV3Pair: two tiles per barrier step (the per-step wait, barrier, loop and
-//    stamps measured ~830 of a tile's ~2240 cycles per wave); the ring slots
-//    are refilled from inside the epilogue (an LDS-DMA issued among VALU costs
-//    a fraction of one issued beside the barrier), and the next tile's
-//    -|c|^2/2 is read between the two blocks' epilogues so its latency hides
-//    behind the second (kV3Ns6: a 6-slot ring, one more step of DMA lead);
-//  * kV3Tiled: the centroid image in the tiled (piece-major) layout of
-//    hbmr_kmeans_image16_tiled: a tile's DMA is lane-linear on both sides and
-//    a lane's k-step s is at a fixed immediate offset (s * 1 KiB) from one
-//    base register — no XOR-swizzle offsets (8 VGPRs) or per-read address
-//    VALU; 16 lanes of one k-step read 256 contiguous bytes (conflict-free).
-constexpr int kV3Jit = 1, kV3Prio = 2, kV3Pipe = 4, kV3Half = 8, kV3Tiled = 16, kV3Stamp = 32,
-              kV3Pair = 64, kV3Ns6 = 128, kV3Reord = 256;
-// kV3Stamp (base path only): s_memtime stamps of 6 points of every tile, per
-// wave, kept in LDS and copied at the end to g_v3_stamps for workgroups < 64
-// (hbmr_kmeans_set_stamps) — where a tile's cycles go
-__device__ uint32_t* g_v3_stamps;
-constexpr int kV3StampBytes = 4 * 32 * 8 * 4;
-
+//  * the centroid image is tiled (piece-major, hbmr_kmeans_image16_tiled): a
+//    tile's DMA is lane-linear on both sides and a lane's k-step s is at a
+//    fixed immediate offset (s * 1 KiB) from one base register — no
+//    XOR-swizzle offsets (8 VGPRs) or per-read address VALU; 16 lanes of one
+//    k-step read 256 contiguous bytes (conflict-free).
+// Measured negatives, removed in round 6 (profiles/r05_exact_v3_ab.json):
+// just-in-time A reads at 4 waves per SIMD, s_setprio over the MFMA chain,
+// epilogue pipelining (two accumulator sets), a half-tile pipeline, two tiles
+// per barrier step, a 6-slot ring and DMA reordering; so was v4, which keeps
+// the centroids stationary in registers and streams the points
+// (profiles/r06_exact_v4_ab.json): its per-block cross-wave merge makes it
+// VALU-issue bound.
 // tiled image: tile t is 32 * D * 2 contiguous bytes already in LDS order
 template <int D>
 __device__ __forceinline__ void stage_tile32t(char* buf, const __bf16* __restrict__ Ct,
@@ -2854,26 +2775,17 @@ __device__ __forceinline__ void top2_insert(PackedTop2x8& am, const f32x16& acc,
   }
 }
 
-template <int D, bool F16, int MODE, int NS = (MODE & kV3Ns6) ? 6 : 4>
+template <int D, bool F16>
 __device__ __forceinline__ void assign_tile_v3(const __bf16* __restrict__ X, long n,
-                                               const __bf16* __restrict__ C,
+                                               const __bf16* __restrict__ Ct,
                                                const float* __restrict__ chalf, int ntiles,
                                                int32_t* __restrict__ labels, long blk, char* smem,
                                                const FusedQ1Fin& fin) {
   static_assert(D <= 128, "v3 keeps two 32-point blocks of D <= 128 in registers");
-  constexpr int PB = 2;
+  constexpr int PB = 2, NS = 4;
   using V = AssignV2<D, NS>;
   static_assert(V::WAVES == 4, "v3: 4 waves per workgroup");
   constexpr int KS = V::KS;
-  constexpr bool PIPE = (MODE & kV3Pipe) != 0;
-  constexpr bool JIT = PIPE || (MODE & kV3Jit) != 0;
-  constexpr bool PRIO = (MODE & kV3Prio) != 0;
-  constexpr bool HALF = (MODE & kV3Half) != 0 && !JIT;
-  constexpr bool TILED = (MODE & kV3Tiled) != 0;
-  constexpr bool STAMP = (MODE & kV3Stamp) != 0;
-  constexpr bool PAIR = (MODE & kV3Pair) != 0 && !JIT && !HALF;
-  constexpr bool REORD = (MODE & kV3Reord) != 0;
-  constexpr int SWZ = AssignCfg<D>::SWZ;
   // the bias sits right after the tile's rows whatever D is
   static_assert(V::TILE_BYTES == 32 * D * 2, "tile layout");
   const int tid = threadIdx.x;
@@ -2882,19 +2794,10 @@ __device__ __forceinline__ void assign_tile_v3(const __bf16* __restrict__ X, lon
   const int h = lane >> 5;
   const int col = lane & 31;
   const long p0 = blk * (V::WAVES * PB * 32) + (long)wave * PB * 32;
-  const int aswz = col & SWZ;
-  // `row` is the tile buffer + rowoff: row-major rows (XOR-swizzled pieces)
-  // or the tiled layout (k-step s of this lane at s KiB)
-  const int rowoff = TILED ? h * 512 + col * 16 : col * (D * 2);
+  // a tile buffer + rowoff: this lane's k-step s at s KiB (tiled layout)
+  const int rowoff = h * 512 + col * 16;
   auto frag = [&](const char* row, int s) __attribute__((always_inline)) {
-    if constexpr (TILED)
-      return *reinterpret_cast<const bf16x8*>(row + s * 1024);
-    else
-      return *reinterpret_cast<const bf16x8*>(row + (((2 * s + h) ^ aswz) << 4));
-  };
-  auto stage = [&](char* buf, int tile) __attribute__((always_inline)) {
-    if constexpr (TILED) stage_tile32t<D>(buf, C, chalf, tile, wave, lane);
-    else stage_tile32<D>(buf, C, chalf, tile, wave, lane);
+    return *reinterpret_cast<const bf16x8*>(row + s * 1024);
   };
   auto bias = [&](const char* buf, f32x16& acc) __attribute__((always_inline)) {
     const float* ch = reinterpret_cast<const float*>(buf + V::TILE_BYTES);
@@ -2908,10 +2811,9 @@ __device__ __forceinline__ void assign_tile_v3(const __bf16* __restrict__ X, lon
     }
   };
 
-  constexpr int LEAD = JIT || HALF || PAIR ? NS - 1 : NS;   // tiles staged before tile 0
 #pragma unroll
-  for (int i = 0; i < LEAD; ++i)
-    if (i < ntiles) stage(smem + i * V::BUF, i);
+  for (int i = 0; i < NS; ++i)
+    if (i < ntiles) stage_tile32t<D>(smem + i * V::BUF, Ct, chalf, i, wave, lane);
 
   bf16x8 bfrag[PB][KS];
 #pragma unroll
@@ -2935,315 +2837,38 @@ __device__ __forceinline__ void assign_tile_v3(const __bf16* __restrict__ X, lon
   const uint32_t top = am[0].top;
   const uint32_t vmask = am[0].vmask;   // one copy for both blocks
 
-  if constexpr (HALF) {
-    // half-tile software pipeline: block 0's MFMA chain of tile t runs beside
-    // block 1's epilogue of tile t-1, block 1's chain beside block 0's epilogue
-    // of tile t and the LDS reads of tile t+1 — each 8-MFMA chain (256 matrix
-    // cycles) carries 40 VALU, 5 per MFMA gap, with no extra accumulator set.
-    // -|c|^2/2 is read straight into an accumulator once its epilogue is done,
-    // so the slot refilled at the top of tile t is tile t-1's (every read of
-    // it retired): tile t+1 must have landed there, a DMA lead of NS-2 tiles.
-    bf16x8 a[KS];
-    f32x16 acc0, acc1;
-    {
-      const char* row = smem + rowoff;
+  // v2's ring (tile t+1's A read during tile t), codes shared, bias into acc
+  bf16x8 a[KS];
+  f32x16 bz;
+  {
+    const char* row = smem + rowoff;
 #pragma unroll
-      for (int s = 0; s < KS; ++s) a[s] = frag(row, s);
-      bias(smem, acc0);
+    for (int s = 0; s < KS; ++s) a[s] = frag(row, s);
+    bias(smem, bz);
+  }
+  int slot = 0;
+  for (int t = 0; t < ntiles; ++t) {
+    wait_tile_dmas<V::P, NS - 2>(max(0, min(NS - 2, ntiles - 2 - t)), w0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    char* rbuf = smem + slot * V::BUF;
+    if (t + NS < ntiles) stage_tile32t<D>(rbuf, Ct, chalf, t + NS, wave, lane);
+    slot = slot + 1 == NS ? 0 : slot + 1;
+    const char* nbuf = smem + slot * V::BUF;
+    const char* nrow = nbuf + rowoff;
+    f32x16 acc[PB];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc1[r] = -3.0e38f;   // "tile -1": displaced
-    }
-    int slot = 0;                // t % NS
-    auto step = [&](int t, uint32_t (&code)[16], const uint32_t (&cprev)[16])
-        __attribute__((always_inline)) {
-      wait_tile_dmas<V::P, NS - 3>(max(0, min(NS - 3, ntiles - 2 - t)), w0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __syncthreads();
-      const int pslot = slot == 0 ? NS - 1 : slot - 1;
-      if (t + NS - 1 < ntiles)
-        stage(smem + pslot * V::BUF, t + NS - 1);
-      const char* cbuf = smem + slot * V::BUF;
-      slot = slot + 1 == NS ? 0 : slot + 1;
-      const char* nbuf = smem + slot * V::BUF;   // tile t+1 (stale past the end)
-      const char* nrow = nbuf + rowoff;
-      tile_codes(top, t, code);
-      // phase A: block 0's chain of tile t, block 1's epilogue of tile t-1
+    for (int s = 0; s < KS; ++s) {
 #pragma unroll
-      for (int s = 0; s < KS; ++s) acc0 = mfma32x32x16<F16>(a[s], bfrag[0][s], acc0);
-      top2_insert(am[1], acc1, cprev, vmask);
-      bias(cbuf, acc1);
-      // (the epilogue first, so the bias reads that follow it have the last
-      // MFMAs of the chain to land before phase B's first MFMA needs them)
-#pragma unroll
-      for (int i = 0; i < KS - 2; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-      // phase B: block 1's chain of tile t, block 0's epilogue of tile t, and
-      // tile t+1's A fragments read as the chain frees their registers
-#pragma unroll
-      for (int s = 0; s < KS; ++s) acc1 = mfma32x32x16<F16>(a[s], bfrag[1][s], acc1);
-      top2_insert(am[0], acc0, code, vmask);
-#pragma unroll
-      for (int s = 0; s < KS; ++s) a[s] = frag(nrow, s);
-      bias(nbuf, acc0);
-#pragma unroll
-      for (int i = 0; i < KS; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-    };
-    uint32_t cA[16], cB[16];
-    tile_codes(top, -1, cB);
-    int t = 0;
-    for (; t + 1 < ntiles; t += 2) {
-      step(t, cA, cB);
-      step(t + 1, cB, cA);
-    }
-    if (t < ntiles) {
-      step(t, cA, cB);
-      top2_insert(am[1], acc1, cA, vmask);
-    } else if (ntiles > 0) {
-      top2_insert(am[1], acc1, cB, vmask);
-    }
-  } else if constexpr (PAIR) {
-    // step j: tiles 2j and 2j+1 behind one barrier.  Tile t's A fragments are
-    // read during tile t-1's MFMAs and its -|c|^2/2 between tile t-1's two
-    // epilogues, so after the barrier at the top of step j every read of the
-    // slots of tiles 2j-1 and 2j has retired: step j refills them with tiles
-    // 2j-1+NS and 2j+NS, and needs tiles 2j+1 and 2j+2 landed at its top.
-    static_assert(NS == 4 || NS == 6, "pair ring depth");
-    bf16x8 a[KS];
-    f32x16 bz;
-    {
-      const char* row = smem + rowoff;
-#pragma unroll
-      for (int s = 0; s < KS; ++s) a[s] = frag(row, s);
-      bias(smem, bz);
-    }
-    uint32_t* stl = reinterpret_cast<uint32_t*>(smem + NS * V::BUF) + wave * 256;
-    auto stamp = [&](int j, int e) __attribute__((always_inline)) {
-      if constexpr (STAMP) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (lane == 0 && j < 32) stl[j * 8 + e] = (uint32_t)__builtin_amdgcn_s_memtime();
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    };
-    // one tile: MFMAs on A(t) (reading A(t+1) from nslot as each k-step frees
-    // its registers), block 1's epilogue, bias(t+1), the refill DMA, block 0's
-    auto tile = [&](int t, const char* nbuf, char* rbuf, int rtile)
-        __attribute__((always_inline)) {
-      const char* nrow = nbuf + rowoff;
-      f32x16 acc[PB];
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-#pragma unroll
-        for (int pb = 0; pb < PB; ++pb)
-          acc[pb] = mfma32x32x16<F16>(a[s], bfrag[pb][s], s == 0 ? bz : acc[pb]);
-        a[s] = frag(nrow, s);
-      }
-      uint32_t code[16];
-      tile_codes(top, t, code);
-      top2_insert(am[1], acc[1], code, vmask);
-      bias(nbuf, bz);
-      if (rtile < ntiles) stage(rbuf, rtile);
-      top2_insert(am[0], acc[0], code, vmask);
-    };
-    for (int j = 0; 2 * j < ntiles; ++j) {
-      const int t0 = 2 * j;
-      stamp(j, 0);
-      if constexpr (NS == 4) {
-        vm_wait<0>();
-      } else {
-        const int y = max(0, min(2, ntiles - 3 - t0));
-        if (y == 2) { if (w0) vm_wait<2 * (V::P + 1)>(); else vm_wait<2 * V::P>(); }
-        else if (y == 1) { if (w0) vm_wait<V::P + 1>(); else vm_wait<V::P>(); }
-        else vm_wait<0>();
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      stamp(j, 1);
-      __syncthreads();
-      stamp(j, 2);
-      // slots: tile t lives in slot t % NS
-      char* s_m1 = smem + ((t0 + NS - 1) % NS) * V::BUF;   // tile 2j-1's slot
-      char* s_0 = smem + (t0 % NS) * V::BUF;               // tile 2j's
-      const char* s_1 = smem + ((t0 + 1) % NS) * V::BUF;   // tile 2j+1's
-      const char* s_2 = smem + ((t0 + 2) % NS) * V::BUF;   // tile 2j+2's
-      tile(t0, s_1, s_m1, t0 - 1 + NS);
-      stamp(j, 3);
-      if (t0 + 1 < ntiles) tile(t0 + 1, s_2, s_0, t0 + NS);
-      stamp(j, 4);
-    }
-    if constexpr (STAMP) {
-      __syncthreads();
-      if (blockIdx.x < 64 && g_v3_stamps)
-        for (int i = lane; i < 256; i += HBMR_WAVE)
-          g_v3_stamps[((size_t)blockIdx.x * 4 + wave) * 256 + i] = stl[i];
-    }
-  } else if constexpr (!JIT) {
-    // v2's ring (tile t+1's A read during tile t), codes shared, bias into acc
-    bf16x8 a[KS];
-    f32x16 bz;
-    {
-      const char* row = smem + rowoff;
-#pragma unroll
-      for (int s = 0; s < KS; ++s) a[s] = frag(row, s);
-      bias(smem, bz);
-    }
-    int slot = 0;
-    uint32_t* stl = reinterpret_cast<uint32_t*>(smem + NS * V::BUF) + wave * 256;
-    auto stamp = [&](int t, int e) __attribute__((always_inline)) {
-      if constexpr (STAMP) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (lane == 0 && t < 32) stl[t * 8 + e] = (uint32_t)__builtin_amdgcn_s_memtime();
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    };
-    for (int t = 0; t < ntiles; ++t) {
-      stamp(t, 0);
-      wait_tile_dmas<V::P, NS - 2>(max(0, min(NS - 2, ntiles - 2 - t)), w0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      stamp(t, 1);
-      __syncthreads();
-      stamp(t, 2);
-      char* rbuf = smem + slot * V::BUF;
-      if constexpr (!REORD)
-        if (t + NS < ntiles) stage(rbuf, t + NS);
-      slot = slot + 1 == NS ? 0 : slot + 1;
-      const char* nbuf = smem + slot * V::BUF;
-      const char* nrow = nbuf + rowoff;
-      stamp(t, 3);
-      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
-      f32x16 acc[PB];
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-#pragma unroll
-        for (int pb = 0; pb < PB; ++pb)
-          acc[pb] = mfma32x32x16<F16>(a[s], bfrag[pb][s], s == 0 ? bz : acc[pb]);
-        a[s] = frag(nrow, s);
-      }
-      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-      stamp(t, 4);
-      uint32_t code[16];
-      tile_codes(top, t, code);
-      if constexpr (REORD) {
-        // block 1's epilogue frees bz's registers (block 1 accumulates in
-        // them), then bias(t+1) and the refill DMA go out among block 0's VALU
-        top2_insert(am[1], acc[1], code, vmask);
-        bias(nbuf, bz);
-        if (t + NS < ntiles) stage(rbuf, t + NS);
-        top2_insert(am[0], acc[0], code, vmask);
-        stamp(t, 5);
-      } else {
-#pragma unroll
-        for (int pb = 0; pb < PB; ++pb) top2_insert(am[pb], acc[pb], code, vmask);
-        stamp(t, 5);
-        bias(nbuf, bz);
-      }
-    }
-    if constexpr (STAMP) {
-      __syncthreads();
-      if (blockIdx.x < 64 && g_v3_stamps)
-        for (int i = lane; i < 256; i += HBMR_WAVE)
-          g_v3_stamps[((size_t)blockIdx.x * 4 + wave) * 256 + i] = stl[i];
-    }
-  } else if constexpr (!PIPE) {
-    int slot = 0;                // t % NS
-    for (int t = 0; t < ntiles; ++t) {
-      // tile t landed for every wave (younger DMAs: tiles t+1 .. t+NS-2), and
-      // every wave's reads of tile t-1's slot retired → that slot is free
-      wait_tile_dmas<V::P, NS - 2>(max(0, min(NS - 2, ntiles - 1 - t)), w0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __syncthreads();
-      const int pslot = slot == 0 ? NS - 1 : slot - 1;
-      if (t + NS - 1 < ntiles)
-        stage(smem + pslot * V::BUF, t + NS - 1);
-      const char* buf = smem + slot * V::BUF;
-      const char* row = buf + rowoff;
-      slot = slot + 1 == NS ? 0 : slot + 1;
-      f32x16 bz;
-      bias(buf, bz);
-      bf16x8 a[2];
-      a[0] = frag(row, 0);
-      a[1] = frag(row, 1);
-      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
-      f32x16 acc[PB];
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-#pragma unroll
-        for (int pb = 0; pb < PB; ++pb)
-          acc[pb] = mfma32x32x16<F16>(a[s & 1], bfrag[pb][s], s == 0 ? bz : acc[pb]);
-        if (s + 2 < KS) a[s & 1] = frag(row, s + 2);
-      }
-      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-      uint32_t code[16];
-      tile_codes(top, t, code);
-#pragma unroll
-      for (int pb = 0; pb < PB; ++pb) top2_insert(am[pb], acc[pb], code, vmask);
-    }
-  } else {
-    // MFMAs of tile t into `acc`, the epilogue of tile t-1 from `prev`
-    int slot = 0;
-    auto step = [&](int t, f32x16 (&acc)[PB], f32x16 (&prev)[PB], bool epi)
-        __attribute__((always_inline)) {
-      wait_tile_dmas<V::P, NS - 2>(max(0, min(NS - 2, ntiles - 1 - t)), w0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __syncthreads();
-      const int pslot = slot == 0 ? NS - 1 : slot - 1;
-      if (t + NS - 1 < ntiles)
-        stage(smem + pslot * V::BUF, t + NS - 1);
-      const char* buf = smem + slot * V::BUF;
-      const char* row = buf + rowoff;
-      slot = slot + 1 == NS ? 0 : slot + 1;
-      f32x16 bz;
-      bias(buf, bz);
-      bf16x8 a[2];
-      a[0] = frag(row, 0);
-      a[1] = frag(row, 1);
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-#pragma unroll
-        for (int pb = 0; pb < PB; ++pb)
-          acc[pb] = mfma32x32x16<F16>(a[s & 1], bfrag[pb][s], s == 0 ? bz : acc[pb]);
-        if (s + 2 < KS) a[s & 1] = frag(row, s + 2);
-      }
-      if (epi) {
-        uint32_t code[16];
-        tile_codes(top, t - 1, code);
-#pragma unroll
-        for (int pb = 0; pb < PB; ++pb) top2_insert(am[pb], prev[pb], code, vmask);
-      }
-#pragma unroll
-      for (int i = 0; i < KS * PB; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);   // then vector ALU
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // and an LDS read
-      }
-    };
-    f32x16 accA[PB], accB[PB];
-    int t = 0;
-    if (ntiles > 0) {
-      step(0, accA, accB, false);
-      t = 1;
-    }
-    for (; t + 1 < ntiles; t += 2) {
-      step(t, accB, accA, true);
-      step(t + 1, accA, accB, true);
+      for (int pb = 0; pb < PB; ++pb)
+        acc[pb] = mfma32x32x16<F16>(a[s], bfrag[pb][s], s == 0 ? bz : acc[pb]);
+      a[s] = frag(nrow, s);
     }
     uint32_t code[16];
-    if (t < ntiles) {
-      step(t, accB, accA, true);
-      tile_codes(top, t, code);
+    tile_codes(top, t, code);
 #pragma unroll
-      for (int pb = 0; pb < PB; ++pb) top2_insert(am[pb], accB[pb], code, vmask);
-    } else if (ntiles > 0) {
-      tile_codes(top, ntiles - 1, code);
-#pragma unroll
-      for (int pb = 0; pb < PB; ++pb) top2_insert(am[pb], accA[pb], code, vmask);
-    }
+    for (int pb = 0; pb < PB; ++pb) top2_insert(am[pb], acc[pb], code, vmask);
+    bias(nbuf, bz);
   }
   fin(am, h, p0, col, n, labels);
 }
@@ -3258,8 +2883,8 @@ struct TopQ1Table {       // the batch's splits, by value (X, per-point norms)
   long blk[kMaxGroup + 1];
 };
 
-template <int D, bool F16, bool PIPE, int NSV = 4>
-__global__ __launch_bounds__(AssignV2<D>::THREADS, PIPE ? 2 : HBMR_EXACT_MINB) void
+template <int D, bool F16>
+__global__ __launch_bounds__(AssignV2<D>::THREADS, HBMR_EXACT_MINB) void
 kmeans_assign_top3_q1_grouped_kernel(const TopQ1Table tbl, const __bf16* __restrict__ C,
                                      const float* __restrict__ chalf, int ntiles,
                                      int32_t* __restrict__ labels, FusedQ1Fin fin) {
@@ -3276,16 +2901,16 @@ kmeans_assign_top3_q1_grouped_kernel(const TopQ1Table tbl, const __bf16* __restr
   fin.xbn2 = tbl.xbn2[s];
   fin.xerr = tbl.xerr[s];
   fin.sidx = s;
-  assign_tile_v2<D, 2, true, F16, false, FusedQ1Fin, PIPE, NSV>(
+  assign_tile_v2<D, 2, true, F16, false, FusedQ1Fin>(
       tbl.X[s], tbl.off[s + 1] - o, C, chalf,
                                                      ntiles, labels + o, nullptr, b - tbl.blk[s],
                                                      smem, nullptr, nullptr, -1, &fin);
 }
 
-// v3 (see assign_tile_v3): MINB workgroups of 4 waves per CU
-template <int D, bool F16, int MODE, int MINB>
-__global__ __launch_bounds__(256, MINB) void kmeans_assign_top3_q1_v3_kernel(
-    const TopQ1Table tbl, const __bf16* __restrict__ C, const float* __restrict__ chalf,
+// v3 (see assign_tile_v3): HBMR_EXACT_MINB workgroups of 4 waves per CU
+template <int D, bool F16>
+__global__ __launch_bounds__(256, HBMR_EXACT_MINB) void kmeans_assign_top3_q1_v3_kernel(
+    const TopQ1Table tbl, const __bf16* __restrict__ Ct, const float* __restrict__ chalf,
     int ntiles, int32_t* __restrict__ labels, FusedQ1Fin fin) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const long b = hbmr_xcd_remap(blockIdx.x, gridDim.x);
@@ -3300,8 +2925,8 @@ __global__ __launch_bounds__(256, MINB) void kmeans_assign_top3_q1_v3_kernel(
   fin.xbn2 = tbl.xbn2[s];
   fin.xerr = tbl.xerr[s];
   fin.sidx = s;
-  assign_tile_v3<D, F16, MODE>(tbl.X[s], tbl.off[s + 1] - o, C, chalf, ntiles, labels + o,
-                               b - tbl.blk[s], smem, fin);
+  assign_tile_v3<D, F16>(tbl.X[s], tbl.off[s + 1] - o, Ct, chalf, ntiles, labels + o,
+                         b - tbl.blk[s], smem, fin);
 }
 
 // 16 features of a row per lane of an 8-lane group: 128m + 32h + 4sub + (0..3)
@@ -3593,413 +3218,6 @@ int refine_version() {
   return v;
 }
 
-// ---------------------------------------------------------------------------
-// v4 of the exact top-3 assign: STATIONARY CENTROIDS, STREAMED POINTS
-// (D = 128, fp16/bf16 operands, k_pad = 256 * TPW, TPW = 1, 2 or 4).
-//
-// v2/v3 keep a wave's 64 points in registers and stream the k centroids through
-// an LDS ring, one workgroup barrier per 32-centroid tile: 16 MFMAs per wave
-// between barriers, and the stamps put ~830 of a tile's ~2240 cycles in the
-// DMA wait + barrier + refill (profiles/r05_exact_v3_ab.json).  v4 turns the
-// loop inside out.  One persistent 8-wave workgroup per CU holds the WHOLE
-// centroid image in registers — wave w owns centroids [32 TPW w, 32 TPW (w+1)),
-// 32 TPW VGPRs of A fragments, loaded once — and streams 32-point blocks
-// through a 4-slot LDS ring.  Per block every wave runs TPW tiles × 8 k-steps
-// = 32 MFMAs (TPW = 4) on the block's B fragments (8 ds_read_b128, shared by
-// all its tiles): ONE barrier per 32 MFMAs per wave (2× v3's), 4× fewer LDS
-// fragment bytes per MFMA, and no centroid DMA at all.  The block's DMA is one
-// 16-B global_load_lds per thread, issued NS-1 blocks ahead.
-//
-// The running top-2-per-track epilogue is v3's (PackedTop2x8, pair insertion);
-// the score's low 10 bits carry the code 2 (511 - (64 w + 16 t + r)) | (1 - h)
-// (wave, tile, register, lane half), so the top-3 of a lane, and the merge of
-// the 16 (wave, half) top-3s of a point, are plain med3 / max3 on packed
-// floats.  The merge runs one step later (its inputs complete at the next
-// barrier): 16 lanes per point, a 4-round butterfly.  Track rule as v3's: when
-// the best and the second share a (wave, half, register & 3) track, the third
-// is replaced by the best (margin 0: certification step 3 decides).
-//
-// vmcnt bookkeeping is explicit: the DMAs and the result stores are inline
-// asm (hipcc neither counts nor drains them), each step issues exactly one
-// DMA and (from step 1) one 4-byte store per lane — past the last block the
-// DMA reloads the last block into the free slot and a lane without a field of
-// its own rewrites its group's label — so "block j landed" is a fixed count.
-namespace v4 {
-constexpr int kNS = 4;                        // point-block ring slots
-constexpr int kRow = 256;                     // bytes of one 128-feature 16-bit row
-constexpr int kSlot = 32 * kRow;              // one 32-point block
-constexpr int kMaxK = 1024;
-constexpr int kMaxGrid = 256;
-// merge buffer: [source = 2 wave + half][point] f32x4 (b, s, t, -), rows padded
-// so the merge's ds_read_b128 lane groups hit distinct 16-byte bank slots
-template <int WAVES> struct Cfg {
-  static constexpr int kThreads = WAVES * HBMR_WAVE;
-  static constexpr int kSrc = 2 * WAVES;                  // sources per point
-  static constexpr int kMStr = WAVES == 8 ? 34 : 36;      // row stride, 16-B slots
-  static constexpr int kMrg = kSrc * kMStr * 16;
-  static constexpr int kP = 512 / kThreads;               // DMAs per thread per block
-  static constexpr int kOffMrg = kNS * kSlot;
-  static constexpr int kOffBias = kOffMrg + 2 * kMrg;
-  static constexpr int kLds = kOffBias + kMaxK * 4;
-};
-}  // namespace v4
-int g_exact_v4 = -1;   // hbmr_kmeans_set_exact_v4 (-1: HBMR_EXACT_V4 / default on)
-
-__device__ __forceinline__ void v4_glds16(uint32_t lds_base, const void* src) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(src), "s"(lds_base)
-      : "memory");
-}
-
-__device__ __forceinline__ void v4_store(void* p, uint32_t v) {
-  asm volatile("global_store_dword %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-}
-
-__device__ __forceinline__ void v4_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-__device__ __forceinline__ void v4_ins3(float& b, float& s, float& t, float u) {
-  t = vmed3(s, t, u);
-  s = vmed3(b, s, u);
-  b = vmax3(b, u, u);
-}
-
-// packed code (low 10 bits): 2 (511 - 16 tile - r) | (1 - h), tile = the
-// global 32-centroid tile, r its accumulator register, h the lane half
-__device__ __forceinline__ int v4_cluster(float v) {
-  const uint32_t c = __float_as_uint(v) & 1023u;
-  const int idx = 511 - (int)(c >> 1);
-  const int r = idx & 15;
-  return (idx >> 4) * 32 + (r & 3) + 8 * (r >> 2) + 4 * (int)(1u - (c & 1u));
-}
-
-// the value's track: (owning wave, lane half, register & (NT - 1))
-template <int TPW>
-__device__ __forceinline__ uint32_t v4_track(float v) {
-  const uint32_t c = __float_as_uint(v) & 1023u;
-  const uint32_t idx = 511u - (c >> 1);
-  return ((idx >> 4) / TPW) * 64u + (c & 1u) * 16u + (idx & (PackedTop2x8::NT - 1));
-}
-
-// A workgroup's blocks ascend (g0, g0 + G, ...): the current split's bounds
-// and pointers stay in SGPRs and are reloaded (a short chain of kernarg loads)
-// only when a block crosses into the next split — every ~100 steps here.
-struct V4Walk {
-  int s = 0;
-  long lo = 0, hi = -1, n = 0, off = 0;
-  const char* X = nullptr;
-  __device__ __forceinline__ void at(const SplitTable& t, long b) {
-    if (b >= hi) {
-      while (s + 1 < t.nsplit && t.blk[s + 1] <= b) ++s;
-      s = __builtin_amdgcn_readfirstlane(s);
-      lo = t.blk[s];
-      hi = t.blk[s + 1];
-      n = t.n[s];
-      off = t.off[s];
-      X = reinterpret_cast<const char*>(t.X[s]);
-    }
-  }
-};
-
-template <int N> __device__ __forceinline__ void v4_vmwait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-template <int CTRL> __device__ __forceinline__ float v4_dpp(float x) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
-}
-
-// one merge round: this lane's top 3 with the top 3 of a lane holding a
-// disjoint set of sources (the DPP partner)
-template <int CTRL> __device__ __forceinline__ void v4_round(float& b, float& s, float& t) {
-  const float o0 = v4_dpp<CTRL>(b), o1 = v4_dpp<CTRL>(s), o2 = v4_dpp<CTRL>(t);
-  v4_ins3(b, s, t, o0);
-  v4_ins3(b, s, t, o1);
-  v4_ins3(b, s, t, o2);
-}
-
-// the top 3 of a point's SRC sources, one source per lane of an aligned group
-template <int SRC> __device__ __forceinline__ void v4_merge_rounds(float& b, float& s, float& t) {
-  if constexpr (SRC == 16) {           // row_ror 1, 2, 4, 8: {i .. i+2R-1} (mod 16)
-    v4_round<0x121>(b, s, t);
-    v4_round<0x122>(b, s, t);
-    v4_round<0x124>(b, s, t);
-    v4_round<0x128>(b, s, t);
-  } else {                             // xor 1, xor 2 (quad), then the other quad
-    static_assert(SRC == 8, "8 or 16 sources");
-    v4_round<0xB1>(b, s, t);           // quad_perm [1,0,3,2]
-    v4_round<0x4E>(b, s, t);           // quad_perm [2,3,0,1]
-    v4_round<0x141>(b, s, t);          // row_half_mirror: lane i <-> 7 - i
-  }
-}
-
-// diagnostic build (STAMP): per wave, s_memtime sums of the DMA wait, the
-// barrier and the step's work, u64 [grid][waves][4] at g_v4_stamps
-__device__ unsigned long long* g_v4_stamps;
-__device__ __forceinline__ unsigned long long v4_time() {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-
-template <int WAVES, int TPW, bool F16, bool STAMP = false>
-__global__ __launch_bounds__(WAVES * HBMR_WAVE, WAVES / 4) void kmeans_assign_top3_v4_kernel(
-    const SplitTable tbl, long nblocks, const __bf16* __restrict__ C,
-    const float* __restrict__ chalf, int32_t* __restrict__ labels, int32_t* __restrict__ cand,
-    float* __restrict__ scores, float* __restrict__ margin, long cs) {
-  using Cf = v4::Cfg<WAVES>;
-  constexpr int K = 32 * WAVES * TPW;
-  static_assert(K <= v4::kMaxK, "k_pad <= 1024");
-  constexpr int D = 128, KS = D / 16, P = Cf::kP, SRC = Cf::kSrc;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = lane >> 5, col = lane & 31;
-  const long g0 = blockIdx.x, G = gridDim.x;
-  if (g0 >= nblocks) return;
-  const long nsteps = (nblocks - 1 - g0) / G + 1;
-  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
-
-  // ---- DMA of step j's block into slot j % 4: P 16-byte pieces per thread
-  // (steps past the end reload the last block: the same count every step)
-  V4Walk wd;
-  auto dma = [&](long j) __attribute__((always_inline)) {
-    const long b = g0 + (j < nsteps ? j : nsteps - 1) * G;
-    wd.at(tbl, b);
-#pragma unroll
-    for (int i = 0; i < P; ++i) {
-      const int row = i * (Cf::kThreads / 16) + wave * 4 + (lane >> 4);
-      long p = (b - wd.lo) * 32 + row;
-      if (p >= wd.n) p = wd.n - 1;
-      const uint32_t dst = __builtin_amdgcn_readfirstlane(
-          lds0 + (uint32_t)(j & (v4::kNS - 1)) * v4::kSlot +
-          (uint32_t)(i * Cf::kThreads + wave * 64) * 16u);
-      v4_glds16(dst, wd.X + p * v4::kRow + (((lane & 15) ^ (row & 15)) * 16));
-    }
-  };
-#pragma unroll
-  for (int j = 0; j < v4::kNS - 1; ++j) dma(j);
-
-  // ---- stationary operands: -|c|^2/2 of every centroid in LDS, this wave's
-  // A fragments (TPW tiles) in registers
-  float* bias = reinterpret_cast<float*>(smem + Cf::kOffBias);
-  for (int i = tid; i < K; i += Cf::kThreads) bias[i] = chalf[i];
-  bf16x8 A[TPW][KS];
-#pragma unroll
-  for (int t = 0; t < TPW; ++t) {
-    const uint4* row =
-        reinterpret_cast<const uint4*>(C + (size_t)((wave * TPW + t) * 32 + col) * D);
-#pragma unroll
-    for (int s = 0; s < KS; ++s) A[t][s] = __builtin_bit_cast(bf16x8, row[2 * s + h]);
-  }
-  // wait for the A loads HERE (and mark the registers as defined by the asm):
-  // otherwise hipcc keeps them pending across the loop's back edge and waits
-  // vmcnt(0) — draining the ring's DMAs — in every step
-#pragma unroll
-  for (int t = 0; t < TPW; ++t)
-#pragma unroll
-    for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(A[t][s]));
-  uint32_t vmask;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(vmask) : "s"(~1023u));
-  const uint32_t hbit = 1u - (uint32_t)h;
-
-  // ---- merge of step jm's block (inputs in merge buffer jm & 1) + its store.
-  // Step 0 merges buffer 1 (never written) into block g0's rows: garbage that
-  // step 1's merge of the same rows overwrites (same lane, same address, in
-  // order) — it keeps the step free of a branch and the store count uniform
-  V4Walk wm;
-  const int q = wave * (64 / SRC) + lane / SRC;       // point of this lane's group
-  const int sub = lane & (SRC - 1);                   // source (2 wave + half) / field
-  auto merge = [&](long jm) __attribute__((always_inline)) {
-    const char* mb = smem + Cf::kOffMrg + (jm & 1) * Cf::kMrg;
-    const f32x4 m = *reinterpret_cast<const f32x4*>(mb + (sub * Cf::kMStr + q) * 16);
-    float b = m[0], s = m[1], t = m[2];
-    v4_merge_rounds<SRC>(b, s, t);
-    if (v4_track<TPW>(b) == v4_track<TPW>(s)) t = b;
-    const long blk = g0 + (jm < 0 ? 0 : jm) * G;
-    wm.at(tbl, blk);
-    long p = (blk - wm.lo) * 32 + q;
-    if (p >= wm.n) p = wm.n - 1;
-    const long pos = wm.off + p;
-    const float bs = __uint_as_float(__float_as_uint(b) & ~1023u);
-    const float ss = __uint_as_float(__float_as_uint(s) & ~1023u);
-    const float ts = __uint_as_float(__float_as_uint(t) & ~1023u);
-    // field of this lane: 0 label, 1 / 2 second / third, 3 score, 4 / 5
-    // margins; the other lanes rewrite the label (selects, not branches)
-    const float fv = sub == 1 ? s : sub == 2 ? t : b;
-    const uint32_t cl = (uint32_t)v4_cluster(fv);
-    const uint32_t v = sub == 3 ? __float_as_uint(bs) : sub == 4 ? __float_as_uint(bs - ss)
-                     : sub == 5 ? __float_as_uint(bs - ts) : cl;
-    char* const fb = sub == 1 || sub == 2 ? reinterpret_cast<char*>(cand)
-                   : sub == 3 ? reinterpret_cast<char*>(scores)
-                   : sub == 4 || sub == 5 ? reinterpret_cast<char*>(margin)
-                   : reinterpret_cast<char*>(labels);
-    v4_store(fb + 4 * (pos + (sub == 2 || sub == 5 ? cs : 0)), v);
-  };
-  auto epilogue = [&](PackedTop2x8& am, const f32x16& acc, int t)
-      __attribute__((always_inline)) {
-    uint32_t code[16];
-    const uint32_t base = (uint32_t)(496 - (wave * TPW + t) * 16) << 1;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      code[r] = base | ((15u - r) << 1);
-      asm("" : "+s"(code[r]));
-    }
-    top2_insert(am, acc, code, vmask);
-  };
-
-  unsigned long long st_vm = 0, st_bar = 0, st_work = 0, st_t0 = 0;
-  if constexpr (STAMP) st_t0 = v4_time();
-  const int bx = col & 15;
-  for (long j = 0; j < nsteps; ++j) {
-    unsigned long long t0 = 0, t1 = 0;
-    if constexpr (STAMP) t0 = v4_time();
-    // block j landed: y younger DMAs / stores of this wave,
-    // y = 2P + min(j, 3) (3 prologue blocks; then per step P DMAs, one store)
-    if (j >= 3) v4_vmwait<2 * P + 3>();
-    else if (j == 2) v4_vmwait<2 * P + 2>();
-    else if (j == 1) v4_vmwait<2 * P + 1>();
-    else v4_vmwait<2 * P>();
-    if constexpr (STAMP) t1 = v4_time();
-    v4_barrier();
-    if constexpr (STAMP) {
-      const unsigned long long t2 = v4_time();
-      st_vm += t1 - t0;
-      st_bar += t2 - t1;
-      st_work -= t2;
-    }
-    dma(j + v4::kNS - 1);
-    const char* slot = smem + (j & (v4::kNS - 1)) * v4::kSlot + col * v4::kRow;
-    bf16x8 B[KS];
-#pragma unroll
-    for (int s = 0; s < KS; ++s)
-      B[s] = *reinterpret_cast<const bf16x8*>(slot + (((2 * s + h) ^ bx) << 4));
-    PackedTop2x8 am;
-#pragma unroll
-    for (int i = 0; i < PackedTop2x8::NT; ++i) am.tb[i] = am.ts[i] = -3.0e38f;
-    // tile t's MFMA chain beside tile t-1's epilogue (two accumulator sets);
-    // tile 0's chain beside the previous block's merge
-    f32x16 acc[2];
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-      f32x16& a = acc[t & 1];
-      const float* bb = bias + (wave * TPW + t) * 32 + 4 * h;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(bb + 8 * g);
-        a[4 * g + 0] = v[0];
-        a[4 * g + 1] = v[1];
-        a[4 * g + 2] = v[2];
-        a[4 * g + 3] = v[3];
-      }
-#pragma unroll
-      for (int s = 0; s < KS; ++s) a = mfma32x32x16<F16>(A[t][s], B[s], a);
-      if (t == 0) merge(j - 1);
-      else epilogue(am, acc[(t - 1) & 1], t - 1);
-    }
-    epilogue(am, acc[(TPW - 1) & 1], TPW - 1);
-    float b, s, t;
-    am.top3(b, s, t);
-    f32x4 o;
-    o[0] = __uint_as_float(__float_as_uint(b) | hbit);
-    o[1] = __uint_as_float(__float_as_uint(s) | hbit);
-    o[2] = __uint_as_float(__float_as_uint(t) | hbit);
-    o[3] = 0.f;
-    *reinterpret_cast<f32x4*>(smem + Cf::kOffMrg + (j & 1) * Cf::kMrg +
-                              ((wave * 2 + h) * Cf::kMStr + col) * 16) = o;
-    if constexpr (STAMP) st_work += v4_time();
-  }
-  v4_barrier();
-  merge(nsteps - 1);
-  // no LDS-DMA may land after the workgroup's LDS is released
-  v4_vmwait<0>();
-  if constexpr (STAMP) {
-    const unsigned long long tot = v4_time() - st_t0;
-    if (lane == 0 && g_v4_stamps) {
-      unsigned long long* o = g_v4_stamps + ((size_t)blockIdx.x * 8 + wave) * 4;
-      o[0] = st_vm;
-      o[1] = st_bar;
-      o[2] = st_work;
-      o[3] = tot;
-    }
-  }
-}
-
-template <int WAVES, int TPW, bool F16, bool STAMP>
-int launch_v4_kernel(unsigned grid, const SplitTable& t, long nb, const void* C,
-                     const float* chalf, int32_t* labels, int32_t* cand, float* scores,
-                     float* margin, long cs, hipStream_t st) {
-  using Cf = v4::Cfg<WAVES>;
-  static bool opt = [] {
-    (void)hipFuncSetAttribute((const void*)kmeans_assign_top3_v4_kernel<WAVES, TPW, F16, STAMP>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, Cf::kLds);
-    (void)hipGetLastError();
-    return true;
-  }();
-  (void)opt;
-  hipLaunchKernelGGL((kmeans_assign_top3_v4_kernel<WAVES, TPW, F16, STAMP>), dim3(grid),
-                     dim3(Cf::kThreads), Cf::kLds, st, t, nb, reinterpret_cast<const __bf16*>(C),
-                     chalf, labels, cand, scores, margin, cs);
-  return (int)hipGetLastError();
-}
-
-// k_pad = 256: 8 waves x 1 tile (two waves per SIMD); 512 / 1024: 4 waves x
-// 4 / 8 tiles at one wave per SIMD, the A fragments partly in AGPRs
-// (hbmr_kmeans_set_exact_v4(3): 8 waves x k_pad / 256 tiles instead)
-template <bool F16, bool STAMP>
-int launch_v4_shape(int k_pad, unsigned grid, const SplitTable& t, long nb, const void* C,
-                    const float* chalf, int32_t* labels, int32_t* cand, float* scores,
-                    float* margin, long cs, hipStream_t st) {
-  const bool eight = g_exact_v4 == 3;
-  switch (k_pad) {
-    case 256:
-      return launch_v4_kernel<8, 1, F16, STAMP>(grid, t, nb, C, chalf, labels, cand, scores, margin, cs, st);
-    case 512:
-      return eight ? launch_v4_kernel<8, 2, F16, STAMP>(grid, t, nb, C, chalf, labels, cand, scores, margin, cs, st)
-                   : launch_v4_kernel<4, 4, F16, STAMP>(grid, t, nb, C, chalf, labels, cand, scores, margin, cs, st);
-    default:
-      return eight ? launch_v4_kernel<8, 4, F16, STAMP>(grid, t, nb, C, chalf, labels, cand, scores, margin, cs, st)
-                   : launch_v4_kernel<4, 8, F16, STAMP>(grid, t, nb, C, chalf, labels, cand, scores, margin, cs, st);
-  }
-}
-
-template <bool F16>
-int launch_assign_top3_v4(int k_pad, const SplitTable& t, long nb, const void* C,
-                          const float* chalf, int32_t* labels, int32_t* cand, float* scores,
-                          float* margin, long cs, hipStream_t st) {
-  static int cus = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      n = v4::kMaxGrid;
-    return std::max(1, std::min(n, v4::kMaxGrid));
-  }();
-  const unsigned grid = (unsigned)std::min<long>(nb, cus);
-  if (g_exact_v4 == 2)   // the stamped diagnostic build (hbmr_kmeans_set_exact_v4(2))
-    return launch_v4_shape<F16, true>(k_pad, grid, t, nb, C, chalf, labels, cand, scores, margin,
-                                      cs, st);
-  return launch_v4_shape<F16, false>(k_pad, grid, t, nb, C, chalf, labels, cand, scores, margin,
-                                     cs, st);
-}
-
-// v4 where it applies unless HBMR_EXACT_V4=0 (read once) or
-// hbmr_kmeans_set_exact_v4(0) (an A/B harness or a test flips it in-process)
-inline bool use_v4(int d, int k_pad) {
-  static const bool env_on = [] {
-    const char* e = getenv("HBMR_EXACT_V4");
-    return !(e && *e && atoi(e) == 0);
-  }();
-  const bool on = g_exact_v4 < 0 ? env_on : g_exact_v4 != 0;
-  return on && d == 128 && (k_pad == 256 || k_pad == 512 || k_pad == 1024);
-}
-
 template <int D, bool F16>
 int launch_assign_top3_grouped(int nsplit, const void* const* X, const long* n, const void* C,
                                const float* chalf, int k_pad, int32_t* labels, int32_t* cand,
@@ -4025,17 +3243,6 @@ int launch_assign_top3_grouped(int nsplit, const void* const* X, const long* n, 
     t.blk[nsplit] = nb;
     if (nb == 0) return 0;
     if (nb > 0x7fffffffL) return (int)hipErrorInvalidValue;
-    if (use_v4(D, k_pad)) {
-      // v4 walks 32-point blocks
-      long nb4 = 0;
-      for (int i = 0; i < nsplit; ++i) {
-        t.blk[i] = nb4;
-        nb4 += (n[i] + 31) / 32;
-      }
-      t.blk[nsplit] = nb4;
-      return launch_assign_top3_v4<F16>(k_pad, t, nb4, C, chalf, labels, cand, scores, margin,
-                                        total, st);
-    }
     static const bool top3 = [] {
       const char* e = getenv("HBMR_EXACT_EPI");
       return e && strcmp(e, "top3") == 0;
@@ -4629,88 +3836,28 @@ int hbmr_kmeans_assign_top3_q1_grouped(int nsplit, const void* const* X, const l
   fin.cmax_p = cmax;
   fin.cerrmax_p = cerrmax;
   (void)inflate;
-  // the epilogue-pipelined kernel (HBMR_EXACT_PIPE, read once; env overrides
-  // the build default) or the 3-waves-per-SIMD one
-  static const bool pipe = [] {
-    const char* e = getenv("HBMR_EXACT_PIPE");
-    return e && *e ? atoi(e) != 0 : HBMR_EXACT_PIPE != 0;
-  }();
-  // centroid-tile ring depth of the fused kernel: 4, or 6 (HBMR_EXACT_NS=6:
-  // two more tiles of DMA lead, 50 KB of LDS per workgroup)
-  static const bool ns6 = [] {
-    const char* e = getenv("HBMR_EXACT_NS");
-    return e && atoi(e) == 6;
-  }();
-  // HBMR_EXACT_V3: the v3 fused kernel (assign_tile_v3) in mode M (bits kV3*:
-  // 1 just-in-time A reads at 4 waves per SIMD, 2 MFMA-chain priority, 4 epilogue
-  // pipelining, 8 half-tile pipeline, 16 tiled image); "v2": v2
-  // (read per launch: an A/B harness flips it within one process)
-  const int v3 = [] {
-    const char* e = getenv("HBMR_EXACT_V3");
-    if (!e || !*e) return HBMR_EXACT_V3_DEFAULT;
-    if (strcmp(e, "v2") == 0) return -1;
-    return atoi(e);
-  }();
-#define HBMR_V3_CASE(D, F, M)                                                                  \
-  case M:                                                                                      \
-    kern = kmeans_assign_top3_q1_v3_kernel<D, F, M,                                            \
-                                           (M & kV3Jit) && !(M & kV3Pipe) ? 4 : 3>;            \
-    break;
-#define HBMR_TOP3Q1_V3(D, F)                                                                   \
-  {                                                                                            \
-    decltype(&kmeans_assign_top3_q1_v3_kernel<D, F, 0, 3>) kern = nullptr;                     \
-    switch (v3) {                                                                              \
-      HBMR_V3_CASE(D, F, 0)                                                                    \
-      HBMR_V3_CASE(D, F, 16)                                                                   \
-      HBMR_V3_CASE(D, F, 18)                                                                   \
-      HBMR_V3_CASE(D, F, 24)                                                                   \
-      HBMR_V3_CASE(D, F, 17)                                                                   \
-      HBMR_V3_CASE(D, F, 19)                                                                   \
-      HBMR_V3_CASE(D, F, 20)                                                                   \
-      HBMR_V3_CASE(D, F, 48)                                                                   \
-      HBMR_V3_CASE(D, F, 80)                                                                   \
-      HBMR_V3_CASE(D, F, 208)                                                                  \
-      HBMR_V3_CASE(D, F, 112)                                                                  \
-      HBMR_V3_CASE(D, F, 272)                                                                  \
-      HBMR_V3_CASE(D, F, 274)                                                                  \
-      HBMR_V3_CASE(D, F, 304)                                                                  \
-      default: return (int)hipErrorInvalidValue;                                               \
-    }                                                                                          \
-    if ((v3 & kV3Tiled) && !Ct) return (int)hipErrorInvalidValue;                             \
-    const size_t lds = ((v3 & kV3Ns6) ? AssignV2<D, 6>::LDS_BYTES : AssignV2<D>::LDS_BYTES) + \
-                       ((v3 & kV3Stamp) ? kV3StampBytes : 0);                                  \
-    hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), lds, st, t,                        \
-                       reinterpret_cast<const __bf16*>((v3 & kV3Tiled) ? Ct : C), chalf,       \
-                       k_pad / 32, labels, fin);                                               \
-    return (int)hipGetLastError();                                                             \
+  // the v3 kernel (default; needs the tiled image Ct), or v2
+  // (hbmr_kmeans_set_exact_kernel(2) / HBMR_EXACT_V3=v2, read once)
+  if (exact_kernel() == 3) {
+    if (!Ct) return (int)hipErrorInvalidValue;
+    auto kern = dp == 64 ? (f16 ? kmeans_assign_top3_q1_v3_kernel<64, true>
+                                : kmeans_assign_top3_q1_v3_kernel<64, false>)
+                         : (f16 ? kmeans_assign_top3_q1_v3_kernel<128, true>
+                                : kmeans_assign_top3_q1_v3_kernel<128, false>);
+    const size_t lds = dp == 64 ? AssignV2<64>::LDS_BYTES : AssignV2<128>::LDS_BYTES;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), lds, st, t,
+                       reinterpret_cast<const __bf16*>(Ct), chalf, k_pad / 32, labels, fin);
+    return (int)hipGetLastError();
   }
-  if (v3 >= 0) {
-    if (dp == 64) {
-      if (f16) HBMR_TOP3Q1_V3(64, true)
-      HBMR_TOP3Q1_V3(64, false)
-    }
-    if (f16) HBMR_TOP3Q1_V3(128, true)
-    HBMR_TOP3Q1_V3(128, false)
-  }
-#undef HBMR_V3_CASE
-#undef HBMR_TOP3Q1_V3
-#define HBMR_TOP3Q1(D)                                                                         \
-  {                                                                                            \
-    auto kern = pipe ? (f16 ? kmeans_assign_top3_q1_grouped_kernel<D, true, true>              \
-                            : kmeans_assign_top3_q1_grouped_kernel<D, false, true>)            \
-              : ns6  ? (f16 ? kmeans_assign_top3_q1_grouped_kernel<D, true, false, 6>          \
-                            : kmeans_assign_top3_q1_grouped_kernel<D, false, false, 6>)        \
-                     : (f16 ? kmeans_assign_top3_q1_grouped_kernel<D, true, false>             \
-                            : kmeans_assign_top3_q1_grouped_kernel<D, false, false>);          \
-    const size_t lds = ns6 && !pipe ? AssignV2<D, 6>::LDS_BYTES : AssignV2<D>::LDS_BYTES;      \
-    hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(AssignV2<D>::THREADS),                   \
-                       lds, st, t, reinterpret_cast<const __bf16*>(C),                         \
-                       chalf, k_pad / 32, labels, fin);                                        \
-    return (int)hipGetLastError();                                                             \
-  }
-  if (dp == 64) HBMR_TOP3Q1(64)
-  HBMR_TOP3Q1(128)
-#undef HBMR_TOP3Q1
+  auto kern = dp == 64 ? (f16 ? kmeans_assign_top3_q1_grouped_kernel<64, true>
+                              : kmeans_assign_top3_q1_grouped_kernel<64, false>)
+                       : (f16 ? kmeans_assign_top3_q1_grouped_kernel<128, true>
+                              : kmeans_assign_top3_q1_grouped_kernel<128, false>);
+  const size_t lds = dp == 64 ? AssignV2<64>::LDS_BYTES : AssignV2<128>::LDS_BYTES;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nb),
+                     dim3(dp == 64 ? AssignV2<64>::THREADS : AssignV2<128>::THREADS), lds, st, t,
+                     reinterpret_cast<const __bf16*>(C), chalf, k_pad / 32, labels, fin);
+  return (int)hipGetLastError();
 }
 
 int hbmr_kmeans_refine_f32(const float* X32, long n, int d, int ldx, const float* xnorm,
@@ -4758,21 +3905,12 @@ int hbmr_kmeans_exact_prep(const float* x, long n, int d, int ldx, int dp, int f
   return (int)hipGetLastError();
 }
 
-// the v4 exact top-3 kernel: 1 on (where it applies), 0 off, -1 the default
-// (HBMR_EXACT_V4, on); returns the previous setting
-int hbmr_kmeans_set_exact_v4(int v) {
-  const int old = g_exact_v4;
-  g_exact_v4 = v < 0 ? -1 : v;
+// the fused exact top-3 kernel: 3 (v3, the default) or 2 (v2); -1 restores the
+// default (HBMR_EXACT_V3=v2 selects v2).  Returns the previous setting.
+int hbmr_kmeans_set_exact_kernel(int v) {
+  const int old = g_exact_kernel;
+  g_exact_kernel = v == 2 || v == 3 ? v : -1;
   return old;
-}
-
-int hbmr_kmeans_set_v4_stamps(void* p) {
-  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_v4_stamps), &p, sizeof(p));
-}
-
-// the v3 kernel's stamp buffer (kV3Stamp): u32 [64 workgroups][4 waves][32 tiles][8]
-int hbmr_kmeans_set_stamps(void* p) {
-  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_v3_stamps), &p, sizeof(p));
 }
 
 int hbmr_kmeans_image16_tiled(const void* c16, int k_pad, int dp, void* c16t, hipStream_t st) {

@@ -401,8 +401,7 @@ def test_exact_batch_labels_at_bench_shape():
     """The bench's shape and distribution (k = 1024 centers, d = 128): the
     packed arg-max keeps 9 fewer mantissa bits at k = 1024 (4 + log2(k/32)),
     yet every certified label is the fp64 arg-min of the fp32 data (up to fp64
-    ties), for the default fused kernel and the round-4 one."""
-    import os
+    ties), for the default fused kernel (v3) and the round-4 one (v2)."""
     from hbmr.ops import kmeans as km
     n, d, k, split = 2_000_000, 128, 1024, 250_000
     x = K.synthetic_points(7, 0, n, d, k, "cuda")
@@ -416,20 +415,17 @@ def test_exact_batch_labels_at_bench_shape():
     sps = [km.ExactSplit(x[a:a + split].contiguous(), km.padded_dim(d))
            for a in range(0, n, split)]
     want = truth_labels(x, c)
-    old = os.environ.get("HBMR_EXACT_V3")
+    lib = km._lib.load()
     try:
-        for mode in ("", "v2"):
-            os.environ["HBMR_EXACT_V3"] = mode
+        for kern in (3, 2):                              # v3 (default) and v2
+            lib.hbmr_kmeans_set_exact_kernel(kern)
             st = torch.zeros(5, dtype=torch.int64, device="cuda")
             got = torch.full((n,), -1, dtype=torch.int32, device="cuda")
             km.assign_exact_batch(sps, img, st, got, {})
             assert _only_ties(x, c, got, want) <= 4
             assert st[0].item() > 0                      # the certification had work
     finally:
-        if old is None:
-            os.environ.pop("HBMR_EXACT_V3", None)
-        else:
-            os.environ["HBMR_EXACT_V3"] = old
+        lib.hbmr_kmeans_set_exact_kernel(-1)
 
 
 @pytest.mark.gpu

@@ -85,23 +85,30 @@ def test_matmul_job_gpu(gemm):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ver", ["2", "3", "4", "5", "6"])
-@pytest.mark.parametrize("m,k,n", [(256, 32, 256), (512, 96, 768), (768, 4096, 512),
+@pytest.mark.parametrize("kern", [1, 8])
+@pytest.mark.parametrize("m,k,n", [(256, 128, 256), (512, 384, 768), (768, 4096, 512),
                                    (2048, 1024, 1536)])
-def test_gemm_variants_match_fp32_reference(ver, m, k, n, monkeypatch):
-    """The A/B variants (HBMR_GEMM: 2 = double-buffered 4-wave, 3-6 = the
-    4-slot ring kernels, 4/8 waves, with and without s_setprio) against the
-    fp32 reference on tile-multiple shapes, K from one ring step to 128."""
-    monkeypatch.setenv("HBMR_GEMM", ver)
-    if ver == "2" and k % 64:
-        pytest.skip("v2 needs K % 64")
-    g = torch.Generator().manual_seed(m * 7 + k + n)
-    a = (torch.rand(m, k, generator=g) * 2 - 1).to(torch.bfloat16)
-    bt = (torch.rand(n, k, generator=g) * 2 - 1).to(torch.bfloat16)
-    ref = a.float() @ bt.float().t()
-    c, cs = G.matmul_tn(a.cuda(), bt.cuda(), with_sum=True)
-    c = c.cpu()
-    assert torch.allclose(c, ref, atol=2e-3 * k ** 0.5, rtol=1e-3), (c - ref).abs().max()
-    assert abs(cs.item() - c.double().sum().item()) <= 1e-9 * max(1.0, c.double().abs().sum().item())
-    cb = G.matmul_tn(a.cuda(), bt.cuda(), out_dtype=torch.bfloat16).cpu().float()
-    assert torch.allclose(cb, ref, atol=0.05 * k ** 0.5, rtol=2e-2)
+def test_gemm_kernels_match_fp32_reference(kern, m, k, n):
+    """The tile-multiple kernels (hbmr_gemm_set_kernel: 1 = v1, 8 = the 8-phase
+    kernel, the default) against the fp32 reference, K from one 8-phase
+    iteration (two K-tiles) to 64 of them, plus the fused checksum."""
+    lib = G._lib.load()
+    old = lib.hbmr_gemm_set_kernel(kern)
+    try:
+        g = torch.Generator().manual_seed(m * 7 + k + n)
+        a = (torch.rand(m, k, generator=g) * 2 - 1).to(torch.bfloat16)
+        bt = (torch.rand(n, k, generator=g) * 2 - 1).to(torch.bfloat16)
+        ref = a.float() @ bt.float().t()
+        c, cs = G.matmul_tn(a.cuda(), bt.cuda(), with_sum=True)
+        c = c.cpu()
+        assert torch.allclose(c, ref, atol=2e-3 * k ** 0.5, rtol=1e-3), (c - ref).abs().max()
+        assert abs(cs.item() - c.double().sum().item()) <= \
+            1e-9 * max(1.0, c.double().abs().sum().item())
+        cb = G.matmul_tn(a.cuda(), bt.cuda(), out_dtype=torch.bfloat16).cpu().float()
+        assert torch.allclose(cb, ref, atol=0.05 * k ** 0.5, rtol=2e-2)
+        # A = I with an asymmetric B: a transposed or misplaced C write shows
+        eye = torch.eye(m, k, dtype=torch.bfloat16)
+        ci = G.matmul_tn(eye.cuda(), bt.cuda()).cpu()
+        assert torch.equal(ci, (eye.float() @ bt.float().t()))
+    finally:
+        lib.hbmr_gemm_set_kernel(old)

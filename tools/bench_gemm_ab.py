@@ -1,6 +1,7 @@
-"""A/B of the GEMM kernel variants (HBMR_GEMM) against hipBLASLt (torch.matmul)
-at 8192^3 bf16, interleaved rounds on one device; uniform [-1, 1) operands
-(zero-filled operands read high).  One JSON line per size."""
+"""A/B of the GEMM kernels (hbmr_gemm_set_kernel: 1 = v1, 8 = the 8-phase
+kernel) against hipBLASLt (torch.matmul) at 8192^3 bf16, interleaved rounds on
+one device; uniform [-1, 1) operands (zero-filled operands read high).  One
+JSON line per size: best and median TF/s per arm over the rounds."""
 import json
 import os
 import sys
@@ -13,7 +14,8 @@ def main():
 
     from hbmr.ops import gemm as G
     sizes = [int(x) for x in (sys.argv[1:] or ["8192", "4096"])]
-    vers = os.environ.get("VERS", "1 2 3 4 5 6").split()
+    vers = os.environ.get("VERS", "1 8 9 10").split()
+    lib = G._lib.load()
     for s in sizes:
         x = torch.rand(s, s, device="cuda", dtype=torch.bfloat16) * 2 - 1
         yt = torch.rand(s, s, device="cuda", dtype=torch.bfloat16) * 2 - 1
@@ -25,7 +27,7 @@ def main():
             if v == "blas":
                 fn = lambda: torch.matmul(x, yt.t())  # noqa: E731
             else:
-                os.environ["HBMR_GEMM"] = v
+                lib.hbmr_gemm_set_kernel(int(v))
                 fn = lambda: G.matmul_tn(x, yt, out_dtype=torch.bfloat16)  # noqa: E731
             fn()
             torch.cuda.synchronize()
@@ -39,14 +41,20 @@ def main():
 
         err = {}
         for v in vers:
-            os.environ["HBMR_GEMM"] = v
+            lib.hbmr_gemm_set_kernel(int(v))
             c = G.matmul_tn(x, yt, out_dtype=torch.bfloat16)
             err[v] = float((c.float() - ref.float()).abs().max())
-        for _ in range(3):
+        allt = {}
+        for _ in range(int(os.environ.get("ROUNDS", "5"))):
             for v in ["blas"] + vers:
                 t = run(v)
                 best[v] = min(best.get(v, 1e9), t)
+                allt.setdefault(v, []).append(t)
+        lib.hbmr_gemm_set_kernel(-1)
+        med = {v: sorted(ts)[len(ts) // 2] for v, ts in allt.items()}
         out = {"size": s, "tflops": {v: round(flops / t / 1e12, 1) for v, t in best.items()},
+               "tflops_median": {v: round(flops / t / 1e12, 1) for v, t in med.items()},
+               "vs_hipblaslt_median": {v: round(med["blas"] / t, 3) for v, t in med.items()},
                "max_abs_diff_vs_hipblaslt": err}
         print(json.dumps(out), flush=True)
         del x, yt, ref

@@ -1,11 +1,12 @@
-"""A/B of the fused exact top-3 assign kernels (v2 vs the v3 modes of
-native/kernels/kmeans.hip assign_tile_v3) on the bench's data: 12.5M points x
-128-d, k=1024, after a few Lloyd iterations.  For each mode: the exact batch
-time (top-3 assign with step 1 fused + step 2 + neighbour scan), and the labels
-and certification statistics, which must equal v2's exactly (the MFMA
-accumulation order and the epilogue arithmetic are the same).
+"""A/B of the fused exact top-3 assign kernels (v2 vs v3 of
+native/kernels/kmeans.hip, selected in-process by hbmr_kmeans_set_exact_kernel)
+on the bench's data: 12.5M points x 128-d, k=1024, after a few Lloyd
+iterations.  For each kernel: the exact batch time (top-3 assign with step 1
+fused + step 2 + neighbour scan), and the labels and certification
+statistics, which must equal v2's exactly (the MFMA accumulation order and
+the epilogue arithmetic are the same).
 
-usage: python tools/kbench_v3.py [--modes v2,0,16,24] [--points N] [--reps R]
+usage: python tools/kbench_v3.py [--modes v2,v3] [--points N] [--reps R]
 """
 import argparse
 import json
@@ -43,8 +44,7 @@ def main():
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--reps", type=int, default=7)
-    ap.add_argument("--modes", default="v2,0,16,18,24,17,20")
-    ap.add_argument("--stamps", default="", help="v3 modes with kV3Stamp to time per phase (48)")
+    ap.add_argument("--modes", default="v2,v3")
     a = ap.parse_args()
     dev = torch.device("cuda")
     n, k, d = a.points, a.k, a.d
@@ -65,8 +65,9 @@ def main():
     ref = None
     ref_stats = None
     scratch = {}
+    lib = km._lib.load()
     for mode in a.modes.split(","):
-        os.environ["HBMR_EXACT_V3"] = mode
+        lib.hbmr_kmeans_set_exact_kernel(2 if mode == "v2" else 3)
         out = torch.full((n,), -1, dtype=torch.int32, device=dev)
         stats = torch.zeros(5, dtype=torch.int64, device=dev)
 
@@ -91,45 +92,7 @@ def main():
             r["labels_equal_v2"] = bool(torch.equal(ref, lab_mode))
             r["stats_equal_v2"] = st1 == ref_stats
         print(json.dumps(r), flush=True)
-    if a.stamps:
-        stamps(a, splits, img, scratch, n)
-
-
-def stamps(a, splits, img, scratch, n):
-    """Per-tile phase cycles of the v3 base kernel (mode 48 = tiled + stamps):
-    medians over workgroups < 64, their 4 waves and tiles 4..27."""
-    from hbmr.ops import _lib
-    dev = splits[0].xb.device
-    buf = torch.zeros(64 * 4 * 256, dtype=torch.int32, device=dev)
-    _lib.load().hbmr_kmeans_set_stamps(km._ptr(buf))
-    for mode in a.stamps.split(","):
-        os.environ["HBMR_EXACT_V3"] = mode
-        out = torch.empty(n, dtype=torch.int32, device=dev)
-        st = torch.zeros(5, dtype=torch.int64, device=dev)
-        buf.zero_()
-        km.assign_exact_batch(splits, img, st, out, scratch)
-        torch.cuda.synchronize()
-        s = buf.view(64, 4, 32, 8).to(torch.int64).cpu()
-        s = (s - s[:, :, :1, :1]) & 0xffffffff          # wrap-safe, per wave
-        pair = int(mode) & 64
-        names = (["dma_wait", "barrier", "tile_a", "tile_b", "to_next_top"] if pair else
-                 ["dma_wait", "barrier", "stage", "mfma_issue", "epilogue", "to_next_top"])
-        lo, hi = (2, 14) if pair else (4, 28)
-        per = {}
-        for i, nm in enumerate(names):
-            last = i == len(names) - 1
-            nxt = s[:, :, lo + 1:hi + 1, 0] if last else s[:, :, lo:hi, i + 1]
-            cur = s[:, :, lo:hi, i]
-            per[nm] = int((nxt - cur).median())
-        step = s[:, :, lo + 1:hi + 1, 0] - s[:, :, lo:hi, 0]
-        per["step_period"] = int(step.median())
-        per["tile_period"] = int(step.median()) // (2 if pair else 1)
-        per["p10_p90_step"] = [int(v) for v in torch.quantile(
-            step.double().flatten(), torch.tensor([0.1, 0.9], dtype=torch.float64))]
-        # the wave's share of a phase: medians per phase over every wave and tile
-        per["sum_of_medians"] = sum(v for kk, v in per.items() if kk in names)
-        print(json.dumps({"stamps_mode": mode, "cycles_per_tile": per}), flush=True)
-    _lib.load().hbmr_kmeans_set_stamps(None)
+    lib.hbmr_kmeans_set_exact_kernel(-1)
 
 
 if __name__ == "__main__":
