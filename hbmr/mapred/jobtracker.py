@@ -125,6 +125,7 @@ class Attempt:
     profile_fraction = 0.0       # >0: sampled probe, timed on this fraction of a split
     slots = 1                    # CPU / reduce slots held (memory matching)
     gated = False                # launched staged, behind another job's reduce
+    tombstone = False            # its job was retired while it still ran
     state = P.RUNNING
 
     def __init__(self, aid, tip, tracker, run_on_gpu, device, speculative=False, start=None):
@@ -1159,6 +1160,14 @@ class JobTracker:
             old.retire()
             index = self.attempt_index
             for aid in old.retired_aids:
+                a = index.get(aid)
+                if a is not None and a.state not in P.TERMINAL:
+                    # still running (a sampled CPU probe is never killed; a failed
+                    # or killed job's attempts may be mid-flight): keep it indexed
+                    # as a tombstone so its last report frees the tracker's slot
+                    # and the cost model's running entry
+                    a.tombstone = True
+                    continue
                 index.pop(aid, None)
             old.retired_aids = ()
             self._retired.append(str(old.job_id))
@@ -1405,6 +1414,9 @@ class JobTracker:
         a = self.attempt_index.get(ts.attempt_id)
         if a is None or a.state in P.TERMINAL:
             return
+        if a.tombstone:
+            self._retired_attempt_status(a, ts, actions)
+            return
         a.progress = ts.progress
         a.counters = ts.counters or a.counters
         if ts.start_time:
@@ -1427,6 +1439,30 @@ class JobTracker:
             elif tip.commit_granted != a.aid:
                 actions.append(P.kill_task_action(a.aid))
         self._update_progress(jip)
+
+    def _retired_attempt_status(self, a: Attempt, ts: P.TaskStatus, actions):
+        """A report for an attempt whose job has been retired: once it ends,
+        free what it held (tracker slot, the cost model's running entry; a
+        sampled probe still contributes its measured time) and drop it; one
+        waiting for a commit is told to die (its job is over)."""
+        if ts.state == P.COMMIT_PENDING:
+            actions.append(P.kill_task_action(a.aid))
+            return
+        if ts.state not in P.TERMINAL and ts.state != P.FAILED_UNCLEAN:
+            return
+        jip = a.tip.job
+        now = ts.finish_time or time.time()
+        self._release(a)
+        if a.tip.is_map:
+            if ts.state == P.SUCCEEDED and a.profile_fraction:
+                meas = ts.device_time if ts.device_time > 0 else now - a.start
+                self.cost_model.task_finished(jip.signature, a.aid, False, a.start,
+                                              a.start + max(0.0, meas) / a.profile_fraction)
+            else:
+                self.cost_model.task_finished(jip.signature, a.aid, a.run_on_gpu, a.start, now,
+                                              succeeded=False)
+        a.state = ts.state if ts.state in P.TERMINAL else P.FAILED
+        self.attempt_index.pop(a.aid, None)
 
     def _release(self, a: Attempt):
         if a.tip.is_map and not a._released:

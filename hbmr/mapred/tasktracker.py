@@ -510,19 +510,27 @@ class TaskTracker:
         if not polling:
             return
         if self.report_news and getattr(self.jt, "report", None) is not None:
+            done = False
             try:
                 while True:
                     if not self._report_once(seq):
                         return
                     with self._lock:
                         if not self._report_again:
+                            # the reporter stands down under the lock that saw no
+                            # more news: a notification after this reports itself
+                            # (clearing the flag in `finally`, after
+                            # the lock was dropped, lost one arriving in between)
+                            self._reporting = False
+                            done = True
                             return
                         self._report_again = False
                         seq = self._notify_seq
             finally:
-                with self._lock:
-                    # (news left by a failed round went to the heartbeat: _news)
-                    self._reporting = self._report_again = False
+                if not done:
+                    with self._lock:
+                        # (news left by a failed round went to the heartbeat: _news)
+                        self._reporting = self._report_again = False
         elif self.report_news:
             with self._lock:
                 self._reporting = False

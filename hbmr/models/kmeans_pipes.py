@@ -141,8 +141,15 @@ def iteration_conf(base, inp, out, cen_file, k, d, cpubin=None, gpubin=None, red
     job.set_boolean("hbmr.kmeans.exact", exact)
     # block mode (kmeans_pipes.h): one record per map carrying every cluster's
     # partial (in-mapper combining) instead of one record per cluster — the
-    # same int64 partials, a k-th of the frames through the parent
+    # same int64 partials, a k-th of the frames through the parent.  A block
+    # has one key, so it would send every partial to one reducer: with several
+    # reduces the per-cluster records spread them instead
+    if block and reduces > 1:
+        block = False
     job.set_boolean("hbmr.kmeans.pipes.block", block)
+    # kmeans_gpu reads only job-level keys: the shared GPU child takes the
+    # conf once per job (hbmr/pipes/mux.py)
+    job.set_boolean("hbmr.pipes.gpu.mux.shared.conf", True)
     # the new centroids as raw fp32 bytes in a SequenceFile (read_centroids),
     # not %.9g text: the same floats without a format and a parse per value
     job.set_boolean("hbmr.kmeans.pipes.binary.output", binary)

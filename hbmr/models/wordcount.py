@@ -342,7 +342,7 @@ class WordCountSplitJob(SplitJob):
         already: merge_tables returns them), so no collective here waits for
         the device; the one host read is the compaction after both exchanges
         are enqueued.  An overflowing slot (impossible with exact maxima, kept
-        as a guard) falls back to all_to_all_v."""
+        as a guard) sends every rank to all_to_all_v (an all-reduced flag)."""
         import torch
 
         from ..parallel.collectives import compact_static
@@ -357,7 +357,13 @@ class WordCountSplitJob(SplitJob):
         rc, rcw = comm.all_to_all_v_static(counts, part_words, cap_w)
         got_b = compact_static(rb, rcb, cap_b)
         got_w = compact_static(rc, rcw, cap_w)
-        if got_b is None or got_w is None:
+        # the fallback is a collective: every rank must take it or none (one
+        # rank entering all_to_all_v alone would hang the gang), so the
+        # overflow flags are all-reduced first
+        over = torch.tensor([int(got_b is None or got_w is None)], dtype=torch.int64)
+        if hasattr(comm, "all_reduce_max"):
+            over = comm.all_reduce_max(over)
+        if int(over[0]):
             return comm.all_to_all_v(blob, part_bytes)[0], comm.all_to_all_v(counts, part_words)[0]
         return got_b[0], got_w[0]
 

@@ -8,8 +8,9 @@ The reference runs a GPU map as a Pipes child of its own
 loop).  Per map that costs a process start (or, with hbmr.pipes.child.reuse,
 a socket round trip between one map's DONE and the next RUN_MAP) on top of a
 device map of ~0.1 ms.  Here the map attempts of one device share one child:
-each attempt's thread appends its task (SET_JOB_CONF when the job changes,
-RUN_MAP) to the child's command stream without waiting for the previous map,
+each attempt's thread appends its task (SET_JOB_CONF with the attempt's own
+conf — once per job for apps that declare hbmr.pipes.gpu.mux.shared.conf —
+then RUN_MAP) to the child's command stream without waiting for the previous map,
 up to ``hbmr.pipes.gpu.queue.depth`` maps in flight, and the uplink reader
 hands the child's messages to the head of the FIFO — the child runs its maps
 back to back (its runtime reads the next command as soon as a map is DONE),
@@ -31,6 +32,15 @@ log = logging.getLogger("hbmr.pipes")
 
 MUX = "hbmr.pipes.gpu.mux"
 DEPTH = "hbmr.pipes.gpu.queue.depth"
+# an app that reads only job-level keys from its JobConf may take the conf
+# once per job; by default every attempt's own conf (its mapred.task.id,
+# partition, work output dir, input file ...) goes down with its RUN_MAP, as
+# the reference's per-attempt Application gives each child its own
+# (PipesGPUMapRunner.java:66-79)
+SHARED_CONF = "hbmr.pipes.gpu.mux.shared.conf"
+TASK_KEYS = ("mapred.task.id", "mapred.tip.id", "mapred.task.partition", "mapred.task.is.map",
+             "mapred.work.output.dir", "mapred.output.dir", "map.input.file",
+             "map.input.start", "map.input.length")
 
 
 def _job_key(job):
@@ -119,7 +129,9 @@ class MuxChild:
         job.set_boolean("hbmr.pipes.child.reuse", True)
         self.app = Application(job, None, None, None, None, executable, run_on_gpu=True,
                                gpu_device_id=device, work_dir=work_dir, reuse=True)
-        self.conf_job = _job_key(job)
+        # (the Application's start sent this attempt's conf)
+        self.conf_job = _job_key(job) if job.get_boolean(SHARED_CONF, False) else \
+            (_job_key(job),) + tuple(job.get(k) for k in TASK_KEYS)
         self.dispatch = _FifoHandler(self)
         self.app.uplink.handler = self.dispatch
 
@@ -132,22 +144,27 @@ class MuxChild:
         h = OutputHandler(collector, reporter, key_class, value_class, partitioner)
         if TRACE.on:
             TRACE.instant("pipes.mux.submit")
-        with self.cond:
-            while len(self.fifo) >= self.depth and self.dead is None:
-                self.cond.wait()
-            if self.dead is not None:
-                raise RuntimeError(f"pipes child failed: {self.dead}")
         with self.send_lock:
-            t = _Ticket(h, _job_key(job))
+            # the depth check and the FIFO append in one critical section (and
+            # under send_lock, so the FIFO order is the command order): two
+            # attempts can no longer both pass a full FIFO's check
             with self.cond:
+                while len(self.fifo) >= self.depth and self.dead is None:
+                    self.cond.wait()
+                if self.dead is not None:
+                    raise RuntimeError(f"pipes child failed: {self.dead}")
+                t = _Ticket(h, _job_key(job))
                 self.fifo.append(t)
-            # the task's conf goes down only when the job changes: the
-            # child's task loop keeps the last SET_JOB_CONF
+            # the child's task loop keeps the last SET_JOB_CONF: it is resent
+            # whenever the conf the child would see differs (every attempt has
+            # its own task keys) unless the app shares one conf per job
             jid = t.job_id
-            if jid != self.conf_job:
+            key = jid if job.get_boolean(SHARED_CONF, False) else \
+                (jid,) + tuple(job.get(k) for k in TASK_KEYS)
+            if key != self.conf_job:
                 job.set_boolean("hbmr.pipes.child.reuse", True)
                 self.app.downlink.set_job_conf(job)
-                self.conf_job = jid
+                self.conf_job = key
                 if TRACE.on:
                     TRACE.instant("pipes.mux.conf_sent")
             self.app.downlink.run_map(split, num_reduces, False)

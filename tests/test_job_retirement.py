@@ -44,3 +44,38 @@ def test_jobtracker_control_cost_per_tracker_is_small():
     # (~0.1-0.25 ms measured on an idle host; this container's CPU time varies
     # up to 2x between runs under a parallel test session)
     assert per_tracker < 1.0, (r1, rn)
+
+
+def test_a_probe_outliving_its_retired_job_frees_its_slot():
+    """a sampled CPU probe is never killed, so its job can retire
+    while it runs.  Its attempt stays indexed as a tombstone; the late report
+    frees the tracker's CPU slot and the cost model's running entry (and still
+    contributes the probe's measured time), then drops it."""
+    import jt_microbench as M
+    from hbmr.mapred import protocol as P
+    h = M.Harness(1, points=64_000, split_points=4_000, k=8, d=4,
+                  conf_overrides={"mapred.jobtracker.completeuserjobs.maximum": "2",
+                                  "hbmr.jobtracker.retired.jobs.maximum": "50"})
+    h.run(1, warmup=1)
+    jt = h.jt
+    job = next(j for j in jt.jobs.values() if j.completed() and j.retired is None)
+    tr = jt.trackers[h.names[0]]
+    cpu0 = tr.running_cpu
+    with jt.lock:
+        act = jt.launch(tr, job.maps[0], on_gpu=False, profile_fraction=0.25)
+    aid = act["task"]["attempt_id"] if isinstance(act, dict) else act.task.attempt_id
+    assert aid in tr.running and tr.running_cpu == cpu0 + 1
+    h.run(5, warmup=1)                          # enough completed jobs to retire `job`
+    assert job.retired is not None
+    a = jt.attempt_index.get(aid)
+    assert a is not None and a.tombstone        # kept: it still runs
+    assert aid in tr.running and tr.running_cpu == cpu0 + 1
+    ts = P.TaskStatus(attempt_id=aid, is_map=True, state=P.SUCCEEDED,
+                      start_time=a.start, finish_time=a.start + 0.5)
+    actions = []
+    with jt.lock:
+        jt._update_task_status(tr, ts, actions)
+    assert aid not in jt.attempt_index
+    assert aid not in tr.running and tr.running_cpu == cpu0
+    st = jt.cost_model.stats(job.signature, False)
+    assert aid not in st.running and st.n >= 1   # the probe's 0.5 s / 0.25 counted

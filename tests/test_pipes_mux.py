@@ -1,0 +1,102 @@
+"""The shared GPU Pipes child (hbmr/pipes/mux.py): what goes down its
+command stream per attempt, and its in-flight depth.  Driven on a
+bare MuxChild with a recording downlink; the GPU path itself runs in
+tests/test_kmeans_pipes.py."""
+import collections
+import threading
+import time
+
+from hbmr.mapred.jobconf import JobConf
+from hbmr.pipes import mux
+
+
+class _Down:
+    def __init__(self):
+        self.log = []
+
+    def set_job_conf(self, job):
+        self.log.append(("conf", job.get("mapred.task.id")))
+
+    def run_map(self, split, num_reduces, piped):
+        self.log.append(("run_map", split))
+
+
+class _App:
+    def __init__(self):
+        self.downlink = _Down()
+
+
+def _bare(depth, first_conf):
+    m = mux.MuxChild.__new__(mux.MuxChild)
+    m.depth = depth
+    m.fifo = collections.deque()
+    m.cond = threading.Condition()
+    m.dead = None
+    m.send_lock = threading.Lock()
+    m.maps = 0
+    m.app = _App()
+    shared = first_conf.get_boolean(mux.SHARED_CONF, False)
+    m.conf_job = mux._job_key(first_conf) if shared else \
+        (mux._job_key(first_conf),) + tuple(first_conf.get(k) for k in mux.TASK_KEYS)
+    return m
+
+
+def _attempt(i, job="202610180000_0001", shared=False):
+    c = JobConf()
+    c.set("mapred.task.id", f"attempt_{job}_m_{i:06d}_0")
+    c.set("mapred.task.partition", str(i))
+    c.set_boolean(mux.SHARED_CONF, shared)
+    return c
+
+
+def test_each_attempt_gets_its_own_conf_by_default():
+    m = _bare(8, _attempt(0))
+    for i in range(3):
+        m.submit(_attempt(i), None, None, None, None, None, f"split{i}", 1)
+    # attempt 0's conf went with the child's start; 1 and 2 get theirs
+    assert m.app.downlink.log == [
+        ("run_map", "split0"),
+        ("conf", "attempt_202610180000_0001_m_000001_0"), ("run_map", "split1"),
+        ("conf", "attempt_202610180000_0001_m_000002_0"), ("run_map", "split2")]
+
+
+def test_shared_conf_apps_get_it_once_per_job():
+    m = _bare(8, _attempt(0, shared=True))
+    for i in range(3):
+        m.submit(_attempt(i, shared=True), None, None, None, None, None, f"s{i}", 1)
+    m.submit(_attempt(0, job="202610180000_0002", shared=True), None, None, None, None, None,
+             "t0", 1)
+    confs = [e for e in m.app.downlink.log if e[0] == "conf"]
+    assert confs == [("conf", "attempt_202610180000_0002_m_000000_0")]
+
+
+def test_maps_in_flight_never_exceed_the_depth():
+    m = _bare(2, _attempt(0))
+    peak = [0]
+    real_append = m.fifo.append
+
+    class Q(collections.deque):
+        def append(self, x):
+            super().append(x)
+            peak[0] = max(peak[0], len(self))
+
+    m.fifo = Q()
+    del real_append
+    threads = [threading.Thread(target=m.submit,
+                                args=(_attempt(i), None, None, None, None, None, i, 1))
+               for i in range(6)]
+    for t in threads:
+        t.start()
+    # a consumer completes maps (the uplink's DONE) one at a time
+    done = 0
+    end = time.time() + 10
+    while done < 6 and time.time() < end:
+        with m.cond:
+            if m.fifo:
+                m.fifo.popleft()
+                done += 1
+                m.cond.notify_all()
+        time.sleep(0.002)
+    for t in threads:
+        t.join(5)
+    assert done == 6 and peak[0] <= 2

@@ -49,3 +49,75 @@ def test_reports_in_flight_coalesce_later_news():
         # one more round carried the three: 2 calls for 4 notifications
         assert len(calls) == 2
         assert not tt._reporting and not tt._report_again
+
+
+class _HookLock:
+    """A lock whose release can run a callback once (in the releasing thread)."""
+
+    def __init__(self, inner):
+        self.inner = inner
+        self.hook = None
+
+    def __enter__(self):
+        self.inner.acquire()
+        return self
+
+    def __exit__(self, *exc):
+        self.inner.release()
+        h, self.hook = self.hook, None
+        if h is not None:
+            h()
+
+    def acquire(self, *a, **kw):
+        return self.inner.acquire(*a, **kw)
+
+    def release(self):
+        self.inner.release()
+
+
+def test_news_between_the_reporters_last_check_and_its_exit_is_reported():
+    """ADVICE r5 (lost wake-up): a task finishing right after the in-flight
+    reporter found no more news, but before it stood down, must not be left
+    to the long-poll's timeout — it reports itself at once.  Driven on a bare
+    TaskTracker (no threads of its own) with the window forced open: the
+    reporter's lock release after its last check runs the late notification."""
+    from hbmr.mapred.tasktracker import TaskTracker
+    tt = TaskTracker.__new__(TaskTracker)
+    lock = _HookLock(threading.Lock())
+    tt._lock = lock
+    tt._notify_seq = 0
+    tt._polling = True
+    tt.report_news = True
+    tt._reporting = tt._report_again = False
+    tt._news = threading.Event()
+    tt.name = "tracker_bare"
+    rung = []
+
+    class JT:
+        def report(self, *a, **kw):
+            return {}
+
+        def wakeup(self, name, seq):
+            rung.append(seq)
+
+    tt.jt = JT()
+    calls = []
+    reporter = threading.current_thread()
+    late = threading.Thread(target=tt.notify_jobtracker)
+
+    def fire():
+        if threading.current_thread() is reporter:
+            late.start()
+            late.join(5)
+
+    def report_once(seq):
+        calls.append(threading.current_thread())
+        if len(calls) == 1:
+            lock.hook = fire            # the reporter's next release: its last check
+        return True
+
+    tt._report_once = report_once
+    tt.notify_jobtracker()
+    assert not late.is_alive()
+    assert calls == [reporter, late]    # the late news was reported, by itself
+    assert not tt._reporting and not tt._report_again
