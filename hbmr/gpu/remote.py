@@ -66,6 +66,7 @@ class RemoteGpuRuntime:
         self.resident: set = set()        # (split key, device) in the worker's HBM cache
         self.jobs_sent: set = set()
         self.devinfo: list = []
+        self.worker_info: dict = {}
         self.generation = 0
         self.restarts = 0
         self.deaths = 0
@@ -124,6 +125,8 @@ class RemoteGpuRuntime:
             rc = self.proc.wait(timeout=30)
             raise RuntimeError(f"GPU worker of {tr.name} failed to start (exit {rc})")
         self.devinfo = msg[1]
+        self.worker_info = msg[3] if len(msg) > 3 else {}   # its devices and HW queues
+        self.worker_info["pid"] = msg[2]
         self.jobs_sent = set()
         self._reader = threading.Thread(target=self._read_loop, args=(parent, self.proc),
                                         daemon=True, name=f"{tr.name}-gpuworker-rx")

@@ -25,7 +25,7 @@ tracker (parent and child only; nothing else can connect).
   tracker -> worker: ("init", dict) ("job", jid, conf) ("maps", jid, [spec])
                      ("cpu", spec) ("reduce", spec) ("kill", aid) ("drop", jid)
                      ("probe", device) ("stop",)
-  worker -> tracker: ("ready", [device status], pid)
+  worker -> tracker: ("ready", [device status], pid, {devices, GPU_MAX_HW_QUEUES})
                      ("batch", [("done", status) | ("bulk", aids, dt, out, ctrs)],
                       cache_added, cache_removed)
                      ("probe", device, reason-or-None)
@@ -258,7 +258,10 @@ def serve(sock):
     status = [g.__dict__ for g in runtime.device_status()]
     from ..utils.gctune import tune
     tune()      # torch and the runtime into the permanent GC generation
-    send_msg(sock, ("ready", status, os.getpid()), host.send_lock)
+    send_msg(sock, ("ready", status, os.getpid(),
+                    {"devices": list(devices),
+                     "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")}),
+             host.send_lock)
 
     def _unknown_job(runs):
         # the tracker sent attempts of a job this worker does not hold (it was
