@@ -85,6 +85,13 @@ def _recv_exact(sock, n):
     return bytes(buf)
 
 
+# HBMR_RPC_DUMP=path: the raw request frames this process serves, appended
+# to path_<pid>.bin (4-byte length + msgpack each) — payload sizes and decode
+# costs of the control plane's real messages, offline (tools/rpc_payloads.py)
+_DUMP = (open(f"{os.environ['HBMR_RPC_DUMP']}_{os.getpid()}.bin", "ab")
+         if os.environ.get("HBMR_RPC_DUMP") else None)
+
+
 def _recv_buffered(f):
     """One message from a connection's buffered reader (the length word and
     the body usually arrive in one recv)."""
@@ -95,6 +102,8 @@ def _recv_buffered(f):
     body = f.read(n)
     if len(body) < n:
         raise ConnectionError("connection closed")
+    if _DUMP is not None:
+        _DUMP.write(head + body)
     return msgpack.unpackb(body, raw=False, strict_map_key=False)
 
 
