@@ -302,7 +302,7 @@ __global__ __launch_bounds__(kGemmThreads, 1) void gemm_bf16_tn_8ph_kernel(
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[mh * 4 + i][nh * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              a[i][kk], b[nh][j][kk], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
+              b[nh][j][kk], a[i][kk], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
   };
@@ -350,27 +350,32 @@ __global__ __launch_bounds__(kGemmThreads, 1) void gemm_bf16_tn_8ph_kernel(
   // the DMAs past the last K-tile must land before the LDS is released
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  // C/D map of 16x16x32: col = lane & 15, row = 4 (lane >> 4) + reg; wave
-  // accumulator [mh·4 + i][nh·2 + j] is rows wm·128 + mh·64 + 16 i, columns
-  // wn·64 + nh·32 + 16 j of the tile
+  // The MFMAs take B as their first operand (C^T = B A^T per 16x16 tile):
+  // D col (lane & 15) is a C row and D row 4 (lane >> 4) + reg a C column, so
+  // each lane holds 4 consecutive columns of one row — one 8-B (bf16) or 16-B
+  // (fp32) store per 16x16 tile instead of 4 scalar ones.  Wave accumulator
+  // [mh·4 + i][nh·2 + j] is rows wm·128 + mh·64 + 16 i, columns
+  // wn·64 + nh·32 + 16 j of the tile.
   double csum = 0.0;
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi) {
+    const long row = m0 + wm * 128 + (mi >> 2) * 64 + (mi & 3) * 16 + fr;
 #pragma unroll
     for (int nj = 0; nj < 4; ++nj) {
-      const long col = n0 + wn * 64 + (nj >> 1) * 32 + (nj & 1) * 16 + fr;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const long row = m0 + wm * 128 + (mi >> 2) * 64 + (mi & 3) * 16 + fq * 4 + r;
-        const float v = acc[mi][nj][r] * alpha;
-        if (OUT_BF16) {
-          const uint16_t hv = hbmr_f32_to_bf16(v);
-          reinterpret_cast<uint16_t*>(Cv)[row * N + col] = hv;
-          csum += (double)__uint_as_float((uint32_t)hv << 16);
-        } else {
-          reinterpret_cast<float*>(Cv)[row * N + col] = v;
-          csum += (double)v;
-        }
+      const long col = n0 + wn * 64 + (nj >> 1) * 32 + (nj & 1) * 16 + fq * 4;
+      const f32x4 v = acc[mi][nj] * alpha;
+      if (OUT_BF16) {
+        const uint16_t h0 = hbmr_f32_to_bf16(v[0]), h1 = hbmr_f32_to_bf16(v[1]),
+                       h2 = hbmr_f32_to_bf16(v[2]), h3 = hbmr_f32_to_bf16(v[3]);
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(Cv) + row * N + col) =
+            make_uint2((uint32_t)h0 | ((uint32_t)h1 << 16), (uint32_t)h2 | ((uint32_t)h3 << 16));
+        csum += (double)__uint_as_float((uint32_t)h0 << 16) +
+                (double)__uint_as_float((uint32_t)h1 << 16) +
+                (double)__uint_as_float((uint32_t)h2 << 16) +
+                (double)__uint_as_float((uint32_t)h3 << 16);
+      } else {
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(Cv) + row * N + col) = v;
+        csum += (double)v[0] + (double)v[1] + (double)v[2] + (double)v[3];
       }
     }
   }
@@ -420,19 +425,10 @@ int hbmr_gemm_bf16_tn_ex(const void* A, const void* Bt, void* C, long M, long N,
   // the 8-phase kernel for tile-multiple shapes with an even K-tile count;
   // v1 (any shape) otherwise or when hbmr_gemm_set_kernel(1) asks for it
   if (!ragged && K % (2 * kBK) == 0 && g_gemm_kernel != 1) {
-    auto kern = out_bf16 ? (g_gemm_kernel == 8 ? gemm_bf16_tn_8ph_kernel<true, 1>
-                            : g_gemm_kernel == 10 ? gemm_bf16_tn_8ph_kernel<true, 4>
-                                                  : gemm_bf16_tn_8ph_kernel<true, 8>)
-                         : (g_gemm_kernel == 8 ? gemm_bf16_tn_8ph_kernel<false, 1>
-                            : g_gemm_kernel == 10 ? gemm_bf16_tn_8ph_kernel<false, 4>
-                                                  : gemm_bf16_tn_8ph_kernel<false, 8>);
+    auto kern = out_bf16 ? gemm_bf16_tn_8ph_kernel<true, 4> : gemm_bf16_tn_8ph_kernel<false, 4>;
     static bool opt = [] {
-      for (const void* f : {(const void*)gemm_bf16_tn_8ph_kernel<true, 1>,
-                            (const void*)gemm_bf16_tn_8ph_kernel<true, 4>,
-                            (const void*)gemm_bf16_tn_8ph_kernel<true, 8>,
-                            (const void*)gemm_bf16_tn_8ph_kernel<false, 1>,
-                            (const void*)gemm_bf16_tn_8ph_kernel<false, 4>,
-                            (const void*)gemm_bf16_tn_8ph_kernel<false, 8>})
+      for (const void* f : {(const void*)gemm_bf16_tn_8ph_kernel<true, 4>,
+                            (const void*)gemm_bf16_tn_8ph_kernel<false, 4>})
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kGemmLds);
       (void)hipGetLastError();
       return true;
@@ -459,7 +455,7 @@ int hbmr_gemm_bf16_tn_ex(const void* A, const void* Bt, void* C, long M, long N,
 // it in-process)
 int hbmr_gemm_set_kernel(int v) {
   const int old = g_gemm_kernel;
-  g_gemm_kernel = v == 1 || v == 8 || v == 9 || v == 10 ? v : -1;
+  g_gemm_kernel = v == 1 || v == 8 ? v : -1;
   return old;
 }
 
