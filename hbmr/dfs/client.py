@@ -258,12 +258,19 @@ class DistributedFileSystem:
 
     globStatus = glob_status  # noqa: N815
 
-    def mkdirs(self, path):
-        return self.nn.mkdirs(self._p(path))
+    def mkdirs(self, path, permission=None, owner=None):
+        if permission is None and owner is None:
+            return self.nn.mkdirs(self._p(path))
+        return self.nn.mkdirs(self._p(path), owner=owner, permission=permission)
 
-    def create(self, path, overwrite=True, replication=None, block_size=None):
+    def create(self, path, overwrite=True, replication=None, block_size=None, permission=None,
+               owner=None):
         p = self._p(path)
-        r = self.nn.create(p, overwrite, replication, block_size, self.client)
+        if permission is None and owner is None:
+            r = self.nn.create(p, overwrite, replication, block_size, self.client)
+        else:
+            r = self.nn.create(p, overwrite, replication, block_size, self.client, owner=owner,
+                               permission=permission)
         return io.BufferedWriter(DFSOutputStream(self, p, r["block_size"]), 1 << 20)
 
     def open(self, path, buffering=1 << 20):
@@ -283,6 +290,43 @@ class DistributedFileSystem:
 
     def get_content_summary(self, path):
         return self.nn.get_content_summary(self._p(path))
+
+    def set_owner(self, path, owner=None, group=None):
+        return self.nn.set_owner(self._p(path), owner, group)
+
+    def set_permission(self, path, permission):
+        return self.nn.set_permission(self._p(path), permission)
+
+    def set_times(self, path, mtime=-1, atime=-1):
+        return self.nn.set_times(self._p(path), mtime, atime)
+
+    def get_file_checksum(self, path):
+        """MD5MD5CRC32FileChecksum (DFSClient.getFileChecksum): the MD5 of the
+        per-block MD5s of each block's CRC32s (``io.bytes.per.checksum`` chunks);
+        crcPerBlock is 0 for a one-block file.  Returns (algorithm, 28 bytes)."""
+        import hashlib
+        import struct
+        p = self._p(path)
+        if self.is_dir(path):
+            raise FileNotFoundError(f"{path} is a directory")
+        blocks = self.nn.get_block_locations(p, 0, None)
+        md5s, bpc, cpb = [], 512, 0
+        for i, b in enumerate(blocks):
+            last = None
+            for dn in b["dns"]:
+                try:
+                    r = resolve_datanode(self.nn, dn).block_checksum(b["block"])
+                    break
+                except Exception as e:  # noqa: BLE001 — try the next replica
+                    last = e
+            else:
+                raise IOError(f"no replica of block {b['block']} answered: {last}")
+            md5s.append(bytes.fromhex(r["md5"]))
+            bpc = r["bpc"]
+            if i == 0 and len(blocks) > 1:
+                cpb = r["crc_per_block"]
+        md5 = hashlib.md5(b"".join(md5s)).digest()
+        return f"MD5-of-{cpb}MD5-of-{bpc}CRC32", struct.pack(">iq", bpc, cpb) + md5
 
     def get_file_block_locations(self, path, start, length):
         """[(offset, length, [hosts])] of the blocks overlapping [start, start+length)."""

@@ -48,7 +48,7 @@ def resolve_datanode(nn, dn_id):
 
 
 class DataNode:
-    METHODS = ["write_block", "read_block", "block_length", "ping"]
+    METHODS = ["write_block", "read_block", "block_length", "block_checksum", "ping"]
 
     def __init__(self, conf, namenode, dn_id, host, data_dir, rack="/default-rack",
                  serve_rpc=False):
@@ -152,6 +152,18 @@ class DataNode:
             if struct.pack(">I", zlib.crc32(piece) & 0xFFFFFFFF) != sums[4 * i:4 * i + 4]:
                 raise ChecksumError(f"checksum error in block {bid} chunk {c0 + i} on {self.id}")
         return chunk[offset - c0 * b:end - c0 * b]
+
+    def block_checksum(self, bid):
+        """OP_BLOCK_CHECKSUM: bytes per CRC, CRCs in the block, MD5 of its CRCs."""
+        import hashlib
+        p = self._path(bid) + ".meta"
+        if not os.path.exists(p):
+            raise FileNotFoundError(f"block {bid} not on {self.id}")
+        with open(p, "rb") as f:
+            meta = f.read()
+        crcs = meta[4:]
+        return {"bpc": struct.unpack(">I", meta[:4])[0], "crc_per_block": len(crcs) // 4,
+                "md5": hashlib.md5(crcs).hexdigest()}
 
     def verify_all(self):
         """DataBlockScanner pass: returns (and reports) corrupt block ids."""

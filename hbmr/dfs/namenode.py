@@ -64,7 +64,7 @@ class NameNode:
                "report_bad_block", "fsck", "datanode_report", "save_namespace", "safemode",
                "datanode_address", "decommission", "roll_edit_log", "get_checkpoint_files",
                "install_checkpoint", "get_blocks", "move_block", "pending_moves",
-               "set_quota", "get_content_summary"]
+               "set_quota", "get_content_summary", "set_owner", "set_permission", "set_times"]
 
     def __init__(self, conf=None, name_dir=None, checkpoint_only=False):
         """checkpoint_only: load image + edits for an offline merge (the
@@ -78,6 +78,10 @@ class NameNode:
         self.monitor_interval = g("dfs.replication.interval.ms", 1000) / 1000.0
         self.safemode_pct = gf("dfs.safemode.threshold.pct", 0.999)
         self.name_dir = name_dir
+        import getpass
+        self.superuser = getpass.getuser()      # the NameNode's user owns what no one else does
+        self.supergroup = conf.get("dfs.permissions.supergroup", "supergroup") \
+            if conf is not None else "supergroup"
         self.lock = threading.RLock()
         self.inodes: dict[str, dict] = {"/": {"type": "dir", "mtime": time.time()}}
         self.blocks: dict[int, dict] = {}         # id -> {"len", "locs": set, "file"}
@@ -154,11 +158,13 @@ class NameNode:
         op = e["op"]
         if op == "segment":
             return
+        attrs = {k: e[k] for k in self.ATTRS if k in e}
         if op == "mkdir":
-            self.inodes[e["path"]] = {"type": "dir", "mtime": e["t"]}
+            self.inodes[e["path"]] = {"type": "dir", "mtime": e["t"], **attrs}
         elif op == "create":
             self.inodes[e["path"]] = {"type": "file", "blocks": [], "repl": e["repl"],
-                                      "bs": e["bs"], "len": 0, "mtime": e["t"], "uc": True}
+                                      "bs": e["bs"], "len": 0, "mtime": e["t"], "uc": True,
+                                      **attrs}
         elif op == "add_block":
             ino = self.inodes[e["path"]]
             if ino["blocks"]:
@@ -186,6 +192,10 @@ class NameNode:
             self.blocks.pop(e["id"], None)
         elif op == "set_quota":
             self.quotas[e["path"]] = {"ns": e["ns"], "ds": e["ds"]}
+        elif op == "set_attrs":
+            self.inodes[e["path"]].update(attrs)
+        elif op == "set_times":
+            self.inodes[e["path"]].update({k: e[k] for k in ("mtime", "atime") if k in e})
 
     def _image(self, through):
         return {"inodes": self.inodes, "next_block": self.next_block, "quotas": self.quotas,
@@ -272,7 +282,7 @@ class NameNode:
             out.append(p)
         return out
 
-    def mkdirs(self, path):
+    def mkdirs(self, path, owner=None, permission=None):
         p = norm(path)
         with self.lock:
             self._check_safe()
@@ -283,13 +293,15 @@ class NameNode:
             for q in reversed([p] + self._parents(p)):
                 ino = self.inodes.get(q)
                 if ino is None:
-                    self._log("mkdir", path=q, t=t)
-                    self.inodes[q] = {"type": "dir", "mtime": t}
+                    attrs = self._new_attrs(owner, permission if q == p else None)
+                    self._log("mkdir", path=q, t=t, **attrs)
+                    self.inodes[q] = {"type": "dir", "mtime": t, **attrs}
                 elif ino["type"] != "dir":
                     raise NotADirectoryError(q)
         return True
 
-    def create(self, path, overwrite=True, replication=None, block_size=None, client=""):
+    def create(self, path, overwrite=True, replication=None, block_size=None, client="",
+               owner=None, permission=None):
         p = norm(path)
         with self.lock:
             self._check_safe()
@@ -304,14 +316,15 @@ class NameNode:
                 self._delete_locked(p)
             parent = posixpath.dirname(p)
             if parent not in self.inodes:
-                self.mkdirs(parent)
+                self.mkdirs(parent, owner)
             self._check_ns_quota(p, 1)
             repl = int(replication or self.replication)
             bs = int(block_size or self.block_size)
             t = time.time()
-            self._log("create", path=p, repl=repl, bs=bs, t=t)
+            attrs = self._new_attrs(owner, permission)
+            self._log("create", path=p, repl=repl, bs=bs, t=t, **attrs)
             self.inodes[p] = {"type": "file", "blocks": [], "repl": repl, "bs": bs, "len": 0,
-                              "mtime": t, "uc": True}
+                              "mtime": t, "uc": True, **attrs}
             self.leases[p] = client
             self.lease_time[p] = time.time()
         return {"block_size": bs, "replication": repl}
@@ -449,12 +462,72 @@ class NameNode:
             return len(self.moves)
 
     def _info(self, p, ino):
-        if ino["type"] == "dir":
+        isdir = ino["type"] == "dir"
+        perm = ino.get("perm", 0o777 if p == "/" else 0o755 if isdir else 0o644)
+        attrs = {"owner": ino.get("owner") or self.superuser, "group": ino.get("group") or
+                 self.supergroup, "permission": perm, "atime": ino.get("atime", 0.0 if isdir else
+                                                                      ino["mtime"])}
+        if isdir:
             return {"path": p, "length": 0, "is_dir": True, "block_size": 0, "replication": 0,
-                    "mtime": ino["mtime"]}
+                    "mtime": ino["mtime"], **attrs}
         return {"path": p, "length": ino["len"], "is_dir": False, "block_size": ino["bs"],
                 "replication": ino["repl"], "mtime": ino["mtime"],
-                "under_construction": bool(ino.get("uc"))}
+                "under_construction": bool(ino.get("uc")), **attrs}
+
+    # -- owner / permission / times (FSNamesystem.setOwner/setPermission/setTimes) -------
+    ATTRS = ("owner", "group", "perm", "atime")
+
+    def _new_attrs(self, owner, permission):
+        a = {}
+        if owner:
+            a["owner"] = str(owner)
+        if permission is not None:
+            a["perm"] = int(permission) & 0o7777
+        return a
+
+    def _set_attrs(self, path, **attrs):
+        p = norm(path)
+        with self.lock:
+            self._check_safe()
+            ino = self.inodes.get(p)
+            if ino is None:
+                raise FileNotFoundError(p)
+            self._log("set_attrs", path=p, **attrs)
+            ino.update(attrs)
+        return True
+
+    def set_owner(self, path, owner=None, group=None):
+        """Both None is an error (HDFS: "Both owner and group are null")."""
+        if not owner and not group:
+            raise ValueError("Both owner and group are empty")
+        a = {}
+        if owner:
+            a["owner"] = str(owner)
+        if group:
+            a["group"] = str(group)
+        return self._set_attrs(path, **a)
+
+    def set_permission(self, path, permission):
+        return self._set_attrs(path, perm=int(permission) & 0o7777)
+
+    def set_times(self, path, mtime=-1, atime=-1):
+        """Seconds since the epoch; -1 leaves a time unchanged."""
+        a = {}
+        if mtime is not None and mtime >= 0:
+            a["mtime"] = float(mtime)
+        if atime is not None and atime >= 0:
+            a["atime"] = float(atime)
+        if not a:
+            return True
+        p = norm(path)
+        with self.lock:
+            self._check_safe()
+            ino = self.inodes.get(p)
+            if ino is None:
+                raise FileNotFoundError(p)
+            self._log("set_times", path=p, **a)
+            ino.update(a)
+        return True
 
     def get_file_info(self, path):
         p = norm(path)
@@ -548,7 +621,7 @@ class NameNode:
         with self.lock:
             self._check_safe()
             ino = self.inodes.get(p)
-            if ino is None:
+            if ino is None or p == "/":   # FSDirectory refuses to delete the root
                 return False
             if ino["type"] == "dir" and not recursive and self.list_status(p):
                 raise OSError(f"{p} is a non-empty directory")

@@ -179,15 +179,16 @@ class LocalFileSystem:
 
 
 def is_dfs(path) -> bool:
-    """True for paths served by a non-local FileSystem (hdfs://, har://)."""
-    return str(path).startswith(("hdfs://", "har://"))
+    """True for paths served by a non-local FileSystem (hdfs://, webhdfs://, har://)."""
+    return str(path).startswith(("hdfs://", "webhdfs://", "har://"))
 
 
 _HAR_CACHE: dict = {}
 
 
 def get_fs(path=None, conf=None):
-    """FileSystem for a path: ``hdfs://authority/...`` → hbmr.dfs, ``har://...`` →
+    """FileSystem for a path: ``hdfs://authority/...`` → hbmr.dfs, ``webhdfs://host:port/...``
+    → its REST API (hbmr.dfs.webhdfs), ``har://...`` →
     a read-only Hadoop archive, else local."""
     p = str(path or "")
     if p.startswith("har://"):
@@ -200,6 +201,9 @@ def get_fs(path=None, conf=None):
     if p.startswith("hdfs://"):
         from ..dfs.client import DistributedFileSystem, split_uri
         return DistributedFileSystem(split_uri(p)[0], conf)
+    if p.startswith("webhdfs://"):
+        from ..dfs.webhdfs import WebHdfsFileSystem, split_uri
+        return WebHdfsFileSystem(split_uri(p)[0], conf)
     if "://" in p and not p.startswith("file://"):
         raise ValueError(f"unsupported filesystem scheme in {p!r} (use file:// or hdfs://)")
     return LocalFileSystem(conf)
