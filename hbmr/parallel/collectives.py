@@ -263,16 +263,34 @@ class TorchComm(Comm):
         dev = outs[0].device
         if self._staged("all_to_all", outs[0]):
             return [x.to(dev) for x in self._all_to_all_host([o.cpu() for o in outs])]
-        # sizes first (tensors may differ in length along dim 0)
-        sizes = torch.tensor([o.shape[0] for o in outs], dtype=torch.int64, device=dev)
-        in_sizes = torch.empty_like(sizes)
-        self.dist.all_to_all_single(in_sizes, sizes, group=self._grp(outs[0]))
-        if self.stats is not None:
-            self.stats["ALL_TO_ALL_HOST_READS"] += dev.type != "cpu"
-        ins = [torch.empty((int(n),) + tuple(outs[0].shape[1:]), dtype=outs[0].dtype, device=dev)
-               for n in in_sizes.tolist()]
+        # sizes first (tensors may differ in length along dim 0); they are
+        # known on the host, so they travel over the host group
+        in_sizes = self._exchange_sizes([int(o.shape[0]) for o in outs], dev, "ALL_TO_ALL")
+        ins = [torch.empty((n,) + tuple(outs[0].shape[1:]), dtype=outs[0].dtype, device=dev)
+               for n in in_sizes]
         self.dist.all_to_all(ins, [o.contiguous() for o in outs], group=self._grp(outs[0]))
         return ins
+
+    def _exchange_sizes(self, sizes, dev, op, group=None):
+        """Per-destination row counts → per-source row counts.  The counts are
+        host integers, so they go over the host (gloo) group as a host tensor:
+        nothing waits for the device, and the data all-to-all is enqueued on
+        the device stream behind the kernels that produced it.  Only a comm
+        with no host group (an RCCL group alone) exchanges them on the device
+        and reads the result back — counted as ``<OP>_HOST_READS``."""
+        if self.cpu_group is not None or self.stage or dev.type == "cpu":
+            hg = self.cpu_group if self.cpu_group is not None else \
+                (self.group if self.stage else group)
+            sc = torch.tensor(sizes, dtype=torch.int64)
+            rc = torch.empty_like(sc)
+            self.dist.all_to_all_single(rc, sc, group=hg)
+            return [int(x) for x in rc.tolist()]
+        sc = torch.tensor(sizes, dtype=torch.int64, device=dev)
+        rc = torch.empty_like(sc)
+        self.dist.all_to_all_single(rc, sc, group=group if group is not None else self.group)
+        if self.stats is not None:
+            self.stats[f"{op}_HOST_READS"] += 1
+        return [int(x) for x in rc.tolist()]
 
     def _all_to_all_host(self, outs):
         send, counts = torch.cat(outs), [int(o.shape[0]) for o in outs]
@@ -292,12 +310,7 @@ class TorchComm(Comm):
         # one all_to_all_single with split sizes: a single RCCL alltoallv (grouped
         # point-to-point over the xGMI mesh) instead of per-peer tensors
         dev = send.device
-        sc = torch.tensor([int(c) for c in counts], dtype=torch.int64, device=dev)
-        rc = torch.empty_like(sc)
-        self.dist.all_to_all_single(rc, sc, group=group)
-        if self.stats is not None:
-            self.stats["ALL_TO_ALL_V_HOST_READS"] += dev.type != "cpu"
-        rcounts = [int(x) for x in rc.tolist()]
+        rcounts = self._exchange_sizes([int(c) for c in counts], dev, "ALL_TO_ALL_V", group)
         recv = torch.empty((sum(rcounts),) + tuple(send.shape[1:]), dtype=send.dtype, device=dev)
         self.dist.all_to_all_single(recv, send.contiguous(), output_split_sizes=rcounts,
                                     input_split_sizes=[int(c) for c in counts], group=group)

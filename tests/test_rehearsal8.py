@@ -104,6 +104,8 @@ def test_eight_ranks_take_the_8_gpu_path_and_match_one_process(tmp_path):
             assert w not in got
             got[w] = int(n)
     assert got == want
-    # its shuffle read no sizes on the host inside a collective
-    wc = res["wordcount_counters"]
-    assert wc.get("ALL_TO_ALL_V_HOST_READS", 0) == 0 and wc.get("ALL_TO_ALL_HOST_READS", 0) == 0
+    # no shuffle read sizes on the host inside a collective
+    for job in ("terasort", "wordcount"):
+        cs = res[f"{job}_counters"]
+        assert cs.get("ALL_TO_ALL_V_HOST_READS", 0) == 0, (job, cs)
+        assert cs.get("ALL_TO_ALL_HOST_READS", 0) == 0, (job, cs)
