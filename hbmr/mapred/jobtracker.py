@@ -1634,7 +1634,7 @@ class JobTracker:
             with jp.events_cond:
                 jp.events_cond.notify_all()
             done_ids = [a.aid for a in done]
-            self.cost_model.tasks_finished(jip.signature, done_ids, True, dt)
+            self.cost_model.tasks_finished(jip.signature, done_ids, True, dt, jip.job_id)
             if rep.get("counters"):
                 jip.add_counters(rep["counters"])
             self.history.log("TASKS_FINISHED", attempts=done_ids, tracker=tr.name,

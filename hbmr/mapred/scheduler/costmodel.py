@@ -49,13 +49,41 @@ class TimeStats:
     # tracked the last batch's share alone: 15 µs against 0.25 ms per split)
     wnum: float = 0.0
     wden: float = 0.0
+    # GPU batches of jobs not folded into (wnum, wden) yet: job -> [time, tasks].
+    # A job's batches' shares of the device sum to its busy time only over the
+    # whole job (the first batches of each slot stream get most of the union,
+    # the last ones little), so the decay steps once per job — a step per
+    # window of tasks weighted a job's cheap tail and read ~14 % low at job end
+    open_jobs: dict = field(default_factory=dict)
+
+    def _refresh(self):
+        num, den = self.wnum, self.wden
+        for t, k in self.open_jobs.values():
+            num += t
+            den += k
+        self.ewma = num / den if den > 0 else 0.0
 
     def _decay(self, dt_total: float, n: int, alpha: float, per: float = 1.0):
         # one step of (1 - alpha) per ``per`` tasks
         keep = (1.0 - alpha) ** (n / per)
         self.wnum = keep * self.wnum + dt_total
         self.wden = keep * self.wden + n
-        self.ewma = self.wnum / self.wden if self.wden > 0 else 0.0
+        self._refresh()
+
+    def add_job_batch(self, job, dt_total: float, n: int, alpha: float, keep_open: int = 2):
+        """A batch of ``n`` tasks of ``job`` charged ``dt_total`` seconds.  The
+        ``keep_open`` latest jobs stay whole; an older one folds in with one
+        decay step of (1 - alpha)."""
+        acc = self.open_jobs.get(job)
+        if acc is None:
+            while len(self.open_jobs) >= keep_open:
+                t, k = self.open_jobs.pop(next(iter(self.open_jobs)))
+                self.wnum = (1.0 - alpha) * self.wnum + t
+                self.wden = (1.0 - alpha) * self.wden + k
+            acc = self.open_jobs[job] = [0.0, 0]
+        acc[0] += dt_total
+        acc[1] += n
+        self._refresh()
 
     def add(self, dt: float, alpha: float):
         self.n += 1
@@ -123,9 +151,9 @@ class CostModel:
             for a in attempts:
                 run[a] = t
 
-    def tasks_finished(self, sig, attempts, on_gpu, dt_each):
-        """A batch of attempts that each took ``dt_each`` seconds (GPU tasks
-        completed by one event pair share its device time)."""
+    def tasks_finished(self, sig, attempts, on_gpu, dt_each, job=None):
+        """A batch of attempts of ``job`` that each took ``dt_each`` seconds
+        (GPU tasks completed by one event pair share its device time)."""
         with self._lock:
             st = self._get(sig)["gpu" if on_gpu else "cpu"]
             pop = st.running.pop
@@ -133,10 +161,12 @@ class CostModel:
                 pop(a, None)
             if dt_each >= 0 and attempts:
                 n = len(attempts)
-                # a step per GPU_WINDOW tasks: the window spans about a
-                # 128-split job, whose batches' shares sum to its busy time
-                # (a job's last batches alone are charged little)
-                st._decay(dt_each * n, n, self.alpha, GPU_WINDOW)
+                if job is not None:
+                    st.add_job_batch(job, dt_each * n, n, self.alpha)
+                else:
+                    # no job identity: a step per GPU_WINDOW tasks (about a
+                    # 128-split job's worth of batches)
+                    st._decay(dt_each * n, n, self.alpha, GPU_WINDOW)
                 st.n += n
                 st.total += dt_each * n
                 st.min = min(st.min, dt_each)
