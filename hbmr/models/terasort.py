@@ -202,10 +202,11 @@ class TeraSortSplitJob(SplitJob):
                 f"hbmr.terasort.hbm.budget.gb) runs its reduce on one rank; this job "
                 f"would run on {len(trackers)} trackers")
         ranges = self._ranges()
-        # default R: one per tracker, and at least one per ~2 GB of input so a
-        # single GPU sorts the output a partition at a time
+        # default R: one per tracker, and at least one per ~1.2 GB of input so a
+        # single GPU sorts the output a partition at a time, each partition
+        # below the packed-key sort's group size (hbmr.ops.sort.PACK_GROUP_MAX)
         total = sum(r[2] for r in ranges) * S.RECORD
-        nparts = self.nparts_conf or max(1, len(trackers), -(-total // (2 << 30)))
+        nparts = self.nparts_conf or max(1, len(trackers), -(-total // (1200 << 20)))
         mk = (self.input, self.split_rows, self.sample, nparts)
         splitters = _SPLITTER_MEMO.get(mk) if self.input.startswith("teragen:") else None
         if splitters is None:
@@ -252,13 +253,16 @@ class TeraSortSplitJob(SplitJob):
             torch.zeros(0, dtype=torch.int64), torch.zeros(0, dtype=torch.int64))
         n = recs.shape[0]
         # key words + partition + partition sizes, scan, one tile-ranked scatter
-        hp, lp, row, offs = S.tera_partition(recs, shi, slo, stream=stream)
+        hp, lp, row, offs, kbytes = S.tera_partition(recs, shi, slo, stream=stream,
+                                                     kbytes=True)
         # order-independent checksum of the input keys, kept on the device
-        csum = hp.sum() + lp.sum()
+        # (summed by the partition kernel)
+        csum = kbytes[1]
         ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_INPUT_RECORDS, n)
         ctx.reporter.incrCounter(C.TASK_GROUP, C.MAP_OUTPUT_RECORDS, n)
         return {"records": recs, "hi": hp, "lo": lp, "row": row, "offsets": offs,
-                "checksum": csum, "nparts": nparts, "splitters": data["splitters"]}
+                "checksum": csum, "nparts": nparts, "splitters": data["splitters"],
+                "kbytes": kbytes}
 
     def _map_spill(self, ctx, data):
         """Spill mode: sort the whole split by key (a range partition is a key
@@ -391,20 +395,25 @@ class TeraSortSplitJob(SplitJob):
                 "peak_hbm_bytes": int(peak)}
 
     def _sorted_partition(self, his, los, rows, starts, lens, bases, dev, stream=None,
-                          hi_range=None):
+                          hi_range=None, defer=False, gid=True, alphabet=None, bounds=None):
         """Collect one partition's pieces from every map output, sort its keys,
         gather its records: (records, sorted hi, sorted lo).  The packed-id
-        path (v4, hbmr.terasort.reduce.gid) when the map outputs allow it."""
-        if self.gid and len(bases) <= S.GID_MAX_SPLITS and \
+        path (v4, hbmr.terasort.reduce.gid) when the map outputs allow it.
+        ``defer``: (records, hi, lo, flag) without a host read; a non-zero
+        device flag means the group must be redone with ``gid=False``."""
+        if gid and self.gid and len(bases) <= S.GID_MAX_SPLITS and \
                 max(b.shape[0] for b in bases) < S.GID_MAX_ROWS:
             got = S.sort_gathered(his, rows, starts, lens, bases, stream=stream,
-                                  hi_range=hi_range)
+                                  hi_range=hi_range, defer=defer, alphabet=alphabet,
+                                  bounds=bounds)
             if got is not None:
                 return got
         h, lw, split, row = S.tera_collect(his, los, rows, starts, lens, stream=stream)
         perm, hs, ls = S.sort_keys(h, lw, stream=stream)
         del h, lw
         recs = S.gather_records_multi(bases, split, row, perm, stream=stream)
+        if defer:
+            return recs, hs, ls, None
         return recs, hs, ls
 
     def _reduce_local(self, ctx, outs, offs, nparts, dev):
@@ -412,30 +421,50 @@ class TeraSortSplitJob(SplitJob):
         partitions are sorted in groups of about ``group_bytes`` (a partition is
         a key range, so a group sorts to its partitions in order and is cut by
         their counts), so peak HBM is the input splits + 20 B/record of map
-        output + one group."""
+        output + one group.  In HBM (no output) the groups run without a host
+        read; if any group's tie runs were too long for the in-place fix, the
+        whole reduce runs again on the full-key path."""
         if not outs:
             return 0, None
+        n, st, flags = self._reduce_local_groups(ctx, outs, offs, nparts, dev, True)
+        if flags is not None and int(flags.max()):
+            n, st, _ = self._reduce_local_groups(ctx, outs, offs, nparts, dev, False)
+        return n, st
+
+    def _reduce_local_groups(self, ctx, outs, offs, nparts, dev, use_gid):
+        flags = None
         his = [o["hi"] for o in outs]
         los = [o["lo"] for o in outs]
         rows = [o["row"] for o in outs]
         bases = [o["records"] for o in outs]
-        zero = torch.zeros((), dtype=torch.int64, device=dev)
-        bad = zero.clone()
-        csum = zero.clone()
+        # (out of order, checksum) and the stats kernel's scratch
+        gstats = torch.zeros(S.GROUP_STATS_LEN, dtype=torch.int64, device=dev)
         prev_last = None
         first = last = None
         n = 0
         sizes = (offs[:, 1:] - offs[:, :-1]).sum(axis=0)     # records per partition
         groups, pa = [], 0
+        # a group stays below the packed-key sort's record limit when its
+        # partitions allow (one larger partition sorts as pairs)
+        lim = min(self.group_bytes // S.RECORD, S.PACK_GROUP_MAX - 1) if self.gid else \
+            self.group_bytes // S.RECORD
         while pa < nparts:
             pb, acc = pa, 0
-            while pb < nparts and (pb == pa or (acc + int(sizes[pb])) * S.RECORD <=
-                                   self.group_bytes):
+            while pb < nparts and (pb == pa or acc + int(sizes[pb]) <= lim):
                 acc += int(sizes[pb])
                 pb += 1
             groups.append((pa, pb))
             pa = pb
         spl_hi = [int(h[:16], 16) for h in outs[0].get("splitters") or []] if nparts > 1 else []
+        # the key alphabet [0, 2^bits) holding every key byte of the high
+        # words (the maps' OR of them): the packed sort's dense window needs
+        # it (one host read)
+        alphabet = None
+        if use_gid and all(o.get("kbytes") is not None for o in outs):
+            orb = 0
+            for x in torch.stack([o["kbytes"][0].to(dev) for o in outs]).tolist():
+                orb |= int(x)
+            alphabet = (0, 1 << max(1, orb.bit_length()))
         for pa, pb in groups:
             starts = offs[:, pa]
             lens = offs[:, pb] - offs[:, pa]
@@ -447,16 +476,31 @@ class TeraSortSplitJob(SplitJob):
             hr = (spl_hi[pa - 1] if pa > 0 else 0,
                   spl_hi[pb - 1] if pb < nparts else (1 << 64) - 1) \
                 if len(spl_hi) == nparts - 1 else None
-            recs, hs, ls = self._sorted_partition(his, los, rows, starts, lens, bases, dev,
-                                                  hi_range=hr)
-            bad = bad + S.count_unsorted_dev(hs, ls)
-            if prev_last is not None:
-                bad = bad + S.pair_greater(prev_last, (hs[:1], ls[:1]))
+            # the window's bounds: the group's splitters (None at the ends:
+            # sort_gathered takes the group's own smallest / largest key)
+            bnd = (spl_hi[pa - 1] if pa > 0 else None, spl_hi[pb - 1] if pb < nparts else None) \
+                if len(spl_hi) == nparts - 1 else (None, None)
+            if self.out:
+                # output: each group's order is final before its part files
+                recs, hs, ls = self._sorted_partition(his, los, rows, starts, lens, bases, dev,
+                                                      hi_range=hr, gid=use_gid,
+                                                      alphabet=alphabet, bounds=bnd)
+            else:
+                # in HBM: no host read per group; the tie-run flags are read
+                # once after the last group (a flagged job is redone below)
+                recs, hs, ls, flag = self._sorted_partition(his, los, rows, starts, lens, bases,
+                                                            dev, hi_range=hr, defer=True,
+                                                            gid=use_gid, alphabet=alphabet,
+                                                            bounds=bnd)
+                if flag is not None:
+                    flags = flag if flags is None else flags + flag
+            # order within the group and across the seam to the previous one,
+            # and the key checksum, in one pass into gstats (no host read)
+            S.tera_group_stats(hs, ls, prev_last, gstats)
             prev_last = (hs[-1:], ls[-1:])
             if first is None:
                 first = (hs[:1], ls[:1])
             last = (hs[-1:], ls[-1:])
-            csum = csum + hs.sum() + ls.sum()
             n += m
             if self.out:
                 at, items = 0, []
@@ -464,11 +508,10 @@ class TeraSortSplitJob(SplitJob):
                     items.append((p, recs[at:at + int(sizes[p])]))
                     at += int(sizes[p])
                 self._write_parts(ctx, items)
-            del recs, hs, ls
+            del recs
         if first is None:
-            return 0, None
-        return n, torch.cat([bad.reshape(1), csum.reshape(1), first[0], first[1], last[0],
-                             last[1]])
+            return 0, None, flags
+        return n, torch.cat([gstats[:2], first[0], first[1], last[0], last[1]]), flags
 
     def _groups(self, sizes, nparts, limit):
         """Consecutive partitions in groups of at most ``limit`` record bytes

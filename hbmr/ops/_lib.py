@@ -23,6 +23,8 @@ _lib = None
 c_void_p = ctypes.c_void_p
 c_long = ctypes.c_long
 c_int = ctypes.c_int
+c_uint = ctypes.c_uint
+c_uint64 = ctypes.c_uint64
 c_double_p = ctypes.POINTER(ctypes.c_double)
 
 _SIGS = {
@@ -96,6 +98,11 @@ _SIGS = {
     "hbmr_f32_to_bf16_pad": (c_int, [c_void_p, c_long, c_int, c_int, c_void_p, c_void_p]),
     # sort / shuffle (native/kernels/sort.hip)
     "hbmr_radix_sort_workspace_bytes": (c_long, [c_long]),
+    "hbmr_radix_onesweep_workspace_bytes": (c_long, [c_long]),
+    "hbmr_radix_onesweep_status_bytes": (c_long, [c_long]),
+    "hbmr_radix_sort_keys_u64": (c_int, [c_void_p, c_void_p, c_long, c_int, c_int, c_void_p,
+                                         c_long, c_void_p, c_long, c_void_p, c_void_p, c_int,
+                                         c_void_p]),
     "hbmr_radix_sort_pairs_u64": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_int,
                                           c_int, c_void_p, c_long, c_void_p]),
     "hbmr_teragen": (c_int, [c_long, c_long, c_void_p, c_void_p]),
@@ -115,16 +122,22 @@ _SIGS = {
                                           c_void_p, c_void_p]),
     "hbmr_tera_partition_workspace_bytes": (c_long, [c_long, c_int]),
     "hbmr_tera_collect_gid": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_long,
-                                      c_void_p, c_void_p, c_void_p]),
-    "hbmr_gather_records_gid": (c_int, [c_void_p, c_void_p, c_long, c_int, c_void_p, c_void_p,
-                                        c_void_p, c_void_p]),
-    "hbmr_tera_tie_fix_records": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_int, c_int,
-                                          c_void_p, c_void_p]),
+                                      c_int, c_uint64, c_uint, c_uint, c_int, c_void_p, c_void_p,
+                                      c_void_p]),
+    "hbmr_gather_records_gid": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p,
+                                        c_void_p, c_void_p, c_void_p]),
+    "hbmr_tera_group_stats": (c_int, [c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p,
+                                      c_void_p]),
+    "hbmr_tera_tie_fix_scratch_bytes": (c_long, [c_long, c_int]),
+    "hbmr_tera_tie_fix_records": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_int, c_uint64,
+                                          c_uint, c_uint, c_int, c_void_p, c_void_p, c_long,
+                                          c_void_p]),
     "hbmr_merge_path": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p,
                                 c_long, c_void_p, c_void_p, c_void_p, c_void_p]),
     "hbmr_tera_tie_fix": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p]),
     "hbmr_tera_partition": (c_int, [c_void_p, c_long, c_int, c_void_p, c_void_p, c_int, c_void_p,
-                                    c_void_p, c_void_p, c_void_p, c_void_p, c_long, c_void_p]),
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_long,
+                                    c_void_p]),
     # text / WordCount (native/kernels/text.hip)
     "hbmr_wc_tiles": (c_long, [c_long]),
     "hbmr_wc_tokenize_count": (c_int, [c_void_p, c_long, c_void_p, c_void_p]),

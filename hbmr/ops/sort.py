@@ -11,6 +11,7 @@ the native library must load (no silent fallback).
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import numpy as np
@@ -86,6 +87,62 @@ def radix_sort_pairs(keys: torch.Tensor, vals: torch.Tensor, begin_bit: int = 0,
     rc = lib.hbmr_radix_sort_pairs_u64(_ptr(keys), _ptr(vals), _ptr(tk), _ptr(tv), n, begin_bit,
                                        end_bit, _ptr(ws), wsb, _lib.stream_handle(stream))
     _lib.check(rc, "hbmr_radix_sort_pairs_u64")
+
+
+ONESWEEP_MAX = 1 << 30
+# per (device, stream): the onesweep look-back status words, zeroed once and
+# tagged with a fresh epoch per pass (no memset before every pass), and the
+# epoch counter the native side advances.  Calls on one stream run in order,
+# so one status array per stream is never used by two sorts at once.
+_ONESWEEP_STATUS: dict = {}
+
+
+def _onesweep_status(device, nbytes, stream):
+    key = (str(device), _lib.stream_handle(stream))
+    ent = _ONESWEEP_STATUS.get(key)
+    if ent is None or ent[0].numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        ent = _ONESWEEP_STATUS[key] = (buf, ctypes.c_uint(0))   # 0: zeroed on first use
+    return ent
+
+
+def radix_sort_keys(keys: torch.Tensor, begin_bit: int = 0, end_bit: int = 64, stream=None,
+                    err: torch.Tensor | None = None, inplace: bool = True) -> torch.Tensor:
+    """In place: sort ``keys`` (int64 storage of uint64) by bits [begin_bit,
+    end_bit), keys only, stable — the onesweep kernels (one histogram read for
+    every digit, a decoupled look-back scatter per digit).  ``err`` (int32[1],
+    device) is set non-zero if a look-back timed out (the order check of the
+    caller then fails); n < 2^30.  Returns the sorted tensor: ``keys``, or
+    with ``inplace=False`` whichever of keys and its scratch twin the last
+    pass wrote (no copy back after an odd number of passes)."""
+    n = keys.numel()
+    if keys.dtype != torch.int64:
+        raise ValueError("keys int64[n] required")
+    if n <= 1:
+        return keys
+    if not _on_gpu(keys):
+        k = keys.numpy().view(np.uint64)
+        w = end_bit - begin_bit
+        mask = np.uint64((1 << w) - 1 if w < 64 else 0xFFFFFFFFFFFFFFFF)
+        order = np.argsort((k >> np.uint64(begin_bit)) & mask, kind="stable")
+        keys.copy_(torch.from_numpy(k[order].view(np.int64).copy()))
+        return keys
+    if n >= ONESWEEP_MAX:
+        raise ValueError("onesweep radix sort: n must be below 2^30")
+    lib = _lib.load()
+    tk = torch.empty_like(keys)
+    wsb = int(lib.hbmr_radix_onesweep_workspace_bytes(n))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=keys.device)
+    if err is None:
+        err = torch.zeros(1, dtype=torch.int32, device=keys.device)
+    status, epoch = _onesweep_status(keys.device, int(lib.hbmr_radix_onesweep_status_bytes(n)),
+                                     stream)
+    rc = lib.hbmr_radix_sort_keys_u64(_ptr(keys), _ptr(tk), n, begin_bit, end_bit, _ptr(ws), wsb,
+                                      _ptr(status), status.numel(), ctypes.byref(epoch),
+                                      _ptr(err), int(inplace), _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_radix_sort_keys_u64")
+    passes = (end_bit - begin_bit + 7) // 8
+    return tk if (not inplace and passes % 2) else keys
 
 
 def argsort_u64(keys: torch.Tensor, stream=None):
@@ -336,12 +393,15 @@ def tera_keys_part(records: torch.Tensor, split_hi: torch.Tensor, split_lo: torc
 
 
 def tera_partition(records: torch.Tensor, split_hi: torch.Tensor, split_lo: torch.Tensor,
-                   stream=None):
+                   stream=None, kbytes=False):
     """Range-partition a split: (hi, lo, row, offsets) — key words and record
     numbers in partition order (order inside a partition unspecified) and
     offsets[R+1] of the R = #splitters + 1 partitions (int64, on the records'
     device).  On the GPU: one key/partition/count kernel, an on-device scan and
-    one tile-ranked scatter (no sort, no gathers)."""
+    one tile-ranked scatter (no sort, no gathers).  ``kbytes``: also an
+    int64[2] on the device — the OR of every key's high-word bytes (the key
+    alphabet [0, 2^bits(OR)) the reduce's dense window needs) and the split's
+    key checksum sum(hi + lo) mod 2^64."""
     n, stride = records.shape
     ns = split_hi.numel()
     nparts = ns + 1
@@ -351,6 +411,10 @@ def tera_partition(records: torch.Tensor, split_hi: torch.Tensor, split_lo: torc
         counts = torch.bincount(pid, minlength=nparts)
         offs = torch.zeros(nparts + 1, dtype=torch.int64)
         torch.cumsum(counts, 0, out=offs[1:])
+        if kbytes:
+            orb = int(np.bitwise_or.reduce(records[:, :8].numpy(), axis=None)) if n else 0
+            kmm = torch.stack([torch.tensor(orb, dtype=torch.int64), hi.sum() + lo.sum()])
+            return hi[order], lo[order], order.to(torch.int32), offs, kmm
         return hi[order], lo[order], order.to(torch.int32), offs
     if ns > 4096:
         raise ValueError("at most 4096 splitters (4097 partitions)")
@@ -362,12 +426,15 @@ def tera_partition(records: torch.Tensor, split_hi: torch.Tensor, split_lo: torc
     offs = torch.empty(nparts + 1, dtype=torch.int64, device=dev)
     wsb = int(lib.hbmr_tera_partition_workspace_bytes(n, nparts))
     ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
-    sh = split_hi.to(dev)
-    sl = split_lo.to(dev)
+    sh = split_hi if split_hi.device == dev else split_hi.pin_memory().to(dev, non_blocking=True)
+    sl = split_lo if split_lo.device == dev else split_lo.pin_memory().to(dev, non_blocking=True)
+    kmm = torch.zeros(2, dtype=torch.int64, device=dev) if kbytes else None
     rc = lib.hbmr_tera_partition(_ptr(records), n, stride, _ptr(sh) if ns else None,
                                  _ptr(sl) if ns else None, ns, _ptr(hi), _ptr(lo), _ptr(row),
-                                 _ptr(offs), _ptr(ws), wsb, _lib.stream_handle(stream))
+                                 _ptr(offs), _ptr(kmm), _ptr(ws), wsb, _lib.stream_handle(stream))
     _lib.check(rc, "hbmr_tera_partition")
+    if kbytes:
+        return hi, lo, row, offs, kmm
     return hi, lo, row, offs
 
 
@@ -408,8 +475,29 @@ def merge_runs(runs, stream=None):
     return runs[0]
 
 
+_PTR_TABLES: dict = {}
+
+
+def _h2d_i64(values, device):
+    """int64 values on the device without a blocking copy: a pinned staging
+    tensor and an asynchronous copy on the current stream (a pageable copy
+    waits for the device to drain everything queued before it)."""
+    h = torch.as_tensor(np.asarray(values, dtype=np.int64))
+    if device.type != "cuda":
+        return h.to(device)
+    return h.pin_memory().to(device, non_blocking=True)
+
+
 def _ptr_table(ts, device):
-    return torch.tensor([t.data_ptr() for t in ts], dtype=torch.int64, device=device)
+    """Device table of the tensors' base addresses, cached by the addresses
+    (a TeraSort reduce passes the same map outputs for every group)."""
+    key = (str(device), tuple(t.data_ptr() for t in ts))
+    tab = _PTR_TABLES.get(key)
+    if tab is None:
+        if len(_PTR_TABLES) > 64:
+            _PTR_TABLES.clear()
+        tab = _PTR_TABLES[key] = _h2d_i64(key[1], device)
+    return tab
 
 
 def tera_collect(his, los, rows, starts, lens, with_keys=True, stream=None):
@@ -428,7 +516,7 @@ def tera_collect(his, los, rows, starts, lens, with_keys=True, stream=None):
                 torch.cat([lw[sl] for lw, sl in zip(los, sel)]), split, row)
     prefix = np.zeros(S + 1, dtype=np.int64)
     np.cumsum(np.asarray(lens, dtype=np.int64), out=prefix[1:])
-    meta = torch.from_numpy(np.concatenate([np.asarray(starts, dtype=np.int64), prefix])).to(dev)
+    meta = _h2d_i64(np.concatenate([np.asarray(starts, dtype=np.int64), prefix]), dev)
     split = torch.empty(n, dtype=torch.int32, device=dev)
     row = torch.empty(n, dtype=torch.int32, device=dev)
     ohi = torch.empty(n, dtype=torch.int64, device=dev) if with_keys else None
@@ -483,10 +571,49 @@ GID_MAX_SPLITS = 256
 GID_MAX_ROWS = 1 << 24
 
 
-def tera_collect_gid(his, rows, starts, lens, stream=None):
+PACK_GROUP_MAX = 1 << 24  # records per packed-key group: bounds the tie runs of a 32-bit window
+
+
+class KeyWindow:
+    """The order-preserving dense map of a key's high word h used by the
+    packed reduce (native KeyWindow): v(h) = h's 8 bytes as base-R digits
+    (every key byte in [m, m + R)), window = (v(h) - vlo) >> sh.  For a group
+    with keys' v in [vlo, vup] (its splitters), sh makes the window fit in 32
+    bits.  m = 0, R = 256, vlo = 0 is the plain shift h >> sh."""
+
+    def __init__(self, m=0, R=256, vlo=0, sh=0):
+        self.m, self.R, self.vlo, self.sh = int(m), int(R), int(vlo), int(sh)
+
+    def v(self, h: int) -> int:
+        x = 0
+        for b in range(7, -1, -1):
+            x = x * self.R + (((h >> (8 * b)) & 0xFF) - self.m)
+        return x
+
+    @classmethod
+    def for_group(cls, m, R, lo_hi=None, up_hi=None, bits=32):
+        """lo_hi / up_hi: the group's bounding splitter high words (None: the
+        first / last group — the alphabet's ends)."""
+        w = cls(m, R)
+        vlo = 0 if lo_hi is None else w.v(int(lo_hi))
+        vup = R ** 8 - 1 if up_hi is None else w.v(int(up_hi))
+        span = max(1, vup - vlo + 1)
+        return cls(m, R, vlo, max(0, span.bit_length() - bits))
+
+    def apply_np(self, h: np.ndarray) -> np.ndarray:
+        v = np.zeros(h.shape, dtype=np.uint64)
+        for b in range(7, -1, -1):
+            d = ((h >> np.uint64(8 * b)) & np.uint64(0xFF)).astype(np.int64) - self.m
+            v = v * np.uint64(self.R) + d.astype(np.uint64)
+        return (v - np.uint64(self.vlo & 0xFFFFFFFFFFFFFFFF)) >> np.uint64(self.sh)
+
+
+def tera_collect_gid(his, rows, starts, lens, stream=None, window: KeyWindow | None = None):
     """Pieces [starts[s], +lens[s]) of per-split (hi, row) arrays → (hi, gid)
     with gid = s << 24 | row (int32 storage): the record ids the v4 reduce
-    sorts and gathers by (at most 256 splits of < 2^24 records)."""
+    sorts and gathers by (at most 256 splits of < 2^24 records).  With
+    ``window``: (packed, None) — one sortable int64 per record, the key's
+    32-bit window above the record's id."""
     S = len(rows)
     if S > GID_MAX_SPLITS:
         raise ValueError(f"at most {GID_MAX_SPLITS} map outputs per packed-id collect")
@@ -496,25 +623,37 @@ def tera_collect_gid(his, rows, starts, lens, stream=None):
         sel = [slice(int(a), int(a) + int(m)) for a, m in zip(starts, lens)]
         gid = torch.cat([(r[sl].to(torch.int64) | (s << 24)).to(torch.int32)
                          for s, (r, sl) in enumerate(zip(rows, sel))])
-        return torch.cat([h[sl] for h, sl in zip(his, sel)]), gid
+        hi = torch.cat([h[sl] for h, sl in zip(his, sel)])
+        if window is None:
+            return hi, gid
+        w = window.apply_np(hi.numpy().view(np.uint64)) & np.uint64(0xFFFFFFFF)
+        pk = (w << np.uint64(32)) | gid.numpy().view(np.uint32).astype(np.uint64)
+        return torch.from_numpy(pk.view(np.int64).copy()), None
     prefix = np.zeros(S + 1, dtype=np.int64)
     np.cumsum(np.asarray(lens, dtype=np.int64), out=prefix[1:])
-    meta = torch.from_numpy(np.concatenate([np.asarray(starts, dtype=np.int64), prefix])).to(dev)
+    meta = _h2d_i64(np.concatenate([np.asarray(starts, dtype=np.int64), prefix]), dev)
     ohi = torch.empty(n, dtype=torch.int64, device=dev)
-    gid = torch.empty(n, dtype=torch.int32, device=dev)
+    gid = None if window is not None else torch.empty(n, dtype=torch.int32, device=dev)
     th, tr = _ptr_table(his, dev), _ptr_table(rows, dev)
+    kw = window or KeyWindow()
     rc = _lib.load().hbmr_tera_collect_gid(_ptr(th), _ptr(tr), _ptr(meta), _ptr(meta) + 8 * S, S,
-                                            n, _ptr(ohi), _ptr(gid), _lib.stream_handle(stream))
+                                            n, int(window is not None),
+                                            kw.vlo & 0xFFFFFFFFFFFFFFFF, kw.m, kw.R, kw.sh,
+                                            _ptr(ohi), _ptr(gid), _lib.stream_handle(stream))
     _lib.check(rc, "hbmr_tera_collect_gid")
     return ohi, gid
 
 
 def gather_records_gid(bases, gid: torch.Tensor, stream=None, keys=None) -> torch.Tensor:
-    """out[i] = bases[gid[i] >> 24][gid[i] & 0xFFFFFF] (100-byte records).
+    """out[i] = bases[g >> 24][g & 0xFFFFFF] (100-byte records) with g =
+    gid[i]: int32 ids, or int64 packed keys whose low 32 bits are the ids.
     ``keys`` = (hi, lo) int64 [n] tensors also receive the gathered records'
-    keys (as tera_keys would read them back), on the GPU in the same pass."""
+    keys (as tera_keys would read them back), on the GPU in the same pass; hi
+    may be the packed keys themselves (each record's id is read before its
+    key is written over it)."""
     n = gid.numel()
     rb = bases[0].shape[1]
+    packed = gid.dtype == torch.int64
     if not _on_gpu(gid):
         g = gid.to(torch.int64) & 0xFFFFFFFF
         s, r = g >> 24, g & 0xFFFFFF
@@ -531,40 +670,87 @@ def gather_records_gid(bases, gid: torch.Tensor, stream=None, keys=None) -> torc
     res = torch.empty(n, rb, dtype=torch.uint8, device=gid.device)
     tb = _ptr_table(bases, gid.device)
     kh, kl = keys if keys is not None else (None, None)
-    rc = _lib.load().hbmr_gather_records_gid(_ptr(tb), _ptr(gid), n, rb, _ptr(res), _ptr(kh),
-                                              _ptr(kl), _lib.stream_handle(stream))
+    rc = _lib.load().hbmr_gather_records_gid(_ptr(tb), None if packed else _ptr(gid),
+                                              _ptr(gid) if packed else None, n, rb, _ptr(res),
+                                              _ptr(kh), _ptr(kl), _lib.stream_handle(stream))
     _lib.check(rc, "hbmr_gather_records_gid")
     return res
 
 
-def sort_gathered(his, rows, starts, lens, bases, stream=None, hi_range=None):
+def sort_gathered(his, rows, starts, lens, bases, stream=None, hi_range=None, defer=False,
+                  alphabet=None, bounds=None):
     """TeraSort reduce v4 for one group: (hi, gid) collect, radix passes over
-    the top 64 - TIE_SHIFT bits of hi carrying the gid, ONE record gather by
-    gid, the low key words read back from the sorted records, and runs of an
-    equal sorted prefix ordered by the full key in place.  Returns (records,
-    hi, lo), or None when such a run is too long for the in-place fix-up (the
-    caller takes the full-key path).  ``hi_range`` (the group's hi bounds)
-    narrows the radix passes to the bits below the group's common prefix."""
-    h, gid = tera_collect_gid(his, rows, starts, lens, stream=stream)
-    # the window's bits of hi (by default the 48 below the group's common
-    # prefix: 6 passes); the tie fix orders equal sorted prefixes by the full
-    # key read back from the records
+    a window of hi, ONE record gather, the low key words read back from the
+    sorted records, and runs of an equal sorted prefix ordered by the full key
+    in place.  Returns (records, hi, lo), or None when such a run is too long
+    for the in-place fix-up (the caller takes the full-key path).
+    ``hi_range`` (the group's hi bounds) places the window just below the
+    group's common prefix.
+
+    Groups below PACK_GROUP_MAX records, given the job's key ``alphabet``
+    (m, R) and the group's splitter high words ``bounds`` (lo, up; None at
+    the ends), sort packed keys — the key's dense 32-bit window (KeyWindow)
+    above the 32-bit record id in one int64, keys only, by the onesweep
+    kernels: 4 passes of 8 bytes per record and one histogram read, against 5
+    passes of 12 bytes plus a histogram read each for (hi, gid) pairs over 40
+    bits.  Equal windows (well under 1 % of a 12M-record group) are ordered
+    by the tie fix.  Otherwise the pairs.
+
+    ``defer``: no host read — returns (records, hi, lo, flag) with flag a
+    device int32[1] the caller checks once for all groups (non-zero: this
+    group's order is not final and must be redone on the full-key path)."""
+    n = int(sum(lens))
     begin, end = sort_window(hi_range)
-    radix_sort_pairs(h, gid, begin, end, stream=stream)
-    # the sorted keys come with the gather (lo is new; h is rewritten with the
-    # same values): no second pass over the records
-    lo = torch.empty_like(h)
-    recs = gather_records_gid(bases, gid, stream=stream, keys=(h, lo))
-    del gid
+    kw = KeyWindow(sh=begin)
+    if n < PACK_GROUP_MAX and alphabet is not None and bounds is not None:
+        lo_b, up_b = bounds
+        if (lo_b is None or up_b is None) and n:
+            # an end group: its own smallest / largest high word bound the
+            # window (the alphabet's ends would widen it many times over)
+            # (uint64 order through int64: flip the sign bit both ways)
+            pieces = [h[int(a):int(a) + int(m)] ^ _SIGN for h, a, m in zip(his, starts, lens)
+                      if int(m)]
+            mm = torch.stack([torch.stack([p.min(), p.max()]) for p in pieces]) ^ _SIGN
+            if _on_gpu(mm):
+                mm = mm.cpu()
+            mu = mm.numpy().view(np.uint64)
+            lo_b = int(mu[:, 0].min()) if lo_b is None else lo_b
+            up_b = int(mu[:, 1].max()) if up_b is None else up_b
+        kw = KeyWindow.for_group(alphabet[0], alphabet[1], lo_b, up_b)
+        h, _ = tera_collect_gid(his, rows, starts, lens, stream=stream, window=kw)
+        radix_sort_keys(h, 32, 64, stream=stream)
+        lo = torch.empty_like(h)
+        # each record's id is read from its packed word before the gather
+        # writes the record's full hi key over it
+        recs = gather_records_gid(bases, h, stream=stream, keys=(h, lo))
+    else:
+        h, gid = tera_collect_gid(his, rows, starts, lens, stream=stream)
+        radix_sort_pairs(h, gid, begin, end, stream=stream)
+        # the sorted keys come with the gather (lo is new; h is rewritten with
+        # the same values): no second pass over the records
+        lo = torch.empty_like(h)
+        recs = gather_records_gid(bases, gid, stream=stream, keys=(h, lo))
+        del gid
     if not _on_gpu(recs):
         order = np.lexsort((lo.numpy().view(np.uint64), h.numpy().view(np.uint64)))
         o = torch.from_numpy(order)
+        if defer:
+            return recs[o], h[o], lo[o], torch.zeros(1, dtype=torch.int32)
         return recs[o], h[o], lo[o]
     flag = torch.zeros(1, dtype=torch.int32, device=recs.device)
-    rc = _lib.load().hbmr_tera_tie_fix_records(_ptr(h), _ptr(lo), _ptr(recs), recs.shape[0],
-                                                recs.shape[1], begin, _ptr(flag),
-                                                _lib.stream_handle(stream))
+    lib = _lib.load()
+    # moved records of the tie runs go through a compact scratch: room for a
+    # quarter of the group (a few percent move with a 32-bit window)
+    cap = max(4096, recs.shape[0] // 4)
+    scratch = torch.empty(int(lib.hbmr_tera_tie_fix_scratch_bytes(cap, recs.shape[1])),
+                          dtype=torch.uint8, device=recs.device)
+    rc = lib.hbmr_tera_tie_fix_records(_ptr(h), _ptr(lo), _ptr(recs), recs.shape[0],
+                                       recs.shape[1], kw.vlo & 0xFFFFFFFFFFFFFFFF, kw.m, kw.R,
+                                       kw.sh, _ptr(flag), _ptr(scratch), cap,
+                                       _lib.stream_handle(stream))
     _lib.check(rc, "hbmr_tera_tie_fix_records")
+    if defer:
+        return recs, h, lo, flag
     if int(flag.item()):
         return None
     return recs, h, lo
@@ -617,6 +803,28 @@ def count_unsorted_dev(hi: torch.Tensor, lo: torch.Tensor, stream=None) -> torch
 
 
 _SIGN = -0x8000000000000000
+GROUP_STATS_LEN = 2 + 2 * 1024
+
+
+def tera_group_stats(hi: torch.Tensor, lo: torch.Tensor, prev, acc: torch.Tensor, stream=None):
+    """acc[:2] (int64[GROUP_STATS_LEN], the keys' device; the rest is the
+    kernel's scratch) += (records out of order — record 0 against ``prev``,
+    the previous group's last (hi, lo) 1-element tensors, or None — and
+    sum(hi + lo) mod 2^64), with no host read."""
+    n = hi.numel()
+    if n == 0:
+        return
+    if not _on_gpu(hi):
+        bad = count_unsorted(hi, lo)
+        if prev is not None:
+            bad += int(pair_greater(prev, (hi[:1], lo[:1])))
+        s = (hi.sum() + lo.sum()).reshape(())
+        acc[:2] += torch.stack([torch.tensor(bad, dtype=torch.int64), s])
+        return
+    ph, pl = (prev[0], prev[1]) if prev is not None else (None, None)
+    rc = _lib.load().hbmr_tera_group_stats(_ptr(hi), _ptr(lo), n, _ptr(ph), _ptr(pl), _ptr(acc),
+                                            _lib.stream_handle(stream))
+    _lib.check(rc, "hbmr_tera_group_stats")
 
 
 def pair_greater(a, b) -> torch.Tensor:

@@ -137,13 +137,23 @@ int hbmr_gather_records_multi(const void* const* bases, const uint32_t* split, c
                               const uint32_t* perm, long n, int record_bytes, void* dst,
                               hipStream_t st);
 int hbmr_tera_collect_gid(const uint64_t* const* his, const uint32_t* const* rows,
-                          const long* starts, const long* prefix, int S, long n, uint64_t* ohi,
+                          const long* starts, const long* prefix, int S, long n, int pack,
+                          uint64_t vlo, unsigned int m, unsigned int R, int sh, uint64_t* ohi,
                           uint32_t* ogid, hipStream_t st);
-int hbmr_gather_records_gid(const void* const* bases, const uint32_t* gid, long n,
-                            int record_bytes, void* dst, uint64_t* hi, uint64_t* lo,
+int hbmr_gather_records_gid(const void* const* bases, const uint32_t* gid, const uint64_t* packed,
+                            long n, int record_bytes, void* dst, uint64_t* hi, uint64_t* lo,
                             hipStream_t st);
-int hbmr_tera_tie_fix_records(uint64_t* hi, uint64_t* lo, void* rec, long n,
-                              int record_bytes, int shift, unsigned int* flag, hipStream_t st);
+long hbmr_radix_onesweep_workspace_bytes(long n);
+long hbmr_radix_onesweep_status_bytes(long n);
+int hbmr_radix_sort_keys_u64(uint64_t* keys, uint64_t* tkeys, long n, int begin_bit, int end_bit,
+                             void* ws, long ws_bytes, void* status, long status_bytes,
+                             unsigned int* epoch, uint32_t* err, int copy_back, hipStream_t st);
+long hbmr_tera_tie_fix_scratch_bytes(long cap, int record_bytes);
+int hbmr_tera_group_stats(const uint64_t* hi, const uint64_t* lo, long n, const uint64_t* ph,
+                          const uint64_t* pl, unsigned long long* acc, hipStream_t st);
+int hbmr_tera_tie_fix_records(uint64_t* hi, uint64_t* lo, void* rec, long n, int record_bytes,
+                              uint64_t vlo, unsigned int m, unsigned int R, int sh,
+                              unsigned int* flag, void* scratch, long cap, hipStream_t st);
 int hbmr_merge_path(const uint64_t* ahi, const uint64_t* alo, const uint32_t* av, long na,
                     const uint64_t* bhi, const uint64_t* blo, const uint32_t* bv, long nb,
                     uint64_t* ohi, uint64_t* olo, uint32_t* ov, hipStream_t st);
@@ -151,7 +161,8 @@ int hbmr_tera_tie_fix(const uint64_t* hi, uint64_t* lo, uint32_t* perm, long n,
                       unsigned int* flag, hipStream_t st);
 int hbmr_tera_partition(const void* records, long n, int stride, const uint64_t* shi,
                         const uint64_t* slo, int nsplit, uint64_t* ohi, uint64_t* olo,
-                        uint32_t* orow, long* offsets, void* ws, long ws_bytes, hipStream_t st);
+                        uint32_t* orow, long* offsets, unsigned long long* kmm, void* ws,
+                        long ws_bytes, hipStream_t st);
 #endif
 long hbmr_radix_sort_workspace_bytes(long n);
 long hbmr_tera_partition_workspace_bytes(long n, int nparts);

@@ -51,25 +51,6 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t x, uint32_t* s_w
   return base + v - x;
 }
 
-// (1) digit histogram per tile, digit-major: hist[d * ntiles + tile]
-__global__ __launch_bounds__(kSortThreads) void radix_hist_kernel(const uint64_t* __restrict__ keys,
-                                                                  long n, int shift, long ntiles,
-                                                                  uint32_t* __restrict__ hist) {
-  __shared__ uint32_t s[kSortWaves][kRadix];  // per-wave bins: 4x less same-address contention
-  const int w = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < kSortWaves * kRadix; i += kSortThreads) (&s[0][0])[i] = 0u;
-  __syncthreads();
-  const long base = (long)blockIdx.x * kSortTile;
-#pragma unroll 4
-  for (int i = 0; i < kSortItems; ++i) {
-    const long e = base + (long)i * kSortThreads + threadIdx.x;
-    if (e < n) atomicAdd(&s[w][digit_of(keys[e], shift)], 1u);
-  }
-  __syncthreads();
-  const int d = threadIdx.x;
-  hist[(long)d * ntiles + blockIdx.x] = s[0][d] + s[1][d] + s[2][d] + s[3][d];
-}
-
 // (2) one workgroup per digit: exclusive scan over tiles in place, column total
 __global__ __launch_bounds__(1024) void radix_scan_kernel(uint32_t* __restrict__ hist, long ntiles,
                                                           uint32_t* __restrict__ totals) {
@@ -109,88 +90,6 @@ __global__ __launch_bounds__(1024) void radix_scan_kernel(uint32_t* __restrict__
     __syncthreads();
   }
   if (t == 0) totals[blockIdx.x] = s_carry;
-}
-
-// (3) stable scatter of one tile
-__global__ __launch_bounds__(kSortThreads) void radix_scatter_kernel(
-    const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin, uint64_t* __restrict__ kout,
-    uint32_t* __restrict__ vout, long n, int shift, long ntiles, const uint32_t* __restrict__ hist,
-    const uint32_t* __restrict__ totals) {
-  __shared__ uint64_t s_k[kSortTile];
-  __shared__ uint32_t s_v[kSortTile];
-  __shared__ uint32_t s_wc[kSortWaves][kRadix];
-  __shared__ uint32_t s_run[kRadix];
-  __shared__ uint32_t s_toff[kRadix];
-  __shared__ uint32_t s_gbase[kRadix];
-  __shared__ uint32_t s_w[4];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const long tile = blockIdx.x;
-  const long base = tile * kSortTile;
-  const int tile_n = (int)min((long)kSortTile, n - base);
-
-  // global start of digit t for this tile, and the tile's own digit offsets
-  const uint32_t hd = hist[(long)t * ntiles + tile];
-  const uint32_t cnt = (tile + 1 < ntiles ? hist[(long)t * ntiles + tile + 1] : totals[t]) - hd;
-  const uint32_t gb = block_excl_scan256(totals[t], s_w);
-  s_gbase[t] = gb + hd;
-  const uint32_t toff = block_excl_scan256(cnt, s_w);
-  s_toff[t] = toff;
-  s_run[t] = 0u;
-#pragma unroll
-  for (int i = 0; i < kSortWaves; ++i) s_wc[i][t] = 0u;
-
-  uint64_t k[kSortItems];
-  uint32_t v[kSortItems];
-#pragma unroll
-  for (int i = 0; i < kSortItems; ++i) {
-    const long e = base + (long)i * kSortThreads + t;
-    if (e < n) {
-      k[i] = kin[e];
-      v[i] = vin ? vin[e] : (uint32_t)e;
-    }
-  }
-  __syncthreads();
-  const uint64_t lt = __lanemask_lt();
-#pragma unroll 1
-  for (int i = 0; i < kSortItems; ++i) {
-    const bool valid = i * kSortThreads + t < tile_n;
-    const uint32_t d = valid ? digit_of(k[i], shift) : 0u;
-    uint64_t m = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      const uint64_t bal = __ballot((d >> b) & 1u);
-      m &= ((d >> b) & 1u) ? bal : ~bal;
-    }
-    const uint32_t pre = __popcll(m & lt);
-    if (valid && pre == 0) s_wc[w][d] = __popcll(m);
-    __syncthreads();
-    if (valid) {
-      uint32_t off = s_run[d] + pre;
-      for (int ww = 0; ww < w; ++ww) off += s_wc[ww][d];
-      const uint32_t local = s_toff[d] + off;
-      s_k[local] = k[i];
-      s_v[local] = v[i];
-    }
-    __syncthreads();
-    {
-      uint32_t sum = 0;
-#pragma unroll
-      for (int ww = 0; ww < kSortWaves; ++ww) {
-        sum += s_wc[ww][t];
-        s_wc[ww][t] = 0u;
-      }
-      s_run[t] += sum;
-    }
-    __syncthreads();
-  }
-  // the tile is grouped by digit in LDS: write each digit run to its place
-  for (int j = t; j < tile_n; j += kSortThreads) {
-    const uint64_t key = s_k[j];
-    const uint32_t d = digit_of(key, shift);
-    const long dst = (long)s_gbase[d] + (j - (long)s_toff[d]);
-    kout[dst] = key;
-    vout[dst] = s_v[j];
-  }
 }
 
 // (3') stable scatter with wave-private ranking.  Each wave owns a contiguous
@@ -324,6 +223,162 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist_v2_kernel(const uint6
   }
   __syncthreads();
   hist[(long)t * ntiles + blockIdx.x] = s[0][t] + s[1][t] + s[2][t] + s[3][t];
+}
+
+// ---------------------------------------------------------------- onesweep (keys only)
+// LSD radix sort of uint64 keys by bits [begin, begin + 8·passes) with ONE read
+// of the keys for every digit's histogram and one scatter pass per digit whose
+// tile offsets come from a decoupled look-back instead of a per-pass
+// histogram + scan (radix_hist_v2 + radix_scan: one more read of the keys and
+// two more launches per pass).  Tiles take their index from an atomic ticket,
+// so every tile a tile waits on was scheduled before it.  Status words per
+// (tile, digit), 64-bit: bits 63-48 the pass's epoch, 47-46 the kind (0
+// empty, 1 aggregate = this tile's count, 2 inclusive prefix through this
+// tile), 31-0 the value.  A word from another epoch reads as empty, so the
+// status array is zeroed once when allocated, not before every pass.
+// A look-back that sees nothing for kSpinLimit polls sets *err and moves on
+// (the output is then wrong and the caller's order check sees it): every wave
+// reaches the kernel's end.
+constexpr uint64_t kStAgg = 1ull << 46, kStInc = 2ull << 46, kStKind = 3ull << 46;
+constexpr int kSpinLimit = 1 << 22;
+constexpr int kMaxPasses = 8;
+
+__global__ __launch_bounds__(kSortThreads) void radix_hist_all_kernel(
+    const uint64_t* __restrict__ keys, long n, int begin, int end, int passes,
+    uint32_t* __restrict__ ghist) {
+  __shared__ uint32_t s[kMaxPasses][kRadix];
+  const int t = threadIdx.x;
+  for (int p = 0; p < passes; ++p) s[p][t] = 0u;
+  __syncthreads();
+  for (long base = (long)blockIdx.x * kSortTile; base < n; base += (long)gridDim.x * kSortTile) {
+#pragma unroll 4
+    for (int i = 0; i < kSortItems; ++i) {
+      const long e = base + (long)i * kSortThreads + t;
+      if (e < n) {
+        const uint64_t k = keys[e];
+        for (int p = 0; p < passes; ++p) {
+          const int sh = begin + 8 * p;
+          atomicAdd(&s[p][(uint32_t)(k >> sh) & ((1u << min(8, end - sh)) - 1u)], 1u);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int p = 0; p < passes; ++p)
+    if (s[p][t]) atomicAdd(&ghist[p * kRadix + t], s[p][t]);
+}
+
+// one workgroup per pass: exclusive scan of the digit counts in place
+__global__ __launch_bounds__(kSortThreads) void radix_bases_kernel(uint32_t* __restrict__ ghist) {
+  __shared__ uint32_t s_w[4];
+  uint32_t* h = ghist + blockIdx.x * kRadix;
+  const uint32_t x = h[threadIdx.x];
+  const uint32_t e = block_excl_scan256(x, s_w);
+  h[threadIdx.x] = e;
+}
+
+__global__ __launch_bounds__(kSortThreads) void radix_onesweep_kernel(
+    const uint64_t* __restrict__ kin, uint64_t* __restrict__ kout, long n, int shift,
+    uint32_t dmask, const uint32_t* __restrict__ gbase, uint64_t* __restrict__ status,
+    uint64_t epoch, uint32_t* __restrict__ ticket, uint32_t* __restrict__ err) {
+  __shared__ uint64_t s_k[kSortTile];
+  __shared__ uint32_t s_wh[kSortWaves][kRadix];
+  __shared__ uint32_t s_toff[kRadix];
+  __shared__ uint32_t s_g[kRadix];
+  __shared__ uint32_t s_w[4];
+  __shared__ uint32_t s_tile;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t == 0) s_tile = atomicAdd(ticket, 1u);
+#pragma unroll
+  for (int i = 0; i < kSortWaves; ++i) s_wh[i][t] = 0u;
+  __syncthreads();
+  const long tile = s_tile;
+  const long base = tile * kSortTile;
+  const int tile_n = (int)min((long)kSortTile, n - base);
+  constexpr int kWaveSpan = kSortTile / kSortWaves;
+  uint64_t k[kSortItems];
+  const long wbase = base + (long)w * kWaveSpan;
+#pragma unroll
+  for (int i = 0; i < kSortItems; ++i) {
+    const long e = wbase + i * HBMR_WAVE + lane;
+    k[i] = e < n ? kin[e] : 0ull;
+  }
+  const uint64_t lt = __lanemask_lt();
+  uint32_t rank[kSortItems];
+#pragma unroll
+  for (int i = 0; i < kSortItems; ++i) {
+    const bool valid = w * kWaveSpan + i * HBMR_WAVE + lane < tile_n;
+    const uint32_t d = valid ? ((uint32_t)(k[i] >> shift) & dmask) : 0u;
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const uint64_t bal = __ballot((d >> b) & 1u);
+      m &= ((d >> b) & 1u) ? bal : ~bal;
+    }
+    const uint32_t pre = __popcll(m & lt);
+    uint32_t old = 0u;
+    if (valid) old = s_wh[w][d];
+    __builtin_amdgcn_wave_barrier();
+    rank[i] = old + pre;
+    if (valid && pre == 0) s_wh[w][d] = old + (uint32_t)__popcll(m);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  {
+    // thread t = digit t: publish the tile's count, look back for its prefix
+    uint32_t c[kSortWaves], cnt = 0;
+#pragma unroll
+    for (int i = 0; i < kSortWaves; ++i) {
+      c[i] = s_wh[i][t];
+      cnt += c[i];
+    }
+    uint64_t* st = status + tile * kRadix + t;
+    const uint64_t ep = epoch << 48;
+    uint32_t excl = 0;
+    if (tile == 0) {
+      __hip_atomic_store(st, ep | kStInc | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(st, ep | kStAgg | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (long p = tile - 1; p >= 0; --p) {
+        const uint64_t* q = status + p * kRadix + t;
+        uint64_t v = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int spins = 0;
+        while (((v >> 48) != epoch || (v & kStKind) == 0u) && ++spins < kSpinLimit) {
+          __builtin_amdgcn_s_sleep(1);
+          v = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if ((v >> 48) != epoch || (v & kStKind) == 0u) {
+          atomicOr(err, 1u);
+          break;
+        }
+        excl += (uint32_t)v;
+        if ((v & kStKind) == kStInc) break;
+      }
+      __hip_atomic_store(st, ep | kStInc | (excl + cnt), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_g[t] = gbase[t] + excl;
+    const uint32_t toff = block_excl_scan256(cnt, s_w);
+    s_toff[t] = toff;
+    uint32_t run = toff;
+#pragma unroll
+    for (int i = 0; i < kSortWaves; ++i) {
+      s_wh[i][t] = run;
+      run += c[i];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kSortItems; ++i) {
+    if (w * kWaveSpan + i * HBMR_WAVE + lane < tile_n)
+      s_k[s_wh[w][((uint32_t)(k[i] >> shift) & dmask)] + rank[i]] = k[i];
+  }
+  __syncthreads();
+  for (int j = t; j < tile_n; j += kSortThreads) {
+    const uint64_t key = s_k[j];
+    const uint32_t d = ((uint32_t)(key >> shift) & dmask);
+    kout[(long)s_g[d] + (j - (long)s_toff[d])] = key;
+  }
 }
 
 // ------------------------------------------------------------------------ TeraSort
@@ -465,11 +520,136 @@ __global__ __launch_bounds__(256) void check_sorted_kernel(const uint64_t* __res
   if ((threadIdx.x & 63) == 0 && m) atomicAdd(bad, (unsigned long long)__popcll(m));
 }
 
+// One group of the one-rank reduce, after its sort: acc[0] += the records out
+// of order (against the previous record; record 0 against the previous
+// group's last key *ph / *pl when given), acc[1] += sum(hi + lo) mod 2^64 (the
+// order-independent key checksum) — one pass, one atomic per wave, in place
+// of an order check, two reductions and the elementwise seam check.
+__global__ __launch_bounds__(256) void tera_group_stats_kernel(
+    const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo, long n,
+    const uint64_t* __restrict__ ph, const uint64_t* __restrict__ pl,
+    unsigned long long* __restrict__ parts) {
+  __shared__ unsigned long long s[2][4];
+  uint64_t sum = 0, bad = 0;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const uint64_t h = hi[i], l = lo[i];
+    sum += h + l;
+    if (i > 0) {
+      const uint64_t h0 = hi[i - 1], l0 = lo[i - 1];
+      bad += h0 > h || (h0 == h && l0 > l);
+    } else if (ph != nullptr) {
+      bad += *ph > h || (*ph == h && *pl > l);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    sum += __shfl_xor(sum, o);
+    bad += __shfl_xor(bad, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s[0][threadIdx.x >> 6] = bad;
+    s[1][threadIdx.x >> 6] = sum;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    parts[2 * blockIdx.x] = s[0][0] + s[0][1] + s[0][2] + s[0][3];
+    parts[2 * blockIdx.x + 1] = s[1][0] + s[1][1] + s[1][2] + s[1][3];
+  }
+}
+
 // Key words + range partition of each record: pid = number of splitters <= key
 // (partition p holds keys in [split[p-1], split[p]), as split_offsets cuts a
 // sorted run).  Splitters are staged in LDS once per workgroup; each workgroup
 // then walks a grid-stride slice of the records.
 constexpr int kMaxSplitters = 4096;
+
+// An order-preserving map of a key's high word to a dense integer: with every
+// key byte in [m, m + R) (the job's key alphabet: the maps measure the OR of
+// all key bytes, so m = 0 and R = 2^bits — 128 for printable keys),
+// v(h) = the 8 bytes of h as base-R digits, and the window (v(h) - vlo) >> sh
+// for a group whose keys' v lie in [vlo, vlo + span), sh chosen so the
+// window fits in 32 bits.  For printable keys (R = 128) the window keeps ~30
+// bits of the group's spread where the raw top 32 bits of h keep ~22 (their
+// bytes use 95 of 256 codes and the group fixes most of the first one).
+// R = 256, m = 0, vlo = 0 is the plain shift h >> sh.
+struct KeyWindow {
+  uint64_t vlo;
+  uint32_t m, R;
+  int sh;
+};
+
+__device__ __forceinline__ uint64_t key_window(uint64_t h, const KeyWindow& kw) {
+  uint64_t v = 0;
+#pragma unroll
+  for (int b = 7; b >= 0; --b) v = v * kw.R + (((h >> (8 * b)) & 0xFFu) - kw.m);
+  return (v - kw.vlo) >> kw.sh;
+}
+
+// running OR of a high word's bytes (folded to one byte at the flush): every
+// key byte is at most the OR of all of them, so [0, 2^bits(OR)) is an
+// alphabet that holds them; and the key checksum sum(hi + lo) mod 2^64 the
+// map reports.  A few VALU per record: this kernel is latency bound (the
+// splitter search), and a per-record byte or word min / max cost it 2.4x.
+__device__ __forceinline__ void byte_range(uint64_t h, uint32_t l, uint32_t& orb, uint64_t& sum) {
+  orb |= (uint32_t)h | (uint32_t)(h >> 32);
+  sum += h + l;
+}
+
+// the block's (OR of key bytes, key checksum) into parts[blockIdx] — no
+// global atomics on one address (across 8 XCDs they serialise at ~0.2 us
+// each: 16k blocks cost the kernel 3.5 ms); reduce_pairs_kernel folds them
+__device__ __forceinline__ void flush_byte_range(uint32_t orb, uint64_t sum,
+                                                 unsigned long long* s_ks,
+                                                 unsigned long long* parts) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    orb |= __shfl_xor(orb, o);
+    sum += __shfl_xor(sum, o);
+  }
+  orb |= orb >> 16;
+  orb |= orb >> 8;
+  if ((threadIdx.x & 63) == 0) {
+    atomicOr(&s_ks[0], (unsigned long long)(orb & 0xFFu));
+    atomicAdd(&s_ks[1], (unsigned long long)sum);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && parts != nullptr) {
+    parts[2 * blockIdx.x] = s_ks[0];
+    parts[2 * blockIdx.x + 1] = s_ks[1];
+  }
+}
+
+// one workgroup: out[0] (|= or +=, by or0) and out[1] += over nparts pairs
+__global__ __launch_bounds__(256) void reduce_pairs_kernel(const unsigned long long* __restrict__ parts,
+                                                           long nparts, int or0,
+                                                           unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long s[2][4];
+  unsigned long long a = 0, b = 0;
+  for (long i = threadIdx.x; i < nparts; i += 256) {
+    a = or0 ? (a | parts[2 * i]) : a + parts[2 * i];
+    b += parts[2 * i + 1];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long x = __shfl_xor(a, o);
+    a = or0 ? (a | x) : a + x;
+    b += __shfl_xor(b, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s[0][threadIdx.x >> 6] = a;
+    s[1][threadIdx.x >> 6] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long x = out[0], y = out[1];
+    for (int w = 0; w < 4; ++w) {
+      x = or0 ? (x | s[0][w]) : x + s[0][w];
+      y += s[1][w];
+    }
+    out[0] = x;
+    out[1] = y;
+  }
+}
 
 __global__ __launch_bounds__(256) void tera_keys_part_kernel(
     const uint8_t* __restrict__ rec, long n, int stride, const uint64_t* __restrict__ shi,
@@ -556,45 +736,30 @@ __global__ __launch_bounds__(256) void tera_collect_slots_kernel(
   }
 }
 
-// dst record i = record row[k] of split split[k], k = perm ? perm[i] : i
-// (split kNoSplit: record i is left unwritten); records
-// of `words` 4-byte words, one word per lane (25 lanes cover a 100-byte record)
-// A workgroup copies 256 / words whole records per step: lane t moves word
-// t % words of record t / words (one 32-bit division per thread, not one
-// 64-bit division per word), so each record's index loads are shared by its
-// lanes and its words are read and written as one contiguous run.
-__global__ __launch_bounds__(256) void gather_records_multi_kernel(
-    const uint32_t* const* __restrict__ bases, const uint32_t* __restrict__ split,
-    const uint32_t* __restrict__ row, const uint32_t* __restrict__ perm, long n, int words,
-    uint32_t* __restrict__ dst) {
-  const int rpb = 256 / words;
-  const int t = threadIdx.x;
-  if (t >= rpb * words) return;
-  const int lr = t / words;
-  const int w = t - lr * words;
-  for (long r = (long)blockIdx.x * rpb + lr; r < n; r += (long)gridDim.x * rpb) {
-    const long k = perm ? (long)perm[r] : r;
-    const uint32_t sp = split[k];
-    if (sp != kNoSplit) dst[r * words + w] = bases[sp][(long)row[k] * words + w];
-  }
-}
-
 // ---- TeraSort map v3: partition without a sort ------------------------------
 // (A) key words + partition id of every record, and the partition sizes: a
 // per-workgroup LDS histogram flushed with one global add per touched bin.
 __global__ __launch_bounds__(256) void tera_part_count_kernel(
     const uint8_t* __restrict__ rec, long n, int stride, const uint64_t* __restrict__ shi,
     const uint64_t* __restrict__ slo, int nsplit, uint64_t* __restrict__ hi,
-    uint64_t* __restrict__ lo, uint16_t* __restrict__ pid, unsigned int* __restrict__ counts) {
+    uint64_t* __restrict__ lo, uint16_t* __restrict__ pid, unsigned int* __restrict__ counts,
+    unsigned long long* __restrict__ kmm) {
   __shared__ uint64_t s_hi[kMaxSplitters];
   __shared__ uint16_t s_lo[kMaxSplitters];
   __shared__ unsigned int s_cnt[kMaxSplitters + 1];
+  __shared__ unsigned long long s_ks[2];
+  uint32_t korb = 0u;
+  uint64_t ksum = 0;
   const int nparts = nsplit + 1;
   for (int j = threadIdx.x; j < nsplit; j += 256) {
     s_hi[j] = shi[j];
     s_lo[j] = (uint16_t)slo[j];
   }
   for (int j = threadIdx.x; j < nparts; j += 256) s_cnt[j] = 0u;
+  if (threadIdx.x == 0) {
+    s_ks[0] = 0ull;
+    s_ks[1] = 0ull;
+  }
   __syncthreads();
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
     const uint8_t* r = rec + i * stride;
@@ -612,8 +777,9 @@ __global__ __launch_bounds__(256) void tera_part_count_kernel(
     lo[i] = l;
     pid[i] = (uint16_t)a;
     atomicAdd(&s_cnt[a], 1u);
+    byte_range(h, l, korb, ksum);
   }
-  __syncthreads();
+  flush_byte_range(korb, ksum, s_ks, kmm);
   for (int j = threadIdx.x; j < nparts; j += 256)
     if (s_cnt[j]) atomicAdd(&counts[j], s_cnt[j]);
 }
@@ -701,16 +867,24 @@ __global__ __launch_bounds__(kSortThreads) void tera_part_scatter_kernel(
 __global__ __launch_bounds__(256) void tera_part_count_w_kernel(
     const uint32_t* __restrict__ rec, long n, int stride_words, const uint64_t* __restrict__ shi,
     const uint64_t* __restrict__ slo, int nsplit, uint64_t* __restrict__ hi,
-    uint64_t* __restrict__ lo, uint16_t* __restrict__ pid, unsigned int* __restrict__ counts) {
+    uint64_t* __restrict__ lo, uint16_t* __restrict__ pid, unsigned int* __restrict__ counts,
+    unsigned long long* __restrict__ kmm) {
   __shared__ uint64_t s_hi[kMaxSplitters];
   __shared__ uint16_t s_lo[kMaxSplitters];
   __shared__ unsigned int s_cnt[kMaxSplitters + 1];
+  __shared__ unsigned long long s_ks[2];
+  uint32_t korb = 0u;
+  uint64_t ksum = 0;
   const int nparts = nsplit + 1;
   for (int j = threadIdx.x; j < nsplit; j += 256) {
     s_hi[j] = shi[j];
     s_lo[j] = (uint16_t)slo[j];
   }
   for (int j = threadIdx.x; j < nparts; j += 256) s_cnt[j] = 0u;
+  if (threadIdx.x == 0) {
+    s_ks[0] = 0ull;
+    s_ks[1] = 0ull;
+  }
   __syncthreads();
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
     const uint32_t* r = rec + i * stride_words;
@@ -727,8 +901,9 @@ __global__ __launch_bounds__(256) void tera_part_count_w_kernel(
     lo[i] = l;
     pid[i] = (uint16_t)a;
     atomicAdd(&s_cnt[a], 1u);
+    byte_range(h, l, korb, ksum);
   }
-  __syncthreads();
+  flush_byte_range(korb, ksum, s_ks, kmm);
   for (int j = threadIdx.x; j < nparts; j += 256)
     if (s_cnt[j]) atomicAdd(&counts[j], s_cnt[j]);
 }
@@ -864,8 +1039,8 @@ __global__ __launch_bounds__(256) void merge_path_kernel(
 // ONE dependent index load per record (v3: perm, then split and row).
 __global__ __launch_bounds__(256) void tera_collect_gid_kernel(
     const uint64_t* const* __restrict__ his, const uint32_t* const* __restrict__ rows,
-    const long* __restrict__ starts, const long* __restrict__ prefix, int S, long n,
-    uint64_t* __restrict__ ohi, uint32_t* __restrict__ ogid) {
+    const long* __restrict__ starts, const long* __restrict__ prefix, int S, long n, int pack,
+    KeyWindow kw, uint64_t* __restrict__ ohi, uint32_t* __restrict__ ogid) {
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
     int a = 0, b = S;          // largest s with prefix[s] <= i
     while (b - a > 1) {
@@ -873,17 +1048,24 @@ __global__ __launch_bounds__(256) void tera_collect_gid_kernel(
       if (prefix[m] <= i) a = m; else b = m;
     }
     const long j = starts[a] + (i - prefix[a]);
-    ohi[i] = his[a][j];
-    ogid[i] = ((uint32_t)a << 24) | rows[a][j];
+    const uint32_t g = ((uint32_t)a << 24) | rows[a][j];
+    if (pack) {
+      // one sortable word: the key's 32-bit window above the record id
+      ohi[i] = ((key_window(his[a][j], kw) & 0xFFFFFFFFull) << 32) | g;
+    } else {
+      ohi[i] = his[a][j];
+      ogid[i] = g;
+    }
   }
 }
 
 // (with key outputs: the lanes holding words 0-2 of a record also store its
 // key — hi as two byte-swapped halves, lo from word 2 — so the sorted keys
 // need no second pass over the gathered records)
-template <int U, bool NT = false>
+template <int U>
 __global__ __launch_bounds__(256) void gather_records_gid_kernel(
-    const uint32_t* const* __restrict__ bases, const uint32_t* __restrict__ gid, long n,
+    const uint32_t* const* __restrict__ bases, const uint32_t* __restrict__ gid,
+    const uint64_t* packed, long n,
     int words, uint32_t* __restrict__ dst, uint32_t* __restrict__ khi,
     uint64_t* __restrict__ klo) {
   const int rpb = 256 / words;
@@ -899,7 +1081,7 @@ __global__ __launch_bounds__(256) void gather_records_gid_kernel(
       const long r = r0 + j * stride;
       src[j] = nullptr;
       if (r < n) {
-        const uint32_t g = gid[r];
+        const uint32_t g = packed ? (uint32_t)packed[r] : gid[r];
         src[j] = bases[g >> 24] + (long)(g & 0xFFFFFFu) * words;
       }
     }
@@ -910,10 +1092,7 @@ __global__ __launch_bounds__(256) void gather_records_gid_kernel(
     for (int j = 0; j < U; ++j) {
       const long r = r0 + j * stride;
       if (r < n) {
-        if constexpr (NT)
-          __builtin_nontemporal_store(v[j], dst + r * words + w);  // streamed: no L2 reuse
-        else
-          dst[r * words + w] = v[j];
+        dst[r * words + w] = v[j];
       }
     }
     if (khi != nullptr && w < 3) {
@@ -943,9 +1122,10 @@ typedef u32x4_t __attribute__((aligned(4))) u32x4_a4;
 typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
 typedef u32x2_t __attribute__((aligned(4))) u32x2_a4;
 
-template <int U, bool NT>
+template <int U>
 __global__ __launch_bounds__(256) void gather_records_gid16_kernel(
-    const uint32_t* const* __restrict__ bases, const uint32_t* __restrict__ gid, long n,
+    const uint32_t* const* __restrict__ bases, const uint32_t* __restrict__ gid,
+    const uint64_t* packed, long n,
     int words, uint32_t* __restrict__ dst, uint32_t* __restrict__ khi,
     uint64_t* __restrict__ klo) {
   const int L = (words + 3) >> 2;            // lanes per record
@@ -965,7 +1145,7 @@ __global__ __launch_bounds__(256) void gather_records_gid16_kernel(
       const long r = r0 + j * stride;
       src[j] = nullptr;
       if (r < n) {
-        const uint32_t g = gid[r];
+        const uint32_t g = packed ? (uint32_t)packed[r] : gid[r];
         src[j] = bases[g >> 24] + (long)(g & 0xFFFFFFu) * words + w0;
       }
     }
@@ -992,10 +1172,7 @@ __global__ __launch_bounds__(256) void gather_records_gid16_kernel(
       if (r >= n) continue;
       uint32_t* d = dst + r * words + w0;
       if (nw == 4) {
-        if constexpr (NT)
-          __builtin_nontemporal_store(v[j], reinterpret_cast<u32x4_a4*>(d));
-        else
-          *reinterpret_cast<u32x4_a4*>(d) = v[j];
+        *reinterpret_cast<u32x4_a4*>(d) = v[j];
       } else if (nw == 2) {
         *reinterpret_cast<u32x2_a4*>(d) = u32x2_t{v[j].x, v[j].y};
       } else {
@@ -1012,41 +1189,64 @@ __global__ __launch_bounds__(256) void gather_records_gid16_kernel(
   }
 }
 
-// After the sort on the high key word's top 64 - shift bits and the record
-// gather: order each run of an equal sorted prefix (hi >> shift) by the full
-// key (hi, lo), moving hi, lo and the (already gathered) records themselves;
-// runs longer than kTieRun are flagged for the full-key path.  shift = 16
-// saves two of eight radix passes: among the ~10^8 keys of a group, equal
-// 48-bit prefixes come in a few dozen pairs.
-__global__ __launch_bounds__(256) void tera_tie_fix_records_kernel(
-    uint64_t* __restrict__ hi, uint64_t* __restrict__ lo, uint32_t* __restrict__ rec,
-    long n, int words, int shift, unsigned int* __restrict__ flag) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n - 1) return;
-  const uint64_t h = hi[i] >> shift;
-  if ((hi[i + 1] >> shift) != h || (i > 0 && (hi[i - 1] >> shift) == h)) return;
-  long e = i + 1;
-  while (e < n && (hi[e] >> shift) == h && e - i < kTieRun) ++e;
-  if (e < n && (hi[e] >> shift) == h) {
+// After the sort on a window of the high key word and the record gather:
+// order each run of an equal sorted prefix (hi >> shift) by the full key
+// (hi, lo), moving hi, lo and the (already gathered) records themselves.
+// Two passes, one thread per record: (1) a record in a run ranks itself
+// among the run's members by (hi, lo, position) and, if its place changes,
+// copies itself to a compact scratch slot with its destination; (2) every
+// scratch slot is written to its destination.  Runs longer than kTieRun (or
+// more moved records than the scratch holds) are flagged for the full-key
+// path.  A 32-bit window over ~12M keys leaves equal prefixes on a few
+// percent of them, in pairs and triples.
+__global__ __launch_bounds__(256) void tera_tie_rank_kernel(
+    const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo,
+    const uint32_t* __restrict__ rec, long n, int words, KeyWindow kw, long cap,
+    unsigned int* __restrict__ cnt, uint32_t* __restrict__ sdst, uint64_t* __restrict__ shi,
+    uint64_t* __restrict__ slo, uint32_t* __restrict__ srec, unsigned int* __restrict__ flag) {
+  const long j = (long)blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  const uint64_t hj = hi[j], lj = lo[j], h = key_window(hj, kw);
+  const bool prev = j > 0 && key_window(hi[j - 1], kw) == h;
+  const bool next = j + 1 < n && key_window(hi[j + 1], kw) == h;
+  if (!prev && !next) return;
+  long s0 = j, e = j + 1;
+  while (s0 > 0 && key_window(hi[s0 - 1], kw) == h && j - s0 < kTieRun) --s0;
+  while (e < n && key_window(hi[e], kw) == h && e - j < kTieRun) ++e;
+  if ((s0 > 0 && key_window(hi[s0 - 1], kw) == h) || (e < n && key_window(hi[e], kw) == h) ||
+      e - s0 > kTieRun) {
     atomicOr(flag, 1u);
     return;
   }
-  // insertion sort by adjacent swaps (no per-lane record buffer)
-  for (long a = i + 1; a < e; ++a) {
-    for (long b = a - 1;
-         b >= i && (hi[b] > hi[b + 1] || (hi[b] == hi[b + 1] && lo[b] > lo[b + 1])); --b) {
-      const uint64_t th = hi[b];
-      hi[b] = hi[b + 1];
-      hi[b + 1] = th;
-      const uint64_t t = lo[b];
-      lo[b] = lo[b + 1];
-      lo[b + 1] = t;
-      for (int w = 0; w < words; ++w) {
-        const uint32_t x = rec[b * words + w];
-        rec[b * words + w] = rec[(b + 1) * words + w];
-        rec[(b + 1) * words + w] = x;
-      }
-    }
+  long rank = 0;
+  for (long k = s0; k < e; ++k) {
+    const uint64_t hk = hi[k], lk = lo[k];
+    rank += hk < hj || (hk == hj && (lk < lj || (lk == lj && k < j)));
+  }
+  const long d = s0 + rank;
+  if (d == j) return;
+  const unsigned int slot = atomicAdd(cnt, 1u);
+  if ((long)slot >= cap) {
+    atomicOr(flag, 1u);
+    return;
+  }
+  sdst[slot] = (uint32_t)d;
+  shi[slot] = hj;
+  slo[slot] = lj;
+  for (int w = 0; w < words; ++w) srec[(long)slot * words + w] = rec[j * words + w];
+}
+
+__global__ __launch_bounds__(256) void tera_tie_move_kernel(
+    uint64_t* __restrict__ hi, uint64_t* __restrict__ lo, uint32_t* __restrict__ rec, int words,
+    long cap, const unsigned int* __restrict__ cnt, const uint32_t* __restrict__ sdst,
+    const uint64_t* __restrict__ shi, const uint64_t* __restrict__ slo,
+    const uint32_t* __restrict__ srec) {
+  const long m = min((long)*cnt, cap);
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < m; i += (long)gridDim.x * 256) {
+    const long d = sdst[i];
+    hi[d] = shi[i];
+    lo[d] = slo[i];
+    for (int w = 0; w < words; ++w) rec[d * words + w] = srec[i * words + w];
   }
 }
 
@@ -1079,26 +1279,13 @@ int hbmr_radix_sort_pairs_u64(uint64_t* keys, uint32_t* vals, uint64_t* tkeys, u
   uint32_t* va = vals;
   uint64_t* kb = tkeys;
   uint32_t* vb = tvals;
-  // HBMR_RADIX_V1=1: the round-1 kernels (per-key atomics, 3 barriers per key), for A/B
-  static const bool v1 = [] {
-    const char* e = getenv("HBMR_RADIX_V1");
-    return e && *e == '1';
-  }();
   int passes = 0;
   for (int shift = begin_bit; shift < end_bit; shift += 8, ++passes) {
-    if (v1)
-      hipLaunchKernelGGL(radix_hist_kernel, dim3((unsigned)ntiles), dim3(kSortThreads), 0, st, ka,
-                         n, shift, ntiles, hist);
-    else
-      hipLaunchKernelGGL(radix_hist_v2_kernel, dim3((unsigned)ntiles), dim3(kSortThreads), 0, st,
-                         ka, n, shift, ntiles, hist);
+    hipLaunchKernelGGL(radix_hist_v2_kernel, dim3((unsigned)ntiles), dim3(kSortThreads), 0, st,
+                       ka, n, shift, ntiles, hist);
     hipLaunchKernelGGL(radix_scan_kernel, dim3(kRadix), dim3(1024), 0, st, hist, ntiles, totals);
-    if (v1)
-      hipLaunchKernelGGL(radix_scatter_kernel, dim3((unsigned)ntiles), dim3(kSortThreads), 0, st,
-                         ka, va, kb, vb, n, shift, ntiles, hist, totals);
-    else
-      hipLaunchKernelGGL(radix_scatter_v2_kernel, dim3((unsigned)ntiles), dim3(kSortThreads), 0, st,
-                         ka, va, kb, vb, n, shift, ntiles, hist, totals);
+    hipLaunchKernelGGL(radix_scatter_v2_kernel, dim3((unsigned)ntiles), dim3(kSortThreads), 0, st,
+                       ka, va, kb, vb, n, shift, ntiles, hist, totals);
     std::swap(ka, kb);
     std::swap(va, vb);
   }
@@ -1106,6 +1293,60 @@ int hbmr_radix_sort_pairs_u64(uint64_t* keys, uint32_t* vals, uint64_t* tkeys, u
     HBMR_RETURN_IF_ERROR(hipMemcpyAsync(keys, ka, n * 8, hipMemcpyDeviceToDevice, st));
     HBMR_RETURN_IF_ERROR(hipMemcpyAsync(vals, va, n * 4, hipMemcpyDeviceToDevice, st));
   }
+  return (int)hipGetLastError();
+}
+
+long hbmr_radix_onesweep_workspace_bytes(long n) {
+  return (long)(kMaxPasses * kRadix + kMaxPasses + 1) * 4;
+}
+
+long hbmr_radix_onesweep_status_bytes(long n) {
+  return std::max(1L, ceil_div(n, kSortTile)) * kRadix * 8;
+}
+
+// Sort uint64 keys by bits [begin_bit, end_bit) (8-bit digits, LSD, stable),
+// keys only, onesweep: one histogram read for all digits, then per digit one
+// look-back scatter.  keys holds the input and receives the output; tkeys is
+// scratch of the same size; *err (device) is set if a look-back timed out.
+// status (hbmr_radix_onesweep_status_bytes) is reused across calls on one
+// stream: each pass tags its words with a fresh epoch from *epoch (a host
+// counter; at 0 or 0xFFFF the status is zeroed first and the count restarts).
+// copy_back = 0 leaves an odd pass count's result in tkeys.
+int hbmr_radix_sort_keys_u64(uint64_t* keys, uint64_t* tkeys, long n, int begin_bit, int end_bit,
+                             void* ws, long ws_bytes, void* status, long status_bytes,
+                             unsigned int* epoch, uint32_t* err, int copy_back, hipStream_t st) {
+  if (n <= 1) return 0;
+  const int passes = (end_bit - begin_bit + 7) / 8;
+  if (n >= (1L << 30) || begin_bit < 0 || end_bit > 64 || begin_bit >= end_bit ||
+      passes > kMaxPasses || epoch == nullptr)
+    return (int)hipErrorInvalidValue;
+  if (ws_bytes < hbmr_radix_onesweep_workspace_bytes(n) ||
+      status_bytes < hbmr_radix_onesweep_status_bytes(n))
+    return (int)hipErrorInvalidValue;
+  const long ntiles = ceil_div(n, kSortTile);
+  uint32_t* ghist = reinterpret_cast<uint32_t*>(ws);
+  uint32_t* tickets = ghist + kMaxPasses * kRadix;
+  HBMR_RETURN_IF_ERROR(hipMemsetAsync(ghist, 0, (kMaxPasses * kRadix + kMaxPasses) * 4, st));
+  const long hgrid = std::min<long>(ntiles, 2048);
+  hipLaunchKernelGGL(radix_hist_all_kernel, dim3((unsigned)hgrid), dim3(kSortThreads), 0, st,
+                     keys, n, begin_bit, end_bit, passes, ghist);
+  hipLaunchKernelGGL(radix_bases_kernel, dim3((unsigned)passes), dim3(kSortThreads), 0, st, ghist);
+  uint64_t* ka = keys;
+  uint64_t* kb = tkeys;
+  for (int p = 0; p < passes; ++p) {
+    if (*epoch == 0 || *epoch >= 0xFFFFu) {
+      HBMR_RETURN_IF_ERROR(hipMemsetAsync(status, 0, status_bytes, st));
+      *epoch = 0;
+    }
+    const uint64_t ep = ++*epoch;
+    hipLaunchKernelGGL(radix_onesweep_kernel, dim3((unsigned)ntiles), dim3(kSortThreads), 0, st,
+                       ka, kb, n, begin_bit + 8 * p,
+                       (1u << std::min(8, end_bit - begin_bit - 8 * p)) - 1u, ghist + p * kRadix,
+                       reinterpret_cast<uint64_t*>(status), ep, tickets + p, err);
+    std::swap(ka, kb);
+  }
+  if ((passes & 1) && copy_back)
+    HBMR_RETURN_IF_ERROR(hipMemcpyAsync(keys, ka, n * 8, hipMemcpyDeviceToDevice, st));
   return (int)hipGetLastError();
 }
 
@@ -1159,6 +1400,19 @@ int hbmr_check_sorted(const uint64_t* hi, const uint64_t* lo, long n, unsigned l
   return (int)hipGetLastError();
 }
 
+// acc: device u64[2 + 2 * 1024]: (out of order, checksum) accumulators, then
+// the per-block partials
+int hbmr_tera_group_stats(const uint64_t* hi, const uint64_t* lo, long n, const uint64_t* ph,
+                          const uint64_t* pl, unsigned long long* acc, hipStream_t st) {
+  if (n <= 0) return 0;
+  if ((ph == nullptr) != (pl == nullptr)) return (int)hipErrorInvalidValue;
+  const long grid = std::min<long>(ceil_div(n, 256 * 4), 1024);
+  hipLaunchKernelGGL(tera_group_stats_kernel, dim3((unsigned)grid), dim3(256), 0, st, hi, lo, n,
+                     ph, pl, acc + 2);
+  hipLaunchKernelGGL(reduce_pairs_kernel, dim3(1), dim3(256), 0, st, acc + 2, grid, 0, acc);
+  return (int)hipGetLastError();
+}
+
 int hbmr_tera_keys_part(const void* records, long n, int stride, const uint64_t* shi,
                         const uint64_t* slo, int nsplit, uint64_t* hi, uint64_t* lo,
                         uint64_t* pid, hipStream_t st) {
@@ -1197,13 +1451,18 @@ int hbmr_tera_collect(const uint64_t* const* his, const uint64_t* const* los,
 // TeraSort map v3: (hi, lo, row) of n records in partition order and the
 // partition boundaries offsets[0..nparts] (int64, device).  ws: device scratch
 // of hbmr_tera_partition_workspace_bytes(n, nparts) bytes.
+constexpr long kPartGridMax = 256L * 64;
+
 long hbmr_tera_partition_workspace_bytes(long n, int nparts) {
-  return n * 8 * 2 + n * 2 + 2L * (nparts + 1) * 4 + 64;
+  return n * 8 * 2 + n * 2 + 2L * (nparts + 1) * 4 + 64 + kPartGridMax * 16;
 }
 
+// kst (nullable, device uint64[2] the caller zeroes): [0] |= every key's
+// high-word bytes, [1] += sum(hi + lo) over the split (its key checksum)
 int hbmr_tera_partition(const void* records, long n, int stride, const uint64_t* shi,
                         const uint64_t* slo, int nsplit, uint64_t* ohi, uint64_t* olo,
-                        uint32_t* orow, long* offsets, void* ws, long ws_bytes, hipStream_t st) {
+                        uint32_t* orow, long* offsets, unsigned long long* kmm, void* ws,
+                        long ws_bytes, hipStream_t st) {
   const int nparts = nsplit + 1;
   if (nsplit < 0 || nsplit > kMaxSplitters) return (int)hipErrorInvalidValue;
   if (n < 0 || n >= (1L << 32)) return (int)hipErrorInvalidValue;
@@ -1215,24 +1474,25 @@ int hbmr_tera_partition(const void* records, long n, int stride, const uint64_t*
   unsigned int* counts = reinterpret_cast<unsigned int*>(
       (reinterpret_cast<uintptr_t>(pid + n) + 15) & ~uintptr_t(15));
   unsigned int* cursor = counts + (nparts + 1);
+  unsigned long long* kparts = reinterpret_cast<unsigned long long*>(
+      (reinterpret_cast<uintptr_t>(cursor + (nparts + 1)) + 15) & ~uintptr_t(15));
   HBMR_RETURN_IF_ERROR(hipMemsetAsync(counts, 0, (size_t)(nparts + 1) * 4, st));
-  // HBMR_TERA_PART=v1: the byte-load count (rounds 3-4)
-  static const bool v1 = [] {
-    const char* e = getenv("HBMR_TERA_PART");
-    return e && std::string(e) == "v1";
-  }();
-  const bool words = !v1 && stride % 4 == 0 && stride >= 12 &&
+  // word loads of the key when the records allow them, else byte loads
+  const bool words = stride % 4 == 0 && stride >= 12 &&
                      reinterpret_cast<uintptr_t>(records) % 4 == 0;
   if (n > 0) {
-    const long grid = std::min<long>(ceil_div(n, 256), 256L * 64);
+    const long grid = std::min<long>(ceil_div(n, 256), kPartGridMax);
+    unsigned long long* kp = kmm != nullptr ? kparts : nullptr;
     if (words)
       hipLaunchKernelGGL(tera_part_count_w_kernel, dim3((unsigned)grid), dim3(256), 0, st,
                          reinterpret_cast<const uint32_t*>(records), n, stride / 4, shi, slo,
-                         nsplit, hi, lo, pid, counts);
+                         nsplit, hi, lo, pid, counts, kp);
     else
       hipLaunchKernelGGL(tera_part_count_kernel, dim3((unsigned)grid), dim3(256), 0, st,
                          reinterpret_cast<const uint8_t*>(records), n, stride, shi, slo, nsplit,
-                         hi, lo, pid, counts);
+                         hi, lo, pid, counts, kp);
+    if (kmm != nullptr)
+      hipLaunchKernelGGL(reduce_pairs_kernel, dim3(1), dim3(256), 0, st, kparts, grid, 1, kmm);
   }
   hipLaunchKernelGGL(tera_part_offsets_kernel, dim3(1), dim3(1024), 0, st, counts, nparts, cursor,
                      offsets);
@@ -1265,70 +1525,80 @@ int hbmr_merge_path(const uint64_t* ahi, const uint64_t* alo, const uint32_t* av
   return (int)hipGetLastError();
 }
 
+// pack != 0: ohi = window << 32 | gid with the window of key_window(vlo, m,
+// R, sh) (< 2^32 for the group's keys), ogid unused
 int hbmr_tera_collect_gid(const uint64_t* const* his, const uint32_t* const* rows,
-                          const long* starts, const long* prefix, int S, long n, uint64_t* ohi,
+                          const long* starts, const long* prefix, int S, long n, int pack,
+                          uint64_t vlo, unsigned int m, unsigned int R, int sh, uint64_t* ohi,
                           uint32_t* ogid, hipStream_t st) {
   if (n <= 0) return 0;
-  if (S <= 0 || S > 256) return (int)hipErrorInvalidValue;
+  if (S <= 0 || S > 256 || (!pack && ogid == nullptr) || R < 2 || R > 256 || m + R > 256 ||
+      sh < 0 || sh > 63)
+    return (int)hipErrorInvalidValue;
+  const KeyWindow kw{vlo, m, R, sh};
   const long grid = std::min<long>(ceil_div(n, 256), 256L * 256);
   hipLaunchKernelGGL(tera_collect_gid_kernel, dim3((unsigned)grid), dim3(256), 0, st, his, rows,
-                     starts, prefix, S, n, ohi, ogid);
+                     starts, prefix, S, n, pack, kw, ohi, ogid);
   return (int)hipGetLastError();
 }
 
-int hbmr_gather_records_gid(const void* const* bases, const uint32_t* gid, long n,
-                            int record_bytes, void* dst, uint64_t* hi, uint64_t* lo,
+// gid: the record ids (split << 24 | row), or nullptr and packed: sorted keys
+// whose low 32 bits are the ids (hi may be packed itself: each record's id is
+// read before its key is written over it, by the same lanes)
+int hbmr_gather_records_gid(const void* const* bases, const uint32_t* gid, const uint64_t* packed,
+                            long n, int record_bytes, void* dst, uint64_t* hi, uint64_t* lo,
                             hipStream_t st) {
   if (n <= 0) return 0;
-  if (record_bytes % 4 || record_bytes > 4 * 64) return (int)hipErrorInvalidValue;
+  if (record_bytes % 4 || record_bytes > 4 * 64 || (gid == nullptr) == (packed == nullptr))
+    return (int)hipErrorInvalidValue;
   if ((hi == nullptr) != (lo == nullptr) || (hi != nullptr && record_bytes < 12))
     return (int)hipErrorInvalidValue;
   const int words = record_bytes / 4;
-  // HBMR_GATHER=u8 / nt / u8nt: 8 records in flight per lane and/or streamed
-  // (non-temporal) stores of the gathered records, for A/B
-  static const int mode = [] {
-    const char* e = getenv("HBMR_GATHER");
-    if (!e) return 0;
-    const std::string m(e);
-    return (m.find("u8") != std::string::npos ? 1 : 0) | (m.find("nt") != std::string::npos ? 2 : 0);
-  }();
-  const int U = (mode & 1) ? 8 : 4;
-  // HBMR_GATHER=w1...: the word-per-lane kernel (round 3-4) for A/B
-  static const bool word_lanes = [] {
-    const char* e = getenv("HBMR_GATHER");
-    return e && std::string(e).find("w1") != std::string::npos;
-  }();
-  if (!word_lanes && words >= 3) {
-    auto k16 = mode == 0 ? gather_records_gid16_kernel<4, false>
-             : mode == 1 ? gather_records_gid16_kernel<8, false>
-             : mode == 2 ? gather_records_gid16_kernel<4, true>
-                         : gather_records_gid16_kernel<8, true>;
+  constexpr int U = 4;
+  if (words >= 3) {
     const long rpb = (long)(HBMR_WAVE / ((words + 3) / 4)) * (256 / HBMR_WAVE);
     const long grid16 = std::min<long>(ceil_div(n, rpb * U), 1L << 18);
-    hipLaunchKernelGGL(k16, dim3((unsigned)grid16), dim3(256), 0, st,
-                       reinterpret_cast<const uint32_t* const*>(bases), gid, n, words,
+    hipLaunchKernelGGL(gather_records_gid16_kernel<U>, dim3((unsigned)grid16), dim3(256), 0, st,
+                       reinterpret_cast<const uint32_t* const*>(bases), gid, packed, n, words,
                        reinterpret_cast<uint32_t*>(dst), reinterpret_cast<uint32_t*>(hi), lo);
     return (int)hipGetLastError();
   }
-  auto kern = mode == 0 ? gather_records_gid_kernel<4, false>
-            : mode == 1 ? gather_records_gid_kernel<8, false>
-            : mode == 2 ? gather_records_gid_kernel<4, true>
-                        : gather_records_gid_kernel<8, true>;
   const long grid = std::min<long>(ceil_div(n, (256 / words) * U), 1L << 18);
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), 0, st,
-                     reinterpret_cast<const uint32_t* const*>(bases), gid, n, words,
+  hipLaunchKernelGGL(gather_records_gid_kernel<U>, dim3((unsigned)grid), dim3(256), 0, st,
+                     reinterpret_cast<const uint32_t* const*>(bases), gid, packed, n, words,
                      reinterpret_cast<uint32_t*>(dst), reinterpret_cast<uint32_t*>(hi), lo);
   return (int)hipGetLastError();
 }
 
-int hbmr_tera_tie_fix_records(uint64_t* hi, uint64_t* lo, void* rec, long n,
-                              int record_bytes, int shift, unsigned int* flag, hipStream_t st) {
+long hbmr_tera_tie_fix_scratch_bytes(long cap, int record_bytes) {
+  return 16 + cap * (4 + 8 + 8 + (long)record_bytes);
+}
+
+// scratch: hbmr_tera_tie_fix_scratch_bytes(cap, record_bytes) for at most cap
+// moved records (more are flagged)
+// runs: equal key_window(vlo, m, R, sh) of hi (m = 0, R = 256, vlo = 0: hi >> sh)
+int hbmr_tera_tie_fix_records(uint64_t* hi, uint64_t* lo, void* rec, long n, int record_bytes,
+                              uint64_t vlo, unsigned int m, unsigned int R, int sh,
+                              unsigned int* flag, void* scratch, long cap, hipStream_t st) {
   if (n <= 1) return 0;
-  if (record_bytes % 4 || record_bytes > 4 * 64 || shift < 0 || shift > 63)
+  if (record_bytes % 4 || record_bytes > 4 * 64 || sh < 0 || sh > 63 || cap < 1 ||
+      n >= (1L << 32) || R < 2 || R > 256 || m + R > 256)
     return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(tera_tie_fix_records_kernel, dim3((unsigned)ceil_div(n - 1, 256)), dim3(256),
-                     0, st, hi, lo, reinterpret_cast<uint32_t*>(rec), n, record_bytes / 4, shift,
-                     flag);
+  const KeyWindow kw{vlo, m, R, sh};
+  char* sc = reinterpret_cast<char*>(scratch);
+  unsigned int* cnt = reinterpret_cast<unsigned int*>(sc);
+  uint64_t* shi = reinterpret_cast<uint64_t*>(sc + 16);
+  uint64_t* slo = shi + cap;
+  uint32_t* sdst = reinterpret_cast<uint32_t*>(slo + cap);
+  uint32_t* srec = sdst + cap;
+  const int words = record_bytes / 4;
+  HBMR_RETURN_IF_ERROR(hipMemsetAsync(cnt, 0, 4, st));
+  hipLaunchKernelGGL(tera_tie_rank_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, hi,
+                     lo, reinterpret_cast<const uint32_t*>(rec), n, words, kw, cap, cnt, sdst,
+                     shi, slo, srec, flag);
+  const long grid = std::min<long>(ceil_div(cap, 256), 4096);
+  hipLaunchKernelGGL(tera_tie_move_kernel, dim3((unsigned)grid), dim3(256), 0, st, hi, lo,
+                     reinterpret_cast<uint32_t*>(rec), words, cap, cnt, sdst, shi, slo, srec);
   return (int)hipGetLastError();
 }
 
@@ -1338,22 +1608,11 @@ int hbmr_gather_records_multi(const void* const* bases, const uint32_t* split, c
   if (n <= 0) return 0;
   if (record_bytes % 4 || record_bytes > 4 * 256) return (int)hipErrorInvalidValue;
   const int words = record_bytes / 4;
-  static const bool v1 = [] {
-    const char* e = getenv("HBMR_GATHER_V1");
-    return e && *e == '1';
-  }();
-  if (v1) {
-    const long grid = std::min<long>(ceil_div(n, 256 / words), 1L << 20);
-    hipLaunchKernelGGL(gather_records_multi_kernel, dim3((unsigned)grid), dim3(256), 0, st,
-                       reinterpret_cast<const uint32_t* const*>(bases), split, row, perm, n, words,
-                       reinterpret_cast<uint32_t*>(dst));
-  } else {
-    constexpr int U = 4;
-    const long grid = std::min<long>(ceil_div(n, (256 / words) * U), 1L << 18);
-    hipLaunchKernelGGL(gather_records_multi_v3_kernel<U>, dim3((unsigned)grid), dim3(256), 0, st,
-                       reinterpret_cast<const uint32_t* const*>(bases), split, row, perm, n, words,
-                       reinterpret_cast<uint32_t*>(dst));
-  }
+  constexpr int U = 4;
+  const long grid = std::min<long>(ceil_div(n, (256 / words) * U), 1L << 18);
+  hipLaunchKernelGGL(gather_records_multi_v3_kernel<U>, dim3((unsigned)grid), dim3(256), 0, st,
+                     reinterpret_cast<const uint32_t* const*>(bases), split, row, perm, n, words,
+                     reinterpret_cast<uint32_t*>(dst));
   return (int)hipGetLastError();
 }
 

@@ -100,6 +100,37 @@ def test_terasort_partition_groups_one_rank(tmp_path, group_bytes, gid):
     assert T.teravalidate(str(out))["misordered"] == 0
 
 
+def test_terasort_in_hbm_redoes_a_flagged_group_on_the_full_key_path(monkeypatch):
+    """In HBM the one-rank reduce reads no flag per group: a group whose tie
+    runs were too long (flag set) is noticed after the last group and the
+    reduce runs again on the full-key path — same validated result."""
+    calls = {"gathered": 0, "full": 0}
+    orig_sg, orig_tc = S.sort_gathered, S.tera_collect
+
+    def sg(*a, **k):
+        calls["gathered"] += 1
+        got = orig_sg(*a, **k)
+        if k.get("defer") and calls["gathered"] == 2:
+            got = got[:3] + (torch.ones(1, dtype=torch.int32),)
+        return got
+
+    def tc(*a, **k):
+        calls["full"] += 1
+        return orig_tc(*a, **k)
+    monkeypatch.setattr(S, "sort_gathered", sg)
+    monkeypatch.setattr(S, "tera_collect", tc)
+    rows = 12000
+    conf = T.terasort_conf(rows=rows, split_rows=2500, partitions=5)
+    conf.set("hbmr.terasort.reduce.group.bytes", str(300_000))
+    with LocalCluster(JobConf(), num_trackers=1, cpu_slots=2) as cl:
+        rj = cl.submit_job(conf)
+        rj.waitForCompletion(120)
+        assert rj.isSuccessful(), rj.getFailureInfo()
+        res = rj._impl.jip.result[0]
+    assert res["unsorted"] == 0 and res["checksum_ok"] and res["records"] == rows
+    assert calls["gathered"] == 5 and calls["full"] == 5
+
+
 @pytest.mark.parametrize("trackers", [1, 2, 3])
 def test_terasort_more_partitions_than_trackers(tmp_path, trackers):
     """R part files for any R (TeraSort.java writes one per reduce): a rank
@@ -186,6 +217,25 @@ def test_gpu_radix_sort_pairs_matches_numpy(n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 1000, 4096, 4097, 100003, 3 << 20])
+@pytest.mark.parametrize("window", [(32, 64), (0, 64), (3, 29), (40, 41)])
+def test_gpu_onesweep_radix_sort_keys_matches_numpy(n, window):
+    """Keys-only onesweep sort (decoupled look-back): the stable numpy order
+    of the window's bits, every tile count and window width (a last digit
+    narrower than 8 bits), and the look-back never timed out."""
+    g = torch.Generator().manual_seed(n + window[0])
+    k = torch.randint(-(1 << 62), 1 << 62, (n,), generator=g, dtype=torch.int64)
+    k[::5] = k[1]   # duplicates: stability matters
+    kd = k.cuda()
+    err = torch.zeros(1, dtype=torch.int32, device="cuda")
+    S.radix_sort_keys(kd, *window, err=err)
+    kc = k.clone()
+    S.radix_sort_keys(kc, *window)     # numpy stable reference
+    assert int(err.item()) == 0
+    assert torch.equal(kd.cpu(), kc)
+
+
+@pytest.mark.gpu
 def test_gpu_sort_records_and_partition():
     recs = S.teragen(0, 300000, device="cuda")
     srt, hs, ls = S.sort_records(recs)
@@ -268,8 +318,9 @@ def test_gpu_tera_partition_matches_cpu():
     recs_c = torch.from_numpy(S.teragen_cpu(4242, n))
     sp = T.create_partitions(recs_c.numpy()[::89, :10].copy(), 29)
     shi, slo = (torch.from_numpy(x.view(np.int64)) for x in T._key_words(sp))
-    hg, lg, rg, og = S.tera_partition(recs_c.cuda(), shi, slo)
-    hc, lc, rc, oc = S.tera_partition(recs_c, shi, slo)
+    hg, lg, rg, og, kg = S.tera_partition(recs_c.cuda(), shi, slo, kbytes=True)
+    hc, lc, rc, oc, kc = S.tera_partition(recs_c, shi, slo, kbytes=True)
+    assert kg.cpu().tolist() == kc.tolist()
     assert torch.equal(og.cpu(), oc)
     hg, lg, rg = hg.cpu(), lg.cpu(), rg.cpu()
     for p in range(29):
@@ -354,16 +405,19 @@ def test_gpu_merge_runs_matches_cpu(sizes):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("packed", [False, True])
 @pytest.mark.parametrize("window", [None, "full", "narrow"])
 @pytest.mark.parametrize("ties", [0, 5, 100, "prefix"])
-def test_gpu_sort_gathered_packed_ids(ties, window):
+def test_gpu_sort_gathered_packed_ids(ties, window, packed):
     """Reduce v4 (hi + packed-id sort, one gather, lo from the gathered records,
     in-place tie fix-up): the records of three map outputs come out in key
     order; ties = equal 8-byte prefixes per run (100: longer than the fix-up
     handles -> None, the caller's full-key path).  window: the group's hi
     bounds given (full range, or every key under one top byte), so the radix
     passes cover only the SORT_BITS below the common prefix and the tie fix-up
-    orders the longer equal-prefix runs."""
+    orders the longer equal-prefix runs.  packed: the key alphabet from the
+    maps and the group's bounds given, so the packed-key onesweep path runs
+    (dense 32-bit window over base-R digits, window ties fixed in place)."""
     parts_c = [torch.from_numpy(S.teragen_cpu(1000 * i, 20_000 + i)) for i in range(3)]
     hi_range = {None: None, "full": (0, (1 << 64) - 1),
                 "narrow": (0x5A << 56, (0x5B << 56) - 1)}[window]
@@ -382,11 +436,20 @@ def test_gpu_sort_gathered_packed_ids(ties, window):
                 p[k * 8:(k + 1) * 8, :8] = p[k * 8, :8]
     parts = [p.cuda() for p in parts_c]
     outs = [S.tera_partition(p, torch.zeros(0, dtype=torch.int64),
-                             torch.zeros(0, dtype=torch.int64)) for p in parts]
+                             torch.zeros(0, dtype=torch.int64), kbytes=True) for p in parts]
     his = [o[0] for o in outs]
     rows = [o[2] for o in outs]
     lens = [p.shape[0] for p in parts]
-    got = S.sort_gathered(his, rows, [0, 0, 0], lens, parts, hi_range=hi_range)
+    kw = {}
+    if packed:
+        orb = 0
+        for o in outs:
+            orb |= int(o[4][0])
+        assert orb == int(np.bitwise_or.reduce(torch.cat(parts_c)[:, :8].numpy(), axis=None))
+        hall = torch.cat(his).cpu().numpy().view(np.uint64)
+        bounds = (int(hall.min()), int(hall.max())) if window == "narrow" else (None, None)
+        kw = {"alphabet": (0, 1 << orb.bit_length()), "bounds": bounds}
+    got = S.sort_gathered(his, rows, [0, 0, 0], lens, parts, hi_range=hi_range, **kw)
     if ties == 100:
         assert got is None
         return
