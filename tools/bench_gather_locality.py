@@ -23,26 +23,38 @@ def main():
     bases = [torch.empty(rows, 100, dtype=torch.uint8, device=dev) for _ in range(nsplits)]
     g = torch.Generator(device=dev).manual_seed(0)
     out = {}
-    for span in (1, 2, 10, 100):     # splits the sources come from (x 1 GB)
-        s = torch.randint(0, span, (n,), device=dev, generator=g, dtype=torch.int64)
+    from hbmr.ops import _lib
+    lib = _lib.load()
+    for u in (1, 2, 4, 8):
+        lib.hbmr_gather_set_unroll(u)
+        s = torch.randint(0, nsplits, (n,), device=dev, generator=g, dtype=torch.int64)
         r = torch.randint(0, rows, (n,), device=dev, generator=g, dtype=torch.int64)
         gid = ((s << 24) | r).to(torch.int32)
-        order = torch.randperm(n, device=dev, generator=g).to(torch.int64)
-        for mode in ("gid", "order"):
-            ts = []
-            for rep in range(6):
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-                if mode == "gid":
-                    S.gather_records_gid(bases, gid)
-                else:
-                    S.gather_records_gid(bases, gid, order=order)
-                torch.cuda.synchronize()
-                if rep:
-                    ts.append(time.perf_counter() - t0)
-            ms = 1e3 * sorted(ts)[len(ts) // 2]
-            out[f"{span}GB_{mode}"] = {"ms": round(ms, 3), "GBps": round(2 * n * 100 / ms / 1e6, 1)}
-        print(json.dumps(out), flush=True)
+        ts = []
+        for rep in range(6):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            S.gather_records_gid(bases, gid)
+            torch.cuda.synchronize()
+            if rep:
+                ts.append(time.perf_counter() - t0)
+        ms = 1e3 * sorted(ts)[len(ts) // 2]
+        out[f"unroll{u}"] = {"ms": round(ms, 3), "GBps": round(2 * n * 100 / ms / 1e6, 1)}
+    lib.hbmr_gather_set_unroll(-1)
+    # a plain streaming copy of the same bytes, for the ceiling
+    src = bases[0][:n]
+    dstb = torch.empty_like(src)
+    ts = []
+    for rep in range(6):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dstb.copy_(src)
+        torch.cuda.synchronize()
+        if rep:
+            ts.append(time.perf_counter() - t0)
+    ms = 1e3 * sorted(ts)[len(ts) // 2]
+    out["copy_same_bytes"] = {"ms": round(ms, 3), "GBps": round(2 * n * 100 / ms / 1e6, 1)}
+    print(json.dumps(out), flush=True)
     return 0
 
 
