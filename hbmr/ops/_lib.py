@@ -128,6 +128,7 @@ _SIGS = {
                                         c_void_p, c_void_p, c_void_p]),
     "hbmr_tera_group_stats": (c_int, [c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p,
                                       c_void_p]),
+    "hbmr_radix_set_onesweep_waves": (c_int, [c_int]),
     "hbmr_gather_set_unroll": (c_int, [c_int]),
     "hbmr_tera_tie_fix_scratch_bytes": (c_long, [c_long, c_int]),
     "hbmr_tera_tie_fix_records": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_int, c_uint64,

@@ -392,6 +392,25 @@ def tera_keys_part(records: torch.Tensor, split_hi: torch.Tensor, split_lo: torc
     return hi, lo, torch.from_numpy(pid)
 
 
+_SPLITTERS_DEV: dict = {}
+
+
+def _splitters_on(dev, split_hi, split_lo):
+    """(hi, lo) of a job's splitters on ``dev``, uploaded once per splitter
+    set (every map of a job partitions by the same ones)."""
+    if split_hi.device == dev:
+        return split_hi, split_lo
+    hb = split_hi.numpy().tobytes()
+    key = (str(dev), hb, split_lo.numpy().tobytes())
+    got = _SPLITTERS_DEV.get(key)
+    if got is None:
+        if len(_SPLITTERS_DEV) > 16:
+            _SPLITTERS_DEV.clear()
+        got = _SPLITTERS_DEV[key] = tuple(
+            t.pin_memory().to(dev, non_blocking=True) for t in (split_hi, split_lo))
+    return got
+
+
 def tera_partition(records: torch.Tensor, split_hi: torch.Tensor, split_lo: torch.Tensor,
                    stream=None, kbytes=False):
     """Range-partition a split: (hi, lo, row, offsets) — key words and record
@@ -426,8 +445,7 @@ def tera_partition(records: torch.Tensor, split_hi: torch.Tensor, split_lo: torc
     offs = torch.empty(nparts + 1, dtype=torch.int64, device=dev)
     wsb = int(lib.hbmr_tera_partition_workspace_bytes(n, nparts))
     ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
-    sh = split_hi if split_hi.device == dev else split_hi.pin_memory().to(dev, non_blocking=True)
-    sl = split_lo if split_lo.device == dev else split_lo.pin_memory().to(dev, non_blocking=True)
+    sh, sl = _splitters_on(dev, split_hi, split_lo)
     kmm = torch.zeros(2, dtype=torch.int64, device=dev) if kbytes else None
     rc = lib.hbmr_tera_partition(_ptr(records), n, stride, _ptr(sh) if ns else None,
                                  _ptr(sl) if ns else None, ns, _ptr(hi), _ptr(lo), _ptr(row),

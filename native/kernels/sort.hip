@@ -277,25 +277,31 @@ __global__ __launch_bounds__(kSortThreads) void radix_bases_kernel(uint32_t* __r
   h[threadIdx.x] = e;
 }
 
-__global__ __launch_bounds__(kSortThreads) void radix_onesweep_kernel(
+// WAVES waves of 64 lanes, 16 keys per lane: a tile of WAVES·1024 keys.  More
+// keys per tile make longer digit runs for the scatter's writes (8 waves:
+// 32 keys = 256 B per digit on average) and fewer look-backs.
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void radix_onesweep_kernel(
     const uint64_t* __restrict__ kin, uint64_t* __restrict__ kout, long n, int shift,
     uint32_t dmask, const uint32_t* __restrict__ gbase, uint64_t* __restrict__ status,
     uint64_t epoch, uint32_t* __restrict__ ticket, uint32_t* __restrict__ err) {
-  __shared__ uint64_t s_k[kSortTile];
-  __shared__ uint32_t s_wh[kSortWaves][kRadix];
+  constexpr int kThreads = WAVES * 64;
+  constexpr int kTile = kThreads * kSortItems;
+  constexpr int kWaveSpan = kSortItems * 64;
+  static_assert(WAVES >= 4, "one thread per digit");
+  __shared__ uint64_t s_k[kTile];
+  __shared__ uint32_t s_wh[WAVES][kRadix];
+  __shared__ uint32_t s_cnt[kRadix];
   __shared__ uint32_t s_toff[kRadix];
   __shared__ uint32_t s_g[kRadix];
-  __shared__ uint32_t s_w[4];
   __shared__ uint32_t s_tile;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   if (t == 0) s_tile = atomicAdd(ticket, 1u);
-#pragma unroll
-  for (int i = 0; i < kSortWaves; ++i) s_wh[i][t] = 0u;
+  for (int i = t; i < WAVES * kRadix; i += kThreads) (&s_wh[0][0])[i] = 0u;
   __syncthreads();
   const long tile = s_tile;
-  const long base = tile * kSortTile;
-  const int tile_n = (int)min((long)kSortTile, n - base);
-  constexpr int kWaveSpan = kSortTile / kSortWaves;
+  const long base = tile * kTile;
+  const int tile_n = (int)min((long)kTile, n - base);
   uint64_t k[kSortItems];
   const long wbase = base + (long)w * kWaveSpan;
 #pragma unroll
@@ -324,14 +330,11 @@ __global__ __launch_bounds__(kSortThreads) void radix_onesweep_kernel(
     __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
-  {
+  if (t < kRadix) {
     // thread t = digit t: publish the tile's count, look back for its prefix
-    uint32_t c[kSortWaves], cnt = 0;
+    uint32_t cnt = 0;
 #pragma unroll
-    for (int i = 0; i < kSortWaves; ++i) {
-      c[i] = s_wh[i][t];
-      cnt += c[i];
-    }
+    for (int i = 0; i < WAVES; ++i) cnt += s_wh[i][t];
     uint64_t* st = status + tile * kRadix + t;
     const uint64_t ep = epoch << 48;
     uint32_t excl = 0;
@@ -358,13 +361,35 @@ __global__ __launch_bounds__(kSortThreads) void radix_onesweep_kernel(
                          __HIP_MEMORY_SCOPE_AGENT);
     }
     s_g[t] = gbase[t] + excl;
-    const uint32_t toff = block_excl_scan256(cnt, s_w);
-    s_toff[t] = toff;
-    uint32_t run = toff;
+    s_cnt[t] = cnt;
+  }
+  __syncthreads();
+  if (w == 0) {
+    // the tile's digit offsets: exclusive scan of 256 counts, 4 per lane
+    const uint32_t a0 = s_cnt[4 * lane], a1 = s_cnt[4 * lane + 1], a2 = s_cnt[4 * lane + 2],
+                   a3 = s_cnt[4 * lane + 3];
+    const uint32_t sum = a0 + a1 + a2 + a3;
+    uint32_t x = sum;
 #pragma unroll
-    for (int i = 0; i < kSortWaves; ++i) {
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(x, o);
+      if (lane >= o) x += u;
+    }
+    const uint32_t e0 = x - sum;
+    s_toff[4 * lane] = e0;
+    s_toff[4 * lane + 1] = e0 + a0;
+    s_toff[4 * lane + 2] = e0 + a0 + a1;
+    s_toff[4 * lane + 3] = e0 + a0 + a1 + a2;
+  }
+  __syncthreads();
+  if (t < kRadix) {
+    // each wave's start inside the digit's run
+    uint32_t run = s_toff[t];
+#pragma unroll
+    for (int i = 0; i < WAVES; ++i) {
+      const uint32_t c = s_wh[i][t];
       s_wh[i][t] = run;
-      run += c[i];
+      run += c;
     }
   }
   __syncthreads();
@@ -374,7 +399,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_onesweep_kernel(
       s_k[s_wh[w][((uint32_t)(k[i] >> shift) & dmask)] + rank[i]] = k[i];
   }
   __syncthreads();
-  for (int j = t; j < tile_n; j += kSortThreads) {
+  for (int j = t; j < tile_n; j += kThreads) {
     const uint64_t key = s_k[j];
     const uint32_t d = ((uint32_t)(key >> shift) & dmask);
     kout[(long)s_g[d] + (j - (long)s_toff[d])] = key;
@@ -869,9 +894,15 @@ __global__ __launch_bounds__(256) void tera_part_count_w_kernel(
     const uint64_t* __restrict__ slo, int nsplit, uint64_t* __restrict__ hi,
     uint64_t* __restrict__ lo, uint16_t* __restrict__ pid, unsigned int* __restrict__ counts,
     unsigned long long* __restrict__ kmm) {
-  __shared__ uint64_t s_hi[kMaxSplitters];
-  __shared__ uint16_t s_lo[kMaxSplitters];
-  __shared__ unsigned int s_cnt[kMaxSplitters + 1];
+  // LDS sized by the splitter count (part_count_w_lds), not a static
+  // 4096-entry table (56 KB: two workgroups per CU).  The kernel reads about
+  // every sector of the records (a 12-byte key every 100 bytes), so it runs
+  // near the copy rate; a 12-bit prefix table that spared 98 % of the
+  // splitter searches measured no faster.
+  extern __shared__ __align__(16) unsigned char s_dyn[];
+  uint64_t* s_hi = reinterpret_cast<uint64_t*>(s_dyn);
+  unsigned int* s_cnt = reinterpret_cast<unsigned int*>(s_hi + nsplit);
+  uint16_t* s_lo = reinterpret_cast<uint16_t*>(s_cnt + nsplit + 1);
   __shared__ unsigned long long s_ks[2];
   uint32_t korb = 0u;
   uint64_t ksum = 0;
@@ -1252,6 +1283,7 @@ __global__ __launch_bounds__(256) void tera_tie_move_kernel(
 
 inline long ceil_div(long a, long b) { return (a + b - 1) / b; }
 
+int g_onesweep_waves = 8;  // waves per onesweep tile (hbmr_radix_set_onesweep_waves, A/B)
 int g_gather_unroll = 2;   // records in flight per lane group (hbmr_gather_set_unroll, A/B)
 
 }  // namespace
@@ -1303,7 +1335,7 @@ long hbmr_radix_onesweep_workspace_bytes(long n) {
 }
 
 long hbmr_radix_onesweep_status_bytes(long n) {
-  return std::max(1L, ceil_div(n, kSortTile)) * kRadix * 8;
+  return std::max(1L, ceil_div(n, kSortTile)) * kRadix * 8;   // tiles of >= 4096 keys
 }
 
 // Sort uint64 keys by bits [begin_bit, end_bit) (8-bit digits, LSD, stable),
@@ -1335,16 +1367,28 @@ int hbmr_radix_sort_keys_u64(uint64_t* keys, uint64_t* tkeys, long n, int begin_
   hipLaunchKernelGGL(radix_bases_kernel, dim3((unsigned)passes), dim3(kSortThreads), 0, st, ghist);
   uint64_t* ka = keys;
   uint64_t* kb = tkeys;
+  const int waves = g_onesweep_waves;
+  const long tiles = ceil_div(n, (long)waves * 64 * kSortItems);
   for (int p = 0; p < passes; ++p) {
     if (*epoch == 0 || *epoch >= 0xFFFFu) {
       HBMR_RETURN_IF_ERROR(hipMemsetAsync(status, 0, status_bytes, st));
       *epoch = 0;
     }
     const uint64_t ep = ++*epoch;
-    hipLaunchKernelGGL(radix_onesweep_kernel, dim3((unsigned)ntiles), dim3(kSortThreads), 0, st,
-                       ka, kb, n, begin_bit + 8 * p,
-                       (1u << std::min(8, end_bit - begin_bit - 8 * p)) - 1u, ghist + p * kRadix,
-                       reinterpret_cast<uint64_t*>(status), ep, tickets + p, err);
+    const int sh = begin_bit + 8 * p;
+    const uint32_t dm = (1u << std::min(8, end_bit - begin_bit - 8 * p)) - 1u;
+    if (waves == 16)
+      hipLaunchKernelGGL(radix_onesweep_kernel<16>, dim3((unsigned)tiles), dim3(1024), 0, st, ka,
+                         kb, n, sh, dm, ghist + p * kRadix, reinterpret_cast<uint64_t*>(status),
+                         ep, tickets + p, err);
+    else if (waves == 8)
+      hipLaunchKernelGGL(radix_onesweep_kernel<8>, dim3((unsigned)tiles), dim3(512), 0, st, ka, kb,
+                         n, sh, dm, ghist + p * kRadix, reinterpret_cast<uint64_t*>(status), ep,
+                         tickets + p, err);
+    else
+      hipLaunchKernelGGL(radix_onesweep_kernel<4>, dim3((unsigned)tiles), dim3(256), 0, st, ka, kb,
+                         n, sh, dm, ghist + p * kRadix, reinterpret_cast<uint64_t*>(status), ep,
+                         tickets + p, err);
     std::swap(ka, kb);
   }
   if ((passes & 1) && copy_back)
@@ -1455,6 +1499,10 @@ int hbmr_tera_collect(const uint64_t* const* his, const uint64_t* const* los,
 // of hbmr_tera_partition_workspace_bytes(n, nparts) bytes.
 constexpr long kPartGridMax = 256L * 64;
 
+inline size_t part_count_w_lds(int nsplit) {
+  return (size_t)nsplit * 8 + (size_t)(nsplit + 1) * 4 + (size_t)nsplit * 2 + 16;
+}
+
 long hbmr_tera_partition_workspace_bytes(long n, int nparts) {
   return n * 8 * 2 + n * 2 + 2L * (nparts + 1) * 4 + 64 + kPartGridMax * 16;
 }
@@ -1486,7 +1534,8 @@ int hbmr_tera_partition(const void* records, long n, int stride, const uint64_t*
     const long grid = std::min<long>(ceil_div(n, 256), kPartGridMax);
     unsigned long long* kp = kmm != nullptr ? kparts : nullptr;
     if (words)
-      hipLaunchKernelGGL(tera_part_count_w_kernel, dim3((unsigned)grid), dim3(256), 0, st,
+      hipLaunchKernelGGL(tera_part_count_w_kernel, dim3((unsigned)grid), dim3(256),
+                         part_count_w_lds(nsplit), st,
                          reinterpret_cast<const uint32_t*>(records), n, stride / 4, shi, slo,
                          nsplit, hi, lo, pid, counts, kp);
     else
@@ -1574,6 +1623,16 @@ int hbmr_gather_records_gid(const void* const* bases, const uint32_t* gid, const
                      reinterpret_cast<const uint32_t* const*>(bases), gid, packed, n, words,
                      reinterpret_cast<uint32_t*>(dst), reinterpret_cast<uint32_t*>(hi), lo);
   return (int)hipGetLastError();
+}
+
+// waves per onesweep scatter tile: 4 (4096 keys), 8 (default: 80M keys in
+// 2.02 ms against 2.54 for 4 — longer digit runs per write, fewer look-backs)
+// or 16 (1.98 ms, one workgroup per CU);
+// returns the previous setting
+int hbmr_radix_set_onesweep_waves(int w) {
+  const int old = g_onesweep_waves;
+  g_onesweep_waves = w == 4 || w == 16 ? w : 8;
+  return old;
 }
 
 // records each lane group of the packed-id gather keeps in flight: 1, 2

@@ -217,9 +217,10 @@ def test_gpu_radix_sort_pairs_matches_numpy(n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [2, 1000, 4096, 4097, 100003, 3 << 20])
+@pytest.mark.parametrize("waves", [4, 8, 16])
+@pytest.mark.parametrize("n", [2, 1000, 4096, 4097, 16385, 100003, 3 << 20])
 @pytest.mark.parametrize("window", [(32, 64), (0, 64), (3, 29), (40, 41)])
-def test_gpu_onesweep_radix_sort_keys_matches_numpy(n, window):
+def test_gpu_onesweep_radix_sort_keys_matches_numpy(n, window, waves):
     """Keys-only onesweep sort (decoupled look-back): the stable numpy order
     of the window's bits, every tile count and window width (a last digit
     narrower than 8 bits), and the look-back never timed out."""
@@ -228,7 +229,12 @@ def test_gpu_onesweep_radix_sort_keys_matches_numpy(n, window):
     k[::5] = k[1]   # duplicates: stability matters
     kd = k.cuda()
     err = torch.zeros(1, dtype=torch.int32, device="cuda")
-    S.radix_sort_keys(kd, *window, err=err)
+    from hbmr.ops import _lib
+    old = _lib.load().hbmr_radix_set_onesweep_waves(waves)
+    try:
+        S.radix_sort_keys(kd, *window, err=err)
+    finally:
+        _lib.load().hbmr_radix_set_onesweep_waves(old)
     kc = k.clone()
     S.radix_sort_keys(kc, *window)     # numpy stable reference
     assert int(err.item()) == 0

@@ -73,8 +73,18 @@ def main():
     def tsort():
         kk = packed.clone()
         return lambda: torch.sort(kk)
+    from hbmr.ops import _lib
+    lib = _lib.load()
     out["ms_pairs_40bit_5pass"] = timeit(pairs)
-    out["ms_onesweep_keys_32bit_4pass"] = timeit(onesweep)
+    for wv in (4, 8, 16):
+        lib.hbmr_radix_set_onesweep_waves(wv)
+        x = k.clone()
+        S.radix_sort_keys(x, 32, 64)
+        kh = k.cpu().numpy().view(np.uint64)
+        order = np.argsort(kh >> np.uint64(32), kind="stable")
+        out[f"check_waves{wv}"] = bool((x.cpu().numpy().view(np.uint64) == kh[order]).all())
+        out[f"ms_onesweep_keys_32bit_4pass_waves{wv}"] = timeit(onesweep)
+    lib.hbmr_radix_set_onesweep_waves(-1)
     out["ms_torch_sort_64bit"] = timeit(tsort)
     print(json.dumps(out), flush=True)
     return 0
