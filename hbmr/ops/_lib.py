@@ -125,15 +125,15 @@ _SIGS = {
                                       c_int, c_uint64, c_uint, c_uint, c_int, c_void_p, c_void_p,
                                       c_void_p]),
     "hbmr_gather_records_gid": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p,
-                                        c_void_p, c_void_p, c_void_p]),
+                                        c_void_p, c_void_p, c_void_p, c_void_p]),
     "hbmr_tera_group_stats": (c_int, [c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p,
                                       c_void_p]),
     "hbmr_radix_set_onesweep_waves": (c_int, [c_int]),
     "hbmr_gather_set_unroll": (c_int, [c_int]),
     "hbmr_tera_tie_fix_scratch_bytes": (c_long, [c_long, c_int]),
     "hbmr_tera_tie_fix_records": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_int, c_uint64,
-                                          c_uint, c_uint, c_int, c_void_p, c_void_p, c_long,
-                                          c_void_p]),
+                                          c_uint, c_uint, c_int, c_void_p, c_void_p, c_void_p,
+                                          c_long, c_void_p]),
     "hbmr_merge_path": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p,
                                 c_long, c_void_p, c_void_p, c_void_p, c_void_p]),
     "hbmr_tera_tie_fix": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_void_p, c_void_p]),

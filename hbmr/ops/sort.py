@@ -662,13 +662,15 @@ def tera_collect_gid(his, rows, starts, lens, stream=None, window: KeyWindow | N
     return ohi, gid
 
 
-def gather_records_gid(bases, gid: torch.Tensor, stream=None, keys=None) -> torch.Tensor:
+def gather_records_gid(bases, gid: torch.Tensor, stream=None, keys=None,
+                       win: torch.Tensor | None = None) -> torch.Tensor:
     """out[i] = bases[g >> 24][g & 0xFFFFFF] (100-byte records) with g =
     gid[i]: int32 ids, or int64 packed keys whose low 32 bits are the ids.
     ``keys`` = (hi, lo) int64 [n] tensors also receive the gathered records'
     keys (as tera_keys would read them back), on the GPU in the same pass; hi
     may be the packed keys themselves (each record's id is read before its
-    key is written over it)."""
+    key is written over it).  ``win`` (int32 [n], packed ids only) receives
+    each record's sort window (the packed key's high half) for the tie fix."""
     n = gid.numel()
     rb = bases[0].shape[1]
     packed = gid.dtype == torch.int64
@@ -690,7 +692,8 @@ def gather_records_gid(bases, gid: torch.Tensor, stream=None, keys=None) -> torc
     kh, kl = keys if keys is not None else (None, None)
     rc = _lib.load().hbmr_gather_records_gid(_ptr(tb), None if packed else _ptr(gid),
                                               _ptr(gid) if packed else None, n, rb, _ptr(res),
-                                              _ptr(kh), _ptr(kl), _lib.stream_handle(stream))
+                                              _ptr(kh), _ptr(kl), _ptr(win),
+                                              _lib.stream_handle(stream))
     _lib.check(rc, "hbmr_gather_records_gid")
     return res
 
@@ -738,10 +741,12 @@ def sort_gathered(his, rows, starts, lens, bases, stream=None, hi_range=None, de
         h, _ = tera_collect_gid(his, rows, starts, lens, stream=stream, window=kw)
         radix_sort_keys(h, 32, 64, stream=stream)
         lo = torch.empty_like(h)
+        win = torch.empty(n, dtype=torch.int32, device=h.device) if _on_gpu(h) else None
         # each record's id is read from its packed word before the gather
-        # writes the record's full hi key over it
-        recs = gather_records_gid(bases, h, stream=stream, keys=(h, lo))
+        # writes the record's full hi key over it (and its window into win)
+        recs = gather_records_gid(bases, h, stream=stream, keys=(h, lo), win=win)
     else:
+        win = None
         h, gid = tera_collect_gid(his, rows, starts, lens, stream=stream)
         radix_sort_pairs(h, gid, begin, end, stream=stream)
         # the sorted keys come with the gather (lo is new; h is rewritten with
@@ -764,7 +769,7 @@ def sort_gathered(his, rows, starts, lens, bases, stream=None, hi_range=None, de
                           dtype=torch.uint8, device=recs.device)
     rc = lib.hbmr_tera_tie_fix_records(_ptr(h), _ptr(lo), _ptr(recs), recs.shape[0],
                                        recs.shape[1], kw.vlo & 0xFFFFFFFFFFFFFFFF, kw.m, kw.R,
-                                       kw.sh, _ptr(flag), _ptr(scratch), cap,
+                                       kw.sh, _ptr(win), _ptr(flag), _ptr(scratch), cap,
                                        _lib.stream_handle(stream))
     _lib.check(rc, "hbmr_tera_tie_fix_records")
     if defer:

@@ -142,7 +142,7 @@ int hbmr_tera_collect_gid(const uint64_t* const* his, const uint32_t* const* row
                           uint32_t* ogid, hipStream_t st);
 int hbmr_gather_records_gid(const void* const* bases, const uint32_t* gid, const uint64_t* packed,
                             long n, int record_bytes, void* dst, uint64_t* hi, uint64_t* lo,
-                            hipStream_t st);
+                            uint32_t* win, hipStream_t st);
 long hbmr_radix_onesweep_workspace_bytes(long n);
 long hbmr_radix_onesweep_status_bytes(long n);
 int hbmr_radix_sort_keys_u64(uint64_t* keys, uint64_t* tkeys, long n, int begin_bit, int end_bit,
@@ -153,7 +153,8 @@ int hbmr_tera_group_stats(const uint64_t* hi, const uint64_t* lo, long n, const 
                           const uint64_t* pl, unsigned long long* acc, hipStream_t st);
 int hbmr_tera_tie_fix_records(uint64_t* hi, uint64_t* lo, void* rec, long n, int record_bytes,
                               uint64_t vlo, unsigned int m, unsigned int R, int sh,
-                              unsigned int* flag, void* scratch, long cap, hipStream_t st);
+                              const uint32_t* win, unsigned int* flag, void* scratch, long cap,
+                              hipStream_t st);
 int hbmr_merge_path(const uint64_t* ahi, const uint64_t* alo, const uint32_t* av, long na,
                     const uint64_t* bhi, const uint64_t* blo, const uint32_t* bv, long nb,
                     uint64_t* ohi, uint64_t* olo, uint32_t* ov, hipStream_t st);

@@ -1098,7 +1098,7 @@ __global__ __launch_bounds__(256) void gather_records_gid_kernel(
     const uint32_t* const* __restrict__ bases, const uint32_t* __restrict__ gid,
     const uint64_t* packed, long n,
     int words, uint32_t* __restrict__ dst, uint32_t* __restrict__ khi,
-    uint64_t* __restrict__ klo) {
+    uint64_t* __restrict__ klo, uint32_t* __restrict__ kwin) {
   const int rpb = 256 / words;
   const int t = threadIdx.x;
   if (t >= rpb * words) return;
@@ -1158,7 +1158,7 @@ __global__ __launch_bounds__(256) void gather_records_gid16_kernel(
     const uint32_t* const* __restrict__ bases, const uint32_t* __restrict__ gid,
     const uint64_t* packed, long n,
     int words, uint32_t* __restrict__ dst, uint32_t* __restrict__ khi,
-    uint64_t* __restrict__ klo) {
+    uint64_t* __restrict__ klo, uint32_t* __restrict__ kwin) {
   const int L = (words + 3) >> 2;            // lanes per record
   const int rpw = HBMR_WAVE / L;             // records per wave
   const int lane = threadIdx.x & (HBMR_WAVE - 1), wave = threadIdx.x / HBMR_WAVE;
@@ -1171,12 +1171,21 @@ __global__ __launch_bounds__(256) void gather_records_gid16_kernel(
   const long stride = (long)gridDim.x * rpb;
   for (long r0 = (long)blockIdx.x * rpb + wave * rpw + lr; r0 < n; r0 += stride * U) {
     const uint32_t* src[U];
+    uint32_t win[U];
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       const long r = r0 + j * stride;
       src[j] = nullptr;
+      win[j] = 0u;
       if (r < n) {
-        const uint32_t g = packed ? (uint32_t)packed[r] : gid[r];
+        uint32_t g;
+        if (packed) {
+          const uint64_t pk = packed[r];
+          g = (uint32_t)pk;
+          win[j] = (uint32_t)(pk >> 32);
+        } else {
+          g = gid[r];
+        }
         src[j] = bases[g >> 24] + (long)(g & 0xFFFFFFu) * words + w0;
       }
     }
@@ -1215,6 +1224,7 @@ __global__ __launch_bounds__(256) void gather_records_gid16_kernel(
         khi[2 * r + 1] = __builtin_bswap32(v[j].x);   // hi = bytes 0-7, big-endian
         khi[2 * r] = __builtin_bswap32(v[j].y);
         klo[r] = ((uint64_t)(v[j].z & 0xFFu) << 8) | ((v[j].z >> 8) & 0xFFu);   // bytes 8-9
+        if (kwin != nullptr) kwin[r] = win[j];    // the sort window, for the tie fix
       }
     }
   }
@@ -1232,20 +1242,23 @@ __global__ __launch_bounds__(256) void gather_records_gid16_kernel(
 // percent of them, in pairs and triples.
 __global__ __launch_bounds__(256) void tera_tie_rank_kernel(
     const uint64_t* __restrict__ hi, const uint64_t* __restrict__ lo,
-    const uint32_t* __restrict__ rec, long n, int words, KeyWindow kw, long cap,
-    unsigned int* __restrict__ cnt, uint32_t* __restrict__ sdst, uint64_t* __restrict__ shi,
-    uint64_t* __restrict__ slo, uint32_t* __restrict__ srec, unsigned int* __restrict__ flag) {
+    const uint32_t* __restrict__ rec, long n, int words, KeyWindow kw,
+    const uint32_t* __restrict__ win, long cap, unsigned int* __restrict__ cnt,
+    uint32_t* __restrict__ sdst, uint64_t* __restrict__ shi, uint64_t* __restrict__ slo,
+    uint32_t* __restrict__ srec, unsigned int* __restrict__ flag) {
   const long j = (long)blockIdx.x * 256 + threadIdx.x;
   if (j >= n) return;
-  const uint64_t hj = hi[j], lj = lo[j], h = key_window(hj, kw);
-  const bool prev = j > 0 && key_window(hi[j - 1], kw) == h;
-  const bool next = j + 1 < n && key_window(hi[j + 1], kw) == h;
+  // the records' windows: as the gather stored them, else recomputed from hi
+  auto wnd = [&](long x) -> uint64_t { return win ? (uint64_t)win[x] : key_window(hi[x], kw); };
+  const uint64_t h = wnd(j);
+  const bool prev = j > 0 && wnd(j - 1) == h;
+  const bool next = j + 1 < n && wnd(j + 1) == h;
   if (!prev && !next) return;
+  const uint64_t hj = hi[j], lj = lo[j];
   long s0 = j, e = j + 1;
-  while (s0 > 0 && key_window(hi[s0 - 1], kw) == h && j - s0 < kTieRun) --s0;
-  while (e < n && key_window(hi[e], kw) == h && e - j < kTieRun) ++e;
-  if ((s0 > 0 && key_window(hi[s0 - 1], kw) == h) || (e < n && key_window(hi[e], kw) == h) ||
-      e - s0 > kTieRun) {
+  while (s0 > 0 && wnd(s0 - 1) == h && j - s0 < kTieRun) --s0;
+  while (e < n && wnd(e) == h && e - j < kTieRun) ++e;
+  if ((s0 > 0 && wnd(s0 - 1) == h) || (e < n && wnd(e) == h) || e - s0 > kTieRun) {
     atomicOr(flag, 1u);
     return;
   }
@@ -1598,7 +1611,7 @@ int hbmr_tera_collect_gid(const uint64_t* const* his, const uint32_t* const* row
 // read before its key is written over it, by the same lanes)
 int hbmr_gather_records_gid(const void* const* bases, const uint32_t* gid, const uint64_t* packed,
                             long n, int record_bytes, void* dst, uint64_t* hi, uint64_t* lo,
-                            hipStream_t st) {
+                            uint32_t* win, hipStream_t st) {
   if (n <= 0) return 0;
   if (record_bytes % 4 || record_bytes > 4 * 64 || (gid == nullptr) == (packed == nullptr))
     return (int)hipErrorInvalidValue;
@@ -1615,13 +1628,15 @@ int hbmr_gather_records_gid(const void* const* bases, const uint32_t* gid, const
            : u == 8 ? gather_records_gid16_kernel<8> : gather_records_gid16_kernel<2>;
     hipLaunchKernelGGL(k, dim3((unsigned)grid16), dim3(256), 0, st,
                        reinterpret_cast<const uint32_t* const*>(bases), gid, packed, n, words,
-                       reinterpret_cast<uint32_t*>(dst), reinterpret_cast<uint32_t*>(hi), lo);
+                       reinterpret_cast<uint32_t*>(dst), reinterpret_cast<uint32_t*>(hi), lo,
+                       packed != nullptr ? win : nullptr);
     return (int)hipGetLastError();
   }
   const long grid = std::min<long>(ceil_div(n, (256 / words) * U), 1L << 18);
   hipLaunchKernelGGL(gather_records_gid_kernel<U>, dim3((unsigned)grid), dim3(256), 0, st,
                      reinterpret_cast<const uint32_t* const*>(bases), gid, packed, n, words,
-                     reinterpret_cast<uint32_t*>(dst), reinterpret_cast<uint32_t*>(hi), lo);
+                     reinterpret_cast<uint32_t*>(dst), reinterpret_cast<uint32_t*>(hi), lo,
+                     nullptr);
   return (int)hipGetLastError();
 }
 
@@ -1651,10 +1666,12 @@ long hbmr_tera_tie_fix_scratch_bytes(long cap, int record_bytes) {
 
 // scratch: hbmr_tera_tie_fix_scratch_bytes(cap, record_bytes) for at most cap
 // moved records (more are flagged)
-// runs: equal key_window(vlo, m, R, sh) of hi (m = 0, R = 256, vlo = 0: hi >> sh)
+// runs: equal key_window(vlo, m, R, sh) of hi (m = 0, R = 256, vlo = 0: hi >> sh),
+// read from win (the gather's copy of each record's window) when given
 int hbmr_tera_tie_fix_records(uint64_t* hi, uint64_t* lo, void* rec, long n, int record_bytes,
                               uint64_t vlo, unsigned int m, unsigned int R, int sh,
-                              unsigned int* flag, void* scratch, long cap, hipStream_t st) {
+                              const uint32_t* win, unsigned int* flag, void* scratch, long cap,
+                              hipStream_t st) {
   if (n <= 1) return 0;
   if (record_bytes % 4 || record_bytes > 4 * 64 || sh < 0 || sh > 63 || cap < 1 ||
       n >= (1L << 32) || R < 2 || R > 256 || m + R > 256)
@@ -1669,7 +1686,7 @@ int hbmr_tera_tie_fix_records(uint64_t* hi, uint64_t* lo, void* rec, long n, int
   const int words = record_bytes / 4;
   HBMR_RETURN_IF_ERROR(hipMemsetAsync(cnt, 0, 4, st));
   hipLaunchKernelGGL(tera_tie_rank_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, st, hi,
-                     lo, reinterpret_cast<const uint32_t*>(rec), n, words, kw, cap, cnt, sdst,
+                     lo, reinterpret_cast<const uint32_t*>(rec), n, words, kw, win, cap, cnt, sdst,
                      shi, slo, srec, flag);
   const long grid = std::min<long>(ceil_div(cap, 256), 4096);
   hipLaunchKernelGGL(tera_tie_move_kernel, dim3((unsigned)grid), dim3(256), 0, st, hi, lo,
