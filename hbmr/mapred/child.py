@@ -263,11 +263,14 @@ class ChildManager:
                     ch.kill(msg)
 
     # -- one attempt ------------------------------------------------------------------------
-    def run_task(self, job_id, conf, payload, reporter, kill_event, progress_cb=None):
+    def run_task(self, job_id, conf, payload, reporter, kill_event, progress_cb=None,
+                 spawn_conf=None):
         """Run one attempt in a child; returns the task's result (map output path or
         None).  Mirrors counters/status/progress into ``reporter`` as they arrive.
-        Raises on failure (ChildDied when the process died or was killed)."""
-        ch = self.acquire(job_id, conf)
+        Raises on failure (ChildDied when the process died or was killed).
+        ``spawn_conf``: the conf a new child starts from (environment, reuse
+        count), if not the task's own (a pool shared by several jobs)."""
+        ch = self.acquire(job_id, spawn_conf if spawn_conf is not None else conf)
         ch.busy_attempt = payload["attempt_id"]
         key = "mapred.job.map.memory.mb" if payload["is_map"] else "mapred.job.reduce.memory.mb"
         ch.memory_limit_mb = max(0, conf.get_int(key, -1))

@@ -74,6 +74,57 @@ class _LocalJob(_Waitable):
         return list(self.map_reports if is_map else self.reduce_reports)
 
 
+_POOLS: dict = {}
+_POOLS_LOCK = threading.Lock()
+
+
+def _local_children(job):
+    """A warm pool of child processes shared by this process's local jobs
+    (the LocalJobRunner's parallel maps, ``mapred.task.isolation=process``):
+    children are started once and kept across jobs with the same child
+    environment — each task carries its own conf and work directory — and
+    leave after ``hbmr.task.child.idle.ms`` idle.  Starting 8 interpreters per
+    job cost more than the maps of a 64 MB WordCount (219 MB/s with 8 map
+    processes against 509 serial in round 5).  Returns (manager, pool key)."""
+    from .child import ChildManager
+    from .jobconf import JobConf
+    env = (job.get("mapred.child.env") or "", job.get_int("mapred.child.ulimit", 0))
+    key = f"local:{hash(env) & 0xFFFFFFFF:08x}"
+    with _POOLS_LOCK:
+        mgr = _POOLS.get(key)
+        if mgr is None:
+            conf = JobConf()
+            conf.set("mapred.child.env", env[0])
+            conf.set_int("mapred.child.ulimit", env[1])
+            conf.set_int("mapred.job.reuse.jvm.num.tasks", -1)
+            conf.set_int("hbmr.task.child.idle.ms", job.get_int("hbmr.task.child.idle.ms", 5000))
+            mgr = _POOLS[key] = (ChildManager("local-pool", tempfile.mkdtemp(prefix="hbmr-lpool-"),
+                                              conf), conf)
+            if len(_POOLS) == 1:
+                import atexit
+                atexit.register(_shutdown_pools)
+    return _PooledChildren(*mgr), key
+
+
+class _PooledChildren:
+    """run_task on the pool with the pool's spawn conf (unlimited reuse)."""
+
+    def __init__(self, mgr, spawn_conf):
+        self.mgr, self.spawn_conf = mgr, spawn_conf
+
+    def run_task(self, key, job, payload, reporter, kill_event):
+        return self.mgr.run_task(key, job, payload, reporter, kill_event,
+                                 spawn_conf=self.spawn_conf)
+
+
+def _shutdown_pools():
+    with _POOLS_LOCK:
+        pools = list(_POOLS.values())
+        _POOLS.clear()
+    for mgr, _conf in pools:
+        mgr.shutdown()
+
+
 class LocalJobRunner:
     def __init__(self, conf=None):
         self.conf = conf
@@ -113,9 +164,9 @@ class LocalJobRunner:
             nthreads = max(1, job.get_int("mapred.local.map.tasks.maximum", 1))
             # parallel local maps in child processes (past the GIL) when asked for
             children = None
+            pool_key = str(jid)
             if nthreads > 1 and use_child_process(job):
-                from .child import ChildManager
-                children = ChildManager(f"local-{jid}", local_root, job)
+                children, pool_key = _local_children(job)
                 conf_dict = job.to_dict()
 
             def run_map(i):
@@ -131,7 +182,7 @@ class LocalJobRunner:
                                          "data": sp.serialize().hex()},
                                "conf": conf_dict, "work_dir": work, "progress_interval": 1.0}
                     t.start_time = time.time()
-                    outputs[i] = children.run_task(str(jid), job, payload, t.reporter,
+                    outputs[i] = children.run_task(pool_key, job, payload, t.reporter,
                                                    threading.Event())
                     t.finish_time = time.time()
                 else:
@@ -145,12 +196,8 @@ class LocalJobRunner:
                 for i in range(len(maps)):
                     run_map(i)
             else:
-                try:
-                    with cf.ThreadPoolExecutor(nthreads) as ex:
-                        list(ex.map(run_map, range(len(maps))))
-                finally:
-                    if children is not None:
-                        children.shutdown()
+                with cf.ThreadPoolExecutor(nthreads) as ex:
+                    list(ex.map(run_map, range(len(maps))))
             lj._counters.incr(C.JOB_GROUP, C.TOTAL_LAUNCHED_MAPS, len(maps))
             lj._counters.incr(C.JOB_GROUP, C.CPU_MAP_TASKS, len(maps))
             st.map_progress = 1.0

@@ -187,3 +187,27 @@ def test_local_runner_parallel_child_maps(tmp_path):
     assert {k: int(v) for k, v in _read(tmp_path / "out").items()} == dict(cnt)
     assert rj.getCounters().get("org.apache.hadoop.mapred.Task$Counter",
                                 "MAP_INPUT_RECORDS") == 240
+
+
+def test_local_runner_child_pool_is_warm_across_jobs(tmp_path):
+    """Parallel local maps in child processes reuse one warm pool across jobs
+    (tasks carry their own conf): the second job starts no interpreter, and
+    its output is still right."""
+    from hbmr.mapred import local_runner as LR
+    inp, cnt = _words(tmp_path)
+    conf = JobConf()
+    conf.set("mapred.job.tracker", "local")
+    conf.set_int("mapred.local.map.tasks.maximum", 3)
+    conf.set("mapred.task.isolation", "process")
+    conf.set("mapred.child.env", "HBMR_POOL_TEST=1")     # a pool of its own
+    spawned = []
+    for i in range(2):
+        job = wordcount.make_job(str(inp), str(tmp_path / f"out{i}"), reduces=1, conf=conf)
+        rj = JobClient.runJob(job, verbose=False)
+        assert rj.isSuccessful()
+        assert {k: int(v) for k, v in _read(tmp_path / f"out{i}").items()} == dict(cnt)
+        mgrs = [m for k, (m, c) in LR._POOLS.items() if c.get("mapred.child.env") ==
+                "HBMR_POOL_TEST=1"]
+        assert len(mgrs) == 1
+        spawned.append(mgrs[0].spawned)
+    assert 1 <= spawned[0] <= 3 and spawned[1] == spawned[0]

@@ -64,6 +64,9 @@ def wordcount(a):
             # LocalJobRunner maps on child processes (the reference's runner is serial)
             conf.set_int("mapred.local.map.tasks.maximum", a.procs)
             conf.set("mapred.task.isolation", "process")
+        elif a.threads > 1:
+            # ... or on threads of this process (the native map runner releases the GIL)
+            conf.set_int("mapred.local.map.tasks.maximum", a.threads)
         times = []
         for i in range(a.steps):
             job = W.make_job(inp, os.path.join(tmp, f"out{i}"), reduces=1, conf=conf)
@@ -75,6 +78,7 @@ def wordcount(a):
         print(json.dumps({
             "config": "WordCount on LocalJobRunner, CPU-only mappers (BASELINE config 1)",
             "input_mb": a.mb, "words": words, "map_processes": a.procs,
+            "map_threads": a.threads if a.procs <= 1 else 1,
             "job_seconds": [round(t, 3) for t in times],
             "mb_per_s": round(a.mb / best, 2), "words_per_s": round(words / best, 1),
             "map_input_records": cs.get("org.apache.hadoop.mapred.Task$Counter",
@@ -259,6 +263,7 @@ def main():
     ap.add_argument("--maps", type=int, default=1)
     ap.add_argument("--lines", type=int, default=100)
     ap.add_argument("--procs", type=int, default=1, help="wordcount: parallel map processes")
+    ap.add_argument("--threads", type=int, default=1, help="wordcount: parallel map threads")
     ap.add_argument("--cpu-slots", type=int, default=0)
     ap.add_argument("-D", dest="defines", action="append", default=[], metavar="KEY=VALUE",
                     help="kmeans-pipes: extra cluster/job conf")
