@@ -141,6 +141,17 @@ def wordcount_gpu(a):
 def kmeans_pipes(a):
     import torch
 
+    from hbmr.utils.sampler import dump_profiles, maybe_profile_threads
+    cprof = maybe_profile_threads()   # HBMR_CPROFILE=path: cProfile of every thread
+    try:
+        _kmeans_pipes(a, torch)
+    finally:
+        if cprof:
+            dump_profiles(cprof)
+
+
+def _kmeans_pipes(a, torch):
+
     from hbmr.mapred.cluster import LocalCluster
     from hbmr.mapred.jobconf import JobConf
     from hbmr.models import kmeans as K
