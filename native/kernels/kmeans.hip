@@ -2726,7 +2726,9 @@ struct FusedQ1Fin {
 // per barrier step, a 6-slot ring and DMA reordering; so was v4, which keeps
 // the centroids stationary in registers and streams the points
 // (profiles/r06_exact_v4_ab.json): its per-block cross-wave merge makes it
-// VALU-issue bound.
+// VALU-issue bound; and v5, which takes the barrier out by giving each wave a
+// private one-tile slot refilled chunk by chunk (profiles/r06_exact_v5_ab.json):
+// 4x the L2->LDS bytes and DMA issues cost more than the barrier (+13 %).
 // tiled image: tile t is 32 * D * 2 contiguous bytes already in LDS order
 template <int D>
 __device__ __forceinline__ void stage_tile32t(char* buf, const __bf16* __restrict__ Ct,
@@ -2926,159 +2928,6 @@ __global__ __launch_bounds__(256, HBMR_EXACT_MINB) void kmeans_assign_top3_q1_v3
   fin.xerr = tbl.xerr[s];
   fin.sidx = s;
   assign_tile_v3<D, F16>(tbl.X[s], tbl.off[s + 1] - o, Ct, chalf, ntiles, labels + o,
-                         b - tbl.blk[s], smem, fin);
-}
-
-// v5: v3 without the per-tile barrier.  Each wave streams the centroid tiles
-// through its OWN one-tile LDS slot (same LDS per workgroup as v3's 4-slot
-// shared ring), so only the wave's own vmcnt orders its reads behind its
-// DMAs and nothing in the loop waits on another wave.  The slot is refilled
-// one 1-KiB chunk (= one k-step of a tile) at a time, right behind the read of
-// that chunk: k-step s of tile t reads chunk s of tile t+1 into registers and
-// then re-DMAs chunk s-1 (tile t+2) over the bytes read one step earlier.  In
-// that order a fixed vmcnt(KS-1) (KS-2 at k-step 0) retires exactly the chunk
-// about to be read, at every k-step and tile (tile indices past the end are
-// clamped: the loads stay in bounds and their bytes are never read).  The cost is 4× the
-// L2→LDS bytes of v3 (each wave fetches every tile) and KS+1 DMAs per wave
-// and tile instead of KS/4.
-template <int D> struct AssignV5 {
-  static constexpr int KS = D / 16;
-  static constexpr int TILE_BYTES = 32 * D * 2;          // KS chunks of 1 KiB
-  static constexpr int BUF = TILE_BYTES + 64 * 4;        // + -|c|^2/2 (and a copy)
-  static_assert(TILE_BYTES == KS * 1024, "one 1-KiB DMA chunk per k-step");
-};
-
-template <int D, bool F16>
-__device__ __forceinline__ void assign_tile_v5(const __bf16* __restrict__ X, long n,
-                                               const __bf16* __restrict__ Ct,
-                                               const float* __restrict__ chalf, int ntiles,
-                                               int32_t* __restrict__ labels, long blk, char* smem,
-                                               const FusedQ1Fin& fin) {
-  static_assert(D <= 128, "v5 keeps two 32-point blocks of D <= 128 in registers");
-  constexpr int PB = 2;
-  using V = AssignV5<D>;
-  constexpr int KS = V::KS;
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid / HBMR_WAVE);
-  const int lane = tid & (HBMR_WAVE - 1);
-  const int h = lane >> 5;
-  const int col = lane & 31;
-  const long p0 = blk * (4 * PB * 32) + (long)wave * PB * 32;
-  char* slot = smem + wave * V::BUF;
-  const char* arow = slot + h * 512 + col * 16;
-  const uint32_t loff = (uint32_t)lane * 16u;
-  const uint32_t boff = (uint32_t)(lane & 31) * 4u;
-  const char* cbase = reinterpret_cast<const char*>(Ct);
-  const int last = ntiles - 1;
-  auto dma = [&](int tile, int c) __attribute__((always_inline)) {
-    const char* g = cbase + (size_t)min(tile, last) * V::TILE_BYTES + c * 1024;
-    __builtin_amdgcn_global_load_lds((const void*)(g + loff), (void*)(slot + c * 1024), 16, 0, 0);
-  };
-  // all 64 lanes (no exec branch in the loop): the upper half lands a copy
-  auto dma_bias = [&](int tile) __attribute__((always_inline)) {
-    const char* g = reinterpret_cast<const char*>(chalf + (size_t)min(tile, last) * 32);
-    __builtin_amdgcn_global_load_lds((const void*)(g + boff), (void*)(slot + V::TILE_BYTES), 4, 0,
-                                     0);
-  };
-  auto frag = [&](int s) __attribute__((always_inline)) {
-    return *reinterpret_cast<const bf16x8*>(arow + s * 1024);
-  };
-  auto bias = [&](f32x16& acc) __attribute__((always_inline)) {
-    const float* ch = reinterpret_cast<const float*>(slot + V::TILE_BYTES);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(ch + 8 * g + 4 * h);
-      acc[4 * g + 0] = v[0];
-      acc[4 * g + 1] = v[1];
-      acc[4 * g + 2] = v[2];
-      acc[4 * g + 3] = v[3];
-    }
-  };
-
-#pragma unroll
-  for (int c = 0; c < KS; ++c) dma(0, c);
-  dma_bias(0);
-  bf16x8 bfrag[PB][KS];
-#pragma unroll
-  for (int pb = 0; pb < PB; ++pb) {
-    long p = p0 + pb * 32 + col;
-    if (p >= n) p = n - 1;
-    const uint4* row = reinterpret_cast<const uint4*>(X + p * D);
-#pragma unroll
-    for (int s = 0; s < KS; ++s) bfrag[pb][s] = __builtin_bit_cast(bf16x8, row[2 * s + h]);
-  }
-  PackedTop2x8 am[PB];
-#pragma unroll
-  for (int pb = 0; pb < PB; ++pb) am[pb].init(ntiles);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int pb = 0; pb < PB; ++pb)
-#pragma unroll
-    for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(bfrag[pb][s]));
-  const uint32_t top = am[0].top;
-  const uint32_t vmask = am[0].vmask;
-
-  bf16x8 a[KS];
-  f32x16 bz;
-#pragma unroll
-  for (int s = 0; s < KS; ++s) a[s] = frag(s);
-  bias(bz);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  // tile 1 but its last chunk and bias (k-step 0 of tile 0 issues those)
-#pragma unroll
-  for (int c = 0; c < KS - 1; ++c) dma(1, c);
-
-  for (int t = 0; t < ntiles; ++t) {
-    f32x16 acc[PB];
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-#pragma unroll
-      for (int pb = 0; pb < PB; ++pb)
-        acc[pb] = mfma32x32x16<F16>(a[s], bfrag[pb][s], s == 0 ? bz : acc[pb]);
-      // chunk s of tile t+1 has landed: every DMA issued since it may still fly
-      if (s == 0) vm_wait<KS - 2>(); else vm_wait<KS - 1>();
-      a[s] = frag(s);
-      // all but that read have returned: chunk s-1 of tile t+1 (at s = 0,
-      // chunk KS-1 and the bias of tile t) may be overwritten
-      asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
-      if (s == 0) {
-        dma(t + 1, KS - 1);
-        dma_bias(t + 1);
-      } else {
-        dma(t + 2, s - 1);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    uint32_t code[16];
-    tile_codes(top, t, code);
-#pragma unroll
-    for (int pb = 0; pb < PB; ++pb) top2_insert(am[pb], acc[pb], code, vmask);
-    vm_wait<KS - 1>();                     // tile t+1's bias
-    bias(bz);
-  }
-  // no DMA may still be landing in the slot when the workgroup retires
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  fin(am, h, p0, col, n, labels);
-}
-
-template <int D, bool F16>
-__global__ __launch_bounds__(256, HBMR_EXACT_MINB) void kmeans_assign_top3_q1_v5_kernel(
-    const TopQ1Table tbl, const __bf16* __restrict__ Ct, const float* __restrict__ chalf,
-    int ntiles, int32_t* __restrict__ labels, FusedQ1Fin fin) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const long b = hbmr_xcd_remap(blockIdx.x, gridDim.x);
-  int lo = 0, hi = tbl.nsplit;
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (tbl.blk[mid] <= b) lo = mid; else hi = mid;
-  }
-  const int s = __builtin_amdgcn_readfirstlane(lo);
-  const long o = tbl.off[s];
-  fin.xnorm = tbl.xnorm[s];
-  fin.xbn2 = tbl.xbn2[s];
-  fin.xerr = tbl.xerr[s];
-  fin.sidx = s;
-  assign_tile_v5<D, F16>(tbl.X[s], tbl.off[s + 1] - o, Ct, chalf, ntiles, labels + o,
                          b - tbl.blk[s], smem, fin);
 }
 
@@ -3991,17 +3840,6 @@ int hbmr_kmeans_assign_top3_q1_grouped(int nsplit, const void* const* X, const l
   (void)inflate;
   // the v3 kernel (default; needs the tiled image Ct), or v2
   // (hbmr_kmeans_set_exact_kernel(2) / HBMR_EXACT_V3=v2, read once)
-  if (exact_kernel() == 5) {
-    if (!Ct) return (int)hipErrorInvalidValue;
-    auto kern = dp == 64 ? (f16 ? kmeans_assign_top3_q1_v5_kernel<64, true>
-                                : kmeans_assign_top3_q1_v5_kernel<64, false>)
-                         : (f16 ? kmeans_assign_top3_q1_v5_kernel<128, true>
-                                : kmeans_assign_top3_q1_v5_kernel<128, false>);
-    const size_t lds = 4 * (dp == 64 ? AssignV5<64>::BUF : AssignV5<128>::BUF);
-    hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(256), lds, st, t,
-                       reinterpret_cast<const __bf16*>(Ct), chalf, k_pad / 32, labels, fin);
-    return (int)hipGetLastError();
-  }
   if (exact_kernel() == 3) {
     if (!Ct) return (int)hipErrorInvalidValue;
     auto kern = dp == 64 ? (f16 ? kmeans_assign_top3_q1_v3_kernel<64, true>
@@ -4073,7 +3911,7 @@ int hbmr_kmeans_exact_prep(const float* x, long n, int d, int ldx, int dp, int f
 // default (HBMR_EXACT_V3=v2 selects v2).  Returns the previous setting.
 int hbmr_kmeans_set_exact_kernel(int v) {
   const int old = g_exact_kernel;
-  g_exact_kernel = v == 2 || v == 3 || v == 5 ? v : -1;
+  g_exact_kernel = v == 2 || v == 3 ? v : -1;
   return old;
 }
 

@@ -401,8 +401,7 @@ def test_exact_batch_labels_at_bench_shape():
     """The bench's shape and distribution (k = 1024 centers, d = 128): the
     packed arg-max keeps 9 fewer mantissa bits at k = 1024 (4 + log2(k/32)),
     yet every certified label is the fp64 arg-min of the fp32 data (up to fp64
-    ties), for the default fused kernel (v3), the barrier-free one (v5) and the
-    round-4 one (v2)."""
+    ties), for the default fused kernel (v3) and the round-4 one (v2)."""
     from hbmr.ops import kmeans as km
     n, d, k, split = 2_000_000, 128, 1024, 250_000
     x = K.synthetic_points(7, 0, n, d, k, "cuda")
@@ -418,7 +417,7 @@ def test_exact_batch_labels_at_bench_shape():
     want = truth_labels(x, c)
     lib = km._lib.load()
     try:
-        for kern in (3, 5, 2):                           # v3 (default), v5, v2
+        for kern in (3, 2):                              # v3 (default) and v2
             lib.hbmr_kmeans_set_exact_kernel(kern)
             st = torch.zeros(5, dtype=torch.int64, device="cuda")
             got = torch.full((n,), -1, dtype=torch.int32, device="cuda")

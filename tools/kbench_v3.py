@@ -67,7 +67,7 @@ def main():
     scratch = {}
     lib = km._lib.load()
     for mode in a.modes.split(","):
-        lib.hbmr_kmeans_set_exact_kernel({"v2": 2, "v5": 5}.get(mode, 3))
+        lib.hbmr_kmeans_set_exact_kernel(2 if mode == "v2" else 3)
         out = torch.full((n,), -1, dtype=torch.int32, device=dev)
         stats = torch.zeros(5, dtype=torch.int64, device=dev)
 
