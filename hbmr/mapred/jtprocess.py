@@ -71,6 +71,8 @@ def main() -> int:
     tune()
     cprof = maybe_profile_threads()     # HBMR_CPROFILE / HBMR_SAMPLE_PROF cover this process
     sampler = maybe_start()
+    from ..utils.phaseprof import maybe_install
+    maybe_install()                     # HBMR_PHASE_PROF: per-method thread CPU
     try:
         return serve(conf_dict)
     finally:
