@@ -121,3 +121,31 @@ def test_news_between_the_reporters_last_check_and_its_exit_is_reported():
     assert not late.is_alive()
     assert calls == [reporter, late]    # the late news was reported, by itself
     assert not tt._reporting and not tt._report_again
+
+
+def test_a_bulk_launched_batch_of_per_attempt_maps_reports_once():
+    """The per-attempt GPU maps of one bulk launch (Pipes GPU executables)
+    share a _ReportGroup: successes before the batch's last are queued
+    without ringing the JobTracker (their statuses ride on the last one's
+    report; the defer timer bounds the wait), a failure rings at once."""
+    from hbmr.mapred.tasktracker import TaskTracker, _ReportGroup, _Running
+
+    class _Stub:
+        def __init__(self):
+            self._news = threading.Event()
+            self.armed = 0
+
+        def _arm_defer_flush(self):
+            self.armed += 1
+
+    tt = _Stub()
+    grp = _ReportGroup(3)
+    runs = [_Running(None, None, None) for _ in range(3)]
+    for r in runs:
+        r.group = grp
+    assert TaskTracker._group_wake(tt, runs[0], True) is False
+    assert tt._news.is_set() and tt.armed == 1
+    assert TaskTracker._group_wake(tt, runs[1], False) is True       # a failure: now
+    assert TaskTracker._group_wake(tt, runs[2], True) is True        # the last one
+    lone = _Running(None, None, None)
+    assert TaskTracker._group_wake(tt, lone, True) is True           # no group
