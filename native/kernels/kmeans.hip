@@ -2375,7 +2375,16 @@ constexpr int kQShards = 8;
 constexpr int kQ1Per = 4;            // points per thread in the step-1 scan
 constexpr int kQ2Lanes = 8;          // lanes per Q1 entry in step 2
 constexpr int kQ2Per = HBMR_WAVE / kQ2Lanes;
-constexpr int kRefineGrid = 2048;    // persistent grid of q2 (q3: a quarter)
+constexpr int kRefineGrid = 2048;    // persistent grid of q2 and q3
+// HBMR_REFINE_GRID (read once) overrides it, for tuning runs
+inline long refine_grid() {
+  static const long g = [] {
+    const char* e = getenv("HBMR_REFINE_GRID");
+    const long v = e ? atol(e) : 0;
+    return v > 0 ? v : (long)kRefineGrid;
+  }();
+  return g;
+}
 // workspace header: Q1 / Q2 shard counts (8 + 8 u32) and the sharded stats
 // (8 shards x 4 u64 at kStatsOff): one word per stat took every block's
 // atomic at the kernels' tails; kmeans_refine_stats_kernel folds them
@@ -2407,7 +2416,7 @@ inline RefineLayout refine_layout(int nsplit, const long* ns) {
   // the fused top-3 epilogue appends from 256-point workgroups, shard =
   // blockIdx % kQShards: at most ceil(nb / kQShards) workgroups per shard
   L.cap1 = std::max<long>(cap1, ceil_div(nb_fused, kQShards) * 256);
-  L.g2 = (unsigned)std::max<long>(1, std::min<long>(kRefineGrid, ceil_div(total, 4 * kQ2Per)));
+  L.g2 = (unsigned)std::max<long>(1, std::min<long>(refine_grid(), ceil_div(total, 4 * kQ2Per)));
   const long per_iter = (long)L.g2 * 4 * kQ2Per;           // Q1 entries per grid iteration
   L.cap2 = ceil_div(L.g2, kQShards) * 4 * kQ2Per * std::max<long>(1, ceil_div(total, per_iter));
   L.off1 = kRefineHdr;
