@@ -161,13 +161,22 @@ class MuxChild:
             jid = t.job_id
             key = jid if job.get_boolean(SHARED_CONF, False) else \
                 (jid,) + tuple(job.get(k) for k in TASK_KEYS)
-            if key != self.conf_job:
-                job.set_boolean("hbmr.pipes.child.reuse", True)
-                self.app.downlink.set_job_conf(job)
-                self.conf_job = key
-                if TRACE.on:
-                    TRACE.instant("pipes.mux.conf_sent")
-            self.app.downlink.run_map(split, num_reduces, False)
+            try:
+                if key != self.conf_job:
+                    job.set_boolean("hbmr.pipes.child.reuse", True)
+                    self.app.downlink.set_job_conf(job)
+                    self.conf_job = key
+                    if TRACE.on:
+                        TRACE.instant("pipes.mux.conf_sent")
+                self.app.downlink.run_map(split, num_reduces, False)
+            except OSError as e:
+                # the child is gone (its uplink reader fails the FIFO): say why
+                with self.cond:
+                    if t in self.fifo:
+                        self.fifo.remove(t)
+                    self.dead = self.dead or e
+                    self.cond.notify_all()
+                raise RuntimeError(f"pipes child failed: {e}; {self.app._stderr_tail()}") from e
             self.maps += 1
             if TRACE.on:
                 TRACE.instant("pipes.mux.run_map_sent", fifo=len(self.fifo))

@@ -258,10 +258,14 @@ class UplinkReader(threading.Thread):
                     h.authenticate(self._bytes().decode())
                 else:
                     raise IOError(f"Bad command code: {cmd}")
+        # (the handler installed NOW: one swapped in while this thread was
+        # blocked reading — a reused child's next task, the GPU mux's FIFO
+        # dispatcher — is the one waiting for the outcome; the stale one left
+        # a mux child's maps waiting forever on a child that had died)
         except EOFError:
-            h.failed(IOError("pipe child exited before DONE"))
+            self.handler.failed(IOError("pipe child exited before DONE"))
         except BaseException as e:  # noqa: BLE001
-            h.failed(e)
+            self.handler.failed(e)
 
 
 def read_all(data: bytes):

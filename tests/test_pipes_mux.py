@@ -100,3 +100,34 @@ def test_maps_in_flight_never_exceed_the_depth():
     for t in threads:
         t.join(5)
     assert done == 6 and peak[0] <= 2
+
+
+def test_a_child_dying_after_the_handler_swap_fails_the_new_handler():
+    """The uplink reader reports EOF to the handler installed when the child
+    dies, not the one it held while blocked in its read: the mux swaps in its
+    FIFO dispatcher after the child started, and a child that then died
+    (e.g. a bad input file) left every queued map waiting forever."""
+    import socket
+
+    from hbmr.pipes.protocol import UplinkReader
+
+    class _H:
+        def __init__(self):
+            self.err = None
+            self.ev = threading.Event()
+
+        def failed(self, e):
+            self.err = e
+            self.ev.set()
+
+    a, b = socket.socketpair()
+    first, second = _H(), _H()
+    r = UplinkReader(a, first)
+    r.start()
+    time.sleep(0.05)                 # the reader is blocked in its first read
+    r.handler = second
+    b.close()                        # the child exits
+    assert second.ev.wait(5)
+    assert isinstance(second.err, IOError) and first.err is None
+    r.join(5)
+    a.close()
