@@ -854,7 +854,7 @@ class ReduceTask(Task):
         if not merger.on_disk:
             if kind is not None:
                 # stable sort of the concatenated map outputs == Merger's k-way merge
-                b = sortbuf.Batch.from_ifile_bodies(merger.memory_bodies())
+                b = sortbuf.Batch.for_reduce(merger.memory_bodies())
                 perm = b.sort(kind, np.zeros(b.n, np.int32))
                 return self._reduce_native(job, b, perm, kind, kcls, vcls)
             merged = merge_segments(merger.memory_records(), job.get_int("io.sort.factor", 10))

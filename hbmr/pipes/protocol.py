@@ -84,6 +84,21 @@ def frame_of_serialized(cls):
     return lambda s: encode_vint(len(s)) + s
 
 
+def frame_parts_of_serialized(cls):
+    """frame_of_serialized as (VInt prefix, body view) — the frame written in
+    two pieces, so a large value (a K-Means partials block, ~1 MB) goes to the
+    socket from where it lies instead of through a joined copy."""
+    if not RAW_FRAMES:
+        return None
+    if cls is Text:
+        return lambda s: (b"", s)
+    if cls is BytesWritable:
+        return lambda s: (encode_vint(len(s) - 4), memoryview(s)[4:])
+    if issubclass(cls, (Text, BytesWritable)) or not issubclass(cls, Writable):
+        return None
+    return lambda s: (encode_vint(len(s)), s)
+
+
 class DownwardProtocol:
     def __init__(self, sock):
         self.sock = sock
@@ -182,6 +197,18 @@ class DownwardProtocol:
             for f in value_frames:
                 w(sep)
                 w(f)
+
+    def reduce_group_parts(self, key_frame: bytes, parts: list):
+        """reduce_group with each value frame as (prefix, body) pieces
+        (frame_parts_of_serialized): no per-value joined copy."""
+        sep = _SMALL_VINTS[REDUCE_VALUE]
+        with self._lock:
+            w = self.out.write
+            w(_SMALL_VINTS[REDUCE_KEY])
+            w(key_frame)
+            for pre, body in parts:
+                w(sep + pre if pre else sep)
+                w(body)
 
     def end_of_input(self):
         with self._lock:

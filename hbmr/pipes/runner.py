@@ -22,7 +22,7 @@ from ..mapred.api import InputFormat, MapRunnable, Partitioner, RecordReader, Re
 from ..mapred.formats import FileSplit
 from ..utils.reflection import load_class, new_instance
 from .application import POOL, Application
-from .protocol import frame_of_serialized
+from .protocol import frame_of_serialized, frame_parts_of_serialized
 
 JAVA_RR = "hadoop.pipes.java.recordreader"
 JAVA_MAPPER = "hadoop.pipes.java.mapper"
@@ -199,12 +199,18 @@ class PipesReducer(Reducer):
         kf, vf = frame_of_serialized(key_class), frame_of_serialized(value_class)
         if kf is None or vf is None:
             return None
+        vp = frame_parts_of_serialized(value_class)
 
         def reduce_raw(kb, vbs, output, reporter):
             if self.app is None:
                 self.reporter = reporter
                 self._start(output, reporter)
-            self.app.downlink.reduce_group(kf(kb), [vf(v) for v in vbs])
+            d = self.app.downlink
+            if vp is not None and sum(map(len, vbs)) >= (1 << 20):
+                # large values (K-Means partials blocks): written in place
+                d.reduce_group_parts(kf(kb), [vp(v) for v in vbs])
+            else:
+                d.reduce_group(kf(kb), [vf(v) for v in vbs])
             reporter.progress()
         return reduce_raw
 
