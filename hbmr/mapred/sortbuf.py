@@ -241,24 +241,41 @@ class _ViewBatch(Batch):
     def ifile_body(self, perm, lo, hi) -> bytes:
         raise NotImplementedError("a reduce-side view batch is not re-encoded")
 
-def write_segment(f, body: bytes, codec=None):
+def write_segment(f, body: bytes, codec=None, crc=True):
     """Append one IFile segment (body [+codec] + CRC32) to f; returns
-    (start, raw_length, part_length) for the SpillRecord."""
+    (start, raw_length, part_length) for the SpillRecord.  ``crc`` False
+    leaves the CRC word zero (an in-memory map output, read only as a
+    VerifiedSegment; fill_crcs completes it if it goes to a file after all)."""
     start = f.tell()
     raw_len = len(body) + 4
     if codec is not None:
         body = codec.compress(body)
     f.write(body)
-    f.write(struct.pack(">I", zlib.crc32(body) & 0xFFFFFFFF))
+    f.write(struct.pack(">I", zlib.crc32(body) & 0xFFFFFFFF) if crc else b"\0\0\0\0")
     return start, raw_len, len(body) + 4
+
+
+def fill_crcs(data: bytes, rec) -> bytes:
+    """``data`` (a spill's segments written with crc=False) with every
+    partition segment's CRC32 computed, per its SpillRecord ``rec``."""
+    out = bytearray(data)
+    mv = memoryview(out)
+    for p in range(len(rec)):
+        start, _raw, plen = rec.get(p)
+        if plen >= 4:
+            c = zlib.crc32(mv[start:start + plen - 4]) & 0xFFFFFFFF
+            out[start + plen - 4:start + plen] = struct.pack(">I", c)
+    return bytes(out)
 
 
 class VerifiedSegment(bytes):
     """A map-output segment that never left this process (an in-memory map
-    output, hbmr/mapred/mapoutput.py): no disk or wire between its CRC and
+    output, hbmr/mapred/mapoutput.py): no disk or wire between its writer and
     here, so the reduce skips the check (zlib's CRC runs ~1 GB/s: a 1 MB
-    K-Means partials block per map made it most of the copy phase)."""
+    K-Means partials block per map made it most of the copy phase) — and its
+    writer skips computing one (write_segment crc=False: the CRC word is 0)."""
     __slots__ = ()
+    verified = True
 
 
 def segment_body(data: bytes, codec=None, verify=True) -> bytes:

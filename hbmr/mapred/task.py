@@ -284,13 +284,16 @@ class MapOutputBuffer(OutputCollector):
         self._ensure_dir()
         return open(path, "wb")
 
-    def _commit_spill(self, path, f, rec):
+    def _commit_spill(self, path, f, rec, crc_pending=False):
         """Close a spill: its index file next to it, or both held in memory
-        (a store over its cap gets the files after all)."""
+        (a store over its cap gets the files after all — with their CRCs,
+        which an in-memory output skipped: ``crc_pending``)."""
         if self._to_memory:
             data = f.getvalue()
             if mapoutput.STORE.put(path, data, rec, self.mem_total):
                 return
+            if crc_pending:
+                data = sortbuf.fill_crcs(data, rec)
             self._ensure_dir()
             with open(path, "wb") as out:
                 out.write(data)
@@ -508,11 +511,14 @@ class MapOutputBuffer(OutputCollector):
                 else:
                     body, nrec = b.ifile_body(perm, lo, hi), hi - lo
                 spilled += nrec
-                rec.put(p, *sortbuf.write_segment(f, body, self.codec))
+                # (an in-memory output's CRC is never read: fill_crcs makes it
+                # only if the store turns it away, _commit_spill)
+                rec.put(p, *sortbuf.write_segment(f, body, self.codec,
+                                                  crc=not self._to_memory))
         except BaseException:
             f.close()
             raise
-        self._commit_spill(path, f, rec)
+        self._commit_spill(path, f, rec, crc_pending=self._to_memory)
         self.spills.append((path, rec))
         self.reporter.incrCounter(C.TASK_GROUP, C.SPILLED_RECORDS, spilled)
 

@@ -39,7 +39,26 @@ def test_memory_output_reads_like_the_file(tmp_path):
             assert mapoutput.STORE.drop_prefix(str(tmp_path / name)) == 1
         else:
             assert os.path.exists(path) and os.path.exists(path + ".index")
-    assert outs["disk"] == outs["mem"]
+    # the same records; the in-memory output carries no CRC (it is read only
+    # as a VerifiedSegment, never checked), the file's CRC is checked
+    assert [bytes(x[:-4]) for x in outs["disk"]] == [bytes(x[:-4]) for x in outs["mem"]]
+    from hbmr.io.ifile import read_segment
+    for d, m in zip(outs["disk"], outs["mem"]):
+        assert read_segment(d) == read_segment(m)
+
+
+def test_memory_output_the_store_turns_away_gets_its_crcs(tmp_path):
+    """An output meant for memory (CRC skipped) that the store refuses (its
+    total cap) is written to its files with every segment's CRC filled in."""
+    from hbmr.io.ifile import read_segment
+    buf = _buffer(tmp_path, "full", True)
+    buf.mem_total = 1                                   # the store is full
+    for i in range(300):
+        buf.collect(Text(f"k{i % 31}"), Text("w" * (i % 17)))
+    path = buf.flush()
+    assert os.path.exists(path) and mapoutput.STORE.get(path) is None
+    segs = [MapOutputLocation("a", path).read_partition(p) for p in range(3)]
+    assert sum(len(read_segment(x)) for x in segs) == 300     # CRCs verify
 
 
 def test_memory_output_over_the_cap_goes_to_disk(tmp_path):
