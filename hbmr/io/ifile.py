@@ -59,9 +59,12 @@ class IFileWriter:
 
 def read_segment(data: bytes, codec=None, verify=True):
     """Parse one IFile segment (as stored, incl. CRC). Returns list of (k, v)."""
-    body, crc = data[:-4], struct.unpack(">I", data[-4:])[0]
     # (a segment that never left this process — hbmr.mapred.sortbuf.
-    # VerifiedSegment — carries no CRC to check)
+    # VerifiedSegment, or a memoryview into the in-memory map output store —
+    # carries no CRC to check)
+    if data.__class__ is memoryview:
+        data, verify = data.tobytes(), False
+    body, crc = data[:-4], struct.unpack(">I", data[-4:])[0]
     if verify and not getattr(data, "verified", False) and \
             (zlib.crc32(body) & 0xFFFFFFFF) != crc:
         raise IOError("IFile checksum error")

@@ -190,15 +190,16 @@ class Batch:
                                    _addr(perm), lo, hi, _addr(ends))
         return ends[:nr]
 
-    def ifile_body(self, perm, lo, hi) -> bytes:
-        """IFile segment body (records + EOF marker, no CRC) of perm[lo:hi]."""
+    def ifile_body(self, perm, lo, hi, view=False):
+        """IFile segment body (records + EOF marker, no CRC) of perm[lo:hi]
+        (``view``: a memoryview of the encode buffer, not a bytes copy)."""
         sel = perm[lo:hi]
         bound = int(self.klen[sel].sum() + self.vlen[sel].sum()) + 10 * (hi - lo) + 4
         out = np.empty(bound, np.uint8)
         n = lib().hbmr_ifile_encode(_addr(self._karr), _addr(self.kpos), _addr(self.klen),
                                     _addr(self._varr), _addr(self.vpos), _addr(self.vlen),
                                     _addr(perm), lo, hi, _addr(out))
-        return out[:n].tobytes()
+        return memoryview(out)[:n] if view else out[:n].tobytes()
 
     def key(self, r) -> bytes:
         p = int(self.kpos[r])
@@ -238,8 +239,9 @@ class _ViewBatch(Batch):
     def value_view(self, r) -> memoryview:
         return self.views[r]
 
-    def ifile_body(self, perm, lo, hi) -> bytes:
+    def ifile_body(self, perm, lo, hi, view=False):
         raise NotImplementedError("a reduce-side view batch is not re-encoded")
+
 
 def write_segment(f, body: bytes, codec=None, crc=True):
     """Append one IFile segment (body [+codec] + CRC32) to f; returns
@@ -278,10 +280,17 @@ class VerifiedSegment(bytes):
     verified = True
 
 
+def in_process(data) -> bool:
+    """A segment that never left this process: a VerifiedSegment, or a
+    memoryview into the in-memory map output store (MapOutputLocation.
+    read_partition: no copy; every fetch from a file or the wire is bytes)."""
+    return data.__class__ is VerifiedSegment or data.__class__ is memoryview
+
+
 def segment_body(data: bytes, codec=None, verify=True) -> bytes:
     """Stored IFile segment (incl. CRC) → decompressed body."""
     body, crc = memoryview(data)[:-4], struct.unpack(">I", data[-4:])[0]
-    if verify and data.__class__ is not VerifiedSegment and \
+    if verify and not in_process(data) and \
             (zlib.crc32(body) & 0xFFFFFFFF) != crc:
         raise IOError("IFile checksum error")
     return codec.decompress(bytes(body)) if codec is not None else body

@@ -289,7 +289,8 @@ class MapOutputBuffer(OutputCollector):
         (a store over its cap gets the files after all — with their CRCs,
         which an in-memory output skipped: ``crc_pending``)."""
         if self._to_memory:
-            data = f.getvalue()
+            # (f: the spill's BytesIO, or its joined bytes already)
+            data = f if isinstance(f, bytes) else f.getvalue()
             if mapoutput.STORE.put(path, data, rec, self.mem_total):
                 return
             if crc_pending:
@@ -502,6 +503,26 @@ class MapOutputBuffer(OutputCollector):
         path = self._spill_path(idx)
         rec = SpillRecord(self.R)
         spilled = 0
+        if self._to_memory and self.codec is None:
+            # an in-memory output: the segments are joined once into the bytes
+            # the store holds (no file object; each encode buffer is a view);
+            # their CRC words stay 0 — never read in this process, filled in
+            # if the store turns the output away (_commit_spill)
+            pieces, pos = [], 0
+            for p in range(self.R):
+                lo, hi = int(starts[p]), int(starts[p + 1])
+                if self.combiner_cls is not None and hi > lo:
+                    body, nrec = self._combine_native(b, perm, lo, hi)
+                else:
+                    body, nrec = b.ifile_body(perm, lo, hi, view=True), hi - lo
+                spilled += nrec
+                pieces += (body, b"\0\0\0\0")
+                rec.put(p, pos, len(body) + 4, len(body) + 4)
+                pos += len(body) + 4
+            self._commit_spill(path, b"".join(pieces), rec, crc_pending=True)
+            self.spills.append((path, rec))
+            self.reporter.incrCounter(C.TASK_GROUP, C.SPILLED_RECORDS, spilled)
+            return
         f = self._open_spill(path)
         try:
             for p in range(self.R):
@@ -511,8 +532,6 @@ class MapOutputBuffer(OutputCollector):
                 else:
                     body, nrec = b.ifile_body(perm, lo, hi), hi - lo
                 spilled += nrec
-                # (an in-memory output's CRC is never read: fill_crcs makes it
-                # only if the store turns it away, _commit_spill)
                 rec.put(p, *sortbuf.write_segment(f, body, self.codec,
                                                   crc=not self._to_memory))
         except BaseException:
@@ -765,7 +784,8 @@ class MapOutputLocation:
         if held is not None:            # an in-memory map output of this process
             data, idx = held
             start, _raw, plen = idx.get(part)
-            return sortbuf.VerifiedSegment(memoryview(data)[start:start + plen])
+            # a view, not a copy (sortbuf.in_process: no CRC to check)
+            return memoryview(data)[start:start + plen]
         idx = SpillRecord.read(self.path + ".index")
         start, _raw, plen = idx.get(part)
         with open(self.path, "rb") as f:
