@@ -449,6 +449,31 @@ def _bytes_payload(raw: bytes) -> bytes:
     return _I32.pack(len(raw)) + raw
 
 
+def serialize_in_place(ser, raw, room=8):
+    """``ser(raw)`` without copying a large payload: ``raw`` a memoryview
+    that starts ``room`` bytes into its own bytearray (the Pipes uplink's
+    large values, UplinkReader._value) gets its serialisation prefix written
+    into that room and comes back as a view of prefix + payload."""
+    if raw.__class__ is memoryview:
+        buf = raw.obj
+        if buf.__class__ is bytearray and len(buf) == len(raw) + room:
+            pre = _prefix_of(ser, len(raw))
+            if pre is not None and len(pre) <= room:
+                start = room - len(pre)
+                buf[start:room] = pre
+                return memoryview(buf)[start:]
+        return ser(bytes(raw))
+    return ser(raw)
+
+
+def _prefix_of(ser, n):
+    if ser is _bytes_payload:
+        return _I32.pack(n)
+    if ser is _text_payload:
+        return _VINT1[n] if n < 128 else encode_vint(n)
+    return None
+
+
 def payload_serializer(cls):
     """raw payload bytes -> ``cls``'s serialised form, for the classes whose
     Pipes wire form is the bare payload (Text, BytesWritable; BinaryProtocol.

@@ -32,7 +32,7 @@ from ..fs import mkdirs_fast
 from ..io.compress import get_codec
 from ..io.ifile import IFileWriter, SpillRecord, read_segment
 from ..io.serializer import to_bytes
-from ..io.writable import payload_serializer
+from ..io.writable import payload_serializer, serialize_in_place
 from ..utils.reflection import new_instance
 from ..utils.trace import TRACE
 from . import counters as C
@@ -366,14 +366,19 @@ class MapOutputBuffer(OutputCollector):
         R, native_hash, kind = self.R, self.native_hash, self.kind
 
         def sink(k, v, part):
-            kb, vb = kser(k), vser(v)
+            kb = kser(k)
+            # (a large value off the uplink: serialised in its own buffer;
+            # the native path takes any bytes-like value)
+            vb = serialize_in_place(vser, v) if kind is not None and \
+                v.__class__ is memoryview else vser(v if v.__class__ is not memoryview
+                                                   else bytes(v))
             if native_hash:
                 self.keys.append(kb)
                 self.vals.append(vb)
             else:
                 if part is None:
                     part = 0 if R == 1 else self.partitioner.getPartition(
-                        self.kcls.deserialize(kb), self.vcls.deserialize(vb), R)
+                        self.kcls.deserialize(kb), self.vcls.deserialize(bytes(vb)), R)
                 if not 0 <= part < R:
                     raise ValueError(f"Illegal partition for {k!r} ({part})")
                 if kind is not None:

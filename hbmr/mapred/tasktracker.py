@@ -170,6 +170,8 @@ class TaskTracker:
         # thread can wait that long for the interpreter while another one
         # runs bookkeeping, idling the GPU.  0.2 ms keeps hand-offs prompt.
         self.defer_map_reports = conf.get_boolean("hbmr.tracker.defer.map.reports", True)
+        from ..utils.gctune import tune_malloc
+        tune_malloc()                        # MB-sized task buffers from the heap
         # bulk-launched per-attempt GPU maps report once per batch (_ReportGroup)
         self.batch_reports = conf.get_boolean("hbmr.tracker.batch.reports", True)
         self._act_lock = threading.RLock()   # JobTracker actions, applied one at a time

@@ -53,6 +53,8 @@ class OutputHandler:
         if self.sink is not None:
             self.sink(k, v, None)
         else:
+            if v.__class__ is memoryview:      # a large value read in place
+                v = bytes(v)
             self.collector.collect(from_wire(k, self.kcls), from_wire(v, self.vcls))
         self.records += 1
 

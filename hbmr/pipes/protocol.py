@@ -249,6 +249,29 @@ class UplinkReader(threading.Thread):
         n = read_vint(self.inp)
         return self.inp.read(n) if n else b""
 
+    #: room left in front of a large value read by _value: the longest
+    #: serialisation prefix of a Text / BytesWritable payload (a 5-byte VInt)
+    ROOM = 8
+
+    def _value(self):
+        """An OUTPUT value: small ones as bytes; a large one (a K-Means block)
+        read in place into a buffer with ROOM spare bytes in front and handed
+        on as a memoryview of its payload, so the map output buffer can put
+        the serialisation prefix there instead of copying the value
+        (hbmr.io.writable.serialize_in_place)."""
+        n = read_vint(self.inp)
+        if n < (1 << 16):
+            return self.inp.read(n) if n else b""
+        buf = bytearray(self.ROOM + n)
+        mv = memoryview(buf)
+        got = self.ROOM
+        while got < len(buf):
+            r = self.inp.readinto(mv[got:])
+            if not r:
+                raise EOFError("pipe child exited in a value")
+            got += r
+        return mv[self.ROOM:]
+
     def run(self):
         h = self.handler
         try:
@@ -257,12 +280,12 @@ class UplinkReader(threading.Thread):
                 h = self.handler
                 if cmd == OUTPUT:
                     k = self._bytes()
-                    v = self._bytes()
+                    v = self._value()
                     h.output(k, v)
                 elif cmd == PARTITIONED_OUTPUT:
                     part = read_vint(self.inp)
                     k = self._bytes()
-                    v = self._bytes()
+                    v = self._value()
                     h.partitioned_output(part, k, v)
                 elif cmd == STATUS:
                     h.status(self._bytes().decode(errors="replace"))

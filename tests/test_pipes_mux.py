@@ -131,3 +131,45 @@ def test_a_child_dying_after_the_handler_swap_fails_the_new_handler():
     assert isinstance(second.err, IOError) and first.err is None
     r.join(5)
     a.close()
+
+
+def test_a_large_output_value_is_serialised_in_its_own_buffer():
+    """The uplink reads a large OUTPUT value (a K-Means partials block) in
+    place, with room in front; the map output buffer writes the Writable's
+    prefix there (serialize_in_place) instead of copying the value, and the
+    bytes equal the copying serialisation for BytesWritable and Text."""
+    import socket
+
+    from hbmr.io.vint import encode_vint
+    from hbmr.io.writable import BytesWritable, Text, payload_serializer, serialize_in_place
+    from hbmr.pipes.protocol import OUTPUT, UplinkReader
+
+    got = []
+
+    class _H:
+        def output(self, k, v):
+            got.append((k, v))
+
+        def failed(self, e):
+            got.append(("failed", e))
+
+    a, b = socket.socketpair()
+    big = bytes(range(256)) * 600                  # 153,600 bytes
+    msg = encode_vint(OUTPUT) + encode_vint(1) + b"*" + encode_vint(len(big)) + big
+    msg += encode_vint(OUTPUT) + encode_vint(1) + b"s" + encode_vint(3) + b"abc"
+    r = UplinkReader(a, _H())
+    r.start()
+    b.sendall(msg)
+    b.close()
+    r.join(5)
+    (k1, v1), (k2, v2) = got[0], got[1]
+    assert k1 == b"*" and v1.__class__ is memoryview and bytes(v1) == big
+    assert v2 == b"abc"
+    for cls in (BytesWritable, Text):
+        ser = payload_serializer(cls)
+        want = ser(big)
+        bb = bytearray(8 + len(big))
+        bb[8:] = big
+        assert bytes(serialize_in_place(ser, memoryview(bb)[8:])) == want
+        assert serialize_in_place(ser, b"xyz") == ser(b"xyz")
+    a.close()
