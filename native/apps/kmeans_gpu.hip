@@ -31,6 +31,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <ctime>
 #include <map>
 #include <stdexcept>
@@ -132,6 +133,12 @@ struct DeviceState {
   DevBuf x32stage, lab, sums, counts, ws, rws, stats;
   float* pinned = nullptr;
   size_t pinned_cap = 0;
+  // a map's partials come back into pinned memory (a pageable 1 MB D2H at
+  // k = 1024 is staged by the runtime) and are emitted from a block buffer
+  // kept across maps (no 1 MB allocation and zero-fill per map)
+  long long* hpart = nullptr;
+  size_t hpart_cap = 0;
+  std::string block;
   std::map<std::string, CachedSplit> splits;
   size_t cached_bytes = 0, cache_cap = 0;
   CentroidImage img;
@@ -143,6 +150,15 @@ struct DeviceState {
     HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     const char* mb = getenv("HBMR_PIPES_SPLIT_CACHE_MB");
     cache_cap = (size_t)(mb ? atol(mb) : 65536) << 20;
+  }
+
+  long long* partials(size_t n) {
+    if (n > hpart_cap) {
+      if (hpart) HIP_OK(hipHostFree(hpart));
+      HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&hpart), 8 * n));
+      hpart_cap = n;
+    }
+    return hpart;
   }
 
   float* staging(size_t bytes) {
@@ -330,16 +346,18 @@ class KMeansGpuMapper : public HadoopPipes::Mapper {
     tmark("map.start");
     const CachedSplit& cs = split(ctx.getInputKey());
     const long n = cs.n;
-    std::vector<long long> sums((size_t)p_.k * dp_), counts((size_t)p_.k);
+    const size_t nsums = (size_t)p_.k * dp_;
+    long long* sums = S.partials(nsums + (size_t)p_.k);
+    long long* counts = sums + nsums;
     unsigned long long st[5] = {0, 0, 0, 0, 0};
     if (n > 0) {
       const long wsb = hbmr_kmeans_accum_workspace_bytes(n, p_.k);
       int32_t* lab = static_cast<int32_t*>(S.lab.get(4 * (size_t)n));
-      long long* dsums = static_cast<long long*>(S.sums.get(8 * sums.size()));
-      long long* dcounts = static_cast<long long*>(S.counts.get(8 * counts.size()));
+      long long* dsums = static_cast<long long*>(S.sums.get(8 * nsums));
+      long long* dcounts = static_cast<long long*>(S.counts.get(8 * (size_t)p_.k));
       void* ws = S.ws.get((size_t)wsb);
-      HIP_OK(hipMemsetAsync(dsums, 0, 8 * sums.size(), S.st));
-      HIP_OK(hipMemsetAsync(dcounts, 0, 8 * counts.size(), S.st));
+      HIP_OK(hipMemsetAsync(dsums, 0, 8 * nsums, S.st));
+      HIP_OK(hipMemsetAsync(dcounts, 0, 8 * (size_t)p_.k, S.st));
       if (exact_) {
         auto* dstats = static_cast<unsigned long long*>(S.stats.get(sizeof(st)));
         HIP_OK(hipMemsetAsync(dstats, 0, sizeof(st), S.st));
@@ -371,15 +389,16 @@ class KMeansGpuMapper : public HadoopPipes::Mapper {
         LIB_OK(hbmr_kmeans_accum_bf16(cs.xb, n, dp_, lab, p_.k, dsums, dcounts, p_.fx, ws, wsb, 0,
                                       S.st));
       }
-      HIP_OK(hipMemcpyAsync(sums.data(), dsums, 8 * sums.size(), hipMemcpyDeviceToHost, S.st));
-      HIP_OK(hipMemcpyAsync(counts.data(), dcounts, 8 * counts.size(), hipMemcpyDeviceToHost,
-                            S.st));
+      HIP_OK(hipMemcpyAsync(sums, dsums, 8 * nsums, hipMemcpyDeviceToHost, S.st));
+      HIP_OK(hipMemcpyAsync(counts, dcounts, 8 * (size_t)p_.k, hipMemcpyDeviceToHost, S.st));
       HIP_OK(hipStreamSynchronize(S.st));
+    } else {
+      std::memset(sums, 0, 8 * (nsums + (size_t)p_.k));
     }
     tmark("map.device_done");
     if (tmp_.n || tmp_.xb || tmp_.x32) tmp_.release();   // an uncached split
-    kmp::emit_partials(ctx, p_, reinterpret_cast<const int64_t*>(sums.data()), dp_,
-                       reinterpret_cast<const int64_t*>(counts.data()));
+    kmp::emit_partials(ctx, p_, reinterpret_cast<const int64_t*>(sums), dp_,
+                       reinterpret_cast<const int64_t*>(counts), &S.block);
     ctx.incrementCounter(points_, (uint64_t)n);
     ctx.incrementCounter(gpu_, 1);
     if (cache_hit_) ctx.incrementCounter(hits_, 1);
