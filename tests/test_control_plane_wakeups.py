@@ -5,7 +5,10 @@ the chain ahead of the others has no report coming; staging a job behind a
 staged job rings it — counting only attempts it was actually sent as its work
 (the plan's own attempts sit in its running set before delivery: a ring
 decided on ``running`` alone never came, and the job waited out the 200 ms
-long-poll; 8-rank rehearsal, profiles/r05_control_plane_rehearsal.json)."""
+long-poll; 8-rank rehearsal, profiles/r05_control_plane_rehearsal.json).
+Since round 6 a job staged behind a RUNNING one rings only such idle
+trackers too (ahead=1 stages every job that way); busy ones get the plan
+with their next report."""
 import os
 import random
 import sys
@@ -16,7 +19,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
                                 "tools"))
 
 
-@pytest.mark.parametrize("ahead", [2, 3])
+@pytest.mark.parametrize("ahead", [1, 2, 3])
 @pytest.mark.parametrize("seed", [0, 3, 7])
 def test_parked_trackers_get_every_staged_plan(ahead, seed):
     import jt_microbench as M
