@@ -53,6 +53,12 @@ class HybridTaskScheduler(TaskScheduler):
             self.policy = "optional"
         self.queue_depth = max(1, conf.get_int("hbmr.gpu.queue.depth", 4))
         self.locality_wait = conf.get_int("hbmr.locality.wait.ms", 500) / 1000.0
+        # a classic (per-attempt) job's GPU maps for one device in one
+        # response go out as one bulk launch too: the tracker then sends
+        # Pipes maps to the device's child ahead of their threads and
+        # reports them once per batch (TaskTracker._prelaunch_pipes,
+        # _ReportGroup)
+        self.classic_bulk = conf.get_boolean("hbmr.scheduler.gpu.bulk.classic", True)
         self.max_reduces_per_hb = conf.get_int("hbmr.scheduler.max.reduces.per.heartbeat", 4)
         self.speculate_after = conf.get_float("hbmr.speculative.slowdown", 3.0)
         # stock Hadoop only backs up attempts that ran > SPECULATIVE_LAG (60 s,
@@ -239,7 +245,7 @@ class HybridTaskScheduler(TaskScheduler):
                         tip, level = got
                         if level < 3:
                             self._skips.pop(key, None)
-                        if bulk:
+                        if self.classic_bulk:
                             batch.append(tip)
                         else:
                             actions.append(jt.launch(tr, tip, on_gpu=True, device=dev))

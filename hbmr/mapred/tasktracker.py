@@ -944,6 +944,7 @@ class TaskTracker:
                 # per batch (hbmr.tracker.batch.reports)
                 grp = _ReportGroup(len(runs)) if len(runs) > 1 and self.batch_reports \
                     else None
+                self._prelaunch_pipes(js, runs)
                 for r in runs:
                     r.group = grp
                     self.gpu_pipes_pool.submit(self._run_cpu_map, r)
@@ -955,6 +956,45 @@ class TaskTracker:
             else:
                 for r in runs:
                     self.gpu_runtime.submit(r)
+
+    def _prelaunch_pipes(self, js, runs):
+        """A bulk launch of GPU Pipes maps whose child reads its own input
+        through the device's shared child (hbmr/pipes/mux.py): send their
+        RUN_MAPs now, from here, so the child runs them back to back while
+        the task threads set up (``hbmr.pipes.gpu.prelaunch``, default on).
+        Each thread's PipesGPUMapRunner then takes over its map's messages
+        (mux.PRELAUNCHED); a map that could not be sent ahead (full FIFO, no
+        child) goes the ordinary way."""
+        conf = js.conf
+        if len(runs) < 2 or not conf.get_gpu_executable() or \
+                not conf.get_boolean("hbmr.pipes.gpu.prelaunch", True) or \
+                not conf.get_boolean("hbmr.pipes.gpu.mux", True) or \
+                conf.get_boolean("hadoop.pipes.java.recordreader", False):
+            return
+        from ..pipes import mux
+        from ..pipes.runner import PipesGPUMapRunner, _work_dir
+        if conf.get_gpu_map_runner_class() is not PipesGPUMapRunner:
+            return
+        exe, depth = conf.get_gpu_executable(), conf.get_int(mux.DEPTH, 8)
+        nred = conf.get_num_reduce_tasks()
+        for r in runs:
+            spec = r.spec
+            if r.kill.is_set():
+                continue
+            try:
+                tconf = type(conf)(conf)
+                tconf.set("mapred.task.id", spec.attempt_id)
+                dev = spec.gpu_device_id
+                child = mux.REGISTRY.get(tconf, exe, dev,
+                                         lambda c=tconf, d=dev: _work_dir(c, f"gpumux{d}"), depth)
+                split = _split_from_dict(spec.split)
+                sb = split.serialize() if hasattr(split, "serialize") else bytes(split or b"")
+                t = child.prelaunch(tconf, sb, nred)
+            except Exception:  # noqa: BLE001 — the task thread reports it its own way
+                return
+            if t is None:
+                return
+            mux.PRELAUNCHED[spec.attempt_id] = (child, t)
 
     def _maybe_inject_fault(self, run):
         if self.fault_p > 0 and self._rng.random() < self.fault_p:
@@ -968,6 +1008,9 @@ class TaskTracker:
             TRACE.instant("tt.map.start", attempt=spec.attempt_id)
         try:
             if run.kill.is_set():
+                pm = sys.modules.get("hbmr.pipes.mux")
+                if pm is not None:
+                    pm.PRELAUNCHED.pop(spec.attempt_id, None)
                 self._group_wake(run, False)
                 self._finish(run, P.KILLED, "killed before start")
                 return
@@ -999,6 +1042,9 @@ class TaskTracker:
             state = P.KILLED if run.kill.is_set() else P.FAILED
             if state == P.FAILED:
                 self._keep_task_files(spec, js, failed=True)
+            pm = sys.modules.get("hbmr.pipes.mux")
+            if pm is not None:
+                pm.PRELAUNCHED.pop(spec.attempt_id, None)   # (never taken over)
             self._group_wake(run, False)
             self._finish(run, state, f"{type(e).__name__}: {e}\n{traceback.format_exc()[-2000:]}")
 

@@ -113,6 +113,58 @@ class _FifoHandler:
         self.boot.failed(e)
 
 
+class _Pending:
+    """The handler of a map sent to the child ahead of its task thread
+    (MuxChild.prelaunch): the child's messages for it are kept until the
+    thread attaches its own OutputHandler, then replayed in order and
+    forwarded from there on."""
+
+    def __init__(self):
+        self.lock = threading.Lock()
+        self.target = None
+        self.buf: list = []
+
+    def _call(self, name, *args):
+        with self.lock:
+            t = self.target
+            if t is None:
+                self.buf.append((name, args))
+                return
+        getattr(t, name)(*args)
+
+    def output(self, k, v):
+        self._call("output", k, v)
+
+    def partitioned_output(self, part, k, v):
+        self._call("partitioned_output", part, k, v)
+
+    def status(self, msg):
+        self._call("status", msg)
+
+    def progress(self, p):
+        self._call("progress", p)
+
+    def register_counter(self, cid, group, name):
+        self._call("register_counter", cid, group, name)
+
+    def increment_counter(self, cid, amount):
+        self._call("increment_counter", cid, amount)
+
+    def done(self):
+        self._call("done")
+
+    def failed(self, e):
+        self._call("failed", e)
+
+    def attach(self, handler):
+        # (under the lock: a message arriving meanwhile waits for the replay)
+        with self.lock:
+            for name, args in self.buf:
+                getattr(handler, name)(*args)
+            self.buf = []
+            self.target = handler
+
+
 class MuxChild:
     """A reused GPU Pipes child shared by the map attempts of one device."""
 
@@ -182,6 +234,43 @@ class MuxChild:
                 TRACE.instant("pipes.mux.run_map_sent", fifo=len(self.fifo))
         return t
 
+    def prelaunch(self, job, split, num_reduces):
+        """Send a map to the child now, before its task thread exists (the
+        TaskTracker, for every attempt of a bulk launch): the child starts
+        on it while the threads set their tasks up (config 2's 8 maps were
+        ~0.3 ms of Python each, one after another under the GIL, ahead of
+        their RUN_MAPs).  Its messages are held by a _Pending handler until
+        PipesGPUMapRunner attaches its own.  None (nothing sent) when the
+        FIFO is full: that map takes the ordinary submit path."""
+        h = _Pending()
+        with self.send_lock:
+            with self.cond:
+                if len(self.fifo) >= self.depth or self.dead is not None:
+                    return None
+                t = _Ticket(h, _job_key(job))
+                self.fifo.append(t)
+            jid = t.job_id
+            key = jid if job.get_boolean(SHARED_CONF, False) else \
+                (jid,) + tuple(job.get(k) for k in TASK_KEYS)
+            try:
+                if key != self.conf_job:
+                    job.set_boolean("hbmr.pipes.child.reuse", True)
+                    self.app.downlink.set_job_conf(job)
+                    self.conf_job = key
+                self.app.downlink.run_map(split, num_reduces, False)
+                self.app.downlink.flush()
+            except OSError as e:
+                with self.cond:
+                    if t in self.fifo:
+                        self.fifo.remove(t)
+                    self.dead = self.dead or e
+                    self.cond.notify_all()
+                return None
+            self.maps += 1
+        if TRACE.on:
+            TRACE.instant("pipes.mux.prelaunched")
+        return t
+
     def wait(self, ticket):
         try:
             ticket.handler.wait_for_finish()
@@ -223,3 +312,7 @@ class MuxRegistry:
 
 
 REGISTRY = MuxRegistry()
+
+# attempt id -> (MuxChild, ticket) of the maps sent ahead of their threads
+PRELAUNCHED: dict = {}
+PRELAUNCH = "hbmr.pipes.gpu.prelaunch"

@@ -147,6 +147,18 @@ class PipesGPUMapRunner(PipesMapRunner):
             return super().run(reader, output, reporter)
         part = getattr(output, "partitioner", None)
         partitioner = part if isinstance(part, PipesPartitioner) else None
+        pre = mux.PRELAUNCHED.pop(job.get("mapred.task.id"), None)
+        if pre is not None:
+            # sent to the child by the TaskTracker at launch: take over its
+            # messages (those that came already are replayed here)
+            child, t = pre
+            from .application import OutputHandler
+            h = OutputHandler(output, reporter, job.get_map_output_key_class(),
+                              job.get_map_output_value_class(), partitioner)
+            t.handler.attach(h)
+            t.handler = h
+            child.wait(t)
+            return
         # (the work dir is made only when a child is started: one per child,
         # not a directory per map)
         child = mux.REGISTRY.get(job, self.executable(), self.device(),
