@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--skip-split-job", action="store_true")
     ap.add_argument("--trace", default=None, help="event timeline of the last Pipes iteration")
+    ap.add_argument("-D", dest="defines", action="append", default=[], metavar="KEY=VALUE",
+                    help="extra conf for the Pipes job's cluster")
     a = ap.parse_args()
     import torch
 
@@ -100,6 +102,9 @@ def main():
             torch.cuda.empty_cache()
         conf = JobConf()
         conf.set_int("hbmr.gpu.queue.depth", max(16, a.files))
+        for kv in a.defines:
+            kk, _, vv = kv.partition("=")
+            conf.set(kk, vv)
         # one map per file, as the split job's 128 splits (FileInputFormat
         # would cut each 420 MB file into 64 MB blocks: 7x the map tasks)
         conf.set_long("mapred.min.split.size", 1 << 40)
