@@ -155,6 +155,7 @@ class Configuration:
         if name in self._final:
             return
         self._props[name] = value
+        self._gen += 1
         if final:
             self._final.add(name)
 
@@ -189,16 +190,22 @@ class Configuration:
             return default
         return self._substitute(v)
 
+    #: mutation count (set / unset): lets a reader cache values derived from
+    #: this conf (MapOutputBuffer's per-job settings) and see a later change
+    _gen = 0
+
     def set(self, name, value):
         name = DEPRECATED_KEYS.get(name, name)
         v = "" if value is None else (str(value).lower() if isinstance(value, bool) else str(value))
         self._props[name] = v
         self._overlay[name] = v
+        self._gen += 1
 
     def unset(self, name):
         name = DEPRECATED_KEYS.get(name, name)
         self._props.pop(name, None)
         self._overlay.pop(name, None)
+        self._gen += 1
 
     def set_if_unset(self, name, value):
         if self.get_raw(name) is None:

@@ -218,35 +218,72 @@ def run_combiner(combiner_cls, job, kcls, vcls, records, reporter):
 class MapOutputBuffer(OutputCollector):
     """Collect → partition → sort → (combine) → spill, then merge spills."""
 
+    #: the job-level settings below, per job conf object (a TaskTracker's
+    #: JobState conf, shared by the job's attempts, whose task confs differ
+    #: only in task keys): ~20 typed conf reads and class resolutions were a
+    #: quarter of a small Pipes map's task-thread time (config 2)
+    _SETTINGS = ("R", "kcls", "vcls", "sort_key", "pcls", "combiner_cls", "soft_limit", "factor",
+                 "min_spills_for_combine", "codec", "mem_max_conf", "mem_total", "kind",
+                 "native_hash", "spill_async")
+
+    @staticmethod
+    def _settings(job) -> dict:
+        sort_bytes = job.get_int("hbmr.io.sort.bytes", job.get_int("io.sort.mb", 100) << 20)
+        kind = sortbuf.key_kind(job)
+        return {
+            "R": job.get_num_reduce_tasks(),
+            "kcls": job.get_map_output_key_class(),
+            "vcls": job.get_map_output_value_class(),
+            "sort_key": job.get_output_key_comparator(),
+            "pcls": job.get_partitioner_class(),
+            "combiner_cls": job.get_combiner_class(),
+            "soft_limit": int(sort_bytes * job.get_float("io.sort.spill.percent", 0.8)),
+            "factor": max(2, job.get_int("io.sort.factor", 10)),
+            "min_spills_for_combine": job.get_int("min.num.spills.for.combine", 3),
+            "codec": get_codec(job.get("mapred.map.output.compression.codec",
+                                       "org.apache.hadoop.io.compress.DefaultCodec"))
+            if job.get_compress_map_output() else None,
+            "mem_max_conf": job.get_long(mapoutput.MAX_KEY, 4 << 20),
+            "mem_total": job.get_long(mapoutput.TOTAL_KEY, 256 << 20),
+            # native sort path (hbmr/mapred/sortbuf.py): serialised records
+            # only, partition + sort + group + IFile encode per spill in C++
+            "kind": kind,
+            "native_hash": kind is not None and sortbuf.hash_partitioned(job),
+            "spill_async": job.get_boolean("hbmr.map.spill.async", True),
+        }
+
     def __init__(self, task: "MapTask", job, reporter, out_dir):
         self.task = task
         self.job = job
         self.reporter = reporter
-        self.R = job.get_num_reduce_tasks()
-        self.kcls = job.get_map_output_key_class()
-        self.vcls = job.get_map_output_value_class()
-        self.sort_key = job.get_output_key_comparator()
-        self.partitioner = new_instance(job.get_partitioner_class(), job)
-        self.combiner_cls = job.get_combiner_class()
-        sort_bytes = job.get_int("hbmr.io.sort.bytes", job.get_int("io.sort.mb", 100) << 20)
-        self.soft_limit = int(sort_bytes * job.get_float("io.sort.spill.percent", 0.8))
-        self.factor = max(2, job.get_int("io.sort.factor", 10))
-        self.min_spills_for_combine = job.get_int("min.num.spills.for.combine", 3)
-        self.codec = get_codec(job.get("mapred.map.output.compression.codec",
-                                       "org.apache.hadoop.io.compress.DefaultCodec")) \
-            if job.get_compress_map_output() else None
+        base = getattr(task, "job", None)
+        st = None
+        if base is not None and base is not job:
+            cached = base.__dict__.get("_mob_settings")
+            # (keyed by the shared conf's props dict and mutation count: a
+            # conf changed since, or rebuilt, recomputes them)
+            if cached is not None and cached[0] is base._props and cached[1] == base._gen:
+                st = cached[2]
+        if st is None:
+            st = self._settings(job)
+            if base is not None and base is not job:
+                base._mob_settings = (base._props, base._gen, st)
+        self.R, self.kcls, self.vcls = st["R"], st["kcls"], st["vcls"]
+        self.sort_key = st["sort_key"]
+        self.partitioner = new_instance(st["pcls"], job)
+        self.combiner_cls = st["combiner_cls"]
+        self.soft_limit, self.factor = st["soft_limit"], st["factor"]
+        self.min_spills_for_combine = st["min_spills_for_combine"]
+        self.codec = st["codec"]
         self.out_dir = out_dir
         self._dir_made = False
         # a small single-spill output stays in this process's memory when the
         # tracker's reduces read here (hbmr/mapred/mapoutput.py)
-        self.mem_max = job.get_long(mapoutput.MAX_KEY, 4 << 20) \
-            if getattr(task, "memory_outputs", False) else 0
-        self.mem_total = job.get_long(mapoutput.TOTAL_KEY, 256 << 20)
+        self.mem_max = st["mem_max_conf"] if getattr(task, "memory_outputs", False) else 0
+        self.mem_total = st["mem_total"]
         self._to_memory = False
-        # native sort path (hbmr/mapred/sortbuf.py): serialised records only,
-        # partition + sort + group + IFile encode per spill in C++
-        self.kind = sortbuf.key_kind(job)
-        self.native_hash = self.kind is not None and sortbuf.hash_partitioned(job)
+        self.kind = st["kind"]
+        self.native_hash = st["native_hash"]
         self.keys: list = []
         self.vals: list = []
         self.parts: list = []
@@ -260,7 +297,7 @@ class MapOutputBuffer(OutputCollector):
         # SpillThread (MapTask.java:913-915, 1346): a full buffer is sorted and
         # spilled in the background while map() keeps collecting into a fresh
         # one; collect blocks only if that one fills while a spill is running
-        self.spill_async = job.get_boolean("hbmr.map.spill.async", True)
+        self.spill_async = st["spill_async"]
         self._spill_thread = None
         self._spill_error = None
         self._direct_final = False
