@@ -966,9 +966,12 @@ class TaskTracker:
         (mux.PRELAUNCHED); a map that could not be sent ahead (full FIFO, no
         child) goes the ordinary way."""
         conf = js.conf
+        # (only for apps that take one conf per job: an attempt's own task
+        # conf — work dir, input file, ... — is built by its task thread)
         if len(runs) < 2 or not conf.get_gpu_executable() or \
                 not conf.get_boolean("hbmr.pipes.gpu.prelaunch", True) or \
                 not conf.get_boolean("hbmr.pipes.gpu.mux", True) or \
+                not conf.get_boolean("hbmr.pipes.gpu.mux.shared.conf", False) or \
                 conf.get_boolean("hadoop.pipes.java.recordreader", False):
             return
         from ..pipes import mux
